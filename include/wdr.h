@@ -1,0 +1,195 @@
+/*
+ * wdr.h — C ABI of libwdr, the MI355X-native drop-in for the hot path of
+ * tmoroney/whisper-diarize-rs (Engine::transcribe_audio and the five seam calls it
+ * makes).
+ *
+ * Everything is extern "C", plain pointers and sizes; no C++ exceptions cross it.
+ * Status convention: int return 0 = ok, < 0 = error; the message is kept per thread
+ * and returned by wdr_last_error() (the Rust shim maps it to eyre::Report).
+ *
+ * Option<T> encoding: Option<bool> -> int8_t (-1 None, 0 false, 1 true);
+ * Option<i32/usize/f32/f64> -> value + int8_t has_ flag; Option<String> -> nullable
+ * NUL-terminated UTF-8.
+ *
+ * Reference interface each entry point replaces (file:line in the reference crate):
+ *   wdr_engine_new / wdr_engine_free     Engine::new                      src/engine.rs:58-63
+ *   wdr_transcribe_audio                 Engine::transcribe_audio         src/engine.rs:65-200
+ *   wdr_read_wav                         audio::read_wav                  src/audio.rs:4-24
+ *   wdr_vad_get_segments                 vad::get_segments                src/vad.rs:6-85
+ *   wdr_vad_merge                        (the crate's own merge, src/vad.rs:33-84)
+ *   wdr_context_create / _free           transcribe::create_context       src/transcribe.rs:89-166
+ *   wdr_run_pipeline                     transcribe::run_transcription_pipeline src/transcribe.rs:323-535
+ *   wdr_segment_list_free                (drop of Vec<Segment>)
+ * The wdr_dbg_* functions are kernel-level test seams (parity tests call them).
+ */
+#ifndef WDR_H
+#define WDR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WDR_ABI_VERSION 1
+
+typedef struct wdr_engine wdr_engine;
+typedef struct wdr_context wdr_context;   /* ~ whisper_rs::WhisperContext (+ its state) */
+
+/* EngineConfig, src/engine.rs:9-18 */
+typedef struct {
+  const char* cache_dir;                  /* PathBuf; default "./cache" */
+  int8_t enable_dtw;                      /* Option<bool>, default Some(true) */
+  int8_t enable_flash_attn;               /* Option<bool>, default Some(false) */
+  int8_t use_gpu;                         /* Option<bool>, default Some(true) */
+  int8_t has_gpu_device;
+  int32_t gpu_device;                     /* Option<i32> */
+  const char* vad_model_path;             /* Option<String> */
+  const char* diarize_segment_model_path; /* Option<String> */
+  const char* diarize_embedding_model_path; /* Option<String> */
+} wdr_engine_config;
+
+/* AdvancedTranscribe, src/types.rs:16-24 */
+typedef struct {
+  const char* sampling_strategy;          /* "beam_search" | "greedy" | NULL */
+  int8_t has_best_of_or_beam_size; int32_t best_of_or_beam_size;
+  int8_t has_n_threads; int32_t n_threads;
+  int8_t has_temperature; float temperature;
+  int8_t has_max_text_ctx; int32_t max_text_ctx;
+  const char* init_prompt;
+  int8_t has_diarize_threshold; float diarize_threshold;
+} wdr_advanced;
+
+/* TranscribeOptions, src/types.rs:28-45 */
+typedef struct {
+  int8_t has_offset; double offset;       /* default Some(0.0) */
+  const char* model;                      /* default "base" */
+  const char* lang;                       /* default Some("auto") */
+  int8_t whisper_to_english;              /* default Some(false) */
+  const char* translate_target;           /* network translation: out of scope (error if set) */
+  int8_t enable_vad;                      /* default Some(true) */
+  int8_t enable_diarize;                  /* default None */
+  int8_t has_max_speakers; uint64_t max_speakers;
+  const wdr_advanced* advanced;           /* nullable */
+} wdr_transcribe_options;
+
+/* Synthetic-weights / workload knobs (no checkpoints on this machine).
+ * Not part of the reference API; NULL everywhere means defaults. */
+typedef struct {
+  double weight_std;                      /* default 0.02 */
+  double emb_std;                         /* default 0.02 */
+  float force_len_rate;                   /* >0: pin decode length (tokens per audio second) */
+  int8_t disable_fallback;                /* 1: logprob/entropy fallback thresholds off */
+} wdr_synthetic;
+
+/* FormattingOverrides, src/formatting.rs:37-51 (accepted; subtitle formatting is §8(f) "next") */
+typedef struct {
+  int8_t has_max_chars_per_line; uint64_t max_chars_per_line;
+  int8_t has_max_lines; uint64_t max_lines;
+  int8_t has_cps_cap; double cps_cap;
+  int8_t has_split_gap_sec; double split_gap_sec;
+} wdr_formatting_overrides;
+
+/* WordTimestamp, src/types.rs:64-70 */
+typedef struct {
+  const char* text;
+  double start, end;
+  int8_t has_probability; float probability;
+} wdr_word;
+
+/* Segment, src/types.rs:74-82 */
+typedef struct {
+  double start, end;
+  const char* text;
+  const wdr_word* words; size_t n_words;  /* words == NULL <-> None */
+  const char* speaker_id;                 /* NULL <-> None */
+} wdr_segment;
+
+typedef struct {
+  wdr_segment* segments; size_t n_segments;
+  const char* detected_lang;              /* Option<String> (run_transcription_pipeline's second result) */
+} wdr_segment_list;
+
+/* SpeechSegment, src/types.rs:86-90 (samples borrowed) */
+typedef struct {
+  double start, end;
+  const int16_t* samples; size_t n_samples;
+} wdr_speech_segment;
+
+/* Callbacks, src/engine.rs:35-40 + src/types.rs:12-13; all fire on the calling thread */
+typedef struct {
+  void* user;
+  void (*progress)(void* user, int32_t pct, int32_t type /*0 Download,1 Transcribe,2 Translate*/, const char* label);
+  void (*new_segment)(void* user, const wdr_segment* seg);   /* borrowed for the callback only */
+  int (*is_cancelled)(void* user);
+} wdr_callbacks;
+
+/* per-stage wall-clock accounting of the last run (seconds) */
+typedef struct {
+  double mel, encode, decode, dtw, vad, total;
+  int64_t windows, decode_steps, prefills;
+} wdr_stage_times;
+
+const char* wdr_last_error(void);
+int wdr_abi_version(void);
+int wdr_device_count(void);
+
+/* ---- Engine (whole-call drop-in) ---- */
+int wdr_engine_new(const wdr_engine_config* cfg, wdr_engine** out);
+void wdr_engine_free(wdr_engine* e);
+int wdr_engine_set_synthetic(wdr_engine* e, const wdr_synthetic* syn);
+int wdr_transcribe_audio(wdr_engine* e, const char* audio_path, const wdr_transcribe_options* opts,
+                         const wdr_formatting_overrides* fmt, const wdr_callbacks* cb, wdr_segment_list** out);
+
+/* ---- seams ---- */
+int wdr_read_wav(const char* path, int16_t** samples, size_t* n);
+void wdr_free(void* p);
+int wdr_vad_merge(const double* starts_cs, const double* ends_cs, size_t n_segs, const int16_t* samples,
+                  size_t n_samples, double* mask_out /* [2*n_segs] */, size_t* n_mask,
+                  double* merged_out /* [2*n_segs] start,end seconds */, int64_t* merged_idx /* [2*n_segs] */,
+                  size_t* n_merged);
+int wdr_context_create(const char* model_path, const char* model_name, int8_t has_gpu_device, int32_t gpu_device,
+                       int8_t use_gpu, int8_t enable_dtw, int8_t enable_flash_attn, int8_t has_num_samples,
+                       uint64_t num_samples, const wdr_synthetic* syn, wdr_context** out);
+void wdr_context_free(wdr_context* c);
+int wdr_run_pipeline(wdr_context* c, const wdr_speech_segment* segs, size_t n_segs, const wdr_transcribe_options* opts,
+                     const wdr_synthetic* syn, const wdr_callbacks* cb, wdr_segment_list** out);
+void wdr_segment_list_free(wdr_segment_list* l);
+int wdr_context_stage_times(wdr_context* c, wdr_stage_times* out);
+int wdr_context_hparams(wdr_context* c, int32_t* out /* [10] */);
+
+/* ---- whisper_full-level test seam: one state.full() call, raw token data ---- */
+typedef struct {
+  int32_t id, tid;
+  float p, plog, pt, ptsum;
+  int64_t t0, t1, t_dtw;
+} wdr_token;
+typedef struct {
+  int64_t t0, t1;
+  const char* text;
+  const wdr_token* tokens; size_t n_tokens;
+} wdr_result_seg;
+int wdr_state_full(wdr_context* c, const float* samples, size_t n, const wdr_transcribe_options* opts,
+                   const wdr_synthetic* syn, const char* initial_prompt, wdr_result_seg** segs, size_t* n_segs,
+                   int32_t* lang_id);
+void wdr_result_free(wdr_result_seg* segs, size_t n);
+
+/* ---- kernel-level test seams (host buffers in / out) ---- */
+int wdr_dbg_log_mel(wdr_context* c, const float* x, size_t n, int32_t seek, float* window_out /* [n_mels][3000] */);
+int wdr_dbg_energy(const float* x, size_t n, float* out);
+int wdr_dbg_encode(wdr_context* c, const float* mel_window /* [n_mels][3000] */, float* enc_out /* [1500][d] */);
+int wdr_dbg_decode(wdr_context* c, const int32_t* tokens, size_t n, float* logits_out /* [n_vocab] */);
+int wdr_dbg_capture(wdr_context* c, const int32_t* tokens, size_t n, float* cap_out /* [n_aheads][n][1500] */);
+int wdr_dbg_dtw(const float* cap, int32_t n_heads, int32_t n_tok, int32_t n_audio, int32_t sot_len, int32_t seek,
+                float* x_out /* [n_tok-sot_len-1][n_audio] */, int32_t* times_out, int32_t* n_times);
+int wdr_dbg_dtw_dp(const float* x, int32_t rows, int32_t cols, int32_t seek, int32_t* times_out, int32_t* n_times);
+int wdr_dbg_proj(const uint16_t* a_f16, const uint16_t* w_f16, const float* bias, int32_t M, int32_t N, int32_t K,
+                 int32_t epi, float* out /* [M][N] f32 (f16 epilogues are widened) */);
+int wdr_dbg_attn(const uint16_t* q, const uint16_t* k, const uint16_t* v, int32_t Tq, int32_t Tk, int32_t n_head,
+                 int32_t causal, float* out /* [Tq][n_head*64] */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WDR_H */

@@ -24,11 +24,22 @@ import numpy as np
 
 
 def norm_over_tokens(w: np.ndarray, eps: float = 1e-9) -> np.ndarray:
-    """w: [H][N][M]; ggml_norm along the token axis for every (head, column)."""
+    """w: [H][N][M]; ggml_norm (f32) along the token axis for every (head, column):
+    mean = float(double sum / N); v = x - mean; var = float(double sum of f32 v*v / N);
+    scale = 1 / sqrtf(var + eps); y = v * scale.  Sums run in token order."""
     w = w.astype(np.float32)
-    mean = w.mean(axis=1, keepdims=True, dtype=np.float64)
-    var = ((w - mean) ** 2).mean(axis=1, keepdims=True, dtype=np.float64)
-    return ((w - mean) / np.sqrt(var + eps)).astype(np.float32)
+    H, N, M = w.shape
+    s = np.zeros((H, M), np.float64)
+    for t in range(N):
+        s += w[:, t, :].astype(np.float64)
+    mean = (s / N).astype(np.float32)
+    s2 = np.zeros((H, M), np.float64)
+    for t in range(N):
+        v = (w[:, t, :] - mean).astype(np.float32)
+        s2 += (v * v).astype(np.float32).astype(np.float64)
+    var = (s2 / N).astype(np.float32)
+    scale = (np.float32(1.0) / np.sqrt((var + np.float32(eps)).astype(np.float32))).astype(np.float32)
+    return ((w - mean[:, None, :]).astype(np.float32) * scale[:, None, :]).astype(np.float32)
 
 
 def median_filter(w: np.ndarray, width: int = 7) -> np.ndarray:
@@ -111,12 +122,16 @@ def dtw(x: np.ndarray):
 
 def alignment_matrix(qk: np.ndarray, n_frames: int, sot_len: int, medfilt: int = 7) -> np.ndarray:
     """qk: [H][N_tok][1500] post-softmax alignment-head attention.  Returns the
-    [N_tok - sot_len - 1][n_frames//2] matrix DTW runs on."""
+    [N_tok - sot_len - 1][n_frames//2] matrix DTW runs on (ggml_mean: double sum over
+    heads in head order, cast to float, / H, then scaled by -1)."""
     n_audio = n_frames // 2
     w = qk[:, :, :n_audio]
     w = norm_over_tokens(w)
     w = median_filter(w, medfilt)
-    w = -w.mean(axis=0, dtype=np.float64).astype(np.float32)
+    s = np.zeros(w.shape[1:], np.float64)
+    for h in range(w.shape[0]):
+        s += w[h].astype(np.float64)
+    w = ((s.astype(np.float32) / np.float32(w.shape[0])) * np.float32(-1.0)).astype(np.float32)
     return w[sot_len:w.shape[0] - 1]
 
 

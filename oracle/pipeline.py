@@ -107,9 +107,12 @@ def vad_merge(segs_cs, int_samples: np.ndarray):
         else:
             merged.append((st, en))
     out = []
+    def rround(v):   # Rust f32::round: half away from zero
+        v = float(v)
+        return float(np.sign(v) * np.floor(abs(v) + 0.5))
     for st, en in merged:
-        si = int(min(max(np.round(np.float32(st) * SR), np.float32(0)), n_f32))
-        ei = int(min(max(np.round(np.float32(en) * SR), np.float32(0)), n_f32))
+        si = int(min(max(rround(np.float32(st) * SR), 0.0), float(n_f32)))
+        ei = int(min(max(rround(np.float32(en) * SR), 0.0), float(n_f32)))
         smp = int_samples[si:ei].copy() if ei > si else np.zeros(0, np.int16)
         seg = SpeechSegment(st, en, smp)
         if seg.end > seg.start and smp.size > 0:

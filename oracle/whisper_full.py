@@ -496,7 +496,7 @@ class WhisperState:
                 while k < n_samples - 1 and energy[k] > thold:
                     k += 1
                 toks[j].t1 = s2ts(k)
-                if j < ns - 1 and toks[j].t1 > toks[j + 1].t0:
+                if j < ns - 1 and j + 1 < n and toks[j].t1 > toks[j + 1].t0:
                     toks[j].t1 = toks[j + 1].t0
                 else:
                     s1 = k

@@ -1,0 +1,97 @@
+"""CPU-side tests: libwdr loads and exports the C ABI, and the host-only seams
+(read_wav, the reference's VAD merge) match the oracle's restatement of the reference glue."""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from oracle import pipeline as op
+from wdr import _lib
+import wdr
+
+
+def test_library_exports_every_header_symbol(lib):
+    syms = _lib.header_symbols()
+    assert len(syms) >= 25
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert lib.wdr_abi_version() == 1
+
+
+def _wav(path, samples, ch=1, rate=16000, bits=16, fmt=1):
+    data = np.asarray(samples, np.int16).tobytes() if bits == 16 else bytes(len(samples))
+    hdr = b"RIFF" + struct.pack("<I", 36 + len(data)) + b"WAVE"
+    hdr += b"fmt " + struct.pack("<IHHIIHH", 16, fmt, ch, rate, rate * ch * bits // 8, ch * bits // 8, bits)
+    hdr += b"data" + struct.pack("<I", len(data))
+    with open(path, "wb") as f:
+        f.write(hdr + data)
+
+
+def test_read_wav_roundtrip_and_reference_errors(tmp_path):
+    x = (np.random.default_rng(0).standard_normal(16000) * 3000).astype(np.int16)
+    p = str(tmp_path / "a.wav")
+    op.write_wav(p, x)
+    np.testing.assert_array_equal(wdr.read_wav(p), x)
+    np.testing.assert_array_equal(op.read_wav(p), x)
+    cases = [
+        (dict(ch=2), "expected mono audio file and found 2 channels!"),
+        (dict(rate=44100), "expected 16KHz sample rate"),
+        (dict(bits=8), "expected 16 bits per sample"),
+        (dict(fmt=3), "expected integer sample format"),
+    ]
+    for kw, msg in cases:
+        q = str(tmp_path / "b.wav")
+        _wav(q, x[:100], **kw)
+        with pytest.raises(wdr.WdrError, match=msg):
+            wdr.read_wav(q)
+        with pytest.raises(op.WavError, match=msg):
+            op.read_wav(q)
+    with pytest.raises(wdr.WdrError, match="failed to read file"):
+        wdr.read_wav(str(tmp_path / "missing.wav"))
+
+
+def test_transcribe_audio_missing_file_message():
+    e = wdr.Engine(wdr.EngineConfig())
+    with pytest.raises(wdr.WdrError, match="audio file doesn't exist"):
+        e.transcribe_audio("/nonexistent/x.wav", wdr.TranscribeOptions())
+
+
+def test_vad_merge_matches_reference_glue():
+    rng = np.random.default_rng(3)
+    samples = rng.integers(-3000, 3000, 16000 * 20).astype(np.int16)
+    for trial in range(30):
+        k = int(rng.integers(0, 12))
+        st = np.sort(rng.uniform(0, 2000, k))
+        segs = [(float(a), float(a + rng.uniform(-5, 300))) for a in st]
+        rng.shuffle(segs)
+        m_ref, out_ref = op.vad_merge(segs, samples)
+        m_got, out_got = wdr.vad_merge(segs, samples)
+        assert len(m_ref) == len(m_got)
+        for (a, b), (c, d) in zip(m_ref, m_got):
+            assert a == c and b == d
+        assert len(out_ref) == len(out_got)
+        for r, g in zip(out_ref, out_got):
+            assert r.start == g.start and r.end == g.end
+            np.testing.assert_array_equal(r.samples, g.samples)
+
+
+def test_vad_merge_edge_cases():
+    s = np.zeros(1000, np.int16)
+    assert wdr.vad_merge([], s) == ([], [])
+    m, out = wdr.vad_merge([(10.0, 5.0)], s)          # end <= start dropped
+    assert m == [] and out == []
+    m, out = wdr.vad_merge([(0.0, 100.0)], s)         # clamped to the sample count
+    assert len(out) == 1 and out[0].samples.size == 1000
+
+
+def test_synthetic_audio_is_deterministic():
+    from wdr.synth import synth_speech
+    a, sa = synth_speech(20.0, seed=1, n_speakers=3)
+    b, sb = synth_speech(20.0, seed=1, n_speakers=3)
+    np.testing.assert_array_equal(a, b)
+    assert sa == sb and len(sa) >= 2
+    assert {s[2] for s in sa} <= {0, 1, 2}
+    for (s0, e0, _), (s1, e1, _) in zip(sa, sa[1:]):
+        assert 1.5 - 1e-3 <= e0 - s0 <= 8.0 + 1e-3
+        assert s1 - e0 >= 0.3 - 1e-3

@@ -1,0 +1,149 @@
+"""Kernel-level parity of the HIP path (through the C ABI) against the CPU oracle /
+a plain fp32 reference of the same op.  Tolerances are stated per test."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from oracle import dtw as odtw
+from oracle import mel as omel
+from wdr import _lib
+import wdr
+
+pytestmark = pytest.mark.gpu
+
+U16 = C.POINTER(C.c_uint16)
+F32 = C.POINTER(C.c_float)
+I32 = C.POINTER(C.c_int32)
+
+
+def _f16bits(a):
+    return np.ascontiguousarray(a.astype(np.float16)).view(np.uint16)
+
+
+def _proj(lib, a, w, bias, epi, out0=None):
+    M, K = a.shape
+    N = w.shape[0]
+    out = np.zeros((M, N), np.float32) if out0 is None else out0.copy()
+    ab, wb = _f16bits(a), _f16bits(w)
+    b = None if bias is None else np.ascontiguousarray(bias, np.float32)
+    _lib.check(lib.wdr_dbg_proj(ab.ctypes.data_as(U16), wb.ctypes.data_as(U16),
+                                None if b is None else b.ctypes.data_as(F32), M, N, K, epi, out.ctypes.data_as(F32)))
+    return out
+
+
+def _gelu(x):
+    return 0.5 * x * (1 + np.tanh(0.7978845608028654 * (x + 0.044715 * x ** 3)))
+
+
+@pytest.mark.parametrize("M", [1, 3, 8, 9, 300, 1500])
+def test_projection_matches_fp32_reference(lib, M):
+    rng = np.random.default_rng(M)
+    K, N = 256, 384
+    a = rng.standard_normal((M, K)).astype(np.float16).astype(np.float32)
+    w = (rng.standard_normal((N, K)) * 0.05).astype(np.float16).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32) * 0.1
+    ref = a.astype(np.float64) @ w.T.astype(np.float64) + bias
+    # f32 output: accumulation-order error only
+    np.testing.assert_allclose(_proj(lib, a, w, bias, 3), ref, rtol=0, atol=2e-4)
+    # f16 output (+GELU): f16 rounding of the result, |err| <= 2^-10 relative
+    np.testing.assert_allclose(_proj(lib, a, w, bias, 0), ref, rtol=2e-3, atol=2e-3)
+    np.testing.assert_allclose(_proj(lib, a, w, bias, 1), _gelu(ref), rtol=2e-3, atol=2e-3)
+    base = rng.standard_normal((M, N)).astype(np.float32)
+    np.testing.assert_allclose(_proj(lib, a, w, bias, 2, base), base + ref, rtol=0, atol=2e-4)
+
+
+def test_projection_logits_shape(lib):
+    """decoder logits: N not a multiple of the tile (51866 x d), M = 1 (GEMV path)."""
+    rng = np.random.default_rng(7)
+    K, N = 128, 51866
+    a = rng.standard_normal((1, K)).astype(np.float16).astype(np.float32)
+    w = (rng.standard_normal((N, K)) * 0.1).astype(np.float16).astype(np.float32)
+    ref = a.astype(np.float64) @ w.T.astype(np.float64)
+    np.testing.assert_allclose(_proj(lib, a, w, None, 3), ref, rtol=0, atol=2e-4)
+
+
+def _attn_ref(q, k, v, H, causal):
+    Tq, Tk = q.shape[0], k.shape[0]
+    out = np.zeros((Tq, H * 64))
+    for h in range(H):
+        s = q[:, h * 64:(h + 1) * 64].astype(np.float64) @ k[:, h * 64:(h + 1) * 64].T.astype(np.float64) / 8.0
+        if causal:
+            s = s + np.triu(np.full((Tq, Tk), -np.inf), 1)
+        p = np.exp(s - s.max(1, keepdims=True))
+        p /= p.sum(1, keepdims=True)
+        out[:, h * 64:(h + 1) * 64] = p @ v[:, h * 64:(h + 1) * 64]
+    return out
+
+
+@pytest.mark.parametrize("Tq,Tk,H,causal", [(1500, 1500, 2, 0), (37, 1500, 3, 0), (129, 129, 2, 1), (5, 5, 1, 1)])
+def test_flash_attention_matches_fp32_reference(lib, Tq, Tk, H, causal):
+    rng = np.random.default_rng(Tq + Tk)
+    q = (rng.standard_normal((Tq, H * 64)) * 1.0).astype(np.float16)
+    k = (rng.standard_normal((Tk, H * 64)) * 1.0).astype(np.float16)
+    v = rng.standard_normal((Tk, H * 64)).astype(np.float16)
+    out = np.zeros((Tq, H * 64), np.float32)
+    _lib.check(lib.wdr_dbg_attn(q.view(np.uint16).ctypes.data_as(U16), k.view(np.uint16).ctypes.data_as(U16),
+                                v.view(np.uint16).ctypes.data_as(U16), Tq, Tk, H, causal, out.ctypes.data_as(F32)))
+    ref = _attn_ref(q.astype(np.float32), k.astype(np.float32), v.astype(np.float32), H, causal)
+    # P enters P.V as f16 (as in ggml), output rounded to f16
+    np.testing.assert_allclose(out, ref, rtol=0, atol=1e-2)
+    assert np.abs(out - ref).mean() < 1.5e-3
+
+
+def test_signal_energy_is_bit_exact(lib):
+    rng = np.random.default_rng(0)
+    for n in (1, 64, 65, 1000, 160000):
+        x = (rng.standard_normal(n) * 0.2).astype(np.float32)
+        out = np.zeros(n, np.float32)
+        _lib.check(lib.wdr_dbg_energy(x.ctypes.data_as(F32), n, out.ctypes.data_as(F32)))
+        np.testing.assert_array_equal(out, omel.signal_energy(x))
+
+
+def _dtw_dp(lib, x, seek):
+    x = np.ascontiguousarray(x, np.float32)
+    rows, cols = x.shape
+    t = np.zeros(rows + 8, np.int32)
+    nt = C.c_int32()
+    _lib.check(lib.wdr_dbg_dtw_dp(x.ctypes.data_as(F32), rows, cols, seek, t.ctypes.data_as(I32), C.byref(nt)))
+    return list(t[:nt.value])
+
+
+def test_dtw_dp_bit_exact_against_golden_including_ties(lib):
+    import os
+    from conftest import GOLDEN
+    g = np.load(os.path.join(GOLDEN, "dtw_cases.npz"))
+    for key in [k for k in g.files if k.startswith("x")]:
+        x = g[key]
+        ti, tj = g["ti" + key[1:]], g["tj" + key[1:]]
+        want, last = [], 0
+        for v, t in zip(ti.tolist(), tj.tolist()):
+            if v != last:
+                want.append(2 * t + 100)
+                last = v
+        assert _dtw_dp(lib, x, 100) == want, key
+
+
+def test_dtw_dp_max_size(lib):
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((221, 1500)).astype(np.float32)
+    assert _dtw_dp(lib, x, 0) == odtw.token_times(x, 0)
+    x = np.round(rng.standard_normal((40, 1500))).astype(np.float32)   # ties everywhere
+    assert _dtw_dp(lib, x, 3000) == odtw.token_times(x, 3000)
+
+
+def test_dtw_preprocessing_bit_exact(lib):
+    rng = np.random.default_rng(9)
+    A, N, n_audio, sot_len = 5, 23, 731, 1
+    logits = rng.standard_normal((A, N, 1500)).astype(np.float32) * 3
+    cap = np.exp(logits - logits.max(-1, keepdims=True))
+    cap = (cap / cap.sum(-1, keepdims=True)).astype(np.float32)
+    rows = N - sot_len - 1
+    x = np.zeros((rows, n_audio), np.float32)
+    t = np.zeros(N + 8, np.int32)
+    nt = C.c_int32()
+    _lib.check(lib.wdr_dbg_dtw(cap.ctypes.data_as(F32), A, N, n_audio, sot_len, 200, x.ctypes.data_as(F32),
+                               t.ctypes.data_as(I32), C.byref(nt)))
+    xr = odtw.alignment_matrix(cap, 2 * n_audio, sot_len)
+    np.testing.assert_array_equal(x, xr)
+    assert list(t[:nt.value]) == odtw.token_times(xr, 200)

@@ -1,0 +1,153 @@
+"""Model-level parity: the HIP Whisper path (libwdr through the C ABI) against the CPU
+oracle (numpy restatement of the ggml graph + whisper_full loop + reference glue) on the
+same synthetic weights and inputs.
+
+Tolerances: normalised log-mel |err| <= 2e-3 (f32 DFT vs double FFT); encoder output and
+logits compared relative to their spread (f16 operands, f32 accumulation on both sides,
+different summation order); token ids / text identical; DTW anchors within 2 cs;
+word times within 20 ms (the north-star bar)."""
+import numpy as np
+import pytest
+
+import wdr
+from oracle.mel import log_mel, pcm_i16_to_f32
+from oracle.model import DecoderState, Whisper
+from oracle.pipeline import SpeechSegment as OSeg
+from oracle.pipeline import run_transcription_pipeline
+from oracle.vocab import Vocab
+from oracle.weights import hparams_for, synth_weights
+from oracle.whisper_full import FullParams, WhisperState
+from wdr.synth import synth_speech
+
+pytestmark = pytest.mark.gpu
+
+EMB_STD = 0.5
+SYN = wdr.Synthetic(weight_std=0.02, emb_std=EMB_STD, force_len_rate=3.3, disable_fallback=True)
+
+
+@pytest.fixture(scope="module", params=["tiny-test", "tiny-test-ml"])
+def model(request):
+    name = request.param
+    ctx = wdr.WhisperContext(name, synthetic=SYN)
+    hp = hparams_for(name)
+    W = synth_weights(hp, std=0.02, emb_std=EMB_STD)
+    return name, ctx, hp, W
+
+
+@pytest.fixture(scope="module")
+def audio():
+    pcm, spurts = synth_speech(40.0, seed=0)
+    return pcm, spurts
+
+
+def test_log_mel_window_matches_oracle(model, audio):
+    name, ctx, hp, W = model
+    pcm, spurts = audio
+    for a, b, _ in spurts[:3]:
+        x = pcm_i16_to_f32(pcm[int(a * 16000):int(b * 16000)])
+        got = ctx.log_mel_window(x, 0)
+        ref = log_mel(x, hp.n_mels)[:, :3000]
+        assert np.abs(got - ref).max() < 2e-3
+    x = pcm_i16_to_f32(pcm[:16000 * 35])            # > 30 s: second window
+    got = ctx.log_mel_window(x, 3000)
+    ref = log_mel(x, hp.n_mels)[:, 3000:6000]
+    assert np.abs(got - ref).max() < 2e-3
+
+
+def test_encoder_matches_oracle(model):
+    name, ctx, hp, W = model
+    rng = np.random.default_rng(11)
+    mel = (rng.standard_normal((hp.n_mels, 3000)) * 0.4).astype(np.float32)
+    got = ctx.encode(mel)
+    ref = Whisper(hp, W).encode(mel)
+    err = np.abs(got - ref)
+    assert err.max() < 5e-2 and err.mean() < 4e-3, (err.max(), err.mean())
+
+
+def test_decoder_logits_and_capture_match_oracle(model):
+    name, ctx, hp, W = model
+    rng = np.random.default_rng(12)
+    mel = (rng.standard_normal((hp.n_mels, 3000)) * 0.4).astype(np.float32)
+    ctx.encode(mel)
+    m = Whisper(hp, W)
+    cross = m.cross_kv(m.encode(mel))
+    v = Vocab(hp.n_vocab)
+    for toks in ([v.sot], [v.sot, v.beg, 1234, 40000, 77], list(rng.integers(0, 50000, 20))):
+        got = ctx.decode(toks)
+        ref = DecoderState(m).forward(list(toks), cross)
+        scale = ref.std()
+        assert np.abs(got - ref).max() < 0.02 * scale + 0.02, (np.abs(got - ref).max(), scale)
+        assert int(np.argmax(got)) == int(np.argmax(ref))
+    toks = [v.sot, v.not_] + list(rng.integers(0, 50000, 12)) + [v.eot]
+    from oracle.whisper_full import aheads_for_model_name
+    ah = aheads_for_model_name(name)
+    cap = ctx.capture(toks, len(ah))
+    _, qk = DecoderState(m).forward(toks, cross, want_logits=None, aheads=ah)
+    assert np.abs(cap - qk).max() < 2e-3
+    np.testing.assert_allclose(cap.sum(-1), 1.0, atol=1e-3)
+
+
+def _oracle_state(name, hp, W):
+    return WhisperState(Whisper(hp, W), Vocab(hp.n_vocab), name)
+
+
+def _params(lang="auto"):
+    return FullParams(strategy="greedy", language=lang, force_len_rate=3.3, logprob_thold=-np.inf,
+                      entropy_thold=-1.0)
+
+
+@pytest.mark.parametrize("lang", ["auto", "en"])
+def test_state_full_matches_oracle(model, audio, lang):
+    name, ctx, hp, W = model
+    pcm, spurts = audio
+    st = _oracle_state(name, hp, W)
+    opts = wdr.TranscribeOptions(lang=lang, advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    prompt = None
+    for a, b, _ in spurts[:3]:
+        x = pcm_i16_to_f32(pcm[int(a * 16000):int(b * 16000)])
+        got, lang_id = ctx.state_full(x, opts, initial_prompt=prompt)
+        p = _params(lang)
+        p.initial_prompt = prompt
+        st.full(x, p)
+        ref = st.result_all
+        assert len(got) == len(ref)
+        for g, r in zip(got, ref):
+            assert [t["id"] for t in g["tokens"]] == [t.id for t in r.tokens]
+            assert g["text"] == r.text
+            assert (g["t0"], g["t1"]) == (r.t0, r.t1)
+            for tg, tr in zip(g["tokens"], r.tokens):
+                assert abs(tg["t_dtw"] - tr.t_dtw) <= 2, (tg, tr)
+                assert abs(tg["t0"] - tr.t0) <= 2 and abs(tg["t1"] - tr.t1) <= 2, (tg, tr)
+                assert abs(tg["p"] - tr.p) < 1e-3
+        if lang == "auto":
+            assert lang_id == st.lang_id
+        prompt = ref[-1].text.lstrip() if ref else prompt
+
+
+def test_pipeline_matches_oracle_glue(model, audio):
+    """run_transcription_pipeline: prompt chain, offsets, overlap clipping, callbacks order."""
+    name, ctx, hp, W = model
+    pcm, spurts = audio
+    segs = [wdr.SpeechSegment(a, b, pcm[int(a * 16000):int(b * 16000)]) for a, b, _ in spurts[:4]]
+    events = []
+    cb = wdr.Callbacks(progress=lambda p, t, l: events.append(("p", p, int(t), l)),
+                       new_segment_callback=lambda s: events.append(("s", s.text)))
+    opts = wdr.TranscribeOptions(lang="auto", offset=1.5, advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    got, lang = ctx.run_pipeline(segs, opts, cb)
+    st = _oracle_state(name, hp, W)
+    ref, rlang = run_transcription_pipeline(st, [OSeg(s.start, s.end, s.samples) for s in segs],
+                                            dict(lang="auto", offset=1.5, advanced=dict(sampling_strategy="greedy"),
+                                                 synthetic=dict(force_len_rate=3.3, logprob_thold=-np.inf,
+                                                                entropy_thold=-1.0)))
+    assert lang == rlang
+    assert [s.text for s in got] == [s.text for s in ref]
+    for g, r in zip(got, ref):
+        assert abs(g.start - r.start) <= 0.02 and abs(g.end - r.end) <= 0.02
+        assert len(g.words) == len(r.words)
+        for wg, wr in zip(g.words, r.words):
+            assert wg.text == wr.text
+            assert abs(wg.start - wr.start) <= 0.02 and abs(wg.end - wr.end) <= 0.02
+    kinds = [e[0] for e in events]
+    assert kinds == ["s", "p"] * len(got)
+    assert [e[1] for e in events if e[0] == "p"] == [int((i + 1) / 4 * 100) for i in range(4)][:len(got)]
+    assert all(e[3] == "Transcribing audio" and e[2] == 1 for e in events if e[0] == "p")

@@ -1,0 +1,79 @@
+// Shared HIP helpers for libwdr (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+
+namespace wdr {
+
+struct HipError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define WDR_HIP(call)                                                                       \
+  do {                                                                                      \
+    hipError_t e_ = (call);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      throw ::wdr::HipError(std::string("HIP error ") + hipGetErrorString(e_) + " at " +    \
+                            __FILE__ + ":" + std::to_string(__LINE__) + " (" #call ")");    \
+  } while (0)
+
+#define WDR_CHECK(cond, msg)                                                                \
+  do {                                                                                      \
+    if (!(cond)) throw std::runtime_error(std::string(msg));                                \
+  } while (0)
+
+typedef _Float16 f16;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Epilogue selectors for the projection kernels (GEMM / GEMV).
+enum Epi : int {
+  EPI_F16 = 0,         // out16 = acc + bias
+  EPI_F16_GELU = 1,    // out16 = gelu_tanh(acc + bias)
+  EPI_F32_RESID = 2,   // out32 += acc + bias          (pre-LN residual stream update)
+  EPI_F32 = 3,         // out32 = acc + bias
+  EPI_F32_GELU_POS = 4 // out32 = gelu_tanh(acc + bias) + pos[row % pos_rows]  (conv2 + positional)
+};
+
+__host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  // ggml_gelu (tanh form): 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3)))
+  const float c = 0.7978845608028654f;
+  return 0.5f * x * (1.0f + tanhf(c * (x + 0.044715f * x * x * x)));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Projection launchers (kernels/gemm.hip).
+struct ProjArgs {
+  const f16* A; int lda;            // activations [M][K] f16
+  const f16* B; int ldb;            // weights     [N][K] f16 (nn.Linear / ggml layout)
+  const float* bias;                // [N] or null
+  void* out; int ldo;               // f16 or f32 [M][N]
+  const float* pos; int pos_rows;   // EPI_F32_GELU_POS only
+  int M, N, K;
+  int epi;
+};
+void launch_proj(const ProjArgs& a, hipStream_t s);   // picks GEMV (M<=8) or MFMA GEMM
+
+}  // namespace wdr

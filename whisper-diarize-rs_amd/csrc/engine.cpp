@@ -1,0 +1,791 @@
+// libwdr C ABI (include/wdr.h): Engine, the seam calls, and the reference crate's own
+// Rust glue restated in C++:
+//   src/audio.rs:4-24            read_wav (hound checks, verbatim messages)
+//   src/vad.rs:33-84             cs -> s mask, sort, merge gaps < 200 ms, sample slicing
+//   src/transcribe.rs:20-87      setup_params
+//   src/transcribe.rs:171-320    token text cleanup + DTW-midpoint word bounds
+//   src/transcribe.rs:323-535    run_transcription_pipeline (prompt chain, offsets, clipping,
+//                                callbacks in reference order)
+//   src/engine.rs:65-200         transcribe_audio (segmentation choice, context, pipeline)
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <string>
+#include <sys/stat.h>
+#include <vector>
+
+#include "../../include/wdr.h"
+#include "whisper.h"
+
+using namespace wdr;
+
+static thread_local std::string g_err;
+
+static int fail(const std::string& m) {
+  g_err = m;
+  return -1;
+}
+
+#define WDR_GUARD(...)                          \
+  try {                                         \
+    __VA_ARGS__                                 \
+  } catch (const std::exception& ex) {          \
+    return fail(ex.what());                     \
+  } catch (...) {                               \
+    return fail("unknown error");               \
+  }
+
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// ------------------------------------------------------------------ text helpers (Rust semantics)
+// Rust char::is_whitespace over UTF-8: ASCII whitespace + the Unicode White_Space code points.
+static size_t ws_len(const std::string& s, size_t i) {
+  const unsigned char c = s[i];
+  if (c == ' ' || (c >= 0x09 && c <= 0x0D)) return 1;
+  if (c == 0xC2 && i + 1 < s.size() && ((unsigned char)s[i + 1] == 0x85 || (unsigned char)s[i + 1] == 0xA0)) return 2;
+  if (c == 0xE1 && i + 2 < s.size() && (unsigned char)s[i + 1] == 0x9A && (unsigned char)s[i + 2] == 0x80) return 3;
+  if (c == 0xE2 && i + 2 < s.size()) {
+    const unsigned char b = s[i + 1], d = s[i + 2];
+    if (b == 0x80 && ((d >= 0x80 && d <= 0x8A) || d == 0xA8 || d == 0xA9 || d == 0xAF)) return 3;
+    if (b == 0x81 && d == 0x9F) return 3;
+  }
+  if (c == 0xE3 && i + 2 < s.size() && (unsigned char)s[i + 1] == 0x80 && (unsigned char)s[i + 2] == 0x80) return 3;
+  return 0;
+}
+static size_t utf8_len(unsigned char c) { return c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : 4; }
+
+static std::string trim_start(const std::string& s) {
+  size_t i = 0;
+  while (i < s.size()) {
+    const size_t w = ws_len(s, i);
+    if (!w) break;
+    i += w;
+  }
+  return s.substr(i);
+}
+static bool is_ws_end(const std::string& s, size_t end, size_t* w) {   // whitespace code point ending at `end`
+  for (size_t k = 1; k <= 3 && k <= end; ++k) {
+    const size_t st = end - k;
+    if (utf8_len((unsigned char)s[st]) == k || (k == 1 && (unsigned char)s[st] < 0x80)) {
+      if (ws_len(s, st) == k) { *w = k; return true; }
+    }
+  }
+  return false;
+}
+static std::string trim(const std::string& s) {
+  std::string t = trim_start(s);
+  size_t e = t.size(), w;
+  while (e > 0 && is_ws_end(t, e, &w)) e -= w;
+  return t.substr(0, e);
+}
+static std::string trim_nul_then_ws(const std::string& s) {   // s.trim_matches('\0').trim()
+  size_t a = 0, b = s.size();
+  while (a < b && s[a] == '\0') ++a;
+  while (b > a && s[b - 1] == '\0') --b;
+  return trim(s.substr(a, b - a));
+}
+
+// src/transcribe.rs:205-212
+static bool is_whole_control_token(const std::string& s) {
+  const std::string t = trim_nul_then_ws(s);
+  if (!(t.size() >= 2 && t.compare(0, 2, "[_") == 0 && t.back() == ']')) return false;
+  if (t.size() < 3) return false;
+  const std::string inner = t.substr(2, t.size() - 3);
+  if (inner.empty()) return false;
+  for (unsigned char c : inner)
+    if (!((c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '_')) return false;
+  return true;
+}
+
+// src/transcribe.rs:215-240
+static std::string strip_embedded_control_markers(const std::string& s) {
+  std::string r;
+  size_t i = 0;
+  while (i < s.size()) {
+    if (i + 1 < s.size() && s[i] == '[' && s[i + 1] == '_') {
+      size_t j = i + 2;
+      while (j < s.size() && s[j] != ']') ++j;
+      if (j < s.size() && is_whole_control_token(s.substr(i, j - i + 1))) {
+        i = j + 1;
+        continue;
+      }
+    }
+    r.push_back(s[i]);
+    ++i;
+  }
+  return r;
+}
+
+struct Word {
+  std::string text;
+  double start, end;
+  bool has_p;
+  float p;
+};
+struct Seg {
+  double start, end;
+  std::string text;
+  std::vector<Word> words;
+  bool has_words = false;
+  bool has_speaker = false;
+  std::string speaker;
+};
+
+static double cs_to_s(long long cs) { return (double)cs * 0.01; }
+
+// src/transcribe.rs:242-320
+static std::vector<Word> get_token_timestamps(const ResultSeg& seg, const Vocab& v) {
+  struct Tok {
+    std::string text;
+    float p;
+    double t0, t1;
+    bool has_a;
+    double a;
+  };
+  std::vector<Tok> toks;
+  for (const auto& t : seg.tokens) {
+    const std::string& raw = v.id_to_token[t.id];
+    if (is_whole_control_token(raw)) continue;
+    std::string clean = strip_embedded_control_markers(raw);
+    if (trim_nul_then_ws(clean).empty()) continue;
+    toks.push_back({clean, t.p, cs_to_s(t.t0), cs_to_s(t.t1), t.t_dtw >= 0, t.t_dtw >= 0 ? cs_to_s(t.t_dtw) : 0.0});
+  }
+  std::vector<Word> out;
+  for (size_t i = 0; i < toks.size(); ++i) {
+    const bool hp = i > 0 && toks[i - 1].has_a, hh = toks[i].has_a, hn = i + 1 < toks.size() && toks[i + 1].has_a;
+    const double start = (hp && hh) ? 0.5 * (toks[i - 1].a + toks[i].a) : toks[i].t0;
+    const double end = (hh && hn) ? 0.5 * (toks[i].a + toks[i + 1].a) : toks[i].t1;
+    out.push_back({toks[i].text, start, end, true, toks[i].p});
+  }
+  return out;
+}
+
+// src/transcribe.rs:171-203 (alphanumeric count: ASCII alnum + every non-ASCII code point)
+static std::vector<Word> interpolate_word_timestamps(const std::string& line, double start, double end) {
+  std::vector<Word> out;
+  const double dur = std::max(end - start, 0.0);
+  if (dur <= 0.0) return out;
+  std::vector<std::string> toks;
+  size_t i = 0;
+  while (i < line.size()) {
+    size_t w = ws_len(line, i);
+    if (w) { i += w; continue; }
+    size_t j = i;
+    while (j < line.size() && !ws_len(line, j)) j += utf8_len((unsigned char)line[j]);
+    std::string t = line.substr(i, j - i);
+    if (!trim_nul_then_ws(t).empty()) toks.push_back(t);
+    i = j;
+  }
+  if (toks.empty()) return out;
+  std::vector<size_t> wts;
+  size_t tot = 0;
+  for (auto& t : toks) {
+    size_t c = 0;
+    for (size_t k = 0; k < t.size(); k += utf8_len((unsigned char)t[k])) {
+      const unsigned char ch = t[k];
+      if (ch >= 0x80 || std::isalnum(ch)) ++c;
+    }
+    wts.push_back(std::max<size_t>(c, 1));
+    tot += wts.back();
+  }
+  size_t acc = 0;
+  for (size_t k = 0; k < toks.size(); ++k) {
+    const double t0 = start + ((double)acc / tot) * dur;
+    const double t1 = k + 1 == toks.size() ? end : start + ((double)(acc + wts[k]) / tot) * dur;
+    acc += wts[k];
+    out.push_back({toks[k], t0, t1, false, 0.f});
+  }
+  return out;
+}
+
+// ------------------------------------------------------------------ ABI objects
+struct wdr_context {
+  std::unique_ptr<Context> ctx;
+  std::unique_ptr<State> st;
+  double load_s = 0;
+};
+
+struct SynCfg {
+  double weight_std = 0.02, emb_std = 0.02;
+  float force_len_rate = 0.f;
+  bool disable_fallback = false;
+};
+static SynCfg syn_of(const wdr_synthetic* s) {
+  SynCfg c;
+  if (s) {
+    if (s->weight_std > 0) c.weight_std = s->weight_std;
+    if (s->emb_std > 0) c.emb_std = s->emb_std;
+    c.force_len_rate = s->force_len_rate;
+    c.disable_fallback = s->disable_fallback != 0;
+  }
+  return c;
+}
+
+struct wdr_engine {
+  wdr_engine_config cfg{};
+  std::string cache_dir, vad_path, seg_path, emb_path;
+  SynCfg syn;
+  std::map<std::string, std::unique_ptr<wdr_context>> contexts;
+};
+
+// src/transcribe.rs:20-87
+static FullParams setup_params(const wdr_transcribe_options* o, const SynCfg& syn) {
+  FullParams p;
+  const wdr_advanced* a = o ? o->advanced : nullptr;
+  int n = 5;
+  if (a && a->has_best_of_or_beam_size) n = a->best_of_or_beam_size;
+  n = std::max(1, n);
+  p.greedy = a && a->sampling_strategy && std::string(a->sampling_strategy) == "greedy";
+  p.best_of = n;
+  p.beam_size = n;
+  p.suppress_blank = true;
+  p.token_timestamps = true;
+  p.single_segment = true;
+  if (o && o->lang) p.language = o->lang;
+  if (o && o->whisper_to_english == 1) p.translate = true;
+  if (a) {
+    if (a->has_temperature) p.temperature = a->temperature;
+    if (a->has_max_text_ctx) p.n_max_text_ctx = a->max_text_ctx;
+    if (a->init_prompt) {
+      p.initial_prompt = a->init_prompt;
+      p.has_initial_prompt = true;
+    }
+  }
+  p.force_len_rate = syn.force_len_rate;
+  if (syn.disable_fallback) {
+    p.logprob_thold = -INFINITY;
+    p.entropy_thold = -1.f;
+  }
+  return p;
+}
+
+static bool file_exists(const char* p) {
+  struct stat st;
+  return p && stat(p, &st) == 0;
+}
+
+// src/transcribe.rs:89-166.  No ggml loader yet: the named model's
+// hparams are instantiated with synthetic weights.
+static std::unique_ptr<wdr_context> make_context(const std::string& model_name, bool has_dev, int dev, int8_t use_gpu,
+                                                 int8_t enable_dtw, const SynCfg& syn) {
+  HParams hp;
+  if (!hparams_for(model_name, &hp)) throw std::runtime_error("failed to open model: unknown model '" + model_name + "'");
+  ContextParams cp;
+  if (use_gpu == 0) cp.use_gpu = false;
+  if (has_dev) cp.gpu_device = dev;
+  cp.dtw = enable_dtw == 1;
+  cp.flash_attn = false;
+  cp.weight_std = syn.weight_std;
+  cp.emb_std = syn.emb_std;
+  auto c = std::make_unique<wdr_context>();
+  const double t = now_s();
+  try {
+    c->ctx = std::make_unique<Context>(model_name, hp, cp);
+    c->st = std::make_unique<State>(*c->ctx);
+  } catch (const std::exception& ex) {
+    throw std::runtime_error(std::string("create whisper context crash: ") + ex.what());
+  }
+  c->load_s = now_s() - t;
+  return c;
+}
+
+struct CallbackCtx {
+  const wdr_callbacks* cb;
+};
+
+static wdr_segment_list* to_list(const std::vector<Seg>& segs, const std::string* lang) {
+  auto* l = (wdr_segment_list*)calloc(1, sizeof(wdr_segment_list));
+  l->n_segments = segs.size();
+  l->segments = (wdr_segment*)calloc(std::max<size_t>(1, segs.size()), sizeof(wdr_segment));
+  for (size_t i = 0; i < segs.size(); ++i) {
+    wdr_segment& o = l->segments[i];
+    o.start = segs[i].start;
+    o.end = segs[i].end;
+    o.text = strdup(segs[i].text.c_str());
+    if (segs[i].has_words) {
+      auto* w = (wdr_word*)calloc(std::max<size_t>(1, segs[i].words.size()), sizeof(wdr_word));
+      for (size_t k = 0; k < segs[i].words.size(); ++k) {
+        w[k].text = strdup(segs[i].words[k].text.c_str());
+        w[k].start = segs[i].words[k].start;
+        w[k].end = segs[i].words[k].end;
+        w[k].has_probability = segs[i].words[k].has_p;
+        w[k].probability = segs[i].words[k].p;
+      }
+      o.words = w;
+      o.n_words = segs[i].words.size();
+    }
+    o.speaker_id = segs[i].has_speaker ? strdup(segs[i].speaker.c_str()) : nullptr;
+  }
+  l->detected_lang = lang ? strdup(lang->c_str()) : nullptr;
+  return l;
+}
+
+static void emit_segment(const wdr_callbacks* cb, const Seg& s) {
+  if (!cb || !cb->new_segment) return;
+  std::vector<wdr_word> w(s.words.size());
+  for (size_t k = 0; k < s.words.size(); ++k)
+    w[k] = {s.words[k].text.c_str(), s.words[k].start, s.words[k].end, (int8_t)s.words[k].has_p, s.words[k].p};
+  wdr_segment o{s.start, s.end, s.text.c_str(), s.has_words ? w.data() : nullptr, s.has_words ? w.size() : 0,
+                s.has_speaker ? s.speaker.c_str() : nullptr};
+  cb->new_segment(cb->user, &o);
+}
+
+// src/transcribe.rs:323-535 (diarization branch: not yet on this path)
+static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speech_segment>& segs,
+                                     const wdr_transcribe_options* o, const SynCfg& syn, const wdr_callbacks* cb,
+                                     std::string* detected_lang, bool* has_lang) {
+  if (o && o->enable_diarize == 1) throw std::runtime_error("diarization is not available on this path yet");
+  FullParams params = setup_params(o, syn);
+  const Vocab& v = c->ctx->vocab;
+  const double user_offset = (o && o->has_offset) ? o->offset : 0.0;
+  std::vector<Seg> out;
+  bool have_prev = false;
+  std::string previous_text;
+  *has_lang = false;
+  if (o && o->lang && std::string(o->lang) != "auto") {
+    *detected_lang = o->lang;
+    *has_lang = true;
+  }
+  const bool translated = o && o->whisper_to_english == 1;
+  std::vector<float> samples;
+  for (size_t i = 0; i < segs.size(); ++i) {
+    const wdr_speech_segment& ss = segs[i];
+    samples.resize(ss.n_samples);
+    for (size_t k = 0; k < ss.n_samples; ++k) samples[k] = (float)ss.samples[k] / 32768.0f;
+    if (have_prev) {
+      params.initial_prompt = previous_text;
+      params.has_initial_prompt = true;
+    }
+    if (cb && cb->is_cancelled && cb->is_cancelled(cb->user)) throw std::runtime_error("failed to transcribe");
+    int rc;
+    try {
+      rc = c->st->full(params, samples.data(), (int)samples.size());
+    } catch (const std::exception& ex) {
+      throw std::runtime_error(std::string("failed to transcribe: ") + ex.what());
+    }
+    if (rc != 0) throw std::runtime_error("failed to transcribe");
+    if (!*has_lang) {
+      *detected_lang = kLangs[std::max(0, std::min(99, c->st->lang_id))];
+      *has_lang = true;
+    }
+    const double base_offset = ss.start + user_offset;
+    for (const ResultSeg& r : c->st->result_all) {
+      std::string text = trim_start(r.text);
+      const double approx_start = base_offset + cs_to_s(r.t0);
+      const double approx_end = base_offset + cs_to_s(r.t1);
+      std::vector<Word> words;
+      if (translated) {
+        words = interpolate_word_timestamps(text, approx_start, approx_end);
+      } else {
+        words = get_token_timestamps(r, v);
+        for (auto& w : words) {
+          w.start += base_offset;
+          w.end += base_offset;
+        }
+      }
+      const double seg_start = words.empty() ? approx_start : words.front().start;
+      const double seg_end = words.empty() ? approx_end : words.back().end;
+      if (!out.empty()) {
+        Seg& last = out.back();
+        if (last.end > seg_start) last.end = seg_start;
+        if (last.has_words && !last.words.empty() && last.words.back().end > last.end) last.words.back().end = last.end;
+      }
+      have_prev = !trim(text).empty();
+      if (have_prev) previous_text = text;
+      Seg s;
+      s.start = seg_start;
+      s.end = seg_end;
+      s.text = text;
+      s.has_words = !words.empty();
+      s.words = std::move(words);
+      emit_segment(cb, s);
+      if (cb && cb->progress) {
+        const int pct = (int)((double)(i + 1) / (double)segs.size() * 100.0);
+        cb->progress(cb->user, pct, 1, "Transcribing audio");
+      }
+      out.push_back(std::move(s));
+    }
+  }
+  return out;
+}
+
+// ------------------------------------------------------------------ read_wav (src/audio.rs:4-24)
+static std::vector<int16_t> read_wav_impl(const char* path) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("failed to read file");
+  std::vector<char> data((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  auto u32 = [&](size_t o) { uint32_t v; memcpy(&v, &data[o], 4); return v; };
+  auto u16 = [&](size_t o) { uint16_t v; memcpy(&v, &data[o], 2); return v; };
+  if (data.size() < 12 || memcmp(&data[0], "RIFF", 4) || memcmp(&data[8], "WAVE", 4))
+    throw std::runtime_error("failed to read file");
+  size_t pos = 12;
+  bool have_fmt = false, have_data = false;
+  uint16_t tag = 0, ch = 0, bits = 0;
+  uint32_t rate = 0;
+  size_t dpos = 0, dlen = 0;
+  while (pos + 8 <= data.size()) {
+    const uint32_t sz = u32(pos + 4);
+    if (!memcmp(&data[pos], "fmt ", 4) && pos + 8 + 16 <= data.size()) {
+      tag = u16(pos + 8); ch = u16(pos + 10); rate = u32(pos + 12); bits = u16(pos + 22);
+      have_fmt = true;
+    } else if (!memcmp(&data[pos], "data", 4)) {
+      dpos = pos + 8;
+      dlen = std::min<size_t>(sz, data.size() - dpos);
+      have_data = true;
+    }
+    pos += 8 + (size_t)sz + (sz & 1);
+  }
+  if (!have_fmt || !have_data) throw std::runtime_error("failed to read file");
+  if (ch != 1) throw std::runtime_error("expected mono audio file and found " + std::to_string(ch) + " channels!");
+  if (!(tag == 1 || tag == 0xFFFE)) throw std::runtime_error("expected integer sample format");
+  if (rate != 16000) throw std::runtime_error("expected 16KHz sample rate");
+  if (bits != 16) throw std::runtime_error("expected 16 bits per sample");
+  std::vector<int16_t> out(dlen / 2);
+  if (!out.empty()) memcpy(out.data(), &data[dpos], out.size() * 2);
+  return out;
+}
+
+// ------------------------------------------------------------------ ABI
+extern "C" {
+
+const char* wdr_last_error(void) { return g_err.c_str(); }
+int wdr_abi_version(void) { return WDR_ABI_VERSION; }
+int wdr_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+void wdr_free(void* p) { free(p); }
+
+int wdr_engine_new(const wdr_engine_config* cfg, wdr_engine** out) {
+  WDR_GUARD({
+    auto* e = new wdr_engine();
+    if (cfg) {
+      e->cfg = *cfg;
+      if (cfg->cache_dir) e->cache_dir = cfg->cache_dir;
+      if (cfg->vad_model_path) e->vad_path = cfg->vad_model_path;
+      if (cfg->diarize_segment_model_path) e->seg_path = cfg->diarize_segment_model_path;
+      if (cfg->diarize_embedding_model_path) e->emb_path = cfg->diarize_embedding_model_path;
+    } else {
+      e->cfg.enable_dtw = 1;
+      e->cfg.enable_flash_attn = 0;
+      e->cfg.use_gpu = 1;
+      e->cache_dir = "./cache";
+    }
+    *out = e;
+    return 0;
+  })
+}
+
+void wdr_engine_free(wdr_engine* e) { delete e; }
+
+int wdr_engine_set_synthetic(wdr_engine* e, const wdr_synthetic* syn) {
+  WDR_GUARD({
+    e->syn = syn_of(syn);
+    e->contexts.clear();
+    return 0;
+  })
+}
+
+int wdr_transcribe_audio(wdr_engine* e, const char* audio_path, const wdr_transcribe_options* o,
+                         const wdr_formatting_overrides* fmt, const wdr_callbacks* cb, wdr_segment_list** out) {
+  (void)fmt;
+  WDR_GUARD({
+    if (!audio_path || !file_exists(audio_path)) return fail("audio file doesn't exist");
+    const std::string model = (o && o->model) ? o->model : "base";
+    std::vector<int16_t> pcm = read_wav_impl(audio_path);
+    std::vector<wdr_speech_segment> segs;
+    if (o && o->enable_diarize == 1) return fail("diarization is not available on this path yet");
+    const bool vad = !o || o->enable_vad != 0;   // default Some(true)
+    if (vad) return fail("Silero VAD is not available on this path yet (set enable_vad = false)");
+    segs.push_back({0.0, (double)pcm.size() / 16000.0, pcm.data(), pcm.size()});
+    auto it = e->contexts.find(model);
+    if (it == e->contexts.end()) {
+      it = e->contexts.emplace(model, make_context(model, e->cfg.has_gpu_device, e->cfg.gpu_device, e->cfg.use_gpu,
+                                                   e->cfg.enable_dtw, e->syn)).first;
+    }
+    if (o && o->translate_target && !(o->whisper_to_english == 1))
+      return fail("translate_target: network translation is out of scope for libwdr");
+    std::string lang;
+    bool has_lang = false;
+    std::vector<Seg> res = run_pipeline(it->second.get(), segs, o, e->syn, cb, &lang, &has_lang);
+    *out = to_list(res, has_lang ? &lang : nullptr);
+    return 0;
+  })
+}
+
+int wdr_read_wav(const char* path, int16_t** samples, size_t* n) {
+  WDR_GUARD({
+    std::vector<int16_t> v = read_wav_impl(path);
+    *samples = (int16_t*)malloc(std::max<size_t>(1, v.size()) * 2);
+    if (!v.empty()) memcpy(*samples, v.data(), v.size() * 2);
+    *n = v.size();
+    return 0;
+  })
+}
+
+// src/vad.rs:33-84: input = whisper.cpp VAD segments in centiseconds
+int wdr_vad_merge(const double* st_cs, const double* en_cs, size_t n_segs, const int16_t* samples, size_t n_samples,
+                  double* mask_out, size_t* n_mask, double* merged_out, int64_t* merged_idx, size_t* n_merged) {
+  (void)samples;
+  WDR_GUARD({
+    std::vector<std::pair<double, double>> mask;
+    for (size_t i = 0; i < n_segs; ++i) {
+      const double a = (double)(float)st_cs[i] / 100.0, b = (double)(float)en_cs[i] / 100.0;
+      if (b > a) mask.push_back({a, b});
+    }
+    std::stable_sort(mask.begin(), mask.end(), [](auto& x, auto& y) { return x.first < y.first; });
+    std::vector<std::pair<double, double>> merged;
+    for (auto& m : mask) {
+      if (!merged.empty() && m.first - merged.back().second < 0.200) merged.back().second = std::max(m.second, merged.back().second);
+      else merged.push_back(m);
+    }
+    const float SR = 16000.0f, nf = (float)n_samples;
+    size_t k = 0;
+    for (auto& m : merged) {
+      const size_t si = (size_t)std::min(std::max(std::round((float)m.first * SR), 0.0f), nf);
+      const size_t ei = (size_t)std::min(std::max(std::round((float)m.second * SR), 0.0f), nf);
+      if (!(m.second > m.first) || !(ei > si)) continue;
+      merged_out[2 * k] = m.first;
+      merged_out[2 * k + 1] = m.second;
+      merged_idx[2 * k] = (int64_t)si;
+      merged_idx[2 * k + 1] = (int64_t)ei;
+      ++k;
+    }
+    for (size_t i = 0; i < mask.size(); ++i) {
+      mask_out[2 * i] = mask[i].first;
+      mask_out[2 * i + 1] = mask[i].second;
+    }
+    *n_mask = mask.size();
+    *n_merged = k;
+    return 0;
+  })
+}
+
+int wdr_context_create(const char* model_path, const char* model_name, int8_t has_gpu_device, int32_t gpu_device,
+                       int8_t use_gpu, int8_t enable_dtw, int8_t enable_flash_attn, int8_t has_num_samples,
+                       uint64_t num_samples, const wdr_synthetic* syn, wdr_context** out) {
+  (void)enable_flash_attn;
+  (void)has_num_samples;
+  (void)num_samples;
+  WDR_GUARD({
+    if (model_path && *model_path && !file_exists(model_path)) return fail("whisper file doesn't exist");
+    *out = make_context(model_name ? model_name : "base", has_gpu_device == 1, gpu_device, use_gpu, enable_dtw,
+                        syn_of(syn))
+               .release();
+    return 0;
+  })
+}
+
+void wdr_context_free(wdr_context* c) { delete c; }
+
+int wdr_run_pipeline(wdr_context* c, const wdr_speech_segment* segs, size_t n_segs, const wdr_transcribe_options* o,
+                     const wdr_synthetic* syn, const wdr_callbacks* cb, wdr_segment_list** out) {
+  WDR_GUARD({
+    std::vector<wdr_speech_segment> v(segs, segs + n_segs);
+    std::string lang;
+    bool has_lang = false;
+    const double t = now_s();
+    c->st->times = StageTimes{};
+    std::vector<Seg> res = run_pipeline(c, v, o, syn_of(syn), cb, &lang, &has_lang);
+    c->st->times.glue = now_s() - t;   // total wall for this pipeline call
+    *out = to_list(res, has_lang ? &lang : nullptr);
+    return 0;
+  })
+}
+
+void wdr_segment_list_free(wdr_segment_list* l) {
+  if (!l) return;
+  for (size_t i = 0; i < l->n_segments; ++i) {
+    wdr_segment& s = l->segments[i];
+    free((void*)s.text);
+    for (size_t k = 0; k < s.n_words; ++k) free((void*)s.words[k].text);
+    free((void*)s.words);
+    free((void*)s.speaker_id);
+  }
+  free(l->segments);
+  free((void*)l->detected_lang);
+  free(l);
+}
+
+int wdr_context_stage_times(wdr_context* c, wdr_stage_times* o) {
+  WDR_GUARD({
+    const StageTimes& t = c->st->times;
+    *o = wdr_stage_times{t.mel, t.encode, t.decode, t.dtw, 0.0, t.glue, t.windows, t.decode_steps, t.prefills};
+    return 0;
+  })
+}
+
+int wdr_context_hparams(wdr_context* c, int32_t* o) {
+  WDR_GUARD({
+    const HParams& h = c->ctx->model.hp;
+    const int32_t v[10] = {h.n_vocab, h.n_audio_ctx, h.n_audio_state, h.n_audio_head, h.n_audio_layer,
+                           h.n_text_ctx, h.n_text_state, h.n_text_head, h.n_text_layer, h.n_mels};
+    memcpy(o, v, sizeof v);
+    return 0;
+  })
+}
+
+int wdr_state_full(wdr_context* c, const float* samples, size_t n, const wdr_transcribe_options* o,
+                   const wdr_synthetic* syn, const char* initial_prompt, wdr_result_seg** segs, size_t* n_segs,
+                   int32_t* lang_id) {
+  WDR_GUARD({
+    FullParams p = setup_params(o, syn_of(syn));
+    if (initial_prompt) {
+      p.initial_prompt = initial_prompt;
+      p.has_initial_prompt = true;
+    }
+    const int rc = c->st->full(p, samples, (int)n);
+    if (rc != 0) return fail("failed to transcribe");
+    const auto& r = c->st->result_all;
+    *n_segs = r.size();
+    *segs = (wdr_result_seg*)calloc(std::max<size_t>(1, r.size()), sizeof(wdr_result_seg));
+    for (size_t i = 0; i < r.size(); ++i) {
+      (*segs)[i].t0 = r[i].t0;
+      (*segs)[i].t1 = r[i].t1;
+      (*segs)[i].text = strdup(r[i].text.c_str());
+      auto* t = (wdr_token*)calloc(std::max<size_t>(1, r[i].tokens.size()), sizeof(wdr_token));
+      for (size_t k = 0; k < r[i].tokens.size(); ++k) {
+        const TokenData& d = r[i].tokens[k];
+        t[k] = {d.id, d.tid, d.p, d.plog, d.pt, d.ptsum, d.t0, d.t1, d.t_dtw};
+      }
+      (*segs)[i].tokens = t;
+      (*segs)[i].n_tokens = r[i].tokens.size();
+    }
+    *lang_id = c->st->lang_id;
+    return 0;
+  })
+}
+
+void wdr_result_free(wdr_result_seg* segs, size_t n) {
+  if (!segs) return;
+  for (size_t i = 0; i < n; ++i) {
+    free((void*)segs[i].text);
+    free((void*)segs[i].tokens);
+  }
+  free(segs);
+}
+
+int wdr_dbg_log_mel(wdr_context* c, const float* x, size_t n, int32_t seek, float* out) {
+  WDR_GUARD({
+    c->st->compute_mel(x, (int)n);
+    c->st->read_mel_window(seek, out);
+    return 0;
+  })
+}
+
+int wdr_dbg_energy(const float* x, size_t n, float* out) {
+  WDR_GUARD({
+    DevMem dx(std::max<size_t>(1, n) * 4), de(std::max<size_t>(1, n) * 4);
+    WDR_HIP(hipMemcpy(dx.p, x, n * 4, hipMemcpyHostToDevice));
+    launch_energy(dx.as<float>(), (int)n, de.as<float>(), nullptr);
+    WDR_HIP(hipMemcpy(out, de.p, n * 4, hipMemcpyDeviceToHost));
+    return 0;
+  })
+}
+
+int wdr_dbg_encode(wdr_context* c, const float* mel_window, float* enc_out) {
+  WDR_GUARD({
+    c->st->encode_from_mel_window(mel_window);
+    c->st->read_encoder_out(enc_out);
+    return 0;
+  })
+}
+
+int wdr_dbg_decode(wdr_context* c, const int32_t* tokens, size_t n, float* logits_out) {
+  WDR_GUARD({
+    c->st->decode_logits(tokens, (int)n, logits_out);
+    return 0;
+  })
+}
+
+int wdr_dbg_capture(wdr_context* c, const int32_t* tokens, size_t n, float* cap_out) {
+  WDR_GUARD({
+    if (c->ctx->aheads.empty()) return fail("context created without DTW");
+    c->st->dtw_capture(tokens, (int)n, cap_out);
+    return 0;
+  })
+}
+
+int wdr_dbg_dtw(const float* cap, int32_t A, int32_t N, int32_t M, int32_t sot_len, int32_t seek, float* x_out,
+                int32_t* times_out, int32_t* n_times) {
+  WDR_GUARD({
+    DevMem dcap((size_t)A * N * 1500 * 4), dn((size_t)A * N * M * 4), dx((size_t)N * M * 4), dt((N + 8) * 4);
+    WDR_HIP(hipMemcpy(dcap.p, cap, dcap.bytes, hipMemcpyHostToDevice));
+    launch_dtw(dcap.as<float>(), A, N, 1500, M, sot_len, seek, dn.as<float>(), dx.as<float>(), dt.as<int>(),
+               dt.as<int>() + N + 4, nullptr);
+    WDR_HIP(hipDeviceSynchronize());
+    const int rows = N - sot_len - 1;
+    WDR_HIP(hipMemcpy(x_out, dx.p, (size_t)rows * M * 4, hipMemcpyDeviceToHost));
+    std::vector<int> t(N + 8);
+    WDR_HIP(hipMemcpy(t.data(), dt.p, t.size() * 4, hipMemcpyDeviceToHost));
+    *n_times = t[N + 4];
+    for (int i = 0; i < *n_times; ++i) times_out[i] = t[i];
+    return 0;
+  })
+}
+
+int wdr_dbg_dtw_dp(const float* x, int32_t rows, int32_t cols, int32_t seek, int32_t* times_out, int32_t* n_times) {
+  WDR_GUARD({
+    DevMem dx((size_t)rows * cols * 4), dt((rows + 8) * 4);
+    WDR_HIP(hipMemcpy(dx.p, x, dx.bytes, hipMemcpyHostToDevice));
+    launch_dtw_dp_only(dx.as<float>(), rows, cols, seek, dt.as<int>(), dt.as<int>() + rows + 4, nullptr);
+    std::vector<int> t(rows + 8);
+    WDR_HIP(hipMemcpy(t.data(), dt.p, t.size() * 4, hipMemcpyDeviceToHost));
+    *n_times = t[rows + 4];
+    for (int i = 0; i < *n_times; ++i) times_out[i] = t[i];
+    return 0;
+  })
+}
+
+int wdr_dbg_proj(const uint16_t* a16, const uint16_t* w16, const float* bias, int32_t M, int32_t N, int32_t K,
+                 int32_t epi, float* out) {
+  WDR_GUARD({
+    DevMem da((size_t)M * K * 2), dw((size_t)N * K * 2), db(bias ? (size_t)N * 4 : 0), dout((size_t)M * N * 4);
+    WDR_HIP(hipMemcpy(da.p, a16, da.bytes, hipMemcpyHostToDevice));
+    WDR_HIP(hipMemcpy(dw.p, w16, dw.bytes, hipMemcpyHostToDevice));
+    if (bias) WDR_HIP(hipMemcpy(db.p, bias, db.bytes, hipMemcpyHostToDevice));
+    const bool f16out = epi == EPI_F16 || epi == EPI_F16_GELU;
+    std::vector<f16> h16;
+    if (!f16out) WDR_HIP(hipMemcpy(dout.p, out, dout.bytes, hipMemcpyHostToDevice));
+    ProjArgs a{da.as<f16>(), K, dw.as<f16>(), K, bias ? db.as<float>() : nullptr, dout.p, N, nullptr, 0, M, N, K, epi};
+    launch_proj(a, nullptr);
+    WDR_HIP(hipDeviceSynchronize());
+    if (f16out) {
+      h16.resize((size_t)M * N);
+      WDR_HIP(hipMemcpy(h16.data(), dout.p, h16.size() * 2, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < h16.size(); ++i) out[i] = (float)h16[i];
+    } else {
+      WDR_HIP(hipMemcpy(out, dout.p, dout.bytes, hipMemcpyDeviceToHost));
+    }
+    return 0;
+  })
+}
+
+int wdr_dbg_attn(const uint16_t* q, const uint16_t* k, const uint16_t* v, int32_t Tq, int32_t Tk, int32_t H,
+                 int32_t causal, float* out) {
+  WDR_GUARD({
+    const int d = H * 64;
+    DevMem dq((size_t)Tq * d * 2), dk((size_t)Tk * d * 2), dv((size_t)Tk * d * 2), dout((size_t)Tq * d * 2);
+    WDR_HIP(hipMemcpy(dq.p, q, dq.bytes, hipMemcpyHostToDevice));
+    WDR_HIP(hipMemcpy(dk.p, k, dk.bytes, hipMemcpyHostToDevice));
+    WDR_HIP(hipMemcpy(dv.p, v, dv.bytes, hipMemcpyHostToDevice));
+    FlashArgs fa{dq.as<f16>(), d, 0, dk.as<f16>(), d, 0, dv.as<f16>(), d, 0, dout.as<f16>(), d, 0, nullptr, Tq, Tk, H,
+                 causal, 0.125f};
+    launch_flash_attn(fa, 1, nullptr);
+    std::vector<f16> h((size_t)Tq * d);
+    WDR_HIP(hipMemcpy(h.data(), dout.p, h.size() * 2, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < h.size(); ++i) out[i] = (float)h[i];
+    return 0;
+  })
+}
+
+}  // extern "C"

@@ -1,0 +1,324 @@
+// Attention kernels (SURVEY.md §8(a) a6 encoder self-attention, a9 decoder self- and
+// cross-attention, a12 alignment-head capture for DTW).
+//
+//  * k_flash_attn   — MFMA flash attention for >8 query rows (encoder T=1500, prompt
+//    prefill, DTW re-forward).  Swapped product S^T = K.Q^T so that a query's scores live
+//    in ONE lane pair (lane, lane^32): the row max / row sum need one lane exchange, and the
+//    f32 accumulator tile of S^T is directly the B operand of O^T = V^T.P^T (no LDS round
+//    trip for P).  K tile staged row-major (72-half stride: conflict-free ds_read_b128),
+//    V staged transposed (68-half stride: conflict-free ds_read_b64).  d_head = 64.
+//    Optionally writes each query row's (max, sum) so the DTW capture can materialise the
+//    exact softmax of the alignment heads without a second full pass.
+//  * k_dec_self_attn — one wave per (decoder row, head) over that row's KV cache.
+//  * k_xattn_partial / k_xattn_combine — split-K ("flash decode") cross-attention for the
+//    <=8 decoder rows of a step: the 1500 cross keys are split in 128-key chunks over
+//    workgroups so every CU streams the cross K/V once for all beams.
+//  * k_aheads_capture — softmax(QK^T) of the alignment heads over all 1500 keys.
+#include "../common.h"
+#include "kernels.h"
+
+namespace wdr {
+
+
+constexpr int FA_KB = 64, FA_KS = 72, FA_VS = 68;
+
+__global__ __launch_bounds__(256) void k_flash_attn(FlashArgs a) {
+  __shared__ __attribute__((aligned(16))) f16 Ks[FA_KB * FA_KS];
+  __shared__ __attribute__((aligned(16))) f16 Vt[64 * FA_VS];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const f16* Q = a.q + b * a.q_bs + h * 64;
+  const f16* K = a.k + b * a.k_bs + h * 64;
+  const f16* V = a.v + b * a.v_bs + h * 64;
+  const int fr = lane & 31, hh = lane >> 5;
+  const int qrow = qb * 128 + wid * 32 + fr;
+  const int qrow_c = qrow < a.Tq ? qrow : a.Tq - 1;
+
+  f16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = *(const f16x8*)(Q + (long long)qrow_c * a.ldq + 16 * s + 8 * hh);
+
+  f32x16 o0, o1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; }
+  float m = -INFINITY, l = 0.f;
+  int kmax = a.Tk;
+  if (a.causal) {
+    const int last_q = qb * 128 + 127;
+    kmax = kmax < last_q + 1 ? kmax : last_q + 1;
+  }
+  for (int k0 = 0; k0 < kmax; k0 += FA_KB) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c >> 3, col = (c & 7) * 8;
+      int key = k0 + r;
+      key = key < a.Tk ? key : a.Tk - 1;
+      const f16x8 kv = *(const f16x8*)(K + (long long)key * a.ldk + col);
+      *(f16x8*)(Ks + r * FA_KS + col) = kv;
+      const f16x8 vv = *(const f16x8*)(V + (long long)key * a.ldv + col);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) Vt[(col + e) * FA_VS + r] = vv[e];
+    }
+    __syncthreads();
+    f32x16 st[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st[t][r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const f16x8 af = *(const f16x8*)(Ks + (32 * t + fr) * FA_KS + 16 * s + 8 * hh);
+        st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, qf[s], st[t], 0, 0, 0);
+      }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const bool ok = key < a.Tk && (!a.causal || key <= qrow);
+        const float sv = ok ? st[t][r] * a.scale : -INFINITY;
+        st[t][r] = sv;
+        mx = fmaxf(mx, sv);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m, mx);
+    const float alpha = (mnew == -INFINITY) ? 1.f : __expf(m - mnew);
+    float rs = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = (st[t][r] == -INFINITY) ? 0.f : __expf(st[t][r] - mnew);
+        st[t][r] = p;
+        rs += p;
+      }
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mnew;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        f16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[j] = (f16)st[t][8 * s + j];
+        const int kc = 32 * t + 16 * s + 4 * hh;
+        f16x8 va0, va1;
+        {
+          const f16x4 lo = *(const f16x4*)(Vt + (fr)*FA_VS + kc);
+          const f16x4 hi = *(const f16x4*)(Vt + (fr)*FA_VS + kc + 8);
+          va0 = (f16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+        {
+          const f16x4 lo = *(const f16x4*)(Vt + (32 + fr) * FA_VS + kc);
+          const f16x4 hi = *(const f16x4*)(Vt + (32 + fr) * FA_VS + kc + 8);
+          va1 = (f16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+        o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(va0, pb, o0, 0, 0, 0);
+        o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(va1, pb, o1, 0, 0, 0);
+      }
+  }
+  if (qrow < a.Tq) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    f16* O = a.o + b * a.o_bs + (long long)qrow * a.ldo + h * 64;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f16x4 w0, w1;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        w0[e] = (f16)(o0[4 * g + e] * inv);
+        w1[e] = (f16)(o1[4 * g + e] * inv);
+      }
+      *(f16x4*)(O + 8 * g + 4 * hh) = w0;
+      *(f16x4*)(O + 32 + 8 * g + 4 * hh) = w1;
+    }
+    if (a.ml && hh == 0) a.ml[((long long)b * a.n_head + h) * a.Tq + qrow] = make_float2(m, l);
+  }
+}
+
+void launch_flash_attn(const FlashArgs& a, int n_batch, hipStream_t s) {
+  WDR_CHECK(a.Tq > 0 && a.Tk > 0, "attention: empty");
+  dim3 grid(cdiv(a.Tq, 128), a.n_head, n_batch);
+  hipLaunchKernelGGL(k_flash_attn, grid, dim3(256), 0, s, a);
+  WDR_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------- decoder self-attention
+
+__global__ __launch_bounds__(64) void k_dec_self_attn(DecSelfArgs a) {
+  __shared__ float qs[64];
+  __shared__ float sc[448];
+  const int r = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
+  const int seq = a.row_seq[r];
+  const int nk = a.row_pos[r] + 1;
+  qs[lane] = (float)a.q[(long long)r * a.ldq + h * 64 + lane];
+  __syncthreads();
+  const f16* K = a.kc + seq * a.seq_stride + h * 64;
+  const f16* V = a.vc + seq * a.seq_stride + h * 64;
+  float mx = -INFINITY;
+  for (int k = lane; k < nk; k += 64) {
+    const f16* kr = K + (long long)k * a.d;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 64; c += 8) {
+      const f16x8 kv = *(const f16x8*)(kr + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += qs[c + e] * (float)kv[e];
+    }
+    s *= a.scale;
+    sc[k] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int k = lane; k < nk; k += 64) {
+    const float p = __expf(sc[k] - mx);
+    sc[k] = p;
+    sum += p;
+  }
+  sum = wave_sum(sum);
+  __syncthreads();
+  const float inv = 1.f / sum;
+  float acc = 0.f;
+  for (int k = 0; k < nk; ++k) {
+    const float p = (float)(f16)(sc[k] * inv);
+    acc += p * (float)V[(long long)k * a.d + lane];
+  }
+  a.o[(long long)r * a.ldo + h * 64 + lane] = (f16)acc;
+}
+
+void launch_dec_self_attn(const DecSelfArgs& a, int R, int n_head, hipStream_t s) {
+  hipLaunchKernelGGL(k_dec_self_attn, dim3(R, n_head), dim3(64), 0, s, a);
+  WDR_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------- decoder cross-attention (split)
+
+constexpr int XA_KC = 128, XA_RMAX = 8;
+
+__global__ __launch_bounds__(256) void k_xattn_partial(XAttnArgs a) {
+  __shared__ float qs[XA_RMAX][64];
+  __shared__ float sc[XA_RMAX][XA_KC];
+  __shared__ float red[4][XA_RMAX][64];
+  __shared__ float2 mls[XA_RMAX];
+  const int c = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
+  const int R = a.R;
+  for (int i = tid; i < R * 64; i += 256) qs[i / 64][i % 64] = (float)a.q[(long long)(i / 64) * a.ldq + h * 64 + (i % 64)];
+  __syncthreads();
+  const int key0 = c * XA_KC;
+  if (tid < XA_KC) {
+    const int key = key0 + tid;
+    if (key < a.Tk) {
+      const f16* kr = a.k + (long long)key * a.ldkv + h * 64;
+      f16x8 kv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kv[j] = *(const f16x8*)(kr + 8 * j);
+      for (int r = 0; r < R; ++r) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s += qs[r][8 * j + e] * (float)kv[j][e];
+        sc[r][tid] = s * a.scale;
+      }
+    } else {
+      for (int r = 0; r < R; ++r) sc[r][tid] = -INFINITY;
+    }
+  }
+  __syncthreads();
+  const int wid = tid >> 6, lane = tid & 63;
+  for (int r = wid; r < R; r += 4) {
+    const float s0 = sc[r][lane], s1 = sc[r][lane + 64];
+    const float mx = wave_max(fmaxf(s0, s1));
+    const float p0 = s0 == -INFINITY ? 0.f : __expf(s0 - mx);
+    const float p1 = s1 == -INFINITY ? 0.f : __expf(s1 - mx);
+    sc[r][lane] = p0;
+    sc[r][lane + 64] = p1;
+    const float l = wave_sum(p0 + p1);
+    if (lane == 0) mls[r] = make_float2(mx, l);
+  }
+  __syncthreads();
+  const int dh = tid & 63, qtr = tid >> 6;
+  float acc[XA_RMAX];
+#pragma unroll
+  for (int r = 0; r < XA_RMAX; ++r) acc[r] = 0.f;
+  for (int kk = qtr * 32; kk < qtr * 32 + 32; ++kk) {
+    const int key = key0 + kk;
+    if (key >= a.Tk) break;
+    const float vv = (float)a.v[(long long)key * a.ldkv + h * 64 + dh];
+#pragma unroll
+    for (int r = 0; r < XA_RMAX; ++r)
+      if (r < R) acc[r] += (float)(f16)sc[r][kk] * vv;
+  }
+#pragma unroll
+  for (int r = 0; r < XA_RMAX; ++r)
+    if (r < R) red[qtr][r][dh] = acc[r];
+  __syncthreads();
+  for (int i = tid; i < R * 64; i += 256) {
+    const int r = i / 64, d = i % 64;
+    const float s = red[0][r][d] + red[1][r][d] + red[2][r][d] + red[3][r][d];
+    a.part_o[(((long long)c * R + r) * a.n_head + h) * 64 + d] = s;
+  }
+  if (tid < R) a.part_ml[((long long)c * R + tid) * a.n_head + h] = mls[tid];
+}
+
+__global__ __launch_bounds__(64) void k_xattn_combine(XAttnArgs a, int nsplit) {
+  const int r = blockIdx.x, h = blockIdx.y, d = threadIdx.x;
+  float M = -INFINITY;
+  for (int c = 0; c < nsplit; ++c) M = fmaxf(M, a.part_ml[((long long)c * a.R + r) * a.n_head + h].x);
+  float L = 0.f, acc = 0.f;
+  for (int c = 0; c < nsplit; ++c) {
+    const float2 ml = a.part_ml[((long long)c * a.R + r) * a.n_head + h];
+    const float w = ml.x == -INFINITY ? 0.f : __expf(ml.x - M);
+    L += ml.y * w;
+    acc += a.part_o[(((long long)c * a.R + r) * a.n_head + h) * 64 + d] * w;
+  }
+  a.o[(long long)r * a.ldo + h * 64 + d] = (f16)(acc / L);
+}
+
+void launch_xattn(const XAttnArgs& a, hipStream_t s) {
+  WDR_CHECK(a.R >= 1 && a.R <= XA_RMAX, "cross-attention decode: R out of range");
+  const int nsplit = cdiv(a.Tk, XA_KC);
+  hipLaunchKernelGGL(k_xattn_partial, dim3(nsplit, a.n_head), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_xattn_combine, dim3(a.R, a.n_head), dim3(64), 0, s, a, nsplit);
+  WDR_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------- alignment-head capture
+
+__global__ __launch_bounds__(256) void k_aheads_capture(CaptureArgs a) {
+  __shared__ float qs[64];
+  const int r = blockIdx.x, i = blockIdx.y, tid = threadIdx.x;
+  const int h = a.heads[i];
+  if (tid < 64) qs[tid] = (float)a.q[(long long)r * a.ldq + h * 64 + tid];
+  __syncthreads();
+  // identical arithmetic to k_flash_attn's f32 accumulate is not guaranteed; the capture
+  // recomputes q.k in f32 from the same f16 operands.
+  const float2 ml = a.ml[(long long)h * a.R + r];
+  const float inv = 1.f / ml.y;
+  float* out = a.out + ((long long)(a.slot0 + i) * a.R + r) * a.Tk;
+  for (int key = tid; key < a.Tk; key += 256) {
+    const f16* kr = a.k + (long long)key * a.ldk + h * 64;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 64; c += 8) {
+      const f16x8 kv = *(const f16x8*)(kr + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += qs[c + e] * (float)kv[e];
+    }
+    out[key] = __expf(s * a.scale - ml.x) * inv;
+  }
+}
+
+void launch_aheads_capture(const CaptureArgs& a, int n_sel, hipStream_t s) {
+  hipLaunchKernelGGL(k_aheads_capture, dim3(a.R, n_sel), dim3(256), 0, s, a);
+  WDR_HIP(hipGetLastError());
+}
+
+}  // namespace wdr

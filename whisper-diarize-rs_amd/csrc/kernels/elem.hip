@@ -1,0 +1,639 @@
+// Front-end, normalisation, decoding-rule and alignment kernels (HBM / latency bound).
+//
+//  k_mel_frames      a4  log-mel: reflect/zero padding, periodic Hann(400), 201-bin DFT
+//                        (f32, LDS twiddle table), mel dot in double, log10, global max.
+//  k_im2col_mel      a4/a5 clamp (max-8) + (x+4)/4 normalisation fused into the conv1
+//                        im2col of one 3000-frame window (f16, ggml im2col precision).
+//  k_im2col_conv2    a5  stride-2 im2col of the conv1 output.
+//  k_energy          a3  whisper.cpp get_signal_energy, bit-exact (same f32 add order).
+//  k_layernorm       a6/a9 ggml_norm (double sums) * gamma + beta -> f16 matmul input.
+//  k_embed           a9  token + positional embedding.
+//  k_kv_scatter      a9  K/V rows of the current tokens into the self-attention cache.
+//  k_logits_process  a10 whisper.cpp whisper_process_logits + greedy pick + timestamp
+//                        probabilities + no-speech probability, one workgroup per row.
+//  k_dtw_norm / k_dtw_medmean / k_dtw_dp   a12 DTW preprocessing and the DP
+//                        (anti-diagonal wavefront, 2-bit trace in LDS, backtrace).
+//  k_synth_fill      synthetic seeded weights (oracle/weights.py hash, bit-identical).
+#include "../common.h"
+#include "kernels.h"
+
+namespace wdr {
+
+// ---------------------------------------------------------------- synthetic weights
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  uint64_t z = x;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// dst [rows][dst_cols]; element (r, c < src_cols) is element r*src_cols + c of the named tensor,
+// padding columns are zero.  mode 0 = hash, mode 1 = constant cval.
+__global__ void k_synth_fill(void* dst, long long rows, int src_cols, int dst_cols, uint64_t seed, float scale,
+                             int is_f16, float cval, int mode) {
+  const long long n = rows * dst_cols;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const long long r = i / dst_cols;
+    const int c = (int)(i - r * dst_cols);
+    float w = 0.f;
+    if (c < src_cols) {
+      if (mode == 0) {
+        const uint64_t h = splitmix64(seed + (uint64_t)(r * src_cols + c));
+        const float v = (float)(uint32_t)(h >> 40) * 1.1920928955078125e-07f - 1.0f;
+        w = v * scale;
+      } else {
+        w = cval;
+      }
+    }
+    if (is_f16) ((f16*)dst)[i] = (f16)w;
+    else ((float*)dst)[i] = w;
+  }
+}
+
+void launch_synth_fill(void* dst, long long rows, int src_cols, int dst_cols, uint64_t seed, float scale, bool f16out,
+                       int mode, float cval, hipStream_t s) {
+  const long long n = rows * dst_cols;
+  long long blocks = (n + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k_synth_fill, dim3((unsigned)blocks), dim3(256), 0, s, dst, rows, src_cols, dst_cols, seed, scale,
+                     f16out ? 1 : 0, cval, mode);
+  WDR_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------- log-mel
+__device__ __forceinline__ int f2ord(float f) {
+  int i = __float_as_int(f);
+  return i >= 0 ? i : i ^ 0x7FFFFFFF;
+}
+__device__ __forceinline__ float ord2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7FFFFFFF); }
+
+constexpr int MEL_FB = 8;   // frames per workgroup
+
+__global__ __launch_bounds__(256) void k_mel_frames(MelArgs a) {
+  __shared__ float xs[MEL_FB][400];
+  __shared__ float cs[400], sn[400];
+  __shared__ float pw[MEL_FB][201];
+  __shared__ int bmax;
+  const int tid = threadIdx.x;
+  const int f0 = blockIdx.x * MEL_FB;
+  if (tid == 0) bmax = f2ord(-INFINITY);
+  for (int i = tid; i < 400; i += 256) {
+    cs[i] = a.cos_tab[i];
+    sn[i] = a.sin_tab[i];
+  }
+  const int n = a.n;
+  const int n_eff = n + 200;
+  for (int i = tid; i < MEL_FB * 400; i += 256) {
+    const int fl = i / 400, j = i % 400;
+    const int f = f0 + fl;
+    float v = 0.f;
+    if (f < a.n_frames) {
+      const int p = f * 160 + j;             // index into the padded signal
+      if (p < n_eff) {
+        if (p >= 200) v = a.x[p - 200];
+        else {
+          const int src = 200 - p;           // reverse_copy(samples + 1, samples + 201)
+          v = src < n ? a.x[src] : 0.f;
+        }
+      }
+      v *= a.hann[j];
+    }
+    xs[fl][j] = v;
+  }
+  __syncthreads();
+  for (int i = tid; i < MEL_FB * 201; i += 256) {
+    const int fl = i / 201, k = i % 201;
+    float re = 0.f, im = 0.f;
+    int idx = 0;
+    for (int j = 0; j < 400; ++j) {
+      const float xv = xs[fl][j];
+      re = fmaf(xv, cs[idx], re);
+      im = fmaf(xv, sn[idx], im);
+      idx += k;
+      if (idx >= 400) idx -= 400;
+    }
+    pw[fl][k] = re * re + im * im;
+  }
+  __syncthreads();
+  int lmax = f2ord(-INFINITY);
+  for (int i = tid; i < MEL_FB * a.n_mels; i += 256) {
+    const int fl = i / a.n_mels, mm = i % a.n_mels;
+    const int f = f0 + fl;
+    if (f >= a.n_frames) continue;
+    const float* flt = a.filters + mm * 201;
+    double sum = 0.0;
+    for (int k = 0; k < 201; ++k) sum += (double)(pw[fl][k] * flt[k]);
+    const double lv = log10(sum > 1e-10 ? sum : 1e-10);
+    const float out = (float)lv;
+    a.mel[(long long)f * a.n_mels + mm] = out;
+    lmax = max(lmax, f2ord(out));
+  }
+  atomicMax(&bmax, lmax);
+  __syncthreads();
+  if (tid == 0) atomicMax(a.gmax, bmax);
+}
+
+void launch_mel(const MelArgs& a, hipStream_t s) {
+  if (a.n_frames > 0) {
+    hipLaunchKernelGGL(k_mel_frames, dim3(cdiv(a.n_frames, MEL_FB)), dim3(256), 0, s, a);
+    WDR_HIP(hipGetLastError());
+  }
+}
+
+__device__ __forceinline__ float mel_norm(float raw, float gmax) {
+  const double mmax = (double)gmax - 8.0;
+  double v = raw;
+  float f = raw;
+  if (v < mmax) f = (float)mmax;
+  return (float)(((double)f + 4.0) / 4.0);
+}
+
+__global__ void k_im2col_mel(Im2colMelArgs a) {
+  const long long total = 3000ll * a.kp;
+  const float gmax = ord2f(*a.gmax);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int t = (int)(i / a.kp), col = (int)(i % a.kp);
+    float v = 0.f;
+    if (col < a.n_mels * 3) {
+      const int ci = col / 3, k = col % 3;
+      const int u = t + k - 1;
+      if (u >= 0 && u < 3000) {
+        const int f = a.seek + u;
+        const float raw = f < a.n_fft_frames ? a.mel[(long long)f * a.n_mels + ci] : -10.f;
+        v = mel_norm(raw, gmax);
+      }
+    }
+    a.out[i] = (f16)v;
+  }
+}
+
+void launch_im2col_mel(const Im2colMelArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_im2col_mel, dim3(2048), dim3(256), 0, s, a);
+  WDR_HIP(hipGetLastError());
+}
+
+__global__ void k_im2col_conv2(const f16* x, int d, f16* out) {
+  const long long total = 1500ll * 3 * d;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int t = (int)(i / (3 * d)), col = (int)(i % (3 * d));
+    const int ci = col / 3, k = col % 3;
+    const int u = 2 * t + k - 1;
+    out[i] = (u >= 0 && u < 3000) ? x[(long long)u * d + ci] : (f16)0.f;
+  }
+}
+
+void launch_im2col_conv2(const f16* x, int d, f16* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_im2col_conv2, dim3(4096), dim3(256), 0, s, x, d, out);
+  WDR_HIP(hipGetLastError());
+}
+
+// read back the normalised window as f32 [n_mels][3000] (debug / tests)
+__global__ void k_mel_window(const float* mel, int n_mels, int n_fft_frames, const int* gmax_ord, int seek, float* out) {
+  const float gmax = ord2f(*gmax_ord);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_mels * 3000; i += gridDim.x * blockDim.x) {
+    const int ci = i / 3000, u = i % 3000;
+    const int f = seek + u;
+    const float raw = f < n_fft_frames ? mel[(long long)f * n_mels + ci] : -10.f;
+    out[i] = mel_norm(raw, gmax);
+  }
+}
+
+void launch_mel_window(const float* mel, int n_mels, int n_fft_frames, const int* gmax, int seek, float* out,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(k_mel_window, dim3(512), dim3(256), 0, s, mel, n_mels, n_fft_frames, gmax, seek, out);
+  WDR_HIP(hipGetLastError());
+}
+
+__global__ void k_set_int(int* p, int v) { *p = v; }
+void launch_gmax_init(int* gmax, hipStream_t s) {
+  // the zero-padded tail always exists (n_len > n_fft_frames), so the max starts at -10
+  union { float f; int i; } u;
+  u.f = -10.f;
+  hipLaunchKernelGGL(k_set_int, dim3(1), dim3(1), 0, s, gmax, u.i);
+  WDR_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------- signal energy
+__global__ void k_energy(const float* x, int n, float* e) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float sum = 0.f;
+  for (int j = -32; j <= 32; ++j) {
+    const int p = i + j;
+    if (p >= 0 && p < n) sum += fabsf(x[p]);
+  }
+  e[i] = sum / 65;
+}
+
+void launch_energy(const float* x, int n, float* e, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_energy, dim3(cdiv(n, 256)), dim3(256), 0, s, x, n, e);
+  WDR_HIP(hipGetLastError());
+}
+
+__global__ void k_i16_to_f32(const int16_t* in, int n, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (float)in[i] / 32768.0f;
+}
+void launch_i16_to_f32(const int16_t* in, int n, float* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_i16_to_f32, dim3(cdiv(n, 256)), dim3(256), 0, s, in, n, out);
+  WDR_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------- LayerNorm / embedding / KV
+__global__ __launch_bounds__(256) void k_layernorm(const float* x, int ldx, const float* g, const float* b, f16* y,
+                                                   int ldy, int rows, int d) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* xr = x + (long long)row * ldx;
+  double s = 0.0;
+  for (int c = lane; c < d; c += 64) s += (double)xr[c];
+  s = wave_sum_d(s);
+  const float mean = (float)(s / d);
+  double s2 = 0.0;
+  for (int c = lane; c < d; c += 64) {
+    const float v = xr[c] - mean;
+    s2 += (double)(v * v);
+  }
+  s2 = wave_sum_d(s2);
+  const float var = (float)(s2 / d);
+  const float scale = 1.0f / sqrtf(var + 1e-5f);
+  f16* yr = y + (long long)row * ldy;
+  for (int c = lane; c < d; c += 64) {
+    const float v = (xr[c] - mean) * scale;
+    yr[c] = (f16)(v * g[c] + b[c]);
+  }
+}
+
+void launch_layernorm(const float* x, int ldx, const float* g, const float* b, f16* y, int ldy, int rows, int d,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_layernorm, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, g, b, y, ldy, rows, d);
+  WDR_HIP(hipGetLastError());
+}
+
+__global__ void k_embed(const f16* E, const float* P, const int* tok, const int* pos, int d, float* x) {
+  const int r = blockIdx.x;
+  const int t = tok[r], p = pos[r];
+  for (int c = threadIdx.x; c < d; c += blockDim.x)
+    x[(long long)r * d + c] = (float)E[(long long)t * d + c] + P[(long long)p * d + c];
+}
+
+void launch_embed(const f16* E, const float* P, const int* tok, const int* pos, int R, int d, float* x, hipStream_t s) {
+  hipLaunchKernelGGL(k_embed, dim3(R), dim3(256), 0, s, E, P, tok, pos, d, x);
+  WDR_HIP(hipGetLastError());
+}
+
+__global__ void k_kv_scatter(const f16* qkv, int ldqkv, int d, const int* row_seq, const int* row_pos, f16* kc,
+                             f16* vc, long long seq_stride) {
+  const int r = blockIdx.x;
+  const long long dst = row_seq[r] * seq_stride + (long long)row_pos[r] * d;
+  for (int c = threadIdx.x * 8; c < d; c += blockDim.x * 8) {
+    *(f16x8*)(kc + dst + c) = *(const f16x8*)(qkv + (long long)r * ldqkv + d + c);
+    *(f16x8*)(vc + dst + c) = *(const f16x8*)(qkv + (long long)r * ldqkv + 2 * d + c);
+  }
+}
+
+void launch_kv_scatter(const f16* qkv, int ldqkv, int d, const int* row_seq, const int* row_pos, int R, f16* kc, f16* vc,
+                       long long seq_stride, hipStream_t s) {
+  hipLaunchKernelGGL(k_kv_scatter, dim3(R), dim3(64), 0, s, qkv, ldqkv, d, row_seq, row_pos, kc, vc, seq_stride);
+  WDR_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------- logits rules
+template <typename T>
+__device__ __forceinline__ T block_reduce(T v, T* sh, int op) {   // op 0 = max, 1 = sum ; blockDim 1024
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int o = 32; o > 0; o >>= 1) {
+    const T u = __shfl_xor(v, o, 64);
+    v = op == 0 ? (v > u ? v : u) : v + u;
+  }
+  __syncthreads();
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  if (w == 0) {
+    v = lane < 16 ? sh[lane] : (op == 0 ? (T)-INFINITY : (T)0);
+    for (int o = 32; o > 0; o >>= 1) {
+      const T u = __shfl_xor(v, o, 64);
+      v = op == 0 ? (v > u ? v : u) : v + u;
+    }
+    if (lane == 0) sh[0] = v;
+  }
+  __syncthreads();
+  const T r = sh[0];
+  __syncthreads();
+  return r;
+}
+
+// argmax with whisper.cpp's tie rule: the first index holding the maximum (strict <).
+__device__ __forceinline__ void amax_merge(float& v, int& i, float v2, int i2) {
+  if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
+}
+__device__ void block_argmax(float& v, int& idx, float* shv, int* shi) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int o = 32; o > 0; o >>= 1) {
+    const float v2 = __shfl_xor(v, o, 64);
+    const int i2 = __shfl_xor(idx, o, 64);
+    amax_merge(v, idx, v2, i2);
+  }
+  __syncthreads();
+  if (lane == 0) { shv[w] = v; shi[w] = idx; }
+  __syncthreads();
+  if (w == 0) {
+    v = lane < 16 ? shv[lane] : -INFINITY;
+    idx = lane < 16 ? shi[lane] : 0x7fffffff;
+    for (int o = 32; o > 0; o >>= 1) {
+      const float v2 = __shfl_xor(v, o, 64);
+      const int i2 = __shfl_xor(idx, o, 64);
+      amax_merge(v, idx, v2, i2);
+    }
+    if (lane == 0) { shv[0] = v; shi[0] = idx; }
+  }
+  __syncthreads();
+  v = shv[0];
+  idx = shi[0];
+  __syncthreads();
+}
+
+__device__ __forceinline__ float rule_mask(float x, int i, const LogitsCtl& c, const VocabIds& v) {
+  const bool initial = c.n_tokens == 0;
+  if (c.temperature > 0.f) x = x / c.temperature;
+  if (v.suppress_blank && initial && (i == v.eot || i == v.space)) return -INFINITY;
+  if (i == v.not_ || i == v.sot || i == v.nosp || i == v.solm || i == v.translate || i == v.transcribe || i == v.prev)
+    return -INFINITY;
+  if (i >= v.lang0 && i < v.lang0 + v.n_lang) return -INFINITY;
+  if (c.last_ts) {
+    if (c.pen_ts) {
+      if (i >= v.beg) return -INFINITY;
+    } else if (i < v.eot) {
+      return -INFINITY;
+    }
+  }
+  if (initial && v.max_initial_tid >= 0 && i > v.beg + v.max_initial_tid) return -INFINITY;
+  if (c.has_ts && i >= v.beg && i < v.beg + c.seek_delta / 2) return -INFINITY;
+  if (c.force_kind == 1 && i != c.force_tok) return -INFINITY;
+  if (c.force_kind == 2 && (i == v.eot || i >= v.beg)) return -INFINITY;
+  return x;
+}
+
+__global__ __launch_bounds__(1024) void k_logits_process(const float* logits, int ld, const LogitsCtl* ctls, VocabIds v,
+                                                         float* work, TokOut* out) {
+  __shared__ float shf[16];
+  __shared__ double shd[16];
+  __shared__ int shi[16];
+  const int r = blockIdx.x, tid = threadIdx.x;
+  const float* L = logits + (long long)r * ld;
+  float* X = work + (long long)r * ld;
+  const LogitsCtl c = ctls[r];
+  const int V = v.n_vocab;
+  // (1) no-speech probability from the raw logits (before any filter)
+  float m0 = -INFINITY;
+  for (int i = tid; i < V; i += 1024) m0 = fmaxf(m0, L[i]);
+  m0 = block_reduce<float>(m0, shf, 0);
+  float s0 = 0.f;
+  for (int i = tid; i < V; i += 1024) s0 += __expf(L[i] - m0);
+  s0 = block_reduce<float>(s0, shf, 1);
+  const float lse0 = logf(s0) + m0;
+  // (2) filters
+  float m1 = -INFINITY;
+  for (int i = tid; i < V; i += 1024) {
+    float x = rule_mask(L[i], i, c, v);
+    X[i] = x;
+    m1 = fmaxf(m1, x);
+  }
+  m1 = block_reduce<float>(m1, shf, 0);
+  bool forced_empty = false;
+  if (c.force_kind == 1 && m1 == -INFINITY) {   // forced token was filtered: keep it alone
+    forced_empty = true;
+    m1 = 0.f;
+  }
+  if (forced_empty && tid == 0) X[c.force_tok] = 0.f;
+  __syncthreads();
+  float s1 = 0.f;
+  for (int i = tid; i < V; i += 1024)
+    if (X[i] > -INFINITY) s1 += __expf(X[i] - m1);
+  s1 = block_reduce<float>(s1, shf, 1);
+  const float lse = logf(s1) + m1;
+  // (3) timestamp mass vs best text token
+  float mts = -INFINITY, mtx = -INFINITY;
+  for (int i = tid; i < V; i += 1024) {
+    const float lp = X[i] > -INFINITY ? X[i] - lse : -INFINITY;
+    if (i >= v.beg) mts = fmaxf(mts, lp);
+    else mtx = fmaxf(mtx, lp);
+  }
+  mts = block_reduce<float>(mts, shf, 0);
+  mtx = block_reduce<float>(mtx, shf, 0);
+  float sts = 0.f;
+  if (mts > -INFINITY)
+    for (int i = v.beg + tid; i < V; i += 1024)
+      if (X[i] > -INFINITY) sts += __expf((X[i] - lse) - mts);
+  sts = block_reduce<float>(sts, shf, 1);
+  const float ts_lp = sts > 0.f ? logf(sts) + mts : -INFINITY;
+  const bool mask_text = ts_lp > mtx;
+  // (4) probabilities, greedy pick, timestamp statistics
+  float bp = 0.f;
+  int bi = 0x7fffffff;
+  float tp = 0.f;
+  int ti = 0x7fffffff;
+  double tsum = 0.0;
+  for (int i = tid; i < V; i += 1024) {
+    float x = X[i];
+    if (mask_text && i < v.beg) x = -INFINITY;
+    const float p = x == -INFINITY ? 0.f : __expf(x - lse);
+    if (p > 0.f) amax_merge(bp, bi, p, i);
+    if (i >= v.beg) {
+      tsum += (double)p;
+      if (p > 0.f) amax_merge(tp, ti, p, i);
+    }
+    X[i] = p;     // probs (kept for t > 0 sampling on the host)
+  }
+  block_argmax(bp, bi, shf, shi);
+  block_argmax(tp, ti, shf, shi);
+  tsum = block_reduce<double>(tsum, shd, 1);
+  if (tid == 0) {
+    TokOut o;
+    o.nosp_prob = __expf(L[v.nosp] - lse0);
+    o.ptsum = (float)tsum;
+    o.pt = (float)((double)(ti == 0x7fffffff ? 0.f : tp) / (tsum + 1e-10));
+    o.tid = ti == 0x7fffffff ? 0 : ti;
+    if (bi == 0x7fffffff) {
+      o.id = 0; o.p = 0.f; o.plog = 0.f;
+    } else {
+      o.id = bi; o.p = bp;
+      float x = rule_mask(L[bi], bi, c, v);
+      if (forced_empty && bi == c.force_tok) x = 0.f;
+      o.plog = x - lse;
+    }
+    if (o.id >= v.beg) { o.tid = o.id; o.pt = o.p; }
+    out[r] = o;
+  }
+}
+
+void launch_logits_process(const float* logits, int ld, const LogitsCtl* ctls, const VocabIds& v, int R, float* work,
+                           TokOut* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_logits_process, dim3(R), dim3(1024), 0, s, logits, ld, ctls, v, work, out);
+  WDR_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------- DTW
+// ggml_norm over tokens for every (head, column): float mean from a double sum, v = x - mean,
+// double sum of v*v, scale = 1/sqrtf(var + 1e-9).
+__global__ void k_dtw_norm(const float* cap, int A, int N, int Tk, int M, float* nrm) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A * M) return;
+  const int a = i / M, col = i % M;
+  const float* src = cap + (long long)a * N * Tk + col;
+  double s = 0.0;
+  for (int t = 0; t < N; ++t) s += (double)src[(long long)t * Tk];
+  const float mean = (float)(s / N);
+  double s2 = 0.0;
+  for (int t = 0; t < N; ++t) {
+    const float v = src[(long long)t * Tk] - mean;
+    s2 += (double)(v * v);
+  }
+  const float var = (float)(s2 / N);
+  const float scale = 1.0f / sqrtf(var + 1e-9f);
+  float* dst = nrm + (long long)a * N * M + col;
+  for (int t = 0; t < N; ++t) dst[(long long)t * M] = (src[(long long)t * Tk] - mean) * scale;
+}
+
+__device__ __forceinline__ void cswap(float& a, float& b) {
+  const float lo = fminf(a, b), hi = fmaxf(a, b);
+  a = lo;
+  b = hi;
+}
+
+// median-7 along columns (reflect), mean over heads (double sum), negate; rows [sot_len, N-1)
+__global__ void k_dtw_medmean(const float* nrm, int A, int N, int M, int sot_len, float* x) {
+  const int rows = N - sot_len - 1;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * M) return;
+  const int r = i / M, col = i % M;
+  const int t = r + sot_len;
+  double sum = 0.0;
+  for (int a = 0; a < A; ++a) {
+    const float* row = nrm + ((long long)a * N + t) * M;
+    float w[7];
+#pragma unroll
+    for (int o = 0; o < 7; ++o) {
+      int idx = col + o - 3;
+      if (idx < 0) idx = -idx;
+      else if (idx >= M) idx = 2 * (M - 1) - idx;
+      w[o] = row[idx];
+    }
+    // sorting network for 7 elements
+    cswap(w[0], w[6]); cswap(w[2], w[3]); cswap(w[4], w[5]);
+    cswap(w[0], w[2]); cswap(w[1], w[4]); cswap(w[3], w[6]);
+    cswap(w[0], w[1]); cswap(w[2], w[5]); cswap(w[3], w[4]);
+    cswap(w[1], w[2]); cswap(w[4], w[6]);
+    cswap(w[2], w[3]); cswap(w[4], w[5]);
+    cswap(w[1], w[2]); cswap(w[3], w[4]); cswap(w[5], w[6]);
+    sum += (double)w[3];
+  }
+  const float mean = (float)sum / (float)A;
+  x[(long long)r * M + col] = mean * -1.0f;
+}
+
+constexpr int DTW_NMAX = 256, DTW_MMAX = 1504, DTW_WPR = DTW_MMAX / 16;
+
+// x [N][M] -> t_dtw for each change of the token index along the backtraced path.
+__global__ __launch_bounds__(256) void k_dtw_dp(const float* x, int N, int M, int seek, int* times, int* n_times) {
+  __shared__ uint32_t tr[DTW_NMAX * DTW_WPR];
+  __shared__ float dg[3][DTW_NMAX + 1];
+  __shared__ short pi[DTW_NMAX + DTW_MMAX + 4], pj[DTW_NMAX + DTW_MMAX + 4];
+  const int tid = threadIdx.x;
+  const int i = tid + 1;   // row handled by this thread (1..N)
+  for (int k = tid; k <= DTW_NMAX; k += 256) {
+    dg[0][k] = INFINITY;
+    dg[1][k] = INFINITY;
+    dg[2][k] = INFINITY;
+  }
+  __syncthreads();
+  if (tid == 0) dg[0][0] = 0.f;   // diagonal s = 0 holds cost[0][0]
+  __syncthreads();
+  const float* xr = x + (long long)(i - 1) * M;
+  // each thread walks its own row left to right one column per step: keep an 8-deep
+  // shift register of x so the global loads run 8 steps ahead of their use.
+  float w[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) w[q] = (i <= N && q < M) ? xr[q] : 0.f;
+  uint32_t acc = 0;
+  for (int s = 2; s <= N + M; ++s) {
+    const float* d2 = dg[(s - 2) % 3];
+    const float* d1 = dg[(s - 1) % 3];
+    float* d0 = dg[s % 3];
+    const int j = s - i;
+    float nv = INFINITY;
+    if (i <= N && j >= 1 && j <= M) {
+      const float c0 = d2[i - 1], c1 = d1[i - 1], c2 = d1[i];
+      float c;
+      uint32_t t;
+      if (c0 < c1 && c0 < c2) { c = c0; t = 0; }
+      else if (c1 < c0 && c1 < c2) { c = c1; t = 1; }
+      else { c = c2; t = 2; }
+      nv = w[0] + c;
+#pragma unroll
+      for (int q = 0; q < 7; ++q) w[q] = w[q + 1];
+      w[7] = (j - 1 + 8 < M) ? xr[j - 1 + 8] : 0.f;
+      acc |= t << (2 * ((j - 1) & 15));
+      if (((j - 1) & 15) == 15 || j == M) {
+        tr[(i - 1) * DTW_WPR + ((j - 1) >> 4)] = acc;
+        acc = 0;
+      }
+    }
+    if (i <= N) d0[i] = nv;
+    if (tid == 0) d0[0] = INFINITY;   // cost[0][s] for s > 0
+    __syncthreads();
+  }
+  if (tid == 0) {
+    // backtrace from (N, M); trace[0][:] = 2, trace[:][0] = 1
+    int ii = N, jj = M, len = 0;
+    while (ii > 0 || jj > 0) {
+      pi[len] = (short)(ii - 1);
+      pj[len] = (short)(jj - 1);
+      ++len;
+      int t;
+      if (ii == 0) t = 2;
+      else if (jj == 0) t = 1;
+      else t = (tr[(ii - 1) * DTW_WPR + ((jj - 1) >> 4)] >> (2 * ((jj - 1) & 15))) & 3;
+      if (t == 0) { --ii; --jj; }
+      else if (t == 1) --ii;
+      else --jj;
+    }
+    int last_v = 0, nt = 0;
+    for (int k = len - 1; k >= 0; --k) {
+      const int v = pi[k];
+      if (v != last_v) {
+        times[nt++] = 2 * pj[k] + seek;
+        last_v = v;
+      }
+    }
+    *n_times = nt;
+  }
+}
+
+void launch_dtw(const float* cap, int A, int N_tok, int Tk, int n_audio, int sot_len, int seek, float* nrm, float* x,
+                int* times, int* n_times, hipStream_t s) {
+  const int M = n_audio;
+  const int rows = N_tok - sot_len - 1;
+  WDR_CHECK(rows >= 1 && rows <= DTW_NMAX, "DTW: token count out of range");
+  WDR_CHECK(M >= 1 && M <= 1500, "DTW: frame count out of range");
+  hipLaunchKernelGGL(k_dtw_norm, dim3(cdiv(A * M, 256)), dim3(256), 0, s, cap, A, N_tok, Tk, M, nrm);
+  hipLaunchKernelGGL(k_dtw_medmean, dim3(cdiv(rows * M, 256)), dim3(256), 0, s, nrm, A, N_tok, M, sot_len, x);
+  hipLaunchKernelGGL(k_dtw_dp, dim3(1), dim3(256), 0, s, x, rows, M, seek, times, n_times);
+  WDR_HIP(hipGetLastError());
+}
+
+void launch_dtw_dp_only(const float* x, int rows, int M, int seek, int* times, int* n_times, hipStream_t s) {
+  WDR_CHECK(rows >= 1 && rows <= DTW_NMAX && M >= 1 && M <= 1500, "DTW: shape out of range");
+  hipLaunchKernelGGL(k_dtw_dp, dim3(1), dim3(256), 0, s, x, rows, M, seek, times, n_times);
+  WDR_HIP(hipGetLastError());
+}
+
+}  // namespace wdr

@@ -1,0 +1,110 @@
+// Kernel argument structs and launchers shared by the runtime (csrc/*.cpp) and kernels.
+#pragma once
+#include "../common.h"
+
+namespace wdr {
+
+struct MelArgs {
+  const float* x; int n;           // segment samples (f32), unpadded
+  int n_frames;                    // frames computed through the FFT: min(n_eff/160 + 1, n_len)
+  int n_mels;
+  const float* hann;               // [400]
+  const float* cos_tab; const float* sin_tab;   // [400]: cos(2 pi k / 400), -sin(2 pi k / 400)
+  const float* filters;            // [n_mels][201]
+  float* mel;                      // [n_frames][n_mels] raw log10
+  int* gmax;                       // ordered-int running max of the raw log-mel
+};
+void launch_mel(const MelArgs& a, hipStream_t s);
+void launch_gmax_init(int* gmax, hipStream_t s);
+
+struct Im2colMelArgs {
+  const float* mel; int n_mels, n_fft_frames;
+  const int* gmax;
+  int seek;
+  int kp;                          // padded K (multiple of 32)
+  f16* out;                        // [3000][kp]
+};
+void launch_im2col_mel(const Im2colMelArgs& a, hipStream_t s);
+void launch_im2col_conv2(const f16* x, int d, f16* out, hipStream_t s);
+void launch_mel_window(const float* mel, int n_mels, int n_fft_frames, const int* gmax, int seek, float* out,
+                       hipStream_t s);
+void launch_energy(const float* x, int n, float* e, hipStream_t s);
+void launch_i16_to_f32(const int16_t* in, int n, float* out, hipStream_t s);
+void launch_synth_fill(void* dst, long long rows, int src_cols, int dst_cols, uint64_t seed, float scale, bool f16out,
+                       int mode, float cval, hipStream_t s);
+void launch_layernorm(const float* x, int ldx, const float* g, const float* b, f16* y, int ldy, int rows, int d,
+                      hipStream_t s);
+void launch_embed(const f16* E, const float* P, const int* tok, const int* pos, int R, int d, float* x, hipStream_t s);
+void launch_kv_scatter(const f16* qkv, int ldqkv, int d, const int* row_seq, const int* row_pos, int R, f16* kc, f16* vc,
+                       long long seq_stride, hipStream_t s);
+
+struct LogitsCtl {
+  int n_tokens;        // tokens already sampled in this sequence (0 -> initial step)
+  int last_ts, pen_ts; // last / penultimate token is a timestamp (pen_ts also when < 2 tokens)
+  int has_ts, seek_delta;
+  int force_kind;      // 0 none, 1 only force_tok, 2 text only (synthetic workload pin)
+  int force_tok;
+  float temperature;
+};
+struct VocabIds {
+  int n_vocab, eot, sot, translate, transcribe, solm, prev, nosp, not_, beg, space;
+  int lang0, n_lang;
+  int max_initial_tid;  // round(max_initial_ts / precision); -1 disables
+  int suppress_blank;
+};
+struct TokOut {
+  int id, tid;
+  float p, plog, pt, ptsum;
+  float nosp_prob;
+  int pad;
+};
+void launch_logits_process(const float* logits, int ld, const LogitsCtl* ctls, const VocabIds& v, int R, float* work,
+                           TokOut* out, hipStream_t s);
+
+void launch_dtw(const float* cap, int A, int N_tok, int Tk, int n_audio, int sot_len, int seek, float* nrm, float* x,
+                int* times, int* n_times, hipStream_t s);
+void launch_dtw_dp_only(const float* x, int rows, int M, int seek, int* times, int* n_times, hipStream_t s);
+
+// attention (kernels/attn.hip)
+struct FlashArgs {
+  const f16* q; int ldq; long long q_bs;
+  const f16* k; int ldk; long long k_bs;
+  const f16* v; int ldv; long long v_bs;
+  f16* o; int ldo; long long o_bs;
+  float2* ml;
+  int Tq, Tk, n_head;
+  int causal;
+  float scale;
+};
+void launch_flash_attn(const FlashArgs& a, int n_batch, hipStream_t s);
+struct DecSelfArgs {
+  const f16* q; int ldq;
+  const f16* kc; const f16* vc;
+  long long seq_stride; int d;
+  const int* row_seq; const int* row_pos;
+  f16* o; int ldo;
+  float scale;
+};
+void launch_dec_self_attn(const DecSelfArgs& a, int R, int n_head, hipStream_t s);
+struct XAttnArgs {
+  const f16* q; int ldq;
+  const f16* k; const f16* v; int ldkv;
+  int Tk, R, n_head;
+  float scale;
+  float* part_o;
+  float2* part_ml;
+  f16* o; int ldo;
+};
+void launch_xattn(const XAttnArgs& a, hipStream_t s);
+struct CaptureArgs {
+  const f16* q; int ldq;
+  const f16* k; int ldk;
+  const float2* ml;
+  const int* heads;
+  float* out;
+  int slot0, R, Tk;
+  float scale;
+};
+void launch_aheads_capture(const CaptureArgs& a, int n_sel, hipStream_t s);
+
+}  // namespace wdr

@@ -1,0 +1,161 @@
+// Whisper model, context and state on one MI355X (csrc side of SURVEY.md §8(a) a2-a13).
+//
+// Context  ~ whisper.cpp whisper_context  (created by transcribe::create_context,
+//            src/transcribe.rs:89-166): hparams, vocab, weights resident in HBM,
+//            DTW preset (alignment heads).
+// State    ~ whisper.cpp whisper_state (ctx.create_state(), src/transcribe.rs:335):
+//            device work buffers, KV caches, streams, and the host-side decode loop
+//            `full()` = whisper_full_with_state as the reference drives it.
+#pragma once
+#include <memory>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "common.h"
+#include "kernels/kernels.h"
+#include "vocab.h"
+
+namespace wdr {
+
+struct HParams {
+  int n_vocab = 51864, n_audio_ctx = 1500, n_audio_state = 512, n_audio_head = 8, n_audio_layer = 6;
+  int n_text_ctx = 448, n_text_state = 512, n_text_head = 8, n_text_layer = 6, n_mels = 80;
+};
+bool hparams_for(const std::string& name, HParams* hp);
+
+std::vector<std::pair<int, int>> alignment_heads_for(const std::string& model_name);
+
+struct DevMem {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevMem() = default;
+  explicit DevMem(size_t n);
+  ~DevMem();
+  DevMem(const DevMem&) = delete;
+  DevMem& operator=(const DevMem&) = delete;
+  DevMem(DevMem&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+  DevMem& operator=(DevMem&& o) noexcept;
+  template <typename T> T* as() const { return (T*)p; }
+};
+
+struct EncLayer {
+  f16 *w_qkv, *w_o, *w_fc1, *w_fc2;
+  float *b_qkv, *b_o, *b_fc1, *b_fc2, *ln1_g, *ln1_b, *ln2_g, *ln2_b;
+};
+struct DecLayer {
+  f16 *w_qkv, *w_o, *w_xq, *w_xo, *w_fc1, *w_fc2;
+  float *b_qkv, *b_o, *b_xq, *b_xo, *b_fc1, *b_fc2;
+  float *ln1_g, *ln1_b, *ln2_g, *ln2_b, *ln3_g, *ln3_b;
+};
+
+struct Model {
+  HParams hp;
+  int kp1 = 0;   // conv1 im2col K padded to a multiple of 32
+  f16 *conv1_w = nullptr, *conv2_w = nullptr;
+  float *conv1_b = nullptr, *conv2_b = nullptr, *enc_pos = nullptr, *ln_post_g = nullptr, *ln_post_b = nullptr;
+  std::vector<EncLayer> enc;
+  std::vector<DecLayer> dec;
+  f16* w_xkv = nullptr;    // [L*2d][d]: per decoder layer cross K rows then cross V rows
+  float* b_xkv = nullptr;  // [L*2d]
+  f16* tok_emb = nullptr;
+  float *dec_pos = nullptr, *ln_g = nullptr, *ln_b = nullptr;
+  float *mel_filters = nullptr, *hann = nullptr, *cos_tab = nullptr, *sin_tab = nullptr;
+  DevMem storage;
+  size_t weight_bytes = 0;
+};
+
+struct ContextParams {
+  bool use_gpu = true;
+  int gpu_device = 0;
+  bool dtw = true;
+  bool flash_attn = false;
+  double weight_std = 0.02;   // synthetic weights (oracle/weights.py uses the same doubles)
+  double emb_std = 0.02;
+};
+
+class Context {
+ public:
+  Context(const std::string& model_name, const HParams& hp, const ContextParams& cp);
+  ~Context();
+  std::string name;
+  ContextParams cp;
+  Model model;
+  Vocab vocab;
+  std::vector<std::pair<int, int>> aheads;        // (layer, head) DTW preset
+  std::vector<std::vector<int>> aheads_per_layer;
+  DevMem aheads_dev;                              // per-layer head lists (device)
+  std::vector<int> aheads_dev_off;
+  hipStream_t stream = nullptr;
+};
+
+struct FullParams {
+  bool greedy = false;      // strategy: greedy vs beam search (src/transcribe.rs:25-33)
+  int best_of = 5, beam_size = 5;
+  std::string language = "auto";
+  bool translate = false;
+  int n_max_text_ctx = 16384;
+  std::string initial_prompt;
+  bool has_initial_prompt = false;
+  float temperature = 0.f, temperature_inc = 0.2f;
+  float entropy_thold = 2.4f, logprob_thold = -1.f, no_speech_thold = 0.6f;
+  float thold_pt = 0.01f, thold_ptsum = 0.01f, max_initial_ts = 1.f, length_penalty = -1.f;
+  bool suppress_blank = true, single_segment = true, token_timestamps = true;
+  int max_tokens = 0;
+  float force_len_rate = 0.f;   // synthetic workload pin (0 = off)
+};
+
+struct TokenData {
+  int id = 0, tid = 0;
+  float p = 0, plog = 0, pt = 0, ptsum = 0;
+  long long t0 = -1, t1 = -1, t_dtw = -1;
+  float vlen = 0;
+};
+
+struct ResultSeg {
+  long long t0, t1;
+  std::string text;
+  std::vector<TokenData> tokens;
+};
+
+struct StageTimes {   // host wall-clock per phase (seconds), accumulated
+  double mel = 0, encode = 0, decode = 0, dtw = 0, glue = 0;
+  long long windows = 0, decode_steps = 0, prefills = 0;
+};
+
+class State {
+ public:
+  explicit State(Context& ctx);
+  ~State();
+  // whisper_full_with_state on host f32 samples. Returns 0 on success.
+  int full(const FullParams& p, const float* samples, int n);
+  std::vector<ResultSeg> result_all;
+  int lang_id = 0;
+  StageTimes times;
+  long long t_beg = 0, t_last = 0, tid_last = 0;
+  std::vector<float> energy;
+
+  // test seams
+  void compute_mel(const float* x_host, int n);
+  void read_mel_window(int seek, float* out);              // [n_mels][3000] normalised
+  void encode_window(int seek);
+  void encode_from_mel_window(const float* mel_window);    // [n_mels][3000] normalised, host
+  void read_encoder_out(float* out);                       // [1500][d] (ln_post output, f16 -> f32)
+  void decode_logits(const int* toks, int n, float* logits_out);   // prefill from an empty cache
+  void dtw_capture(const int* toks, int n, float* cap_out);        // [n_aheads][n][1500]
+
+  struct Impl;
+
+ private:
+  Context& ctx_;
+  hipStream_t s_;
+  std::unique_ptr<Impl> m_;
+  // pieces of full()
+  void decoder_prefill(const int* toks, int n, int seq, bool want_logits, bool capture);
+  void decoder_step(const int* toks, const int* seqs, const int* pos, int R);
+  void run_logits(int R, const LogitsCtl* ctl, TokenData* out, float* nosp);
+  void heuristic_timestamps(int i_segment, const FullParams& p);
+  void dtw_timestamps(int i_segment, int n_segments, int seek, int n_frames, const std::string& language);
+};
+
+}  // namespace wdr

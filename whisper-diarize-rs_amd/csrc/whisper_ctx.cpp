@@ -1,0 +1,1021 @@
+// Whisper context / state: weights in HBM, encoder + decoder forward, and the
+// whisper_full_with_state decode loop as the reference drives it
+// (src/transcribe.rs:20-87 params, :389 state.full).  Mirrors oracle/whisper_full.py.
+#include "whisper.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <map>
+
+namespace wdr {
+
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// ------------------------------------------------------------------ hparams / presets
+bool hparams_for(const std::string& name, HParams* hp) {
+  HParams h;
+  if (name == "base.en" || name == "base") {
+    if (name == "base") h.n_vocab = 51865;
+  } else if (name == "tiny.en" || name == "tiny") {
+    h.n_audio_state = h.n_text_state = 384;
+    h.n_audio_head = h.n_text_head = 6;
+    h.n_audio_layer = h.n_text_layer = 4;
+    if (name == "tiny") h.n_vocab = 51865;
+  } else if (name == "small.en" || name == "small") {
+    h.n_audio_state = h.n_text_state = 768;
+    h.n_audio_head = h.n_text_head = 12;
+    h.n_audio_layer = h.n_text_layer = 12;
+    if (name == "small") h.n_vocab = 51865;
+  } else if (name == "medium.en" || name == "medium") {
+    h.n_audio_state = h.n_text_state = 1024;
+    h.n_audio_head = h.n_text_head = 16;
+    h.n_audio_layer = h.n_text_layer = 24;
+    if (name == "medium") h.n_vocab = 51865;
+  } else if (name == "large-v3" || name == "large-v3-turbo") {
+    h.n_vocab = 51866;
+    h.n_mels = 128;
+    h.n_audio_state = h.n_text_state = 1280;
+    h.n_audio_head = h.n_text_head = 20;
+    h.n_audio_layer = 32;
+    h.n_text_layer = name == "large-v3" ? 32 : 4;
+  } else if (name == "tiny-test") {
+    h.n_audio_state = h.n_text_state = 128;
+    h.n_audio_head = h.n_text_head = 2;
+    h.n_audio_layer = h.n_text_layer = 2;
+  } else if (name == "tiny-test-ml") {
+    h.n_vocab = 51866;
+    h.n_mels = 128;
+    h.n_audio_state = h.n_text_state = 128;
+    h.n_audio_head = h.n_text_head = 2;
+    h.n_audio_layer = h.n_text_layer = 2;
+  } else {
+    return false;
+  }
+  *hp = h;
+  return true;
+}
+
+// whisper.cpp g_aheads_* presets (OpenAI _ALIGNMENT_HEADS); src/transcribe.rs:117-129 maps
+// model names to presets and falls back to Small for unknown names.
+std::vector<std::pair<int, int>> alignment_heads_for(const std::string& n) {
+  static const std::map<std::string, std::vector<std::pair<int, int>>> tab = {
+      {"tiny.en", {{1, 0}, {2, 0}, {2, 5}, {3, 0}, {3, 1}, {3, 2}, {3, 3}, {3, 4}}},
+      {"tiny", {{2, 2}, {3, 0}, {3, 2}, {3, 3}, {3, 4}, {3, 5}}},
+      {"base.en", {{3, 3}, {4, 7}, {5, 1}, {5, 5}, {5, 7}}},
+      {"base", {{3, 1}, {4, 2}, {4, 3}, {4, 7}, {5, 1}, {5, 2}, {5, 4}, {5, 6}}},
+      {"small.en", {{6, 6}, {7, 0}, {7, 3}, {7, 8}, {8, 2}, {8, 5}, {8, 7}, {9, 0}, {9, 4}, {9, 8},
+                    {9, 10}, {10, 0}, {10, 1}, {10, 2}, {10, 3}, {10, 6}, {10, 11}, {11, 2}, {11, 4}}},
+      {"small", {{5, 3}, {5, 9}, {8, 0}, {8, 4}, {8, 7}, {8, 8}, {9, 0}, {9, 7}, {9, 9}, {10, 5}}},
+      {"medium.en", {{11, 4}, {14, 1}, {14, 12}, {14, 14}, {15, 4}, {16, 0}, {16, 4}, {16, 9}, {17, 12},
+                     {17, 14}, {18, 7}, {18, 10}, {18, 15}, {20, 0}, {20, 3}, {20, 9}, {20, 14}, {21, 12}}},
+      {"medium", {{13, 15}, {15, 4}, {15, 15}, {16, 1}, {20, 0}, {23, 4}}},
+      {"large-v3", {{7, 0}, {10, 17}, {12, 18}, {13, 12}, {16, 1}, {17, 14}, {19, 11}, {21, 4}, {24, 1}, {25, 6}}},
+      {"large-v3-turbo", {{2, 4}, {2, 11}, {3, 3}, {3, 6}, {3, 11}, {3, 14}}},
+      {"tiny-test", {{1, 0}, {1, 1}}},
+      {"tiny-test-ml", {{1, 0}, {1, 1}}},
+  };
+  auto it = tab.find(n);
+  return it != tab.end() ? it->second : tab.at("small");
+}
+
+// ------------------------------------------------------------------ device memory
+DevMem::DevMem(size_t n) : bytes(n) {
+  if (n) WDR_HIP(hipMalloc(&p, n));
+}
+DevMem::~DevMem() {
+  if (p) (void)hipFree(p);
+}
+DevMem& DevMem::operator=(DevMem&& o) noexcept {
+  if (this != &o) {
+    if (p) (void)hipFree(p);
+    p = o.p;
+    bytes = o.bytes;
+    o.p = nullptr;
+    o.bytes = 0;
+  }
+  return *this;
+}
+
+static uint64_t fnv1a64(const std::string& s) {
+  uint64_t h = 0xCBF29CE484222325ull;
+  for (unsigned char c : s) {
+    h ^= c;
+    h *= 0x100000001B3ull;
+  }
+  return h;
+}
+
+// host restatement of librosa slaney mel filters (oracle/mel.py mel_filters)
+static std::vector<float> mel_filters_host(int n_mels) {
+  const double f_sp = 200.0 / 3, min_log_hz = 1000.0, min_log_mel = 1000.0 / f_sp, logstep = std::log(6.4) / 27.0;
+  auto hz2mel = [&](double f) { return f >= min_log_hz ? min_log_mel + std::log(f / min_log_hz) / logstep : f / f_sp; };
+  auto mel2hz = [&](double m) { return m >= min_log_mel ? min_log_hz * std::exp(logstep * (m - min_log_mel)) : f_sp * m; };
+  const int nb = 201;
+  std::vector<double> fftf(nb), melf(n_mels + 2);
+  for (int i = 0; i < nb; ++i) fftf[i] = 8000.0 * i / (nb - 1);
+  const double m0 = hz2mel(0.0), m1 = hz2mel(8000.0);
+  for (int i = 0; i < n_mels + 2; ++i) melf[i] = mel2hz(m0 + (m1 - m0) * i / (n_mels + 1));
+  std::vector<float> w((size_t)n_mels * nb);
+  for (int i = 0; i < n_mels; ++i) {
+    const double enorm = 2.0 / (melf[i + 2] - melf[i]);
+    for (int k = 0; k < nb; ++k) {
+      const double lower = -(melf[i] - fftf[k]) / (melf[i + 1] - melf[i]);
+      const double upper = (melf[i + 2] - fftf[k]) / (melf[i + 2] - melf[i + 1]);
+      const double v = std::max(0.0, std::min(lower, upper));
+      w[(size_t)i * nb + k] = (float)(v * enorm);
+    }
+  }
+  return w;
+}
+
+// ------------------------------------------------------------------ context (weights)
+namespace {
+struct Alloc {
+  size_t off = 0;
+  std::vector<std::pair<size_t*, size_t>> dummy;
+  size_t take(size_t bytes) {
+    const size_t o = off;
+    off += (bytes + 255) & ~size_t(255);
+    return o;
+  }
+};
+}  // namespace
+
+Context::Context(const std::string& model_name, const HParams& hp, const ContextParams& p)
+    : name(model_name), cp(p), vocab(hp.n_vocab) {
+  WDR_CHECK(cp.use_gpu, "libwdr has no CPU backend: use_gpu=false is not supported (the CPU restatement is test-only)");
+  WDR_HIP(hipSetDevice(cp.gpu_device));
+  WDR_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  Model& m = model;
+  m.hp = hp;
+  const int d = hp.n_audio_state, dt = hp.n_text_state;
+  WDR_CHECK(d == dt, "encoder and decoder widths must match");
+  WDR_CHECK(hp.n_audio_state / hp.n_audio_head == 64 && hp.n_text_state / hp.n_text_head == 64, "d_head must be 64");
+  WDR_CHECK(d % 128 == 0, "model width must be a multiple of 128");
+  m.kp1 = ((hp.n_mels * 3 + 31) / 32) * 32;
+  const int L = hp.n_text_layer;
+
+  // ---- layout
+  Alloc A;
+  auto H = [&](size_t n) { return A.take(n * 2); };
+  auto F = [&](size_t n) { return A.take(n * 4); };
+  const size_t o_c1w = H((size_t)d * m.kp1), o_c1b = F(d), o_c2w = H((size_t)d * 3 * d), o_c2b = F(d);
+  const size_t o_epos = F((size_t)hp.n_audio_ctx * d), o_lnpg = F(d), o_lnpb = F(d);
+  struct EO { size_t qkv, bqkv, o, bo, f1, bf1, f2, bf2, l1g, l1b, l2g, l2b; };
+  std::vector<EO> eo(hp.n_audio_layer);
+  for (auto& e : eo) {
+    e.qkv = H((size_t)3 * d * d); e.bqkv = F(3 * d); e.o = H((size_t)d * d); e.bo = F(d);
+    e.f1 = H((size_t)4 * d * d); e.bf1 = F(4 * d); e.f2 = H((size_t)4 * d * d); e.bf2 = F(d);
+    e.l1g = F(d); e.l1b = F(d); e.l2g = F(d); e.l2b = F(d);
+  }
+  struct DO { size_t qkv, bqkv, o, bo, xq, bxq, xo, bxo, f1, bf1, f2, bf2, l1g, l1b, l2g, l2b, l3g, l3b; };
+  std::vector<DO> dd(L);
+  for (auto& e : dd) {
+    e.qkv = H((size_t)3 * dt * dt); e.bqkv = F(3 * dt); e.o = H((size_t)dt * dt); e.bo = F(dt);
+    e.xq = H((size_t)dt * dt); e.bxq = F(dt); e.xo = H((size_t)dt * dt); e.bxo = F(dt);
+    e.f1 = H((size_t)4 * dt * dt); e.bf1 = F(4 * dt); e.f2 = H((size_t)4 * dt * dt); e.bf2 = F(dt);
+    e.l1g = F(dt); e.l1b = F(dt); e.l2g = F(dt); e.l2b = F(dt); e.l3g = F(dt); e.l3b = F(dt);
+  }
+  const size_t o_xkv = H((size_t)L * 2 * dt * d), o_bxkv = F((size_t)L * 2 * dt);
+  const size_t o_tok = H((size_t)hp.n_vocab * dt), o_dpos = F((size_t)hp.n_text_ctx * dt);
+  const size_t o_lng = F(dt), o_lnb = F(dt);
+  const size_t o_filt = F((size_t)hp.n_mels * 201), o_hann = F(400), o_cos = F(400), o_sin = F(400);
+  m.weight_bytes = A.off;
+  m.storage = DevMem(A.off);
+  char* base = m.storage.as<char>();
+  auto h16 = [&](size_t o) { return (f16*)(base + o); };
+  auto f32 = [&](size_t o) { return (float*)(base + o); };
+  m.conv1_w = h16(o_c1w); m.conv1_b = f32(o_c1b); m.conv2_w = h16(o_c2w); m.conv2_b = f32(o_c2b);
+  m.enc_pos = f32(o_epos); m.ln_post_g = f32(o_lnpg); m.ln_post_b = f32(o_lnpb);
+  for (auto& e : eo)
+    m.enc.push_back({h16(e.qkv), h16(e.o), h16(e.f1), h16(e.f2), f32(e.bqkv), f32(e.bo), f32(e.bf1), f32(e.bf2),
+                     f32(e.l1g), f32(e.l1b), f32(e.l2g), f32(e.l2b)});
+  for (auto& e : dd)
+    m.dec.push_back({h16(e.qkv), h16(e.o), h16(e.xq), h16(e.xo), h16(e.f1), h16(e.f2), f32(e.bqkv), f32(e.bo),
+                     f32(e.bxq), f32(e.bxo), f32(e.bf1), f32(e.bf2), f32(e.l1g), f32(e.l1b), f32(e.l2g), f32(e.l2b),
+                     f32(e.l3g), f32(e.l3b)});
+  m.w_xkv = h16(o_xkv); m.b_xkv = f32(o_bxkv); m.tok_emb = h16(o_tok); m.dec_pos = f32(o_dpos);
+  m.ln_g = f32(o_lng); m.ln_b = f32(o_lnb);
+  m.mel_filters = f32(o_filt); m.hann = f32(o_hann); m.cos_tab = f32(o_cos); m.sin_tab = f32(o_sin);
+
+  // ---- synthetic weights (oracle/weights.py naming + hash)
+  hipStream_t s = stream;
+  const double sq3 = std::sqrt(3.0);
+  auto fill = [&](void* dst, const std::string& nm, long long rows, int src_cols, int dst_cols, bool is16, double sd) {
+    launch_synth_fill(dst, rows, src_cols, dst_cols, fnv1a64(nm), (float)(sd * sq3), is16, 0, 0.f, s);
+  };
+  auto cfill = [&](float* dst, long long n, float v) { launch_synth_fill(dst, 1, (int)n, (int)n, 0, 0.f, false, 1, v, s); };
+  const double sd = cp.weight_std;
+  fill(m.conv1_w, "encoder.conv1.weight", d, hp.n_mels * 3, m.kp1, true, sd);
+  fill(m.conv1_b, "encoder.conv1.bias", 1, d, d, false, sd);
+  fill(m.conv2_w, "encoder.conv2.weight", d, 3 * d, 3 * d, true, sd);
+  fill(m.conv2_b, "encoder.conv2.bias", 1, d, d, false, sd);
+  fill(m.enc_pos, "encoder.positional_embedding", hp.n_audio_ctx, d, d, false, sd);
+  for (int i = 0; i < hp.n_audio_layer; ++i) {
+    const std::string p = "encoder.blocks." + std::to_string(i) + ".";
+    const EncLayer& e = m.enc[i];
+    fill(e.w_qkv, p + "attn.query.weight", d, d, d, true, sd);
+    fill(e.w_qkv + (size_t)d * d, p + "attn.key.weight", d, d, d, true, sd);
+    fill(e.w_qkv + (size_t)2 * d * d, p + "attn.value.weight", d, d, d, true, sd);
+    fill(e.b_qkv, p + "attn.query.bias", 1, d, d, false, sd);
+    cfill(e.b_qkv + d, d, 0.f);
+    fill(e.b_qkv + 2 * d, p + "attn.value.bias", 1, d, d, false, sd);
+    fill(e.w_o, p + "attn.out.weight", d, d, d, true, sd);
+    fill(e.b_o, p + "attn.out.bias", 1, d, d, false, sd);
+    fill(e.w_fc1, p + "mlp.0.weight", 4 * d, d, d, true, sd);
+    fill(e.b_fc1, p + "mlp.0.bias", 1, 4 * d, 4 * d, false, sd);
+    fill(e.w_fc2, p + "mlp.2.weight", d, 4 * d, 4 * d, true, sd);
+    fill(e.b_fc2, p + "mlp.2.bias", 1, d, d, false, sd);
+    cfill(e.ln1_g, d, 1.f); cfill(e.ln1_b, d, 0.f); cfill(e.ln2_g, d, 1.f); cfill(e.ln2_b, d, 0.f);
+  }
+  cfill(m.ln_post_g, d, 1.f);
+  cfill(m.ln_post_b, d, 0.f);
+  fill(m.tok_emb, "decoder.token_embedding.weight", hp.n_vocab, dt, dt, true, cp.emb_std);
+  fill(m.dec_pos, "decoder.positional_embedding", hp.n_text_ctx, dt, dt, false, sd);
+  for (int i = 0; i < L; ++i) {
+    const std::string p = "decoder.blocks." + std::to_string(i) + ".";
+    const DecLayer& e = m.dec[i];
+    fill(e.w_qkv, p + "attn.query.weight", dt, dt, dt, true, sd);
+    fill(e.w_qkv + (size_t)dt * dt, p + "attn.key.weight", dt, dt, dt, true, sd);
+    fill(e.w_qkv + (size_t)2 * dt * dt, p + "attn.value.weight", dt, dt, dt, true, sd);
+    fill(e.b_qkv, p + "attn.query.bias", 1, dt, dt, false, sd);
+    cfill(e.b_qkv + dt, dt, 0.f);
+    fill(e.b_qkv + 2 * dt, p + "attn.value.bias", 1, dt, dt, false, sd);
+    fill(e.w_o, p + "attn.out.weight", dt, dt, dt, true, sd);
+    fill(e.b_o, p + "attn.out.bias", 1, dt, dt, false, sd);
+    fill(e.w_xq, p + "cross_attn.query.weight", dt, dt, dt, true, sd);
+    fill(e.b_xq, p + "cross_attn.query.bias", 1, dt, dt, false, sd);
+    fill(m.w_xkv + (size_t)i * 2 * dt * d, p + "cross_attn.key.weight", dt, d, d, true, sd);
+    fill(m.w_xkv + (size_t)(i * 2 + 1) * dt * d, p + "cross_attn.value.weight", dt, d, d, true, sd);
+    cfill(m.b_xkv + (size_t)i * 2 * dt, dt, 0.f);
+    fill(m.b_xkv + (size_t)(i * 2 + 1) * dt, p + "cross_attn.value.bias", 1, dt, dt, false, sd);
+    fill(e.w_xo, p + "cross_attn.out.weight", dt, dt, dt, true, sd);
+    fill(e.b_xo, p + "cross_attn.out.bias", 1, dt, dt, false, sd);
+    fill(e.w_fc1, p + "mlp.0.weight", 4 * dt, dt, dt, true, sd);
+    fill(e.b_fc1, p + "mlp.0.bias", 1, 4 * dt, 4 * dt, false, sd);
+    fill(e.w_fc2, p + "mlp.2.weight", dt, 4 * dt, 4 * dt, true, sd);
+    fill(e.b_fc2, p + "mlp.2.bias", 1, dt, dt, false, sd);
+    cfill(e.ln1_g, dt, 1.f); cfill(e.ln1_b, dt, 0.f); cfill(e.ln2_g, dt, 1.f); cfill(e.ln2_b, dt, 0.f);
+    cfill(e.ln3_g, dt, 1.f); cfill(e.ln3_b, dt, 0.f);
+  }
+  cfill(m.ln_g, dt, 1.f);
+  cfill(m.ln_b, dt, 0.f);
+  // mel front-end constants
+  std::vector<float> filt = mel_filters_host(hp.n_mels), hann(400), cs(400), sn(400);
+  for (int i = 0; i < 400; ++i) {
+    hann[i] = (float)(0.5 * (1.0 - std::cos(2.0 * M_PI * i / 400.0)));
+    cs[i] = (float)std::cos(2.0 * M_PI * i / 400.0);
+    sn[i] = (float)(-std::sin(2.0 * M_PI * i / 400.0));
+  }
+  WDR_HIP(hipMemcpyAsync(m.mel_filters, filt.data(), filt.size() * 4, hipMemcpyHostToDevice, s));
+  WDR_HIP(hipMemcpyAsync(m.hann, hann.data(), 1600, hipMemcpyHostToDevice, s));
+  WDR_HIP(hipMemcpyAsync(m.cos_tab, cs.data(), 1600, hipMemcpyHostToDevice, s));
+  WDR_HIP(hipMemcpyAsync(m.sin_tab, sn.data(), 1600, hipMemcpyHostToDevice, s));
+
+  // ---- DTW preset
+  if (cp.dtw) {
+    aheads = alignment_heads_for(name);
+    aheads_per_layer.assign(L, {});
+    for (auto& a : aheads) {
+      WDR_CHECK(a.first < L && a.second < hp.n_text_head, "alignment head out of range for this model");
+      aheads_per_layer[a.first].push_back(a.second);
+    }
+    std::vector<int> flat;
+    for (int l = 0; l < L; ++l) {
+      aheads_dev_off.push_back((int)flat.size());
+      for (int h : aheads_per_layer[l]) flat.push_back(h);
+    }
+    aheads_dev = DevMem(std::max<size_t>(4, flat.size() * 4));
+    if (!flat.empty()) WDR_HIP(hipMemcpyAsync(aheads_dev.p, flat.data(), flat.size() * 4, hipMemcpyHostToDevice, s));
+  }
+  WDR_HIP(hipStreamSynchronize(s));
+}
+
+Context::~Context() {
+  if (stream) (void)hipStreamDestroy(stream);
+}
+
+// ------------------------------------------------------------------ state buffers
+static constexpr int RMAX = 448;   // max decoder rows in one forward (n_text_ctx)
+static constexpr int NSEQ = 8;     // max concurrent decoder sequences
+static constexpr int NSPLIT = 12;  // cross-attention key chunks (1500 / 128)
+
+struct State::Impl {
+  int d, L, H, V, n_mels, kp1;
+  // front-end
+  DevMem x;  int x_cap = 0;   // samples f32
+  DevMem mel; int mel_cap = 0;
+  DevMem gmax, energy_d;
+  int n_fft_frames = 0, n_samples = 0;
+  // encoder
+  DevMem im2col, c1, ex, eh, eqkv, eatt, emlp, xkv;
+  // decoder
+  DevMem xd, hd, qkvd, attd, qx, mlpd, logits, work, tokout, ctl, ml, cap, part_o, part_ml;
+  DevMem rows_tok, rows_pos, rows_seq;
+  DevMem kc, vc;
+  long long seq_stride = 0;   // elements per (layer, seq)
+  // dtw
+  DevMem nrm, xdtw, times;
+  // host pinned
+  int* h_rows = nullptr;       // 3 * RMAX
+  TokOut* h_tok = nullptr;
+  LogitsCtl* h_ctl = nullptr;
+  int* h_times = nullptr;
+  VocabIds vids;
+};
+
+State::State(Context& ctx) : ctx_(ctx), s_(ctx.stream), m_(new Impl) {
+  WDR_HIP(hipSetDevice(ctx.cp.gpu_device));
+  const HParams& hp = ctx.model.hp;
+  Impl& m = *m_;
+  m.d = hp.n_text_state;
+  m.L = hp.n_text_layer;
+  m.H = hp.n_text_head;
+  m.V = hp.n_vocab;
+  m.n_mels = hp.n_mels;
+  m.kp1 = ctx.model.kp1;
+  const int d = m.d;
+  m.gmax = DevMem(16);
+  m.im2col = DevMem((size_t)3000 * std::max(m.kp1, 3 * d) * 2);
+  m.c1 = DevMem((size_t)3000 * d * 2);
+  m.ex = DevMem((size_t)1500 * d * 4);
+  m.eh = DevMem((size_t)1500 * d * 2);
+  m.eqkv = DevMem((size_t)1500 * 3 * d * 2);
+  m.eatt = DevMem((size_t)1500 * d * 2);
+  m.emlp = DevMem((size_t)1500 * 4 * d * 2);
+  m.xkv = DevMem((size_t)1500 * m.L * 2 * d * 2);
+  m.xd = DevMem((size_t)RMAX * d * 4);
+  m.hd = DevMem((size_t)RMAX * d * 2);
+  m.qkvd = DevMem((size_t)RMAX * 3 * d * 2);
+  m.attd = DevMem((size_t)RMAX * d * 2);
+  m.qx = DevMem((size_t)RMAX * d * 2);
+  m.mlpd = DevMem((size_t)RMAX * 4 * d * 2);
+  m.logits = DevMem((size_t)NSEQ * m.V * 4);
+  m.work = DevMem((size_t)NSEQ * m.V * 4);
+  m.tokout = DevMem(NSEQ * sizeof(TokOut));
+  m.ctl = DevMem(NSEQ * sizeof(LogitsCtl));
+  m.ml = DevMem((size_t)m.H * RMAX * sizeof(float2));
+  const int A = std::max<int>(1, (int)ctx.aheads.size());
+  m.cap = DevMem((size_t)A * RMAX * 1500 * 4);
+  m.part_o = DevMem((size_t)NSPLIT * NSEQ * m.H * 64 * 4);
+  m.part_ml = DevMem((size_t)NSPLIT * NSEQ * m.H * sizeof(float2));
+  m.rows_tok = DevMem(RMAX * 4);
+  m.rows_pos = DevMem(RMAX * 4);
+  m.rows_seq = DevMem(RMAX * 4);
+  m.seq_stride = (long long)hp.n_text_ctx * d;
+  m.kc = DevMem((size_t)m.L * NSEQ * m.seq_stride * 2);
+  m.vc = DevMem((size_t)m.L * NSEQ * m.seq_stride * 2);
+  m.nrm = DevMem((size_t)A * RMAX * 1500 * 4);
+  m.xdtw = DevMem((size_t)RMAX * 1500 * 4);
+  m.times = DevMem((RMAX + 8) * 4);
+  WDR_HIP(hipHostMalloc((void**)&m.h_rows, 3 * RMAX * 4, hipHostMallocDefault));
+  WDR_HIP(hipHostMalloc((void**)&m.h_tok, NSEQ * sizeof(TokOut), hipHostMallocDefault));
+  WDR_HIP(hipHostMalloc((void**)&m.h_ctl, NSEQ * sizeof(LogitsCtl), hipHostMallocDefault));
+  WDR_HIP(hipHostMalloc((void**)&m.h_times, (RMAX + 8) * 4, hipHostMallocDefault));
+  const Vocab& v = ctx.vocab;
+  m.vids = VocabIds{v.n_vocab, v.eot, v.sot, v.translate, v.transcribe, v.solm, v.prev, v.nosp, v.not_, v.beg,
+                    v.token_to_id.at(" "), v.sot + 1, 100, -1, 1};
+}
+
+State::~State() {
+  if (m_) {
+    (void)hipHostFree(m_->h_rows);
+    (void)hipHostFree(m_->h_tok);
+    (void)hipHostFree(m_->h_ctl);
+    (void)hipHostFree(m_->h_times);
+  }
+}
+
+// ------------------------------------------------------------------ front-end
+void State::compute_mel(const float* x_host, int n) {
+  Impl& m = *m_;
+  if (n > m.x_cap) {
+    m.x = DevMem((size_t)std::max(n, 1) * 4);
+    m.energy_d = DevMem((size_t)std::max(n, 1) * 4);
+    m.x_cap = n;
+  }
+  const int n_len = (n + 480000 + 400 - 400) / 160;
+  const int n_eff = n + 200;
+  m.n_fft_frames = std::min(n_eff / 160 + 1, n_len);
+  m.n_samples = n;
+  if (m.n_fft_frames > m.mel_cap) {
+    m.mel = DevMem((size_t)m.n_fft_frames * m.n_mels * 4);
+    m.mel_cap = m.n_fft_frames;
+  }
+  if (n > 0) WDR_HIP(hipMemcpyAsync(m.x.p, x_host, (size_t)n * 4, hipMemcpyHostToDevice, s_));
+  launch_gmax_init(m.gmax.as<int>(), s_);
+  MelArgs a{m.x.as<float>(), n, m.n_fft_frames, m.n_mels, ctx_.model.hann, ctx_.model.cos_tab, ctx_.model.sin_tab,
+            ctx_.model.mel_filters, m.mel.as<float>(), m.gmax.as<int>()};
+  launch_mel(a, s_);
+}
+
+void State::read_mel_window(int seek, float* out) {
+  Impl& m = *m_;
+  DevMem tmp((size_t)m.n_mels * 3000 * 4);
+  launch_mel_window(m.mel.as<float>(), m.n_mels, m.n_fft_frames, m.gmax.as<int>(), seek, tmp.as<float>(), s_);
+  WDR_HIP(hipMemcpyAsync(out, tmp.p, tmp.bytes, hipMemcpyDeviceToHost, s_));
+  WDR_HIP(hipStreamSynchronize(s_));
+}
+
+// ------------------------------------------------------------------ encoder
+static void proj(hipStream_t s, const f16* A, int lda, const f16* W, int ldw, const float* bias, void* out, int ldo, int M,
+                 int N, int K, int epi, const float* pos = nullptr, int pos_rows = 0) {
+  ProjArgs a{A, lda, W, ldw, bias, out, ldo, pos, pos_rows, M, N, K, epi};
+  launch_proj(a, s);
+}
+
+static void encoder_body(Context& ctx, State::Impl& m, hipStream_t s) {
+  const Model& md = ctx.model;
+  const HParams& hp = md.hp;
+  const int d = hp.n_audio_state;
+  // conv1 (+GELU) -> c1 f16 [3000][d]
+  proj(s, m.im2col.as<f16>(), md.kp1, md.conv1_w, md.kp1, md.conv1_b, m.c1.p, d, 3000, d, md.kp1, EPI_F16_GELU);
+  launch_im2col_conv2(m.c1.as<f16>(), d, m.im2col.as<f16>(), s);
+  // conv2 (+GELU) + positional -> ex f32 [1500][d]
+  proj(s, m.im2col.as<f16>(), 3 * d, md.conv2_w, 3 * d, md.conv2_b, m.ex.p, d, 1500, d, 3 * d, EPI_F32_GELU_POS,
+       md.enc_pos, hp.n_audio_ctx);
+  const float scale = 1.0f / 8.0f;   // d_head^-1/2
+  for (int l = 0; l < hp.n_audio_layer; ++l) {
+    const EncLayer& e = md.enc[l];
+    launch_layernorm(m.ex.as<float>(), d, e.ln1_g, e.ln1_b, m.eh.as<f16>(), d, 1500, d, s);
+    proj(s, m.eh.as<f16>(), d, e.w_qkv, d, e.b_qkv, m.eqkv.p, 3 * d, 1500, 3 * d, d, EPI_F16);
+    FlashArgs fa{m.eqkv.as<f16>(), 3 * d, 0, m.eqkv.as<f16>() + d, 3 * d, 0, m.eqkv.as<f16>() + 2 * d, 3 * d, 0,
+                 m.eatt.as<f16>(), d, 0, nullptr, 1500, 1500, hp.n_audio_head, 0, scale};
+    launch_flash_attn(fa, 1, s);
+    proj(s, m.eatt.as<f16>(), d, e.w_o, d, e.b_o, m.ex.p, d, 1500, d, d, EPI_F32_RESID);
+    launch_layernorm(m.ex.as<float>(), d, e.ln2_g, e.ln2_b, m.eh.as<f16>(), d, 1500, d, s);
+    proj(s, m.eh.as<f16>(), d, e.w_fc1, d, e.b_fc1, m.emlp.p, 4 * d, 1500, 4 * d, d, EPI_F16_GELU);
+    proj(s, m.emlp.as<f16>(), 4 * d, e.w_fc2, 4 * d, e.b_fc2, m.ex.p, d, 1500, d, 4 * d, EPI_F32_RESID);
+  }
+  launch_layernorm(m.ex.as<float>(), d, md.ln_post_g, md.ln_post_b, m.eh.as<f16>(), d, 1500, d, s);
+  // cross K/V for every decoder layer in one GEMM: [1500][L*2d]
+  const int L = hp.n_text_layer;
+  proj(s, m.eh.as<f16>(), d, md.w_xkv, d, md.b_xkv, m.xkv.p, L * 2 * d, 1500, L * 2 * d, d, EPI_F16);
+}
+
+void State::encode_window(int seek) {
+  Impl& m = *m_;
+  Im2colMelArgs ia{m.mel.as<float>(), m.n_mels, m.n_fft_frames, m.gmax.as<int>(), seek, m.kp1, m.im2col.as<f16>()};
+  launch_im2col_mel(ia, s_);
+  encoder_body(ctx_, m, s_);
+}
+
+void State::encode_from_mel_window(const float* w) {
+  Impl& m = *m_;
+  std::vector<f16> col((size_t)3000 * m.kp1, (f16)0.f);
+  for (int t = 0; t < 3000; ++t)
+    for (int ci = 0; ci < m.n_mels; ++ci)
+      for (int k = 0; k < 3; ++k) {
+        const int u = t + k - 1;
+        if (u >= 0 && u < 3000) col[(size_t)t * m.kp1 + ci * 3 + k] = (f16)w[(size_t)ci * 3000 + u];
+      }
+  WDR_HIP(hipMemcpyAsync(m.im2col.p, col.data(), col.size() * 2, hipMemcpyHostToDevice, s_));
+  encoder_body(ctx_, m, s_);
+  WDR_HIP(hipStreamSynchronize(s_));
+}
+
+void State::read_encoder_out(float* out) {
+  Impl& m = *m_;
+  std::vector<f16> h((size_t)1500 * m.d);
+  WDR_HIP(hipMemcpyAsync(h.data(), m.eh.p, h.size() * 2, hipMemcpyDeviceToHost, s_));
+  WDR_HIP(hipStreamSynchronize(s_));
+  for (size_t i = 0; i < h.size(); ++i) out[i] = (float)h[i];
+}
+
+// ------------------------------------------------------------------ decoder
+// Prefill of `n` tokens into sequence `seq` from an empty cache (positions 0..n-1):
+// whisper.cpp clears the KV cache before the prompt decode and before the DTW pass.
+void State::decoder_prefill(const int* toks, int n, int seq, bool want_logits, bool capture) {
+  Impl& m = *m_;
+  const Model& md = ctx_.model;
+  const HParams& hp = md.hp;
+  const int d = m.d, L = m.L;
+  WDR_CHECK(n >= 1 && n <= RMAX, "decoder prefill: token count out of range");
+  for (int i = 0; i < n; ++i) {
+    m.h_rows[i] = toks[i];
+    m.h_rows[RMAX + i] = i;
+    m.h_rows[2 * RMAX + i] = seq;
+  }
+  WDR_HIP(hipMemcpyAsync(m.rows_tok.p, m.h_rows, n * 4, hipMemcpyHostToDevice, s_));
+  WDR_HIP(hipMemcpyAsync(m.rows_pos.p, m.h_rows + RMAX, n * 4, hipMemcpyHostToDevice, s_));
+  WDR_HIP(hipMemcpyAsync(m.rows_seq.p, m.h_rows + 2 * RMAX, n * 4, hipMemcpyHostToDevice, s_));
+  launch_embed(md.tok_emb, md.dec_pos, m.rows_tok.as<int>(), m.rows_pos.as<int>(), n, d, m.xd.as<float>(), s_);
+  const float scale = 1.0f / 8.0f;
+  const int ldxkv = L * 2 * d;
+  for (int l = 0; l < L; ++l) {
+    const DecLayer& e = md.dec[l];
+    f16* kc = m.kc.as<f16>() + (size_t)l * NSEQ * m.seq_stride;
+    f16* vc = m.vc.as<f16>() + (size_t)l * NSEQ * m.seq_stride;
+    launch_layernorm(m.xd.as<float>(), d, e.ln1_g, e.ln1_b, m.hd.as<f16>(), d, n, d, s_);
+    proj(s_, m.hd.as<f16>(), d, e.w_qkv, d, e.b_qkv, m.qkvd.p, 3 * d, n, 3 * d, d, EPI_F16);
+    launch_kv_scatter(m.qkvd.as<f16>(), 3 * d, d, m.rows_seq.as<int>(), m.rows_pos.as<int>(), n, kc, vc, m.seq_stride,
+                      s_);
+    FlashArgs sa{m.qkvd.as<f16>(), 3 * d, 0, m.qkvd.as<f16>() + d, 3 * d, 0, m.qkvd.as<f16>() + 2 * d, 3 * d, 0,
+                 m.attd.as<f16>(), d, 0, nullptr, n, n, hp.n_text_head, 1, scale};
+    launch_flash_attn(sa, 1, s_);
+    proj(s_, m.attd.as<f16>(), d, e.w_o, d, e.b_o, m.xd.p, d, n, d, d, EPI_F32_RESID);
+    launch_layernorm(m.xd.as<float>(), d, e.ln2_g, e.ln2_b, m.hd.as<f16>(), d, n, d, s_);
+    proj(s_, m.hd.as<f16>(), d, e.w_xq, d, e.b_xq, m.qx.p, d, n, d, d, EPI_F16);
+    const f16* xk = m.xkv.as<f16>() + (size_t)l * 2 * d;
+    const f16* xv = xk + d;
+    const bool cap_layer = capture && !ctx_.aheads_per_layer.empty() && !ctx_.aheads_per_layer[l].empty();
+    if (n > NSEQ || cap_layer) {
+      FlashArgs xa{m.qx.as<f16>(), d, 0, xk, ldxkv, 0, xv, ldxkv, 0, m.attd.as<f16>(), d, 0,
+                   cap_layer ? m.ml.as<float2>() : nullptr, n, 1500, hp.n_text_head, 0, scale};
+      launch_flash_attn(xa, 1, s_);
+      if (cap_layer) {
+        int slot0 = 0;
+        for (int q = 0; q < l; ++q) slot0 += (int)ctx_.aheads_per_layer[q].size();
+        CaptureArgs ca{m.qx.as<f16>(), d, xk, ldxkv, m.ml.as<float2>(), ctx_.aheads_dev.as<int>() + ctx_.aheads_dev_off[l],
+                       m.cap.as<float>(), slot0, n, 1500, scale};
+        launch_aheads_capture(ca, (int)ctx_.aheads_per_layer[l].size(), s_);
+      }
+    } else {
+      XAttnArgs xa{m.qx.as<f16>(), d, xk, xv, ldxkv, 1500, n, hp.n_text_head, scale, m.part_o.as<float>(),
+                   m.part_ml.as<float2>(), m.attd.as<f16>(), d};
+      launch_xattn(xa, s_);
+    }
+    proj(s_, m.attd.as<f16>(), d, e.w_xo, d, e.b_xo, m.xd.p, d, n, d, d, EPI_F32_RESID);
+    launch_layernorm(m.xd.as<float>(), d, e.ln3_g, e.ln3_b, m.hd.as<f16>(), d, n, d, s_);
+    proj(s_, m.hd.as<f16>(), d, e.w_fc1, d, e.b_fc1, m.mlpd.p, 4 * d, n, 4 * d, d, EPI_F16_GELU);
+    proj(s_, m.mlpd.as<f16>(), 4 * d, e.w_fc2, 4 * d, e.b_fc2, m.xd.p, d, n, d, 4 * d, EPI_F32_RESID);
+  }
+  if (want_logits) {
+    launch_layernorm(m.xd.as<float>() + (size_t)(n - 1) * d, d, md.ln_g, md.ln_b, m.hd.as<f16>(), d, 1, d, s_);
+    proj(s_, m.hd.as<f16>(), d, md.tok_emb, d, nullptr, m.logits.p, m.V, 1, m.V, d, EPI_F32);
+  }
+  times.prefills++;
+}
+
+// One decode step for R rows: row r appends token toks[r] at position pos[r] of sequence seqs[r].
+void State::decoder_step(const int* toks, const int* seqs, const int* pos, int R) {
+  Impl& m = *m_;
+  const Model& md = ctx_.model;
+  const HParams& hp = md.hp;
+  const int d = m.d, L = m.L;
+  WDR_CHECK(R >= 1 && R <= NSEQ, "decoder step: row count out of range");
+  for (int i = 0; i < R; ++i) {
+    m.h_rows[i] = toks[i];
+    m.h_rows[RMAX + i] = pos[i];
+    m.h_rows[2 * RMAX + i] = seqs[i];
+  }
+  WDR_HIP(hipMemcpyAsync(m.rows_tok.p, m.h_rows, R * 4, hipMemcpyHostToDevice, s_));
+  WDR_HIP(hipMemcpyAsync(m.rows_pos.p, m.h_rows + RMAX, R * 4, hipMemcpyHostToDevice, s_));
+  WDR_HIP(hipMemcpyAsync(m.rows_seq.p, m.h_rows + 2 * RMAX, R * 4, hipMemcpyHostToDevice, s_));
+  launch_embed(md.tok_emb, md.dec_pos, m.rows_tok.as<int>(), m.rows_pos.as<int>(), R, d, m.xd.as<float>(), s_);
+  const float scale = 1.0f / 8.0f;
+  const int ldxkv = L * 2 * d;
+  for (int l = 0; l < L; ++l) {
+    const DecLayer& e = md.dec[l];
+    f16* kc = m.kc.as<f16>() + (size_t)l * NSEQ * m.seq_stride;
+    f16* vc = m.vc.as<f16>() + (size_t)l * NSEQ * m.seq_stride;
+    launch_layernorm(m.xd.as<float>(), d, e.ln1_g, e.ln1_b, m.hd.as<f16>(), d, R, d, s_);
+    proj(s_, m.hd.as<f16>(), d, e.w_qkv, d, e.b_qkv, m.qkvd.p, 3 * d, R, 3 * d, d, EPI_F16);
+    launch_kv_scatter(m.qkvd.as<f16>(), 3 * d, d, m.rows_seq.as<int>(), m.rows_pos.as<int>(), R, kc, vc, m.seq_stride,
+                      s_);
+    DecSelfArgs sa{m.qkvd.as<f16>(), 3 * d, kc, vc, m.seq_stride, d, m.rows_seq.as<int>(), m.rows_pos.as<int>(),
+                   m.attd.as<f16>(), d, scale};
+    launch_dec_self_attn(sa, R, hp.n_text_head, s_);
+    proj(s_, m.attd.as<f16>(), d, e.w_o, d, e.b_o, m.xd.p, d, R, d, d, EPI_F32_RESID);
+    launch_layernorm(m.xd.as<float>(), d, e.ln2_g, e.ln2_b, m.hd.as<f16>(), d, R, d, s_);
+    proj(s_, m.hd.as<f16>(), d, e.w_xq, d, e.b_xq, m.qx.p, d, R, d, d, EPI_F16);
+    const f16* xk = m.xkv.as<f16>() + (size_t)l * 2 * d;
+    XAttnArgs xa{m.qx.as<f16>(), d, xk, xk + d, ldxkv, 1500, R, hp.n_text_head, scale, m.part_o.as<float>(),
+                 m.part_ml.as<float2>(), m.attd.as<f16>(), d};
+    launch_xattn(xa, s_);
+    proj(s_, m.attd.as<f16>(), d, e.w_xo, d, e.b_xo, m.xd.p, d, R, d, d, EPI_F32_RESID);
+    launch_layernorm(m.xd.as<float>(), d, e.ln3_g, e.ln3_b, m.hd.as<f16>(), d, R, d, s_);
+    proj(s_, m.hd.as<f16>(), d, e.w_fc1, d, e.b_fc1, m.mlpd.p, 4 * d, R, 4 * d, d, EPI_F16_GELU);
+    proj(s_, m.mlpd.as<f16>(), 4 * d, e.w_fc2, 4 * d, e.b_fc2, m.xd.p, d, R, d, 4 * d, EPI_F32_RESID);
+  }
+  launch_layernorm(m.xd.as<float>(), d, md.ln_g, md.ln_b, m.hd.as<f16>(), d, R, d, s_);
+  proj(s_, m.hd.as<f16>(), d, md.tok_emb, d, nullptr, m.logits.p, m.V, R, m.V, d, EPI_F32);
+  times.decode_steps++;
+}
+
+void State::run_logits(int R, const LogitsCtl* ctl, TokenData* out, float* nosp) {
+  Impl& m = *m_;
+  memcpy(m.h_ctl, ctl, R * sizeof(LogitsCtl));
+  WDR_HIP(hipMemcpyAsync(m.ctl.p, m.h_ctl, R * sizeof(LogitsCtl), hipMemcpyHostToDevice, s_));
+  launch_logits_process(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, m.work.as<float>(),
+                        m.tokout.as<TokOut>(), s_);
+  WDR_HIP(hipMemcpyAsync(m.h_tok, m.tokout.p, R * sizeof(TokOut), hipMemcpyDeviceToHost, s_));
+  WDR_HIP(hipStreamSynchronize(s_));
+  for (int r = 0; r < R; ++r) {
+    const TokOut& o = m.h_tok[r];
+    TokenData t;
+    t.id = o.id;
+    t.tid = o.tid;
+    t.p = o.p;
+    t.plog = o.plog;
+    t.pt = o.pt;
+    t.ptsum = o.ptsum;
+    out[r] = t;
+    if (nosp) nosp[r] = o.nosp_prob;
+  }
+}
+
+void State::decode_logits(const int* toks, int n, float* logits_out) {
+  decoder_prefill(toks, n, 0, true, false);
+  WDR_HIP(hipMemcpyAsync(logits_out, m_->logits.p, (size_t)m_->V * 4, hipMemcpyDeviceToHost, s_));
+  WDR_HIP(hipStreamSynchronize(s_));
+}
+
+void State::dtw_capture(const int* toks, int n, float* cap_out) {
+  decoder_prefill(toks, n, 0, false, true);
+  const size_t A = ctx_.aheads.size();
+  WDR_HIP(hipMemcpyAsync(cap_out, m_->cap.p, A * n * 1500 * 4, hipMemcpyDeviceToHost, s_));
+  WDR_HIP(hipStreamSynchronize(s_));
+}
+
+// ------------------------------------------------------------------ timestamps
+static float voice_length(const std::string& text) {
+  float res = 0.f;
+  for (char c : text) {
+    if (c == ' ') res += 0.01f;
+    else if (c == ',') res += 2.00f;
+    else if (c == '.' || c == '!' || c == '?') res += 3.00f;
+    else if (c >= '0' && c <= '9') res += 3.00f;
+    else res += 1.00f;
+  }
+  return res;
+}
+
+void State::heuristic_timestamps(int i_segment, const FullParams& p) {
+  const Vocab& v = ctx_.vocab;
+  ResultSeg& seg = result_all[i_segment];
+  auto& tk = seg.tokens;
+  const int n_samples = (int)energy.size();
+  if (n_samples == 0) return;
+  const long long t0 = seg.t0, t1 = seg.t1;
+  const int n = (int)tk.size();
+  if (n == 0) return;
+  if (n == 1) {
+    tk[0].t0 = t0;
+    tk[0].t1 = t1;
+    return;
+  }
+  for (int j = 0; j < n; ++j) {
+    TokenData& t = tk[j];
+    if (j == 0) {
+      if (t.id == v.beg) {
+        tk[0].t0 = t0;
+        tk[0].t1 = t0;
+        tk[1].t0 = t0;
+        t_beg = t0;
+        t_last = t0;
+        tid_last = v.beg;
+      } else {
+        tk[0].t0 = t_last;
+      }
+    }
+    const long long tt = t_beg + 2 * (long long)(t.tid - v.beg);
+    t.vlen = voice_length(v.id_to_token[t.id]);
+    if (t.pt > p.thold_pt && t.ptsum > p.thold_ptsum && t.tid > tid_last && tt <= t1) {
+      if (j > 0) tk[j - 1].t1 = tt;
+      t.t0 = tt;
+      tid_last = t.tid;
+    }
+  }
+  tk[n - 2].t1 = t1;
+  tk[n - 1].t0 = t1;
+  tk[n - 1].t1 = t1;
+  t_last = t1;
+  {
+    int p0 = 0, p1 = 0;
+    while (true) {
+      while (p1 < n && tk[p1].t1 < 0) p1++;
+      if (p1 >= n) p1--;
+      if (p1 > p0) {
+        double psum = 0.0;
+        for (int j = p0; j <= p1; j++) psum += tk[j].vlen;
+        const double dt = (double)(tk[p1].t1 - tk[p0].t0);
+        for (int j = p0 + 1; j <= p1; j++) {
+          const double ct = tk[j - 1].t0 + dt * tk[j - 1].vlen / psum;
+          tk[j - 1].t1 = (long long)ct;
+          tk[j].t0 = (long long)ct;
+        }
+      }
+      p1++;
+      p0 = p1;
+      if (p1 >= n) break;
+    }
+  }
+  for (int j = 0; j < n - 1; j++) {
+    if (tk[j].t1 < 0) tk[j + 1].t0 = tk[j].t1;
+    if (j > 0 && tk[j - 1].t1 > tk[j].t0) {
+      tk[j].t0 = tk[j - 1].t1;
+      tk[j].t1 = std::max(tk[j].t0, tk[j].t1);
+    }
+  }
+  const int hw = 16000 / 8;
+  auto ts2s = [&](long long t) { return (int)std::max(0LL, std::min((long long)n_samples - 1, (t * 16000) / 100)); };
+  auto s2ts = [&](int i) { return (100LL * i) / 16000; };
+  for (int j = 0; j < n; j++) {
+    if (tk[j].id >= v.eot) continue;
+    int s0 = ts2s(tk[j].t0);
+    int s1 = ts2s(tk[j].t1);
+    const int ss0 = std::max(s0 - hw, 0);
+    const int ss1 = std::min(s1 + hw, n_samples);
+    const int ns = ss1 - ss0;
+    float sum = 0.0f;
+    for (int k = ss0; k < ss1; k++) sum += energy[k];
+    const float thold = 0.5 * sum / ns;
+    {
+      int k = s0;
+      if (energy[k] > thold && j > 0) {
+        while (k > 0 && energy[k] > thold) k--;
+        tk[j].t0 = s2ts(k);
+        if (tk[j].t0 < tk[j - 1].t1) tk[j].t0 = tk[j - 1].t1;
+        else s0 = k;
+      } else {
+        while (energy[k] < thold && k < s1) k++;
+        s0 = k;
+        tk[j].t0 = s2ts(k);
+      }
+    }
+    {
+      int k = s1;
+      if (energy[k] > thold) {
+        while (k < n_samples - 1 && energy[k] > thold) k++;
+        tk[j].t1 = s2ts(k);
+        if (j < ns - 1 && j + 1 < n && tk[j].t1 > tk[j + 1].t0) tk[j].t1 = tk[j + 1].t0;
+        else s1 = k;
+      } else {
+        while (energy[k] < thold && k > s0) k--;
+        s1 = k;
+        tk[j].t1 = s2ts(k);
+      }
+    }
+  }
+}
+
+void State::dtw_timestamps(int i_segment, int n_segments, int seek, int n_frames, const std::string& language) {
+  Impl& m = *m_;
+  const Vocab& v = ctx_.vocab;
+  std::vector<int> toks = {v.sot};
+  if (v.multilingual) toks.push_back(v.token_lang(std::max(0, lang_id_from_str(language))));
+  const int sot_len = (int)toks.size();
+  toks.push_back(v.not_);
+  for (int s = i_segment; s < i_segment + n_segments; ++s)
+    for (auto& t : result_all[s].tokens)
+      if (t.id < v.eot) toks.push_back(t.id);
+  toks.push_back(v.eot);
+  const int N = (int)toks.size();
+  decoder_prefill(toks.data(), N, 0, false, true);
+  const int n_audio = n_frames / 2;
+  launch_dtw(m.cap.as<float>(), (int)ctx_.aheads.size(), N, 1500, n_audio, sot_len, seek, m.nrm.as<float>(),
+             m.xdtw.as<float>(), m.times.as<int>(), m.times.as<int>() + RMAX + 4, s_);
+  WDR_HIP(hipMemcpyAsync(m.h_times, m.times.p, (RMAX + 8) * 4, hipMemcpyDeviceToHost, s_));
+  WDR_HIP(hipStreamSynchronize(s_));
+  const int nt = m.h_times[RMAX + 4];
+  int k = 0;
+  for (int s = i_segment; s < i_segment + n_segments && k < nt; ++s)
+    for (auto& t : result_all[s].tokens) {
+      if (k >= nt) break;
+      if (t.id < v.eot) t.t_dtw = m.h_times[k++];
+    }
+}
+
+// ------------------------------------------------------------------ whisper_full
+static int c_round(double x) { return x >= 0 ? (int)std::floor(x + 0.5) : -(int)std::floor(-x + 0.5); }
+
+struct Seq {
+  std::vector<TokenData> tokens;
+  int result_len = 0, seek_delta = 3000;
+  bool has_ts = false, failed = false, completed = false;
+  double sum_logprobs = -INFINITY, avg_logprobs = -INFINITY, entropy = 0.0, score = -INFINITY;
+  float no_speech_prob = 0.f;
+};
+
+static void score_sequence(Seq& s, const FullParams& p) {
+  if (s.result_len == 0) return;
+  double res = 0.0;
+  for (int i = 0; i < s.result_len; ++i) res += s.tokens[i].plog;
+  s.sum_logprobs = res;
+  s.avg_logprobs = res / s.result_len;
+  double pen = s.result_len;
+  if (p.length_penalty > 0.0f) pen = std::pow((5.0 + pen) / 6.0, p.length_penalty);
+  s.score = res / pen;
+  std::map<int, int> cnt;
+  int tot = 0;
+  for (int i = std::max(0, s.result_len - 32); i < s.result_len; ++i) {
+    cnt[s.tokens[i].id]++;
+    tot++;
+  }
+  double ent = 0.0;
+  for (auto& kv : cnt) {
+    const double pr = kv.second / (double)tot;
+    ent -= pr * std::log(pr);
+  }
+  s.entropy = ent;
+}
+
+int State::full(const FullParams& params, const float* samples, int n) {
+  WDR_HIP(hipSetDevice(ctx_.cp.gpu_device));
+  Impl& m = *m_;
+  const Vocab& v = ctx_.vocab;
+  const HParams& hp = ctx_.model.hp;
+  WDR_CHECK(params.greedy, "beam-search decoding is not available yet: set sampling_strategy = \"greedy\"");
+  result_all.clear();
+  double t_start = now_s();
+  compute_mel(samples, n);
+  if (params.token_timestamps) {
+    t_beg = t_last = tid_last = 0;
+    energy.assign(n, 0.f);
+    if (n > 0) {
+      launch_energy(m.x.as<float>(), n, m.energy_d.as<float>(), s_);
+      WDR_HIP(hipMemcpyAsync(energy.data(), m.energy_d.p, (size_t)n * 4, hipMemcpyDeviceToHost, s_));
+    }
+  }
+  WDR_HIP(hipStreamSynchronize(s_));
+  times.mel += now_s() - t_start;
+  const int seek_start = 0;
+  const int seek_end = 1 + (int)((n + 200 - 400) / 160);
+  const int delta_min = 10;
+  if (seek_end < seek_start + delta_min) return 0;
+
+  std::vector<int> prompt_past;
+  if (params.has_initial_prompt && !params.initial_prompt.empty()) prompt_past = v.tokenize(params.initial_prompt);
+
+  int encoded_seek = -1;
+  auto encode = [&](int seek) {
+    if (encoded_seek != seek) {
+      const double t = now_s();
+      encode_window(seek);
+      WDR_HIP(hipStreamSynchronize(s_));
+      times.encode += now_s() - t;
+      times.windows++;
+      encoded_seek = seek;
+    }
+  };
+
+  std::string language = params.language;
+  if (language.empty() || language == "auto") {
+    encode(seek_start);
+    const double t = now_s();
+    const int sot = v.sot;
+    decoder_prefill(&sot, 1, 0, true, false);
+    std::vector<float> ll(100);
+    WDR_HIP(hipMemcpyAsync(ll.data(), m.logits.as<float>() + v.sot + 1, 100 * 4, hipMemcpyDeviceToHost, s_));
+    WDR_HIP(hipStreamSynchronize(s_));
+    int best = 0;
+    for (int i = 1; i < 100; ++i)
+      if (ll[i] > ll[best]) best = i;
+    lang_id = best;
+    language = kLangs[best];
+    times.decode += now_s() - t;
+  }
+  std::vector<int> prompt_init = {v.sot};
+  if (v.multilingual) {
+    lang_id = std::max(0, lang_id_from_str(language));
+    prompt_init.push_back(v.token_lang(lang_id));
+    prompt_init.push_back(params.translate ? v.translate : v.transcribe);
+  }
+  std::vector<float> temps;
+  if (params.temperature_inc > 0.0f) {
+    for (float t = params.temperature; t < 1.0f + 1e-6f; t += params.temperature_inc) temps.push_back(t);
+  } else {
+    temps.push_back(params.temperature);
+  }
+  if (params.max_initial_ts > 0.0f) {
+    const float precision = 30.0f / hp.n_audio_ctx;
+    m.vids.max_initial_tid = (int)std::round(params.max_initial_ts / precision);
+  } else {
+    m.vids.max_initial_tid = -1;
+  }
+  m.vids.suppress_blank = params.suppress_blank ? 1 : 0;
+
+  int seek = seek_start;
+  const int n_text_ctx = hp.n_text_ctx;
+  std::vector<int> prompt;
+  while (true) {
+    if (seek + 100 >= seek_end) break;
+    encode(seek);
+    if (seek > seek_start && seek + 500 >= seek_end) prompt_past.clear();
+    Seq best;
+    const double t_dec = now_s();
+    for (size_t it = 0; it < temps.size(); ++it) {
+      const float t_cur = temps[it];
+      WDR_CHECK(t_cur <= 0.0f, "temperature fallback sampling (t > 0) is not available yet");
+      prompt.clear();
+      if (!prompt_past.empty() && t_cur < 0.5f && params.n_max_text_ctx > 0) {
+        const int n_take = std::min(std::min(params.n_max_text_ctx, n_text_ctx / 2), (int)prompt_past.size());
+        prompt.push_back(v.prev);
+        prompt.insert(prompt.end(), prompt_past.end() - n_take, prompt_past.end());
+      }
+      prompt.insert(prompt.end(), prompt_init.begin(), prompt_init.end());
+      decoder_prefill(prompt.data(), (int)prompt.size(), 0, true, false);
+      const int window = std::min(seek_end - seek, 3000);
+      int Lf = 0;
+      if (params.force_len_rate > 0.f) Lf = std::max(3, c_round(params.force_len_rate * window / 100.0) + 3);
+      Seq sq;
+      const int n_max = n_text_ctx / 2 - 4;
+      float nosp = 0.f;
+      for (int i = 0; i < n_max; ++i) {
+        LogitsCtl c{};
+        c.n_tokens = (int)sq.tokens.size();
+        c.last_ts = !sq.tokens.empty() && sq.tokens.back().id >= v.beg;
+        c.pen_ts = sq.tokens.size() < 2 || sq.tokens[sq.tokens.size() - 2].id >= v.beg;
+        c.has_ts = sq.has_ts;
+        c.seek_delta = sq.seek_delta;
+        c.temperature = t_cur;
+        if (Lf) {
+          if (i == 0) { c.force_kind = 1; c.force_tok = v.beg; }
+          else if (i < Lf - 2) c.force_kind = 2;
+          else if (i == Lf - 2) { c.force_kind = 1; c.force_tok = v.beg + std::min(1500, std::max(1, (window - delta_min - 1) / 2)); }
+          else { c.force_kind = 1; c.force_tok = v.eot; }
+        }
+        TokenData tok;
+        float ns = 0.f;
+        run_logits(1, &c, &tok, &ns);
+        if (i == 0) nosp = ns;
+        sq.tokens.push_back(tok);
+        if (tok.id > v.beg) {
+          const int sdn = 2 * (tok.id - v.beg);
+          if (sq.has_ts && sq.seek_delta > sdn && sq.result_len < i) {
+            sq.failed = true;
+            break;
+          }
+          sq.seek_delta = sdn;
+          sq.result_len = i + 1;
+          sq.has_ts = true;
+        }
+        if (tok.id == v.eot || (params.max_tokens > 0 && i >= params.max_tokens) ||
+            (sq.has_ts && seek + sq.seek_delta + delta_min >= seek_end)) {
+          if (sq.result_len == 0) {
+            if (seek + sq.seek_delta + delta_min >= seek_end) {
+              sq.result_len = i + 1;
+            } else {
+              sq.failed = true;
+              break;
+            }
+          }
+          if (params.single_segment) {
+            sq.result_len = i + 1;
+            sq.seek_delta = 3000;
+          }
+          sq.completed = true;
+          break;
+        }
+        if (i == n_max - 1 && (sq.result_len == 0 || sq.seek_delta < 3000 / 2)) {
+          sq.failed = true;
+          break;
+        }
+        const int pos = (int)prompt.size() + i;
+        const int seq0 = 0;
+        decoder_step(&tok.id, &seq0, &pos, 1);
+      }
+      sq.tokens.resize(std::min((int)sq.tokens.size(), sq.result_len));
+      score_sequence(sq, params);
+      if (!sq.failed && sq.result_len > 32 && sq.entropy < params.entropy_thold) sq.failed = true;
+      sq.no_speech_prob = nosp;
+      best = sq;
+      bool success = true;
+      if (it != temps.size() - 1) {
+        if (sq.failed || (sq.avg_logprobs < params.logprob_thold && sq.no_speech_prob < params.no_speech_thold))
+          success = false;
+      }
+      if (success) break;
+    }
+    times.decode += now_s() - t_dec;
+    int seek_delta = best.seek_delta;
+    const int result_len = best.result_len;
+    auto& tokens_cur = best.tokens;
+    const size_t n_before = result_all.size();
+    const bool is_no_speech = best.no_speech_prob > params.no_speech_thold && best.avg_logprobs < params.logprob_thold;
+    std::vector<int> new_past;
+    if (!prompt.empty() && prompt.front() == v.prev)
+      new_past.insert(new_past.end(), prompt.begin() + 1, prompt.end() - prompt_init.size());
+    for (int i = 0; i < result_len && !is_no_speech; ++i) new_past.push_back(tokens_cur[i].id);
+    prompt_past = new_past;
+    if (!tokens_cur.empty() && !is_no_speech) {
+      const long long t0 = seek + 2LL * (tokens_cur.front().tid - v.beg);
+      std::string text;
+      for (auto& t : tokens_cur)
+        if (t.id < v.eot) text += v.id_to_token[t.id];
+      if (!text.empty()) {
+        const long long t1 = seek + seek_delta;
+        result_all.push_back({t0, t1, text, tokens_cur});
+        if (params.token_timestamps) heuristic_timestamps((int)result_all.size() - 1, params);
+      }
+    }
+    const int n_new = (int)(result_all.size() - n_before);
+    if (!ctx_.aheads.empty() && n_new) {
+      const double t = now_s();
+      const int n_frames = std::min(std::min(3000, seek_delta), seek_end - seek);
+      dtw_timestamps((int)n_before, n_new, seek, n_frames, language);
+      times.dtw += now_s() - t;
+    }
+    if (tokens_cur.size() > 1 && tokens_cur[tokens_cur.size() - 2].id < v.beg && tokens_cur.back().id > v.beg)
+      seek_delta = std::min(seek_end - seek, 3000);
+    seek += seek_delta;
+  }
+  return 0;
+}
+
+}  // namespace wdr

@@ -1,0 +1,374 @@
+"""Python mirror of the whisper-diarize-rs public API over libwdr's C ABI.
+
+Same names, argument meaning and error behaviour as the reference crate
+(src/lib.rs:12-17 re-exports; src/types.rs; src/engine.rs), so a caller of
+`Engine::transcribe_audio` finds the same surface.  Every call goes through
+libwdr.so (HIP, gfx950); there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import dataclasses
+import enum
+from typing import Callable, List, Optional
+
+import numpy as np
+
+from . import _lib as L
+
+__all__ = ["Engine", "EngineConfig", "TranscribeOptions", "AdvancedTranscribe", "Segment", "WordTimestamp",
+           "ProgressType", "Callbacks", "Synthetic", "WhisperContext", "SpeechSegment", "read_wav", "vad_merge",
+           "WdrError"]
+
+WdrError = L.WdrError
+
+
+class ProgressType(enum.IntEnum):          # src/types.rs:5-9
+    Download = 0
+    Transcribe = 1
+    Translate = 2
+
+
+@dataclasses.dataclass
+class AdvancedTranscribe:                  # src/types.rs:16-24
+    sampling_strategy: Optional[str] = None
+    best_of_or_beam_size: Optional[int] = None
+    n_threads: Optional[int] = None
+    temperature: Optional[float] = None
+    max_text_ctx: Optional[int] = None
+    init_prompt: Optional[str] = None
+    diarize_threshold: Optional[float] = None
+
+
+@dataclasses.dataclass
+class TranscribeOptions:                   # src/types.rs:28-61 (defaults)
+    offset: Optional[float] = 0.0
+    model: str = "base"
+    lang: Optional[str] = "auto"
+    whisper_to_english: Optional[bool] = False
+    translate_target: Optional[str] = None
+    enable_vad: Optional[bool] = True
+    enable_diarize: Optional[bool] = None
+    max_speakers: Optional[int] = None
+    advanced: Optional[AdvancedTranscribe] = None
+
+
+@dataclasses.dataclass
+class WordTimestamp:                       # src/types.rs:64-70
+    text: str
+    start: float
+    end: float
+    probability: Optional[float] = None
+
+
+@dataclasses.dataclass
+class Segment:                             # src/types.rs:74-82
+    start: float
+    end: float
+    text: str
+    words: Optional[List[WordTimestamp]] = None
+    speaker_id: Optional[str] = None
+
+
+@dataclasses.dataclass
+class SpeechSegment:                       # src/types.rs:86-90
+    start: float
+    end: float
+    samples: np.ndarray
+
+
+@dataclasses.dataclass
+class EngineConfig:                        # src/engine.rs:9-33 (defaults)
+    cache_dir: str = "./cache"
+    enable_dtw: Optional[bool] = True
+    enable_flash_attn: Optional[bool] = False
+    use_gpu: Optional[bool] = True
+    gpu_device: Optional[int] = None
+    vad_model_path: Optional[str] = None
+    diarize_segment_model_path: Optional[str] = None
+    diarize_embedding_model_path: Optional[str] = None
+
+
+@dataclasses.dataclass
+class Callbacks:                           # src/engine.rs:35-40
+    progress: Optional[Callable[[int, ProgressType, str], None]] = None
+    new_segment_callback: Optional[Callable[[Segment], None]] = None
+    is_cancelled: Optional[Callable[[], bool]] = None
+
+
+@dataclasses.dataclass
+class Synthetic:
+    """Synthetic-weight / workload-pin knobs (no checkpoints here)."""
+    weight_std: float = 0.02
+    emb_std: float = 0.02
+    force_len_rate: float = 0.0
+    disable_fallback: bool = False
+
+
+def _ob(v):
+    return -1 if v is None else (1 if v else 0)
+
+
+def _s(v):
+    return None if v is None else v.encode()
+
+
+class _Keep:
+    """Keeps ctypes buffers alive for the duration of a call."""
+
+    def __init__(self):
+        self.objs = []
+
+    def __call__(self, o):
+        self.objs.append(o)
+        return o
+
+
+def _opts(o: Optional[TranscribeOptions], keep: _Keep):
+    if o is None:
+        return None
+    t = L.TranscribeOptions()
+    t.has_offset = 0 if o.offset is None else 1
+    t.offset = o.offset or 0.0
+    t.model = keep(_s(o.model))
+    t.lang = keep(_s(o.lang))
+    t.whisper_to_english = _ob(o.whisper_to_english)
+    t.translate_target = keep(_s(o.translate_target))
+    t.enable_vad = _ob(o.enable_vad)
+    t.enable_diarize = _ob(o.enable_diarize)
+    t.has_max_speakers = 0 if o.max_speakers is None else 1
+    t.max_speakers = o.max_speakers or 0
+    if o.advanced is not None:
+        a = o.advanced
+        A = L.Advanced()
+        A.sampling_strategy = keep(_s(a.sampling_strategy))
+        for f in ("best_of_or_beam_size", "n_threads", "temperature", "max_text_ctx", "diarize_threshold"):
+            v = getattr(a, f)
+            setattr(A, "has_" + f, 0 if v is None else 1)
+            setattr(A, f, v or 0)
+        A.init_prompt = keep(_s(a.init_prompt))
+        keep(A)
+        t.advanced = C.pointer(A)
+    return keep(t)
+
+
+def _syn(s: Optional[Synthetic]):
+    if s is None:
+        return None
+    return L.Synthetic(s.weight_std, s.emb_std, s.force_len_rate, 1 if s.disable_fallback else 0)
+
+
+def _segments(lst_ptr) -> tuple:
+    lst = lst_ptr.contents
+    out = []
+    for i in range(lst.n_segments):
+        s = lst.segments[i]
+        words = None
+        if s.words:
+            words = [WordTimestamp(s.words[k].text.decode("utf-8", "replace"), s.words[k].start, s.words[k].end,
+                                   s.words[k].probability if s.words[k].has_probability else None)
+                     for k in range(s.n_words)]
+        out.append(Segment(s.start, s.end, s.text.decode("utf-8", "replace"), words,
+                           s.speaker_id.decode() if s.speaker_id else None))
+    lang = lst.detected_lang.decode() if lst.detected_lang else None
+    L.load().wdr_segment_list_free(lst_ptr)
+    return out, lang
+
+
+def _callbacks(cb: Optional[Callbacks], keep: _Keep):
+    if cb is None:
+        return None
+    c = L.Callbacks()
+    if cb.progress:
+        c.progress = keep(L.PROGRESS_FN(lambda u, p, t, lbl: cb.progress(int(p), ProgressType(t), lbl.decode())))
+    if cb.new_segment_callback:
+        def seg_cb(u, sp):
+            s = sp.contents
+            words = None
+            if s.words:
+                words = [WordTimestamp(s.words[k].text.decode(), s.words[k].start, s.words[k].end,
+                                       s.words[k].probability if s.words[k].has_probability else None)
+                         for k in range(s.n_words)]
+            cb.new_segment_callback(Segment(s.start, s.end, s.text.decode(), words,
+                                            s.speaker_id.decode() if s.speaker_id else None))
+        c.new_segment = keep(L.SEGMENT_FN(seg_cb))
+    if cb.is_cancelled:
+        c.is_cancelled = keep(L.CANCEL_FN(lambda u: 1 if cb.is_cancelled() else 0))
+    return keep(c)
+
+
+def read_wav(path: str) -> np.ndarray:
+    """audio::read_wav (src/audio.rs:4-24)."""
+    lib = L.load()
+    p = C.POINTER(C.c_int16)()
+    n = C.c_size_t()
+    L.check(lib.wdr_read_wav(path.encode(), C.byref(p), C.byref(n)))
+    out = np.ctypeslib.as_array(p, shape=(n.value,)).copy() if n.value else np.zeros(0, np.int16)
+    lib.wdr_free(p)
+    return out
+
+
+def vad_merge(segs_cs, samples: np.ndarray):
+    """The crate's own post-processing of whisper.cpp VAD segments (src/vad.rs:33-84)."""
+    lib = L.load()
+    st = np.ascontiguousarray([s for s, _ in segs_cs], np.float64)
+    en = np.ascontiguousarray([e for _, e in segs_cs], np.float64)
+    n = len(st)
+    mask = np.zeros(2 * max(n, 1))
+    merged = np.zeros(2 * max(n, 1))
+    idx = np.zeros(2 * max(n, 1), np.int64)
+    nm, nmr = C.c_size_t(), C.c_size_t()
+    smp = np.ascontiguousarray(samples, np.int16)
+    L.check(lib.wdr_vad_merge(st.ctypes.data_as(C.POINTER(C.c_double)), en.ctypes.data_as(C.POINTER(C.c_double)), n,
+                              smp.ctypes.data_as(C.POINTER(C.c_int16)), smp.size,
+                              mask.ctypes.data_as(C.POINTER(C.c_double)), C.byref(nm),
+                              merged.ctypes.data_as(C.POINTER(C.c_double)), idx.ctypes.data_as(C.POINTER(C.c_int64)),
+                              C.byref(nmr)))
+    m = [(mask[2 * i], mask[2 * i + 1]) for i in range(nm.value)]
+    out = [SpeechSegment(merged[2 * i], merged[2 * i + 1], smp[idx[2 * i]:idx[2 * i + 1]].copy())
+           for i in range(nmr.value)]
+    return m, out
+
+
+class WhisperContext:
+    """transcribe::create_context (src/transcribe.rs:89-166) + its whisper_state."""
+
+    def __init__(self, model_name: str, model_path: Optional[str] = None, gpu_device: Optional[int] = None,
+                 use_gpu: Optional[bool] = None, enable_dtw: Optional[bool] = True,
+                 enable_flash_attn: Optional[bool] = None, num_samples: Optional[int] = None,
+                 synthetic: Optional[Synthetic] = None):
+        lib = L.load()
+        self._lib = lib
+        h = C.c_void_p()
+        syn = _syn(synthetic)
+        L.check(lib.wdr_context_create(_s(model_path), model_name.encode(), 0 if gpu_device is None else 1,
+                                       gpu_device or 0, _ob(use_gpu), _ob(enable_dtw), _ob(enable_flash_attn),
+                                       0 if num_samples is None else 1, num_samples or 0,
+                                       C.byref(syn) if syn else None, C.byref(h)))
+        self.h = h
+        self.synthetic = synthetic
+        hp = (C.c_int32 * 10)()
+        L.check(lib.wdr_context_hparams(h, hp))
+        keys = ["n_vocab", "n_audio_ctx", "n_audio_state", "n_audio_head", "n_audio_layer", "n_text_ctx",
+                "n_text_state", "n_text_head", "n_text_layer", "n_mels"]
+        self.hparams = dict(zip(keys, list(hp)))
+
+    def close(self):
+        if self.h:
+            self._lib.wdr_context_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- run_transcription_pipeline (src/transcribe.rs:323-535)
+    def run_pipeline(self, speech_segments, options: TranscribeOptions, callbacks: Optional[Callbacks] = None,
+                     synthetic: Optional[Synthetic] = None):
+        keep = _Keep()
+        arr = (L.SpeechSegment * max(1, len(speech_segments)))()
+        for i, s in enumerate(speech_segments):
+            smp = keep(np.ascontiguousarray(s.samples, np.int16))
+            arr[i] = L.SpeechSegment(s.start, s.end, smp.ctypes.data_as(C.POINTER(C.c_int16)), smp.size)
+        out = C.POINTER(L.SegmentList)()
+        syn = _syn(synthetic or self.synthetic)
+        L.check(self._lib.wdr_run_pipeline(self.h, arr, len(speech_segments), _opts(options, keep),
+                                           C.byref(syn) if syn else None, _callbacks(callbacks, keep),
+                                           C.byref(out)))
+        return _segments(out)
+
+    def stage_times(self) -> dict:
+        t = L.StageTimes()
+        L.check(self._lib.wdr_context_stage_times(self.h, C.byref(t)))
+        return {f: getattr(t, f) for f, _ in L.StageTimes._fields_}
+
+    # -- test seams
+    def state_full(self, samples_f32: np.ndarray, options: TranscribeOptions, initial_prompt: Optional[str] = None,
+                   synthetic: Optional[Synthetic] = None):
+        keep = _Keep()
+        x = np.ascontiguousarray(samples_f32, np.float32)
+        segs = C.POINTER(L.ResultSeg)()
+        n = C.c_size_t()
+        lang = C.c_int32()
+        syn = _syn(synthetic or self.synthetic)
+        L.check(self._lib.wdr_state_full(self.h, x.ctypes.data_as(C.POINTER(C.c_float)), x.size, _opts(options, keep),
+                                         C.byref(syn) if syn else None, _s(initial_prompt), C.byref(segs), C.byref(n),
+                                         C.byref(lang)))
+        out = []
+        for i in range(n.value):
+            s = segs[i]
+            toks = [dict(id=t.id, tid=t.tid, p=t.p, plog=t.plog, pt=t.pt, ptsum=t.ptsum, t0=t.t0, t1=t.t1,
+                         t_dtw=t.t_dtw) for t in (s.tokens[k] for k in range(s.n_tokens))]
+            out.append(dict(t0=s.t0, t1=s.t1, text=s.text.decode(), tokens=toks))
+        self._lib.wdr_result_free(segs, n.value)
+        return out, lang.value
+
+    def log_mel_window(self, x: np.ndarray, seek: int = 0) -> np.ndarray:
+        x = np.ascontiguousarray(x, np.float32)
+        out = np.zeros((self.hparams["n_mels"], 3000), np.float32)
+        L.check(self._lib.wdr_dbg_log_mel(self.h, x.ctypes.data_as(C.POINTER(C.c_float)), x.size, seek,
+                                          out.ctypes.data_as(C.POINTER(C.c_float))))
+        return out
+
+    def encode(self, mel_window: np.ndarray) -> np.ndarray:
+        m = np.ascontiguousarray(mel_window, np.float32)
+        out = np.zeros((1500, self.hparams["n_audio_state"]), np.float32)
+        L.check(self._lib.wdr_dbg_encode(self.h, m.ctypes.data_as(C.POINTER(C.c_float)),
+                                         out.ctypes.data_as(C.POINTER(C.c_float))))
+        return out
+
+    def decode(self, tokens) -> np.ndarray:
+        t = np.ascontiguousarray(tokens, np.int32)
+        out = np.zeros(self.hparams["n_vocab"], np.float32)
+        L.check(self._lib.wdr_dbg_decode(self.h, t.ctypes.data_as(C.POINTER(C.c_int32)), t.size,
+                                         out.ctypes.data_as(C.POINTER(C.c_float))))
+        return out
+
+    def capture(self, tokens, n_aheads: int) -> np.ndarray:
+        t = np.ascontiguousarray(tokens, np.int32)
+        out = np.zeros((n_aheads, t.size, 1500), np.float32)
+        L.check(self._lib.wdr_dbg_capture(self.h, t.ctypes.data_as(C.POINTER(C.c_int32)), t.size,
+                                          out.ctypes.data_as(C.POINTER(C.c_float))))
+        return out
+
+
+class Engine:
+    """Engine (src/engine.rs:52-217)."""
+
+    def __init__(self, cfg: Optional[EngineConfig] = None, synthetic: Optional[Synthetic] = None):
+        cfg = cfg or EngineConfig()
+        lib = L.load()
+        self._lib = lib
+        self._keep = _Keep()
+        c = L.EngineConfig(self._keep(_s(cfg.cache_dir)), _ob(cfg.enable_dtw), _ob(cfg.enable_flash_attn),
+                           _ob(cfg.use_gpu), 0 if cfg.gpu_device is None else 1, cfg.gpu_device or 0,
+                           self._keep(_s(cfg.vad_model_path)), self._keep(_s(cfg.diarize_segment_model_path)),
+                           self._keep(_s(cfg.diarize_embedding_model_path)))
+        h = C.c_void_p()
+        L.check(lib.wdr_engine_new(C.byref(c), C.byref(h)))
+        self.h = h
+        if synthetic is not None:
+            s = _syn(synthetic)
+            L.check(lib.wdr_engine_set_synthetic(h, C.byref(s)))
+
+    def transcribe_audio(self, audio_path: str, options: TranscribeOptions,
+                         formatting_overrides=None, cb: Optional[Callbacks] = None) -> List[Segment]:
+        keep = _Keep()
+        out = C.POINTER(L.SegmentList)()
+        L.check(self._lib.wdr_transcribe_audio(self.h, audio_path.encode(), _opts(options, keep), None,
+                                               _callbacks(cb, keep), C.byref(out)))
+        segs, _ = _segments(out)
+        return segs
+
+    def close(self):
+        if self.h:
+            self._lib.wdr_engine_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
