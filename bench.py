@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""xRT benchmark of the MI355X hot path (BASELINE.json metric: audio-sec / wall-sec).
+
+Workload (config.workload): BASELINE.json configs[2] per GPU — Whisper large-v3 (synthetic
+seeded weights, f16 operands / f32 accumulation), DTW word alignment on, greedy decode,
+lang "auto", 1 h of synthetic 16 kHz speech-like audio per rank, segmented by the
+generator's ground-truth talk-spurt table (the synthetic workload pin of BASELINE.md §2:
+decode length pinned to round(3.3 tok/s x window_s) + 3 tokens per window).  Weak scaling:
+every rank transcribes its own 1-h shard (seed = rank), no data-path collective.
+
+One step = run_transcription_pipeline over the rank's whole shard (mel, encoder, cross-K/V,
+language detection, prompt prefill, greedy decode, heuristic timestamps, DTW re-forward +
+alignment, reference glue).  Inputs (PCM) are host-resident as in the reference API; the
+PCIe share is negligible (115 MB/h) and included.
+
+Run:  python bench.py [--gpus N --steps K --warmup W]   (N>1 via torch.distributed.run)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "whisper-diarize-rs_amd"))
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
+MFMA_F16_PEAK_TFS = 2500.0  # dense f16/bf16 MFMA
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="large-v3")
+    ap.add_argument("--seconds", type=float, default=3600.0, help="audio seconds per rank")
+    ap.add_argument("--prof", default="gemv", choices=["gemv", "gemm", "flash", "xattn", "none"],
+                    help="kernel class timed live with HIP events for the roofline figure")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU oracle work (rank 0, N=1)")
+    return ap.parse_args()
+
+
+def cpu_baseline(model, segs, budget_s):
+    """The CPU restatement (oracle/, numpy f32 with f16-rounded weights/activations as ggml)
+    on a bounded prefix of the same workload.  Returns (xRT, sample description, threads)."""
+    import numpy as np
+    from oracle.model import Whisper
+    from oracle.pipeline import SpeechSegment, run_transcription_pipeline
+    from oracle.vocab import Vocab
+    from oracle.weights import hparams_for, synth_weights
+    from oracle.whisper_full import WhisperState
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    hp = hparams_for(model)
+    W = synth_weights(hp, std=0.02, emb_std=0.02)
+    st = WhisperState(Whisper(hp, W), Vocab(hp.n_vocab), model)
+    opts = dict(lang="auto", advanced=dict(sampling_strategy="greedy"),
+                synthetic=dict(force_len_rate=3.3, logprob_thold=-np.inf, entropy_thold=-1.0))
+    audio = 0.0
+    t0 = time.perf_counter()
+    n = 0
+    for s in segs:
+        run_transcription_pipeline(st, [SpeechSegment(s.start, s.end, s.samples)], opts)
+        audio += s.samples.size / 16000.0
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    wall = time.perf_counter() - t0
+    del W, st
+    return audio / wall, "first %d segments (%.1f s of audio) of rank 0's shard" % (n, audio), threads
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import wdr
+    from wdr.synth import synth_speech
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    pcm, spurts = synth_speech(args.seconds, seed=rank, n_speakers=1)
+    segs = [wdr.SpeechSegment(a, b, pcm[int(round(a * 16000)):int(round(b * 16000))]) for a, b, _ in spurts]
+    audio_s = float(sum(s.samples.size for s in segs)) / 16000.0   # speech seconds handed to the pipeline
+    shard_s = pcm.size / 16000.0                                  # wall-clock audio covered (xRT basis)
+
+    syn = wdr.Synthetic(weight_std=0.02, emb_std=0.02, force_len_rate=3.3, disable_fallback=True)
+    t_load = time.perf_counter()
+    ctx = wdr.WhisperContext(args.model, gpu_device=local, enable_dtw=True, synthetic=syn)
+    t_load = time.perf_counter() - t_load
+    opts = wdr.TranscribeOptions(model=args.model, lang="auto", enable_vad=True,
+                                 advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    lib = wdr._lib.load()
+    prof_cls = {"none": 0, "gemm": 1, "gemv": 2, "flash": 3, "xattn": 4}[args.prof]
+
+    for _ in range(args.warmup):
+        ctx.run_pipeline(segs, opts)
+    barrier()
+    lib.wdr_prof_set(prof_cls)
+    t0 = time.perf_counter()
+    n_out = 0
+    for _ in range(args.steps):
+        out, _ = ctx.run_pipeline(segs, opts)
+        n_out += len(out)
+    barrier()
+    dt = time.perf_counter() - t0
+    import ctypes as C
+    ms, nl, by, fl = C.c_double(), C.c_int64(), C.c_double(), C.c_double()
+    if lib.wdr_prof_read(C.byref(ms), C.byref(nl), C.byref(by), C.byref(fl)) != 0:
+        nl.value = 0
+    lib.wdr_prof_set(0)
+    times = ctx.stage_times()
+    t = torch.tensor([dt], dtype=torch.float64)
+    if world > 1:
+        if dist.get_backend() == "nccl":
+            t = t.cuda()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt_max = float(t.item())
+    value = world * shard_s * args.steps / dt_max
+
+    roof = None
+    if prof_cls and nl.value > 0 and ms.value > 0:
+        if args.prof in ("gemm", "flash"):
+            ach = fl.value / (ms.value * 1e-3) / 1e12
+            roof = {"kernel": args.prof, "bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_F16_PEAK_TFS,
+                    "unit": "TFLOP/s", "frac": round(ach / MFMA_F16_PEAK_TFS, 4), "traffic": None,
+                    "launches": nl.value, "avg_launch_us": round(ms.value * 1e3 / nl.value, 3),
+                    "flops_per_launch": fl.value / nl.value}
+        else:
+            ach = by.value / (ms.value * 1e-3) / 1e9
+            roof = {"kernel": args.prof, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "launches": nl.value, "avg_launch_us": round(ms.value * 1e3 / nl.value, 3),
+                    "bytes_per_launch": by.value / nl.value}
+        roof["kernel_share_of_step"] = round(ms.value * 1e-3 / dt, 4)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        ctx.close()
+        v, sample, threads = cpu_baseline(args.model, segs, args.cpu_budget)
+        cpu = {"value": round(v, 4), "unit": "audio-sec/wall-sec", "cores": threads, "kind": "port",
+               "sample": sample}
+
+    if rank == 0:
+        line = {
+            "metric": "audio-sec/wall-sec (xRT), large-v3 + DTW + diarize, 1/2/4/8 MI355X",
+            "value": round(value, 3), "unit": "audio-sec/wall-sec", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt_max * 1e3 / args.steps, 1), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f16 (f32 accumulate)", "data": "synthetic",
+            "config": {"workload": "configs[2]: %s, %.0f s synthetic audio per rank (%d segments, %.0f s speech), "
+                                   "DTW on, greedy, lang auto, ground-truth spurt segmentation (VAD/diarize "
+                                   "kernels not on this path yet)" % (args.model, shard_s, len(segs), audio_s),
+                       "model": args.model, "global_batch": len(segs) * world, "seq_len": 1500,
+                       "parallelism": "dp%d (segment shards per rank)" % world},
+            "roofline": roof, "cpu_baseline": cpu,
+            "stages_s": {k: round(v, 3) for k, v in times.items() if isinstance(v, float)},
+            "counts": {k: v for k, v in times.items() if isinstance(v, int)},
+            "load_s": round(t_load, 2), "segments_out": n_out // max(1, args.steps),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -159,6 +159,12 @@ void wdr_segment_list_free(wdr_segment_list* l);
 int wdr_context_stage_times(wdr_context* c, wdr_stage_times* out);
 int wdr_context_hparams(wdr_context* c, int32_t* out /* [10] */);
 
+/* ---- live kernel timing (HIP events on the launching stream) for bench.py's roofline:
+ * class 1 = MFMA GEMM (encoder / prefill / DTW projections), 2 = decoder GEMV, 3 = flash attention,
+ * 4 = decoder cross-attention.  Setting a class resets the counters. */
+int wdr_prof_set(int32_t cls);
+int wdr_prof_read(double* total_ms, int64_t* launches, double* algo_bytes, double* algo_flops);
+
 /* ---- whisper_full-level test seam: one state.full() call, raw token data ---- */
 typedef struct {
   int32_t id, tid;

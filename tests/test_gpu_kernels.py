@@ -36,7 +36,7 @@ def _gelu(x):
     return 0.5 * x * (1 + np.tanh(0.7978845608028654 * (x + 0.044715 * x ** 3)))
 
 
-@pytest.mark.parametrize("M", [1, 3, 8, 9, 300, 1500])
+@pytest.mark.parametrize("M", [1, 3, 8, 9, 17, 33, 64, 65, 300, 1500])
 def test_projection_matches_fp32_reference(lib, M):
     rng = np.random.default_rng(M)
     K, N = 256, 384

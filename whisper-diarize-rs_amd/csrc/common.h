@@ -36,11 +36,12 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // Epilogue selectors for the projection kernels (GEMM / GEMV).
 enum Epi : int {
-  EPI_F16 = 0,         // out16 = acc + bias
-  EPI_F16_GELU = 1,    // out16 = gelu_tanh(acc + bias)
-  EPI_F32_RESID = 2,   // out32 += acc + bias          (pre-LN residual stream update)
-  EPI_F32 = 3,         // out32 = acc + bias
-  EPI_F32_GELU_POS = 4 // out32 = gelu_tanh(acc + bias) + pos[row % pos_rows]  (conv2 + positional)
+  EPI_F16 = 0,          // out16 = acc + bias
+  EPI_F16_GELU = 1,     // out16 = gelu_tanh(acc + bias)
+  EPI_F32_RESID = 2,    // out32 += acc + bias          (pre-LN residual stream update)
+  EPI_F32 = 3,          // out32 = acc + bias
+  EPI_F32_GELU_POS = 4, // out32 = gelu_tanh(acc + bias) + pos[row % pos_rows]  (conv2 + positional)
+  EPI_QKV_CACHE = 5     // cols [0,d) -> out16 (Q); [d,2d) / [2d,3d) -> K / V self-attention cache rows
 };
 
 __host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
@@ -73,6 +74,12 @@ struct ProjArgs {
   const float* pos; int pos_rows;   // EPI_F32_GELU_POS only
   int M, N, K;
   int epi;
+  // fused LayerNorm prologue (decoder GEMV): A is ignored, rows come from the f32 residual
+  // stream ln_x [M][ldln] normalised with (ln_g, ln_b) -- ggml_norm eps 1e-5.
+  const float* ln_x = nullptr; int ldln = 0; const float* ln_g = nullptr; const float* ln_b = nullptr;
+  // EPI_QKV_CACHE
+  f16* kc = nullptr; f16* vc = nullptr; long long seq_stride = 0; const int* row_seq = nullptr;
+  const int* row_pos = nullptr; int d = 0;
 };
 void launch_proj(const ProjArgs& a, hipStream_t s);   // picks GEMV (M<=8) or MFMA GEMM
 

@@ -780,6 +780,14 @@ int wdr_dbg_attn(const uint16_t* q, const uint16_t* k, const uint16_t* v, int32_
     WDR_HIP(hipMemcpy(dv.p, v, dv.bytes, hipMemcpyHostToDevice));
     FlashArgs fa{dq.as<f16>(), d, 0, dk.as<f16>(), d, 0, dv.as<f16>(), d, 0, dout.as<f16>(), d, 0, nullptr, Tq, Tk, H,
                  causal, 0.125f};
+    DevMem po, pml;
+    if (!causal && Tq <= 256 && Tk >= 512) {   // exercise the split-K path the decoder prefill uses
+      fa.nsplit = 12;
+      po = DevMem((size_t)12 * Tq * H * 64 * 4);
+      pml = DevMem((size_t)12 * H * Tq * 8);
+      fa.part_o = po.as<float>();
+      fa.part_ml = pml.as<float2>();
+    }
     launch_flash_attn(fa, 1, nullptr);
     std::vector<f16> h((size_t)Tq * d);
     WDR_HIP(hipMemcpy(h.data(), dout.p, h.size() * 2, hipMemcpyDeviceToHost));

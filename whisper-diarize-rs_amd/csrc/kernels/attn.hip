@@ -16,6 +16,7 @@
 //  * k_aheads_capture — softmax(QK^T) of the alignment heads over all 1500 keys.
 #include "../common.h"
 #include "kernels.h"
+#include "../prof.h"
 
 namespace wdr {
 
@@ -30,6 +31,7 @@ __global__ __launch_bounds__(256) void k_flash_attn(FlashArgs a) {
   const f16* Q = a.q + b * a.q_bs + h * 64;
   const f16* K = a.k + b * a.k_bs + h * 64;
   const f16* V = a.v + b * a.v_bs + h * 64;
+  if (a.nsplit > 1) Q = a.q + h * 64;
   const int fr = lane & 31, hh = lane >> 5;
   const int qrow = qb * 128 + wid * 32 + fr;
   const int qrow_c = qrow < a.Tq ? qrow : a.Tq - 1;
@@ -42,19 +44,27 @@ __global__ __launch_bounds__(256) void k_flash_attn(FlashArgs a) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; }
   float m = -INFINITY, l = 0.f;
-  int kmax = a.Tk;
+  int kmax = a.Tk, kbeg = 0;
+  if (a.nsplit > 1) {   // blockIdx.z = key split (n_batch == 1)
+    const int ks = ((a.Tk + a.nsplit - 1) / a.nsplit + FA_KB - 1) / FA_KB * FA_KB;
+    kbeg = b * ks;
+    kmax = min(a.Tk, kbeg + ks);
+    Q = a.q + h * 64;
+    K = a.k + h * 64;
+    V = a.v + h * 64;
+  }
   if (a.causal) {
     const int last_q = qb * 128 + 127;
     kmax = kmax < last_q + 1 ? kmax : last_q + 1;
   }
-  for (int k0 = 0; k0 < kmax; k0 += FA_KB) {
+  for (int k0 = kbeg; k0 < kmax; k0 += FA_KB) {
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int c = tid + 256 * i;
       const int r = c >> 3, col = (c & 7) * 8;
       int key = k0 + r;
-      key = key < a.Tk ? key : a.Tk - 1;
+      key = key < kmax ? key : kmax - 1;
       const f16x8 kv = *(const f16x8*)(K + (long long)key * a.ldk + col);
       *(f16x8*)(Ks + r * FA_KS + col) = kv;
       const f16x8 vv = *(const f16x8*)(V + (long long)key * a.ldv + col);
@@ -79,7 +89,7 @@ __global__ __launch_bounds__(256) void k_flash_attn(FlashArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        const bool ok = key < a.Tk && (!a.causal || key <= qrow);
+        const bool ok = key < kmax && (!a.causal || key <= qrow);
         const float sv = ok ? st[t][r] * a.scale : -INFINITY;
         st[t][r] = sv;
         mx = fmaxf(mx, sv);
@@ -124,6 +134,18 @@ __global__ __launch_bounds__(256) void k_flash_attn(FlashArgs a) {
         o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(va1, pb, o1, 0, 0, 0);
       }
   }
+  if (a.nsplit > 1) {
+    if (qrow < a.Tq) {
+      float* po = a.part_o + (((long long)b * a.Tq + qrow) * a.n_head + h) * 64;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        *(float4*)(po + 8 * g + 4 * hh) = make_float4(o0[4 * g], o0[4 * g + 1], o0[4 * g + 2], o0[4 * g + 3]);
+        *(float4*)(po + 32 + 8 * g + 4 * hh) = make_float4(o1[4 * g], o1[4 * g + 1], o1[4 * g + 2], o1[4 * g + 3]);
+      }
+      if (hh == 0) a.part_ml[((long long)b * a.n_head + h) * a.Tq + qrow] = make_float2(m, l);
+    }
+    return;
+  }
   if (qrow < a.Tq) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
     f16* O = a.o + b * a.o_bs + (long long)qrow * a.ldo + h * 64;
@@ -142,11 +164,44 @@ __global__ __launch_bounds__(256) void k_flash_attn(FlashArgs a) {
   }
 }
 
+// merge the key splits: O = sum_c e^{m_c - M} O_c / L, (M, L) kept for the DTW capture
+__global__ __launch_bounds__(64) void k_flash_combine(FlashArgs a) {
+  const int q = blockIdx.x, h = blockIdx.y, d = threadIdx.x;
+  float2 ml = make_float2(-INFINITY, 0.f);
+  if (d < a.nsplit) ml = a.part_ml[((long long)d * a.n_head + h) * a.Tq + q];
+  const float M = wave_max(ml.x);
+  const float w = (d < a.nsplit && ml.x != -INFINITY) ? __expf(ml.x - M) : 0.f;
+  const float L = wave_sum(ml.y * w);
+  float acc = 0.f;
+  for (int c = 0; c < a.nsplit; ++c) acc += a.part_o[(((long long)c * a.Tq + q) * a.n_head + h) * 64 + d] * __shfl(w, c, 64);
+  a.o[(long long)q * a.ldo + h * 64 + d] = (f16)(acc / L);
+  if (a.ml && d == 0) a.ml[(long long)h * a.Tq + q] = make_float2(M, L);
+}
+
 void launch_flash_attn(const FlashArgs& a, int n_batch, hipStream_t s) {
   WDR_CHECK(a.Tq > 0 && a.Tk > 0, "attention: empty");
+  if (a.nsplit > 1) {
+    WDR_CHECK(n_batch == 1 && !a.causal && a.nsplit <= 64 && a.part_o && a.part_ml, "flash split: bad args");
+    const bool prof = prof_on(PROF_FLASH);
+    hipEvent_t e0 = nullptr;
+    if (prof) prof_begin(s, &e0);
+    hipLaunchKernelGGL(k_flash_attn, dim3(cdiv(a.Tq, 128), a.n_head, a.nsplit), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_flash_combine, dim3(a.Tq, a.n_head), dim3(64), 0, s, a);
+    WDR_HIP(hipGetLastError());
+    if (prof) prof_end(s, e0, (double)a.n_head * 64 * 2 * (2.0 * a.Tq + 2.0 * a.Tk), (double)a.n_head * a.Tq * a.Tk * 64 * 4);
+    return;
+  }
   dim3 grid(cdiv(a.Tq, 128), a.n_head, n_batch);
+  const bool prof = prof_on(PROF_FLASH);
+  hipEvent_t e0 = nullptr;
+  if (prof) prof_begin(s, &e0);
   hipLaunchKernelGGL(k_flash_attn, grid, dim3(256), 0, s, a);
   WDR_HIP(hipGetLastError());
+  if (prof) {
+    const double pairs = a.causal ? 0.5 * (double)a.Tq * a.Tk : (double)a.Tq * a.Tk;
+    const double bytes = (double)n_batch * a.n_head * 64 * 2 * (2.0 * a.Tq + 2.0 * a.Tk);
+    prof_end(s, e0, bytes, (double)n_batch * a.n_head * pairs * 64 * 4);
+  }
 }
 
 // ---------------------------------------------------------------- decoder self-attention
@@ -200,84 +255,83 @@ void launch_dec_self_attn(const DecSelfArgs& a, int R, int n_head, hipStream_t s
 
 // ---------------------------------------------------------------- decoder cross-attention (split)
 
-constexpr int XA_KC = 128, XA_RMAX = 8;
+constexpr int XA_KC = 64, XA_RMAX = 8;
 
+// one workgroup per (64-key chunk, head): the chunk's K and V (8 KB each) are fetched with all
+// 16-B loads issued up front, staged in LDS and shared by every decoder row (beam) of the step.
 __global__ __launch_bounds__(256) void k_xattn_partial(XAttnArgs a) {
+  __shared__ __attribute__((aligned(16))) f16 Ks[XA_KC * 72];
+  __shared__ __attribute__((aligned(16))) f16 Vs[XA_KC * 64];
   __shared__ float qs[XA_RMAX][64];
-  __shared__ float sc[XA_RMAX][XA_KC];
-  __shared__ float red[4][XA_RMAX][64];
+  __shared__ float ps[XA_RMAX][XA_KC];
   __shared__ float2 mls[XA_RMAX];
   const int c = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
   const int R = a.R;
-  for (int i = tid; i < R * 64; i += 256) qs[i / 64][i % 64] = (float)a.q[(long long)(i / 64) * a.ldq + h * 64 + (i % 64)];
-  __syncthreads();
   const int key0 = c * XA_KC;
-  if (tid < XA_KC) {
-    const int key = key0 + tid;
-    if (key < a.Tk) {
-      const f16* kr = a.k + (long long)key * a.ldkv + h * 64;
-      f16x8 kv[8];
+  f16x8 kv[2], vv[2];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) kv[j] = *(const f16x8*)(kr + 8 * j);
-      for (int r = 0; r < R; ++r) {
-        float s = 0.f;
+  for (int i = 0; i < 2; ++i) {
+    const int ch = tid + 256 * i;
+    int key = key0 + (ch >> 3);
+    key = key < a.Tk ? key : a.Tk - 1;
+    const long long off = (long long)key * a.ldkv + h * 64 + (ch & 7) * 8;
+    kv[i] = *(const f16x8*)(a.k + off);
+    vv[i] = *(const f16x8*)(a.v + off);
+  }
+  for (int i = tid; i < R * 64; i += 256) qs[i >> 6][i & 63] = (float)a.q[(long long)(i >> 6) * a.ldq + h * 64 + (i & 63)];
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+  for (int i = 0; i < 2; ++i) {
+    const int ch = tid + 256 * i;
+    *(f16x8*)(Ks + (ch >> 3) * 72 + (ch & 7) * 8) = kv[i];
+    *(f16x8*)(Vs + (ch >> 3) * 64 + (ch & 7) * 8) = vv[i];
+  }
+  __syncthreads();
+  const int key = tid & 63;
+  const bool kok = key0 + key < a.Tk;
+  for (int r = tid >> 6; r < R; r += 4) {
+    float sc = 0.f;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) s += qs[r][8 * j + e] * (float)kv[j][e];
-        sc[r][tid] = s * a.scale;
-      }
-    } else {
-      for (int r = 0; r < R; ++r) sc[r][tid] = -INFINITY;
+    for (int j = 0; j < 64; j += 8) {
+      const f16x8 k8 = *(const f16x8*)(Ks + key * 72 + j);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sc += qs[r][j + e] * (float)k8[e];
     }
+    ps[r][key] = kok ? sc * a.scale : -INFINITY;
   }
   __syncthreads();
   const int wid = tid >> 6, lane = tid & 63;
   for (int r = wid; r < R; r += 4) {
-    const float s0 = sc[r][lane], s1 = sc[r][lane + 64];
-    const float mx = wave_max(fmaxf(s0, s1));
-    const float p0 = s0 == -INFINITY ? 0.f : __expf(s0 - mx);
-    const float p1 = s1 == -INFINITY ? 0.f : __expf(s1 - mx);
-    sc[r][lane] = p0;
-    sc[r][lane + 64] = p1;
-    const float l = wave_sum(p0 + p1);
+    const float sv = ps[r][lane];
+    const float mx = wave_max(sv);
+    const float p = sv == -INFINITY ? 0.f : __expf(sv - mx);
+    ps[r][lane] = p;
+    const float l = wave_sum(p);
     if (lane == 0) mls[r] = make_float2(mx, l);
   }
   __syncthreads();
-  const int dh = tid & 63, qtr = tid >> 6;
-  float acc[XA_RMAX];
-#pragma unroll
-  for (int r = 0; r < XA_RMAX; ++r) acc[r] = 0.f;
-  for (int kk = qtr * 32; kk < qtr * 32 + 32; ++kk) {
-    const int key = key0 + kk;
-    if (key >= a.Tk) break;
-    const float vv = (float)a.v[(long long)key * a.ldkv + h * 64 + dh];
-#pragma unroll
-    for (int r = 0; r < XA_RMAX; ++r)
-      if (r < R) acc[r] += (float)(f16)sc[r][kk] * vv;
-  }
-#pragma unroll
-  for (int r = 0; r < XA_RMAX; ++r)
-    if (r < R) red[qtr][r][dh] = acc[r];
-  __syncthreads();
-  for (int i = tid; i < R * 64; i += 256) {
-    const int r = i / 64, d = i % 64;
-    const float s = red[0][r][d] + red[1][r][d] + red[2][r][d] + red[3][r][d];
-    a.part_o[(((long long)c * R + r) * a.n_head + h) * 64 + d] = s;
+  const int dh = tid & 63;
+  for (int r = tid >> 6; r < R; r += 4) {
+    float acc = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < XA_KC; ++k) acc += (float)(f16)ps[r][k] * (float)Vs[k * 64 + dh];
+    a.part_o[(((long long)c * R + r) * a.n_head + h) * 64 + dh] = acc;
   }
   if (tid < R) a.part_ml[((long long)c * R + tid) * a.n_head + h] = mls[tid];
 }
 
 __global__ __launch_bounds__(64) void k_xattn_combine(XAttnArgs a, int nsplit) {
   const int r = blockIdx.x, h = blockIdx.y, d = threadIdx.x;
-  float M = -INFINITY;
-  for (int c = 0; c < nsplit; ++c) M = fmaxf(M, a.part_ml[((long long)c * a.R + r) * a.n_head + h].x);
-  float L = 0.f, acc = 0.f;
+  // lane c < nsplit fetches chunk c's (max, sum); one wave reduction gives the global max
+  float2 ml = make_float2(-INFINITY, 0.f);
+  if (d < nsplit) ml = a.part_ml[((long long)d * a.R + r) * a.n_head + h];
+  const float M = wave_max(ml.x);
+  const float w = (d < nsplit && ml.x != -INFINITY) ? __expf(ml.x - M) : 0.f;
+  const float L = wave_sum(ml.y * w);
+  float acc = 0.f;
+#pragma unroll 8
   for (int c = 0; c < nsplit; ++c) {
-    const float2 ml = a.part_ml[((long long)c * a.R + r) * a.n_head + h];
-    const float w = ml.x == -INFINITY ? 0.f : __expf(ml.x - M);
-    L += ml.y * w;
-    acc += a.part_o[(((long long)c * a.R + r) * a.n_head + h) * 64 + d] * w;
+    const float wc = __shfl(w, c, 64);
+    acc += a.part_o[(((long long)c * a.R + r) * a.n_head + h) * 64 + d] * wc;
   }
   a.o[(long long)r * a.ldo + h * 64 + d] = (f16)(acc / L);
 }
@@ -285,9 +339,13 @@ __global__ __launch_bounds__(64) void k_xattn_combine(XAttnArgs a, int nsplit) {
 void launch_xattn(const XAttnArgs& a, hipStream_t s) {
   WDR_CHECK(a.R >= 1 && a.R <= XA_RMAX, "cross-attention decode: R out of range");
   const int nsplit = cdiv(a.Tk, XA_KC);
+  const bool prof = prof_on(PROF_XATTN);
+  hipEvent_t e0 = nullptr;
+  if (prof) prof_begin(s, &e0);
   hipLaunchKernelGGL(k_xattn_partial, dim3(nsplit, a.n_head), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_xattn_combine, dim3(a.R, a.n_head), dim3(64), 0, s, a, nsplit);
   WDR_HIP(hipGetLastError());
+  if (prof) prof_end(s, e0, (double)a.Tk * a.n_head * 64 * 2 * 2, (double)a.R * a.Tk * a.n_head * 64 * 4);
 }
 
 // ---------------------------------------------------------------- alignment-head capture

@@ -253,27 +253,40 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* x, int ldx, cons
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
   const float* xr = x + (long long)row * ldx;
-  double s = 0.0;
-  for (int c = lane; c < d; c += 64) s += (double)xr[c];
-  s = wave_sum_d(s);
-  const float mean = (float)(s / d);
-  double s2 = 0.0;
-  for (int c = lane; c < d; c += 64) {
-    const float v = xr[c] - mean;
-    s2 += (double)(v * v);
+  // d <= 1280: each lane keeps its <= 20 values in registers (float4 loads)
+  float v[20];
+  int nv = 0;
+  float s = 0.f;
+  for (int c = lane * 4; c < d; c += 256) {
+    const float4 q = *(const float4*)(xr + c);
+    v[nv] = q.x; v[nv + 1] = q.y; v[nv + 2] = q.z; v[nv + 3] = q.w;
+    s += (q.x + q.y) + (q.z + q.w);
+    nv += 4;
   }
-  s2 = wave_sum_d(s2);
-  const float var = (float)(s2 / d);
-  const float scale = 1.0f / sqrtf(var + 1e-5f);
+  s = wave_sum(s);
+  const float mean = s / d;
+  float s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 20; ++i)
+    if (i < nv) {
+      const float t = v[i] - mean;
+      s2 += t * t;
+    }
+  s2 = wave_sum(s2);
+  const float scale = 1.0f / sqrtf(s2 / d + 1e-5f);
   f16* yr = y + (long long)row * ldy;
-  for (int c = lane; c < d; c += 64) {
-    const float v = (xr[c] - mean) * scale;
-    yr[c] = (f16)(v * g[c] + b[c]);
+  int i = 0;
+  for (int c = lane * 4; c < d; c += 256, i += 4) {
+    f16x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (f16)((v[i + e] - mean) * scale * g[c + e] + b[c + e]);
+    *(f16x4*)(yr + c) = o;
   }
 }
 
 void launch_layernorm(const float* x, int ldx, const float* g, const float* b, f16* y, int ldy, int rows, int d,
                       hipStream_t s) {
+  WDR_CHECK(d % 4 == 0 && d <= 1280 && ldx % 4 == 0 && ldy % 4 == 0, "layernorm: unsupported width");
   hipLaunchKernelGGL(k_layernorm, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, g, b, y, ldy, rows, d);
   WDR_HIP(hipGetLastError());
 }
@@ -364,86 +377,133 @@ __device__ void block_argmax(float& v, int& idx, float* shv, int* shi) {
 __device__ __forceinline__ float rule_mask(float x, int i, const LogitsCtl& c, const VocabIds& v) {
   const bool initial = c.n_tokens == 0;
   if (c.temperature > 0.f) x = x / c.temperature;
-  if (v.suppress_blank && initial && (i == v.eot || i == v.space)) return -INFINITY;
+  bool masked = false;
+  if (v.suppress_blank && initial && (i == v.eot || i == v.space)) masked = true;
   if (i == v.not_ || i == v.sot || i == v.nosp || i == v.solm || i == v.translate || i == v.transcribe || i == v.prev)
-    return -INFINITY;
-  if (i >= v.lang0 && i < v.lang0 + v.n_lang) return -INFINITY;
+    masked = true;
+  if (i >= v.lang0 && i < v.lang0 + v.n_lang) masked = true;
   if (c.last_ts) {
     if (c.pen_ts) {
-      if (i >= v.beg) return -INFINITY;
+      if (i >= v.beg) masked = true;
     } else if (i < v.eot) {
-      return -INFINITY;
+      masked = true;
     }
   }
-  if (initial && v.max_initial_tid >= 0 && i > v.beg + v.max_initial_tid) return -INFINITY;
-  if (c.has_ts && i >= v.beg && i < v.beg + c.seek_delta / 2) return -INFINITY;
-  if (c.force_kind == 1 && i != c.force_tok) return -INFINITY;
-  if (c.force_kind == 2 && (i == v.eot || i >= v.beg)) return -INFINITY;
-  return x;
+  if (initial && v.max_initial_tid >= 0 && i > v.beg + v.max_initial_tid) masked = true;
+  if (c.has_ts && i >= v.beg && i < v.beg + c.seek_delta / 2) masked = true;
+  // synthetic workload pin (applied after whisper.cpp's own rules)
+  if (c.force_kind == 1) return i == c.force_tok ? (masked ? 0.f : x) : -INFINITY;
+  if (c.force_kind == 2 && (i == v.eot || i >= v.beg)) masked = true;
+  return masked ? -INFINITY : x;
 }
 
-__global__ __launch_bounds__(1024) void k_logits_process(const float* logits, int ld, const LogitsCtl* ctls, VocabIds v,
-                                                         float* work, TokOut* out) {
-  __shared__ float shf[16];
-  __shared__ double shd[16];
-  __shared__ int shi[16];
-  const int r = blockIdx.x, tid = threadIdx.x;
+// online (max, sum-of-exp) pair
+struct MS {
+  float m, s;
+};
+__device__ __forceinline__ MS ms_add(MS a, float x) {
+  if (x == -INFINITY) return a;
+  if (x > a.m) return MS{x, a.s * __expf(a.m - x) + 1.f};
+  return MS{a.m, a.s + __expf(x - a.m)};
+}
+__device__ __forceinline__ MS ms_merge(MS a, MS b) {
+  if (b.m == -INFINITY) return a;
+  if (a.m == -INFINITY) return b;
+  const float M = fmaxf(a.m, b.m);
+  return MS{M, a.s * __expf(a.m - M) + b.s * __expf(b.m - M)};
+}
+__device__ __forceinline__ MS ms_wave(MS v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    MS u{__shfl_xor(v.m, o, 64), __shfl_xor(v.s, o, 64)};
+    v = ms_merge(v, u);
+  }
+  return v;
+}
+
+constexpr int LG_NB = 32;   // vocabulary slices (workgroups) per row
+
+struct LgStats {   // per (row, slice)
+  float m0, s0, m1, s1, mts, sts, mtx, pad;
+};
+struct LgPick {
+  float bp; int bi; float tp; int ti; double tsum;
+};
+
+// pass 1: raw and filtered (max, sum-exp), timestamp-range (max, sum-exp), best text logit
+__global__ __launch_bounds__(256) void k_logits_stats(const float* logits, int ld, const LogitsCtl* ctls, VocabIds v,
+                                                      LgStats* st) {
+  __shared__ LgStats sh[4];
+  const int b = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
   const float* L = logits + (long long)r * ld;
-  float* X = work + (long long)r * ld;
   const LogitsCtl c = ctls[r];
-  const int V = v.n_vocab;
-  // (1) no-speech probability from the raw logits (before any filter)
-  float m0 = -INFINITY;
-  for (int i = tid; i < V; i += 1024) m0 = fmaxf(m0, L[i]);
-  m0 = block_reduce<float>(m0, shf, 0);
-  float s0 = 0.f;
-  for (int i = tid; i < V; i += 1024) s0 += __expf(L[i] - m0);
-  s0 = block_reduce<float>(s0, shf, 1);
-  const float lse0 = logf(s0) + m0;
-  // (2) filters
-  float m1 = -INFINITY;
-  for (int i = tid; i < V; i += 1024) {
-    float x = rule_mask(L[i], i, c, v);
-    X[i] = x;
-    m1 = fmaxf(m1, x);
+  const int V = v.n_vocab, chunk = (V + LG_NB - 1) / LG_NB;
+  const int i0 = b * chunk, i1 = min(V, i0 + chunk);
+  MS raw{-INFINITY, 0.f}, all{-INFINITY, 0.f}, ts{-INFINITY, 0.f};
+  float mtx = -INFINITY;
+  for (int i = i0 + tid; i < i1; i += 256) {
+    const float l = L[i];
+    raw = ms_add(raw, l);
+    const float x = rule_mask(l, i, c, v);
+    all = ms_add(all, x);
+    if (i >= v.beg) ts = ms_add(ts, x);
+    else mtx = fmaxf(mtx, x);
   }
-  m1 = block_reduce<float>(m1, shf, 0);
-  bool forced_empty = false;
-  if (c.force_kind == 1 && m1 == -INFINITY) {   // forced token was filtered: keep it alone
-    forced_empty = true;
-    m1 = 0.f;
-  }
-  if (forced_empty && tid == 0) X[c.force_tok] = 0.f;
+  raw = ms_wave(raw);
+  all = ms_wave(all);
+  ts = ms_wave(ts);
+  mtx = wave_max(mtx);
+  const int w = tid >> 6;
+  if ((tid & 63) == 0) sh[w] = LgStats{raw.m, raw.s, all.m, all.s, ts.m, ts.s, mtx, 0.f};
   __syncthreads();
-  float s1 = 0.f;
-  for (int i = tid; i < V; i += 1024)
-    if (X[i] > -INFINITY) s1 += __expf(X[i] - m1);
-  s1 = block_reduce<float>(s1, shf, 1);
-  const float lse = logf(s1) + m1;
-  // (3) timestamp mass vs best text token
-  float mts = -INFINITY, mtx = -INFINITY;
-  for (int i = tid; i < V; i += 1024) {
-    const float lp = X[i] > -INFINITY ? X[i] - lse : -INFINITY;
-    if (i >= v.beg) mts = fmaxf(mts, lp);
-    else mtx = fmaxf(mtx, lp);
+  if (tid == 0) {
+    MS a{sh[0].m0, sh[0].s0}, bb{sh[0].m1, sh[0].s1}, t{sh[0].mts, sh[0].sts};
+    float mx = sh[0].mtx;
+    for (int k = 1; k < 4; ++k) {
+      a = ms_merge(a, MS{sh[k].m0, sh[k].s0});
+      bb = ms_merge(bb, MS{sh[k].m1, sh[k].s1});
+      t = ms_merge(t, MS{sh[k].mts, sh[k].sts});
+      mx = fmaxf(mx, sh[k].mtx);
+    }
+    st[r * LG_NB + b] = LgStats{a.m, a.s, bb.m, bb.s, t.m, t.s, mx, 0.f};
   }
-  mts = block_reduce<float>(mts, shf, 0);
-  mtx = block_reduce<float>(mtx, shf, 0);
-  float sts = 0.f;
-  if (mts > -INFINITY)
-    for (int i = v.beg + tid; i < V; i += 1024)
-      if (X[i] > -INFINITY) sts += __expf((X[i] - lse) - mts);
-  sts = block_reduce<float>(sts, shf, 1);
-  const float ts_lp = sts > 0.f ? logf(sts) + mts : -INFINITY;
-  const bool mask_text = ts_lp > mtx;
-  // (4) probabilities, greedy pick, timestamp statistics
-  float bp = 0.f;
-  int bi = 0x7fffffff;
-  float tp = 0.f;
-  int ti = 0x7fffffff;
+}
+
+__device__ __forceinline__ void lg_global(const LgStats* st, int r, LgStats& g) {
+  MS a{-INFINITY, 0.f}, bb{-INFINITY, 0.f}, t{-INFINITY, 0.f};
+  float mx = -INFINITY;
+  for (int k = 0; k < LG_NB; ++k) {
+    const LgStats& p = st[r * LG_NB + k];
+    a = ms_merge(a, MS{p.m0, p.s0});
+    bb = ms_merge(bb, MS{p.m1, p.s1});
+    t = ms_merge(t, MS{p.mts, p.sts});
+    mx = fmaxf(mx, p.mtx);
+  }
+  g = LgStats{a.m, a.s, bb.m, bb.s, t.m, t.s, mx, 0.f};
+}
+
+// pass 2: probabilities exp(x - lse) (text masked when the timestamp mass wins), first-index
+// argmax over them, timestamp argmax and timestamp probability sum (double)
+__global__ __launch_bounds__(256) void k_logits_pick(const float* logits, int ld, const LogitsCtl* ctls, VocabIds v,
+                                                     const LgStats* st, LgPick* pk) {
+  __shared__ LgStats g;
+  __shared__ float shv[8];
+  __shared__ int shi[8];
+  __shared__ double shd[4];
+  const int b = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
+  if (tid == 0) lg_global(st, r, g);
+  __syncthreads();
+  const float* L = logits + (long long)r * ld;
+  const LogitsCtl c = ctls[r];
+  const float lse = logf(g.s1) + g.m1;
+  const float ts_lp = (g.mts == -INFINITY || !(g.sts > 0.f)) ? -INFINITY : logf(g.sts) + (g.mts - lse);
+  const bool mask_text = ts_lp > g.mtx - lse;
+  const int V = v.n_vocab, chunk = (V + LG_NB - 1) / LG_NB;
+  const int i0 = b * chunk, i1 = min(V, i0 + chunk);
+  float bp = 0.f, tp = 0.f;
+  int bi = 0x7fffffff, ti = 0x7fffffff;
   double tsum = 0.0;
-  for (int i = tid; i < V; i += 1024) {
-    float x = X[i];
+  for (int i = i0 + tid; i < i1; i += 256) {
+    float x = rule_mask(L[i], i, c, v);
     if (mask_text && i < v.beg) x = -INFINITY;
     const float p = x == -INFINITY ? 0.f : __expf(x - lse);
     if (p > 0.f) amax_merge(bp, bi, p, i);
@@ -451,33 +511,71 @@ __global__ __launch_bounds__(1024) void k_logits_process(const float* logits, in
       tsum += (double)p;
       if (p > 0.f) amax_merge(tp, ti, p, i);
     }
-    X[i] = p;     // probs (kept for t > 0 sampling on the host)
   }
-  block_argmax(bp, bi, shf, shi);
-  block_argmax(tp, ti, shf, shi);
-  tsum = block_reduce<double>(tsum, shd, 1);
+  for (int o = 32; o > 0; o >>= 1) {
+    const float v2 = __shfl_xor(bp, o, 64);
+    const int i2 = __shfl_xor(bi, o, 64);
+    amax_merge(bp, bi, v2, i2);
+    const float t2 = __shfl_xor(tp, o, 64);
+    const int j2 = __shfl_xor(ti, o, 64);
+    amax_merge(tp, ti, t2, j2);
+  }
+  tsum = wave_sum_d(tsum);
+  const int w = tid >> 6;
+  if ((tid & 63) == 0) {
+    shv[w] = bp; shi[w] = bi; shv[4 + w] = tp; shi[4 + w] = ti; shd[w] = tsum;
+  }
+  __syncthreads();
   if (tid == 0) {
-    TokOut o;
-    o.nosp_prob = __expf(L[v.nosp] - lse0);
-    o.ptsum = (float)tsum;
-    o.pt = (float)((double)(ti == 0x7fffffff ? 0.f : tp) / (tsum + 1e-10));
-    o.tid = ti == 0x7fffffff ? 0 : ti;
-    if (bi == 0x7fffffff) {
-      o.id = 0; o.p = 0.f; o.plog = 0.f;
-    } else {
-      o.id = bi; o.p = bp;
-      float x = rule_mask(L[bi], bi, c, v);
-      if (forced_empty && bi == c.force_tok) x = 0.f;
-      o.plog = x - lse;
+    for (int k = 1; k < 4; ++k) {
+      amax_merge(shv[0], shi[0], shv[k], shi[k]);
+      amax_merge(shv[4], shi[4], shv[4 + k], shi[4 + k]);
     }
-    if (o.id >= v.beg) { o.tid = o.id; o.pt = o.p; }
-    out[r] = o;
+    pk[r * LG_NB + b] = LgPick{shv[0], shi[0], shv[4], shi[4], shd[0] + shd[1] + shd[2] + shd[3]};
   }
+}
+
+__global__ void k_logits_final(const float* logits, int ld, const LogitsCtl* ctls, VocabIds v, const LgStats* st,
+                               const LgPick* pk, TokOut* out) {
+  const int r = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  LgStats g;
+  lg_global(st, r, g);
+  const float* L = logits + (long long)r * ld;
+  const LogitsCtl c = ctls[r];
+  float bp = 0.f, tp = 0.f;
+  int bi = 0x7fffffff, ti = 0x7fffffff;
+  double tsum = 0.0;
+  for (int k = 0; k < LG_NB; ++k) {
+    const LgPick& p = pk[r * LG_NB + k];
+    amax_merge(bp, bi, p.bp, p.bi);
+    amax_merge(tp, ti, p.tp, p.ti);
+    tsum += p.tsum;
+  }
+  const float lse = logf(g.s1) + g.m1;
+  TokOut o;
+  o.nosp_prob = __expf(L[v.nosp] - (logf(g.s0) + g.m0));
+  o.ptsum = (float)tsum;
+  o.pt = (float)((double)(ti == 0x7fffffff ? 0.f : tp) / (tsum + 1e-10));
+  o.tid = ti == 0x7fffffff ? 0 : ti;
+  if (bi == 0x7fffffff) {
+    o.id = 0; o.p = 0.f; o.plog = 0.f;
+  } else {
+    o.id = bi; o.p = bp;
+    o.plog = rule_mask(L[bi], bi, c, v) - lse;
+  }
+  if (o.id >= v.beg) { o.tid = o.id; o.pt = o.p; }
+  o.pad = 0;
+  out[r] = o;
 }
 
 void launch_logits_process(const float* logits, int ld, const LogitsCtl* ctls, const VocabIds& v, int R, float* work,
                            TokOut* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_logits_process, dim3(R), dim3(1024), 0, s, logits, ld, ctls, v, work, out);
+  LgStats* st = (LgStats*)work;
+  LgPick* pk = (LgPick*)(work + (size_t)R * LG_NB * 8);
+  hipLaunchKernelGGL(k_logits_stats, dim3(LG_NB, R), dim3(256), 0, s, logits, ld, ctls, v, st);
+  hipLaunchKernelGGL(k_logits_pick, dim3(LG_NB, R), dim3(256), 0, s, logits, ld, ctls, v, st, pk);
+  hipLaunchKernelGGL(k_logits_final, dim3(R), dim3(64), 0, s, logits, ld, ctls, v, st, pk, out);
   WDR_HIP(hipGetLastError());
 }
 

@@ -75,6 +75,11 @@ struct FlashArgs {
   int Tq, Tk, n_head;
   int causal;
   float scale;
+  // split-K over keys (few query rows against 1500 cross keys): partial O (unnormalised, f32)
+  // and (max, sum) per split, merged by a combine kernel.  nsplit <= 64, n_batch must be 1.
+  int nsplit = 1;
+  float* part_o = nullptr;     // [nsplit][Tq][n_head][64]
+  float2* part_ml = nullptr;   // [nsplit][n_head][Tq]
 };
 void launch_flash_attn(const FlashArgs& a, int n_batch, hipStream_t s);
 struct DecSelfArgs {

@@ -153,6 +153,8 @@ class State {
   // pieces of full()
   void decoder_prefill(const int* toks, int n, int seq, bool want_logits, bool capture);
   void decoder_step(const int* toks, const int* seqs, const int* pos, int R);
+  void decoder_step_body(int R);
+  void step_and_sample(const int* toks, const int* seqs, const int* pos, const LogitsCtl* ctl, int R, TokenData* out);
   void run_logits(int R, const LogitsCtl* ctl, TokenData* out, float* nosp);
   void heuristic_timestamps(int i_segment, const FullParams& p);
   void dtw_timestamps(int i_segment, int n_segments, int seek, int n_frames, const std::string& language);

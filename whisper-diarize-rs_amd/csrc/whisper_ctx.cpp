@@ -2,11 +2,13 @@
 // whisper_full_with_state decode loop as the reference drives it
 // (src/transcribe.rs:20-87 params, :389 state.full).  Mirrors oracle/whisper_full.py.
 #include "whisper.h"
+#include "prof.h"
 
 #include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <cstdlib>
 #include <map>
 
 namespace wdr {
@@ -302,7 +304,7 @@ Context::~Context() {
 // ------------------------------------------------------------------ state buffers
 static constexpr int RMAX = 448;   // max decoder rows in one forward (n_text_ctx)
 static constexpr int NSEQ = 8;     // max concurrent decoder sequences
-static constexpr int NSPLIT = 12;  // cross-attention key chunks (1500 / 128)
+static constexpr int NSPLIT = 24;  // cross-attention key chunks (1500 / 64)
 
 struct State::Impl {
   int d, L, H, V, n_mels, kp1;
@@ -316,6 +318,7 @@ struct State::Impl {
   // decoder
   DevMem xd, hd, qkvd, attd, qx, mlpd, logits, work, tokout, ctl, ml, cap, part_o, part_ml;
   DevMem rows_tok, rows_pos, rows_seq;
+  DevMem fpart_o, fpart_ml;   // split flash-attention partials (prefill cross-attention)
   DevMem kc, vc;
   long long seq_stride = 0;   // elements per (layer, seq)
   // dtw
@@ -326,6 +329,13 @@ struct State::Impl {
   LogitsCtl* h_ctl = nullptr;
   int* h_times = nullptr;
   VocabIds vids;
+  struct StepGraph {
+    hipGraphExec_t exec = nullptr;
+    int prof_cls = -1;
+    std::vector<ProfPair> pairs;
+    VocabIds vids{};
+  };
+  std::map<int, StepGraph> graphs;
 };
 
 State::State(Context& ctx) : ctx_(ctx), s_(ctx.stream), m_(new Impl) {
@@ -363,6 +373,8 @@ State::State(Context& ctx) : ctx_(ctx), s_(ctx.stream), m_(new Impl) {
   m.cap = DevMem((size_t)A * RMAX * 1500 * 4);
   m.part_o = DevMem((size_t)NSPLIT * NSEQ * m.H * 64 * 4);
   m.part_ml = DevMem((size_t)NSPLIT * NSEQ * m.H * sizeof(float2));
+  m.fpart_o = DevMem((size_t)12 * 256 * m.H * 64 * 4);
+  m.fpart_ml = DevMem((size_t)12 * m.H * 256 * sizeof(float2));
   m.rows_tok = DevMem(RMAX * 4);
   m.rows_pos = DevMem(RMAX * 4);
   m.rows_seq = DevMem(RMAX * 4);
@@ -383,6 +395,8 @@ State::State(Context& ctx) : ctx_(ctx), s_(ctx.stream), m_(new Impl) {
 
 State::~State() {
   if (m_) {
+    for (auto& g : m_->graphs)
+      if (g.second.exec) (void)hipGraphExecDestroy(g.second.exec);
     (void)hipHostFree(m_->h_rows);
     (void)hipHostFree(m_->h_tok);
     (void)hipHostFree(m_->h_ctl);
@@ -526,6 +540,11 @@ void State::decoder_prefill(const int* toks, int n, int seq, bool want_logits, b
     if (n > NSEQ || cap_layer) {
       FlashArgs xa{m.qx.as<f16>(), d, 0, xk, ldxkv, 0, xv, ldxkv, 0, m.attd.as<f16>(), d, 0,
                    cap_layer ? m.ml.as<float2>() : nullptr, n, 1500, hp.n_text_head, 0, scale};
+      if (n <= 256) {   // few queries: split the 1500 keys so every CU streams part of the cross K/V
+        xa.nsplit = 12;
+        xa.part_o = m.fpart_o.as<float>();
+        xa.part_ml = m.fpart_ml.as<float2>();
+      }
       launch_flash_attn(xa, 1, s_);
       if (cap_layer) {
         int slot0 = 0;
@@ -551,12 +570,59 @@ void State::decoder_prefill(const int* toks, int n, int seq, bool want_logits, b
   times.prefills++;
 }
 
-// One decode step for R rows: row r appends token toks[r] at position pos[r] of sequence seqs[r].
-void State::decoder_step(const int* toks, const int* seqs, const int* pos, int R) {
+// One decode step for R rows: row r appends token rows_tok[r] at position rows_pos[r] of
+// sequence rows_seq[r] (device arrays, filled by the caller).  LayerNorms are fused into the
+// projections' prologue and K/V go straight into the cache from the QKV epilogue, so a layer
+// is 8 launches: QKV, self-attn, O, cross-Q, cross-attn (2), cross-O, FC1, FC2.
+void State::decoder_step_body(int R) {
   Impl& m = *m_;
   const Model& md = ctx_.model;
   const HParams& hp = md.hp;
   const int d = m.d, L = m.L;
+  launch_embed(md.tok_emb, md.dec_pos, m.rows_tok.as<int>(), m.rows_pos.as<int>(), R, d, m.xd.as<float>(), s_);
+  const float scale = 1.0f / 8.0f;
+  const int ldxkv = L * 2 * d;
+  auto P = [&](const f16* A, int lda, const f16* W, const float* b, void* out, int ldo, int N, int K, int epi,
+               const float* lng = nullptr, const float* lnb = nullptr) {
+    ProjArgs a{A, lda, W, K, b, out, ldo, nullptr, 0, R, N, K, epi};
+    if (lng) {
+      a.ln_x = m.xd.as<float>();
+      a.ldln = d;
+      a.ln_g = lng;
+      a.ln_b = lnb;
+    }
+    return a;
+  };
+  for (int l = 0; l < L; ++l) {
+    const DecLayer& e = md.dec[l];
+    f16* kc = m.kc.as<f16>() + (size_t)l * NSEQ * m.seq_stride;
+    f16* vc = m.vc.as<f16>() + (size_t)l * NSEQ * m.seq_stride;
+    ProjArgs q = P(nullptr, d, e.w_qkv, e.b_qkv, m.qkvd.p, 3 * d, 3 * d, d, EPI_QKV_CACHE, e.ln1_g, e.ln1_b);
+    q.kc = kc;
+    q.vc = vc;
+    q.seq_stride = m.seq_stride;
+    q.row_seq = m.rows_seq.as<int>();
+    q.row_pos = m.rows_pos.as<int>();
+    q.d = d;
+    launch_proj(q, s_);
+    DecSelfArgs sa{m.qkvd.as<f16>(), 3 * d, kc, vc, m.seq_stride, d, m.rows_seq.as<int>(), m.rows_pos.as<int>(),
+                   m.attd.as<f16>(), d, scale};
+    launch_dec_self_attn(sa, R, hp.n_text_head, s_);
+    launch_proj(P(m.attd.as<f16>(), d, e.w_o, e.b_o, m.xd.p, d, d, d, EPI_F32_RESID), s_);
+    launch_proj(P(nullptr, d, e.w_xq, e.b_xq, m.qx.p, d, d, d, EPI_F16, e.ln2_g, e.ln2_b), s_);
+    const f16* xk = m.xkv.as<f16>() + (size_t)l * 2 * d;
+    XAttnArgs xa{m.qx.as<f16>(), d, xk, xk + d, ldxkv, 1500, R, hp.n_text_head, scale, m.part_o.as<float>(),
+                 m.part_ml.as<float2>(), m.attd.as<f16>(), d};
+    launch_xattn(xa, s_);
+    launch_proj(P(m.attd.as<f16>(), d, e.w_xo, e.b_xo, m.xd.p, d, d, d, EPI_F32_RESID), s_);
+    launch_proj(P(nullptr, d, e.w_fc1, e.b_fc1, m.mlpd.p, 4 * d, 4 * d, d, EPI_F16_GELU, e.ln3_g, e.ln3_b), s_);
+    launch_proj(P(m.mlpd.as<f16>(), 4 * d, e.w_fc2, e.b_fc2, m.xd.p, d, d, 4 * d, EPI_F32_RESID), s_);
+  }
+  launch_proj(P(nullptr, d, md.tok_emb, nullptr, m.logits.p, m.V, m.V, d, EPI_F32, md.ln_g, md.ln_b), s_);
+}
+
+void State::decoder_step(const int* toks, const int* seqs, const int* pos, int R) {
+  Impl& m = *m_;
   WDR_CHECK(R >= 1 && R <= NSEQ, "decoder step: row count out of range");
   for (int i = 0; i < R; ++i) {
     m.h_rows[i] = toks[i];
@@ -566,34 +632,74 @@ void State::decoder_step(const int* toks, const int* seqs, const int* pos, int R
   WDR_HIP(hipMemcpyAsync(m.rows_tok.p, m.h_rows, R * 4, hipMemcpyHostToDevice, s_));
   WDR_HIP(hipMemcpyAsync(m.rows_pos.p, m.h_rows + RMAX, R * 4, hipMemcpyHostToDevice, s_));
   WDR_HIP(hipMemcpyAsync(m.rows_seq.p, m.h_rows + 2 * RMAX, R * 4, hipMemcpyHostToDevice, s_));
-  launch_embed(md.tok_emb, md.dec_pos, m.rows_tok.as<int>(), m.rows_pos.as<int>(), R, d, m.xd.as<float>(), s_);
-  const float scale = 1.0f / 8.0f;
-  const int ldxkv = L * 2 * d;
-  for (int l = 0; l < L; ++l) {
-    const DecLayer& e = md.dec[l];
-    f16* kc = m.kc.as<f16>() + (size_t)l * NSEQ * m.seq_stride;
-    f16* vc = m.vc.as<f16>() + (size_t)l * NSEQ * m.seq_stride;
-    launch_layernorm(m.xd.as<float>(), d, e.ln1_g, e.ln1_b, m.hd.as<f16>(), d, R, d, s_);
-    proj(s_, m.hd.as<f16>(), d, e.w_qkv, d, e.b_qkv, m.qkvd.p, 3 * d, R, 3 * d, d, EPI_F16);
-    launch_kv_scatter(m.qkvd.as<f16>(), 3 * d, d, m.rows_seq.as<int>(), m.rows_pos.as<int>(), R, kc, vc, m.seq_stride,
-                      s_);
-    DecSelfArgs sa{m.qkvd.as<f16>(), 3 * d, kc, vc, m.seq_stride, d, m.rows_seq.as<int>(), m.rows_pos.as<int>(),
-                   m.attd.as<f16>(), d, scale};
-    launch_dec_self_attn(sa, R, hp.n_text_head, s_);
-    proj(s_, m.attd.as<f16>(), d, e.w_o, d, e.b_o, m.xd.p, d, R, d, d, EPI_F32_RESID);
-    launch_layernorm(m.xd.as<float>(), d, e.ln2_g, e.ln2_b, m.hd.as<f16>(), d, R, d, s_);
-    proj(s_, m.hd.as<f16>(), d, e.w_xq, d, e.b_xq, m.qx.p, d, R, d, d, EPI_F16);
-    const f16* xk = m.xkv.as<f16>() + (size_t)l * 2 * d;
-    XAttnArgs xa{m.qx.as<f16>(), d, xk, xk + d, ldxkv, 1500, R, hp.n_text_head, scale, m.part_o.as<float>(),
-                 m.part_ml.as<float2>(), m.attd.as<f16>(), d};
-    launch_xattn(xa, s_);
-    proj(s_, m.attd.as<f16>(), d, e.w_xo, d, e.b_xo, m.xd.p, d, R, d, d, EPI_F32_RESID);
-    launch_layernorm(m.xd.as<float>(), d, e.ln3_g, e.ln3_b, m.hd.as<f16>(), d, R, d, s_);
-    proj(s_, m.hd.as<f16>(), d, e.w_fc1, d, e.b_fc1, m.mlpd.p, 4 * d, R, 4 * d, d, EPI_F16_GELU);
-    proj(s_, m.mlpd.as<f16>(), 4 * d, e.w_fc2, 4 * d, e.b_fc2, m.xd.p, d, R, d, 4 * d, EPI_F32_RESID);
+  decoder_step_body(R);
+  times.decode_steps++;
+}
+
+// decode step + logit rules + greedy pick as ONE hipGraph replay per token (captured once per
+// row count; the per-step inputs live in pinned host buffers the graph's copy nodes read).
+void State::step_and_sample(const int* toks, const int* seqs, const int* pos, const LogitsCtl* ctl, int R,
+                            TokenData* out) {
+  Impl& m = *m_;
+  WDR_CHECK(R >= 1 && R <= NSEQ, "decoder step: row count out of range");
+  for (int i = 0; i < R; ++i) {
+    m.h_rows[i] = toks[i];
+    m.h_rows[RMAX + i] = pos[i];
+    m.h_rows[2 * RMAX + i] = seqs[i];
   }
-  launch_layernorm(m.xd.as<float>(), d, md.ln_g, md.ln_b, m.hd.as<f16>(), d, R, d, s_);
-  proj(s_, m.hd.as<f16>(), d, md.tok_emb, d, nullptr, m.logits.p, m.V, R, m.V, d, EPI_F32);
+  memcpy(m.h_ctl, ctl, R * sizeof(LogitsCtl));
+  if (prof_class() != PROF_NONE || getenv("WDR_NO_GRAPH")) {
+    // live per-kernel HIP-event timing cannot read events recorded inside a graph on this
+    // ROCm: run the same kernels eagerly while a profiling class is active
+    decoder_step(toks, seqs, pos, R);
+    run_logits(R, ctl, out, nullptr);
+    return;
+  }
+  Impl::StepGraph& g = m.graphs[R];
+  if (!g.exec || g.prof_cls != prof_class()) {
+    if (g.exec) {
+      (void)hipGraphExecDestroy(g.exec);
+      g.exec = nullptr;
+    }
+    g.pairs.clear();
+    g.prof_cls = prof_class();
+    hipGraph_t graph;
+    prof_capture_begin(&g.pairs);
+    WDR_HIP(hipStreamBeginCapture(s_, hipStreamCaptureModeThreadLocal));
+    WDR_HIP(hipMemcpyAsync(m.rows_tok.p, m.h_rows, R * 4, hipMemcpyHostToDevice, s_));
+    WDR_HIP(hipMemcpyAsync(m.rows_pos.p, m.h_rows + RMAX, R * 4, hipMemcpyHostToDevice, s_));
+    WDR_HIP(hipMemcpyAsync(m.rows_seq.p, m.h_rows + 2 * RMAX, R * 4, hipMemcpyHostToDevice, s_));
+    WDR_HIP(hipMemcpyAsync(m.ctl.p, m.h_ctl, R * sizeof(LogitsCtl), hipMemcpyHostToDevice, s_));
+    decoder_step_body(R);
+    launch_logits_process(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, m.work.as<float>(),
+                          m.tokout.as<TokOut>(), s_);
+    WDR_HIP(hipMemcpyAsync(m.h_tok, m.tokout.p, R * sizeof(TokOut), hipMemcpyDeviceToHost, s_));
+    WDR_HIP(hipStreamEndCapture(s_, &graph));
+    prof_capture_end();
+    WDR_HIP(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
+    WDR_HIP(hipGraphDestroy(graph));
+    g.vids = m.vids;
+  }
+  if (memcmp(&g.vids, &m.vids, sizeof(VocabIds)) != 0) {   // rule constants changed: recapture
+    (void)hipGraphExecDestroy(g.exec);
+    g.exec = nullptr;
+    step_and_sample(toks, seqs, pos, ctl, R, out);
+    return;
+  }
+  WDR_HIP(hipGraphLaunch(g.exec, s_));
+  WDR_HIP(hipStreamSynchronize(s_));
+  if (!g.pairs.empty()) prof_replayed(g.pairs);
+  for (int r = 0; r < R; ++r) {
+    const TokOut& o = m.h_tok[r];
+    TokenData t;
+    t.id = o.id;
+    t.tid = o.tid;
+    t.p = o.p;
+    t.plog = o.plog;
+    t.pt = o.pt;
+    t.ptsum = o.ptsum;
+    out[r] = t;
+  }
   times.decode_steps++;
 }
 
@@ -932,8 +1038,15 @@ int State::full(const FullParams& params, const float* samples, int n) {
         }
         TokenData tok;
         float ns = 0.f;
-        run_logits(1, &c, &tok, &ns);
-        if (i == 0) nosp = ns;
+        if (i == 0) {
+          run_logits(1, &c, &tok, &ns);
+          nosp = ns;
+        } else {
+          const int pos = (int)prompt.size() + i - 1;
+          const int seq0 = 0;
+          const int prev_id = sq.tokens.back().id;
+          step_and_sample(&prev_id, &seq0, &pos, &c, 1, &tok);
+        }
         sq.tokens.push_back(tok);
         if (tok.id > v.beg) {
           const int sdn = 2 * (tok.id - v.beg);
@@ -966,9 +1079,6 @@ int State::full(const FullParams& params, const float* samples, int n) {
           sq.failed = true;
           break;
         }
-        const int pos = (int)prompt.size() + i;
-        const int seq0 = 0;
-        decoder_step(&tok.id, &seq0, &pos, 1);
       }
       sq.tokens.resize(std::min((int)sq.tokens.size(), sq.result_len));
       score_sequence(sq, params);

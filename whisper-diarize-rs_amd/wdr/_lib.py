@@ -104,6 +104,8 @@ _SIGS = {
     "wdr_segment_list_free": (None, [P(SegmentList)]),
     "wdr_context_stage_times": (C.c_int, [vp, P(StageTimes)]),
     "wdr_context_hparams": (C.c_int, [vp, P(i32)]),
+    "wdr_prof_set": (C.c_int, [i32]),
+    "wdr_prof_read": (C.c_int, [P(f64), P(i64), P(f64), P(f64)]),
     "wdr_state_full": (C.c_int, [vp, P(f32), sz, P(TranscribeOptions), P(Synthetic), cstr, P(P(ResultSeg)), P(sz),
                                  P(i32)]),
     "wdr_result_free": (None, [P(ResultSeg), sz]),
