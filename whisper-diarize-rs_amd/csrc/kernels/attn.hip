@@ -182,74 +182,75 @@ void launch_flash_attn(const FlashArgs& a, int n_batch, hipStream_t s) {
   WDR_CHECK(a.Tq > 0 && a.Tk > 0, "attention: empty");
   if (a.nsplit > 1) {
     WDR_CHECK(n_batch == 1 && !a.causal && a.nsplit <= 64 && a.part_o && a.part_ml, "flash split: bad args");
-    const bool prof = prof_on(PROF_FLASH);
-    hipEvent_t e0 = nullptr;
-    if (prof) prof_begin(s, &e0);
-    hipLaunchKernelGGL(k_flash_attn, dim3(cdiv(a.Tq, 128), a.n_head, a.nsplit), dim3(256), 0, s, a);
+    wdr_launch(PROF_FLASH, (double)a.n_head * 64 * 2 * (2.0 * a.Tq + 2.0 * a.Tk), (double)a.n_head * a.Tq * a.Tk * 64 * 4,
+               k_flash_attn, dim3(cdiv(a.Tq, 128), a.n_head, a.nsplit), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_flash_combine, dim3(a.Tq, a.n_head), dim3(64), 0, s, a);
     WDR_HIP(hipGetLastError());
-    if (prof) prof_end(s, e0, (double)a.n_head * 64 * 2 * (2.0 * a.Tq + 2.0 * a.Tk), (double)a.n_head * a.Tq * a.Tk * 64 * 4);
     return;
   }
   dim3 grid(cdiv(a.Tq, 128), a.n_head, n_batch);
-  const bool prof = prof_on(PROF_FLASH);
-  hipEvent_t e0 = nullptr;
-  if (prof) prof_begin(s, &e0);
-  hipLaunchKernelGGL(k_flash_attn, grid, dim3(256), 0, s, a);
+  const double pairs = a.causal ? 0.5 * (double)a.Tq * a.Tk : (double)a.Tq * a.Tk;
+  wdr_launch(PROF_FLASH, (double)n_batch * a.n_head * 64 * 2 * (2.0 * a.Tq + 2.0 * a.Tk),
+             (double)n_batch * a.n_head * pairs * 64 * 4, k_flash_attn, grid, dim3(256), 0, s, a);
   WDR_HIP(hipGetLastError());
-  if (prof) {
-    const double pairs = a.causal ? 0.5 * (double)a.Tq * a.Tk : (double)a.Tq * a.Tk;
-    const double bytes = (double)n_batch * a.n_head * 64 * 2 * (2.0 * a.Tq + 2.0 * a.Tk);
-    prof_end(s, e0, bytes, (double)n_batch * a.n_head * pairs * 64 * 4);
-  }
 }
 
 // ---------------------------------------------------------------- decoder self-attention
-
-__global__ __launch_bounds__(64) void k_dec_self_attn(DecSelfArgs a) {
+// one 256-thread workgroup per (decoder row, head) over that row's cache (<= 448 keys):
+// keys spread over all 4 waves for the scores, 4 key quarters in parallel for P.V.
+__global__ __launch_bounds__(256) void k_dec_self_attn(DecSelfArgs a) {
   __shared__ float qs[64];
   __shared__ float sc[448];
-  const int r = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
+  __shared__ float red[2][4];
+  __shared__ float po[4][64];
+  const int r = blockIdx.x, h = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int seq = a.row_seq[r];
   const int nk = a.row_pos[r] + 1;
-  qs[lane] = (float)a.q[(long long)r * a.ldq + h * 64 + lane];
+  if (tid < 64) qs[tid] = (float)a.q[(long long)r * a.ldq + h * 64 + tid];
   __syncthreads();
   const f16* K = a.kc + seq * a.seq_stride + h * 64;
   const f16* V = a.vc + seq * a.seq_stride + h * 64;
   float mx = -INFINITY;
-  for (int k = lane; k < nk; k += 64) {
+  for (int k = tid; k < nk; k += 256) {
     const f16* kr = K + (long long)k * a.d;
+    f16x8 kv[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) kv[c] = *(const f16x8*)(kr + 8 * c);
     float s = 0.f;
 #pragma unroll
-    for (int c = 0; c < 64; c += 8) {
-      const f16x8 kv = *(const f16x8*)(kr + c);
+    for (int c = 0; c < 8; ++c)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s += qs[c + e] * (float)kv[e];
-    }
+      for (int e = 0; e < 8; ++e) s += qs[8 * c + e] * (float)kv[c][e];
     s *= a.scale;
     sc[k] = s;
     mx = fmaxf(mx, s);
   }
   mx = wave_max(mx);
+  if (lane == 0) red[0][wid] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
   float sum = 0.f;
-  for (int k = lane; k < nk; k += 64) {
+  for (int k = tid; k < nk; k += 256) {
     const float p = __expf(sc[k] - mx);
     sc[k] = p;
     sum += p;
   }
   sum = wave_sum(sum);
+  if (lane == 0) red[1][wid] = sum;
   __syncthreads();
-  const float inv = 1.f / sum;
+  const float inv = 1.f / (red[1][0] + red[1][1] + red[1][2] + red[1][3]);
   float acc = 0.f;
-  for (int k = 0; k < nk; ++k) {
+  for (int k = wid; k < nk; k += 4) {
     const float p = (float)(f16)(sc[k] * inv);
     acc += p * (float)V[(long long)k * a.d + lane];
   }
-  a.o[(long long)r * a.ldo + h * 64 + lane] = (f16)acc;
+  po[wid][lane] = acc;
+  __syncthreads();
+  if (tid < 64) a.o[(long long)r * a.ldo + h * 64 + tid] = (f16)(po[0][tid] + po[1][tid] + po[2][tid] + po[3][tid]);
 }
 
 void launch_dec_self_attn(const DecSelfArgs& a, int R, int n_head, hipStream_t s) {
-  hipLaunchKernelGGL(k_dec_self_attn, dim3(R, n_head), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(k_dec_self_attn, dim3(R, n_head), dim3(256), 0, s, a);
   WDR_HIP(hipGetLastError());
 }
 
@@ -319,33 +320,31 @@ __global__ __launch_bounds__(256) void k_xattn_partial(XAttnArgs a) {
   if (tid < R) a.part_ml[((long long)c * R + tid) * a.n_head + h] = mls[tid];
 }
 
-__global__ __launch_bounds__(64) void k_xattn_combine(XAttnArgs a, int nsplit) {
+template <int NS>
+__global__ __launch_bounds__(64) void k_xattn_combine(XAttnArgs a) {
   const int r = blockIdx.x, h = blockIdx.y, d = threadIdx.x;
-  // lane c < nsplit fetches chunk c's (max, sum); one wave reduction gives the global max
+  float po[NS];
+#pragma unroll
+  for (int c = 0; c < NS; ++c) po[c] = a.part_o[(((long long)c * a.R + r) * a.n_head + h) * 64 + d];
   float2 ml = make_float2(-INFINITY, 0.f);
-  if (d < nsplit) ml = a.part_ml[((long long)d * a.R + r) * a.n_head + h];
+  if (d < NS) ml = a.part_ml[((long long)d * a.R + r) * a.n_head + h];
   const float M = wave_max(ml.x);
-  const float w = (d < nsplit && ml.x != -INFINITY) ? __expf(ml.x - M) : 0.f;
+  const float w = (d < NS && ml.x != -INFINITY) ? __expf(ml.x - M) : 0.f;
   const float L = wave_sum(ml.y * w);
   float acc = 0.f;
-#pragma unroll 8
-  for (int c = 0; c < nsplit; ++c) {
-    const float wc = __shfl(w, c, 64);
-    acc += a.part_o[(((long long)c * a.R + r) * a.n_head + h) * 64 + d] * wc;
-  }
+#pragma unroll
+  for (int c = 0; c < NS; ++c) acc += po[c] * __shfl(w, c, 64);
   a.o[(long long)r * a.ldo + h * 64 + d] = (f16)(acc / L);
 }
 
 void launch_xattn(const XAttnArgs& a, hipStream_t s) {
   WDR_CHECK(a.R >= 1 && a.R <= XA_RMAX, "cross-attention decode: R out of range");
   const int nsplit = cdiv(a.Tk, XA_KC);
-  const bool prof = prof_on(PROF_XATTN);
-  hipEvent_t e0 = nullptr;
-  if (prof) prof_begin(s, &e0);
-  hipLaunchKernelGGL(k_xattn_partial, dim3(nsplit, a.n_head), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_xattn_combine, dim3(a.R, a.n_head), dim3(64), 0, s, a, nsplit);
+  wdr_launch(PROF_XATTN, (double)a.Tk * a.n_head * 64 * 2 * 2, (double)a.R * a.Tk * a.n_head * 64 * 4, k_xattn_partial,
+             dim3(nsplit, a.n_head), dim3(256), 0, s, a);
+  WDR_CHECK(nsplit == 24, "cross-attention decode expects 1500 keys");
+  hipLaunchKernelGGL(k_xattn_combine<24>, dim3(a.R, a.n_head), dim3(64), 0, s, a);
   WDR_HIP(hipGetLastError());
-  if (prof) prof_end(s, e0, (double)a.Tk * a.n_head * 64 * 2 * 2, (double)a.R * a.Tk * a.n_head * 64 * 4);
 }
 
 // ---------------------------------------------------------------- alignment-head capture

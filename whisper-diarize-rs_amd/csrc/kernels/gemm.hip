@@ -225,18 +225,30 @@ __device__ __forceinline__ void gemv_store(const ProjArgs& a, float (&acc)[MR], 
 template <int EPI, int MR, int NCH>
 __global__ __launch_bounds__(256) void k_gemv_ln(ProjArgs a) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // the first weight row is requested before the LayerNorm so its latency overlaps the norm
+  int n = blockIdx.x * 4 + wid;
+  f16x8 wv[NCH];
+  if (n < a.N) {
+    const f16* w = a.B + (size_t)n * a.ldb;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int k = c * 512 + lane * 8;
+      wv[c] = k < a.K ? *(const f16x8*)(w + k) : (f16x8){};
+    }
+  }
   f16x8 xr[MR][NCH];
 #pragma unroll
   for (int r = 0; r < MR; ++r) {
     if (r < a.M) ln_row_regs<NCH>(a, r, lane, xr[r]);
   }
-  for (int n = blockIdx.x * 4 + wid; n < a.N; n += gridDim.x * 4) {
-    const f16* w = a.B + (size_t)n * a.ldb;
-    f16x8 wv[NCH];
+  for (; n < a.N; n += gridDim.x * 4) {
+    if (n != blockIdx.x * 4 + wid) {
+      const f16* w = a.B + (size_t)n * a.ldb;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int k = c * 512 + lane * 8;
-      wv[c] = k < a.K ? *(const f16x8*)(w + k) : (f16x8){};
+      for (int c = 0; c < NCH; ++c) {
+        const int k = c * 512 + lane * 8;
+        wv[c] = k < a.K ? *(const f16x8*)(w + k) : (f16x8){};
+      }
     }
     float acc[MR];
 #pragma unroll
@@ -244,6 +256,31 @@ __global__ __launch_bounds__(256) void k_gemv_ln(ProjArgs a) {
       acc[r] = 0.f;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) acc[r] = dot8(wv[c], xr[r][c], acc[r]);
+    }
+    gemv_store<EPI, MR>(a, acc, lane, n);
+  }
+}
+
+// No-LN GEMV for M <= 2 with K = 512*NCH exactly: every weight and activation load of the
+// row is issued before the first dot product (K = 5120 keeps 10 KB per wave in flight).
+template <int EPI, int MR, int NCH>
+__global__ __launch_bounds__(256) void k_gemv_nc(ProjArgs a) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int n = blockIdx.x * 4 + wid; n < a.N; n += gridDim.x * 4) {
+    const f16* w = a.B + (size_t)n * a.ldb + lane * 8;
+    f16x8 wv[NCH], xv[MR][NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) wv[c] = *(const f16x8*)(w + c * 512);
+#pragma unroll
+    for (int r = 0; r < MR; ++r)
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) xv[r][c] = *(const f16x8*)(a.A + (size_t)r * a.lda + c * 512 + lane * 8);
+    float acc[MR];
+#pragma unroll
+    for (int r = 0; r < MR; ++r) {
+      acc[r] = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) acc[r] = dot8(wv[c], xv[r][c], acc[r]);
     }
     gemv_store<EPI, MR>(a, acc, lane, n);
   }
@@ -344,28 +381,44 @@ __global__ __launch_bounds__(256) void k_skinny(ProjArgs a) {
 
 template <int EPI>
 static void launch_epi(const ProjArgs& a, hipStream_t s) {
-  const int cls = a.M <= 64 ? PROF_GEMV : PROF_GEMM;
-  const bool prof = prof_on(cls);
-  hipEvent_t e0 = nullptr;
-  if (prof) prof_begin(s, &e0);
+  const int ob = (EPI == EPI_F32_RESID || EPI == EPI_F32 || EPI == EPI_F32_GELU_POS) ? 4 : 2;
+  const double bytes = (double)a.N * a.K * 2 + (double)a.M * a.K * 2 + (double)a.M * a.N * ob;
+  const double flops = 2.0 * a.M * a.N * a.K;
   if (a.M <= 8) {
     const int nwg = std::min(cdiv(a.N, 4), 1024);
-    dim3 grid(nwg);
+    dim3 grid(nwg), blk(256);
     const bool ln = a.ln_x != nullptr;
     if (ln && a.M <= 2 && a.K <= 1536) {
       const int nch = cdiv(a.K, 512);
-#define WDR_GLN(MR, NCH) hipLaunchKernelGGL((k_gemv_ln<EPI, MR, NCH>), grid, dim3(256), 0, s, a);
+#define WDR_GLN(MR, NCH) wdr_launch(PROF_GEMV, bytes, flops, k_gemv_ln<EPI, MR, NCH>, grid, blk, 0, s, a);
       if (a.M == 1) {
         if (nch == 1) { WDR_GLN(1, 1) } else if (nch == 2) { WDR_GLN(1, 2) } else { WDR_GLN(1, 3) }
       } else {
         if (nch == 1) { WDR_GLN(2, 1) } else if (nch == 2) { WDR_GLN(2, 2) } else { WDR_GLN(2, 3) }
       }
 #undef WDR_GLN
+    } else if (!ln && a.M <= 2 && a.K % 512 == 0 && a.K <= 5120) {
+      const int nch = a.K / 512;
+#define WDR_GNC(MR, NCH) wdr_launch(PROF_GEMV, bytes, flops, k_gemv_nc<EPI, MR, NCH>, grid, blk, 0, s, a);
+#define WDR_GNC_M(MR)                                                          \
+  switch (nch) {                                                               \
+    case 1: WDR_GNC(MR, 1) break;                                              \
+    case 2: WDR_GNC(MR, 2) break;                                              \
+    case 3: WDR_GNC(MR, 3) break;                                              \
+    case 4: WDR_GNC(MR, 4) break;                                              \
+    case 6: WDR_GNC(MR, 6) break;                                              \
+    case 8: WDR_GNC(MR, 8) break;                                              \
+    case 10: WDR_GNC(MR, 10) break;                                            \
+    default: wdr_launch(PROF_GEMV, bytes, flops, k_gemv<EPI, MR, false>, grid, blk, 0, s, a); \
+  }
+      if (a.M == 1) { WDR_GNC_M(1) } else { WDR_GNC_M(2) }
+#undef WDR_GNC_M
+#undef WDR_GNC
     } else {
-      const size_t lds = ln ? (size_t)a.M * a.K * 2 : 0;
-#define WDR_GEMV(MR)                                                                      \
-  if (ln) hipLaunchKernelGGL((k_gemv<EPI, MR, true>), grid, dim3(256), lds, s, a);       \
-  else hipLaunchKernelGGL((k_gemv<EPI, MR, false>), grid, dim3(256), 0, s, a);
+      const uint32_t lds = ln ? (uint32_t)a.M * a.K * 2 : 0;
+#define WDR_GEMV(MR)                                                                          \
+  if (ln) wdr_launch(PROF_GEMV, bytes, flops, k_gemv<EPI, MR, true>, grid, blk, lds, s, a);  \
+  else wdr_launch(PROF_GEMV, bytes, flops, k_gemv<EPI, MR, false>, grid, blk, 0, s, a);
       if (a.M <= 1) { WDR_GEMV(1) }
       else if (a.M <= 2) { WDR_GEMV(2) }
       else if (a.M <= 4) { WDR_GEMV(4) }
@@ -374,11 +427,11 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
     }
   } else if (a.M <= 64) {
     const bool wide = a.N >= 4096;
-    dim3 grid(cdiv(a.N, wide ? 32 : 16));
+    dim3 grid(cdiv(a.N, wide ? 32 : 16)), blk(256);
     const int mt = cdiv(a.M, 16);
-#define WDR_SK(MTV)                                                                        \
-  if (wide) hipLaunchKernelGGL((k_skinny<EPI, MTV, 2>), grid, dim3(256), 0, s, a);        \
-  else hipLaunchKernelGGL((k_skinny<EPI, MTV, 1>), grid, dim3(256), 0, s, a);
+#define WDR_SK(MTV)                                                                            \
+  if (wide) wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, MTV, 2>, grid, blk, 0, s, a);  \
+  else wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, MTV, 1>, grid, blk, 0, s, a);
     if (mt == 1) { WDR_SK(1) }
     else if (mt == 2) { WDR_SK(2) }
     else if (mt == 3) { WDR_SK(3) }
@@ -386,12 +439,7 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
 #undef WDR_SK
   } else {
     dim3 grid(a.N / GB_N, cdiv(a.M, GB_M));
-    hipLaunchKernelGGL((k_gemm<EPI>), grid, dim3(256), 0, s, a);
-  }
-  if (prof) {
-    const int ob = (EPI == EPI_F32_RESID || EPI == EPI_F32 || EPI == EPI_F32_GELU_POS) ? 4 : 2;
-    const double bytes = (double)a.N * a.K * 2 + (double)a.M * a.K * 2 + (double)a.M * a.N * ob;
-    prof_end(s, e0, bytes, 2.0 * a.M * a.N * a.K);
+    wdr_launch(PROF_GEMM, bytes, flops, k_gemm<EPI>, grid, dim3(256), 0, s, a);
   }
 }
 

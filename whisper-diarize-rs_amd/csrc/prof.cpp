@@ -13,12 +13,37 @@ struct Rec {
 };
 std::mutex g_mu;
 int g_cls = PROF_NONE;
+bool g_broken = false;
+unsigned g_tick = 0;
+constexpr unsigned kEvery = 8;
 std::vector<Rec> g_pending;
 std::vector<hipEvent_t> g_pool;
 double g_ms = 0, g_bytes = 0, g_flops = 0;
 long long g_n = 0;
 
-hipEvent_t get_event() {
+void drain_locked() {
+  for (auto& r : g_pending) {
+    float ms = 0;
+    if (hipEventSynchronize(r.b) != hipSuccess || hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) {
+      (void)hipGetLastError();
+      g_broken = true;
+    }
+    g_ms += ms;
+    g_pool.push_back(r.a);
+    g_pool.push_back(r.b);
+  }
+  g_pending.clear();
+}
+}  // namespace
+
+bool prof_on(int cls) {
+  if (g_cls == PROF_NONE || g_cls != cls) return false;
+  return (g_tick++ % kEvery) == 0;
+}
+int prof_class() { return g_cls; }
+
+hipEvent_t prof_event() {
+  std::lock_guard<std::mutex> l(g_mu);
   if (!g_pool.empty()) {
     hipEvent_t e = g_pool.back();
     g_pool.pop_back();
@@ -29,73 +54,9 @@ hipEvent_t get_event() {
   return e;
 }
 
-void drain_locked() {
-  for (auto& r : g_pending) {
-    WDR_HIP(hipEventSynchronize(r.b));
-    float ms = 0;
-    WDR_HIP(hipEventElapsedTime(&ms, r.a, r.b));
-    g_ms += ms;
-    g_pool.push_back(r.a);
-    g_pool.push_back(r.b);
-  }
-  g_pending.clear();
-}
-}  // namespace
-
-static std::vector<ProfPair>* g_cap = nullptr;
-static bool g_broken = false;
-
-// 1 in kEvery launches of the class is bracketed by events (sampling keeps the event-record
-// overhead out of the timed region; averages are per sampled launch)
-static constexpr unsigned kEvery = 8;
-static unsigned g_tick = 0;
-bool prof_on(int cls) {
-  if (g_cls == PROF_NONE || g_cls != cls) return false;
-  return (g_tick++ % kEvery) == 0;
-}
-int prof_class() { return g_cls; }
-
-void prof_begin(hipStream_t s, hipEvent_t* e0) {
+void prof_push(hipEvent_t a, hipEvent_t b, double bytes, double flops) {
   std::lock_guard<std::mutex> l(g_mu);
-  *e0 = get_event();
-  // inside a stream capture an event record must be an *external* node to be queryable
-  WDR_HIP(hipEventRecord(*e0, s));
-}
-
-void prof_capture_begin(std::vector<ProfPair>* into) {
-  std::lock_guard<std::mutex> l(g_mu);
-  g_cap = into;
-}
-void prof_capture_end() {
-  std::lock_guard<std::mutex> l(g_mu);
-  g_cap = nullptr;
-}
-void prof_replayed(const std::vector<ProfPair>& pairs) {
-  std::lock_guard<std::mutex> l(g_mu);
-  if (g_cls == PROF_NONE) return;
-  for (const auto& p : pairs) {
-    float ms = 0;
-    if (hipEventElapsedTime(&ms, p.a, p.b) != hipSuccess) {   // never fail the pipeline over timing
-      (void)hipGetLastError();
-      g_broken = true;
-      continue;
-    }
-    g_ms += ms;
-    g_bytes += p.bytes;
-    g_flops += p.flops;
-    g_n++;
-  }
-}
-
-void prof_end(hipStream_t s, hipEvent_t e0, double bytes, double flops) {
-  std::lock_guard<std::mutex> l(g_mu);
-  hipEvent_t e1 = get_event();
-  WDR_HIP(hipEventRecord(e1, s));
-  if (g_cap) {
-    g_cap->push_back({e0, e1, bytes, flops});
-    return;
-  }
-  g_pending.push_back({e0, e1});
+  g_pending.push_back({a, b});
   g_bytes += bytes;
   g_flops += flops;
   g_n++;
@@ -107,10 +68,7 @@ void prof_end(hipStream_t s, hipEvent_t e0, double bytes, double flops) {
 extern "C" {
 int wdr_prof_set(int32_t cls) {
   std::lock_guard<std::mutex> l(wdr::g_mu);
-  try {
-    wdr::drain_locked();
-  } catch (...) {
-  }
+  wdr::drain_locked();
   wdr::g_cls = cls;
   wdr::g_broken = false;
   wdr::g_tick = 0;
@@ -120,11 +78,7 @@ int wdr_prof_set(int32_t cls) {
 }
 int wdr_prof_read(double* total_ms, int64_t* launches, double* algo_bytes, double* algo_flops) {
   std::lock_guard<std::mutex> l(wdr::g_mu);
-  try {
-    wdr::drain_locked();
-  } catch (...) {
-    return -1;
-  }
+  wdr::drain_locked();
   if (wdr::g_broken) return -2;
   *total_ms = wdr::g_ms;
   *launches = wdr::g_n;

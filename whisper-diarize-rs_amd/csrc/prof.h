@@ -1,30 +1,33 @@
-// Live per-kernel-class timing with HIP events (bench.py's roofline figure).
-// One class is enabled at a time; every launch of that class records an event pair on
-// the stream it runs on, plus its algorithmic bytes and flops.
+// Live per-kernel-class timing for bench.py's roofline figure.  One class is enabled at a
+// time; 1 in 8 launches of that class is issued with hipExtLaunchKernelGGL start/stop events
+// (timestamps of the dispatch itself, the same interval rocprofv3 reports), together with the
+// launch's algorithmic bytes and flops.  Graph replay is bypassed while a class is enabled.
 #pragma once
-#include "common.h"
+#include <hip/hip_ext.h>
 
 #include <vector>
 
+#include "common.h"
+
 namespace wdr {
 
-enum ProfClass : int { PROF_NONE = 0, PROF_GEMM = 1, PROF_GEMV = 2, PROF_FLASH = 3, PROF_XATTN = 4, PROF_MEL = 5,
-                       PROF_DTW = 6, PROF_LOGITS = 7 };
+enum ProfClass : int { PROF_NONE = 0, PROF_GEMM = 1, PROF_GEMV = 2, PROF_FLASH = 3, PROF_XATTN = 4, PROF_SKINNY = 5 };
 
 bool prof_on(int cls);
 int prof_class();
-void prof_begin(hipStream_t s, hipEvent_t* e0);
-void prof_end(hipStream_t s, hipEvent_t e0, double bytes, double flops);
+hipEvent_t prof_event();
+void prof_push(hipEvent_t a, hipEvent_t b, double bytes, double flops);
 
-// Graph support: while a stream capture is open, prof_end() appends the event pair to the
-// capture list instead of the pending list; each replay of the graph re-records the same
-// events, and prof_replayed() (after the replay completed) accumulates their elapsed times.
-struct ProfPair {
-  hipEvent_t a, b;
-  double bytes, flops;
-};
-void prof_capture_begin(std::vector<ProfPair>* into);
-void prof_capture_end();
-void prof_replayed(const std::vector<ProfPair>& pairs);
+template <typename F, typename... Args>
+inline void wdr_launch(int cls, double bytes, double flops, F kernel, dim3 grid, dim3 block, uint32_t shmem,
+                       hipStream_t s, Args... args) {
+  if (prof_on(cls)) {
+    hipEvent_t a = prof_event(), b = prof_event();
+    hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, a, b, 0, args...);
+    prof_push(a, b, bytes, flops);
+  } else {
+    hipLaunchKernelGGL(kernel, grid, block, shmem, s, args...);
+  }
+}
 
 }  // namespace wdr

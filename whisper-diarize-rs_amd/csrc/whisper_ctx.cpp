@@ -332,7 +332,6 @@ struct State::Impl {
   struct StepGraph {
     hipGraphExec_t exec = nullptr;
     int prof_cls = -1;
-    std::vector<ProfPair> pairs;
     VocabIds vids{};
   };
   std::map<int, StepGraph> graphs;
@@ -661,10 +660,8 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
       (void)hipGraphExecDestroy(g.exec);
       g.exec = nullptr;
     }
-    g.pairs.clear();
     g.prof_cls = prof_class();
     hipGraph_t graph;
-    prof_capture_begin(&g.pairs);
     WDR_HIP(hipStreamBeginCapture(s_, hipStreamCaptureModeThreadLocal));
     WDR_HIP(hipMemcpyAsync(m.rows_tok.p, m.h_rows, R * 4, hipMemcpyHostToDevice, s_));
     WDR_HIP(hipMemcpyAsync(m.rows_pos.p, m.h_rows + RMAX, R * 4, hipMemcpyHostToDevice, s_));
@@ -675,7 +672,6 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
                           m.tokout.as<TokOut>(), s_);
     WDR_HIP(hipMemcpyAsync(m.h_tok, m.tokout.p, R * sizeof(TokOut), hipMemcpyDeviceToHost, s_));
     WDR_HIP(hipStreamEndCapture(s_, &graph));
-    prof_capture_end();
     WDR_HIP(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
     WDR_HIP(hipGraphDestroy(graph));
     g.vids = m.vids;
@@ -688,7 +684,6 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
   }
   WDR_HIP(hipGraphLaunch(g.exec, s_));
   WDR_HIP(hipStreamSynchronize(s_));
-  if (!g.pairs.empty()) prof_replayed(g.pairs);
   for (int r = 0; r < R; ++r) {
     const TokOut& o = m.h_tok[r];
     TokenData t;
