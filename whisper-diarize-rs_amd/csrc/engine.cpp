@@ -355,11 +355,29 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
     *has_lang = true;
   }
   const bool translated = o && o->whisper_to_english == 1;
-  std::vector<float> samples;
+  // every segment's PCM goes to the encode-ahead ring up front (int16 -> f32 on the GPU,
+  // the same x / 32768 as src/transcribe.rs's conversion)
+  {
+    std::vector<const int16_t*> pcm(segs.size());
+    std::vector<int> ns(segs.size());
+    for (size_t i = 0; i < segs.size(); ++i) {
+      WDR_CHECK(segs[i].n_samples < (size_t)INT32_MAX, "speech segment too long");
+      pcm[i] = segs[i].samples;
+      ns[i] = (int)segs[i].n_samples;
+    }
+    c->st->plan(pcm.data(), ns.data(), (int)segs.size());
+  }
+  struct Unplan {
+    State& st;
+    ~Unplan() {
+      try {
+        st.unplan();
+      } catch (...) {
+      }
+    }
+  } unplan_guard{*c->st};
   for (size_t i = 0; i < segs.size(); ++i) {
     const wdr_speech_segment& ss = segs[i];
-    samples.resize(ss.n_samples);
-    for (size_t k = 0; k < ss.n_samples; ++k) samples[k] = (float)ss.samples[k] / 32768.0f;
     if (have_prev) {
       params.initial_prompt = previous_text;
       params.has_initial_prompt = true;
@@ -367,7 +385,7 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
     if (cb && cb->is_cancelled && cb->is_cancelled(cb->user)) throw std::runtime_error("failed to transcribe");
     int rc;
     try {
-      rc = c->st->full(params, samples.data(), (int)samples.size());
+      rc = c->st->full(params, nullptr, 0, (int)i);
     } catch (const std::exception& ex) {
       throw std::runtime_error(std::string("failed to transcribe: ") + ex.what());
     }

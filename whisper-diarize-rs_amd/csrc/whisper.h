@@ -128,7 +128,11 @@ class State {
   explicit State(Context& ctx);
   ~State();
   // whisper_full_with_state on host f32 samples. Returns 0 on success.
-  int full(const FullParams& p, const float* samples, int n);
+  // job >= 0: segment `job` of the current plan (samples / n come from the plan).
+  int full(const FullParams& p, const float* samples, int n, int job = -1);
+  // encode-ahead: the pipeline's whole segment list (int16 PCM), see whisper_ctx.cpp
+  void plan(const int16_t* const* pcm, const int* n, int count);
+  void unplan();
   std::vector<ResultSeg> result_all;
   int lang_id = 0;
   StageTimes times;
@@ -151,6 +155,7 @@ class State {
   hipStream_t s_;
   std::unique_ptr<Impl> m_;
   // pieces of full()
+  void top_up(int job);
   void decoder_prefill(const int* toks, int n, int seq, bool want_logits, bool capture);
   void decoder_step(const int* toks, const int* seqs, const int* pos, int R);
   void decoder_step_body(int R);

@@ -151,7 +151,13 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
     : name(model_name), cp(p), vocab(hp.n_vocab) {
   WDR_CHECK(cp.use_gpu, "libwdr has no CPU backend: use_gpu=false is not supported (the CPU restatement is test-only)");
   WDR_HIP(hipSetDevice(cp.gpu_device));
-  WDR_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  {
+    // the latency-bound decode chain runs at the highest priority; the encode-ahead
+    // stream (State) fills the CUs it leaves idle
+    int lo = 0, hi = 0;
+    WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    WDR_HIP(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, hi));
+  }
   Model& m = model;
   m.hp = hp;
   const int d = hp.n_audio_state, dt = hp.n_text_state;
@@ -308,13 +314,35 @@ static constexpr int NSPLIT = 24;  // cross-attention key chunks (1500 / 64)
 
 struct State::Impl {
   int d, L, H, V, n_mels, kp1;
-  // front-end
-  DevMem x;  int x_cap = 0;   // samples f32
-  DevMem mel; int mel_cap = 0;
-  DevMem gmax, energy_d;
-  int n_fft_frames = 0, n_samples = 0;
-  // encoder
-  DevMem im2col, c1, ex, eh, eqkv, eatt, emlp, xkv;
+  // encoder activations for nb windows stacked along M (rows b*1500 ..): one set for the
+  // encode-ahead stream (nb = kBatch), one single-window set for on-demand windows
+  struct EncBufs {
+    int nb = 0;
+    DevMem im2col, c1, ex, eh, eqkv, eatt, emlp;
+  };
+  EncBufs eb, e1;
+  // cross-K/V ring: one slot per in-flight speech segment, [slot][1500][L*2d] f16, plus a
+  // scratch slot (index S) for un-planned calls.  Each slot also owns its segment's samples,
+  // log-mel and global max, so later windows of a long segment encode from the slot.
+  struct Slot {
+    DevMem x, mel, gmax, pcm;
+    int16_t* h_pcm = nullptr;   // pinned staging for the H2D copy of the segment's PCM
+    int pcm_cap = 0, x_cap = 0, mel_cap = 0, n_fft_frames = 0, n_samples = 0;
+    hipEvent_t ready = nullptr, freed = nullptr;
+  };
+  std::vector<Slot> slots;
+  int S = 0;                  // ring slots (multiple of kBatch)
+  DevMem xkv_ring;
+  size_t xkv_slot_elems = 0;
+  int cur = 0;                // slot the decoder reads (cross-K/V, samples)
+  hipStream_t es = nullptr;   // encode-ahead stream (lower priority than the decode stream)
+  struct Plan {
+    std::vector<const int16_t*> pcm;
+    std::vector<int> n;
+    size_t next_enq = 0;
+  } plan;
+  DevMem energy_d; int energy_cap = 0;
+  const f16* xkv() const { return xkv_ring.as<f16>() + (size_t)cur * xkv_slot_elems; }
   // decoder
   DevMem xd, hd, qkvd, attd, qx, mlpd, logits, work, tokout, ctl, ml, cap, part_o, part_ml;
   DevMem rows_tok, rows_pos, rows_seq;
@@ -334,8 +362,22 @@ struct State::Impl {
     int prof_cls = -1;
     VocabIds vids{};
   };
-  std::map<int, StepGraph> graphs;
+  std::map<int, StepGraph> graphs;   // key: R * 256 + slot (the cross-K/V pointer is baked in)
 };
+
+static constexpr int kBatch = 4;     // encoder windows per encode-ahead launch (M = 6000 rows)
+static constexpr int kSlots = 16;    // in-flight segments in the cross-K/V ring
+
+static void alloc_enc(State::Impl::EncBufs& e, int nb, int d, int kp1) {
+  e.nb = nb;
+  e.im2col = DevMem((size_t)nb * 3000 * std::max(kp1, 3 * d) * 2);
+  e.c1 = DevMem((size_t)nb * 3000 * d * 2);
+  e.ex = DevMem((size_t)nb * 1500 * d * 4);
+  e.eh = DevMem((size_t)nb * 1500 * d * 2);
+  e.eqkv = DevMem((size_t)nb * 1500 * 3 * d * 2);
+  e.eatt = DevMem((size_t)nb * 1500 * d * 2);
+  e.emlp = DevMem((size_t)nb * 1500 * 4 * d * 2);
+}
 
 State::State(Context& ctx) : ctx_(ctx), s_(ctx.stream), m_(new Impl) {
   WDR_HIP(hipSetDevice(ctx.cp.gpu_device));
@@ -348,15 +390,23 @@ State::State(Context& ctx) : ctx_(ctx), s_(ctx.stream), m_(new Impl) {
   m.n_mels = hp.n_mels;
   m.kp1 = ctx.model.kp1;
   const int d = m.d;
-  m.gmax = DevMem(16);
-  m.im2col = DevMem((size_t)3000 * std::max(m.kp1, 3 * d) * 2);
-  m.c1 = DevMem((size_t)3000 * d * 2);
-  m.ex = DevMem((size_t)1500 * d * 4);
-  m.eh = DevMem((size_t)1500 * d * 2);
-  m.eqkv = DevMem((size_t)1500 * 3 * d * 2);
-  m.eatt = DevMem((size_t)1500 * d * 2);
-  m.emlp = DevMem((size_t)1500 * 4 * d * 2);
-  m.xkv = DevMem((size_t)1500 * m.L * 2 * d * 2);
+  alloc_enc(m.e1, 1, d, m.kp1);
+  alloc_enc(m.eb, kBatch, d, m.kp1);
+  m.S = kSlots;
+  m.slots.resize(m.S + 1);
+  for (auto& sl : m.slots) {
+    sl.gmax = DevMem(16);
+    WDR_HIP(hipEventCreateWithFlags(&sl.ready, hipEventDisableTiming));
+    WDR_HIP(hipEventCreateWithFlags(&sl.freed, hipEventDisableTiming));
+  }
+  m.xkv_slot_elems = (size_t)1500 * m.L * 2 * d;
+  m.xkv_ring = DevMem((m.S + 1) * m.xkv_slot_elems * 2);
+  m.cur = m.S;
+  {
+    int lo = 0, hi = 0;
+    WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    WDR_HIP(hipStreamCreateWithPriority(&m.es, hipStreamNonBlocking, lo));
+  }
   m.xd = DevMem((size_t)RMAX * d * 4);
   m.hd = DevMem((size_t)RMAX * d * 2);
   m.qkvd = DevMem((size_t)RMAX * 3 * d * 2);
@@ -400,36 +450,57 @@ State::~State() {
     (void)hipHostFree(m_->h_tok);
     (void)hipHostFree(m_->h_ctl);
     (void)hipHostFree(m_->h_times);
+    if (m_->es) {
+      (void)hipStreamSynchronize(m_->es);
+      (void)hipStreamDestroy(m_->es);
+    }
+    for (auto& sl : m_->slots) {
+      if (sl.h_pcm) (void)hipHostFree(sl.h_pcm);
+      if (sl.ready) (void)hipEventDestroy(sl.ready);
+      if (sl.freed) (void)hipEventDestroy(sl.freed);
+    }
   }
 }
 
 // ------------------------------------------------------------------ front-end
-void State::compute_mel(const float* x_host, int n) {
-  Impl& m = *m_;
-  if (n > m.x_cap) {
-    m.x = DevMem((size_t)std::max(n, 1) * 4);
-    m.energy_d = DevMem((size_t)std::max(n, 1) * 4);
-    m.x_cap = n;
-  }
+// Samples -> slot: f32 samples and the whole segment's log-mel (+ its global max, which
+// normalises every window of the segment: whisper.cpp log_mel_spectrogram).
+static void slot_mel(Context& ctx, State::Impl& m, State::Impl::Slot& sl, int n, hipStream_t s) {
   const int n_len = (n + 480000 + 400 - 400) / 160;
   const int n_eff = n + 200;
-  m.n_fft_frames = std::min(n_eff / 160 + 1, n_len);
-  m.n_samples = n;
-  if (m.n_fft_frames > m.mel_cap) {
-    m.mel = DevMem((size_t)m.n_fft_frames * m.n_mels * 4);
-    m.mel_cap = m.n_fft_frames;
+  sl.n_fft_frames = std::min(n_eff / 160 + 1, n_len);
+  sl.n_samples = n;
+  if (sl.n_fft_frames > sl.mel_cap) {
+    sl.mel = DevMem((size_t)sl.n_fft_frames * m.n_mels * 4);
+    sl.mel_cap = sl.n_fft_frames;
   }
-  if (n > 0) WDR_HIP(hipMemcpyAsync(m.x.p, x_host, (size_t)n * 4, hipMemcpyHostToDevice, s_));
-  launch_gmax_init(m.gmax.as<int>(), s_);
-  MelArgs a{m.x.as<float>(), n, m.n_fft_frames, m.n_mels, ctx_.model.hann, ctx_.model.cos_tab, ctx_.model.sin_tab,
-            ctx_.model.mel_filters, m.mel.as<float>(), m.gmax.as<int>()};
-  launch_mel(a, s_);
+  launch_gmax_init(sl.gmax.as<int>(), s);
+  MelArgs a{sl.x.as<float>(), n, sl.n_fft_frames, m.n_mels, ctx.model.hann, ctx.model.cos_tab, ctx.model.sin_tab,
+            ctx.model.mel_filters, sl.mel.as<float>(), sl.gmax.as<int>()};
+  launch_mel(a, s);
+}
+
+static void slot_reserve_x(State::Impl::Slot& sl, int n) {
+  if (n > sl.x_cap) {
+    sl.x = DevMem((size_t)std::max(n, 1) * 4);
+    sl.x_cap = n;
+  }
+}
+
+void State::compute_mel(const float* x_host, int n) {
+  Impl& m = *m_;
+  m.cur = m.S;
+  Impl::Slot& sl = m.slots[m.S];
+  slot_reserve_x(sl, n);
+  if (n > 0) WDR_HIP(hipMemcpyAsync(sl.x.p, x_host, (size_t)n * 4, hipMemcpyHostToDevice, s_));
+  slot_mel(ctx_, m, sl, n, s_);
 }
 
 void State::read_mel_window(int seek, float* out) {
   Impl& m = *m_;
+  Impl::Slot& sl = m.slots[m.cur];
   DevMem tmp((size_t)m.n_mels * 3000 * 4);
-  launch_mel_window(m.mel.as<float>(), m.n_mels, m.n_fft_frames, m.gmax.as<int>(), seek, tmp.as<float>(), s_);
+  launch_mel_window(sl.mel.as<float>(), m.n_mels, sl.n_fft_frames, sl.gmax.as<int>(), seek, tmp.as<float>(), s_);
   WDR_HIP(hipMemcpyAsync(out, tmp.p, tmp.bytes, hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
 }
@@ -441,44 +512,53 @@ static void proj(hipStream_t s, const f16* A, int lda, const f16* W, int ldw, co
   launch_proj(a, s);
 }
 
-static void encoder_body(Context& ctx, State::Impl& m, hipStream_t s) {
+// nb windows whose conv1 im2col rows are already in e.im2col ([nb*3000][kp1]); writes the
+// cross K/V of window b to xkv_out + b * xkv_slot_elems.  Every GEMM runs with M = nb*1500
+// (or nb*3000 for conv1) so one launch covers the batch.
+static void encoder_body(Context& ctx, State::Impl& m, State::Impl::EncBufs& e, int nb, f16* xkv_out, hipStream_t s) {
   const Model& md = ctx.model;
   const HParams& hp = md.hp;
   const int d = hp.n_audio_state;
-  // conv1 (+GELU) -> c1 f16 [3000][d]
-  proj(s, m.im2col.as<f16>(), md.kp1, md.conv1_w, md.kp1, md.conv1_b, m.c1.p, d, 3000, d, md.kp1, EPI_F16_GELU);
-  launch_im2col_conv2(m.c1.as<f16>(), d, m.im2col.as<f16>(), s);
-  // conv2 (+GELU) + positional -> ex f32 [1500][d]
-  proj(s, m.im2col.as<f16>(), 3 * d, md.conv2_w, 3 * d, md.conv2_b, m.ex.p, d, 1500, d, 3 * d, EPI_F32_GELU_POS,
+  const int M = nb * 1500;
+  // conv1 (+GELU) -> c1 f16 [nb*3000][d]
+  proj(s, e.im2col.as<f16>(), md.kp1, md.conv1_w, md.kp1, md.conv1_b, e.c1.p, d, 2 * M, d, md.kp1, EPI_F16_GELU);
+  for (int b = 0; b < nb; ++b)
+    launch_im2col_conv2(e.c1.as<f16>() + (size_t)b * 3000 * d, d, e.im2col.as<f16>() + (size_t)b * 1500 * 3 * d, s);
+  // conv2 (+GELU) + positional -> ex f32 [nb*1500][d]
+  proj(s, e.im2col.as<f16>(), 3 * d, md.conv2_w, 3 * d, md.conv2_b, e.ex.p, d, M, d, 3 * d, EPI_F32_GELU_POS,
        md.enc_pos, hp.n_audio_ctx);
   const float scale = 1.0f / 8.0f;   // d_head^-1/2
+  const long long bs = 1500ll * 3 * d, obs = 1500ll * d;
   for (int l = 0; l < hp.n_audio_layer; ++l) {
-    const EncLayer& e = md.enc[l];
-    launch_layernorm(m.ex.as<float>(), d, e.ln1_g, e.ln1_b, m.eh.as<f16>(), d, 1500, d, s);
-    proj(s, m.eh.as<f16>(), d, e.w_qkv, d, e.b_qkv, m.eqkv.p, 3 * d, 1500, 3 * d, d, EPI_F16);
-    FlashArgs fa{m.eqkv.as<f16>(), 3 * d, 0, m.eqkv.as<f16>() + d, 3 * d, 0, m.eqkv.as<f16>() + 2 * d, 3 * d, 0,
-                 m.eatt.as<f16>(), d, 0, nullptr, 1500, 1500, hp.n_audio_head, 0, scale};
-    launch_flash_attn(fa, 1, s);
-    proj(s, m.eatt.as<f16>(), d, e.w_o, d, e.b_o, m.ex.p, d, 1500, d, d, EPI_F32_RESID);
-    launch_layernorm(m.ex.as<float>(), d, e.ln2_g, e.ln2_b, m.eh.as<f16>(), d, 1500, d, s);
-    proj(s, m.eh.as<f16>(), d, e.w_fc1, d, e.b_fc1, m.emlp.p, 4 * d, 1500, 4 * d, d, EPI_F16_GELU);
-    proj(s, m.emlp.as<f16>(), 4 * d, e.w_fc2, 4 * d, e.b_fc2, m.ex.p, d, 1500, d, 4 * d, EPI_F32_RESID);
+    const EncLayer& w = md.enc[l];
+    launch_layernorm(e.ex.as<float>(), d, w.ln1_g, w.ln1_b, e.eh.as<f16>(), d, M, d, s);
+    proj(s, e.eh.as<f16>(), d, w.w_qkv, d, w.b_qkv, e.eqkv.p, 3 * d, M, 3 * d, d, EPI_F16);
+    FlashArgs fa{e.eqkv.as<f16>(), 3 * d, bs, e.eqkv.as<f16>() + d, 3 * d, bs, e.eqkv.as<f16>() + 2 * d, 3 * d, bs,
+                 e.eatt.as<f16>(), d, obs, nullptr, 1500, 1500, hp.n_audio_head, 0, scale};
+    launch_flash_attn(fa, nb, s);
+    proj(s, e.eatt.as<f16>(), d, w.w_o, d, w.b_o, e.ex.p, d, M, d, d, EPI_F32_RESID);
+    launch_layernorm(e.ex.as<float>(), d, w.ln2_g, w.ln2_b, e.eh.as<f16>(), d, M, d, s);
+    proj(s, e.eh.as<f16>(), d, w.w_fc1, d, w.b_fc1, e.emlp.p, 4 * d, M, 4 * d, d, EPI_F16_GELU);
+    proj(s, e.emlp.as<f16>(), 4 * d, w.w_fc2, 4 * d, w.b_fc2, e.ex.p, d, M, d, 4 * d, EPI_F32_RESID);
   }
-  launch_layernorm(m.ex.as<float>(), d, md.ln_post_g, md.ln_post_b, m.eh.as<f16>(), d, 1500, d, s);
-  // cross K/V for every decoder layer in one GEMM: [1500][L*2d]
+  launch_layernorm(e.ex.as<float>(), d, md.ln_post_g, md.ln_post_b, e.eh.as<f16>(), d, M, d, s);
+  // cross K/V for every decoder layer in one GEMM: [nb*1500][L*2d] (slots are contiguous)
   const int L = hp.n_text_layer;
-  proj(s, m.eh.as<f16>(), d, md.w_xkv, d, md.b_xkv, m.xkv.p, L * 2 * d, 1500, L * 2 * d, d, EPI_F16);
+  proj(s, e.eh.as<f16>(), d, md.w_xkv, d, md.b_xkv, xkv_out, L * 2 * d, M, L * 2 * d, d, EPI_F16);
 }
 
+// one window of the current slot's segment on the decode stream (on-demand path)
 void State::encode_window(int seek) {
   Impl& m = *m_;
-  Im2colMelArgs ia{m.mel.as<float>(), m.n_mels, m.n_fft_frames, m.gmax.as<int>(), seek, m.kp1, m.im2col.as<f16>()};
+  Impl::Slot& sl = m.slots[m.cur];
+  Im2colMelArgs ia{sl.mel.as<float>(), m.n_mels, sl.n_fft_frames, sl.gmax.as<int>(), seek, m.kp1, m.e1.im2col.as<f16>()};
   launch_im2col_mel(ia, s_);
-  encoder_body(ctx_, m, s_);
+  encoder_body(ctx_, m, m.e1, 1, const_cast<f16*>(m.xkv()), s_);
 }
 
 void State::encode_from_mel_window(const float* w) {
   Impl& m = *m_;
+  m.cur = m.S;
   std::vector<f16> col((size_t)3000 * m.kp1, (f16)0.f);
   for (int t = 0; t < 3000; ++t)
     for (int ci = 0; ci < m.n_mels; ++ci)
@@ -486,17 +566,78 @@ void State::encode_from_mel_window(const float* w) {
         const int u = t + k - 1;
         if (u >= 0 && u < 3000) col[(size_t)t * m.kp1 + ci * 3 + k] = (f16)w[(size_t)ci * 3000 + u];
       }
-  WDR_HIP(hipMemcpyAsync(m.im2col.p, col.data(), col.size() * 2, hipMemcpyHostToDevice, s_));
-  encoder_body(ctx_, m, s_);
+  WDR_HIP(hipMemcpyAsync(m.e1.im2col.p, col.data(), col.size() * 2, hipMemcpyHostToDevice, s_));
+  encoder_body(ctx_, m, m.e1, 1, const_cast<f16*>(m.xkv()), s_);
   WDR_HIP(hipStreamSynchronize(s_));
 }
 
 void State::read_encoder_out(float* out) {
   Impl& m = *m_;
   std::vector<f16> h((size_t)1500 * m.d);
-  WDR_HIP(hipMemcpyAsync(h.data(), m.eh.p, h.size() * 2, hipMemcpyDeviceToHost, s_));
+  WDR_HIP(hipMemcpyAsync(h.data(), m.e1.eh.p, h.size() * 2, hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
   for (size_t i = 0; i < h.size(); ++i) out[i] = (float)h[i];
+}
+
+// ------------------------------------------------------------------ encode-ahead
+// run_pipeline hands over the whole list of speech segments up front (the reference loops
+// over them one whisper_full call at a time, src/transcribe.rs:372-389).  The first window of
+// every segment does not depend on any decode result, so it is encoded ahead on the low-
+// priority stream in batches of kBatch windows into the cross-K/V ring; segment j waits only
+// on its slot's `ready` event, and slot j % S is reused once segment j - S has recorded `freed`.
+void State::plan(const int16_t* const* pcm, const int* n, int count) {
+  Impl& m = *m_;
+  WDR_HIP(hipStreamSynchronize(m.es));
+  m.plan.pcm.assign(pcm, pcm + count);
+  m.plan.n.assign(n, n + count);
+  m.plan.next_enq = 0;
+  top_up(0);
+}
+
+void State::unplan() {
+  Impl& m = *m_;
+  WDR_HIP(hipStreamSynchronize(m.es));
+  m.plan.pcm.clear();
+  m.plan.n.clear();
+  m.plan.next_enq = 0;
+}
+
+// enqueue every group of segments whose slots' previous occupants (j - S ...) have finished
+void State::top_up(int j) {
+  Impl& m = *m_;
+  const int N = (int)m.plan.pcm.size();
+  while ((int)m.plan.next_enq < N) {
+    const int g0 = (int)m.plan.next_enq;
+    const int g1 = std::min(N, g0 + kBatch);
+    if (g1 - 1 > j + m.S - 1) break;
+    const int slot0 = g0 % m.S;
+    for (int k = g0; k < g1; ++k) {
+      Impl::Slot& sl = m.slots[k % m.S];
+      if (k >= m.S) WDR_HIP(hipStreamWaitEvent(m.es, sl.freed, 0));
+      const int nk = m.plan.n[k];
+      if (nk > sl.pcm_cap) {
+        if (sl.h_pcm) WDR_HIP(hipHostFree(sl.h_pcm));
+        WDR_HIP(hipHostMalloc((void**)&sl.h_pcm, (size_t)std::max(nk, 1) * 2, hipHostMallocDefault));
+        sl.pcm = DevMem((size_t)std::max(nk, 1) * 2);
+        sl.pcm_cap = nk;
+      }
+      slot_reserve_x(sl, nk);
+      if (nk > 0) {
+        // the staging buffer's previous H2D copy (segment k - S) completed before its decode
+        memcpy(sl.h_pcm, m.plan.pcm[k], (size_t)nk * 2);
+        WDR_HIP(hipMemcpyAsync(sl.pcm.p, sl.h_pcm, (size_t)nk * 2, hipMemcpyHostToDevice, m.es));
+        launch_i16_to_f32(sl.pcm.as<int16_t>(), nk, sl.x.as<float>(), m.es);
+      }
+      slot_mel(ctx_, m, sl, nk, m.es);
+      Im2colMelArgs ia{sl.mel.as<float>(), m.n_mels, sl.n_fft_frames, sl.gmax.as<int>(), 0, m.kp1,
+                       m.eb.im2col.as<f16>() + (size_t)(k - g0) * 3000 * m.kp1};
+      launch_im2col_mel(ia, m.es);
+    }
+    encoder_body(ctx_, m, m.eb, g1 - g0, m.xkv_ring.as<f16>() + (size_t)slot0 * m.xkv_slot_elems, m.es);
+    for (int k = g0; k < g1; ++k) WDR_HIP(hipEventRecord(m.slots[k % m.S].ready, m.es));
+    m.plan.next_enq = g1;
+    times.windows += g1 - g0;
+  }
 }
 
 // ------------------------------------------------------------------ decoder
@@ -533,7 +674,7 @@ void State::decoder_prefill(const int* toks, int n, int seq, bool want_logits, b
     proj(s_, m.attd.as<f16>(), d, e.w_o, d, e.b_o, m.xd.p, d, n, d, d, EPI_F32_RESID);
     launch_layernorm(m.xd.as<float>(), d, e.ln2_g, e.ln2_b, m.hd.as<f16>(), d, n, d, s_);
     proj(s_, m.hd.as<f16>(), d, e.w_xq, d, e.b_xq, m.qx.p, d, n, d, d, EPI_F16);
-    const f16* xk = m.xkv.as<f16>() + (size_t)l * 2 * d;
+    const f16* xk = m.xkv() + (size_t)l * 2 * d;
     const f16* xv = xk + d;
     const bool cap_layer = capture && !ctx_.aheads_per_layer.empty() && !ctx_.aheads_per_layer[l].empty();
     if (n > NSEQ || cap_layer) {
@@ -609,7 +750,7 @@ void State::decoder_step_body(int R) {
     launch_dec_self_attn(sa, R, hp.n_text_head, s_);
     launch_proj(P(m.attd.as<f16>(), d, e.w_o, e.b_o, m.xd.p, d, d, d, EPI_F32_RESID), s_);
     launch_proj(P(nullptr, d, e.w_xq, e.b_xq, m.qx.p, d, d, d, EPI_F16, e.ln2_g, e.ln2_b), s_);
-    const f16* xk = m.xkv.as<f16>() + (size_t)l * 2 * d;
+    const f16* xk = m.xkv() + (size_t)l * 2 * d;
     XAttnArgs xa{m.qx.as<f16>(), d, xk, xk + d, ldxkv, 1500, R, hp.n_text_head, scale, m.part_o.as<float>(),
                  m.part_ml.as<float2>(), m.attd.as<f16>(), d};
     launch_xattn(xa, s_);
@@ -654,7 +795,7 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
     run_logits(R, ctl, out, nullptr);
     return;
   }
-  Impl::StepGraph& g = m.graphs[R];
+  Impl::StepGraph& g = m.graphs[R * 256 + m.cur];
   if (!g.exec || g.prof_cls != prof_class()) {
     if (g.exec) {
       (void)hipGraphExecDestroy(g.exec);
@@ -916,7 +1057,7 @@ static void score_sequence(Seq& s, const FullParams& p) {
   s.entropy = ent;
 }
 
-int State::full(const FullParams& params, const float* samples, int n) {
+int State::full(const FullParams& params, const float* samples, int n, int job) {
   WDR_HIP(hipSetDevice(ctx_.cp.gpu_device));
   Impl& m = *m_;
   const Vocab& v = ctx_.vocab;
@@ -924,12 +1065,38 @@ int State::full(const FullParams& params, const float* samples, int n) {
   WDR_CHECK(params.greedy, "beam-search decoding is not available yet: set sampling_strategy = \"greedy\"");
   result_all.clear();
   double t_start = now_s();
-  compute_mel(samples, n);
+  const bool planned = job >= 0 && job < (int)m.plan.pcm.size();
+  // the slot goes back to the encode-ahead ring once this segment's last kernel has run
+  struct Release {
+    Impl& m;
+    hipStream_t s;
+    bool on;
+    ~Release() {
+      if (on) (void)hipEventRecord(m.slots[m.cur].freed, s);
+    }
+  } release{m, s_, planned};
+  int encoded_seek = -1;
+  if (planned) {
+    top_up(job);
+    WDR_CHECK((int)m.plan.next_enq > job, "encode-ahead plan out of order");
+    m.cur = job % m.S;
+    n = m.plan.n[job];
+    WDR_HIP(hipEventSynchronize(m.slots[m.cur].ready));
+    times.encode += now_s() - t_start;   // time the decoder waited on the encode-ahead stream
+    t_start = now_s();
+    encoded_seek = 0;
+  } else {
+    compute_mel(samples, n);
+  }
   if (params.token_timestamps) {
     t_beg = t_last = tid_last = 0;
     energy.assign(n, 0.f);
     if (n > 0) {
-      launch_energy(m.x.as<float>(), n, m.energy_d.as<float>(), s_);
+      if (n > m.energy_cap) {
+        m.energy_d = DevMem((size_t)n * 4);
+        m.energy_cap = n;
+      }
+      launch_energy(m.slots[m.cur].x.as<float>(), n, m.energy_d.as<float>(), s_);
       WDR_HIP(hipMemcpyAsync(energy.data(), m.energy_d.p, (size_t)n * 4, hipMemcpyDeviceToHost, s_));
     }
   }
@@ -943,7 +1110,6 @@ int State::full(const FullParams& params, const float* samples, int n) {
   std::vector<int> prompt_past;
   if (params.has_initial_prompt && !params.initial_prompt.empty()) prompt_past = v.tokenize(params.initial_prompt);
 
-  int encoded_seek = -1;
   auto encode = [&](int seek) {
     if (encoded_seek != seek) {
       const double t = now_s();
