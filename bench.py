@@ -29,6 +29,7 @@ sys.path.insert(0, os.path.join(ROOT, "whisper-diarize-rs_amd"))
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_F16_PEAK_TFS = 2500.0  # dense f16/bf16 MFMA
+PROF_SAMPLE = 8             # csrc/prof.cpp kEvery
 
 
 def parse():
@@ -43,6 +44,21 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU oracle work (rank 0, N=1)")
     return ap.parse_args()
+
+
+def pmc_traffic(cls):
+    """HBM bytes per dispatch of the kernel class from the latest committed PMC pass
+    (profiles/rNN/pmc.json, tools/gpu_profile.sh: FETCH_SIZE x2 per the gfx950 correction +
+    WRITE_SIZE, separate rocprofv3 --pmc runs).  None if no pass has been committed."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc.json")))
+    if not files:
+        return None, None
+    c = json.load(open(files[-1]))["classes"].get(cls, {})
+    if "fetch_size_bytes_per_dispatch" not in c:
+        return None, None
+    return c["fetch_size_bytes_per_dispatch"] + c.get("write_size_bytes_per_dispatch", 0.0), \
+        os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(model, segs, budget_s):
@@ -154,7 +170,14 @@ def main():
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                     "launches": nl.value, "avg_launch_us": round(ms.value * 1e3 / nl.value, 3),
                     "bytes_per_launch": by.value / nl.value}
-        roof["kernel_share_of_step"] = round(ms.value * 1e-3 / dt, 4)
+        # 1 in PROF_SAMPLE launches of the class carries events (csrc/prof.h): scale the sampled
+        # kernel time back up for the class's share of the timed region
+        roof["sampled_1_in"] = PROF_SAMPLE
+        roof["kernel_share_of_step"] = round(PROF_SAMPLE * ms.value * 1e-3 / dt, 4)
+        tr, src = pmc_traffic(args.prof)
+        if tr is not None:
+            roof["traffic"] = round(tr)
+            roof["traffic_source"] = src
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
