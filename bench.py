@@ -128,17 +128,29 @@ def main():
     t_load = time.perf_counter() - t_load
     opts = wdr.TranscribeOptions(model=args.model, lang="auto", enable_vad=True,
                                  advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    vad = wdr.Vad(gpu_device=local)
     lib = wdr._lib.load()
     prof_cls = {"none": 0, "gemm": 1, "gemv": 2, "flash": 3, "xattn": 4}[args.prof]
 
+    def step():
+        # Silero VAD over the whole shard runs and is timed; in synthetic mode the segment list
+        # handed downstream is the generator's ground-truth spurt table (BASELINE.md §2 pin)
+        t = time.perf_counter()
+        _, vsegs = vad.get_segments(pcm, materialize=False)
+        vad_t[0] += time.perf_counter() - t
+        vad_t[1] = len(vsegs)
+        return ctx.run_pipeline(segs, opts)
+
+    vad_t = [0.0, 0]
     for _ in range(args.warmup):
-        ctx.run_pipeline(segs, opts)
+        step()
+    vad_t = [0.0, 0]
     barrier()
     lib.wdr_prof_set(prof_cls)
     t0 = time.perf_counter()
     n_out = 0
     for _ in range(args.steps):
-        out, _ = ctx.run_pipeline(segs, opts)
+        out, _ = step()
         n_out += len(out)
     barrier()
     dt = time.perf_counter() - t0
@@ -193,13 +205,15 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(dt_max * 1e3 / args.steps, 1), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f16 (f32 accumulate)", "data": "synthetic",
             "config": {"workload": "configs[2]: %s, %.0f s synthetic audio per rank (%d segments, %.0f s speech), "
-                                   "DTW on, greedy, lang auto, ground-truth spurt segmentation (VAD/diarize "
-                                   "kernels not on this path yet)" % (args.model, shard_s, len(segs), audio_s),
+                                   "DTW on, greedy, lang auto, Silero VAD run + timed, ground-truth spurt "
+                                   "segmentation downstream (synthetic pin); diarize not on this path yet" % (args.model, shard_s, len(segs), audio_s),
                        "model": args.model, "global_batch": len(segs) * world, "seq_len": 1500,
                        "parallelism": "dp%d (segment shards per rank)" % world},
             "roofline": roof, "cpu_baseline": cpu,
             "stages_s": {k: round(v, 3) for k, v in times.items() if isinstance(v, float)},
             "counts": {k: v for k, v in times.items() if isinstance(v, int)},
+            "vad": {"s_per_step": round(vad_t[0] / args.steps, 4), "segments": vad_t[1],
+                    "chunks": (pcm.size + 511) // 512, "us_per_chunk": round(vad.last_us_per_step, 3)},
             "load_s": round(t_load, 2), "segments_out": n_out // max(1, args.steps),
         }
         print(json.dumps(line), flush=True)

@@ -149,6 +149,22 @@ int wdr_vad_merge(const double* starts_cs, const double* ends_cs, size_t n_segs,
                   size_t n_samples, double* mask_out /* [2*n_segs] */, size_t* n_mask,
                   double* merged_out /* [2*n_segs] start,end seconds */, int64_t* merged_idx /* [2*n_segs] */,
                   size_t* n_merged);
+/* Silero VAD (src/vad.rs:6-85; whisper.cpp WhisperVadContext + segments_from_samples).
+ * Weights are synthetic (seeded) until the ggml loader lands; model_path may be NULL. */
+typedef struct wdr_vad wdr_vad;
+int wdr_vad_create(const char* model_path, int8_t has_gpu_device, int32_t gpu_device, wdr_vad** out);
+void wdr_vad_free(wdr_vad* v);
+/* one probability per 512-sample chunk: probs_out[ceil(n/512)]; us_per_step (nullable) = GPU
+ * time of the forward per chunk (the LSTM scan dominates) */
+int wdr_vad_probs(wdr_vad* v, const int16_t* samples, size_t n, float* probs_out, double* us_per_step);
+/* whisper.cpp whisper_vad_segments_from_probs with the reference's params (min silence 100 ms):
+ * cs_out[2*k] = start_cs, [2*k+1] = end_cs; capacity 2*n_probs */
+int wdr_vad_segments_from_probs(const float* probs, size_t n_probs, float* cs_out, size_t* n_out);
+/* vad::get_segments: raw mask (seconds, 2 per entry) + merged speech segments whose samples
+ * point into `samples` (borrowed).  Free both arrays with wdr_free. */
+int wdr_vad_get_segments(wdr_vad* v, const int16_t* samples, size_t n, double** mask_out, size_t* n_mask,
+                         wdr_speech_segment** segs_out, size_t* n_segs);
+
 int wdr_context_create(const char* model_path, const char* model_name, int8_t has_gpu_device, int32_t gpu_device,
                        int8_t use_gpu, int8_t enable_dtw, int8_t enable_flash_attn, int8_t has_num_samples,
                        uint64_t num_samples, const wdr_synthetic* syn, wdr_context** out);

@@ -151,3 +151,22 @@ def test_pipeline_matches_oracle_glue(model, audio):
     assert kinds == ["s", "p"] * len(got)
     assert [e[1] for e in events if e[0] == "p"] == [int((i + 1) / 4 * 100) for i in range(4)][:len(got)]
     assert all(e[3] == "Transcribing audio" and e[2] == 1 for e in events if e[0] == "p")
+
+
+def test_engine_transcribe_audio_with_vad(tmp_path):
+    """Engine::transcribe_audio with enable_vad: WAV -> GPU Silero VAD -> merged segments ->
+    pipeline (src/engine.rs:123-139, 169-178) equals the pieces called one by one."""
+    from oracle.pipeline import write_wav
+    pcm, _ = synth_speech(25.0, seed=4)
+    path = str(tmp_path / "a.wav")
+    write_wav(path, pcm)
+    eng = wdr.Engine(wdr.EngineConfig(), synthetic=SYN)
+    opts = wdr.TranscribeOptions(model="tiny-test", lang="en", enable_vad=True,
+                                 advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    got = eng.transcribe_audio(path, opts)
+    _, vsegs = wdr.Vad().get_segments(pcm)
+    ctx = wdr.WhisperContext("tiny-test", synthetic=SYN)
+    want, _ = ctx.run_pipeline(vsegs, opts)
+    assert len(vsegs) > 0
+    assert [(s.text, round(s.start, 6), round(s.end, 6)) for s in got] == \
+        [(s.text, round(s.start, 6), round(s.end, 6)) for s in want]

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/wdr.h"
+#include "vad.h"
 #include "whisper.h"
 
 using namespace wdr;
@@ -229,12 +230,44 @@ static SynCfg syn_of(const wdr_synthetic* s) {
   return c;
 }
 
+struct wdr_vad {
+  std::unique_ptr<VadModel> m;
+};
+
 struct wdr_engine {
   wdr_engine_config cfg{};
   std::string cache_dir, vad_path, seg_path, emb_path;
   SynCfg syn;
   std::map<std::string, std::unique_ptr<wdr_context>> contexts;
+  std::unique_ptr<VadModel> vad;
 };
+
+// src/vad.rs:6-85 on top of the GPU VAD: probabilities -> whisper.cpp segments (cs) -> the
+// crate's own merge/slice (same code as wdr_vad_merge).  Segments borrow `pcm`.
+static void vad_get_segments(VadModel& vm, const int16_t* pcm, size_t n, std::vector<std::pair<double, double>>* mask,
+                             std::vector<wdr_speech_segment>* segs) {
+  const std::vector<float> pr = vm.probs(pcm, n);
+  const std::vector<std::pair<float, float>> cs = vad_segments_from_probs(pr, VadParams());
+  mask->clear();
+  for (auto& c : cs) {
+    const double a = (double)c.first / 100.0, b = (double)c.second / 100.0;
+    if (b > a) mask->push_back({a, b});
+  }
+  std::stable_sort(mask->begin(), mask->end(), [](auto& x, auto& y) { return x.first < y.first; });
+  std::vector<std::pair<double, double>> merged;
+  for (auto& m : *mask) {
+    if (!merged.empty() && m.first - merged.back().second < 0.200) merged.back().second = std::max(m.second, merged.back().second);
+    else merged.push_back(m);
+  }
+  const float SR = 16000.0f, nf = (float)n;
+  segs->clear();
+  for (auto& m : merged) {
+    const size_t si = (size_t)std::min(std::max(std::round((float)m.first * SR), 0.0f), nf);
+    const size_t ei = (size_t)std::min(std::max(std::round((float)m.second * SR), 0.0f), nf);
+    if (!(m.second > m.first) || !(ei > si)) continue;
+    segs->push_back({m.first, m.second, pcm + si, ei - si});
+  }
+}
 
 // src/transcribe.rs:20-87
 static FullParams setup_params(const wdr_transcribe_options* o, const SynCfg& syn) {
@@ -522,9 +555,15 @@ int wdr_transcribe_audio(wdr_engine* e, const char* audio_path, const wdr_transc
     std::vector<int16_t> pcm = read_wav_impl(audio_path);
     std::vector<wdr_speech_segment> segs;
     if (o && o->enable_diarize == 1) return fail("diarization is not available on this path yet");
-    const bool vad = !o || o->enable_vad != 0;   // default Some(true)
-    if (vad) return fail("Silero VAD is not available on this path yet (set enable_vad = false)");
-    segs.push_back({0.0, (double)pcm.size() / 16000.0, pcm.data(), pcm.size()});
+    const bool vad = !o || o->enable_vad == 1;   // `if let Some(true) = options.enable_vad` (src/engine.rs:123)
+    if (vad) {
+      if (!e->vad) e->vad = std::make_unique<VadModel>(e->cfg.has_gpu_device ? e->cfg.gpu_device : 0);
+      std::vector<std::pair<double, double>> mask;
+      vad_get_segments(*e->vad, pcm.data(), pcm.size(), &mask, &segs);
+    } else {
+      // whole file as one segment (src/engine.rs:141-147)
+      segs.push_back({0.0, (double)pcm.size() / 16000.0, pcm.data(), pcm.size()});
+    }
     auto it = e->contexts.find(model);
     if (it == e->contexts.end()) {
       it = e->contexts.emplace(model, make_context(model, e->cfg.has_gpu_device, e->cfg.gpu_device, e->cfg.use_gpu,
@@ -536,6 +575,59 @@ int wdr_transcribe_audio(wdr_engine* e, const char* audio_path, const wdr_transc
     bool has_lang = false;
     std::vector<Seg> res = run_pipeline(it->second.get(), segs, o, e->syn, cb, &lang, &has_lang);
     *out = to_list(res, has_lang ? &lang : nullptr);
+    return 0;
+  })
+}
+
+int wdr_vad_create(const char* model_path, int8_t has_gpu_device, int32_t gpu_device, wdr_vad** out) {
+  (void)model_path;   // synthetic weights (the ggml loader is SURVEY §8(f) row 2)
+  WDR_GUARD({
+    auto v = std::make_unique<wdr_vad>();
+    v->m = std::make_unique<VadModel>(has_gpu_device ? gpu_device : 0);
+    *out = v.release();
+    return 0;
+  })
+}
+
+void wdr_vad_free(wdr_vad* v) { delete v; }
+
+int wdr_vad_probs(wdr_vad* v, const int16_t* samples, size_t n, float* probs_out, double* us_per_step) {
+  WDR_GUARD({
+    const std::vector<float> p = v->m->probs(samples, n);
+    if (!p.empty()) memcpy(probs_out, p.data(), p.size() * 4);
+    if (us_per_step) *us_per_step = v->m->last_scan_us_per_step;
+    return 0;
+  })
+}
+
+int wdr_vad_segments_from_probs(const float* probs, size_t n_probs, float* cs_out, size_t* n_out) {
+  WDR_GUARD({
+    const std::vector<std::pair<float, float>> cs =
+        vad_segments_from_probs(std::vector<float>(probs, probs + n_probs), VadParams());
+    for (size_t i = 0; i < cs.size(); ++i) {
+      cs_out[2 * i] = cs[i].first;
+      cs_out[2 * i + 1] = cs[i].second;
+    }
+    *n_out = cs.size();
+    return 0;
+  })
+}
+
+int wdr_vad_get_segments(wdr_vad* v, const int16_t* samples, size_t n, double** mask_out, size_t* n_mask,
+                         wdr_speech_segment** segs_out, size_t* n_segs) {
+  WDR_GUARD({
+    std::vector<std::pair<double, double>> mask;
+    std::vector<wdr_speech_segment> segs;
+    vad_get_segments(*v->m, samples, n, &mask, &segs);
+    *mask_out = (double*)malloc(std::max<size_t>(1, mask.size()) * 2 * sizeof(double));
+    for (size_t i = 0; i < mask.size(); ++i) {
+      (*mask_out)[2 * i] = mask[i].first;
+      (*mask_out)[2 * i + 1] = mask[i].second;
+    }
+    *n_mask = mask.size();
+    *segs_out = (wdr_speech_segment*)malloc(std::max<size_t>(1, segs.size()) * sizeof(wdr_speech_segment));
+    if (!segs.empty()) memcpy(*segs_out, segs.data(), segs.size() * sizeof(wdr_speech_segment));
+    *n_segs = segs.size();
     return 0;
   })
 }

@@ -112,4 +112,18 @@ struct CaptureArgs {
 };
 void launch_aheads_capture(const CaptureArgs& a, int n_sel, hipStream_t s);
 
+// Silero VAD (kernels/vad.hip); layouts [out][in*k] f16, biases f32
+struct VadWeights {
+  const f16* stft;                  // [258][256]
+  const f16* c0w; const float* c0b; // [128][129*3]
+  const f16* c1w; const float* c1b; // [64][128*3]
+  const f16* c2w; const float* c2b; // [64][64*3]
+  const f16* c3w; const float* c3b; // [128][64*3]
+  const f16* wih; const float* bih; // [512][128]
+  const f16* whh; const float* bhh; // [512][128]
+  const f16* wo;  const float* bo;  // [128], [1]
+};
+void launch_vad(const float* x, long long n, const VadWeights& w, float* xg, float* hout, float* probs,
+                hipStream_t s);
+
 }  // namespace wdr

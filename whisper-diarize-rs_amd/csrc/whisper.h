@@ -18,6 +18,8 @@
 
 namespace wdr {
 
+uint64_t fnv1a64(const std::string& s);   // synthetic-weight seed of a tensor name
+
 struct HParams {
   int n_vocab = 51864, n_audio_ctx = 1500, n_audio_state = 512, n_audio_head = 8, n_audio_layer = 6;
   int n_text_ctx = 448, n_text_state = 512, n_text_head = 8, n_text_layer = 6, n_mels = 80;

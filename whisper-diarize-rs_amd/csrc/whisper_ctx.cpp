@@ -102,7 +102,7 @@ DevMem& DevMem::operator=(DevMem&& o) noexcept {
   return *this;
 }
 
-static uint64_t fnv1a64(const std::string& s) {
+uint64_t fnv1a64(const std::string& s) {
   uint64_t h = 0xCBF29CE484222325ull;
   for (unsigned char c : s) {
     h ^= c;

@@ -230,6 +230,73 @@ def vad_merge(segs_cs, samples: np.ndarray):
     return m, out
 
 
+def vad_segments_from_probs(probs) -> list:
+    """whisper.cpp whisper_vad_segments_from_probs with the reference's VAD params
+    (src/vad.rs:21-22): [(start_cs, end_cs)] as f32 values."""
+    lib = L.load()
+    p = np.ascontiguousarray(probs, np.float32)
+    out = np.zeros(2 * max(1, p.size), np.float32)
+    n = C.c_size_t()
+    L.check(lib.wdr_vad_segments_from_probs(p.ctypes.data_as(C.POINTER(C.c_float)), p.size,
+                                            out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(n)))
+    return [(float(out[2 * i]), float(out[2 * i + 1])) for i in range(n.value)]
+
+
+class Vad:
+    """Silero VAD on the GPU (src/vad.rs:6-85).  Synthetic seeded weights."""
+
+    def __init__(self, model_path: Optional[str] = None, gpu_device: Optional[int] = None):
+        self._lib = L.load()
+        h = C.c_void_p()
+        L.check(self._lib.wdr_vad_create(_s(model_path), 0 if gpu_device is None else 1, gpu_device or 0, C.byref(h)))
+        self.h = h
+        self.last_us_per_step = 0.0
+
+    def probs(self, samples: np.ndarray) -> np.ndarray:
+        smp = np.ascontiguousarray(samples, np.int16)
+        out = np.zeros((smp.size + 511) // 512, np.float32)
+        us = C.c_double()
+        L.check(self._lib.wdr_vad_probs(self.h, smp.ctypes.data_as(C.POINTER(C.c_int16)), smp.size,
+                                        out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(us)))
+        self.last_us_per_step = us.value
+        return out
+
+    def get_segments(self, samples: np.ndarray, materialize: bool = True):
+        """-> (mask [(start_s, end_s)], [SpeechSegment]) exactly as vad::get_segments.
+        materialize=False returns only the segment (start, end) pairs (no sample copies)."""
+        smp = np.ascontiguousarray(samples, np.int16)
+        mp, nm = C.POINTER(C.c_double)(), C.c_size_t()
+        sp, ns = C.POINTER(L.SpeechSegment)(), C.c_size_t()
+        L.check(self._lib.wdr_vad_get_segments(self.h, smp.ctypes.data_as(C.POINTER(C.c_int16)), smp.size,
+                                               C.byref(mp), C.byref(nm), C.byref(sp), C.byref(ns)))
+        try:
+            mask = [(mp[2 * i], mp[2 * i + 1]) for i in range(nm.value)]
+            base = smp.ctypes.data
+            segs = []
+            for i in range(ns.value):
+                s = sp[i]
+                if not materialize:
+                    segs.append((s.start, s.end))
+                    continue
+                off = (C.cast(s.samples, C.c_void_p).value - base) // 2
+                segs.append(SpeechSegment(s.start, s.end, smp[off:off + s.n_samples].copy()))
+        finally:
+            self._lib.wdr_free(C.cast(mp, C.c_void_p))
+            self._lib.wdr_free(C.cast(sp, C.c_void_p))
+        return mask, segs
+
+    def close(self):
+        if self.h:
+            self._lib.wdr_vad_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class WhisperContext:
     """transcribe::create_context (src/transcribe.rs:89-166) + its whisper_state."""
 

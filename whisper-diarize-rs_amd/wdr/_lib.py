@@ -97,6 +97,11 @@ _SIGS = {
     "wdr_read_wav": (C.c_int, [cstr, P(P(C.c_int16)), P(sz)]),
     "wdr_free": (None, [vp]),
     "wdr_vad_merge": (C.c_int, [P(f64), P(f64), sz, P(C.c_int16), sz, P(f64), P(sz), P(f64), P(i64), P(sz)]),
+    "wdr_vad_create": (C.c_int, [cstr, i8, i32, P(vp)]),
+    "wdr_vad_free": (None, [vp]),
+    "wdr_vad_probs": (C.c_int, [vp, P(C.c_int16), sz, P(f32), P(f64)]),
+    "wdr_vad_segments_from_probs": (C.c_int, [P(f32), sz, P(f32), P(sz)]),
+    "wdr_vad_get_segments": (C.c_int, [vp, P(C.c_int16), sz, P(P(f64)), P(sz), P(P(SpeechSegment)), P(sz)]),
     "wdr_context_create": (C.c_int, [cstr, cstr, i8, i32, i8, i8, i8, i8, u64, P(Synthetic), P(vp)]),
     "wdr_context_free": (None, [vp]),
     "wdr_run_pipeline": (C.c_int, [vp, P(SpeechSegment), sz, P(TranscribeOptions), P(Synthetic), P(Callbacks),
