@@ -157,6 +157,8 @@ void wdr_vad_free(wdr_vad* v);
 /* one probability per 512-sample chunk: probs_out[ceil(n/512)]; us_per_step (nullable) = GPU
  * time of the forward per chunk (the LSTM scan dominates) */
 int wdr_vad_probs(wdr_vad* v, const int16_t* samples, size_t n, float* probs_out, double* us_per_step);
+/* GPU time of the last forward per 512-sample chunk (microseconds) */
+int wdr_vad_stats(wdr_vad* v, double* us_per_chunk);
 /* whisper.cpp whisper_vad_segments_from_probs with the reference's params (min silence 100 ms):
  * cs_out[2*k] = start_cs, [2*k+1] = end_cs; capacity 2*n_probs */
 int wdr_vad_segments_from_probs(const float* probs, size_t n_probs, float* cs_out, size_t* n_out);
@@ -164,6 +166,34 @@ int wdr_vad_segments_from_probs(const float* probs, size_t n_probs, float* cs_ou
  * point into `samples` (borrowed).  Free both arrays with wdr_free. */
 int wdr_vad_get_segments(wdr_vad* v, const int16_t* samples, size_t n, double** mask_out, size_t* n_mask,
                          wdr_speech_segment** segs_out, size_t* n_segs);
+
+/* pyannote diarization (src/engine.rs:89-122, src/transcribe.rs:339-345, 461-497):
+ * segmentation-3.0 + get_segments stitching, Kaldi fbank + CMN, CAM++ embedding.
+ * Weights are synthetic (seeded) until the ONNX initializer reader lands; paths may be NULL. */
+typedef struct wdr_diarizer wdr_diarizer;
+int wdr_diarizer_create(const char* segment_model_path, const char* embedding_model_path, int8_t has_gpu_device,
+                        int32_t gpu_device, wdr_diarizer** out);
+void wdr_diarizer_free(wdr_diarizer* d);
+/* per-frame argmax class of every 10-s window of the zero-padded input (pyannote-rs
+ * find_max_index: last max): cls_out[n_windows * 589], n_windows = n / 160000 + 1;
+ * logprobs_out (nullable) [n_windows][589][7] */
+int wdr_diarize_frame_classes(wdr_diarizer* d, const int16_t* samples, size_t n, int32_t* cls_out, float* logprobs_out);
+/* pyannote_rs::get_segments: one allocation holding the segments and copies of their samples
+ * (slices of the zero-padded buffer); free with wdr_free(*segs_out) */
+int wdr_diarize_get_segments(wdr_diarizer* d, const int16_t* samples, size_t n, wdr_speech_segment** segs_out,
+                             size_t* n_segs);
+/* EmbeddingExtractor::compute pieces: features after CMN [T][80] (capacity n/160 + 1 rows), and
+ * the 512-d embedding; ok = 0 where the reference's ONNX call fails (fewer than 400 samples) */
+int wdr_diarize_fbank(wdr_diarizer* d, const int16_t* samples, size_t n, float* feats_out, size_t* n_frames);
+int wdr_diarize_embedding(wdr_diarizer* d, const int16_t* samples, size_t n, float* emb_out, int8_t* ok);
+/* GPU time of the last segmentation / embedding call (ms) */
+int wdr_diarize_stats(wdr_diarizer* d, double* seg_ms, double* emb_ms);
+/* EmbeddingManager + the reference's choice of get_best_speaker_match / search_speaker
+ * (src/transcribe.rs:478-497); emb NULL -> "?" (embedding error) */
+typedef struct wdr_speakers wdr_speakers;
+int wdr_speakers_new(int8_t has_max_speakers, uint64_t max_speakers, wdr_speakers** out);
+void wdr_speakers_free(wdr_speakers* m);
+int wdr_speakers_assign(wdr_speakers* m, const float* emb, int32_t dim, float threshold, char* id_out, size_t cap);
 
 int wdr_context_create(const char* model_path, const char* model_name, int8_t has_gpu_device, int32_t gpu_device,
                        int8_t use_gpu, int8_t enable_dtw, int8_t enable_flash_attn, int8_t has_num_samples,

@@ -9,6 +9,10 @@ reference's own whisper.cpp / ggml sources are not in the container, SURVEY.md
   dtw_cases.npz     transformers ... generation_whisper._dynamic_time_warping,
                     incl. integer-valued matrices full of ties
   medfilt.npz       transformers ... generation_whisper._median_filter (width 7, reflect)
+  kaldi_fbank.npz   transformers.audio_utils.spectrogram with Kaldi settings (povey, 0.97,
+                    DC removal, 512-pt, kaldi mel 20..8000 Hz, log, FLT_EPSILON floor)
+  pyannote_seg.npz  segmentation-3.0 structure in torch ops (nn.LSTM etc.), oracle weights
+  campplus.npz      CAM++ structure in torch ops (conv2d strides, avg_pool1d ceil_mode), oracle weights
   whisper_tiny.npz  WhisperModel (eager attention, activation 'gelu_new') loaded with the
                     synthetic 'tiny-test' weights: encoder output rows and decoder logits
 
@@ -146,7 +150,93 @@ def main():
                         enc_rows=enc[::25], enc_sum=np.float64(enc.astype(np.float64).sum()),
                         logits_last=logits[-1].astype(np.float32), logits_top=np.argsort(-logits, axis=1)[:, :20],
                         cross_last=cross[-1].astype(np.float32))
+    diarize_golden(np.random.default_rng(77))
     print("golden fixtures written to", HERE)
+
+
+def diarize_golden(rng):
+    """kaldi_fbank.npz / pyannote_seg.npz / campplus.npz: the diarization rows' generic math
+    computed with transformers' Kaldi-compatible spectrogram and torch modules assembled with
+    the oracle's synthetic weights (torch op semantics: InstanceNorm1d, MaxPool1d, the
+    bidirectional nn.LSTM stack, Conv2d strides, avg_pool1d(ceil_mode) segment pooling,
+    unbiased std) -- pins oracle/diarize.py against independent implementations."""
+    import torch
+    import torch.nn.functional as F
+    from transformers.audio_utils import mel_filter_bank, spectrogram, window_function
+    from oracle import diarize as D
+
+    # ---- Kaldi fbank (SeamlessM4T / kaldi-compatible settings of transformers.audio_utils)
+    x = (rng.standard_normal(16000 + 337) * 0.1).astype(np.float32)
+    x += 0.3 * np.sin(2 * np.pi * 440 * np.arange(x.size) / 16000).astype(np.float32)
+    mel = mel_filter_bank(num_frequency_bins=257, num_mel_filters=80, min_frequency=20, max_frequency=8000,
+                          sampling_rate=16000, norm=None, mel_scale="kaldi", triangularize_in_mel_space=True)
+    fb = spectrogram(x, window_function(400, "povey", periodic=False), frame_length=400, hop_length=160,
+                     fft_length=512, power=2.0, center=False, preemphasis=0.97, mel_filters=mel, log_mel="log",
+                     mel_floor=1.192092955078125e-07, remove_dc_offset=True).T
+    np.savez_compressed(os.path.join(HERE, "kaldi_fbank.npz"), x=x, fbank=fb.astype(np.float32))
+
+    torch.set_grad_enabled(False)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a))
+    # ---- segmentation-3.0 with torch modules
+    W = D.seg_weights()
+    win = np.zeros(160000, np.float32)
+    pcm = (rng.standard_normal(120000) * 3000).astype(np.int16).astype(np.float32)
+    win[:120000] = pcm
+    def inorm(x, g, b):
+        m = torch.nn.InstanceNorm1d(x.shape[1], affine=True)
+        m.weight.copy_(T(g)); m.bias.copy_(T(b))
+        return m(x)
+    h = inorm(T(win)[None, None], W["wav_norm.weight"], W["wav_norm.bias"])
+    h = torch.abs(F.conv1d(h, T(W["sinc.weight"]), stride=10))
+    h = F.leaky_relu(inorm(F.max_pool1d(h, 3, 3), W["norm0.weight"], W["norm0.bias"]))
+    h = F.conv1d(h, T(W["conv1.weight"]), T(W["conv1.bias"]))
+    h = F.leaky_relu(inorm(F.max_pool1d(h, 3, 3), W["norm1.weight"], W["norm1.bias"]))
+    h = F.conv1d(h, T(W["conv2.weight"]), T(W["conv2.bias"]))
+    h = F.leaky_relu(inorm(F.max_pool1d(h, 3, 3), W["norm2.weight"], W["norm2.bias"]))
+    lstm = torch.nn.LSTM(60, 128, num_layers=4, bidirectional=True, batch_first=True)
+    for k, v in lstm.named_parameters():
+        v.copy_(T(W["lstm." + k]))
+    h, _ = lstm(h.transpose(1, 2))
+    h = F.leaky_relu(F.linear(h, T(W["linear0.weight"]), T(W["linear0.bias"])))
+    h = F.leaky_relu(F.linear(h, T(W["linear1.weight"]), T(W["linear1.bias"])))
+    lp = torch.log_softmax(F.linear(h, T(W["classifier.weight"]), T(W["classifier.bias"])), -1)[0]
+    np.savez_compressed(os.path.join(HERE, "pyannote_seg.npz"), win=win.astype(np.int16), logprobs=lp.numpy())
+
+    # ---- CAM++ (wespeaker CAMPPlus structure) with torch ops
+    CW = D.cam_weights()
+    feats = (rng.standard_normal((237, 80)) * 2.0).astype(np.float32)
+    bn = lambda x, n, dim=1: x * T(CW[n + ".scale"]).view(*([1] * dim), -1, *([1] * (x.dim() - dim - 1))) + \
+        T(CW[n + ".shift"]).view(*([1] * dim), -1, *([1] * (x.dim() - dim - 1)))
+    x = T(feats).T[None, None]                                     # [1][1][80][T]
+    out = F.relu(bn(F.conv2d(x, T(CW["head.conv1"]), padding=1), "head.bn1"))
+    for L in (1, 2):
+        for b in range(2):
+            p = "head.layer%d.%d" % (L, b)
+            st = 2 if b == 0 else 1
+            y = F.relu(bn(F.conv2d(out, T(CW[p + ".conv1"]), stride=(st, 1), padding=1), p + ".bn1"))
+            y = bn(F.conv2d(y, T(CW[p + ".conv2"]), padding=1), p + ".bn2")
+            sc = bn(F.conv2d(out, T(CW[p + ".shortcut"]), stride=(2, 1)), p + ".shortcut_bn") if b == 0 else out
+            out = F.relu(y + sc)
+    out = F.relu(bn(F.conv2d(out, T(CW["head.conv2"]), stride=(2, 1), padding=1), "head.bn2"))
+    x = out.reshape(1, -1, out.shape[-1])
+    x = F.relu(bn(F.conv1d(x, T(CW["tdnn.linear"]), stride=2, padding=2), "tdnn.bn"))
+    for bi, (nl, k, dil) in enumerate(D.CAM_BLOCKS):
+        for li in range(nl):
+            p = "block%d.%d" % (bi + 1, li)
+            hh = F.relu(bn(F.conv1d(F.relu(bn(x, p + ".bn1")), T(CW[p + ".linear1"])), p + ".bn2"))
+            y = F.conv1d(hh, T(CW[p + ".local"]), padding=(k - 1) // 2 * dil, dilation=dil)
+            seg = F.avg_pool1d(hh, kernel_size=100, stride=100, ceil_mode=True)
+            seg = seg.unsqueeze(-1).expand(*seg.shape, 100).reshape(*seg.shape[:-1], -1)[..., :hh.shape[-1]]
+            c = hh.mean(-1, keepdim=True) + seg
+            c = F.relu(F.conv1d(c, T(CW[p + ".cam1.weight"]), T(CW[p + ".cam1.bias"])))
+            m = torch.sigmoid(F.conv1d(c, T(CW[p + ".cam2.weight"]), T(CW[p + ".cam2.bias"])))
+            x = torch.cat([x, y * m], 1)
+        x = F.conv1d(F.relu(bn(x, "transit%d.bn" % (bi + 1))), T(CW["transit%d.linear" % (bi + 1)]))
+    x = F.relu(bn(x, "out.bn"))
+    stats = torch.cat([x.mean(-1), x.std(-1, unbiased=True)], -1)
+    emb = F.conv1d(stats.unsqueeze(-1), T(CW["dense.linear"])).squeeze(-1)
+    emb = emb * T(CW["dense.bn.scale"]) + T(CW["dense.bn.shift"])
+    np.savez_compressed(os.path.join(HERE, "campplus.npz"), feats=feats, emb=emb[0].numpy())
 
 
 if __name__ == "__main__":

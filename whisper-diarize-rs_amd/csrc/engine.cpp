@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/wdr.h"
+#include "diarize.h"
 #include "vad.h"
 #include "whisper.h"
 
@@ -211,7 +212,9 @@ static std::vector<Word> interpolate_word_timestamps(const std::string& line, do
 struct wdr_context {
   std::unique_ptr<Context> ctx;
   std::unique_ptr<State> st;
+  std::unique_ptr<CamModel> cam;   // EmbeddingExtractor, created on the first diarized run
   double load_s = 0;
+  double embed_s = 0;              // host wall time spent in speaker embeddings
 };
 
 struct SynCfg {
@@ -234,12 +237,37 @@ struct wdr_vad {
   std::unique_ptr<VadModel> m;
 };
 
+struct wdr_diarizer {
+  int device = 0;
+  std::unique_ptr<SegModel> seg;
+  std::unique_ptr<CamModel> cam;
+  SegModel& S() {
+    if (!seg) seg = std::make_unique<SegModel>(device);
+    return *seg;
+  }
+  CamModel& E() {
+    if (!cam) cam = std::make_unique<CamModel>(device);
+    return *cam;
+  }
+};
+
+struct wdr_speakers {
+  std::unique_ptr<SpeakerManager> m;
+};
+
+// DiarizeOptions (src/engine.rs:103-111): threshold default 0.5, max_speakers None/0 -> usize::MAX
+static void diarize_options(const wdr_transcribe_options* o, float* thr, uint64_t* max_spk) {
+  *thr = (o && o->advanced && o->advanced->has_diarize_threshold) ? o->advanced->diarize_threshold : 0.5f;
+  *max_spk = (o && o->has_max_speakers && o->max_speakers != 0) ? o->max_speakers : UINT64_MAX;
+}
+
 struct wdr_engine {
   wdr_engine_config cfg{};
   std::string cache_dir, vad_path, seg_path, emb_path;
   SynCfg syn;
   std::map<std::string, std::unique_ptr<wdr_context>> contexts;
   std::unique_ptr<VadModel> vad;
+  std::unique_ptr<SegModel> seg;
 };
 
 // src/vad.rs:6-85 on top of the GPU VAD: probabilities -> whisper.cpp segments (cs) -> the
@@ -375,7 +403,12 @@ static void emit_segment(const wdr_callbacks* cb, const Seg& s) {
 static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speech_segment>& segs,
                                      const wdr_transcribe_options* o, const SynCfg& syn, const wdr_callbacks* cb,
                                      std::string* detected_lang, bool* has_lang) {
-  if (o && o->enable_diarize == 1) throw std::runtime_error("diarization is not available on this path yet");
+  const bool diarize = o && o->enable_diarize == 1;
+  float dthr = 0.5f;
+  uint64_t dmax = UINT64_MAX;
+  diarize_options(o, &dthr, &dmax);
+  SpeakerManager speakers(dmax);
+  if (diarize && !c->cam) c->cam = std::make_unique<CamModel>(c->ctx->cp.gpu_device);
   FullParams params = setup_params(o, syn);
   const Vocab& v = c->ctx->vocab;
   const double user_offset = (o && o->has_offset) ? o->offset : 0.0;
@@ -428,6 +461,8 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
       *has_lang = true;
     }
     const double base_offset = ss.start + user_offset;
+    std::vector<float> emb(512);
+    bool have_emb = false, emb_ok = false;
     for (const ResultSeg& r : c->st->result_all) {
       std::string text = trim_start(r.text);
       const double approx_start = base_offset + cs_to_s(r.t0);
@@ -457,6 +492,18 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
       s.text = text;
       s.has_words = !words.empty();
       s.words = std::move(words);
+      if (diarize) {
+        // src/transcribe.rs:461-497: embed the whole speech segment (recomputed per whisper
+        // segment in the reference; identical input -> computed once here), then assign
+        if (!have_emb) {
+          const double te = now_s();
+          emb_ok = c->cam->embed(ss.samples, ss.n_samples, emb.data());
+          c->embed_s += now_s() - te;
+          have_emb = true;
+        }
+        s.has_speaker = true;
+        s.speaker = speakers.assign(emb_ok ? emb.data() : nullptr, 512, dthr);
+      }
       emit_segment(cb, s);
       if (cb && cb->progress) {
         const int pct = (int)((double)(i + 1) / (double)segs.size() * 100.0);
@@ -554,9 +601,16 @@ int wdr_transcribe_audio(wdr_engine* e, const char* audio_path, const wdr_transc
     const std::string model = (o && o->model) ? o->model : "base";
     std::vector<int16_t> pcm = read_wav_impl(audio_path);
     std::vector<wdr_speech_segment> segs;
-    if (o && o->enable_diarize == 1) return fail("diarization is not available on this path yet");
+    std::vector<int16_t> dpad;   // owns the samples of pyannote segments (they index the padded buffer)
     const bool vad = !o || o->enable_vad == 1;   // `if let Some(true) = options.enable_vad` (src/engine.rs:123)
-    if (vad) {
+    if (o && o->enable_diarize == 1) {
+      // src/engine.rs:89-122: pyannote segmentation -> SpeechSegments
+      if (!e->seg) e->seg = std::make_unique<SegModel>(e->cfg.has_gpu_device ? e->cfg.gpu_device : 0);
+      const std::vector<DiarSegment> ds = e->seg->get_segments(pcm.data(), pcm.size());
+      dpad.assign(pcm.begin(), pcm.end());
+      dpad.resize(pcm.size() + (160000 - pcm.size() % 160000), 0);
+      for (const DiarSegment& d : ds) segs.push_back({d.start, d.end, dpad.data() + d.start_idx, d.end_idx - d.start_idx});
+    } else if (vad) {
       if (!e->vad) e->vad = std::make_unique<VadModel>(e->cfg.has_gpu_device ? e->cfg.gpu_device : 0);
       std::vector<std::pair<double, double>> mask;
       vad_get_segments(*e->vad, pcm.data(), pcm.size(), &mask, &segs);
@@ -600,6 +654,13 @@ int wdr_vad_probs(wdr_vad* v, const int16_t* samples, size_t n, float* probs_out
   })
 }
 
+int wdr_vad_stats(wdr_vad* v, double* us_per_chunk) {
+  WDR_GUARD({
+    *us_per_chunk = v->m->last_scan_us_per_step;
+    return 0;
+  })
+}
+
 int wdr_vad_segments_from_probs(const float* probs, size_t n_probs, float* cs_out, size_t* n_out) {
   WDR_GUARD({
     const std::vector<std::pair<float, float>> cs =
@@ -628,6 +689,100 @@ int wdr_vad_get_segments(wdr_vad* v, const int16_t* samples, size_t n, double** 
     *segs_out = (wdr_speech_segment*)malloc(std::max<size_t>(1, segs.size()) * sizeof(wdr_speech_segment));
     if (!segs.empty()) memcpy(*segs_out, segs.data(), segs.size() * sizeof(wdr_speech_segment));
     *n_segs = segs.size();
+    return 0;
+  })
+}
+
+int wdr_diarizer_create(const char* segment_model_path, const char* embedding_model_path, int8_t has_gpu_device,
+                        int32_t gpu_device, wdr_diarizer** out) {
+  (void)segment_model_path;   // synthetic weights (the ONNX initializer reader is SURVEY §8(f) row 3)
+  (void)embedding_model_path;
+  WDR_GUARD({
+    auto d = std::make_unique<wdr_diarizer>();
+    d->device = has_gpu_device ? gpu_device : 0;
+    *out = d.release();
+    return 0;
+  })
+}
+
+void wdr_diarizer_free(wdr_diarizer* d) { delete d; }
+
+int wdr_diarize_frame_classes(wdr_diarizer* d, const int16_t* samples, size_t n, int32_t* cls_out, float* logprobs_out) {
+  WDR_GUARD({
+    std::vector<float> lp;
+    const std::vector<int> cls = d->S().frame_classes(samples, n, logprobs_out ? &lp : nullptr);
+    for (size_t i = 0; i < cls.size(); ++i) cls_out[i] = cls[i];
+    if (logprobs_out && !lp.empty()) memcpy(logprobs_out, lp.data(), lp.size() * 4);
+    return 0;
+  })
+}
+
+int wdr_diarize_get_segments(wdr_diarizer* d, const int16_t* samples, size_t n, wdr_speech_segment** segs_out,
+                             size_t* n_segs) {
+  WDR_GUARD({
+    const std::vector<DiarSegment> ds = d->S().get_segments(samples, n);
+    size_t tot = 0;
+    for (auto& x : ds) tot += x.end_idx - x.start_idx;
+    // one allocation: the segment array followed by copies of their (zero-padded) samples
+    const size_t head = std::max<size_t>(1, ds.size()) * sizeof(wdr_speech_segment);
+    char* blk = (char*)malloc(head + std::max<size_t>(1, tot) * 2);
+    wdr_speech_segment* sg = (wdr_speech_segment*)blk;
+    int16_t* dst = (int16_t*)(blk + head);
+    for (size_t i = 0; i < ds.size(); ++i) {
+      const size_t len = ds[i].end_idx - ds[i].start_idx;
+      for (size_t k = 0; k < len; ++k) {
+        const size_t src = ds[i].start_idx + k;
+        dst[k] = src < n ? samples[src] : 0;
+      }
+      sg[i] = {ds[i].start, ds[i].end, dst, len};
+      dst += len;
+    }
+    *segs_out = sg;
+    *n_segs = ds.size();
+    return 0;
+  })
+}
+
+int wdr_diarize_fbank(wdr_diarizer* d, const int16_t* samples, size_t n, float* feats_out, size_t* n_frames) {
+  WDR_GUARD({
+    const std::vector<float> f = d->E().feats(samples, n);
+    if (!f.empty()) memcpy(feats_out, f.data(), f.size() * 4);
+    *n_frames = f.size() / 80;
+    return 0;
+  })
+}
+
+int wdr_diarize_embedding(wdr_diarizer* d, const int16_t* samples, size_t n, float* emb_out, int8_t* ok) {
+  WDR_GUARD({
+    *ok = d->E().embed(samples, n, emb_out) ? 1 : 0;
+    return 0;
+  })
+}
+
+int wdr_diarize_stats(wdr_diarizer* d, double* seg_ms, double* emb_ms) {
+  WDR_GUARD({
+    *seg_ms = d->seg ? d->seg->last_ms : 0.0;
+    *emb_ms = d->cam ? d->cam->last_ms : 0.0;
+    return 0;
+  })
+}
+
+int wdr_speakers_new(int8_t has_max_speakers, uint64_t max_speakers, wdr_speakers** out) {
+  WDR_GUARD({
+    auto m = std::make_unique<wdr_speakers>();
+    m->m = std::make_unique<SpeakerManager>((has_max_speakers && max_speakers != 0) ? max_speakers : UINT64_MAX);
+    *out = m.release();
+    return 0;
+  })
+}
+
+void wdr_speakers_free(wdr_speakers* m) { delete m; }
+
+int wdr_speakers_assign(wdr_speakers* m, const float* emb, int32_t dim, float threshold, char* id_out, size_t cap) {
+  WDR_GUARD({
+    const std::string id = m->m->assign(emb, dim, threshold);
+    WDR_CHECK(cap > id.size(), "speaker id buffer too small");
+    memcpy(id_out, id.c_str(), id.size() + 1);
     return 0;
   })
 }

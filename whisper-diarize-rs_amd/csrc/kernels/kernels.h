@@ -126,4 +126,36 @@ struct VadWeights {
 void launch_vad(const float* x, long long n, const VadWeights& w, float* xg, float* hout, float* probs,
                 hipStream_t s);
 
+// Diarization (kernels/diar.hip), all f32
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_SIGMOID = 3, ACT_ABS = 4 };
+struct Gemm32Args {
+  const float* A; int lda;           // [M][K]
+  const float* B; int ldb;           // [N][K] (torch [out][in...] layout)
+  float* C; int ldc;                 // [M][N]
+  int M, N, K;
+  const float* bias = nullptr;       // [N]
+  const float* scale = nullptr;      // [N] affine after bias (inference BatchNorm)
+  const float* shift = nullptr;
+  const float* pro_scale = nullptr;  // [K] prologue: A' = relu(A * s + b) (BN-ReLU before a linear)
+  const float* pro_shift = nullptr;
+  int act = ACT_NONE;
+  int accum = 0;                     // C = act(v + C_old)
+};
+void launch_gemm32(const Gemm32Args& a, hipStream_t s);
+void launch_im2col_1d(const float* X, int ldx, int T, int C, int k, int stride, int dil, int pad, int To, float* col,
+                      hipStream_t s);
+void launch_im2col_2d(const float* X, int T, int F, int C, int kf, int kt, int sf, int Fo, float* col, hipStream_t s);
+void launch_maxpool3(const float* x, long long bs, int T, int C, int B, float* y, long long ybs, hipStream_t s);
+void launch_inorm(float* y, long long bs, int T, int C, int B, const float* g, const float* beta, int act,
+                  hipStream_t s);
+void launch_lstm_scan(const float* xg, long long xbs, int ldxg, int T, int B, const float* whh, const float* bhh,
+                      float* out, long long obs, int ldo, hipStream_t s);
+void launch_logsoftmax7(float* z, int rows, int* cls, hipStream_t s);
+void launch_fbank(const float* x, int T, const float* povey, const float* cos_t, const float* sin_t, const float* banks,
+                  float* out, hipStream_t s);
+void launch_colstats(float* x, int ld, int T, int C, int mode, float* out, hipStream_t s);
+void launch_cam_context(const float* h, int ldh, int T, int C, float* out, hipStream_t s);
+void launch_i16_scale(const int16_t* in, long long n, float scale, float* out, hipStream_t s);
+void launch_cam_gate(const float* y, int ldy, const float* m, int T, int G, float* out, int ldo, hipStream_t s);
+
 }  // namespace wdr

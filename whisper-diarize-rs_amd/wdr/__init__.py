@@ -269,6 +269,9 @@ class Vad:
         sp, ns = C.POINTER(L.SpeechSegment)(), C.c_size_t()
         L.check(self._lib.wdr_vad_get_segments(self.h, smp.ctypes.data_as(C.POINTER(C.c_int16)), smp.size,
                                                C.byref(mp), C.byref(nm), C.byref(sp), C.byref(ns)))
+        us = C.c_double()
+        L.check(self._lib.wdr_vad_stats(self.h, C.byref(us)))
+        self.last_us_per_step = us.value
         try:
             mask = [(mp[2 * i], mp[2 * i + 1]) for i in range(nm.value)]
             base = smp.ctypes.data
@@ -293,6 +296,93 @@ class Vad:
     def __del__(self):
         try:
             self.close()
+        except Exception:
+            pass
+
+
+class SpeakerManager:
+    """pyannote_rs::EmbeddingManager as the reference drives it (src/transcribe.rs:478-497)."""
+
+    def __init__(self, max_speakers: Optional[int] = None):
+        self._lib = L.load()
+        h = C.c_void_p()
+        L.check(self._lib.wdr_speakers_new(0 if max_speakers is None else 1, max_speakers or 0, C.byref(h)))
+        self.h = h
+
+    def assign(self, emb, threshold: float = 0.5) -> str:
+        buf = C.create_string_buffer(32)
+        if emb is None:
+            L.check(self._lib.wdr_speakers_assign(self.h, None, 0, threshold, buf, 32))
+        else:
+            e = np.ascontiguousarray(emb, np.float32)
+            L.check(self._lib.wdr_speakers_assign(self.h, e.ctypes.data_as(C.POINTER(C.c_float)), e.size, threshold,
+                                                  buf, 32))
+        return buf.value.decode()
+
+    def __del__(self):
+        try:
+            self._lib.wdr_speakers_free(self.h)
+        except Exception:
+            pass
+
+
+class Diarizer:
+    """pyannote segmentation-3.0 + CAM++ on the GPU (src/engine.rs:89-122,
+    src/transcribe.rs:461-497).  Synthetic seeded weights."""
+
+    def __init__(self, gpu_device: Optional[int] = None):
+        self._lib = L.load()
+        h = C.c_void_p()
+        L.check(self._lib.wdr_diarizer_create(None, None, 0 if gpu_device is None else 1, gpu_device or 0,
+                                              C.byref(h)))
+        self.h = h
+
+    def frame_classes(self, samples: np.ndarray, logprobs: bool = False):
+        smp = np.ascontiguousarray(samples, np.int16)
+        nw = smp.size // 160000 + 1
+        cls = np.zeros(nw * 589, np.int32)
+        lp = np.zeros(nw * 589 * 7, np.float32) if logprobs else None
+        L.check(self._lib.wdr_diarize_frame_classes(self.h, smp.ctypes.data_as(C.POINTER(C.c_int16)), smp.size,
+                                                    cls.ctypes.data_as(C.POINTER(C.c_int32)),
+                                                    lp.ctypes.data_as(C.POINTER(C.c_float)) if logprobs else None))
+        cls = cls.reshape(nw, 589)
+        return (cls, lp.reshape(nw, 589, 7)) if logprobs else cls
+
+    def get_segments(self, samples: np.ndarray):
+        smp = np.ascontiguousarray(samples, np.int16)
+        sp, ns = C.POINTER(L.SpeechSegment)(), C.c_size_t()
+        L.check(self._lib.wdr_diarize_get_segments(self.h, smp.ctypes.data_as(C.POINTER(C.c_int16)), smp.size,
+                                                   C.byref(sp), C.byref(ns)))
+        try:
+            return [SpeechSegment(sp[i].start, sp[i].end, np.ctypeslib.as_array(sp[i].samples, (sp[i].n_samples,)).copy()
+                                  if sp[i].n_samples else np.zeros(0, np.int16)) for i in range(ns.value)]
+        finally:
+            self._lib.wdr_free(C.cast(sp, C.c_void_p))
+
+    def fbank(self, samples: np.ndarray) -> np.ndarray:
+        smp = np.ascontiguousarray(samples, np.int16)
+        out = np.zeros((smp.size // 160 + 1, 80), np.float32)
+        nf = C.c_size_t()
+        L.check(self._lib.wdr_diarize_fbank(self.h, smp.ctypes.data_as(C.POINTER(C.c_int16)), smp.size,
+                                            out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(nf)))
+        return out[:nf.value]
+
+    def embedding(self, samples: np.ndarray):
+        smp = np.ascontiguousarray(samples, np.int16)
+        out = np.zeros(512, np.float32)
+        ok = C.c_int8()
+        L.check(self._lib.wdr_diarize_embedding(self.h, smp.ctypes.data_as(C.POINTER(C.c_int16)), smp.size,
+                                                out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(ok)))
+        return out if ok.value else None
+
+    def stats(self):
+        a, b = C.c_double(), C.c_double()
+        L.check(self._lib.wdr_diarize_stats(self.h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def __del__(self):
+        try:
+            self._lib.wdr_diarizer_free(self.h)
         except Exception:
             pass
 

@@ -100,8 +100,19 @@ _SIGS = {
     "wdr_vad_create": (C.c_int, [cstr, i8, i32, P(vp)]),
     "wdr_vad_free": (None, [vp]),
     "wdr_vad_probs": (C.c_int, [vp, P(C.c_int16), sz, P(f32), P(f64)]),
+    "wdr_vad_stats": (C.c_int, [vp, P(f64)]),
     "wdr_vad_segments_from_probs": (C.c_int, [P(f32), sz, P(f32), P(sz)]),
     "wdr_vad_get_segments": (C.c_int, [vp, P(C.c_int16), sz, P(P(f64)), P(sz), P(P(SpeechSegment)), P(sz)]),
+    "wdr_diarizer_create": (C.c_int, [cstr, cstr, i8, i32, P(vp)]),
+    "wdr_diarizer_free": (None, [vp]),
+    "wdr_diarize_frame_classes": (C.c_int, [vp, P(C.c_int16), sz, P(i32), P(f32)]),
+    "wdr_diarize_get_segments": (C.c_int, [vp, P(C.c_int16), sz, P(P(SpeechSegment)), P(sz)]),
+    "wdr_diarize_fbank": (C.c_int, [vp, P(C.c_int16), sz, P(f32), P(sz)]),
+    "wdr_diarize_embedding": (C.c_int, [vp, P(C.c_int16), sz, P(f32), P(i8)]),
+    "wdr_diarize_stats": (C.c_int, [vp, P(f64), P(f64)]),
+    "wdr_speakers_new": (C.c_int, [i8, u64, P(vp)]),
+    "wdr_speakers_free": (None, [vp]),
+    "wdr_speakers_assign": (C.c_int, [vp, P(f32), i32, f32, C.c_char_p, sz]),
     "wdr_context_create": (C.c_int, [cstr, cstr, i8, i32, i8, i8, i8, i8, u64, P(Synthetic), P(vp)]),
     "wdr_context_free": (None, [vp]),
     "wdr_run_pipeline": (C.c_int, [vp, P(SpeechSegment), sz, P(TranscribeOptions), P(Synthetic), P(Callbacks),
