@@ -308,7 +308,9 @@ class WhisperState:
                 seq = dict(tokens=[], result_len=0, seek_delta=N_FRAMES, has_ts=False,
                            failed=False, completed=False)
                 n_max = n_text_ctx // 2 - 4
-                for i in range(n_max):
+                if params.strategy != "greedy":
+                    seq = self.decode_beam(st, logits, cross, prompt, params, t_cur, seek, seek_end, L, window)
+                for i in range(n_max if params.strategy == "greedy" else 0):
                     force = None
                     if L:
                         if i == 0:
@@ -352,10 +354,11 @@ class WhisperState:
                     self.stats["decode_calls"] += 1
                     self.stats["decode_tokens"] += 1
                 # rank (single decoder)
-                seq["tokens"] = seq["tokens"][:seq["result_len"]]
-                score_sequence(seq, params)
-                if seq["failed"] is False and seq["result_len"] > 32 and seq["entropy"] < params.entropy_thold:
-                    seq["failed"] = True
+                if params.strategy == "greedy":
+                    seq["tokens"] = seq["tokens"][:seq["result_len"]]
+                    score_sequence(seq, params)
+                    if seq["failed"] is False and seq["result_len"] > 32 and seq["entropy"] < params.entropy_thold:
+                        seq["failed"] = True
                 seq["no_speech_prob"] = no_speech_prob
                 best = seq
                 success = True
@@ -394,6 +397,119 @@ class WhisperState:
                 seek_delta = min(seek_end - seek, N_FRAMES)
             seek += seek_delta
         return 0
+
+    # ------------------------------------------------------------ beam search
+    def topk(self, logprobs, k):
+        """whisper_sample_token_topk over the processed logits: descending, ties by lower
+        token id; only finite entries are candidates (with the synthetic forcing a row can
+        have fewer than k; whisper.cpp would pad with -inf entries that are never chosen
+        while a finite candidate exists)."""
+        fin = np.nonzero(logprobs > -np.inf)[0]
+        order = fin[np.lexsort((fin, -logprobs[fin].astype(np.float64)))]
+        return [int(i) for i in order[:k]]
+
+    def decode_beam(self, st, logits, cross, prompt, params, t_cur, seek, seek_end, L, window):
+        """whisper.cpp WHISPER_SAMPLING_BEAM_SEARCH at t = 0 (patience -1): K decoders share
+        the prompt; each live decoder proposes its top-K tokens; candidates are ordered by
+        cumulative log-probability (stable: decoder index, then rank), duplicate sequences are
+        dropped, and live decoders take the candidates in order,
+        wrapping around when there are fewer; KV caches follow their parents.  Ranking:
+        score = sum logprob / length (length_penalty -1), entropy check, first best wins."""
+        v = self.v
+        K = max(1, params.beam_size)
+        n_max = self.m.hp.n_text_ctx // 2 - 4
+        dec = [dict(tokens=[], result_len=0, seek_delta=N_FRAMES, has_ts=False, failed=False, completed=False,
+                    sum_all=0.0) for _ in range(K)]
+        states = [st] + [st.copy() for _ in range(K - 1)]
+        row_logits = [logits] * K
+        self._no_speech = None
+        for i in range(n_max):
+            act = [j for j in range(K) if not dec[j]["completed"] and not dec[j]["failed"]]
+            if not act:
+                break
+            force = None
+            if L:
+                if i == 0:
+                    force = ("only", v.beg)
+                elif i < L - 2:
+                    force = ("text", None)
+                elif i == L - 2:
+                    force = ("only", v.beg + min(1500, max(1, (window - DELTA_MIN - 1) // 2)))
+                else:
+                    force = ("only", v.eot)
+            cands = []
+            for j in act:
+                d = dec[j]
+                _, lps, probs = self.process_logits(row_logits[j], d["tokens"], d["has_ts"], d["seek_delta"],
+                                                    params, t_cur, force)
+                g = self.sample_greedy(probs, lps)
+                for tid in self.topk(lps, K):
+                    tok = Token(id=tid, tid=g.tid, p=float(probs[tid]), plog=float(lps[tid]), pt=g.pt, ptsum=g.ptsum)
+                    if tok.id >= v.beg:
+                        tok.tid, tok.pt = tok.id, tok.p
+                    cands.append((j, d["sum_all"] + tok.plog, tok))
+            cands.sort(key=lambda c: -c[1])          # stable
+            uniq = []
+            for c in cands:
+                key = [t.id for t in dec[c[0]]["tokens"]] + [c[2].id]
+                if all(key != [t.id for t in dec[u[0]]["tokens"]] + [u[2].id] for u in uniq):
+                    uniq.append(c)
+            nd, ns = list(dec), list(states)
+            cur = 0
+            for j in act:
+                if cur >= len(uniq):
+                    cur = 0
+                pj, sm, tok = uniq[cur]
+                cur += 1
+                nd[j] = dict(dec[pj], tokens=list(dec[pj]["tokens"]) + [tok], sum_all=sm)
+                ns[j] = states[pj].copy() if pj != j else states[j]
+            dec, states = nd, ns
+            for j in act:
+                d = dec[j]
+                tok = d["tokens"][-1]
+                if tok.id > v.beg:
+                    sdn = 2 * (tok.id - v.beg)
+                    if d["has_ts"] and d["seek_delta"] > sdn and d["result_len"] < i:
+                        d["failed"] = True
+                        continue
+                    d["seek_delta"] = sdn
+                    d["result_len"] = i + 1
+                    d["has_ts"] = True
+                if (tok.id == v.eot or (params.max_tokens > 0 and i >= params.max_tokens)
+                        or (d["has_ts"] and seek + d["seek_delta"] + DELTA_MIN >= seek_end)):
+                    if d["result_len"] == 0:
+                        if seek + d["seek_delta"] + DELTA_MIN >= seek_end:
+                            d["result_len"] = i + 1
+                        else:
+                            d["failed"] = True
+                            continue
+                    if params.single_segment:
+                        d["result_len"] = i + 1
+                        d["seek_delta"] = N_FRAMES
+                    d["completed"] = True
+                    continue
+                if i == n_max - 1 and (d["result_len"] == 0 or d["seek_delta"] < N_FRAMES // 2):
+                    d["failed"] = True
+            live = [j for j in act if not dec[j]["completed"] and not dec[j]["failed"]]
+            for j in live:
+                row_logits[j] = states[j].forward([dec[j]["tokens"][-1].id], cross)
+                self.stats["decode_calls"] += 1
+                self.stats["decode_tokens"] += 1
+        best, best_score = 0, -np.inf
+        for j, d in enumerate(dec):
+            if d["failed"]:
+                continue
+            d["tokens"] = d["tokens"][:d["result_len"]]
+            score_sequence(d, params)
+            if d["result_len"] > 32 and d["entropy"] < params.entropy_thold:
+                d["failed"] = True
+                continue
+            if best_score < d["score"]:
+                best, best_score = j, d["score"]
+        out = dec[best]
+        out["tokens"] = out["tokens"][:out["result_len"]]
+        score_sequence(out, params)
+        return out
 
     # ------------------------------------------------------------ timestamps
     def token_timestamps_heuristic(self, i_segment, params, energy):

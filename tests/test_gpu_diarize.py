@@ -68,7 +68,9 @@ def test_fbank_and_embedding(dz, audio, n):
     if r is None:
         assert e is None
         return
-    np.testing.assert_allclose(e, r, rtol=1e-3, atol=1e-3)
+    np.testing.assert_allclose(e, r, rtol=1e-3, atol=1e-3)   # NaN where the std of 1 frame is NaN (torch too)
+    if np.isnan(r).any():
+        return
     assert D.EmbeddingManager.cosine(e, r) > 0.9999
     assert dz.stats()[1] > 0
 

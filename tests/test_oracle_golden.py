@@ -108,3 +108,28 @@ def test_log_mel_shapes_and_pad_value():
     tail = m[:, -10:]
     assert np.allclose(tail, tail[0, 0])
     assert m.max() == np.float32((m.max() * 4 - 4 + 4) / 4)
+
+
+def test_oracle_beam_search_with_one_beam_is_greedy():
+    """Beam search with K = 1 reduces to greedy (top-1 = argmax, ties by lower id)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "whisper-diarize-rs_amd"))
+    from oracle.model import Whisper
+    from oracle.vocab import Vocab
+    from oracle.weights import hparams_for, synth_weights
+    from oracle.whisper_full import FullParams, WhisperState
+    from oracle.mel import pcm_i16_to_f32
+    from wdr.synth import synth_speech
+    hp = hparams_for("tiny-test")
+    W = synth_weights(hp, std=0.02, emb_std=0.5)
+    pcm, sp = synth_speech(12.0, seed=0)
+    x = pcm_i16_to_f32(pcm[int(sp[0][0] * 16000):int(sp[0][1] * 16000)])
+    out = []
+    for strat, k in (("greedy", 5), ("beam", 1), ("beam", 3)):
+        st = WhisperState(Whisper(hp, W), Vocab(hp.n_vocab), "tiny-test")
+        p = FullParams(strategy=strat, beam_size=k, language="en", force_len_rate=3.3,
+                       logprob_thold=-np.inf, entropy_thold=-1.0)
+        st.full(x, p)
+        out.append([t.id for r in st.result_all for t in r.tokens])
+    assert out[0] == out[1]
+    assert len(out[2]) == len(out[0])

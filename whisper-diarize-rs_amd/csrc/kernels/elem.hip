@@ -569,6 +569,135 @@ __global__ void k_logits_final(const float* logits, int ld, const LogitsCtl* ctl
   out[r] = o;
 }
 
+// ---- beam search: top-K processed logits per row (whisper_sample_token_topk).  Candidates are
+// ordered by the processed logit (= by probability), ties by lower token id; only finite
+// entries are candidates (see oracle/whisper_full.py topk).
+struct LgTop {
+  float x[BEAM_KMAX];
+  int i[BEAM_KMAX];
+};
+
+__device__ __forceinline__ bool top_better(float x, int i, float y, int j) { return x > y || (x == y && i < j); }
+
+__global__ __launch_bounds__(256) void k_logits_topk(const float* logits, int ld, const LogitsCtl* ctls, VocabIds v,
+                                                     const LgStats* st, int K, LgTop* part) {
+  __shared__ LgStats g;
+  __shared__ float shv[4];
+  __shared__ int shi[4];
+  const int b = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
+  if (tid == 0) lg_global(st, r, g);
+  __syncthreads();
+  const float* L = logits + (long long)r * ld;
+  const LogitsCtl c = ctls[r];
+  const float lse = logf(g.s1) + g.m1;
+  const float ts_lp = (g.mts == -INFINITY || !(g.sts > 0.f)) ? -INFINITY : logf(g.sts) + (g.mts - lse);
+  const bool mask_text = ts_lp > g.mtx - lse;
+  const int V = v.n_vocab, chunk = (V + LG_NB - 1) / LG_NB;
+  const int i0 = b * chunk, i1 = min(V, i0 + chunk);
+  // each thread keeps its best K (sorted) over its strided elements
+  float bx[BEAM_KMAX];
+  int bi[BEAM_KMAX];
+  for (int k = 0; k < BEAM_KMAX; ++k) { bx[k] = -INFINITY; bi[k] = 0x7fffffff; }
+  for (int i = i0 + tid; i < i1; i += 256) {
+    float x = rule_mask(L[i], i, c, v);
+    if (mask_text && i < v.beg) x = -INFINITY;
+    if (x == -INFINITY || !top_better(x, i, bx[K - 1], bi[K - 1])) continue;
+    int p = K - 1;
+    while (p > 0 && top_better(x, i, bx[p - 1], bi[p - 1])) { bx[p] = bx[p - 1]; bi[p] = bi[p - 1]; --p; }
+    bx[p] = x; bi[p] = i;
+  }
+  // K rounds of a block-wide argmax over the threads' current heads
+  LgTop out;
+  int head = 0;
+  for (int k = 0; k < K; ++k) {
+    float hv = head < K ? bx[head] : -INFINITY;
+    int hi = head < K ? bi[head] : 0x7fffffff;
+    float wv = hv;
+    int wi = hi;
+    for (int o = 32; o > 0; o >>= 1) {
+      const float v2 = __shfl_xor(wv, o, 64);
+      const int i2 = __shfl_xor(wi, o, 64);
+      if (top_better(v2, i2, wv, wi)) { wv = v2; wi = i2; }
+    }
+    if ((tid & 63) == 0) { shv[tid >> 6] = wv; shi[tid >> 6] = wi; }
+    __syncthreads();
+    float bv = shv[0];
+    int bidx = shi[0];
+    for (int q = 1; q < 4; ++q)
+      if (top_better(shv[q], shi[q], bv, bidx)) { bv = shv[q]; bidx = shi[q]; }
+    __syncthreads();
+    out.x[k] = bv;
+    out.i[k] = bidx;
+    if (head < K && hi == bidx && bidx != 0x7fffffff) ++head;   // indices are unique
+  }
+  if (tid == 0) part[r * LG_NB + b] = out;
+}
+
+__global__ void k_logits_topk_final(const LgStats* st, const LgTop* part, int K, BeamCand* out) {
+  const int r = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  LgStats g;
+  lg_global(st, r, g);
+  const float lse = logf(g.s1) + g.m1;
+  int ptr[LG_NB];
+  for (int b = 0; b < LG_NB; ++b) ptr[b] = 0;
+  for (int k = 0; k < K; ++k) {
+    float bv = -INFINITY;
+    int bidx = 0x7fffffff, bb = -1;
+    for (int b = 0; b < LG_NB; ++b) {
+      if (ptr[b] >= K) continue;
+      const float x = part[r * LG_NB + b].x[ptr[b]];
+      const int i = part[r * LG_NB + b].i[ptr[b]];
+      if (x != -INFINITY && top_better(x, i, bv, bidx)) { bv = x; bidx = i; bb = b; }
+    }
+    BeamCand c;
+    if (bb < 0) {
+      c.id = -1; c.p = 0.f; c.plog = -INFINITY;
+    } else {
+      ptr[bb]++;
+      c.id = bidx;
+      c.plog = bv - lse;
+      c.p = __expf(c.plog);
+    }
+    out[r * K + k] = c;
+  }
+}
+
+void launch_logits_topk(const float* logits, int ld, const LogitsCtl* ctls, const VocabIds& v, int R, int K,
+                        float* work, BeamCand* out, hipStream_t s) {
+  WDR_CHECK(K >= 1 && K <= BEAM_KMAX, "beam size out of range");
+  const LgStats* st = (const LgStats*)work;   // written by launch_logits_process
+  LgTop* part = (LgTop*)(work + (size_t)R * LG_NB * 8 + (size_t)R * LG_NB * 8);
+  hipLaunchKernelGGL(k_logits_topk, dim3(LG_NB, R), dim3(256), 0, s, logits, ld, ctls, v, st, K, part);
+  hipLaunchKernelGGL(k_logits_topk_final, dim3(R), dim3(64), 0, s, st, part, K, out);
+  WDR_HIP(hipGetLastError());
+}
+
+// beam reorder: copy the first n_rows cached K/V rows of sequence src[p] to dst[p], every layer
+__global__ void k_kv_copy(f16* kc, f16* vc, long long seq_stride, int nslot, const int* pairs, int n_rows, int d) {
+  const int l = blockIdx.y, p = blockIdx.z;
+  const int src = pairs[2 * p], dst = pairs[2 * p + 1];
+  const long long n = (long long)n_rows * d / 8;
+  const long long base = (long long)l * nslot * seq_stride;
+  const f16x8* ks = reinterpret_cast<const f16x8*>(kc + base + src * seq_stride);
+  const f16x8* vs = reinterpret_cast<const f16x8*>(vc + base + src * seq_stride);
+  f16x8* kd = reinterpret_cast<f16x8*>(kc + base + dst * seq_stride);
+  f16x8* vd = reinterpret_cast<f16x8*>(vc + base + dst * seq_stride);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    kd[i] = ks[i];
+    vd[i] = vs[i];
+  }
+}
+
+void launch_kv_copy(f16* kc, f16* vc, long long seq_stride, int nslot, int L, const int* pairs_dev, int n_pairs,
+                    int n_rows, int d, hipStream_t s) {
+  if (n_pairs <= 0 || n_rows <= 0) return;
+  WDR_CHECK(d % 8 == 0, "kv copy: d must be a multiple of 8");
+  hipLaunchKernelGGL(k_kv_copy, dim3(std::max(1, std::min(64, n_rows * d / 8 / 256 + 1)), L, n_pairs), dim3(256), 0, s,
+                     kc, vc, seq_stride, nslot, pairs_dev, n_rows, d);
+  WDR_HIP(hipGetLastError());
+}
+
 void launch_logits_process(const float* logits, int ld, const LogitsCtl* ctls, const VocabIds& v, int R, float* work,
                            TokOut* out, hipStream_t s) {
   LgStats* st = (LgStats*)work;

@@ -52,12 +52,21 @@ struct VocabIds {
   int max_initial_tid;  // round(max_initial_ts / precision); -1 disables
   int suppress_blank;
 };
+constexpr int BEAM_KMAX = 8;
+struct BeamCand {   // one beam-search candidate of a row: token, p, log p (id -1: none)
+  int id;
+  float p, plog;
+};
 struct TokOut {
   int id, tid;
   float p, plog, pt, ptsum;
   float nosp_prob;
   int pad;
 };
+void launch_logits_topk(const float* logits, int ld, const LogitsCtl* ctls, const VocabIds& v, int R, int K,
+                        float* work, BeamCand* out, hipStream_t s);
+void launch_kv_copy(f16* kc, f16* vc, long long seq_stride, int nslot, int L, const int* pairs_dev, int n_pairs,
+                    int n_rows, int d, hipStream_t s);
 void launch_logits_process(const float* logits, int ld, const LogitsCtl* ctls, const VocabIds& v, int R, float* work,
                            TokOut* out, hipStream_t s);
 

@@ -125,6 +125,8 @@ struct StageTimes {   // host wall-clock per phase (seconds), accumulated
   long long windows = 0, decode_steps = 0, prefills = 0;
 };
 
+struct Seq;   // one decoder's sequence (whisper_ctx.cpp)
+
 class State {
  public:
   explicit State(Context& ctx);
@@ -158,10 +160,15 @@ class State {
   std::unique_ptr<Impl> m_;
   // pieces of full()
   void top_up(int job);
+  Seq decode_beam(const std::vector<int>& prompt, const FullParams& params, float t_cur, int seek, int seek_end, int Lf,
+                  int window, float* nosp);
   void decoder_prefill(const int* toks, int n, int seq, bool want_logits, bool capture);
   void decoder_step(const int* toks, const int* seqs, const int* pos, int R);
   void decoder_step_body(int R);
-  void step_and_sample(const int* toks, const int* seqs, const int* pos, const LogitsCtl* ctl, int R, TokenData* out);
+  void step_and_sample(const int* toks, const int* seqs, const int* pos, const LogitsCtl* ctl, int R, TokenData* out,
+                       int K = 0, BeamCand* cands = nullptr);
+  void logits_topk(int R, int K, BeamCand* out);
+  void kv_reorder(const std::vector<std::pair<int, int>>& moves, int n_rows);
   void run_logits(int R, const LogitsCtl* ctl, TokenData* out, float* nosp);
   void heuristic_timestamps(int i_segment, const FullParams& p);
   void dtw_timestamps(int i_segment, int n_segments, int seek, int n_frames, const std::string& language);

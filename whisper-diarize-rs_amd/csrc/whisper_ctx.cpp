@@ -309,7 +309,8 @@ Context::~Context() {
 
 // ------------------------------------------------------------------ state buffers
 static constexpr int RMAX = 448;   // max decoder rows in one forward (n_text_ctx)
-static constexpr int NSEQ = 8;     // max concurrent decoder sequences
+static constexpr int NSEQ = 8;     // max decoder rows in one step
+static constexpr int NSLOT = 16;   // self-attention KV-cache sequences (beams + beam-reorder scratch)
 static constexpr int NSPLIT = 24;  // cross-attention key chunks (1500 / 64)
 
 struct State::Impl {
@@ -346,6 +347,9 @@ struct State::Impl {
   // decoder
   DevMem xd, hd, qkvd, attd, qx, mlpd, logits, work, tokout, ctl, ml, cap, part_o, part_ml;
   DevMem rows_tok, rows_pos, rows_seq;
+  DevMem beamc, kvpairs;       // beam candidates [NSEQ][BEAM_KMAX], KV reorder (src, dst) pairs
+  BeamCand* h_beam = nullptr;
+  int* h_pairs = nullptr;
   DevMem fpart_o, fpart_ml;   // split flash-attention partials (prefill cross-attention)
   DevMem kc, vc;
   long long seq_stride = 0;   // elements per (layer, seq)
@@ -424,12 +428,16 @@ State::State(Context& ctx) : ctx_(ctx), s_(ctx.stream), m_(new Impl) {
   m.part_ml = DevMem((size_t)NSPLIT * NSEQ * m.H * sizeof(float2));
   m.fpart_o = DevMem((size_t)12 * 256 * m.H * 64 * 4);
   m.fpart_ml = DevMem((size_t)12 * m.H * 256 * sizeof(float2));
+  m.beamc = DevMem(NSEQ * BEAM_KMAX * sizeof(BeamCand));
+  m.kvpairs = DevMem(2 * 2 * NSEQ * 4);
+  WDR_HIP(hipHostMalloc((void**)&m.h_beam, NSEQ * BEAM_KMAX * sizeof(BeamCand), hipHostMallocDefault));
+  WDR_HIP(hipHostMalloc((void**)&m.h_pairs, 2 * 2 * NSEQ * 4, hipHostMallocDefault));
   m.rows_tok = DevMem(RMAX * 4);
   m.rows_pos = DevMem(RMAX * 4);
   m.rows_seq = DevMem(RMAX * 4);
   m.seq_stride = (long long)hp.n_text_ctx * d;
-  m.kc = DevMem((size_t)m.L * NSEQ * m.seq_stride * 2);
-  m.vc = DevMem((size_t)m.L * NSEQ * m.seq_stride * 2);
+  m.kc = DevMem((size_t)m.L * NSLOT * m.seq_stride * 2);
+  m.vc = DevMem((size_t)m.L * NSLOT * m.seq_stride * 2);
   m.nrm = DevMem((size_t)A * RMAX * 1500 * 4);
   m.xdtw = DevMem((size_t)RMAX * 1500 * 4);
   m.times = DevMem((RMAX + 8) * 4);
@@ -450,6 +458,8 @@ State::~State() {
     (void)hipHostFree(m_->h_tok);
     (void)hipHostFree(m_->h_ctl);
     (void)hipHostFree(m_->h_times);
+    (void)hipHostFree(m_->h_beam);
+    (void)hipHostFree(m_->h_pairs);
     if (m_->es) {
       (void)hipStreamSynchronize(m_->es);
       (void)hipStreamDestroy(m_->es);
@@ -662,8 +672,8 @@ void State::decoder_prefill(const int* toks, int n, int seq, bool want_logits, b
   const int ldxkv = L * 2 * d;
   for (int l = 0; l < L; ++l) {
     const DecLayer& e = md.dec[l];
-    f16* kc = m.kc.as<f16>() + (size_t)l * NSEQ * m.seq_stride;
-    f16* vc = m.vc.as<f16>() + (size_t)l * NSEQ * m.seq_stride;
+    f16* kc = m.kc.as<f16>() + (size_t)l * NSLOT * m.seq_stride;
+    f16* vc = m.vc.as<f16>() + (size_t)l * NSLOT * m.seq_stride;
     launch_layernorm(m.xd.as<float>(), d, e.ln1_g, e.ln1_b, m.hd.as<f16>(), d, n, d, s_);
     proj(s_, m.hd.as<f16>(), d, e.w_qkv, d, e.b_qkv, m.qkvd.p, 3 * d, n, 3 * d, d, EPI_F16);
     launch_kv_scatter(m.qkvd.as<f16>(), 3 * d, d, m.rows_seq.as<int>(), m.rows_pos.as<int>(), n, kc, vc, m.seq_stride,
@@ -735,8 +745,8 @@ void State::decoder_step_body(int R) {
   };
   for (int l = 0; l < L; ++l) {
     const DecLayer& e = md.dec[l];
-    f16* kc = m.kc.as<f16>() + (size_t)l * NSEQ * m.seq_stride;
-    f16* vc = m.vc.as<f16>() + (size_t)l * NSEQ * m.seq_stride;
+    f16* kc = m.kc.as<f16>() + (size_t)l * NSLOT * m.seq_stride;
+    f16* vc = m.vc.as<f16>() + (size_t)l * NSLOT * m.seq_stride;
     ProjArgs q = P(nullptr, d, e.w_qkv, e.b_qkv, m.qkvd.p, 3 * d, 3 * d, d, EPI_QKV_CACHE, e.ln1_g, e.ln1_b);
     q.kc = kc;
     q.vc = vc;
@@ -779,7 +789,7 @@ void State::decoder_step(const int* toks, const int* seqs, const int* pos, int R
 // decode step + logit rules + greedy pick as ONE hipGraph replay per token (captured once per
 // row count; the per-step inputs live in pinned host buffers the graph's copy nodes read).
 void State::step_and_sample(const int* toks, const int* seqs, const int* pos, const LogitsCtl* ctl, int R,
-                            TokenData* out) {
+                            TokenData* out, int K, BeamCand* cands) {
   Impl& m = *m_;
   WDR_CHECK(R >= 1 && R <= NSEQ, "decoder step: row count out of range");
   for (int i = 0; i < R; ++i) {
@@ -793,9 +803,10 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
     // ROCm: run the same kernels eagerly while a profiling class is active
     decoder_step(toks, seqs, pos, R);
     run_logits(R, ctl, out, nullptr);
+    if (K > 0) logits_topk(R, K, cands);
     return;
   }
-  Impl::StepGraph& g = m.graphs[R * 256 + m.cur];
+  Impl::StepGraph& g = m.graphs[(K << 16) + R * 256 + m.cur];
   if (!g.exec || g.prof_cls != prof_class()) {
     if (g.exec) {
       (void)hipGraphExecDestroy(g.exec);
@@ -812,6 +823,11 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
     launch_logits_process(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, m.work.as<float>(),
                           m.tokout.as<TokOut>(), s_);
     WDR_HIP(hipMemcpyAsync(m.h_tok, m.tokout.p, R * sizeof(TokOut), hipMemcpyDeviceToHost, s_));
+    if (K > 0) {
+      launch_logits_topk(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, K, m.work.as<float>(),
+                         m.beamc.as<BeamCand>(), s_);
+      WDR_HIP(hipMemcpyAsync(m.h_beam, m.beamc.p, (size_t)R * K * sizeof(BeamCand), hipMemcpyDeviceToHost, s_));
+    }
     WDR_HIP(hipStreamEndCapture(s_, &graph));
     WDR_HIP(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
     WDR_HIP(hipGraphDestroy(graph));
@@ -820,11 +836,12 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
   if (memcmp(&g.vids, &m.vids, sizeof(VocabIds)) != 0) {   // rule constants changed: recapture
     (void)hipGraphExecDestroy(g.exec);
     g.exec = nullptr;
-    step_and_sample(toks, seqs, pos, ctl, R, out);
+    step_and_sample(toks, seqs, pos, ctl, R, out, K, cands);
     return;
   }
   WDR_HIP(hipGraphLaunch(g.exec, s_));
   WDR_HIP(hipStreamSynchronize(s_));
+  if (K > 0) memcpy(cands, m.h_beam, (size_t)R * K * sizeof(BeamCand));
   for (int r = 0; r < R; ++r) {
     const TokOut& o = m.h_tok[r];
     TokenData t;
@@ -859,6 +876,37 @@ void State::run_logits(int R, const LogitsCtl* ctl, TokenData* out, float* nosp)
     out[r] = t;
     if (nosp) nosp[r] = o.nosp_prob;
   }
+}
+
+// top-K candidates of rows whose logits were just processed by run_logits (same ctl)
+void State::logits_topk(int R, int K, BeamCand* out) {
+  Impl& m = *m_;
+  launch_logits_topk(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, K, m.work.as<float>(),
+                     m.beamc.as<BeamCand>(), s_);
+  WDR_HIP(hipMemcpyAsync(m.h_beam, m.beamc.p, (size_t)R * K * sizeof(BeamCand), hipMemcpyDeviceToHost, s_));
+  WDR_HIP(hipStreamSynchronize(s_));
+  memcpy(out, m.h_beam, (size_t)R * K * sizeof(BeamCand));
+}
+
+// beam reorder (whisper_kv_cache_seq_cp through scratch sequences): sequence dst takes the first
+// n_rows cached rows of sequence src, for every (src, dst) move; scratch slots NSEQ + dst.
+void State::kv_reorder(const std::vector<std::pair<int, int>>& moves, int n_rows) {
+  Impl& m = *m_;
+  if (moves.empty() || n_rows <= 0) return;
+  const int n = (int)moves.size();
+  WDR_CHECK(n <= NSEQ, "kv reorder: too many moves");
+  for (int i = 0; i < n; ++i) {
+    WDR_CHECK(moves[i].first < NSEQ && moves[i].second < NSEQ, "kv reorder: slot out of range");
+    m.h_pairs[2 * i] = moves[i].first;
+    m.h_pairs[2 * i + 1] = NSEQ + moves[i].second;
+    m.h_pairs[2 * NSEQ + 2 * i] = NSEQ + moves[i].second;
+    m.h_pairs[2 * NSEQ + 2 * i + 1] = moves[i].second;
+  }
+  WDR_HIP(hipMemcpyAsync(m.kvpairs.p, m.h_pairs, 4 * NSEQ * 4, hipMemcpyHostToDevice, s_));
+  launch_kv_copy(m.kc.as<f16>(), m.vc.as<f16>(), m.seq_stride, NSLOT, m.L, m.kvpairs.as<int>(), n, n_rows, m.d, s_);
+  launch_kv_copy(m.kc.as<f16>(), m.vc.as<f16>(), m.seq_stride, NSLOT, m.L, m.kvpairs.as<int>() + 2 * NSEQ, n, n_rows,
+                 m.d, s_);
+  WDR_HIP(hipStreamSynchronize(s_));   // the pinned pair table is rewritten by the next reorder
 }
 
 void State::decode_logits(const int* toks, int n, float* logits_out) {
@@ -1057,12 +1105,180 @@ static void score_sequence(Seq& s, const FullParams& p) {
   s.entropy = ent;
 }
 
+// whisper.cpp's beam search at t = 0 (WHISPER_SAMPLING_BEAM_SEARCH, patience -1): K decoders
+// share the prompt; every step each live decoder proposes its top-K tokens, the candidates are
+// ordered by cumulative log-probability (stable: decoder, then rank), duplicate sequences
+// are dropped, and live decoders take the best candidates in order (wrapping around when
+// there are fewer), their KV caches following their new parents.  Mirrors
+// oracle/whisper_full.py WhisperState.decode_beam.
+Seq State::decode_beam(const std::vector<int>& prompt, const FullParams& params, float t_cur, int seek, int seek_end,
+                       int Lf, int window, float* nosp) {
+  const Vocab& v = ctx_.vocab;
+  const int K = std::max(1, std::min(params.beam_size, std::min(NSEQ, BEAM_KMAX)));
+  const int n_max = ctx_.model.hp.n_text_ctx / 2 - 4;
+  const int P = (int)prompt.size();
+  const int delta_min = 10;
+  std::vector<Seq> dec(K);
+  std::vector<double> sum_all(K, 0.0);
+  {
+    std::vector<std::pair<int, int>> share;
+    for (int j = 1; j < K; ++j) share.push_back({0, j});
+    kv_reorder(share, P);
+  }
+  std::vector<BeamCand> bc((size_t)NSEQ * K);
+  std::vector<TokenData> td(NSEQ);
+  for (int i = 0; i < n_max; ++i) {
+    std::vector<int> act;
+    for (int j = 0; j < K; ++j)
+      if (!dec[j].completed && !dec[j].failed) act.push_back(j);
+    if (act.empty()) break;
+    std::vector<LogitsCtl> ctl(act.size());
+    for (size_t r = 0; r < act.size(); ++r) {
+      const Seq& d = dec[act[r]];
+      LogitsCtl& c = ctl[r];
+      c = LogitsCtl{};
+      c.n_tokens = (int)d.tokens.size();
+      c.last_ts = !d.tokens.empty() && d.tokens.back().id >= v.beg;
+      c.pen_ts = d.tokens.size() < 2 || d.tokens[d.tokens.size() - 2].id >= v.beg;
+      c.has_ts = d.has_ts;
+      c.seek_delta = d.seek_delta;
+      c.temperature = t_cur;
+      if (Lf) {
+        if (i == 0) { c.force_kind = 1; c.force_tok = v.beg; }
+        else if (i < Lf - 2) c.force_kind = 2;
+        else if (i == Lf - 2) { c.force_kind = 1; c.force_tok = v.beg + std::min(1500, std::max(1, (window - delta_min - 1) / 2)); }
+        else { c.force_kind = 1; c.force_tok = v.eot; }
+      }
+    }
+    if (i == 0) {
+      // every decoder holds the prompt's logits: process once, replicate
+      float ns = 0.f;
+      run_logits(1, ctl.data(), td.data(), &ns);
+      *nosp = ns;
+      logits_topk(1, K, bc.data());
+      for (size_t r = 1; r < act.size(); ++r) {
+        td[r] = td[0];
+        for (int k = 0; k < K; ++k) bc[r * K + k] = bc[k];
+      }
+    } else {
+      std::vector<int> toks(act.size()), seqs(act.size()), pos(act.size(), P + i - 1);
+      for (size_t r = 0; r < act.size(); ++r) {
+        toks[r] = dec[act[r]].tokens.back().id;
+        seqs[r] = act[r];
+      }
+      step_and_sample(toks.data(), seqs.data(), pos.data(), ctl.data(), (int)act.size(), td.data(), K, bc.data());
+    }
+    struct Cand {
+      int j;
+      double sum;
+      TokenData tok;
+    };
+    std::vector<Cand> cs;
+    for (size_t r = 0; r < act.size(); ++r)
+      for (int k = 0; k < K; ++k) {
+        const BeamCand& b = bc[r * K + k];
+        if (b.id < 0) continue;
+        TokenData t;
+        t.id = b.id;
+        t.tid = td[r].tid;
+        t.p = b.p;
+        t.plog = b.plog;
+        t.pt = td[r].pt;
+        t.ptsum = td[r].ptsum;
+        if (t.id >= v.beg) {
+          t.tid = t.id;
+          t.pt = t.p;
+        }
+        cs.push_back({act[r], sum_all[act[r]] + (double)t.plog, t});
+      }
+    std::stable_sort(cs.begin(), cs.end(), [](const Cand& a, const Cand& b) { return a.sum > b.sum; });
+    std::vector<Cand> uniq;
+    for (const Cand& c : cs) {
+      bool dup = false;
+      for (const Cand& u : uniq) {
+        if (u.tok.id != c.tok.id || dec[u.j].tokens.size() != dec[c.j].tokens.size()) continue;
+        bool same = true;
+        for (size_t q = 0; q < dec[c.j].tokens.size() && same; ++q) same = dec[u.j].tokens[q].id == dec[c.j].tokens[q].id;
+        if (same) { dup = true; break; }
+      }
+      if (!dup) uniq.push_back(c);
+    }
+    WDR_CHECK(!uniq.empty(), "beam search: no finite candidate");
+    std::vector<Seq> nd = dec;
+    std::vector<double> ns = sum_all;
+    std::vector<std::pair<int, int>> moves;
+    size_t cur = 0;
+    for (int j : act) {
+      if (cur >= uniq.size()) cur = 0;
+      const Cand& c = uniq[cur++];
+      nd[j] = dec[c.j];
+      nd[j].tokens.push_back(c.tok);
+      ns[j] = c.sum;
+      if (c.j != j) moves.push_back({c.j, j});
+    }
+    dec.swap(nd);
+    sum_all.swap(ns);
+    kv_reorder(moves, P + i);
+    for (int j : act) {
+      Seq& d = dec[j];
+      const TokenData& tok = d.tokens.back();
+      if (tok.id > v.beg) {
+        const int sdn = 2 * (tok.id - v.beg);
+        if (d.has_ts && d.seek_delta > sdn && d.result_len < i) {
+          d.failed = true;
+          continue;
+        }
+        d.seek_delta = sdn;
+        d.result_len = i + 1;
+        d.has_ts = true;
+      }
+      if (tok.id == v.eot || (params.max_tokens > 0 && i >= params.max_tokens) ||
+          (d.has_ts && seek + d.seek_delta + delta_min >= seek_end)) {
+        if (d.result_len == 0) {
+          if (seek + d.seek_delta + delta_min >= seek_end) {
+            d.result_len = i + 1;
+          } else {
+            d.failed = true;
+            continue;
+          }
+        }
+        if (params.single_segment) {
+          d.result_len = i + 1;
+          d.seek_delta = 3000;
+        }
+        d.completed = true;
+        continue;
+      }
+      if (i == n_max - 1 && (d.result_len == 0 || d.seek_delta < 3000 / 2)) d.failed = true;
+    }
+  }
+  int best = 0;
+  double best_score = -INFINITY;
+  for (int j = 0; j < K; ++j) {
+    Seq& d = dec[j];
+    if (d.failed) continue;
+    d.tokens.resize(std::min((int)d.tokens.size(), d.result_len));
+    score_sequence(d, params);
+    if (d.result_len > 32 && d.entropy < params.entropy_thold) {
+      d.failed = true;
+      continue;
+    }
+    if (best_score < d.score) {
+      best_score = d.score;
+      best = j;
+    }
+  }
+  Seq out = dec[best];
+  out.tokens.resize(std::min((int)out.tokens.size(), out.result_len));
+  score_sequence(out, params);
+  return out;
+}
+
 int State::full(const FullParams& params, const float* samples, int n, int job) {
   WDR_HIP(hipSetDevice(ctx_.cp.gpu_device));
   Impl& m = *m_;
   const Vocab& v = ctx_.vocab;
   const HParams& hp = ctx_.model.hp;
-  WDR_CHECK(params.greedy, "beam-search decoding is not available yet: set sampling_strategy = \"greedy\"");
   result_all.clear();
   double t_start = now_s();
   const bool planned = job >= 0 && job < (int)m.plan.pcm.size();
@@ -1183,7 +1399,10 @@ int State::full(const FullParams& params, const float* samples, int n, int job) 
       Seq sq;
       const int n_max = n_text_ctx / 2 - 4;
       float nosp = 0.f;
-      for (int i = 0; i < n_max; ++i) {
+      if (!params.greedy) {
+        sq = decode_beam(prompt, params, t_cur, seek, seek_end, Lf, window, &nosp);
+      }
+      for (int i = 0; i < n_max && params.greedy; ++i) {
         LogitsCtl c{};
         c.n_tokens = (int)sq.tokens.size();
         c.last_ts = !sq.tokens.empty() && sq.tokens.back().id >= v.beg;
@@ -1241,9 +1460,11 @@ int State::full(const FullParams& params, const float* samples, int n, int job) 
           break;
         }
       }
-      sq.tokens.resize(std::min((int)sq.tokens.size(), sq.result_len));
-      score_sequence(sq, params);
-      if (!sq.failed && sq.result_len > 32 && sq.entropy < params.entropy_thold) sq.failed = true;
+      if (params.greedy) {
+        sq.tokens.resize(std::min((int)sq.tokens.size(), sq.result_len));
+        score_sequence(sq, params);
+        if (!sq.failed && sq.result_len > 32 && sq.entropy < params.entropy_thold) sq.failed = true;
+      }
       sq.no_speech_prob = nosp;
       best = sq;
       bool success = true;
