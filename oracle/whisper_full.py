@@ -144,6 +144,9 @@ class WhisperState:
         self.lang_id = 0
         self.result_all = []
         self.stats = {"encode": 0, "decode_tokens": 0, "decode_calls": 0}
+        # whisper_decoder::rng (std::mt19937): decoder 0 seeded once per state, decoders >= 1
+        # re-seeded with 0 on every whisper_full call (WHISPER_DECODER_INIT) -- parity unpinned
+        self.rngs = [np.random.RandomState(0)] + [None] * 15
 
     # ------------------------------------------------------------ logits
     def process_logits(self, logits, tokens_cur, has_ts, seek_delta, params, temperature, force):
@@ -224,6 +227,8 @@ class WhisperState:
     def full(self, samples: np.ndarray, params: FullParams):
         v, m, hp = self.v, self.m, self.m.hp
         self.result_all = []
+        for j in range(1, len(self.rngs)):
+            self.rngs[j] = np.random.RandomState(0)
         n = samples.shape[0]
         mel = log_mel(samples, hp.n_mels)
         energy = None
@@ -288,8 +293,6 @@ class WhisperState:
                 prompt_past = []
             best = None
             for it, t_cur in enumerate(temps):
-                if t_cur > 0:
-                    raise NotImplementedError("sampling fallback not restated in the oracle")
                 prompt = []
                 if prompt_past and t_cur < 0.5 and params.n_max_text_ctx > 0:
                     n_take = min(min(params.n_max_text_ctx, n_text_ctx // 2), len(prompt_past))
@@ -308,9 +311,12 @@ class WhisperState:
                 seq = dict(tokens=[], result_len=0, seek_delta=N_FRAMES, has_ts=False,
                            failed=False, completed=False)
                 n_max = n_text_ctx // 2 - 4
-                if params.strategy != "greedy":
+                single = params.strategy == "greedy" and t_cur <= 0
+                if t_cur > 0:
+                    seq = self.decode_sample(st, logits, cross, params, t_cur, seek, seek_end, L, window)
+                elif params.strategy != "greedy":
                     seq = self.decode_beam(st, logits, cross, prompt, params, t_cur, seek, seek_end, L, window)
-                for i in range(n_max if params.strategy == "greedy" else 0):
+                for i in range(n_max if single else 0):
                     force = None
                     if L:
                         if i == 0:
@@ -354,7 +360,7 @@ class WhisperState:
                     self.stats["decode_calls"] += 1
                     self.stats["decode_tokens"] += 1
                 # rank (single decoder)
-                if params.strategy == "greedy":
+                if single:
                     seq["tokens"] = seq["tokens"][:seq["result_len"]]
                     score_sequence(seq, params)
                     if seq["failed"] is False and seq["result_len"] > 32 and seq["entropy"] < params.entropy_thold:
@@ -397,6 +403,106 @@ class WhisperState:
                 seek_delta = min(seek_end - seek, N_FRAMES)
             seek += seek_delta
         return 0
+
+    # ------------------------------------------------------------ temperature sampling
+    @staticmethod
+    def discrete_draw(rs, weights):
+        """libstdc++ std::discrete_distribution<int>(w.begin(), w.end())(mt19937): sequential
+        double sum, normalise, sequential partial sums with the last set to 1, then
+        lower_bound of generate_canonical<double, 53> (two 32-bit draws)."""
+        w = np.asarray(weights, np.float32).astype(np.float64)
+        tot = np.cumsum(w)[-1]
+        cp = np.cumsum(w / tot)
+        cp[-1] = 1.0
+        x0, x1 = rs.randint(0, 2 ** 32, size=2, dtype=np.uint32)
+        u = (float(x0) + float(x1) * 4294967296.0) / 18446744073709551616.0
+        if u >= 1.0:
+            u = np.nextafter(1.0, 0.0)
+        return int(np.searchsorted(cp, u, side="left"))
+
+    def decode_sample(self, st, logits, cross, params, t_cur, seek, seek_end, L, window):
+        """t > 0: best_of decoders share the prompt; each draws with its own rng
+        (whisper_sample_token, best = false); ranking as decode_beam."""
+        v = self.v
+        K = max(1, params.best_of)
+        n_max = self.m.hp.n_text_ctx // 2 - 4
+        dec = [dict(tokens=[], result_len=0, seek_delta=N_FRAMES, has_ts=False, failed=False, completed=False)
+               for _ in range(K)]
+        states = [st] + [st.copy() for _ in range(K - 1)]
+        row_logits = [logits] * K
+        for i in range(n_max):
+            act = [j for j in range(K) if not dec[j]["completed"] and not dec[j]["failed"]]
+            if not act:
+                break
+            force = None
+            if L:
+                if i == 0:
+                    force = ("only", v.beg)
+                elif i < L - 2:
+                    force = ("text", None)
+                elif i == L - 2:
+                    force = ("only", v.beg + min(1500, max(1, (window - DELTA_MIN - 1) // 2)))
+                else:
+                    force = ("only", v.eot)
+            for j in act:
+                d = dec[j]
+                _, lps, probs = self.process_logits(row_logits[j], d["tokens"], d["has_ts"], d["seek_delta"],
+                                                    params, t_cur, force)
+                ts = probs[v.beg:].astype(np.float64)
+                sum_ts = float(np.cumsum(ts)[-1]) if ts.size else 0.0
+                mx = float(ts.max()) if ts.size else 0.0
+                tid = v.beg + int(np.argmax(ts)) if mx > 0 else 0
+                tok = Token(id=self.discrete_draw(self.rngs[j], probs), tid=tid, pt=float(mx / (sum_ts + 1e-10)),
+                            ptsum=sum_ts)
+                tok.p, tok.plog = float(probs[tok.id]), float(lps[tok.id])
+                if tok.id >= v.beg:
+                    tok.tid, tok.pt = tok.id, tok.p
+                d["tokens"].append(tok)
+            for j in act:
+                d = dec[j]
+                tok = d["tokens"][-1]
+                if tok.id > v.beg:
+                    sdn = 2 * (tok.id - v.beg)
+                    if d["has_ts"] and d["seek_delta"] > sdn and d["result_len"] < i:
+                        d["failed"] = True
+                        continue
+                    d["seek_delta"] = sdn
+                    d["result_len"] = i + 1
+                    d["has_ts"] = True
+                if (tok.id == v.eot or (params.max_tokens > 0 and i >= params.max_tokens)
+                        or (d["has_ts"] and seek + d["seek_delta"] + DELTA_MIN >= seek_end)):
+                    if d["result_len"] == 0:
+                        if seek + d["seek_delta"] + DELTA_MIN >= seek_end:
+                            d["result_len"] = i + 1
+                        else:
+                            d["failed"] = True
+                            continue
+                    if params.single_segment:
+                        d["result_len"] = i + 1
+                        d["seek_delta"] = N_FRAMES
+                    d["completed"] = True
+                    continue
+                if i == n_max - 1 and (d["result_len"] == 0 or d["seek_delta"] < N_FRAMES // 2):
+                    d["failed"] = True
+            for j in [j for j in act if not dec[j]["completed"] and not dec[j]["failed"]]:
+                row_logits[j] = states[j].forward([dec[j]["tokens"][-1].id], cross)
+                self.stats["decode_calls"] += 1
+                self.stats["decode_tokens"] += 1
+        best, best_score = 0, -np.inf
+        for j, d in enumerate(dec):
+            if d["failed"]:
+                continue
+            d["tokens"] = d["tokens"][:d["result_len"]]
+            score_sequence(d, params)
+            if d["result_len"] > 32 and d["entropy"] < params.entropy_thold:
+                d["failed"] = True
+                continue
+            if best_score < d["score"]:
+                best, best_score = j, d["score"]
+        out = dec[best]
+        out["tokens"] = out["tokens"][:out["result_len"]]
+        score_sequence(out, params)
+        return out
 
     # ------------------------------------------------------------ beam search
     def topk(self, logprobs, k):

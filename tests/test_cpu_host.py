@@ -95,3 +95,24 @@ def test_synthetic_audio_is_deterministic():
     for (s0, e0, _), (s1, e1, _) in zip(sa, sa[1:]):
         assert 1.5 - 1e-3 <= e0 - s0 <= 8.0 + 1e-3
         assert s1 - e0 >= 0.3 - 1e-3
+
+
+def test_oracle_discrete_distribution_matches_libstdcxx(lib):
+    """The t > 0 draw (whisper_sample_token: std::discrete_distribution + std::mt19937):
+    oracle restatement vs the real libstdc++ through a host-only seam."""
+    import ctypes as C
+    from oracle.whisper_full import WhisperState
+    rng = np.random.default_rng(3)
+    for n, zeros in ((7, 0), (51866, 40000), (1, 0), (300, 299)):
+        w = rng.random(n).astype(np.float32) ** 4
+        if zeros:
+            w[rng.choice(n, zeros, replace=False)] = 0
+        if w.sum() == 0:
+            w[-1] = 1
+        out = np.zeros(64, np.int32)
+        seed = int(rng.integers(0, 2 ** 31))
+        _lib.check(lib.wdr_dbg_discrete(w.ctypes.data_as(C.POINTER(C.c_float)), n, seed, 64,
+                                        out.ctypes.data_as(C.POINTER(C.c_int32))))
+        rs = np.random.RandomState(seed)
+        want = [WhisperState.discrete_draw(rs, w) for _ in range(64)]
+        assert out.tolist() == want

@@ -96,21 +96,26 @@ def _params(lang="auto"):
                       entropy_thold=-1.0)
 
 
-@pytest.mark.parametrize("lang,strategy", [("auto", "greedy"), ("en", "greedy"), ("en", "beam_search"),
-                                           ("auto", "beam_search")])
-def test_state_full_matches_oracle(model, audio, lang, strategy):
-    """whisper_full_with_state: greedy and beam search (5 beams, whisper.cpp's default
-    strategy in the reference, src/transcribe.rs:25-33)."""
+@pytest.mark.parametrize("lang,strategy,temp", [("auto", "greedy", None), ("en", "greedy", None),
+                                                ("en", "beam_search", None), ("auto", "beam_search", None),
+                                                ("en", "greedy", 0.4), ("auto", "beam_search", 0.6)])
+def test_state_full_matches_oracle(model, audio, lang, strategy, temp):
+    """whisper_full_with_state: greedy, beam search (5 beams, whisper.cpp's default strategy in
+    the reference, src/transcribe.rs:25-33) and the t > 0 sampling decoders (best_of 5,
+    std::discrete_distribution + std::mt19937 per decoder)."""
     name, ctx, hp, W = model
     pcm, spurts = audio
     st = _oracle_state(name, hp, W)
-    opts = wdr.TranscribeOptions(lang=lang, advanced=wdr.AdvancedTranscribe(sampling_strategy=strategy))
+    opts = wdr.TranscribeOptions(lang=lang, advanced=wdr.AdvancedTranscribe(sampling_strategy=strategy,
+                                                                            temperature=temp))
     prompt = None
     for a, b, _ in spurts[:3]:
         x = pcm_i16_to_f32(pcm[int(a * 16000):int(b * 16000)])
         got, lang_id = ctx.state_full(x, opts, initial_prompt=prompt)
         p = _params(lang)
         p.strategy = "greedy" if strategy == "greedy" else "beam"
+        if temp is not None:
+            p.temperature = temp
         p.initial_prompt = prompt
         st.full(x, p)
         ref = st.result_all

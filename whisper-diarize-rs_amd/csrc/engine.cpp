@@ -16,6 +16,7 @@
 #include <fstream>
 #include <map>
 #include <memory>
+#include <random>
 #include <string>
 #include <sys/stat.h>
 #include <vector>
@@ -783,6 +784,17 @@ int wdr_speakers_assign(wdr_speakers* m, const float* emb, int32_t dim, float th
     const std::string id = m->m->assign(emb, dim, threshold);
     WDR_CHECK(cap > id.size(), "speaker id buffer too small");
     memcpy(id_out, id.c_str(), id.size() + 1);
+    return 0;
+  })
+}
+
+// host seam: libstdc++ std::discrete_distribution over f32 weights driven by std::mt19937(seed)
+// (the draw whisper_sample_token makes at t > 0), to pin the oracle's restatement
+int wdr_dbg_discrete(const float* w, size_t n, uint32_t seed, int32_t n_draws, int32_t* out) {
+  WDR_GUARD({
+    std::mt19937 g(seed);
+    std::discrete_distribution<> d(w, w + n);
+    for (int i = 0; i < n_draws; ++i) out[i] = d(g);
     return 0;
   })
 }

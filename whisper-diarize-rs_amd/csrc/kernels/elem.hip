@@ -673,6 +673,36 @@ void launch_logits_topk(const float* logits, int ld, const LogitsCtl* ctls, cons
   WDR_HIP(hipGetLastError());
 }
 
+// temperature sampling (t > 0): the full processed distribution of each row, p and log p,
+// for the host-side std::discrete_distribution draw (whisper_sample_token, best = false)
+__global__ __launch_bounds__(256) void k_logits_probs(const float* logits, int ld, const LogitsCtl* ctls, VocabIds v,
+                                                      const LgStats* st, float* probs, float* logprobs) {
+  __shared__ LgStats g;
+  const int b = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
+  if (tid == 0) lg_global(st, r, g);
+  __syncthreads();
+  const float* L = logits + (long long)r * ld;
+  const LogitsCtl c = ctls[r];
+  const float lse = logf(g.s1) + g.m1;
+  const float ts_lp = (g.mts == -INFINITY || !(g.sts > 0.f)) ? -INFINITY : logf(g.sts) + (g.mts - lse);
+  const bool mask_text = ts_lp > g.mtx - lse;
+  const int V = v.n_vocab, chunk = (V + LG_NB - 1) / LG_NB;
+  const int i0 = b * chunk, i1 = min(V, i0 + chunk);
+  for (int i = i0 + tid; i < i1; i += 256) {
+    float x = rule_mask(L[i], i, c, v);
+    if (mask_text && i < v.beg) x = -INFINITY;
+    probs[(long long)r * V + i] = x == -INFINITY ? 0.f : __expf(x - lse);
+    logprobs[(long long)r * V + i] = x == -INFINITY ? -INFINITY : x - lse;
+  }
+}
+
+void launch_logits_probs(const float* logits, int ld, const LogitsCtl* ctls, const VocabIds& v, int R, float* work,
+                         float* probs, float* logprobs, hipStream_t s) {
+  const LgStats* st = (const LgStats*)work;   // written by launch_logits_process
+  hipLaunchKernelGGL(k_logits_probs, dim3(LG_NB, R), dim3(256), 0, s, logits, ld, ctls, v, st, probs, logprobs);
+  WDR_HIP(hipGetLastError());
+}
+
 // beam reorder: copy the first n_rows cached K/V rows of sequence src[p] to dst[p], every layer
 __global__ void k_kv_copy(f16* kc, f16* vc, long long seq_stride, int nslot, const int* pairs, int n_rows, int d) {
   const int l = blockIdx.y, p = blockIdx.z;

@@ -65,6 +65,8 @@ struct TokOut {
 };
 void launch_logits_topk(const float* logits, int ld, const LogitsCtl* ctls, const VocabIds& v, int R, int K,
                         float* work, BeamCand* out, hipStream_t s);
+void launch_logits_probs(const float* logits, int ld, const LogitsCtl* ctls, const VocabIds& v, int R, float* work,
+                         float* probs, float* logprobs, hipStream_t s);
 void launch_kv_copy(f16* kc, f16* vc, long long seq_stride, int nslot, int L, const int* pairs_dev, int n_pairs,
                     int n_rows, int d, hipStream_t s);
 void launch_logits_process(const float* logits, int ld, const LogitsCtl* ctls, const VocabIds& v, int R, float* work,

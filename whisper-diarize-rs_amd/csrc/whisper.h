@@ -160,6 +160,8 @@ class State {
   std::unique_ptr<Impl> m_;
   // pieces of full()
   void top_up(int job);
+  Seq decode_sample(const std::vector<int>& prompt, const FullParams& params, float t_cur, int seek, int seek_end,
+                    int Lf, int window, float* nosp);
   Seq decode_beam(const std::vector<int>& prompt, const FullParams& params, float t_cur, int seek, int seek_end, int Lf,
                   int window, float* nosp);
   void decoder_prefill(const int* toks, int n, int seq, bool want_logits, bool capture);

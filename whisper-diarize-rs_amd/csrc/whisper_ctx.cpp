@@ -10,6 +10,7 @@
 #include <cstring>
 #include <cstdlib>
 #include <map>
+#include <random>
 
 namespace wdr {
 
@@ -349,6 +350,9 @@ struct State::Impl {
   DevMem rows_tok, rows_pos, rows_seq;
   DevMem beamc, kvpairs;       // beam candidates [NSEQ][BEAM_KMAX], KV reorder (src, dst) pairs
   BeamCand* h_beam = nullptr;
+  DevMem sprobs, slogp;        // [NSEQ][V] sampled rows (t > 0)
+  std::vector<float> hp_probs, hp_logp;
+  std::mt19937 rng[NSEQ];      // whisper_decoder::rng
   int* h_pairs = nullptr;
   DevMem fpart_o, fpart_ml;   // split flash-attention partials (prefill cross-attention)
   DevMem kc, vc;
@@ -429,6 +433,9 @@ State::State(Context& ctx) : ctx_(ctx), s_(ctx.stream), m_(new Impl) {
   m.fpart_o = DevMem((size_t)12 * 256 * m.H * 64 * 4);
   m.fpart_ml = DevMem((size_t)12 * m.H * 256 * sizeof(float2));
   m.beamc = DevMem(NSEQ * BEAM_KMAX * sizeof(BeamCand));
+  m.sprobs = DevMem((size_t)NSEQ * m.V * 4);
+  m.slogp = DevMem((size_t)NSEQ * m.V * 4);
+  m.rng[0] = std::mt19937(0);   // decoder 0: seeded once per state
   m.kvpairs = DevMem(2 * 2 * NSEQ * 4);
   WDR_HIP(hipHostMalloc((void**)&m.h_beam, NSEQ * BEAM_KMAX * sizeof(BeamCand), hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_pairs, 2 * 2 * NSEQ * 4, hipHostMallocDefault));
@@ -1274,12 +1281,162 @@ Seq State::decode_beam(const std::vector<int>& prompt, const FullParams& params,
   return out;
 }
 
+// temperature fallback (t > 0): best_of decoders share the prompt and each draws its tokens
+// with std::discrete_distribution over the processed probabilities and its own std::mt19937
+// (whisper_sample_token with best = false); ranking as in beam search.  Mirrors
+// oracle/whisper_full.py WhisperState.decode_sample.
+Seq State::decode_sample(const std::vector<int>& prompt, const FullParams& params, float t_cur, int seek, int seek_end,
+                         int Lf, int window, float* nosp) {
+  Impl& m = *m_;
+  const Vocab& v = ctx_.vocab;
+  const int K = std::max(1, std::min(params.best_of, NSEQ));
+  const int n_max = ctx_.model.hp.n_text_ctx / 2 - 4;
+  const int P = (int)prompt.size();
+  const int delta_min = 10;
+  const int V = m.V;
+  std::vector<Seq> dec(K);
+  {
+    std::vector<std::pair<int, int>> share;
+    for (int j = 1; j < K; ++j) share.push_back({0, j});
+    kv_reorder(share, P);
+  }
+  m.hp_probs.resize((size_t)NSEQ * V);
+  m.hp_logp.resize((size_t)NSEQ * V);
+  std::vector<TokenData> td(NSEQ);
+  for (int i = 0; i < n_max; ++i) {
+    std::vector<int> act;
+    for (int j = 0; j < K; ++j)
+      if (!dec[j].completed && !dec[j].failed) act.push_back(j);
+    if (act.empty()) break;
+    std::vector<LogitsCtl> ctl(act.size());
+    for (size_t r = 0; r < act.size(); ++r) {
+      const Seq& d = dec[act[r]];
+      LogitsCtl& c = ctl[r];
+      c = LogitsCtl{};
+      c.n_tokens = (int)d.tokens.size();
+      c.last_ts = !d.tokens.empty() && d.tokens.back().id >= v.beg;
+      c.pen_ts = d.tokens.size() < 2 || d.tokens[d.tokens.size() - 2].id >= v.beg;
+      c.has_ts = d.has_ts;
+      c.seek_delta = d.seek_delta;
+      c.temperature = t_cur;
+      if (Lf) {
+        if (i == 0) { c.force_kind = 1; c.force_tok = v.beg; }
+        else if (i < Lf - 2) c.force_kind = 2;
+        else if (i == Lf - 2) { c.force_kind = 1; c.force_tok = v.beg + std::min(1500, std::max(1, (window - delta_min - 1) / 2)); }
+        else { c.force_kind = 1; c.force_tok = v.eot; }
+      }
+    }
+    int R = (int)act.size();
+    if (i == 0) {
+      float ns = 0.f;
+      run_logits(1, ctl.data(), td.data(), &ns);
+      *nosp = ns;
+      R = 1;
+    } else {
+      std::vector<int> toks(act.size()), seqs(act.size()), pos(act.size(), P + i - 1);
+      for (size_t r = 0; r < act.size(); ++r) {
+        toks[r] = dec[act[r]].tokens.back().id;
+        seqs[r] = act[r];
+      }
+      decoder_step(toks.data(), seqs.data(), pos.data(), R);
+      run_logits(R, ctl.data(), td.data(), nullptr);
+    }
+    launch_logits_probs(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, m.work.as<float>(),
+                        m.sprobs.as<float>(), m.slogp.as<float>(), s_);
+    WDR_HIP(hipMemcpyAsync(m.hp_probs.data(), m.sprobs.p, (size_t)R * V * 4, hipMemcpyDeviceToHost, s_));
+    WDR_HIP(hipMemcpyAsync(m.hp_logp.data(), m.slogp.p, (size_t)R * V * 4, hipMemcpyDeviceToHost, s_));
+    WDR_HIP(hipStreamSynchronize(s_));
+    for (size_t a = 0; a < act.size(); ++a) {
+      const int j = act[a];
+      const int r = i == 0 ? 0 : (int)a;   // at i == 0 every decoder holds the prompt's distribution
+      const float* pr = m.hp_probs.data() + (size_t)r * V;
+      std::discrete_distribution<> dist(pr, pr + V);
+      TokenData t;
+      {   // timestamp statistics exactly as whisper_sample_token (sequential double sums)
+        double sum_ts = 0.0, max_ts = 0.0;
+        int tid = 0;
+        for (int q = v.beg; q < V; ++q) {
+          sum_ts += pr[q];
+          if (max_ts < pr[q]) {
+            max_ts = pr[q];
+            tid = q;
+          }
+        }
+        t.tid = tid;
+        t.pt = (float)(max_ts / (sum_ts + 1e-10));
+        t.ptsum = (float)sum_ts;
+      }
+      t.id = dist(m.rng[j]);
+      t.p = pr[t.id];
+      t.plog = m.hp_logp[(size_t)r * V + t.id];
+      if (t.id >= v.beg) {
+        t.tid = t.id;
+        t.pt = t.p;
+      }
+      dec[j].tokens.push_back(t);
+    }
+    for (int j : act) {
+      Seq& d = dec[j];
+      const TokenData& tok = d.tokens.back();
+      if (tok.id > v.beg) {
+        const int sdn = 2 * (tok.id - v.beg);
+        if (d.has_ts && d.seek_delta > sdn && d.result_len < i) {
+          d.failed = true;
+          continue;
+        }
+        d.seek_delta = sdn;
+        d.result_len = i + 1;
+        d.has_ts = true;
+      }
+      if (tok.id == v.eot || (params.max_tokens > 0 && i >= params.max_tokens) ||
+          (d.has_ts && seek + d.seek_delta + delta_min >= seek_end)) {
+        if (d.result_len == 0) {
+          if (seek + d.seek_delta + delta_min >= seek_end) {
+            d.result_len = i + 1;
+          } else {
+            d.failed = true;
+            continue;
+          }
+        }
+        if (params.single_segment) {
+          d.result_len = i + 1;
+          d.seek_delta = 3000;
+        }
+        d.completed = true;
+        continue;
+      }
+      if (i == n_max - 1 && (d.result_len == 0 || d.seek_delta < 3000 / 2)) d.failed = true;
+    }
+  }
+  int best = 0;
+  double best_score = -INFINITY;
+  for (int j = 0; j < K; ++j) {
+    Seq& d = dec[j];
+    if (d.failed) continue;
+    d.tokens.resize(std::min((int)d.tokens.size(), d.result_len));
+    score_sequence(d, params);
+    if (d.result_len > 32 && d.entropy < params.entropy_thold) {
+      d.failed = true;
+      continue;
+    }
+    if (best_score < d.score) {
+      best_score = d.score;
+      best = j;
+    }
+  }
+  Seq out = dec[best];
+  out.tokens.resize(std::min((int)out.tokens.size(), out.result_len));
+  score_sequence(out, params);
+  return out;
+}
+
 int State::full(const FullParams& params, const float* samples, int n, int job) {
   WDR_HIP(hipSetDevice(ctx_.cp.gpu_device));
   Impl& m = *m_;
   const Vocab& v = ctx_.vocab;
   const HParams& hp = ctx_.model.hp;
   result_all.clear();
+  for (int j = 1; j < NSEQ; ++j) m.rng[j] = std::mt19937(0);   // WHISPER_DECODER_INIT, every call
   double t_start = now_s();
   const bool planned = job >= 0 && job < (int)m.plan.pcm.size();
   // the slot goes back to the encode-ahead ring once this segment's last kernel has run
@@ -1384,7 +1541,6 @@ int State::full(const FullParams& params, const float* samples, int n, int job) 
     const double t_dec = now_s();
     for (size_t it = 0; it < temps.size(); ++it) {
       const float t_cur = temps[it];
-      WDR_CHECK(t_cur <= 0.0f, "temperature fallback sampling (t > 0) is not available yet");
       prompt.clear();
       if (!prompt_past.empty() && t_cur < 0.5f && params.n_max_text_ctx > 0) {
         const int n_take = std::min(std::min(params.n_max_text_ctx, n_text_ctx / 2), (int)prompt_past.size());
@@ -1399,10 +1555,13 @@ int State::full(const FullParams& params, const float* samples, int n, int job) 
       Seq sq;
       const int n_max = n_text_ctx / 2 - 4;
       float nosp = 0.f;
-      if (!params.greedy) {
+      const bool single = params.greedy && t_cur <= 0.f;
+      if (t_cur > 0.f) {
+        sq = decode_sample(prompt, params, t_cur, seek, seek_end, Lf, window, &nosp);
+      } else if (!params.greedy) {
         sq = decode_beam(prompt, params, t_cur, seek, seek_end, Lf, window, &nosp);
       }
-      for (int i = 0; i < n_max && params.greedy; ++i) {
+      for (int i = 0; i < n_max && single; ++i) {
         LogitsCtl c{};
         c.n_tokens = (int)sq.tokens.size();
         c.last_ts = !sq.tokens.empty() && sq.tokens.back().id >= v.beg;
@@ -1460,7 +1619,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job) 
           break;
         }
       }
-      if (params.greedy) {
+      if (single) {
         sq.tokens.resize(std::min((int)sq.tokens.size(), sq.result_len));
         score_sequence(sq, params);
         if (!sq.failed && sq.result_len > 32 && sq.entropy < params.entropy_thold) sq.failed = true;
