@@ -14,6 +14,8 @@
 //    <=8 decoder rows of a step: the 1500 cross keys are split in 128-key chunks over
 //    workgroups so every CU streams the cross K/V once for all beams.
 //  * k_aheads_capture — softmax(QK^T) of the alignment heads over all 1500 keys.
+#include <cstdlib>
+
 #include "../common.h"
 #include "kernels.h"
 #include "../prof.h"
@@ -239,8 +241,18 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecSelfArgs a) {
   if (lane == 0) red[1][wid] = sum;
   __syncthreads();
   const float inv = 1.f / (red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  // P.V: wave w takes keys w, w+4, ... in the same order as before, with 8 independent V
+  // loads in flight per lane instead of one dependent load per key
   float acc = 0.f;
-  for (int k = wid; k < nk; k += 4) {
+  int k = wid;
+  for (; k + 28 < nk; k += 32) {
+    float vv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vv[j] = (float)V[(long long)(k + 4 * j) * a.d + lane];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += (float)(f16)(sc[k + 4 * j] * inv) * vv[j];
+  }
+  for (; k < nk; k += 4) {
     const float p = (float)(f16)(sc[k] * inv);
     acc += p * (float)V[(long long)k * a.d + lane];
   }

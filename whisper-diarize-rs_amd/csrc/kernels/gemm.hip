@@ -221,68 +221,145 @@ __device__ __forceinline__ void gemv_store(const ProjArgs& a, float (&acc)[MR], 
   }
 }
 
-// LN prologue, M <= 2, K <= 512*NCH: normalised rows live in registers.
-template <int EPI, int MR, int NCH>
-__global__ __launch_bounds__(256) void k_gemv_ln(ProjArgs a) {
+// Decode GEMV for M <= 2 (the hot path of every greedy step): each wave owns R consecutive
+// weight rows and issues ALL of their loads before anything else, then (optionally) the
+// LayerNorm of the activation rows -- computed once per wave and amortised over its R rows,
+// its latency hidden under the weight stream -- then the dot products and the fused epilogue.
+// grid = ceil(N / 4R), one pass, no grid-stride loop.
+template <int EPI, int MR, int R, int NCH, bool LN>
+__global__ __launch_bounds__(256) void k_dgemv(ProjArgs a) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  // the first weight row is requested before the LayerNorm so its latency overlaps the norm
-  int n = blockIdx.x * 4 + wid;
-  f16x8 wv[NCH];
-  if (n < a.N) {
+  const int n0 = (blockIdx.x * 4 + wid) * R;
+  const int K = a.K, M = a.M;
+  // Every load below is unconditional (clamped address, masked value): no exec-mask branch
+  // per load, so the whole batch issues back to back.
+  int kc[NCH];
+  bool kin[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int k = c * 512 + lane * 8;
+    kin[c] = k < K;
+    kc[c] = kin[c] ? k : K - 8;
+  }
+  // 1. activations (+ LayerNorm parameters) first: they are L2 hits, and the in-order return of
+  //    vector loads means the LayerNorm can then run while the weight stream is in flight
+  float xf[LN ? MR : 1][LN ? NCH : 1][8];
+  float gv[LN ? NCH : 1][8], bv[LN ? NCH : 1][8];
+  f16x8 xr[MR][NCH];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) {
+    const int mm = m < M ? m : M - 1;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      if constexpr (LN) {
+        const float* xs = a.ln_x + (size_t)mm * a.ldln + kc[c];
+        const float4 p0 = *(const float4*)xs, p1 = *(const float4*)(xs + 4);
+        xf[m][c][0] = p0.x; xf[m][c][1] = p0.y; xf[m][c][2] = p0.z; xf[m][c][3] = p0.w;
+        xf[m][c][4] = p1.x; xf[m][c][5] = p1.y; xf[m][c][6] = p1.z; xf[m][c][7] = p1.w;
+        if (!kin[c])
+#pragma unroll
+          for (int e = 0; e < 8; ++e) xf[m][c][e] = 0.f;
+      } else {
+        const f16x8 t = *(const f16x8*)(a.A + (size_t)mm * a.lda + kc[c]);
+        xr[m][c] = kin[c] ? t : (f16x8){};
+      }
+    }
+  }
+  if constexpr (LN) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const float4 g0 = *(const float4*)(a.ln_g + kc[c]), g1 = *(const float4*)(a.ln_g + kc[c] + 4);
+      const float4 b0 = *(const float4*)(a.ln_b + kc[c]), b1 = *(const float4*)(a.ln_b + kc[c] + 4);
+      gv[c][0] = g0.x; gv[c][1] = g0.y; gv[c][2] = g0.z; gv[c][3] = g0.w;
+      gv[c][4] = g1.x; gv[c][5] = g1.y; gv[c][6] = g1.z; gv[c][7] = g1.w;
+      bv[c][0] = b0.x; bv[c][1] = b0.y; bv[c][2] = b0.z; bv[c][3] = b0.w;
+      bv[c][4] = b1.x; bv[c][5] = b1.y; bv[c][6] = b1.z; bv[c][7] = b1.w;
+    }
+  }
+  // 2. the weight stream: every load of the wave's R rows in flight at once
+  f16x8 wv[R][NCH];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int n = n0 + r < a.N ? n0 + r : a.N - 1;
     const f16* w = a.B + (size_t)n * a.ldb;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      const int k = c * 512 + lane * 8;
-      wv[c] = k < a.K ? *(const f16x8*)(w + k) : (f16x8){};
+      const f16x8 t = *(const f16x8*)(w + kc[c]);
+      wv[r][c] = kin[c] ? t : (f16x8){};
     }
   }
-  f16x8 xr[MR][NCH];
+  const int mrow = lane < M ? lane : 0;   // lane m stores output row m
+  float pbias[R], pold[R];
+  long long cdst = 0;
 #pragma unroll
-  for (int r = 0; r < MR; ++r) {
-    if (r < a.M) ln_row_regs<NCH>(a, r, lane, xr[r]);
+  for (int r = 0; r < R; ++r) {
+    const int n = n0 + r < a.N ? n0 + r : a.N - 1;
+    pbias[r] = a.bias ? a.bias[n] : 0.f;
+    pold[r] = 0.f;
+    if constexpr (EPI == EPI_F32_RESID) pold[r] = ((const float*)a.out)[(size_t)mrow * a.ldo + n];
   }
-  for (; n < a.N; n += gridDim.x * 4) {
-    if (n != blockIdx.x * 4 + wid) {
-      const f16* w = a.B + (size_t)n * a.ldb;
+  if constexpr (EPI == EPI_QKV_CACHE) cdst = a.row_seq[mrow] * a.seq_stride + (long long)a.row_pos[mrow] * a.d;
+  // 3. LayerNorm (ggml_norm, eps 1e-5) once per wave, amortised over its R rows
+  if constexpr (LN) {
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const int k = c * 512 + lane * 8;
-        wv[c] = k < a.K ? *(const f16x8*)(w + k) : (f16x8){};
-      }
+    for (int m = 0; m < MR; ++m) {
+      float sm = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sm += xf[m][c][e];
+      sm = wave_sum(sm);
+      const float mean = sm / a.K;
+      float s2 = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float t = xf[m][c][e] - mean;
+          s2 += kin[c] ? t * t : 0.f;
+        }
+      s2 = wave_sum(s2);
+      const float scale = 1.0f / sqrtf(s2 / a.K + 1e-5f);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xr[m][c][e] = (f16)((xf[m][c][e] - mean) * scale * gv[c][e] + bv[c][e]);
     }
+  }
+  // 4. dot products, wave reductions, fused epilogue
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int n = n0 + r;
     float acc[MR];
 #pragma unroll
-    for (int r = 0; r < MR; ++r) {
-      acc[r] = 0.f;
+    for (int m = 0; m < MR; ++m) {
+      acc[m] = 0.f;
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) acc[r] = dot8(wv[c], xr[r][c], acc[r]);
+      for (int c = 0; c < NCH; ++c) acc[m] = dot8(wv[r][c], xr[m][c], acc[m]);
+      acc[m] = wave_sum(acc[m]);
     }
-    gemv_store<EPI, MR>(a, acc, lane, n);
-  }
-}
-
-// No-LN GEMV for M <= 2 with K = 512*NCH exactly: every weight and activation load of the
-// row is issued before the first dot product (K = 5120 keeps 10 KB per wave in flight).
-template <int EPI, int MR, int NCH>
-__global__ __launch_bounds__(256) void k_gemv_nc(ProjArgs a) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int n = blockIdx.x * 4 + wid; n < a.N; n += gridDim.x * 4) {
-    const f16* w = a.B + (size_t)n * a.ldb + lane * 8;
-    f16x8 wv[NCH], xv[MR][NCH];
+    if (n >= a.N || lane >= MR || lane >= a.M) continue;
+    float v = acc[0];
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) wv[c] = *(const f16x8*)(w + c * 512);
-#pragma unroll
-    for (int r = 0; r < MR; ++r)
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) xv[r][c] = *(const f16x8*)(a.A + (size_t)r * a.lda + c * 512 + lane * 8);
-    float acc[MR];
-#pragma unroll
-    for (int r = 0; r < MR; ++r) {
-      acc[r] = 0.f;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) acc[r] = dot8(wv[c], xv[r][c], acc[r]);
+    for (int m = 1; m < MR; ++m)
+      if (lane == m) v = acc[m];
+    v += pbias[r];
+    const size_t o = (size_t)lane * a.ldo + n;
+    if constexpr (EPI == EPI_F16) {
+      ((f16*)a.out)[o] = (f16)v;
+    } else if constexpr (EPI == EPI_F16_GELU) {
+      ((f16*)a.out)[o] = (f16)gelu_tanh(v);
+    } else if constexpr (EPI == EPI_F32_RESID) {
+      ((float*)a.out)[o] = pold[r] + v;
+    } else if constexpr (EPI == EPI_F32) {
+      ((float*)a.out)[o] = v;
+    } else if constexpr (EPI == EPI_QKV_CACHE) {
+      if (n < a.d) ((f16*)a.out)[o] = (f16)v;
+      else if (n < 2 * a.d) a.kc[cdst + n - a.d] = (f16)v;
+      else a.vc[cdst + n - 2 * a.d] = (f16)v;
+    } else {
+      epi_store<EPI>(a, lane, n, v - pbias[r]);
     }
-    gemv_store<EPI, MR>(a, acc, lane, n);
   }
 }
 
@@ -388,32 +465,31 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
     const int nwg = std::min(cdiv(a.N, 4), 1024);
     dim3 grid(nwg), blk(256);
     const bool ln = a.ln_x != nullptr;
-    if (ln && a.M <= 2 && a.K <= 1536) {
-      const int nch = cdiv(a.K, 512);
-#define WDR_GLN(MR, NCH) wdr_launch(PROF_GEMV, bytes, flops, k_gemv_ln<EPI, MR, NCH>, grid, blk, 0, s, a);
-      if (a.M == 1) {
-        if (nch == 1) { WDR_GLN(1, 1) } else if (nch == 2) { WDR_GLN(1, 2) } else { WDR_GLN(1, 3) }
-      } else {
-        if (nch == 1) { WDR_GLN(2, 1) } else if (nch == 2) { WDR_GLN(2, 2) } else { WDR_GLN(2, 3) }
-      }
-#undef WDR_GLN
-    } else if (!ln && a.M <= 2 && a.K % 512 == 0 && a.K <= 5120) {
-      const int nch = a.K / 512;
-#define WDR_GNC(MR, NCH) wdr_launch(PROF_GEMV, bytes, flops, k_gemv_nc<EPI, MR, NCH>, grid, blk, 0, s, a);
-#define WDR_GNC_M(MR)                                                          \
-  switch (nch) {                                                               \
-    case 1: WDR_GNC(MR, 1) break;                                              \
-    case 2: WDR_GNC(MR, 2) break;                                              \
-    case 3: WDR_GNC(MR, 3) break;                                              \
-    case 4: WDR_GNC(MR, 4) break;                                              \
-    case 6: WDR_GNC(MR, 6) break;                                              \
-    case 8: WDR_GNC(MR, 8) break;                                              \
-    case 10: WDR_GNC(MR, 10) break;                                            \
-    default: wdr_launch(PROF_GEMV, bytes, flops, k_gemv<EPI, MR, false>, grid, blk, 0, s, a); \
+    const int nch = cdiv(a.K, 512);
+    if (a.M <= 2 && ((ln && a.K <= 1536) || (!ln && a.K <= 5120 && (a.K % 512 == 0 || a.K <= 1536)))) {
+      // two rows per wave once there are enough rows to keep every CU busy
+      const int R = a.N >= 1024 ? 2 : 1;
+      dim3 g2(cdiv(a.N, 4 * R));
+#define WDR_DG(MR, RR, NCH)                                                                               \
+  if (ln) wdr_launch(PROF_GEMV, bytes, flops, k_dgemv<EPI, MR, RR, NCH, true>, g2, blk, 0, s, a);        \
+  else wdr_launch(PROF_GEMV, bytes, flops, k_dgemv<EPI, MR, RR, NCH, false>, g2, blk, 0, s, a);
+#define WDR_DG_N(MR, RR)                                                                                  \
+  switch (nch) {                                                                                          \
+    case 1: WDR_DG(MR, RR, 1) break;                                                                      \
+    case 2: WDR_DG(MR, RR, 2) break;                                                                      \
+    case 3: WDR_DG(MR, RR, 3) break;                                                                      \
+    case 4: if (!ln) { wdr_launch(PROF_GEMV, bytes, flops, k_dgemv<EPI, MR, RR, 4, false>, g2, blk, 0, s, a); } break; \
+    case 6: if (!ln) { wdr_launch(PROF_GEMV, bytes, flops, k_dgemv<EPI, MR, RR, 6, false>, g2, blk, 0, s, a); } break; \
+    case 8: if (!ln) { wdr_launch(PROF_GEMV, bytes, flops, k_dgemv<EPI, MR, RR, 8, false>, g2, blk, 0, s, a); } break; \
+    default: if (!ln) { wdr_launch(PROF_GEMV, bytes, flops, k_dgemv<EPI, MR, RR, 10, false>, g2, blk, 0, s, a); } break; \
   }
-      if (a.M == 1) { WDR_GNC_M(1) } else { WDR_GNC_M(2) }
-#undef WDR_GNC_M
-#undef WDR_GNC
+      if (a.M == 1) {
+        if (R == 2) { WDR_DG_N(1, 2) } else { WDR_DG_N(1, 1) }
+      } else {
+        if (R == 2) { WDR_DG_N(2, 2) } else { WDR_DG_N(2, 1) }
+      }
+#undef WDR_DG_N
+#undef WDR_DG
     } else {
       const uint32_t lds = ln ? (uint32_t)a.M * a.K * 2 : 0;
 #define WDR_GEMV(MR)                                                                          \

@@ -713,7 +713,7 @@ void State::decoder_prefill(const int* toks, int n, int seq, bool want_logits, b
     } else {
       XAttnArgs xa{m.qx.as<f16>(), d, xk, xv, ldxkv, 1500, n, hp.n_text_head, scale, m.part_o.as<float>(),
                    m.part_ml.as<float2>(), m.attd.as<f16>(), d};
-      launch_xattn(xa, s_);
+        launch_xattn(xa, s_);
     }
     proj(s_, m.attd.as<f16>(), d, e.w_xo, d, e.b_xo, m.xd.p, d, n, d, d, EPI_F32_RESID);
     launch_layernorm(m.xd.as<float>(), d, e.ln3_g, e.ln3_b, m.hd.as<f16>(), d, n, d, s_);
