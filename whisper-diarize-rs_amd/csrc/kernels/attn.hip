@@ -332,6 +332,51 @@ __global__ __launch_bounds__(256) void k_xattn_partial(XAttnArgs a) {
   if (tid < R) a.part_ml[((long long)c * R + tid) * a.n_head + h] = mls[tid];
 }
 
+// One decoder row (greedy steps): thread t takes key t/4 of the chunk and dims 16*(t%4)..+16
+// for q.k with K read straight from HBM (no LDS staging), V goes through LDS with 16-B loads,
+// and all four waves share the P.V (16 keys each) instead of one wave doing all 64.
+__global__ __launch_bounds__(256) void k_xattn_partial1(XAttnArgs a) {
+  __shared__ __attribute__((aligned(16))) f16 Vs[XA_KC * 64];
+  __shared__ float red[2][4];
+  __shared__ float ps[XA_KC];
+  __shared__ float pv[4][64];
+  const int c = blockIdx.x, h = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int key0 = c * XA_KC;
+  const int kk = tid >> 2, qd = tid & 3;
+  const int key = key0 + kk;
+  const bool kok = key < a.Tk;
+  const long long row = (long long)(kok ? key : a.Tk - 1) * a.ldkv + h * 64 + qd * 16;
+  const f16x8 k0 = *(const f16x8*)(a.k + row), k1 = *(const f16x8*)(a.k + row + 8);
+  const f16x8 v0 = *(const f16x8*)(a.v + row), v1 = *(const f16x8*)(a.v + row + 8);
+  const f16x8 q0 = *(const f16x8*)(a.q + h * 64 + qd * 16), q1 = *(const f16x8*)(a.q + h * 64 + qd * 16 + 8);
+  *(f16x8*)(Vs + kk * 64 + qd * 16) = v0;
+  *(f16x8*)(Vs + kk * 64 + qd * 16 + 8) = v1;
+  float sc = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sc += (float)q0[e] * (float)k0[e] + (float)q1[e] * (float)k1[e];
+  sc += __shfl_xor(sc, 1, 64);
+  sc += __shfl_xor(sc, 2, 64);
+  sc = kok ? sc * a.scale : -INFINITY;
+  const float wm = wave_max(sc);
+  if (lane == 0) red[0][wid] = wm;
+  __syncthreads();
+  const float mx = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+  const float p = sc == -INFINITY ? 0.f : __expf(sc - mx);
+  const float ws = wave_sum(qd == 0 ? p : 0.f);
+  if (qd == 0) ps[kk] = p;
+  if (lane == 0) red[1][wid] = ws;
+  __syncthreads();
+  float acc = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc += (float)(f16)ps[wid * 16 + j] * (float)Vs[(wid * 16 + j) * 64 + lane];
+  pv[wid][lane] = acc;
+  __syncthreads();
+  if (tid < 64) {
+    a.part_o[((long long)c * a.n_head + h) * 64 + tid] = pv[0][tid] + pv[1][tid] + pv[2][tid] + pv[3][tid];
+    if (tid == 0) a.part_ml[(long long)c * a.n_head + h] = make_float2(mx, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  }
+}
+
 template <int NS>
 __global__ __launch_bounds__(64) void k_xattn_combine(XAttnArgs a) {
   const int r = blockIdx.x, h = blockIdx.y, d = threadIdx.x;
@@ -352,9 +397,14 @@ __global__ __launch_bounds__(64) void k_xattn_combine(XAttnArgs a) {
 void launch_xattn(const XAttnArgs& a, hipStream_t s) {
   WDR_CHECK(a.R >= 1 && a.R <= XA_RMAX, "cross-attention decode: R out of range");
   const int nsplit = cdiv(a.Tk, XA_KC);
-  wdr_launch(PROF_XATTN, (double)a.Tk * a.n_head * 64 * 2 * 2, (double)a.R * a.Tk * a.n_head * 64 * 4, k_xattn_partial,
-             dim3(nsplit, a.n_head), dim3(256), 0, s, a);
   WDR_CHECK(nsplit == 24, "cross-attention decode expects 1500 keys");
+  if (a.R == 1) {
+    wdr_launch(PROF_XATTN, (double)a.Tk * a.n_head * 64 * 2 * 2, (double)a.Tk * a.n_head * 64 * 4, k_xattn_partial1,
+               dim3(nsplit, a.n_head), dim3(256), 0, s, a);
+  } else {
+    wdr_launch(PROF_XATTN, (double)a.Tk * a.n_head * 64 * 2 * 2, (double)a.R * a.Tk * a.n_head * 64 * 4,
+               k_xattn_partial, dim3(nsplit, a.n_head), dim3(256), 0, s, a);
+  }
   hipLaunchKernelGGL(k_xattn_combine<24>, dim3(a.R, a.n_head), dim3(64), 0, s, a);
   WDR_HIP(hipGetLastError());
 }
