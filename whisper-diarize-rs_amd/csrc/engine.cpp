@@ -443,28 +443,37 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
       }
     }
   } unplan_guard{*c->st};
-  for (size_t i = 0; i < segs.size(); ++i) {
+  // One-segment lag: segment i's DTW re-forwards run on the DTW stream while segment i+1
+  // decodes; segment i is then finished (word times, speakers, callbacks in order).  The
+  // prompt chain only needs segment i's text, which full() returns at once.
+  struct Pending {
+    size_t i = 0;
+    std::vector<ResultSeg> res;
+    std::vector<DtwTicket> tk;
+  };
+  std::vector<Pending> pend;
+  struct Drain {   // on an error, return any in-flight DTW jobs to the state's pools
+    wdr_context* c;
+    std::vector<Pending>& p;
+    ~Drain() {
+      for (auto& q : p)
+        for (auto& t : q.tk)
+          if (t.blk) {
+            try {
+              c->st->resolve_dtw(t, q.res);
+            } catch (...) {
+            }
+          }
+    }
+  } drain{c, pend};
+  auto finalize = [&](Pending& P) {
+    for (auto& t : P.tk) c->st->resolve_dtw(t, P.res);
+    const size_t i = P.i;
     const wdr_speech_segment& ss = segs[i];
-    if (have_prev) {
-      params.initial_prompt = previous_text;
-      params.has_initial_prompt = true;
-    }
-    if (cb && cb->is_cancelled && cb->is_cancelled(cb->user)) throw std::runtime_error("failed to transcribe");
-    int rc;
-    try {
-      rc = c->st->full(params, nullptr, 0, (int)i);
-    } catch (const std::exception& ex) {
-      throw std::runtime_error(std::string("failed to transcribe: ") + ex.what());
-    }
-    if (rc != 0) throw std::runtime_error("failed to transcribe");
-    if (!*has_lang) {
-      *detected_lang = kLangs[std::max(0, std::min(99, c->st->lang_id))];
-      *has_lang = true;
-    }
     const double base_offset = ss.start + user_offset;
     std::vector<float> emb(512);
     bool have_emb = false, emb_ok = false;
-    for (const ResultSeg& r : c->st->result_all) {
+    for (const ResultSeg& r : P.res) {
       std::string text = trim_start(r.text);
       const double approx_start = base_offset + cs_to_s(r.t0);
       const double approx_end = base_offset + cs_to_s(r.t1);
@@ -485,8 +494,6 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
         if (last.end > seg_start) last.end = seg_start;
         if (last.has_words && !last.words.empty() && last.words.back().end > last.end) last.words.back().end = last.end;
       }
-      have_prev = !trim(text).empty();
-      if (have_prev) previous_text = text;
       Seg s;
       s.start = seg_start;
       s.end = seg_end;
@@ -512,6 +519,42 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
       }
       out.push_back(std::move(s));
     }
+  };
+  for (size_t i = 0; i < segs.size(); ++i) {
+    if (have_prev) {
+      params.initial_prompt = previous_text;
+      params.has_initial_prompt = true;
+    }
+    if (cb && cb->is_cancelled && cb->is_cancelled(cb->user)) throw std::runtime_error("failed to transcribe");
+    int rc;
+    try {
+      rc = c->st->full(params, nullptr, 0, (int)i, /*async_dtw=*/true);
+    } catch (const std::exception& ex) {
+      throw std::runtime_error(std::string("failed to transcribe: ") + ex.what());
+    }
+    if (rc != 0) throw std::runtime_error("failed to transcribe");
+    if (!*has_lang) {
+      *detected_lang = kLangs[std::max(0, std::min(99, c->st->lang_id))];
+      *has_lang = true;
+    }
+    Pending cur;
+    cur.i = i;
+    cur.res = c->st->result_all;
+    cur.tk = c->st->take_dtw_jobs();
+    for (const ResultSeg& r : cur.res) {   // src/transcribe.rs:502 prompt chain
+      const std::string text = trim_start(r.text);
+      have_prev = !trim(text).empty();
+      if (have_prev) previous_text = text;
+    }
+    if (!pend.empty()) {
+      finalize(pend[0]);
+      pend.clear();
+    }
+    pend.push_back(std::move(cur));
+  }
+  if (!pend.empty()) {
+    finalize(pend[0]);
+    pend.clear();
   }
   return out;
 }

@@ -125,7 +125,15 @@ struct StageTimes {   // host wall-clock per phase (seconds), accumulated
   long long windows = 0, decode_steps = 0, prefills = 0;
 };
 
-struct Seq;   // one decoder's sequence (whisper_ctx.cpp)
+struct Seq;           // one decoder's sequence (whisper_ctx.cpp)
+struct PrefillBufs;   // a prefill's working set (whisper_ctx.cpp)
+
+// a window's DTW job in flight on the DTW stream (State::dtw_timestamps)
+struct DtwTicket {
+  int i0 = 0, n = 0;          // result range of the full() call that enqueued it
+  int* blk = nullptr;         // pinned tokens + times
+  void* event = nullptr;      // hipEvent_t
+};
 
 class State {
  public:
@@ -133,7 +141,11 @@ class State {
   ~State();
   // whisper_full_with_state on host f32 samples. Returns 0 on success.
   // job >= 0: segment `job` of the current plan (samples / n come from the plan).
-  int full(const FullParams& p, const float* samples, int n, int job = -1);
+  // async_dtw: leave the windows' DTW jobs in flight (take_dtw_jobs / resolve_dtw); otherwise
+  // full() resolves them into result_all before returning.
+  int full(const FullParams& p, const float* samples, int n, int job = -1, bool async_dtw = false);
+  std::vector<DtwTicket> take_dtw_jobs();
+  void resolve_dtw(DtwTicket& t, std::vector<ResultSeg>& segs);
   // encode-ahead: the pipeline's whole segment list (int16 PCM), see whisper_ctx.cpp
   void plan(const int16_t* const* pcm, const int* n, int count);
   void unplan();
@@ -165,6 +177,8 @@ class State {
   Seq decode_beam(const std::vector<int>& prompt, const FullParams& params, float t_cur, int seek, int seek_end, int Lf,
                   int window, float* nosp);
   void decoder_prefill(const int* toks, int n, int seq, bool want_logits, bool capture);
+  void prefill_on(const int* toks, int n, int seq, bool want_logits, bool capture, const PrefillBufs& b,
+                  hipStream_t st, const f16* xkv_base);
   void decoder_step(const int* toks, const int* seqs, const int* pos, int R);
   void decoder_step_body(int R);
   void step_and_sample(const int* toks, const int* seqs, const int* pos, const LogitsCtl* ctl, int R, TokenData* out,

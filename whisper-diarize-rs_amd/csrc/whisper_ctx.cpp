@@ -311,8 +311,19 @@ Context::~Context() {
 // ------------------------------------------------------------------ state buffers
 static constexpr int RMAX = 448;   // max decoder rows in one forward (n_text_ctx)
 static constexpr int NSEQ = 8;     // max decoder rows in one step
-static constexpr int NSLOT = 16;   // self-attention KV-cache sequences (beams + beam-reorder scratch)
+static constexpr int NSLOT = 17;   // self-attention KV-cache sequences (beams + beam-reorder scratch + DTW)
+static constexpr int DTW_SEQ = 16;  // the DTW re-forward's own sequence (runs on its own stream)
 static constexpr int NSPLIT = 24;  // cross-attention key chunks (1500 / 64)
+
+// Working set of a prefill: the decode stream's own (pointing at the buffers above) and the
+// DTW stream's private copy, so a window's DTW re-forward overlaps the next decode.
+struct PrefillBufs {
+  float* xd; f16* hd; f16* qkvd; f16* attd; f16* qx; f16* mlpd;
+  int* rows_tok; int* rows_pos; int* rows_seq;
+  float* fpart_o; float2* fpart_ml; float2* ml; float* cap; float* part_o; float2* part_ml;
+  float* logits;
+  int* h_rows;
+};
 
 struct State::Impl {
   int d, L, H, V, n_mels, kp1;
@@ -359,6 +370,22 @@ struct State::Impl {
   long long seq_stride = 0;   // elements per (layer, seq)
   // dtw
   DevMem nrm, xdtw, times;
+  PrefillBufs pb_main{}, pb_dtw{};
+  struct DtwSet {
+    DevMem xd, hd, qkvd, attd, qx, mlpd, rows_tok, rows_pos, rows_seq, fpart_o, fpart_ml, ml, cap, part_o, part_ml,
+        nrm, xdtw, times;
+  } dset;
+  hipStream_t sd = nullptr;        // DTW stream
+  hipEvent_t ev_sync = nullptr;    // decode-stream point the DTW stream waits for
+  hipEvent_t ev_dtw = nullptr;     // last DTW job enqueued (on-demand encodes wait for it)
+  struct DtwJob {
+    int i0 = 0, n = 0;             // result_all range of the full() call that produced it
+    int* blk = nullptr;            // pinned: tokens [3*RMAX] then times [RMAX + 8]
+    hipEvent_t done = nullptr;
+  };
+  std::vector<DtwJob> jobs;        // enqueued by the current full() call
+  std::vector<int*> blk_pool;
+  std::vector<hipEvent_t> ev_pool;
   // host pinned
   int* h_rows = nullptr;       // 3 * RMAX
   TokOut* h_tok = nullptr;
@@ -448,10 +475,44 @@ State::State(Context& ctx) : ctx_(ctx), s_(ctx.stream), m_(new Impl) {
   m.nrm = DevMem((size_t)A * RMAX * 1500 * 4);
   m.xdtw = DevMem((size_t)RMAX * 1500 * 4);
   m.times = DevMem((RMAX + 8) * 4);
+  {
+    Impl::DtwSet& D = m.dset;
+    D.xd = DevMem((size_t)RMAX * d * 4);
+    D.hd = DevMem((size_t)RMAX * d * 2);
+    D.qkvd = DevMem((size_t)RMAX * 3 * d * 2);
+    D.attd = DevMem((size_t)RMAX * d * 2);
+    D.qx = DevMem((size_t)RMAX * d * 2);
+    D.mlpd = DevMem((size_t)RMAX * 4 * d * 2);
+    D.rows_tok = DevMem(RMAX * 4);
+    D.rows_pos = DevMem(RMAX * 4);
+    D.rows_seq = DevMem(RMAX * 4);
+    D.fpart_o = DevMem((size_t)12 * 256 * m.H * 64 * 4);
+    D.fpart_ml = DevMem((size_t)12 * m.H * 256 * sizeof(float2));
+    D.ml = DevMem((size_t)m.H * RMAX * sizeof(float2));
+    D.cap = DevMem((size_t)A * RMAX * 1500 * 4);
+    D.part_o = DevMem((size_t)NSPLIT * NSEQ * m.H * 64 * 4);
+    D.part_ml = DevMem((size_t)NSPLIT * NSEQ * m.H * sizeof(float2));
+    D.nrm = DevMem((size_t)A * RMAX * 1500 * 4);
+    D.xdtw = DevMem((size_t)RMAX * 1500 * 4);
+    D.times = DevMem((RMAX + 8) * 4);
+    m.pb_dtw = PrefillBufs{D.xd.as<float>(), D.hd.as<f16>(), D.qkvd.as<f16>(), D.attd.as<f16>(), D.qx.as<f16>(),
+                        D.mlpd.as<f16>(), D.rows_tok.as<int>(), D.rows_pos.as<int>(), D.rows_seq.as<int>(),
+                        D.fpart_o.as<float>(), D.fpart_ml.as<float2>(), D.ml.as<float2>(), D.cap.as<float>(),
+                        D.part_o.as<float>(), D.part_ml.as<float2>(), nullptr, nullptr};
+    int lo = 0, hi = 0;
+    WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    WDR_HIP(hipStreamCreateWithPriority(&m.sd, hipStreamNonBlocking, lo));
+    WDR_HIP(hipEventCreateWithFlags(&m.ev_sync, hipEventDisableTiming));
+    WDR_HIP(hipEventCreateWithFlags(&m.ev_dtw, hipEventDisableTiming));
+  }
   WDR_HIP(hipHostMalloc((void**)&m.h_rows, 3 * RMAX * 4, hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_tok, NSEQ * sizeof(TokOut), hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_ctl, NSEQ * sizeof(LogitsCtl), hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_times, (RMAX + 8) * 4, hipHostMallocDefault));
+  m.pb_main = PrefillBufs{m.xd.as<float>(), m.hd.as<f16>(), m.qkvd.as<f16>(), m.attd.as<f16>(), m.qx.as<f16>(),
+                       m.mlpd.as<f16>(), m.rows_tok.as<int>(), m.rows_pos.as<int>(), m.rows_seq.as<int>(),
+                       m.fpart_o.as<float>(), m.fpart_ml.as<float2>(), m.ml.as<float2>(), m.cap.as<float>(),
+                       m.part_o.as<float>(), m.part_ml.as<float2>(), m.logits.as<float>(), m.h_rows};
   const Vocab& v = ctx.vocab;
   m.vids = VocabIds{v.n_vocab, v.eot, v.sot, v.translate, v.transcribe, v.solm, v.prev, v.nosp, v.not_, v.beg,
                     v.token_to_id.at(" "), v.sot + 1, 100, -1, 1};
@@ -471,6 +532,18 @@ State::~State() {
       (void)hipStreamSynchronize(m_->es);
       (void)hipStreamDestroy(m_->es);
     }
+    if (m_->sd) {
+      (void)hipStreamSynchronize(m_->sd);
+      (void)hipStreamDestroy(m_->sd);
+    }
+    for (auto& j : m_->jobs) {
+      if (j.blk) m_->blk_pool.push_back(j.blk);
+      if (j.done) m_->ev_pool.push_back(j.done);
+    }
+    for (int* b : m_->blk_pool) (void)hipHostFree(b);
+    for (hipEvent_t e : m_->ev_pool) (void)hipEventDestroy(e);
+    if (m_->ev_sync) (void)hipEventDestroy(m_->ev_sync);
+    if (m_->ev_dtw) (void)hipEventDestroy(m_->ev_dtw);
     for (auto& sl : m_->slots) {
       if (sl.h_pcm) (void)hipHostFree(sl.h_pcm);
       if (sl.ready) (void)hipEventDestroy(sl.ready);
@@ -507,6 +580,7 @@ static void slot_reserve_x(State::Impl::Slot& sl, int n) {
 void State::compute_mel(const float* x_host, int n) {
   Impl& m = *m_;
   m.cur = m.S;
+  WDR_HIP(hipStreamWaitEvent(s_, m.ev_dtw, 0));   // the scratch slot may still feed a DTW job
   Impl::Slot& sl = m.slots[m.S];
   slot_reserve_x(sl, n);
   if (n > 0) WDR_HIP(hipMemcpyAsync(sl.x.p, x_host, (size_t)n * 4, hipMemcpyHostToDevice, s_));
@@ -661,68 +735,73 @@ void State::top_up(int j) {
 // Prefill of `n` tokens into sequence `seq` from an empty cache (positions 0..n-1):
 // whisper.cpp clears the KV cache before the prompt decode and before the DTW pass.
 void State::decoder_prefill(const int* toks, int n, int seq, bool want_logits, bool capture) {
+  prefill_on(toks, n, seq, want_logits, capture, m_->pb_main, s_, m_->xkv());
+}
+
+void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool capture, const PrefillBufs& b,
+                       hipStream_t st, const f16* xkv_base) {
   Impl& m = *m_;
   const Model& md = ctx_.model;
   const HParams& hp = md.hp;
   const int d = m.d, L = m.L;
   WDR_CHECK(n >= 1 && n <= RMAX, "decoder prefill: token count out of range");
   for (int i = 0; i < n; ++i) {
-    m.h_rows[i] = toks[i];
-    m.h_rows[RMAX + i] = i;
-    m.h_rows[2 * RMAX + i] = seq;
+    b.h_rows[i] = toks[i];
+    b.h_rows[RMAX + i] = i;
+    b.h_rows[2 * RMAX + i] = seq;
   }
-  WDR_HIP(hipMemcpyAsync(m.rows_tok.p, m.h_rows, n * 4, hipMemcpyHostToDevice, s_));
-  WDR_HIP(hipMemcpyAsync(m.rows_pos.p, m.h_rows + RMAX, n * 4, hipMemcpyHostToDevice, s_));
-  WDR_HIP(hipMemcpyAsync(m.rows_seq.p, m.h_rows + 2 * RMAX, n * 4, hipMemcpyHostToDevice, s_));
-  launch_embed(md.tok_emb, md.dec_pos, m.rows_tok.as<int>(), m.rows_pos.as<int>(), n, d, m.xd.as<float>(), s_);
+  WDR_HIP(hipMemcpyAsync(b.rows_tok, b.h_rows, n * 4, hipMemcpyHostToDevice, st));
+  WDR_HIP(hipMemcpyAsync(b.rows_pos, b.h_rows + RMAX, n * 4, hipMemcpyHostToDevice, st));
+  WDR_HIP(hipMemcpyAsync(b.rows_seq, b.h_rows + 2 * RMAX, n * 4, hipMemcpyHostToDevice, st));
+  launch_embed(md.tok_emb, md.dec_pos, b.rows_tok, b.rows_pos, n, d, b.xd, st);
   const float scale = 1.0f / 8.0f;
   const int ldxkv = L * 2 * d;
   for (int l = 0; l < L; ++l) {
     const DecLayer& e = md.dec[l];
     f16* kc = m.kc.as<f16>() + (size_t)l * NSLOT * m.seq_stride;
     f16* vc = m.vc.as<f16>() + (size_t)l * NSLOT * m.seq_stride;
-    launch_layernorm(m.xd.as<float>(), d, e.ln1_g, e.ln1_b, m.hd.as<f16>(), d, n, d, s_);
-    proj(s_, m.hd.as<f16>(), d, e.w_qkv, d, e.b_qkv, m.qkvd.p, 3 * d, n, 3 * d, d, EPI_F16);
-    launch_kv_scatter(m.qkvd.as<f16>(), 3 * d, d, m.rows_seq.as<int>(), m.rows_pos.as<int>(), n, kc, vc, m.seq_stride,
-                      s_);
-    FlashArgs sa{m.qkvd.as<f16>(), 3 * d, 0, m.qkvd.as<f16>() + d, 3 * d, 0, m.qkvd.as<f16>() + 2 * d, 3 * d, 0,
-                 m.attd.as<f16>(), d, 0, nullptr, n, n, hp.n_text_head, 1, scale};
-    launch_flash_attn(sa, 1, s_);
-    proj(s_, m.attd.as<f16>(), d, e.w_o, d, e.b_o, m.xd.p, d, n, d, d, EPI_F32_RESID);
-    launch_layernorm(m.xd.as<float>(), d, e.ln2_g, e.ln2_b, m.hd.as<f16>(), d, n, d, s_);
-    proj(s_, m.hd.as<f16>(), d, e.w_xq, d, e.b_xq, m.qx.p, d, n, d, d, EPI_F16);
-    const f16* xk = m.xkv() + (size_t)l * 2 * d;
+    launch_layernorm(b.xd, d, e.ln1_g, e.ln1_b, b.hd, d, n, d, st);
+    proj(st, b.hd, d, e.w_qkv, d, e.b_qkv, b.qkvd, 3 * d, n, 3 * d, d, EPI_F16);
+    launch_kv_scatter(b.qkvd, 3 * d, d, b.rows_seq, b.rows_pos, n, kc, vc, m.seq_stride,
+                      st);
+    FlashArgs sa{b.qkvd, 3 * d, 0, b.qkvd + d, 3 * d, 0, b.qkvd + 2 * d, 3 * d, 0,
+                 b.attd, d, 0, nullptr, n, n, hp.n_text_head, 1, scale};
+    launch_flash_attn(sa, 1, st);
+    proj(st, b.attd, d, e.w_o, d, e.b_o, b.xd, d, n, d, d, EPI_F32_RESID);
+    launch_layernorm(b.xd, d, e.ln2_g, e.ln2_b, b.hd, d, n, d, st);
+    proj(st, b.hd, d, e.w_xq, d, e.b_xq, b.qx, d, n, d, d, EPI_F16);
+    const f16* xk = xkv_base + (size_t)l * 2 * d;
     const f16* xv = xk + d;
     const bool cap_layer = capture && !ctx_.aheads_per_layer.empty() && !ctx_.aheads_per_layer[l].empty();
     if (n > NSEQ || cap_layer) {
-      FlashArgs xa{m.qx.as<f16>(), d, 0, xk, ldxkv, 0, xv, ldxkv, 0, m.attd.as<f16>(), d, 0,
-                   cap_layer ? m.ml.as<float2>() : nullptr, n, 1500, hp.n_text_head, 0, scale};
+      FlashArgs xa{b.qx, d, 0, xk, ldxkv, 0, xv, ldxkv, 0, b.attd, d, 0,
+                   cap_layer ? b.ml : nullptr, n, 1500, hp.n_text_head, 0, scale};
       if (n <= 256) {   // few queries: split the 1500 keys so every CU streams part of the cross K/V
         xa.nsplit = 12;
-        xa.part_o = m.fpart_o.as<float>();
-        xa.part_ml = m.fpart_ml.as<float2>();
+        xa.part_o = b.fpart_o;
+        xa.part_ml = b.fpart_ml;
       }
-      launch_flash_attn(xa, 1, s_);
+      launch_flash_attn(xa, 1, st);
       if (cap_layer) {
         int slot0 = 0;
         for (int q = 0; q < l; ++q) slot0 += (int)ctx_.aheads_per_layer[q].size();
-        CaptureArgs ca{m.qx.as<f16>(), d, xk, ldxkv, m.ml.as<float2>(), ctx_.aheads_dev.as<int>() + ctx_.aheads_dev_off[l],
-                       m.cap.as<float>(), slot0, n, 1500, scale};
-        launch_aheads_capture(ca, (int)ctx_.aheads_per_layer[l].size(), s_);
+        CaptureArgs ca{b.qx, d, xk, ldxkv, b.ml, ctx_.aheads_dev.as<int>() + ctx_.aheads_dev_off[l],
+                       b.cap, slot0, n, 1500, scale};
+        launch_aheads_capture(ca, (int)ctx_.aheads_per_layer[l].size(), st);
       }
     } else {
-      XAttnArgs xa{m.qx.as<f16>(), d, xk, xv, ldxkv, 1500, n, hp.n_text_head, scale, m.part_o.as<float>(),
-                   m.part_ml.as<float2>(), m.attd.as<f16>(), d};
-        launch_xattn(xa, s_);
+      XAttnArgs xa{b.qx, d, xk, xv, ldxkv, 1500, n, hp.n_text_head, scale, b.part_o,
+                   b.part_ml, b.attd, d};
+        launch_xattn(xa, st);
     }
-    proj(s_, m.attd.as<f16>(), d, e.w_xo, d, e.b_xo, m.xd.p, d, n, d, d, EPI_F32_RESID);
-    launch_layernorm(m.xd.as<float>(), d, e.ln3_g, e.ln3_b, m.hd.as<f16>(), d, n, d, s_);
-    proj(s_, m.hd.as<f16>(), d, e.w_fc1, d, e.b_fc1, m.mlpd.p, 4 * d, n, 4 * d, d, EPI_F16_GELU);
-    proj(s_, m.mlpd.as<f16>(), 4 * d, e.w_fc2, 4 * d, e.b_fc2, m.xd.p, d, n, d, 4 * d, EPI_F32_RESID);
+    proj(st, b.attd, d, e.w_xo, d, e.b_xo, b.xd, d, n, d, d, EPI_F32_RESID);
+    launch_layernorm(b.xd, d, e.ln3_g, e.ln3_b, b.hd, d, n, d, st);
+    proj(st, b.hd, d, e.w_fc1, d, e.b_fc1, b.mlpd, 4 * d, n, 4 * d, d, EPI_F16_GELU);
+    proj(st, b.mlpd, 4 * d, e.w_fc2, 4 * d, e.b_fc2, b.xd, d, n, d, 4 * d, EPI_F32_RESID);
   }
   if (want_logits) {
-    launch_layernorm(m.xd.as<float>() + (size_t)(n - 1) * d, d, md.ln_g, md.ln_b, m.hd.as<f16>(), d, 1, d, s_);
-    proj(s_, m.hd.as<f16>(), d, md.tok_emb, d, nullptr, m.logits.p, m.V, 1, m.V, d, EPI_F32);
+    launch_layernorm(b.xd + (size_t)(n - 1) * d, d, md.ln_g, md.ln_b, b.hd, d, 1, d, st);
+    proj(st, b.hd, d, md.tok_emb, d, nullptr, b.logits, m.V, 1, m.V, d, EPI_F32);
   }
   times.prefills++;
 }
@@ -1051,6 +1130,11 @@ void State::heuristic_timestamps(int i_segment, const FullParams& p) {
   }
 }
 
+// DTW token timestamps of one window (whisper.cpp whisper_exp_compute_token_level_timestamps_dtw
+// as run after each window): the re-forward with alignment-head capture and the DTW kernels
+// are enqueued on the DTW stream with their own working set and KV sequence, so they overlap
+// the next window's / segment's decode.  The times land in a pinned block; resolve_dtw()
+// copies them into the tokens once the job's event has fired.
 void State::dtw_timestamps(int i_segment, int n_segments, int seek, int n_frames, const std::string& language) {
   Impl& m = *m_;
   const Vocab& v = ctx_.vocab;
@@ -1063,19 +1147,63 @@ void State::dtw_timestamps(int i_segment, int n_segments, int seek, int n_frames
       if (t.id < v.eot) toks.push_back(t.id);
   toks.push_back(v.eot);
   const int N = (int)toks.size();
-  decoder_prefill(toks.data(), N, 0, false, true);
+  Impl::DtwJob job;
+  job.i0 = i_segment;
+  job.n = n_segments;
+  if (m.blk_pool.empty()) {
+    int* blk = nullptr;
+    WDR_HIP(hipHostMalloc((void**)&blk, (3 * RMAX + RMAX + 8) * 4, hipHostMallocDefault));
+    m.blk_pool.push_back(blk);
+  }
+  job.blk = m.blk_pool.back();
+  m.blk_pool.pop_back();
+  if (m.ev_pool.empty()) {
+    hipEvent_t e;
+    WDR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    m.ev_pool.push_back(e);
+  }
+  job.done = m.ev_pool.back();
+  m.ev_pool.pop_back();
+  m.jobs.push_back(job);
+  // the window's cross-K/V (encoded ahead, or on demand on the decode stream) must be in place
+  WDR_HIP(hipEventRecord(m.ev_sync, s_));
+  WDR_HIP(hipStreamWaitEvent(m.sd, m.ev_sync, 0));
+  PrefillBufs pb = m.pb_dtw;
+  pb.h_rows = job.blk;
+  prefill_on(toks.data(), N, DTW_SEQ, false, true, pb, m.sd, m.xkv());
   const int n_audio = n_frames / 2;
-  launch_dtw(m.cap.as<float>(), (int)ctx_.aheads.size(), N, 1500, n_audio, sot_len, seek, m.nrm.as<float>(),
-             m.xdtw.as<float>(), m.times.as<int>(), m.times.as<int>() + RMAX + 4, s_);
-  WDR_HIP(hipMemcpyAsync(m.h_times, m.times.p, (RMAX + 8) * 4, hipMemcpyDeviceToHost, s_));
-  WDR_HIP(hipStreamSynchronize(s_));
-  const int nt = m.h_times[RMAX + 4];
+  Impl::DtwSet& D = m.dset;
+  launch_dtw(D.cap.as<float>(), (int)ctx_.aheads.size(), N, 1500, n_audio, sot_len, seek, D.nrm.as<float>(),
+             D.xdtw.as<float>(), D.times.as<int>(), D.times.as<int>() + RMAX + 4, m.sd);
+  WDR_HIP(hipMemcpyAsync(job.blk + 3 * RMAX, D.times.p, (RMAX + 8) * 4, hipMemcpyDeviceToHost, m.sd));
+  WDR_HIP(hipEventRecord(job.done, m.sd));
+  WDR_HIP(hipEventRecord(m.ev_dtw, m.sd));
+}
+
+std::vector<DtwTicket> State::take_dtw_jobs() {
+  Impl& m = *m_;
+  std::vector<DtwTicket> out;
+  for (auto& j : m.jobs) out.push_back(DtwTicket{j.i0, j.n, j.blk, (void*)j.done});
+  m.jobs.clear();
+  return out;
+}
+
+void State::resolve_dtw(DtwTicket& t, std::vector<ResultSeg>& segs) {
+  Impl& m = *m_;
+  const Vocab& v = ctx_.vocab;
+  WDR_HIP(hipEventSynchronize((hipEvent_t)t.event));
+  const int* times = t.blk + 3 * RMAX;
+  const int nt = times[RMAX + 4];
   int k = 0;
-  for (int s = i_segment; s < i_segment + n_segments && k < nt; ++s)
-    for (auto& t : result_all[s].tokens) {
+  for (int s = t.i0; s < t.i0 + t.n && s < (int)segs.size() && k < nt; ++s)
+    for (auto& tok : segs[s].tokens) {
       if (k >= nt) break;
-      if (t.id < v.eot) t.t_dtw = m.h_times[k++];
+      if (tok.id < v.eot) tok.t_dtw = times[k++];
     }
+  m.blk_pool.push_back(t.blk);
+  m.ev_pool.push_back((hipEvent_t)t.event);
+  t.blk = nullptr;
+  t.event = nullptr;
 }
 
 // ------------------------------------------------------------------ whisper_full
@@ -1430,22 +1558,32 @@ Seq State::decode_sample(const std::vector<int>& prompt, const FullParams& param
   return out;
 }
 
-int State::full(const FullParams& params, const float* samples, int n, int job) {
+int State::full(const FullParams& params, const float* samples, int n, int job, bool async_dtw) {
   WDR_HIP(hipSetDevice(ctx_.cp.gpu_device));
   Impl& m = *m_;
   const Vocab& v = ctx_.vocab;
   const HParams& hp = ctx_.model.hp;
   result_all.clear();
+  {   // jobs a previous caller never collected: drain them
+    std::vector<DtwTicket> stale = take_dtw_jobs();
+    std::vector<ResultSeg> none;
+    for (auto& t : stale) resolve_dtw(t, none);
+  }
   for (int j = 1; j < NSEQ; ++j) m.rng[j] = std::mt19937(0);   // WHISPER_DECODER_INIT, every call
   double t_start = now_s();
   const bool planned = job >= 0 && job < (int)m.plan.pcm.size();
   // the slot goes back to the encode-ahead ring once this segment's last kernel has run
+  // the slot goes back to the encode-ahead ring once the decode stream AND the DTW stream
+  // (this segment's re-forwards read the slot's cross-K/V) are past it
   struct Release {
     Impl& m;
     hipStream_t s;
     bool on;
     ~Release() {
-      if (on) (void)hipEventRecord(m.slots[m.cur].freed, s);
+      if (!on) return;
+      (void)hipEventRecord(m.ev_sync, s);
+      (void)hipStreamWaitEvent(m.sd, m.ev_sync, 0);
+      (void)hipEventRecord(m.slots[m.cur].freed, m.sd);
     }
   } release{m, s_, planned};
   int encoded_seek = -1;
@@ -1486,6 +1624,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job) 
   auto encode = [&](int seek) {
     if (encoded_seek != seek) {
       const double t = now_s();
+      WDR_HIP(hipStreamWaitEvent(s_, m.ev_dtw, 0));   // a DTW job may still read this slot
       encode_window(seek);
       WDR_HIP(hipStreamSynchronize(s_));
       times.encode += now_s() - t;
@@ -1665,6 +1804,10 @@ int State::full(const FullParams& params, const float* samples, int n, int job) 
     if (tokens_cur.size() > 1 && tokens_cur[tokens_cur.size() - 2].id < v.beg && tokens_cur.back().id > v.beg)
       seek_delta = std::min(seek_end - seek, 3000);
     seek += seek_delta;
+  }
+  if (!async_dtw) {
+    std::vector<DtwTicket> tk = take_dtw_jobs();
+    for (auto& t : tk) resolve_dtw(t, result_all);
   }
   return 0;
 }
