@@ -129,6 +129,7 @@ typedef struct {
 typedef struct {
   double mel, encode, decode, dtw, vad, total;
   int64_t windows, decode_steps, prefills;
+  double lang, prompt_gpu, embed;   /* language detect wall, prompt-prefill GPU time, speaker embeddings */
 } wdr_stage_times;
 
 const char* wdr_last_error(void);

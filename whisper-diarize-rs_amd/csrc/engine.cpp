@@ -939,7 +939,8 @@ void wdr_segment_list_free(wdr_segment_list* l) {
 int wdr_context_stage_times(wdr_context* c, wdr_stage_times* o) {
   WDR_GUARD({
     const StageTimes& t = c->st->times;
-    *o = wdr_stage_times{t.mel, t.encode, t.decode, t.dtw, 0.0, t.glue, t.windows, t.decode_steps, t.prefills};
+    *o = wdr_stage_times{t.mel,          t.encode,   t.decode,  t.dtw,        0.0,  t.glue, t.windows,
+                         t.decode_steps, t.prefills, t.lang,    t.prompt_gpu, c->embed_s};
     return 0;
   })
 }

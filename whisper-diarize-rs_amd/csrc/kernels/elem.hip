@@ -253,33 +253,44 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* x, int ldx, cons
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
   const float* xr = x + (long long)row * ldx;
-  // d <= 1280: each lane keeps its <= 20 values in registers (float4 loads)
-  float v[20];
-  int nv = 0;
+  // d <= 1280: each lane keeps its <= 20 values in registers; fully unrolled (compile-time
+  // indices keep them out of scratch) and gamma / beta are loaded together with x
+  float v[5][4], gg[5][4], bb[5][4];
   float s = 0.f;
-  for (int c = lane * 4; c < d; c += 256) {
-    const float4 q = *(const float4*)(xr + c);
-    v[nv] = q.x; v[nv + 1] = q.y; v[nv + 2] = q.z; v[nv + 3] = q.w;
-    s += (q.x + q.y) + (q.z + q.w);
-    nv += 4;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int c = lane * 4 + j * 256;
+    const bool ok = c < d;
+    const int cc = ok ? c : 0;
+    const float4 q = *(const float4*)(xr + cc);
+    const float4 g4 = *(const float4*)(g + cc);
+    const float4 b4 = *(const float4*)(b + cc);
+    v[j][0] = ok ? q.x : 0.f; v[j][1] = ok ? q.y : 0.f; v[j][2] = ok ? q.z : 0.f; v[j][3] = ok ? q.w : 0.f;
+    gg[j][0] = g4.x; gg[j][1] = g4.y; gg[j][2] = g4.z; gg[j][3] = g4.w;
+    bb[j][0] = b4.x; bb[j][1] = b4.y; bb[j][2] = b4.z; bb[j][3] = b4.w;
+    s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
   }
   s = wave_sum(s);
   const float mean = s / d;
   float s2 = 0.f;
 #pragma unroll
-  for (int i = 0; i < 20; ++i)
-    if (i < nv) {
-      const float t = v[i] - mean;
-      s2 += t * t;
-    }
+  for (int j = 0; j < 5; ++j)
+    if (lane * 4 + j * 256 < d)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float t = v[j][e] - mean;
+        s2 += t * t;
+      }
   s2 = wave_sum(s2);
   const float scale = 1.0f / sqrtf(s2 / d + 1e-5f);
   f16* yr = y + (long long)row * ldy;
-  int i = 0;
-  for (int c = lane * 4; c < d; c += 256, i += 4) {
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int c = lane * 4 + j * 256;
+    if (c >= d) continue;
     f16x4 o;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = (f16)((v[i + e] - mean) * scale * g[c + e] + b[c + e]);
+    for (int e = 0; e < 4; ++e) o[e] = (f16)((v[j][e] - mean) * scale * gg[j][e] + bb[j][e]);
     *(f16x4*)(yr + c) = o;
   }
 }

@@ -430,16 +430,34 @@ __global__ __launch_bounds__(256) void k_skinny(ProjArgs a) {
     n = n < a.N ? n : a.N - 1;
     brow[j] = a.B + (size_t)n * a.ldb + fk;
   }
-  for (int k = wid * 32; k < a.K; k += 128) {
-    f16x8 bf[NT], af[MT];
+  // U k-steps per batch: all of a batch's fragment loads are issued before its MFMAs, so each
+  // wave keeps U*(NT+MT) 16-B loads in flight instead of one dependent round trip per step
+  constexpr int U = (MT + NT) <= 3 ? 8 : 4;
+  for (int k0 = wid * 32; k0 < a.K; k0 += 128 * U) {
+    f16x8 bf[U][NT], af[U][MT];
 #pragma unroll
-    for (int j = 0; j < NT; ++j) bf[j] = *(const f16x8*)(brow[j] + k);
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u * 128;
+      const bool ok = k < a.K;
+      const int kk = ok ? k : 0;
 #pragma unroll
-    for (int i = 0; i < MT; ++i) af[i] = *(const f16x8*)(arow[i] + k);
+      for (int j = 0; j < NT; ++j) {
+        const f16x8 t = *(const f16x8*)(brow[j] + kk);
+        bf[u][j] = ok ? t : (f16x8){};
+      }
 #pragma unroll
-    for (int i = 0; i < MT; ++i)
+      for (int i = 0; i < MT; ++i) {
+        const f16x8 t = *(const f16x8*)(arow[i] + kk);
+        af[u][i] = ok ? t : (f16x8){};
+      }
+    }
 #pragma unroll
-      for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[u][i], bf[u][j], acc[i][j], 0, 0, 0);
   }
 #pragma unroll
   for (int i = 0; i < MT; ++i)

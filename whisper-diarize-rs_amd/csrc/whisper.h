@@ -123,6 +123,7 @@ struct ResultSeg {
 struct StageTimes {   // host wall-clock per phase (seconds), accumulated
   double mel = 0, encode = 0, decode = 0, dtw = 0, glue = 0;
   long long windows = 0, decode_steps = 0, prefills = 0;
+  double lang = 0, prompt_gpu = 0;   // language-detect wall time; GPU time of the prompt prefills
 };
 
 struct Seq;           // one decoder's sequence (whisper_ctx.cpp)

@@ -378,6 +378,7 @@ struct State::Impl {
   hipStream_t sd = nullptr;        // DTW stream
   hipEvent_t ev_sync = nullptr;    // decode-stream point the DTW stream waits for
   hipEvent_t ev_dtw = nullptr;     // last DTW job enqueued (on-demand encodes wait for it)
+  hipEvent_t ev_p0 = nullptr, ev_p1 = nullptr;   // prompt-prefill timing
   struct DtwJob {
     int i0 = 0, n = 0;             // result_all range of the full() call that produced it
     int* blk = nullptr;            // pinned: tokens [3*RMAX] then times [RMAX + 8]
@@ -504,6 +505,8 @@ State::State(Context& ctx) : ctx_(ctx), s_(ctx.stream), m_(new Impl) {
     WDR_HIP(hipStreamCreateWithPriority(&m.sd, hipStreamNonBlocking, lo));
     WDR_HIP(hipEventCreateWithFlags(&m.ev_sync, hipEventDisableTiming));
     WDR_HIP(hipEventCreateWithFlags(&m.ev_dtw, hipEventDisableTiming));
+    WDR_HIP(hipEventCreate(&m.ev_p0));
+    WDR_HIP(hipEventCreate(&m.ev_p1));
   }
   WDR_HIP(hipHostMalloc((void**)&m.h_rows, 3 * RMAX * 4, hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_tok, NSEQ * sizeof(TokOut), hipHostMallocDefault));
@@ -761,11 +764,18 @@ void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool c
     f16* kc = m.kc.as<f16>() + (size_t)l * NSLOT * m.seq_stride;
     f16* vc = m.vc.as<f16>() + (size_t)l * NSLOT * m.seq_stride;
     launch_layernorm(b.xd, d, e.ln1_g, e.ln1_b, b.hd, d, n, d, st);
-    proj(st, b.hd, d, e.w_qkv, d, e.b_qkv, b.qkvd, 3 * d, n, 3 * d, d, EPI_F16);
-    launch_kv_scatter(b.qkvd, 3 * d, d, b.rows_seq, b.rows_pos, n, kc, vc, m.seq_stride,
-                      st);
-    FlashArgs sa{b.qkvd, 3 * d, 0, b.qkvd + d, 3 * d, 0, b.qkvd + 2 * d, 3 * d, 0,
-                 b.attd, d, 0, nullptr, n, n, hp.n_text_head, 1, scale};
+    // Q to qkvd, K / V straight into this sequence's cache rows 0..n-1 (the epilogue scatter)
+    ProjArgs qa{b.hd, d, e.w_qkv, d, e.b_qkv, b.qkvd, 3 * d, nullptr, 0, n, 3 * d, d, EPI_QKV_CACHE};
+    qa.kc = kc;
+    qa.vc = vc;
+    qa.seq_stride = m.seq_stride;
+    qa.row_seq = b.rows_seq;
+    qa.row_pos = b.rows_pos;
+    qa.d = d;
+    launch_proj(qa, st);
+    const f16* ks = kc + (size_t)seq * m.seq_stride;
+    const f16* vs = vc + (size_t)seq * m.seq_stride;
+    FlashArgs sa{b.qkvd, 3 * d, 0, ks, d, 0, vs, d, 0, b.attd, d, 0, nullptr, n, n, hp.n_text_head, 1, scale};
     launch_flash_attn(sa, 1, st);
     proj(st, b.attd, d, e.w_o, d, e.b_o, b.xd, d, n, d, d, EPI_F32_RESID);
     launch_layernorm(b.xd, d, e.ln2_g, e.ln2_b, b.hd, d, n, d, st);
@@ -1648,6 +1658,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
     lang_id = best;
     language = kLangs[best];
     times.decode += now_s() - t;
+    times.lang += now_s() - t;
   }
   std::vector<int> prompt_init = {v.sot};
   if (v.multilingual) {
@@ -1687,7 +1698,9 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
         prompt.insert(prompt.end(), prompt_past.end() - n_take, prompt_past.end());
       }
       prompt.insert(prompt.end(), prompt_init.begin(), prompt_init.end());
+      WDR_HIP(hipEventRecord(m.ev_p0, s_));
       decoder_prefill(prompt.data(), (int)prompt.size(), 0, true, false);
+      WDR_HIP(hipEventRecord(m.ev_p1, s_));
       const int window = std::min(seek_end - seek, 3000);
       int Lf = 0;
       if (params.force_len_rate > 0.f) Lf = std::max(3, c_round(params.force_len_rate * window / 100.0) + 3);
@@ -1773,6 +1786,10 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
       if (success) break;
     }
     times.decode += now_s() - t_dec;
+    {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, m.ev_p0, m.ev_p1) == hipSuccess) times.prompt_gpu += ms * 1e-3;
+    }
     int seek_delta = best.seek_delta;
     const int result_len = best.result_len;
     auto& tokens_cur = best.tokens;

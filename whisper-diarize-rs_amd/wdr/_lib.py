@@ -72,7 +72,8 @@ class Callbacks(C.Structure):
 
 class StageTimes(C.Structure):
     _fields_ = [("mel", f64), ("encode", f64), ("decode", f64), ("dtw", f64), ("vad", f64), ("total", f64),
-                ("windows", i64), ("decode_steps", i64), ("prefills", i64)]
+                ("windows", i64), ("decode_steps", i64), ("prefills", i64), ("lang", f64), ("prompt_gpu", f64),
+                ("embed", f64)]
 
 
 class Token(C.Structure):
