@@ -432,7 +432,8 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
       pcm[i] = segs[i].samples;
       ns[i] = (int)segs[i].n_samples;
     }
-    c->st->plan(pcm.data(), ns.data(), (int)segs.size());
+    const bool auto_lang = !o || !o->lang || std::string(o->lang).empty() || std::string(o->lang) == "auto";
+    c->st->plan(pcm.data(), ns.data(), (int)segs.size(), auto_lang);
   }
   struct Unplan {
     State& st;

@@ -148,7 +148,7 @@ class State {
   std::vector<DtwTicket> take_dtw_jobs();
   void resolve_dtw(DtwTicket& t, std::vector<ResultSeg>& segs);
   // encode-ahead: the pipeline's whole segment list (int16 PCM), see whisper_ctx.cpp
-  void plan(const int16_t* const* pcm, const int* n, int count);
+  void plan(const int16_t* const* pcm, const int* n, int count, bool detect_lang = false);
   void unplan();
   std::vector<ResultSeg> result_all;
   int lang_id = 0;

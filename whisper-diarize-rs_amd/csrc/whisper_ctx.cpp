@@ -311,8 +311,9 @@ Context::~Context() {
 // ------------------------------------------------------------------ state buffers
 static constexpr int RMAX = 448;   // max decoder rows in one forward (n_text_ctx)
 static constexpr int NSEQ = 8;     // max decoder rows in one step
-static constexpr int NSLOT = 17;   // self-attention KV-cache sequences (beams + beam-reorder scratch + DTW)
+static constexpr int NSLOT = 18;   // self-attention KV-cache sequences (beams + reorder scratch + DTW + lang)
 static constexpr int DTW_SEQ = 16;  // the DTW re-forward's own sequence (runs on its own stream)
+static constexpr int LANG_SEQ = 17; // encode-ahead language detection's sequence (encode stream)
 static constexpr int NSPLIT = 24;  // cross-attention key chunks (1500 / 64)
 
 // Working set of a prefill: the decode stream's own (pointing at the buffers above) and the
@@ -353,7 +354,14 @@ struct State::Impl {
     std::vector<const int16_t*> pcm;
     std::vector<int> n;
     size_t next_enq = 0;
+    bool detect_lang = false;   // lang "auto": the SOT pass runs right after each window-0 encode
   } plan;
+  // encode-ahead language detection: its own prefill working set and the 100 language
+  // logits of each slot's window 0 (pinned, written by the encode stream before `ready`)
+  struct LangSet {
+    DevMem xd, hd, qkvd, attd, qx, mlpd, rows_tok, rows_pos, rows_seq, part_o, part_ml, logits;
+  } lset;
+  float* h_lang = nullptr;      // [(S + 1)][100]
   DevMem energy_d; int energy_cap = 0;
   const f16* xkv() const { return xkv_ring.as<f16>() + (size_t)cur * xkv_slot_elems; }
   // decoder
@@ -370,7 +378,7 @@ struct State::Impl {
   long long seq_stride = 0;   // elements per (layer, seq)
   // dtw
   DevMem nrm, xdtw, times;
-  PrefillBufs pb_main{}, pb_dtw{};
+  PrefillBufs pb_main{}, pb_dtw{}, pb_lang{};
   struct DtwSet {
     DevMem xd, hd, qkvd, attd, qx, mlpd, rows_tok, rows_pos, rows_seq, fpart_o, fpart_ml, ml, cap, part_o, part_ml,
         nrm, xdtw, times;
@@ -500,6 +508,26 @@ State::State(Context& ctx) : ctx_(ctx), s_(ctx.stream), m_(new Impl) {
                         D.mlpd.as<f16>(), D.rows_tok.as<int>(), D.rows_pos.as<int>(), D.rows_seq.as<int>(),
                         D.fpart_o.as<float>(), D.fpart_ml.as<float2>(), D.ml.as<float2>(), D.cap.as<float>(),
                         D.part_o.as<float>(), D.part_ml.as<float2>(), nullptr, nullptr};
+    Impl::LangSet& G = m.lset;
+    G.xd = DevMem((size_t)d * 4);
+    G.hd = DevMem((size_t)d * 2);
+    G.qkvd = DevMem((size_t)3 * d * 2);
+    G.attd = DevMem((size_t)d * 2);
+    G.qx = DevMem((size_t)d * 2);
+    G.mlpd = DevMem((size_t)4 * d * 2);
+    G.rows_tok = DevMem(64);
+    G.rows_pos = DevMem(64);
+    G.rows_seq = DevMem(64);
+    G.part_o = DevMem((size_t)NSPLIT * m.H * 64 * 4);
+    G.part_ml = DevMem((size_t)NSPLIT * m.H * sizeof(float2));
+    G.logits = DevMem((size_t)m.V * 4);
+    int* lrows = nullptr;
+    WDR_HIP(hipHostMalloc((void**)&lrows, 3 * RMAX * 4, hipHostMallocDefault));
+    m.pb_lang = PrefillBufs{G.xd.as<float>(), G.hd.as<f16>(), G.qkvd.as<f16>(), G.attd.as<f16>(), G.qx.as<f16>(),
+                            G.mlpd.as<f16>(), G.rows_tok.as<int>(), G.rows_pos.as<int>(), G.rows_seq.as<int>(),
+                            nullptr, nullptr, nullptr, nullptr, G.part_o.as<float>(), G.part_ml.as<float2>(),
+                            G.logits.as<float>(), lrows};
+    WDR_HIP(hipHostMalloc((void**)&m.h_lang, (size_t)(kSlots + 1) * 100 * 4, hipHostMallocDefault));
     int lo = 0, hi = 0;
     WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
     WDR_HIP(hipStreamCreateWithPriority(&m.sd, hipStreamNonBlocking, lo));
@@ -546,6 +574,8 @@ State::~State() {
     for (int* b : m_->blk_pool) (void)hipHostFree(b);
     for (hipEvent_t e : m_->ev_pool) (void)hipEventDestroy(e);
     if (m_->ev_sync) (void)hipEventDestroy(m_->ev_sync);
+    if (m_->pb_lang.h_rows) (void)hipHostFree(m_->pb_lang.h_rows);
+    if (m_->h_lang) (void)hipHostFree(m_->h_lang);
     if (m_->ev_dtw) (void)hipEventDestroy(m_->ev_dtw);
     for (auto& sl : m_->slots) {
       if (sl.h_pcm) (void)hipHostFree(sl.h_pcm);
@@ -679,9 +709,10 @@ void State::read_encoder_out(float* out) {
 // every segment does not depend on any decode result, so it is encoded ahead on the low-
 // priority stream in batches of kBatch windows into the cross-K/V ring; segment j waits only
 // on its slot's `ready` event, and slot j % S is reused once segment j - S has recorded `freed`.
-void State::plan(const int16_t* const* pcm, const int* n, int count) {
+void State::plan(const int16_t* const* pcm, const int* n, int count, bool detect_lang) {
   Impl& m = *m_;
   WDR_HIP(hipStreamSynchronize(m.es));
+  m.plan.detect_lang = detect_lang;
   m.plan.pcm.assign(pcm, pcm + count);
   m.plan.n.assign(n, n + count);
   m.plan.next_enq = 0;
@@ -728,7 +759,19 @@ void State::top_up(int j) {
       launch_im2col_mel(ia, m.es);
     }
     encoder_body(ctx_, m, m.eb, g1 - g0, m.xkv_ring.as<f16>() + (size_t)slot0 * m.xkv_slot_elems, m.es);
-    for (int k = g0; k < g1; ++k) WDR_HIP(hipEventRecord(m.slots[k % m.S].ready, m.es));
+    for (int k = g0; k < g1; ++k) {
+      const int slot = k % m.S;
+      if (m.plan.detect_lang) {
+        // whisper.cpp's language detection (one SOT pass over window 0, argmax of the language
+        // logits) depends on nothing decoded, so it runs here, off the decode chain
+        const int sot = ctx_.vocab.sot;
+        prefill_on(&sot, 1, LANG_SEQ, true, false, m.pb_lang, m.es,
+                   m.xkv_ring.as<f16>() + (size_t)slot * m.xkv_slot_elems);
+        WDR_HIP(hipMemcpyAsync(m.h_lang + (size_t)slot * 100, m.pb_lang.logits + ctx_.vocab.sot + 1, 100 * 4,
+                               hipMemcpyDeviceToHost, m.es));
+      }
+      WDR_HIP(hipEventRecord(m.slots[slot].ready, m.es));
+    }
     m.plan.next_enq = g1;
     times.windows += g1 - g0;
   }
@@ -813,7 +856,7 @@ void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool c
     launch_layernorm(b.xd + (size_t)(n - 1) * d, d, md.ln_g, md.ln_b, b.hd, d, 1, d, st);
     proj(st, b.hd, d, md.tok_emb, d, nullptr, b.logits, m.V, 1, m.V, d, EPI_F32);
   }
-  times.prefills++;
+  if (st == s_) times.prefills++;
 }
 
 // One decode step for R rows: row r appends token rows_tok[r] at position rows_pos[r] of
@@ -1647,11 +1690,15 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
   if (language.empty() || language == "auto") {
     encode(seek_start);
     const double t = now_s();
-    const int sot = v.sot;
-    decoder_prefill(&sot, 1, 0, true, false);
     std::vector<float> ll(100);
-    WDR_HIP(hipMemcpyAsync(ll.data(), m.logits.as<float>() + v.sot + 1, 100 * 4, hipMemcpyDeviceToHost, s_));
-    WDR_HIP(hipStreamSynchronize(s_));
+    if (planned && m.plan.detect_lang) {   // computed on the encode stream before `ready`
+      memcpy(ll.data(), m.h_lang + (size_t)m.cur * 100, 100 * 4);
+    } else {
+      const int sot = v.sot;
+      decoder_prefill(&sot, 1, 0, true, false);
+      WDR_HIP(hipMemcpyAsync(ll.data(), m.logits.as<float>() + v.sot + 1, 100 * 4, hipMemcpyDeviceToHost, s_));
+      WDR_HIP(hipStreamSynchronize(s_));
+    }
     int best = 0;
     for (int i = 1; i < 100; ++i)
       if (ll[i] > ll[best]) best = i;
