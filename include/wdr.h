@@ -83,12 +83,21 @@ typedef struct {
   int8_t disable_fallback;                /* 1: logprob/entropy fallback thresholds off */
 } wdr_synthetic;
 
-/* FormattingOverrides, src/formatting.rs:37-51 (accepted; subtitle formatting is §8(f) "next") */
+/* FormattingOverrides, src/formatting.rs:37-51 (every field optional; Option<bool> as -1/0/1) */
 typedef struct {
   int8_t has_max_chars_per_line; uint64_t max_chars_per_line;
   int8_t has_max_lines; uint64_t max_lines;
   int8_t has_cps_cap; double cps_cap;
   int8_t has_split_gap_sec; double split_gap_sec;
+  int8_t has_comma_min_chars_before_allow; uint64_t comma_min_chars_before_allow;
+  int8_t has_min_word_dur; double min_word_dur;
+  int8_t has_min_sub_dur; double min_sub_dur;
+  int8_t has_max_sub_dur; double max_sub_dur;
+  int8_t has_soft_max_words_per_line; uint64_t soft_max_words_per_line;
+  int8_t insert_interword_space;
+  int8_t use_grapheme_len;
+  int8_t enforce_kinsoku;
+  int8_t allow_comma_split;
 } wdr_formatting_overrides;
 
 /* WordTimestamp, src/types.rs:64-70 */
@@ -145,6 +154,11 @@ int wdr_transcribe_audio(wdr_engine* e, const char* audio_path, const wdr_transc
 
 /* ---- seams ---- */
 int wdr_read_wav(const char* path, int16_t** samples, size_t* n);
+/* formatting::process_segments (src/formatting.rs:240-313) with PostProcessConfig::for_language(lang)
+ * + overrides (nullable), and a VadMaskOracle over vad_mask (2 doubles per interval) when
+ * has_mask (src/engine.rs:192-199).  Free the result with wdr_segment_list_free. */
+int wdr_process_segments(const wdr_segment* segs, size_t n_segs, const char* lang, const wdr_formatting_overrides* ov,
+                         int8_t has_mask, const double* vad_mask, size_t n_mask, wdr_segment_list** out);
 void wdr_free(void* p);
 int wdr_vad_merge(const double* starts_cs, const double* ends_cs, size_t n_segs, const int16_t* samples,
                   size_t n_samples, double* mask_out /* [2*n_segs] */, size_t* n_mask,

@@ -173,9 +173,10 @@ def test_engine_transcribe_audio_with_vad(tmp_path):
     opts = wdr.TranscribeOptions(model="tiny-test", lang="en", enable_vad=True,
                                  advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
     got = eng.transcribe_audio(path, opts)
-    _, vsegs = wdr.Vad().get_segments(pcm)
+    mask, vsegs = wdr.Vad().get_segments(pcm)
     ctx = wdr.WhisperContext("tiny-test", synthetic=SYN)
-    want, _ = ctx.run_pipeline(vsegs, opts)
+    want, lang = ctx.run_pipeline(vsegs, opts)
+    want = wdr.process_segments(want, lang or "en", None, mask)   # src/engine.rs:192-199
     assert len(vsegs) > 0
     assert [(s.text, round(s.start, 6), round(s.end, 6)) for s in got] == \
         [(s.text, round(s.start, 6), round(s.end, 6)) for s in want]

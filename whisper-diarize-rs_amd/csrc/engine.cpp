@@ -23,6 +23,7 @@
 
 #include "../../include/wdr.h"
 #include "diarize.h"
+#include "formatting.h"
 #include "vad.h"
 #include "whisper.h"
 
@@ -363,6 +364,64 @@ struct CallbackCtx {
   const wdr_callbacks* cb;
 };
 
+// ---- formatting glue (src/engine.rs:192-199)
+static void apply_overrides(PostProcessConfig& c, const wdr_formatting_overrides* ov) {
+  if (!ov) return;
+  if (ov->has_max_chars_per_line) c.max_chars_per_line = ov->max_chars_per_line;
+  if (ov->has_max_lines) c.max_lines = ov->max_lines;
+  if (ov->has_cps_cap) c.cps_cap = ov->cps_cap;
+  if (ov->has_split_gap_sec) c.split_gap_sec = ov->split_gap_sec;
+  if (ov->has_comma_min_chars_before_allow) c.comma_min_chars_before_allow = ov->comma_min_chars_before_allow;
+  if (ov->has_min_word_dur) c.min_word_dur = ov->min_word_dur;
+  if (ov->has_min_sub_dur) c.min_sub_dur = ov->min_sub_dur;
+  if (ov->has_max_sub_dur) c.max_sub_dur = ov->max_sub_dur;
+  if (ov->has_soft_max_words_per_line) c.soft_max_words_per_line = ov->soft_max_words_per_line;
+  if (ov->insert_interword_space >= 0) c.insert_interword_space = ov->insert_interword_space != 0;
+  if (ov->use_grapheme_len >= 0) c.use_grapheme_len = ov->use_grapheme_len != 0;
+  if (ov->enforce_kinsoku >= 0) c.enforce_kinsoku = ov->enforce_kinsoku != 0;
+  if (ov->allow_comma_split >= 0) c.allow_comma_split = ov->allow_comma_split != 0;
+}
+
+static std::vector<FmtSeg> to_fmt(const std::vector<Seg>& in) {
+  std::vector<FmtSeg> out;
+  for (const Seg& s : in) {
+    FmtSeg f;
+    f.start = s.start;
+    f.end = s.end;
+    f.text = s.text;
+    f.has_words = s.has_words;
+    for (const Word& w : s.words) f.words.push_back({w.text, w.start, w.end, w.has_p, w.p});
+    f.has_speaker = s.has_speaker;
+    f.speaker = s.speaker;
+    out.push_back(std::move(f));
+  }
+  return out;
+}
+
+static std::vector<Seg> from_fmt(const std::vector<FmtSeg>& in) {
+  std::vector<Seg> out;
+  for (const FmtSeg& f : in) {
+    Seg s;
+    s.start = f.start;
+    s.end = f.end;
+    s.text = f.text;
+    s.has_words = f.has_words;
+    for (const FmtWord& w : f.words) {
+      Word x;
+      x.text = w.text;
+      x.start = w.start;
+      x.end = w.end;
+      x.has_p = w.has_p;
+      x.p = w.p;
+      s.words.push_back(std::move(x));
+    }
+    s.has_speaker = f.has_speaker;
+    s.speaker = f.speaker;
+    out.push_back(std::move(s));
+  }
+  return out;
+}
+
 static wdr_segment_list* to_list(const std::vector<Seg>& segs, const std::string* lang) {
   auto* l = (wdr_segment_list*)calloc(1, sizeof(wdr_segment_list));
   l->n_segments = segs.size();
@@ -640,13 +699,14 @@ int wdr_engine_set_synthetic(wdr_engine* e, const wdr_synthetic* syn) {
 
 int wdr_transcribe_audio(wdr_engine* e, const char* audio_path, const wdr_transcribe_options* o,
                          const wdr_formatting_overrides* fmt, const wdr_callbacks* cb, wdr_segment_list** out) {
-  (void)fmt;
   WDR_GUARD({
     if (!audio_path || !file_exists(audio_path)) return fail("audio file doesn't exist");
     const std::string model = (o && o->model) ? o->model : "base";
     std::vector<int16_t> pcm = read_wav_impl(audio_path);
     std::vector<wdr_speech_segment> segs;
     std::vector<int16_t> dpad;   // owns the samples of pyannote segments (they index the padded buffer)
+    std::vector<std::pair<double, double>> vad_mask;   // VadMaskOracle input (VAD branch only)
+    bool have_mask = false;
     const bool vad = !o || o->enable_vad == 1;   // `if let Some(true) = options.enable_vad` (src/engine.rs:123)
     if (o && o->enable_diarize == 1) {
       // src/engine.rs:89-122: pyannote segmentation -> SpeechSegments
@@ -657,8 +717,8 @@ int wdr_transcribe_audio(wdr_engine* e, const char* audio_path, const wdr_transc
       for (const DiarSegment& d : ds) segs.push_back({d.start, d.end, dpad.data() + d.start_idx, d.end_idx - d.start_idx});
     } else if (vad) {
       if (!e->vad) e->vad = std::make_unique<VadModel>(e->cfg.has_gpu_device ? e->cfg.gpu_device : 0);
-      std::vector<std::pair<double, double>> mask;
-      vad_get_segments(*e->vad, pcm.data(), pcm.size(), &mask, &segs);
+      vad_get_segments(*e->vad, pcm.data(), pcm.size(), &vad_mask, &segs);
+      have_mask = true;
     } else {
       // whole file as one segment (src/engine.rs:141-147)
       segs.push_back({0.0, (double)pcm.size() / 16000.0, pcm.data(), pcm.size()});
@@ -673,6 +733,12 @@ int wdr_transcribe_audio(wdr_engine* e, const char* audio_path, const wdr_transc
     std::string lang;
     bool has_lang = false;
     std::vector<Seg> res = run_pipeline(it->second.get(), segs, o, e->syn, cb, &lang, &has_lang);
+    // src/engine.rs:179-199: preset of the detected (else requested) language + overrides,
+    // then process_segments with the VAD mask oracle when VAD produced the segments
+    const std::string eff = has_lang ? lang : ((o && o->lang) ? std::string(o->lang) : std::string("auto"));
+    PostProcessConfig pcfg = config_for_language(eff);
+    apply_overrides(pcfg, fmt);
+    res = from_fmt(process_segments(to_fmt(res), pcfg, have_mask ? &vad_mask : nullptr));
     *out = to_list(res, has_lang ? &lang : nullptr);
     return 0;
   })
@@ -839,6 +905,39 @@ int wdr_dbg_discrete(const float* w, size_t n, uint32_t seed, int32_t n_draws, i
     std::mt19937 g(seed);
     std::discrete_distribution<> d(w, w + n);
     for (int i = 0; i < n_draws; ++i) out[i] = d(g);
+    return 0;
+  })
+}
+
+int wdr_process_segments(const wdr_segment* segs, size_t n_segs, const char* lang, const wdr_formatting_overrides* ov,
+                         int8_t has_mask, const double* vad_mask, size_t n_mask, wdr_segment_list** out) {
+  WDR_GUARD({
+    std::vector<Seg> in;
+    for (size_t i = 0; i < n_segs; ++i) {
+      Seg s;
+      s.start = segs[i].start;
+      s.end = segs[i].end;
+      s.text = segs[i].text ? segs[i].text : "";
+      s.has_words = segs[i].words != nullptr;
+      for (size_t k = 0; s.has_words && k < segs[i].n_words; ++k) {
+        Word w;
+        w.text = segs[i].words[k].text ? segs[i].words[k].text : "";
+        w.start = segs[i].words[k].start;
+        w.end = segs[i].words[k].end;
+        w.has_p = segs[i].words[k].has_probability != 0;
+        w.p = segs[i].words[k].probability;
+        s.words.push_back(std::move(w));
+      }
+      s.has_speaker = segs[i].speaker_id != nullptr;
+      if (s.has_speaker) s.speaker = segs[i].speaker_id;
+      in.push_back(std::move(s));
+    }
+    PostProcessConfig cfg = config_for_language(lang ? lang : "auto");
+    apply_overrides(cfg, ov);
+    std::vector<std::pair<double, double>> mask;
+    for (size_t i = 0; has_mask && i < n_mask; ++i) mask.push_back({vad_mask[2 * i], vad_mask[2 * i + 1]});
+    const std::vector<Seg> res = from_fmt(process_segments(to_fmt(in), cfg, has_mask ? &mask : nullptr));
+    *out = to_list(res, nullptr);
     return 0;
   })
 }

@@ -158,6 +158,73 @@ def _syn(s: Optional[Synthetic]):
     return L.Synthetic(s.weight_std, s.emb_std, s.force_len_rate, 1 if s.disable_fallback else 0)
 
 
+@dataclasses.dataclass
+class FormattingOverrides:                 # src/formatting.rs:37-51
+    max_chars_per_line: Optional[int] = None
+    max_lines: Optional[int] = None
+    cps_cap: Optional[float] = None
+    split_gap_sec: Optional[float] = None
+    comma_min_chars_before_allow: Optional[int] = None
+    min_word_dur: Optional[float] = None
+    min_sub_dur: Optional[float] = None
+    max_sub_dur: Optional[float] = None
+    soft_max_words_per_line: Optional[int] = None
+    insert_interword_space: Optional[bool] = None
+    use_grapheme_len: Optional[bool] = None
+    enforce_kinsoku: Optional[bool] = None
+    allow_comma_split: Optional[bool] = None
+
+
+def _fmt(ov: Optional[FormattingOverrides]):
+    if ov is None:
+        return None
+    f = L.FormattingOverrides()
+    for name in ("max_chars_per_line", "max_lines", "cps_cap", "split_gap_sec", "comma_min_chars_before_allow",
+                 "min_word_dur", "min_sub_dur", "max_sub_dur", "soft_max_words_per_line"):
+        v = getattr(ov, name)
+        setattr(f, "has_" + name, 0 if v is None else 1)
+        setattr(f, name, v or 0)
+    for name in ("insert_interword_space", "use_grapheme_len", "enforce_kinsoku", "allow_comma_split"):
+        setattr(f, name, _ob(getattr(ov, name)))
+    return f
+
+
+def _raw_segments(segs: List[Segment], keep: "_Keep"):
+    arr = (L.Segment * max(1, len(segs)))()
+    for i, sg in enumerate(segs):
+        arr[i].start, arr[i].end = sg.start, sg.end
+        arr[i].text = keep(sg.text.encode())
+        if sg.words is not None:
+            w = (L.Word * max(1, len(sg.words)))()
+            for k, x in enumerate(sg.words):
+                w[k].text = keep(x.text.encode())
+                w[k].start, w[k].end = x.start, x.end
+                w[k].has_probability = 0 if x.probability is None else 1
+                w[k].probability = x.probability or 0.0
+            keep(w)
+            arr[i].words = C.cast(w, C.POINTER(L.Word))
+            arr[i].n_words = len(sg.words)
+        arr[i].speaker_id = keep(None if sg.speaker_id is None else sg.speaker_id.encode())
+    keep(arr)
+    return arr
+
+
+def process_segments(segments: List[Segment], lang: str = "auto", overrides: Optional[FormattingOverrides] = None,
+                     vad_mask=None) -> List[Segment]:
+    """formatting::process_segments with PostProcessConfig::for_language(lang) + overrides and
+    an optional VAD mask oracle (src/engine.rs:192-199)."""
+    lib = L.load()
+    keep = _Keep()
+    arr = _raw_segments(segments, keep)
+    ov = _fmt(overrides)
+    m = np.ascontiguousarray(np.asarray(vad_mask if vad_mask is not None else [], np.float64).reshape(-1))
+    out = C.POINTER(L.SegmentList)()
+    L.check(lib.wdr_process_segments(arr, len(segments), lang.encode(), C.byref(ov) if ov is not None else None,
+                                     0 if vad_mask is None else 1, m.ctypes.data_as(C.POINTER(C.c_double)),
+                                     m.size // 2, C.byref(out)))
+    return _segments(out)[0]
+
+
 def _segments(lst_ptr) -> tuple:
     lst = lst_ptr.contents
     out = []
@@ -514,7 +581,9 @@ class Engine:
                          formatting_overrides=None, cb: Optional[Callbacks] = None) -> List[Segment]:
         keep = _Keep()
         out = C.POINTER(L.SegmentList)()
-        L.check(self._lib.wdr_transcribe_audio(self.h, audio_path.encode(), _opts(options, keep), None,
+        ov = _fmt(formatting_overrides)
+        L.check(self._lib.wdr_transcribe_audio(self.h, audio_path.encode(), _opts(options, keep),
+                                               C.byref(ov) if ov is not None else None,
                                                _callbacks(cb, keep), C.byref(out)))
         segs, _ = _segments(out)
         return segs

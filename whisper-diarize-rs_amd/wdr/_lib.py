@@ -41,7 +41,12 @@ class Synthetic(C.Structure):
 class FormattingOverrides(C.Structure):
     _fields_ = [("has_max_chars_per_line", i8), ("max_chars_per_line", u64), ("has_max_lines", i8),
                 ("max_lines", u64), ("has_cps_cap", i8), ("cps_cap", f64), ("has_split_gap_sec", i8),
-                ("split_gap_sec", f64)]
+                ("split_gap_sec", f64), ("has_comma_min_chars_before_allow", i8),
+                ("comma_min_chars_before_allow", u64), ("has_min_word_dur", i8), ("min_word_dur", f64),
+                ("has_min_sub_dur", i8), ("min_sub_dur", f64), ("has_max_sub_dur", i8), ("max_sub_dur", f64),
+                ("has_soft_max_words_per_line", i8), ("soft_max_words_per_line", u64),
+                ("insert_interword_space", i8), ("use_grapheme_len", i8), ("enforce_kinsoku", i8),
+                ("allow_comma_split", i8)]
 
 
 class Word(C.Structure):
@@ -96,6 +101,8 @@ _SIGS = {
     "wdr_transcribe_audio": (C.c_int, [vp, cstr, P(TranscribeOptions), P(FormattingOverrides), P(Callbacks),
                                        P(P(SegmentList))]),
     "wdr_read_wav": (C.c_int, [cstr, P(P(C.c_int16)), P(sz)]),
+    "wdr_process_segments": (C.c_int, [P(Segment), sz, cstr, P(FormattingOverrides), i8, P(f64), sz,
+                                       P(P(SegmentList))]),
     "wdr_free": (None, [vp]),
     "wdr_vad_merge": (C.c_int, [P(f64), P(f64), sz, P(C.c_int16), sz, P(f64), P(sz), P(f64), P(i64), P(sz)]),
     "wdr_vad_create": (C.c_int, [cstr, i8, i32, P(vp)]),
