@@ -1,17 +1,21 @@
 #!/usr/bin/env python3
 """xRT benchmark of the MI355X hot path (BASELINE.json metric: audio-sec / wall-sec).
 
-Workload (config.workload): BASELINE.json configs[2] per GPU — Whisper large-v3 (synthetic
-seeded weights, f16 operands / f32 accumulation), DTW word alignment on, greedy decode,
-lang "auto", 1 h of synthetic 16 kHz speech-like audio per rank, segmented by the
-generator's ground-truth talk-spurt table (the synthetic workload pin of BASELINE.md §2:
-decode length pinned to round(3.3 tok/s x window_s) + 3 tokens per window).  Weak scaling:
-every rank transcribes its own 1-h shard (seed = rank), no data-path collective.
+Workload (config.workload): the metric's "large-v3 + DTW + diarize" per GPU — BASELINE.json
+configs[3]'s diarized large-v3 pipeline on a 1-h shard per rank, with configs[2]'s greedy
+decode (the largest single-GPU configuration) — Whisper large-v3 (synthetic seeded weights,
+f16 operands / f32 accumulation), DTW word alignment on, lang "auto", 1 h of synthetic 16 kHz
+speech-like audio per rank (3 speakers).  `--seg vad` runs configs[2] exactly (Silero VAD
+instead of pyannote).  Synthetic workload pin: the segmentation kernels run
+and are timed over the whole shard, the segments handed downstream are the generator's
+ground-truth talk spurts, and the decode length is pinned to round(3.3 tok/s x window_s) + 3
+tokens per window.  Weak scaling: every rank transcribes its own 1-h shard (seed = rank).
 
-One step = run_transcription_pipeline over the rank's whole shard (mel, encoder, cross-K/V,
-language detection, prompt prefill, greedy decode, heuristic timestamps, DTW re-forward +
-alignment, reference glue).  Inputs (PCM) are host-resident as in the reference API; the
-PCIe share is negligible (115 MB/h) and included.
+One step = segmentation of the rank's whole shard (pyannote segmentation-3.0, or Silero VAD)
++ run_transcription_pipeline over its speech segments (mel, encoder, cross-K/V, language
+detection, prompt prefill, greedy decode, heuristic timestamps, DTW re-forward + alignment,
+CAM++ speaker embeddings + speaker assignment, reference glue).  Inputs (PCM) are
+host-resident as in the reference API; the PCIe share is negligible (115 MB/h) and included.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]   (N>1 via torch.distributed.run)
 """
@@ -41,6 +45,8 @@ def parse():
     ap.add_argument("--seconds", type=float, default=3600.0, help="audio seconds per rank")
     ap.add_argument("--prof", default="gemv", choices=["gemv", "gemm", "flash", "xattn", "none"],
                     help="kernel class timed live with HIP events for the roofline figure")
+    ap.add_argument("--seg", default="diarize", choices=["diarize", "vad"],
+                    help="segmentation stage: pyannote diarization (default) or Silero VAD")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU oracle work (rank 0, N=1)")
     return ap.parse_args()
@@ -117,7 +123,8 @@ def main():
         if torch.cuda.is_available():
             torch.cuda.synchronize()
 
-    pcm, spurts = synth_speech(args.seconds, seed=rank, n_speakers=1)
+    diarize = args.seg == "diarize"
+    pcm, spurts = synth_speech(args.seconds, seed=rank, n_speakers=3 if diarize else 1)
     segs = [wdr.SpeechSegment(a, b, pcm[int(round(a * 16000)):int(round(b * 16000))]) for a, b, _ in spurts]
     audio_s = float(sum(s.samples.size for s in segs)) / 16000.0   # speech seconds handed to the pipeline
     shard_s = pcm.size / 16000.0                                  # wall-clock audio covered (xRT basis)
@@ -126,19 +133,25 @@ def main():
     t_load = time.perf_counter()
     ctx = wdr.WhisperContext(args.model, gpu_device=local, enable_dtw=True, synthetic=syn)
     t_load = time.perf_counter() - t_load
-    opts = wdr.TranscribeOptions(model=args.model, lang="auto", enable_vad=True,
+    opts = wdr.TranscribeOptions(model=args.model, lang="auto", enable_vad=not diarize,
+                                 enable_diarize=True if diarize else None,
                                  advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
-    vad = wdr.Vad(gpu_device=local)
+    vad = None if diarize else wdr.Vad(gpu_device=local)
+    dia = wdr.Diarizer(gpu_device=local) if diarize else None
     lib = wdr._lib.load()
     prof_cls = {"none": 0, "gemm": 1, "gemv": 2, "flash": 3, "xattn": 4}[args.prof]
 
     def step():
-        # Silero VAD over the whole shard runs and is timed; in synthetic mode the segment list
-        # handed downstream is the generator's ground-truth spurt table (BASELINE.md §2 pin)
+        # the segmentation stage over the whole shard runs and is timed; in synthetic mode the
+        # segment list handed downstream is the generator's ground-truth spurt table
+        # (BASELINE.md §2 pin)
         t = time.perf_counter()
-        _, vsegs = vad.get_segments(pcm, materialize=False)
+        if diarize:
+            n_seg = len(dia.get_segments(pcm))
+        else:
+            n_seg = len(vad.get_segments(pcm, materialize=False)[1])
         vad_t[0] += time.perf_counter() - t
-        vad_t[1] = len(vsegs)
+        vad_t[1] = n_seg
         return ctx.run_pipeline(segs, opts)
 
     vad_t = [0.0, 0]
@@ -204,16 +217,22 @@ def main():
             "value": round(value, 3), "unit": "audio-sec/wall-sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt_max * 1e3 / args.steps, 1), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f16 (f32 accumulate)", "data": "synthetic",
-            "config": {"workload": "configs[2]: %s, %.0f s synthetic audio per rank (%d segments, %.0f s speech), "
-                                   "DTW on, greedy, lang auto, Silero VAD run + timed, ground-truth spurt "
-                                   "segmentation downstream (synthetic pin); diarize not on this path yet" % (args.model, shard_s, len(segs), audio_s),
+            "config": {"workload": ("configs[3] per-GPU shard with configs[2]'s greedy decode: %s + DTW + diarize "
+                                    "(pyannote segmentation-3.0 run + timed, CAM++ embeddings + speaker assignment), "
+                                    "%.0f s synthetic audio per rank (%d segments, %.0f s speech, 3 speakers), lang auto, "
+                                    "ground-truth spurt segments downstream (synthetic pin)" if diarize else
+                                    "configs[2]: %s + DTW, Silero VAD run + timed, %.0f s synthetic audio per rank "
+                                    "(%d segments, %.0f s speech), greedy, lang auto, ground-truth spurt segments "
+                                    "downstream (synthetic pin)") % (args.model, shard_s, len(segs), audio_s),
                        "model": args.model, "global_batch": len(segs) * world, "seq_len": 1500,
                        "parallelism": "dp%d (segment shards per rank)" % world},
             "roofline": roof, "cpu_baseline": cpu,
             "stages_s": {k: round(v, 3) for k, v in times.items() if isinstance(v, float)},
             "counts": {k: v for k, v in times.items() if isinstance(v, int)},
-            "vad": {"s_per_step": round(vad_t[0] / args.steps, 4), "segments": vad_t[1],
-                    "chunks": (pcm.size + 511) // 512, "us_per_chunk": round(vad.last_us_per_step, 3)},
+            "segmentation": ({"stage": "pyannote", "s_per_step": round(vad_t[0] / args.steps, 4), "segments": vad_t[1],
+                              "windows": pcm.size // 160000 + 1, "gpu_ms": round(dia.stats()[0], 2)} if diarize else
+                             {"stage": "silero", "s_per_step": round(vad_t[0] / args.steps, 4), "segments": vad_t[1],
+                              "chunks": (pcm.size + 511) // 512, "us_per_chunk": round(vad.last_us_per_step, 3)}),
             "load_s": round(t_load, 2), "segments_out": n_out // max(1, args.steps),
         }
         print(json.dumps(line), flush=True)

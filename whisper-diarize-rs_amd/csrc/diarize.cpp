@@ -288,7 +288,10 @@ static double mel_k(double f) { return 1127.0 * std::log(1.0 + f / 700.0); }
 
 CamModel::CamModel(int dev) : device(dev) {
   WDR_HIP(hipSetDevice(dev));
-  WDR_HIP(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking));
+  // lowest priority: embeddings run beside the latency-bound decode chain (EmbedAhead)
+  int lo = 0, hi = 0;
+  WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  WDR_HIP(hipStreamCreateWithPriority(&s_, hipStreamNonBlocking, lo));
   WDR_HIP(hipEventCreate(&e0_));
   WDR_HIP(hipEventCreate(&e1_));
   w_ = new W;

@@ -8,6 +8,7 @@
 //                                callbacks in reference order)
 //   src/engine.rs:65-200         transcribe_audio (segmentation choice, context, pipeline)
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -19,6 +20,10 @@
 #include <random>
 #include <string>
 #include <sys/stat.h>
+#include <condition_variable>
+#include <exception>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/wdr.h"
@@ -216,7 +221,55 @@ struct wdr_context {
   std::unique_ptr<State> st;
   std::unique_ptr<CamModel> cam;   // EmbeddingExtractor, created on the first diarized run
   double load_s = 0;
-  double embed_s = 0;              // host wall time spent in speaker embeddings
+  double embed_s = 0;              // wall time the decode chain waited on speaker embeddings
+};
+
+// Speaker embeddings of every speech segment, computed in segment order on a host worker
+// thread that drives CamModel's own low-priority stream, concurrently with the decode chain
+// (an embedding depends on the segment's PCM only, src/transcribe.rs:466).  finalize() of
+// segment i blocks until embedding i is done; errors surface there.
+class EmbedAhead {
+ public:
+  EmbedAhead(CamModel& cam, const std::vector<wdr_speech_segment>& segs)
+      : emb_(segs.size() * 512), ok_(segs.size(), 0) {
+    th_ = std::thread([this, &cam, &segs] {
+      try {
+        for (size_t i = 0; i < segs.size(); ++i) {
+          if (stop_) break;
+          const bool ok = cam.embed(segs[i].samples, segs[i].n_samples, emb_.data() + i * 512);
+          std::lock_guard<std::mutex> g(mu_);
+          ok_[i] = ok;
+          done_ = i + 1;
+          cv_.notify_all();
+        }
+      } catch (...) {
+        std::lock_guard<std::mutex> g(mu_);
+        err_ = std::current_exception();
+        cv_.notify_all();
+      }
+    });
+  }
+  ~EmbedAhead() {
+    stop_ = true;
+    if (th_.joinable()) th_.join();
+  }
+  // embedding of segment i (nullptr where the reference's ORT call fails -> speaker "?")
+  const float* get(size_t i) {
+    std::unique_lock<std::mutex> g(mu_);
+    cv_.wait(g, [&] { return done_ > i || err_; });
+    if (done_ <= i && err_) std::rethrow_exception(err_);
+    return ok_[i] ? emb_.data() + i * 512 : nullptr;
+  }
+
+ private:
+  std::vector<float> emb_;
+  std::vector<char> ok_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  size_t done_ = 0;
+  std::exception_ptr err_;
+  std::atomic<bool> stop_{false};
+  std::thread th_;
 };
 
 struct SynCfg {
@@ -459,7 +512,7 @@ static void emit_segment(const wdr_callbacks* cb, const Seg& s) {
   cb->new_segment(cb->user, &o);
 }
 
-// src/transcribe.rs:323-535 (diarization branch: not yet on this path)
+// src/transcribe.rs:323-535
 static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speech_segment>& segs,
                                      const wdr_transcribe_options* o, const SynCfg& syn, const wdr_callbacks* cb,
                                      std::string* detected_lang, bool* has_lang) {
@@ -469,6 +522,8 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
   diarize_options(o, &dthr, &dmax);
   SpeakerManager speakers(dmax);
   if (diarize && !c->cam) c->cam = std::make_unique<CamModel>(c->ctx->cp.gpu_device);
+  std::unique_ptr<EmbedAhead> embeds;
+  if (diarize) embeds = std::make_unique<EmbedAhead>(*c->cam, segs);
   FullParams params = setup_params(o, syn);
   const Vocab& v = c->ctx->vocab;
   const double user_offset = (o && o->has_offset) ? o->offset : 0.0;
@@ -531,8 +586,8 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
     const size_t i = P.i;
     const wdr_speech_segment& ss = segs[i];
     const double base_offset = ss.start + user_offset;
-    std::vector<float> emb(512);
-    bool have_emb = false, emb_ok = false;
+    const float* emb = nullptr;
+    bool have_emb = false;
     for (const ResultSeg& r : P.res) {
       std::string text = trim_start(r.text);
       const double approx_start = base_offset + cs_to_s(r.t0);
@@ -565,12 +620,12 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
         // segment in the reference; identical input -> computed once here), then assign
         if (!have_emb) {
           const double te = now_s();
-          emb_ok = c->cam->embed(ss.samples, ss.n_samples, emb.data());
+          emb = embeds->get(i);
           c->embed_s += now_s() - te;
           have_emb = true;
         }
         s.has_speaker = true;
-        s.speaker = speakers.assign(emb_ok ? emb.data() : nullptr, 512, dthr);
+        s.speaker = speakers.assign(emb, 512, dthr);
       }
       emit_segment(cb, s);
       if (cb && cb->progress) {
