@@ -247,6 +247,12 @@ int wdr_dbg_log_mel(wdr_context* c, const float* x, size_t n, int32_t seek, floa
 int wdr_dbg_energy(const float* x, size_t n, float* out);
 int wdr_dbg_encode(wdr_context* c, const float* mel_window /* [n_mels][3000] */, float* enc_out /* [1500][d] */);
 int wdr_dbg_decode(wdr_context* c, const int32_t* tokens, size_t n, float* logits_out /* [n_vocab] */);
+/* prefill tokens[0..n-2], then one decode step of tokens[n-1]; mode 0 = the persistent
+ * one-launch step (error if the model width has none), 1 = the per-kernel chain */
+int wdr_dbg_step(wdr_context* c, const int32_t* tokens, size_t n, int32_t mode, float* logits_out /* [n_vocab] */);
+/* timeline of the last persistent step (WDR_STEP_TRACE=1 at context creation): wall_clock64
+ * stamps [67][n_wg] (layer < 4: 16 events per layer; 64 start, 65 logits ready, 66 end) */
+int wdr_dbg_step_trace(wdr_context* c, uint64_t* out, int32_t cap, int32_t* n_wg);
 int wdr_dbg_capture(wdr_context* c, const int32_t* tokens, size_t n, float* cap_out /* [n_aheads][n][1500] */);
 int wdr_dbg_dtw(const float* cap, int32_t n_heads, int32_t n_tok, int32_t n_audio, int32_t sot_len, int32_t seek,
                 float* x_out /* [n_tok-sot_len-1][n_audio] */, int32_t* times_out, int32_t* n_times);

@@ -1183,6 +1183,21 @@ int wdr_dbg_decode(wdr_context* c, const int32_t* tokens, size_t n, float* logit
   })
 }
 
+int wdr_dbg_step(wdr_context* c, const int32_t* tokens, size_t n, int32_t mode, float* logits_out) {
+  WDR_GUARD({
+    if (mode == 0 && !c->st->persistent_step()) return fail("persistent step not available for this model");
+    c->st->dbg_step(tokens, (int)n, mode != 0, logits_out);
+    return 0;
+  })
+}
+
+int wdr_dbg_step_trace(wdr_context* c, uint64_t* out, int32_t cap, int32_t* n_wg) {
+  WDR_GUARD({
+    *n_wg = c->st->step_trace(out, cap);
+    return 0;
+  })
+}
+
 int wdr_dbg_capture(wdr_context* c, const int32_t* tokens, size_t n, float* cap_out) {
   WDR_GUARD({
     if (c->ctx->aheads.empty()) return fail("context created without DTW");

@@ -123,6 +123,34 @@ struct CaptureArgs {
 };
 void launch_aheads_capture(const CaptureArgs& a, int n_sel, hipStream_t s);
 
+// persistent greedy decode step (kernels/step.hip): one decoder row through all layers + logits
+struct StepLayer {
+  const f16 *w_qkv, *w_o, *w_xq, *w_xo, *w_fc1, *w_fc2;
+  const float *b_qkv, *b_o, *b_xq, *b_xo, *b_fc1, *b_fc2;
+  const float *ln1_g, *ln1_b, *ln2_g, *ln2_b, *ln3_g, *ln3_b;
+};
+struct StepArgs {
+  const StepLayer* layers;          // device table [L]
+  int L, d, n_head, V;
+  const f16* tok_emb;               // [V][d] (tied logits weights)
+  const float* ln_g; const float* ln_b;
+  const int* row_seq; const int* row_pos;
+  f16* kc; f16* vc;                 // self-attention caches; layer l at + l * layer_stride
+  long long layer_stride, seq_stride;
+  const f16* xkv; int ldxkv;        // cross K/V slot [1500][L*2d]
+  float* x;                         // [d] residual row (token + positional embedding on entry)
+  f16 *q, *att, *qx, *xatt, *mlp;   // [d] x4, [4d]
+  float* part_o; float2* part_ml;   // [24][n_head][64], [24][n_head]
+  float* logits;                    // [V]
+  unsigned* ctr;                    // step_counters(L, n_head), all zero between launches
+  int* err;                         // set to 1 when a wait gives up
+  float scale;
+  unsigned long long* trace = nullptr;   // optional [67][G] wall_clock64 timeline
+};
+int step_counters(int L, int n_head);
+bool step_supported(int d, int n_head);
+void launch_step(const StepArgs& a, int n_wg, hipStream_t s);
+
 // Silero VAD (kernels/vad.hip); layouts [out][in*k] f16, biases f32
 struct VadWeights {
   const f16* stft;                  // [258][256]

@@ -163,6 +163,9 @@ class State {
   void encode_from_mel_window(const float* mel_window);    // [n_mels][3000] normalised, host
   void read_encoder_out(float* out);                       // [1500][d] (ln_post output, f16 -> f32)
   void decode_logits(const int* toks, int n, float* logits_out);   // prefill from an empty cache
+  void dbg_step(const int* toks, int n, bool classic, float* logits_out);
+  bool persistent_step() const;
+  int step_trace(uint64_t* out, int cap);   // timeline of the last persistent step; returns G
   void dtw_capture(const int* toks, int n, float* cap_out);        // [n_aheads][n][1500]
 
   struct Impl;
@@ -182,6 +185,7 @@ class State {
                   hipStream_t st, const f16* xkv_base);
   void decoder_step(const int* toks, const int* seqs, const int* pos, int R);
   void decoder_step_body(int R);
+  void step_err_check();
   void step_and_sample(const int* toks, const int* seqs, const int* pos, const LogitsCtl* ctl, int R, TokenData* out,
                        int K = 0, BeamCand* cands = nullptr);
   void logits_topk(int R, int K, BeamCand* out);

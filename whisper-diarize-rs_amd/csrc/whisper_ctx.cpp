@@ -407,6 +407,13 @@ struct State::Impl {
     VocabIds vids{};
   };
   std::map<int, StepGraph> graphs;   // key: R * 256 + slot (the cross-K/V pointer is baked in)
+  // persistent one-row step (kernels/step.hip): layer table, counters, hand-off rows
+  bool st_on = false;
+  int st_wg = 0;
+  DevMem st_layers, st_ctr, st_q, st_att, st_qx, st_xatt, st_mlp;
+  DevMem st_trace;             // optional timeline (WDR_STEP_TRACE=1), [67][st_wg]
+  int* h_err = nullptr;        // pinned, mapped: set by the kernel when a wait gives up
+  int* d_err = nullptr;
 };
 
 static constexpr int kBatch = 4;     // encoder windows per encode-ahead launch (M = 6000 rows)
@@ -544,6 +551,39 @@ State::State(Context& ctx) : ctx_(ctx), s_(ctx.stream), m_(new Impl) {
                        m.mlpd.as<f16>(), m.rows_tok.as<int>(), m.rows_pos.as<int>(), m.rows_seq.as<int>(),
                        m.fpart_o.as<float>(), m.fpart_ml.as<float2>(), m.ml.as<float2>(), m.cap.as<float>(),
                        m.part_o.as<float>(), m.part_ml.as<float2>(), m.logits.as<float>(), m.h_rows};
+  // The persistent one-launch step is measured SLOWER than the per-kernel chain on MI355X
+  // (2.7 vs ~1.7 ms per large-v3 step: in-launch all-to-all hand-offs cost 2.5-7 us each, more
+  // than the ~1.2 us kernel boundaries they replace), so it is opt-in.
+  if (step_supported(d, m.H) && getenv("WDR_PSTEP") && atoi(getenv("WDR_PSTEP")) != 0) {
+    hipDeviceProp_t prop;
+    WDR_HIP(hipGetDeviceProperties(&prop, ctx.cp.gpu_device));
+    m.st_wg = prop.multiProcessorCount;   // one workgroup per CU
+    if (m.st_wg >= 12 * m.H && 2 * m.st_wg >= 24 * m.H && 2 * m.st_wg >= d / 4) {
+      std::vector<StepLayer> tab(m.L);
+      for (int l = 0; l < m.L; ++l) {
+        const DecLayer& e = ctx.model.dec[l];
+        tab[l] = StepLayer{e.w_qkv, e.w_o, e.w_xq, e.w_xo, e.w_fc1, e.w_fc2, e.b_qkv, e.b_o, e.b_xq, e.b_xo,
+                           e.b_fc1, e.b_fc2, e.ln1_g, e.ln1_b, e.ln2_g, e.ln2_b, e.ln3_g, e.ln3_b};
+      }
+      m.st_layers = DevMem(tab.size() * sizeof(StepLayer));
+      WDR_HIP(hipMemcpy(m.st_layers.p, tab.data(), tab.size() * sizeof(StepLayer), hipMemcpyHostToDevice));
+      m.st_ctr = DevMem((size_t)step_counters(m.L, m.H) * 4);
+      WDR_HIP(hipMemset(m.st_ctr.p, 0, m.st_ctr.bytes));
+      m.st_q = DevMem((size_t)d * 2);
+      m.st_att = DevMem((size_t)d * 2);
+      m.st_qx = DevMem((size_t)d * 2);
+      m.st_xatt = DevMem((size_t)d * 2);
+      m.st_mlp = DevMem((size_t)4 * d * 2);
+      WDR_HIP(hipHostMalloc((void**)&m.h_err, 64, hipHostMallocMapped | hipHostMallocCoherent));
+      *m.h_err = 0;
+      WDR_HIP(hipHostGetDevicePointer((void**)&m.d_err, m.h_err, 0));
+      if (getenv("WDR_STEP_TRACE")) {
+        m.st_trace = DevMem((size_t)67 * m.st_wg * 8);
+        WDR_HIP(hipMemset(m.st_trace.p, 0, m.st_trace.bytes));
+      }
+      m.st_on = true;
+    }
+  }
   const Vocab& v = ctx.vocab;
   m.vids = VocabIds{v.n_vocab, v.eot, v.sot, v.translate, v.transcribe, v.solm, v.prev, v.nosp, v.not_, v.beg,
                     v.token_to_id.at(" "), v.sot + 1, 100, -1, 1};
@@ -559,6 +599,7 @@ State::~State() {
     (void)hipHostFree(m_->h_times);
     (void)hipHostFree(m_->h_beam);
     (void)hipHostFree(m_->h_pairs);
+    if (m_->h_err) (void)hipHostFree(m_->h_err);
     if (m_->es) {
       (void)hipStreamSynchronize(m_->es);
       (void)hipStreamDestroy(m_->es);
@@ -870,6 +911,16 @@ void State::decoder_step_body(int R) {
   const int d = m.d, L = m.L;
   launch_embed(md.tok_emb, md.dec_pos, m.rows_tok.as<int>(), m.rows_pos.as<int>(), R, d, m.xd.as<float>(), s_);
   const float scale = 1.0f / 8.0f;
+  if (R == 1 && m.st_on) {
+    StepArgs a{m.st_layers.as<StepLayer>(), L, d, m.H, m.V, md.tok_emb, md.ln_g, md.ln_b, m.rows_seq.as<int>(),
+               m.rows_pos.as<int>(), m.kc.as<f16>(), m.vc.as<f16>(), (long long)NSLOT * m.seq_stride, m.seq_stride,
+               m.xkv(), L * 2 * d, m.xd.as<float>(), m.st_q.as<f16>(), m.st_att.as<f16>(), m.st_qx.as<f16>(),
+               m.st_xatt.as<f16>(), m.st_mlp.as<f16>(), m.part_o.as<float>(), m.part_ml.as<float2>(),
+               m.logits.as<float>(), m.st_ctr.as<unsigned>(), m.d_err, scale};
+    a.trace = m.st_trace.p ? m.st_trace.as<unsigned long long>() : nullptr;
+    launch_step(a, m.st_wg, s_);
+    return;
+  }
   const int ldxkv = L * 2 * d;
   auto P = [&](const f16* A, int lda, const f16* W, const float* b, void* out, int ldo, int N, int K, int epi,
                const float* lng = nullptr, const float* lnb = nullptr) {
@@ -908,6 +959,16 @@ void State::decoder_step_body(int R) {
     launch_proj(P(m.mlpd.as<f16>(), 4 * d, e.w_fc2, e.b_fc2, m.xd.p, d, d, 4 * d, EPI_F32_RESID), s_);
   }
   launch_proj(P(nullptr, d, md.tok_emb, nullptr, m.logits.p, m.V, m.V, d, EPI_F32, md.ln_g, md.ln_b), s_);
+}
+
+// after a synchronised step: a persistent-step wait that gave up leaves counters behind
+void State::step_err_check() {
+  Impl& m = *m_;
+  if (!m.h_err || !*(volatile int*)m.h_err) return;
+  WDR_HIP(hipMemsetAsync(m.st_ctr.p, 0, m.st_ctr.bytes, s_));
+  WDR_HIP(hipStreamSynchronize(s_));
+  *(volatile int*)m.h_err = 0;
+  throw std::runtime_error("persistent decode step: a hand-off wait timed out");
 }
 
 void State::decoder_step(const int* toks, const int* seqs, const int* pos, int R) {
@@ -980,6 +1041,7 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
   }
   WDR_HIP(hipGraphLaunch(g.exec, s_));
   WDR_HIP(hipStreamSynchronize(s_));
+  step_err_check();
   if (K > 0) memcpy(cands, m.h_beam, (size_t)R * K * sizeof(BeamCand));
   for (int r = 0; r < R; ++r) {
     const TokOut& o = m.h_tok[r];
@@ -1003,6 +1065,7 @@ void State::run_logits(int R, const LogitsCtl* ctl, TokenData* out, float* nosp)
                         m.tokout.as<TokOut>(), s_);
   WDR_HIP(hipMemcpyAsync(m.h_tok, m.tokout.p, R * sizeof(TokOut), hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
+  step_err_check();
   for (int r = 0; r < R; ++r) {
     const TokOut& o = m.h_tok[r];
     TokenData t;
@@ -1046,6 +1109,37 @@ void State::kv_reorder(const std::vector<std::pair<int, int>>& moves, int n_rows
   launch_kv_copy(m.kc.as<f16>(), m.vc.as<f16>(), m.seq_stride, NSLOT, m.L, m.kvpairs.as<int>() + 2 * NSEQ, n, n_rows,
                  m.d, s_);
   WDR_HIP(hipStreamSynchronize(s_));   // the pinned pair table is rewritten by the next reorder
+}
+
+// test seam: prefill toks[0..n-2] into sequence 0, then ONE decode step of toks[n-1] at
+// position n-1; classic = the per-kernel chain instead of the persistent step
+void State::dbg_step(const int* toks, int n, bool classic, float* logits_out) {
+  Impl& m = *m_;
+  WDR_CHECK(n >= 2 && n <= 448, "dbg_step: need 2..448 tokens");
+  decoder_prefill(toks, n - 1, 0, false, false);
+  const bool on = m.st_on;
+  if (classic) m.st_on = false;
+  const int tok = toks[n - 1], seq = 0, pos = n - 1;
+  try {
+    decoder_step(&tok, &seq, &pos, 1);
+  } catch (...) {
+    m.st_on = on;
+    throw;
+  }
+  m.st_on = on;
+  WDR_HIP(hipMemcpyAsync(logits_out, m.logits.p, (size_t)m.V * 4, hipMemcpyDeviceToHost, s_));
+  WDR_HIP(hipStreamSynchronize(s_));
+  step_err_check();
+}
+
+bool State::persistent_step() const { return m_->st_on; }
+
+int State::step_trace(uint64_t* out, int cap) {
+  Impl& m = *m_;
+  if (!m.st_trace.p) return 0;
+  const int n = std::min(cap, 67 * m.st_wg);
+  WDR_HIP(hipMemcpy(out, m.st_trace.p, (size_t)n * 8, hipMemcpyDeviceToHost));
+  return m.st_wg;
 }
 
 void State::decode_logits(const int* toks, int n, float* logits_out) {

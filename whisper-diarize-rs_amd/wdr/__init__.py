@@ -550,6 +550,15 @@ class WhisperContext:
                                          out.ctypes.data_as(C.POINTER(C.c_float))))
         return out
 
+    def step(self, tokens, classic: bool = False) -> np.ndarray:
+        """Prefill tokens[:-1], then one decode step of tokens[-1] (persistent one-launch step,
+        or the per-kernel chain when classic)."""
+        t = np.ascontiguousarray(tokens, np.int32)
+        out = np.zeros(self.hparams["n_vocab"], np.float32)
+        L.check(self._lib.wdr_dbg_step(self.h, t.ctypes.data_as(C.POINTER(C.c_int32)), t.size, 1 if classic else 0,
+                                       out.ctypes.data_as(C.POINTER(C.c_float))))
+        return out
+
     def capture(self, tokens, n_aheads: int) -> np.ndarray:
         t = np.ascontiguousarray(tokens, np.int32)
         out = np.zeros((n_aheads, t.size, 1500), np.float32)
