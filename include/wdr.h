@@ -118,6 +118,8 @@ typedef struct {
 typedef struct {
   wdr_segment* segments; size_t n_segments;
   const char* detected_lang;              /* Option<String> (run_transcription_pipeline's second result) */
+  const int64_t* speech_index;            /* wdr_run_pipeline only: index of the input SpeechSegment each
+                                             segment came from (NULL elsewhere); not in the Rust API */
 } wdr_segment_list;
 
 /* SpeechSegment, src/types.rs:86-90 (samples borrowed) */
@@ -197,6 +199,10 @@ int wdr_diarize_frame_classes(wdr_diarizer* d, const int16_t* samples, size_t n,
  * (slices of the zero-padded buffer); free with wdr_free(*segs_out) */
 int wdr_diarize_get_segments(wdr_diarizer* d, const int16_t* samples, size_t n, wdr_speech_segment** segs_out,
                              size_t* n_segs);
+/* the same stitching from frame classes computed elsewhere (e.g. window shards on several GPUs):
+ * cls [n / 160000 + 1][589] of the n-sample file; free with wdr_free(*segs_out) */
+int wdr_diarize_segments_from_classes(const int32_t* cls, size_t n_windows, const int16_t* samples, size_t n,
+                                      wdr_speech_segment** segs_out, size_t* n_segs);
 /* EmbeddingExtractor::compute pieces: features after CMN [T][80] (capacity n/160 + 1 rows), and
  * the 512-d embedding; ok = 0 where the reference's ONNX call fails (fewer than 400 samples) */
 int wdr_diarize_fbank(wdr_diarizer* d, const int16_t* samples, size_t n, float* feats_out, size_t* n_frames);
@@ -216,6 +222,11 @@ int wdr_context_create(const char* model_path, const char* model_name, int8_t ha
 void wdr_context_free(wdr_context* c);
 int wdr_run_pipeline(wdr_context* c, const wdr_speech_segment* segs, size_t n_segs, const wdr_transcribe_options* opts,
                      const wdr_synthetic* syn, const wdr_callbacks* cb, wdr_segment_list** out);
+/* run_pipeline without the cross-segment overlap clip and without speaker assignment, with
+ * speech_index set: building block of the multi-GPU one-file path (wdr/distributed.py), which
+ * applies both over the merged, ordered blocks of every GPU */
+int wdr_run_pipeline_raw(wdr_context* c, const wdr_speech_segment* segs, size_t n_segs,
+                         const wdr_transcribe_options* opts, const wdr_synthetic* syn, wdr_segment_list** out);
 void wdr_segment_list_free(wdr_segment_list* l);
 int wdr_context_stage_times(wdr_context* c, wdr_stage_times* out);
 int wdr_context_hparams(wdr_context* c, int32_t* out /* [10] */);

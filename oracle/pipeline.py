@@ -214,8 +214,10 @@ def setup_params(options: dict) -> FullParams:
     return p
 
 
-def run_transcription_pipeline(state: WhisperState, speech_segments, options: dict):
-    """src/transcribe.rs:323-535 without diarization.  Returns (segments, detected_lang)."""
+def run_transcription_pipeline(state: WhisperState, speech_segments, options: dict, raw: bool = False):
+    """src/transcribe.rs:323-535 without diarization.  Returns (segments, detected_lang).
+    raw: no overlap clip against the next segment; returns (results grouped per speech
+    segment, detected_lang) -- the form wdr_run_pipeline_raw / the multi-GPU merge use."""
     vocab = state.v
     params = setup_params(options)
     user_offset = options.get("offset") or 0.0
@@ -226,7 +228,9 @@ def run_transcription_pipeline(state: WhisperState, speech_segments, options: di
     if lang is not None and lang != "auto":
         detected_lang = lang
     translated = bool(options.get("whisper_to_english"))
+    groups = []
     for i, ss in enumerate(speech_segments):
+        groups.append([])
         samples = pcm_i16_to_f32(ss.samples)
         if previous_text is not None:
             params.initial_prompt = previous_text
@@ -248,7 +252,7 @@ def run_transcription_pipeline(state: WhisperState, speech_segments, options: di
                     w.end += base_offset
             seg_start = words[0].start if words else approx_start
             seg_end = words[-1].end if words else approx_end
-            if segments:
+            if segments and not raw:
                 last = segments[-1]
                 if last.end > seg_start:
                     last.end = seg_start
@@ -257,4 +261,7 @@ def run_transcription_pipeline(state: WhisperState, speech_segments, options: di
                         last.words[-1].end = last.end
             previous_text = text if text.strip() else None
             segments.append(Segment(seg_start, seg_end, text, words or None, None))
+            groups[-1].append(segments[-1])
+    if raw:
+        return groups, detected_lang
     return segments, detected_lang

@@ -226,7 +226,10 @@ std::vector<int> SegModel::frame_classes(const int16_t* pcm, size_t n, std::vect
 // lazy iterator yields one queued segment per window and stops at the first window whose
 // queue is empty (restated as published).
 std::vector<DiarSegment> SegModel::get_segments(const int16_t* pcm, size_t n) {
-  const std::vector<int> cls = frame_classes(pcm, n);
+  return diar_stitch(frame_classes(pcm, n), n);
+}
+
+std::vector<DiarSegment> diar_stitch(const std::vector<int>& cls, size_t n) {
   const size_t padded = n + (kWin - n % kWin);
   const size_t nw = padded / kWin;
   size_t offset = kFrameStart;

@@ -18,6 +18,10 @@ struct DiarSegment {   // pyannote_rs::Segment
   size_t start_idx, end_idx;   // into the zero-padded buffer
 };
 
+// pyannote_rs::get_segments' stitching of per-window frame classes [n/160000 + 1][589] of an
+// n-sample file (the classes may come from several GPUs' window shards)
+std::vector<DiarSegment> diar_stitch(const std::vector<int>& cls, size_t n);
+
 class SegModel {
  public:
   explicit SegModel(int device);

@@ -146,6 +146,7 @@ struct Seg {
   bool has_words = false;
   bool has_speaker = false;
   std::string speaker;
+  int64_t src = -1;   // input SpeechSegment index (run_pipeline)
 };
 
 static double cs_to_s(long long cs) { return (double)cs * 0.01; }
@@ -499,6 +500,11 @@ static wdr_segment_list* to_list(const std::vector<Seg>& segs, const std::string
     o.speaker_id = segs[i].has_speaker ? strdup(segs[i].speaker.c_str()) : nullptr;
   }
   l->detected_lang = lang ? strdup(lang->c_str()) : nullptr;
+  if (!segs.empty() && segs[0].src >= 0) {
+    auto* ix = (int64_t*)calloc(segs.size(), sizeof(int64_t));
+    for (size_t i = 0; i < segs.size(); ++i) ix[i] = segs[i].src;
+    l->speech_index = ix;
+  }
   return l;
 }
 
@@ -513,10 +519,12 @@ static void emit_segment(const wdr_callbacks* cb, const Seg& s) {
 }
 
 // src/transcribe.rs:323-535
+// raw: per-segment results only (no overlap clip against the next segment, no speakers): the
+// multi-GPU path (wdr/distributed.py) merges several GPUs' raw blocks and applies both in order.
 static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speech_segment>& segs,
                                      const wdr_transcribe_options* o, const SynCfg& syn, const wdr_callbacks* cb,
-                                     std::string* detected_lang, bool* has_lang) {
-  const bool diarize = o && o->enable_diarize == 1;
+                                     std::string* detected_lang, bool* has_lang, bool raw = false) {
+  const bool diarize = o && o->enable_diarize == 1 && !raw;
   float dthr = 0.5f;
   uint64_t dmax = UINT64_MAX;
   diarize_options(o, &dthr, &dmax);
@@ -604,7 +612,7 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
       }
       const double seg_start = words.empty() ? approx_start : words.front().start;
       const double seg_end = words.empty() ? approx_end : words.back().end;
-      if (!out.empty()) {
+      if (!out.empty() && !raw) {
         Seg& last = out.back();
         if (last.end > seg_start) last.end = seg_start;
         if (last.has_words && !last.words.empty() && last.words.back().end > last.end) last.words.back().end = last.end;
@@ -615,6 +623,7 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
       s.text = text;
       s.has_words = !words.empty();
       s.words = std::move(words);
+      s.src = (int64_t)i;
       if (diarize) {
         // src/transcribe.rs:461-497: embed the whole speech segment (recomputed per whisper
         // segment in the reference; identical input -> computed once here), then assign
@@ -711,6 +720,31 @@ static std::vector<int16_t> read_wav_impl(const char* path) {
 }
 
 // ------------------------------------------------------------------ ABI
+static int diar_segments_out(const std::vector<DiarSegment>& ds, const int16_t* samples, size_t n,
+                             wdr_speech_segment** segs_out, size_t* n_segs) {
+  {
+    size_t tot = 0;
+    for (auto& x : ds) tot += x.end_idx - x.start_idx;
+    // one allocation: the segment array followed by copies of their (zero-padded) samples
+    const size_t head = std::max<size_t>(1, ds.size()) * sizeof(wdr_speech_segment);
+    char* blk = (char*)malloc(head + std::max<size_t>(1, tot) * 2);
+    wdr_speech_segment* sg = (wdr_speech_segment*)blk;
+    int16_t* dst = (int16_t*)(blk + head);
+    for (size_t i = 0; i < ds.size(); ++i) {
+      const size_t len = ds[i].end_idx - ds[i].start_idx;
+      for (size_t k = 0; k < len; ++k) {
+        const size_t src = ds[i].start_idx + k;
+        dst[k] = src < n ? samples[src] : 0;
+      }
+      sg[i] = {ds[i].start, ds[i].end, dst, len};
+      dst += len;
+    }
+    *segs_out = sg;
+    *n_segs = ds.size();
+    return 0;
+  }
+}
+
 extern "C" {
 
 const char* wdr_last_error(void) { return g_err.c_str(); }
@@ -885,27 +919,15 @@ int wdr_diarize_frame_classes(wdr_diarizer* d, const int16_t* samples, size_t n,
 
 int wdr_diarize_get_segments(wdr_diarizer* d, const int16_t* samples, size_t n, wdr_speech_segment** segs_out,
                              size_t* n_segs) {
+  WDR_GUARD({ return diar_segments_out(d->S().get_segments(samples, n), samples, n, segs_out, n_segs); })
+}
+
+int wdr_diarize_segments_from_classes(const int32_t* cls, size_t n_windows, const int16_t* samples, size_t n,
+                                      wdr_speech_segment** segs_out, size_t* n_segs) {
   WDR_GUARD({
-    const std::vector<DiarSegment> ds = d->S().get_segments(samples, n);
-    size_t tot = 0;
-    for (auto& x : ds) tot += x.end_idx - x.start_idx;
-    // one allocation: the segment array followed by copies of their (zero-padded) samples
-    const size_t head = std::max<size_t>(1, ds.size()) * sizeof(wdr_speech_segment);
-    char* blk = (char*)malloc(head + std::max<size_t>(1, tot) * 2);
-    wdr_speech_segment* sg = (wdr_speech_segment*)blk;
-    int16_t* dst = (int16_t*)(blk + head);
-    for (size_t i = 0; i < ds.size(); ++i) {
-      const size_t len = ds[i].end_idx - ds[i].start_idx;
-      for (size_t k = 0; k < len; ++k) {
-        const size_t src = ds[i].start_idx + k;
-        dst[k] = src < n ? samples[src] : 0;
-      }
-      sg[i] = {ds[i].start, ds[i].end, dst, len};
-      dst += len;
-    }
-    *segs_out = sg;
-    *n_segs = ds.size();
-    return 0;
+    if (n_windows != n / 160000 + 1) return fail("frame classes: expected n / 160000 + 1 windows");
+    std::vector<int> c(cls, cls + n_windows * 589);
+    return diar_segments_out(diar_stitch(c, n), samples, n, segs_out, n_segs);
   })
 }
 
@@ -1077,6 +1099,22 @@ int wdr_run_pipeline(wdr_context* c, const wdr_speech_segment* segs, size_t n_se
   })
 }
 
+int wdr_run_pipeline_raw(wdr_context* c, const wdr_speech_segment* segs, size_t n_segs,
+                         const wdr_transcribe_options* o, const wdr_synthetic* syn, wdr_segment_list** out) {
+  WDR_GUARD({
+    std::vector<wdr_speech_segment> v(segs, segs + n_segs);
+    std::string lang;
+    bool has_lang = false;
+    const double t = now_s();
+    c->st->times = StageTimes{};
+    std::vector<Seg> res = run_pipeline(c, v, o, syn_of(syn), nullptr, &lang, &has_lang, true);
+    c->st->times.glue = now_s() - t;
+    *out = to_list(res, has_lang ? &lang : nullptr);
+    if (!(*out)->speech_index && !res.empty()) return fail("raw pipeline: missing speech index");
+    return 0;
+  })
+}
+
 void wdr_segment_list_free(wdr_segment_list* l) {
   if (!l) return;
   for (size_t i = 0; i < l->n_segments; ++i) {
@@ -1088,6 +1126,7 @@ void wdr_segment_list_free(wdr_segment_list* l) {
   }
   free(l->segments);
   free((void*)l->detected_lang);
+  free((void*)l->speech_index);
   free(l);
 }
 

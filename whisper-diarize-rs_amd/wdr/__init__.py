@@ -225,8 +225,9 @@ def process_segments(segments: List[Segment], lang: str = "auto", overrides: Opt
     return _segments(out)[0]
 
 
-def _segments(lst_ptr) -> tuple:
+def _segments(lst_ptr, with_index: bool = False) -> tuple:
     lst = lst_ptr.contents
+    index = [int(lst.speech_index[i]) for i in range(lst.n_segments)] if lst.speech_index else None
     out = []
     for i in range(lst.n_segments):
         s = lst.segments[i]
@@ -239,7 +240,7 @@ def _segments(lst_ptr) -> tuple:
                            s.speaker_id.decode() if s.speaker_id else None))
     lang = lst.detected_lang.decode() if lst.detected_lang else None
     L.load().wdr_segment_list_free(lst_ptr)
-    return out, lang
+    return (out, lang, index) if with_index else (out, lang)
 
 
 def _callbacks(cb: Optional[Callbacks], keep: _Keep):
@@ -426,6 +427,23 @@ class Diarizer:
         finally:
             self._lib.wdr_free(C.cast(sp, C.c_void_p))
 
+    @staticmethod
+    def segments_from_classes(cls: np.ndarray, samples: np.ndarray):
+        """pyannote_rs::get_segments' stitching of frame classes [n/160000 + 1][589] computed
+        elsewhere (window shards of several GPUs)."""
+        smp = np.ascontiguousarray(samples, np.int16)
+        c = np.ascontiguousarray(cls, np.int32)
+        sp, ns = C.POINTER(L.SpeechSegment)(), C.c_size_t()
+        lib = L.load()
+        L.check(lib.wdr_diarize_segments_from_classes(c.ctypes.data_as(C.POINTER(C.c_int32)), c.shape[0],
+                                                      smp.ctypes.data_as(C.POINTER(C.c_int16)), smp.size,
+                                                      C.byref(sp), C.byref(ns)))
+        try:
+            return [SpeechSegment(sp[i].start, sp[i].end, np.ctypeslib.as_array(sp[i].samples, (sp[i].n_samples,)).copy()
+                                  if sp[i].n_samples else np.zeros(0, np.int16)) for i in range(ns.value)]
+        finally:
+            lib.wdr_free(C.cast(sp, C.c_void_p))
+
     def fbank(self, samples: np.ndarray) -> np.ndarray:
         smp = np.ascontiguousarray(samples, np.int16)
         out = np.zeros((smp.size // 160 + 1, 80), np.float32)
@@ -490,7 +508,9 @@ class WhisperContext:
 
     # -- run_transcription_pipeline (src/transcribe.rs:323-535)
     def run_pipeline(self, speech_segments, options: TranscribeOptions, callbacks: Optional[Callbacks] = None,
-                     synthetic: Optional[Synthetic] = None):
+                     synthetic: Optional[Synthetic] = None, with_index: bool = False):
+        """transcribe::run_transcription_pipeline -> (segments, detected_lang) [+ the input
+        SpeechSegment index of every output segment when with_index]."""
         keep = _Keep()
         arr = (L.SpeechSegment * max(1, len(speech_segments)))()
         for i, s in enumerate(speech_segments):
@@ -501,7 +521,22 @@ class WhisperContext:
         L.check(self._lib.wdr_run_pipeline(self.h, arr, len(speech_segments), _opts(options, keep),
                                            C.byref(syn) if syn else None, _callbacks(callbacks, keep),
                                            C.byref(out)))
-        return _segments(out)
+        return _segments(out, with_index)
+
+    def run_pipeline_raw(self, speech_segments, options: TranscribeOptions, synthetic: Optional[Synthetic] = None):
+        """run_pipeline without the cross-segment overlap clip and speaker assignment
+        (wdr_run_pipeline_raw): (segments, detected_lang, speech index per segment)."""
+        keep = _Keep()
+        arr = (L.SpeechSegment * max(1, len(speech_segments)))()
+        for i, s in enumerate(speech_segments):
+            smp = keep(np.ascontiguousarray(s.samples, np.int16))
+            arr[i] = L.SpeechSegment(s.start, s.end, smp.ctypes.data_as(C.POINTER(C.c_int16)), smp.size)
+        out = C.POINTER(L.SegmentList)()
+        syn = _syn(synthetic or self.synthetic)
+        L.check(self._lib.wdr_run_pipeline_raw(self.h, arr, len(speech_segments), _opts(options, keep),
+                                               C.byref(syn) if syn else None, C.byref(out)))
+        segs, lang, index = _segments(out, True)
+        return segs, lang, index or []
 
     def stage_times(self) -> dict:
         t = L.StageTimes()

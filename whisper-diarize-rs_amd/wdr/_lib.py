@@ -59,7 +59,8 @@ class Segment(C.Structure):
 
 
 class SegmentList(C.Structure):
-    _fields_ = [("segments", C.POINTER(Segment)), ("n_segments", sz), ("detected_lang", cstr)]
+    _fields_ = [("segments", C.POINTER(Segment)), ("n_segments", sz), ("detected_lang", cstr),
+                ("speech_index", C.POINTER(C.c_int64))]
 
 
 class SpeechSegment(C.Structure):
@@ -115,6 +116,7 @@ _SIGS = {
     "wdr_diarizer_free": (None, [vp]),
     "wdr_diarize_frame_classes": (C.c_int, [vp, P(C.c_int16), sz, P(i32), P(f32)]),
     "wdr_diarize_get_segments": (C.c_int, [vp, P(C.c_int16), sz, P(P(SpeechSegment)), P(sz)]),
+    "wdr_diarize_segments_from_classes": (C.c_int, [P(i32), sz, P(C.c_int16), sz, P(P(SpeechSegment)), P(sz)]),
     "wdr_diarize_fbank": (C.c_int, [vp, P(C.c_int16), sz, P(f32), P(sz)]),
     "wdr_diarize_embedding": (C.c_int, [vp, P(C.c_int16), sz, P(f32), P(i8)]),
     "wdr_diarize_stats": (C.c_int, [vp, P(f64), P(f64)]),
@@ -123,6 +125,8 @@ _SIGS = {
     "wdr_speakers_assign": (C.c_int, [vp, P(f32), i32, f32, C.c_char_p, sz]),
     "wdr_context_create": (C.c_int, [cstr, cstr, i8, i32, i8, i8, i8, i8, u64, P(Synthetic), P(vp)]),
     "wdr_context_free": (None, [vp]),
+    "wdr_run_pipeline_raw": (C.c_int, [vp, P(SpeechSegment), sz, P(TranscribeOptions), P(Synthetic),
+                                       P(P(SegmentList))]),
     "wdr_run_pipeline": (C.c_int, [vp, P(SpeechSegment), sz, P(TranscribeOptions), P(Synthetic), P(Callbacks),
                                    P(P(SegmentList))]),
     "wdr_segment_list_free": (None, [P(SegmentList)]),
