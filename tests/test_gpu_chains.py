@@ -1,0 +1,48 @@
+"""Multi-chain decoding (engine.cpp decode_chains + StepBatcher): C States decode C contiguous
+blocks of the speech segments concurrently with their greedy steps batched into one C-row
+step, then the exact prompt-chain fix-up.  The result must equal the single-chain pipeline's
+EXACTLY (texts, times, words, speakers), including the sampled path (temperature fallback:
+decoder 0's RNG state replayed from the first segment that drew)."""
+import dataclasses
+
+import numpy as np
+import pytest
+
+import wdr
+from wdr.synth import synth_speech
+
+pytestmark = pytest.mark.gpu
+
+
+def _segs(pcm, spurts):
+    return [wdr.SpeechSegment(a, b, pcm[int(round(a * 16000)):int(round(b * 16000))]) for a, b, _ in spurts]
+
+
+def _run(ctx, segs, opts, chains):
+    ctx.set_chains(chains)
+    out, lang = ctx.run_pipeline(segs, opts)
+    return [dataclasses.asdict(s) for s in out], lang
+
+
+@pytest.mark.parametrize("name,seconds,fallback,diarize", [
+    ("tiny-test", 80.0, False, False),
+    ("tiny-test", 80.0, False, True),
+    ("tiny-test", 60.0, True, False),
+    ("large-v3", 40.0, False, False),
+])
+def test_chains_equal_single_chain(name, seconds, fallback, diarize):
+    syn = wdr.Synthetic(weight_std=0.02, emb_std=0.5, force_len_rate=0.0 if fallback else 3.3,
+                        disable_fallback=not fallback)
+    ctx = wdr.WhisperContext(name, synthetic=syn)
+    pcm, spurts = synth_speech(seconds, seed=11, n_speakers=2)
+    segs = _segs(pcm, spurts)
+    assert len(segs) >= 6
+    opts = wdr.TranscribeOptions(lang="auto", enable_diarize=True if diarize else None,
+                                 advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    ref, lang1 = _run(ctx, segs, opts, 1)
+    for chains in (2, 4):
+        got, lang = _run(ctx, segs, opts, chains)
+        assert lang == lang1
+        assert [s["text"] for s in got] == [s["text"] for s in ref], chains
+        assert got == ref, chains
+    ctx.close()

@@ -67,8 +67,14 @@ def main():
                 vad.get_segments(pcm)   # runs and is discarded (the pin)
             return [wdr.SpeechSegment(x, y, pcm[int(round(x * 16000)):int(round(y * 16000))]) for x, y in spurts]
         pin = pinned
+    import time
+    dist.barrier()
+    t0 = time.perf_counter()
     res = D.transcribe_file(pcm, opts, ctx=ctx, segmentation=args.seg, diarizer=dia, vad=vad,
                             speech_segments_fn=pin)
+    dist.barrier()
+    wall = time.perf_counter() - t0
+    print("rank %d: wall %.3f s, block %s" % (rank, wall, json.dumps(D.last_stats)), file=sys.stderr, flush=True)
     if rank == 0:
         segs, lang = res
         doc = json.dumps({"lang": lang, "segments": [dataclasses.asdict(s) for s in segs]})

@@ -220,6 +220,8 @@ static std::vector<Word> interpolate_word_timestamps(const std::string& line, do
 struct wdr_context {
   std::unique_ptr<Context> ctx;
   std::unique_ptr<State> st;
+  std::vector<std::unique_ptr<State>> chain_st;   // decode chains 1.. (multi-chain pipeline)
+  int chains = 1;                                 // decode chains per run_pipeline call
   std::unique_ptr<CamModel> cam;   // EmbeddingExtractor, created on the first diarized run
   double load_s = 0;
   double embed_s = 0;              // wall time the decode chain waited on speaker embeddings
@@ -407,6 +409,7 @@ static std::unique_ptr<wdr_context> make_context(const std::string& model_name, 
   try {
     c->ctx = std::make_unique<Context>(model_name, hp, cp);
     c->st = std::make_unique<State>(*c->ctx);
+    c->chains = c->ctx->max_chains;   // WDR_DECODE_CHAINS (default 4), wdr_context_set_chains
   } catch (const std::exception& ex) {
     throw std::runtime_error(std::string("create whisper context crash: ") + ex.what());
   }
@@ -518,6 +521,203 @@ static void emit_segment(const wdr_callbacks* cb, const Seg& s) {
   cb->new_segment(cb->user, &o);
 }
 
+// ------------------------------------------------------------------ multi-chain decoding
+// One segment's decode output (DTW resolved), and the prompt state of the reference's segment
+// loop (src/transcribe.rs:384-386, 502): the prompt entering segment i+1 is the text of segment
+// i's last result when that is non-empty, else the prompt segment i used.
+struct SegOut {
+  std::vector<ResultSeg> res;
+  int lang_id = 0;
+  bool sampled = false;            // a t > 0 decoder drew random numbers
+  std::string rng_after;           // decoder 0's RNG right after this segment (when sampled)
+};
+struct Prompt {
+  bool has = false;
+  std::string text;
+  bool operator==(const Prompt& o) const { return has == o.has && (!has || text == o.text); }
+  bool operator!=(const Prompt& o) const { return !(*this == o); }
+};
+static Prompt next_prompt(const Prompt& e, const std::vector<ResultSeg>& res) {
+  if (!res.empty()) {
+    const std::string t = trim_start(res.back().text);
+    if (!trim(t).empty()) return {true, t};
+  }
+  return e;
+}
+static FullParams with_prompt(const FullParams& base, const Prompt& e) {
+  FullParams p = base;
+  p.has_initial_prompt = e.has;
+  p.initial_prompt = e.has ? e.text : std::string();
+  return p;
+}
+static std::vector<float> seg_f32(const wdr_speech_segment& s) {
+  std::vector<float> x(s.n_samples);
+  for (size_t k = 0; k < s.n_samples; ++k) x[k] = (float)s.samples[k] / 32768.0f;
+  return x;
+}
+
+// Decode every speech segment with C chains.  Chain c decodes the contiguous block
+// [a_c, b_c) on its own State and host thread, speculatively from the pipeline's initial
+// prompt; its greedy steps are batched with the other chains' (StepBatcher).  Then, in chain
+// order, chain c's block is re-decoded segment by segment from the true incoming prompt
+// until the prompt entering the next segment equals the speculative run's; from there on
+// the speculative results ARE the sequential ones.  Random draws (t > 0 decoders) make a
+// result depend on every earlier draw (decoder 0's RNG lives in the state): from the first
+// segment that drew, the rest of the file is re-decoded sequentially from that segment's RNG
+// state.  The output equals the single-chain loop's exactly.
+static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_speech_segment>& segs,
+                                         const wdr_transcribe_options* o, const FullParams& params, int C,
+                                         const wdr_callbacks* cb) {
+  const size_t N = segs.size();
+  while ((int)c->chain_st.size() < C - 1)
+    c->chain_st.push_back(std::make_unique<State>(*c->ctx, (int)c->chain_st.size() + 1));
+  auto state = [&](int k) -> State& { return k == 0 ? *c->st : *c->chain_st[k - 1]; };
+  const bool auto_lang = !o || !o->lang || std::string(o->lang).empty() || std::string(o->lang) == "auto";
+  // contiguous blocks balanced by sample count (each chain at least one segment)
+  std::vector<size_t> cut(C + 1, 0);
+  {
+    std::vector<double> P(N + 1, 0.0);
+    for (size_t i = 0; i < N; ++i) P[i + 1] = P[i] + (double)segs[i].n_samples;
+    for (int k = 1; k < C; ++k) {
+      const double t = P[N] * k / C;
+      size_t x = std::lower_bound(P.begin(), P.end(), t) - P.begin();
+      if (x > 0 && t - P[x - 1] <= P[std::min(x, N)] - t) --x;
+      cut[k] = std::min(std::max(x, cut[k - 1] + 1), N - (size_t)(C - k));
+    }
+    cut[C] = N;
+  }
+  std::vector<SegOut> out(N);
+  // spec_out[i]: the prompt leaving segment i in its chain's speculative run (every block
+  // starts from the pipeline's initial prompt e0)
+  std::vector<Prompt> spec_out(N);
+  const Prompt e0{params.has_initial_prompt, params.initial_prompt};
+  std::atomic<bool> stop{false};
+  std::vector<std::exception_ptr> errs(C);
+  auto worker = [&](int k) {
+    State& st = state(k);
+    try {
+      const size_t a = cut[k], b = cut[k + 1];
+      st.times = StageTimes{};
+      st.reset_rng();
+      st.batched = C > 1;
+      std::vector<const int16_t*> pcm;
+      std::vector<int> ns;
+      for (size_t i = a; i < b; ++i) {
+        pcm.push_back(segs[i].samples);
+        ns.push_back((int)segs[i].n_samples);
+      }
+      st.plan(pcm.data(), ns.data(), (int)(b - a), auto_lang);
+      struct Guard {
+        State& st;
+        ~Guard() {
+          st.batched = false;
+          try {
+            st.unplan();
+          } catch (...) {
+          }
+        }
+      } guard{st};
+      Prompt e = e0;
+      std::vector<DtwTicket> prev_tk;
+      for (size_t i = a; i < b && !stop; ++i) {
+        if (st.full(with_prompt(params, e), nullptr, 0, (int)(i - a), true) != 0)
+          throw std::runtime_error("failed to transcribe");
+        out[i].res = st.result_all;
+        out[i].lang_id = st.lang_id;
+        out[i].sampled = st.sampled;
+        if (st.sampled) out[i].rng_after = st.rng_state();
+        std::vector<DtwTicket> tk = st.take_dtw_jobs();
+        if (i > a)
+          for (auto& t : prev_tk) st.resolve_dtw(t, out[i - 1].res);
+        prev_tk = std::move(tk);
+        e = next_prompt(e, out[i].res);
+        spec_out[i] = e;
+      }
+      for (auto& t : prev_tk) st.resolve_dtw(t, out[b - 1].res);
+    } catch (...) {
+      errs[k] = std::current_exception();
+      stop = true;
+    }
+  };
+  {
+    std::atomic<int> live{C};
+    std::vector<std::thread> th;
+    for (int k = 0; k < C; ++k)
+      th.emplace_back([&, k] {
+        worker(k);
+        live--;
+      });
+    // cancellation is polled here: callbacks fire on the calling thread only
+    while (live > 0) {
+      if (!stop && cb && cb->is_cancelled && cb->is_cancelled(cb->user)) stop = true;
+      std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    }
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+      if (e) std::rethrow_exception(e);
+    if (stop) throw std::runtime_error("failed to transcribe");
+  }
+  // fix-ups in chain order (unplanned single-segment decodes, decoder 0's RNG fresh: no
+  // segment before a fixed-up one drew, or the sampled tail below redoes it anyway)
+  Prompt e_true = spec_out[cut[1] - 1];
+  for (int k = 1; k < C; ++k) {
+    const size_t a = cut[k], b = cut[k + 1];
+    if (e_true != e0) {
+      State& st = state(k);
+      Prompt e = e_true;
+      size_t j = a;
+      for (; j < b; ++j) {
+        if (cb && cb->is_cancelled && cb->is_cancelled(cb->user)) throw std::runtime_error("failed to transcribe");
+        const std::vector<float> x = seg_f32(segs[j]);
+        st.reset_rng();
+        if (st.full(with_prompt(params, e), x.data(), (int)x.size(), -1, false) != 0)
+          throw std::runtime_error("failed to transcribe");
+        out[j].res = st.result_all;
+        out[j].lang_id = st.lang_id;
+        out[j].sampled = st.sampled;
+        out[j].rng_after = st.sampled ? st.rng_state() : std::string();
+        e = next_prompt(e, out[j].res);
+        if (e == spec_out[j]) break;
+      }
+      e_true = j < b ? spec_out[b - 1] : e;
+    } else {
+      e_true = spec_out[b - 1];
+    }
+  }
+  // random draws: the first segment (file order) that drew is exact; every later one is
+  // re-decoded in order from its RNG state
+  size_t f = N;
+  for (size_t i = 0; i < N; ++i)
+    if (out[i].sampled) {
+      f = i;
+      break;
+    }
+  if (f + 1 < N) {
+    State& st = *c->st;
+    Prompt e = e0;
+    for (size_t i = 0; i <= f; ++i) e = next_prompt(e, out[i].res);
+    st.set_rng_state(out[f].rng_after);
+    for (size_t i = f + 1; i < N; ++i) {
+      if (cb && cb->is_cancelled && cb->is_cancelled(cb->user)) throw std::runtime_error("failed to transcribe");
+      const std::vector<float> x = seg_f32(segs[i]);
+      if (st.full(with_prompt(params, e), x.data(), (int)x.size(), -1, false) != 0)
+        throw std::runtime_error("failed to transcribe");
+      out[i].res = st.result_all;
+      out[i].lang_id = st.lang_id;
+      e = next_prompt(e, out[i].res);
+    }
+  }
+  // stage accounting: chains' times summed into the context's state
+  for (int k = 1; k < C; ++k) {
+    const StageTimes& t = state(k).times;
+    StageTimes& m = c->st->times;
+    m.mel += t.mel; m.encode += t.encode; m.decode += t.decode; m.dtw += t.dtw;
+    m.windows += t.windows; m.decode_steps += t.decode_steps; m.prefills += t.prefills;
+    m.lang += t.lang; m.prompt_gpu += t.prompt_gpu;
+  }
+  return out;
+}
+
 // src/transcribe.rs:323-535
 // raw: per-segment results only (no overlap clip against the next segment, no speakers): the
 // multi-GPU path (wdr/distributed.py) merges several GPUs' raw blocks and applies both in order.
@@ -544,9 +744,14 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
     *has_lang = true;
   }
   const bool translated = o && o->whisper_to_english == 1;
+  // decode chains: greedy decoding only (its steps batch across chains; beam search and
+  // t > 0 decoders keep one chain)
+  const int C = (params.greedy && params.temperature <= 0.f)
+                    ? std::max(1, std::min({c->chains, c->ctx->max_chains, (int)segs.size()}))
+                    : 1;
   // every segment's PCM goes to the encode-ahead ring up front (int16 -> f32 on the GPU,
-  // the same x / 32768 as src/transcribe.rs's conversion)
-  {
+  // the same x / 32768 as src/transcribe.rs's conversion); multi-chain: per chain block
+  if (C == 1) {
     std::vector<const int16_t*> pcm(segs.size());
     std::vector<int> ns(segs.size());
     for (size_t i = 0; i < segs.size(); ++i) {
@@ -591,6 +796,7 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
   } drain{c, pend};
   auto finalize = [&](Pending& P) {
     for (auto& t : P.tk) c->st->resolve_dtw(t, P.res);
+    P.tk.clear();
     const size_t i = P.i;
     const wdr_speech_segment& ss = segs[i];
     const double base_offset = ss.start + user_offset;
@@ -644,6 +850,22 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
       out.push_back(std::move(s));
     }
   };
+  if (C > 1) {
+    // multi-chain: C States decode C contiguous blocks concurrently (batched greedy steps),
+    // then the exact prompt fix-up; results come back DTW-resolved, finished here in order
+    std::vector<SegOut> res = decode_chains(c, segs, o, params, C, cb);
+    for (size_t i = 0; i < segs.size(); ++i) {
+      if (i == 0 && !*has_lang) {
+        *detected_lang = kLangs[std::max(0, std::min(99, res[0].lang_id))];
+        *has_lang = true;
+      }
+      Pending P;
+      P.i = i;
+      P.res = std::move(res[i].res);
+      finalize(P);
+    }
+    return out;
+  }
   for (size_t i = 0; i < segs.size(); ++i) {
     if (have_prev) {
       params.initial_prompt = previous_text;
@@ -1128,6 +1350,14 @@ void wdr_segment_list_free(wdr_segment_list* l) {
   free((void*)l->detected_lang);
   free((void*)l->speech_index);
   free(l);
+}
+
+int wdr_context_set_chains(wdr_context* c, int32_t n) {
+  WDR_GUARD({
+    if (n < 1) return fail("decode chains: need >= 1");
+    c->chains = std::min<int>(n, c->ctx->max_chains);
+    return 0;
+  })
 }
 
 int wdr_context_stage_times(wdr_context* c, wdr_stage_times* o) {

@@ -335,20 +335,27 @@ __global__ __launch_bounds__(256) void k_xattn_partial(XAttnArgs a) {
 // One decoder row (greedy steps): thread t takes key t/4 of the chunk and dims 16*(t%4)..+16
 // for q.k with K read straight from HBM (no LDS staging), V goes through LDS with 16-B loads,
 // and all four waves share the P.V (16 keys each) instead of one wave doing all 64.
+// ROWS: blockIdx.z = decoder row, each row with its OWN cross K/V (rows of different speech
+// segments batched into one step by the multi-chain decoder, whisper_ctx.cpp StepBatcher)
+template <bool ROWS>
 __global__ __launch_bounds__(256) void k_xattn_partial1(XAttnArgs a) {
   __shared__ __attribute__((aligned(16))) f16 Vs[XA_KC * 64];
   __shared__ float red[2][4];
   __shared__ float ps[XA_KC];
   __shared__ float pv[4][64];
   const int c = blockIdx.x, h = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r = ROWS ? blockIdx.z : 0;
+  const f16* kb = ROWS ? a.row_k[r] + a.layer_off : a.k;
+  const f16* vb = ROWS ? kb + a.n_head * 64 : a.v;
   const int key0 = c * XA_KC;
   const int kk = tid >> 2, qd = tid & 3;
   const int key = key0 + kk;
   const bool kok = key < a.Tk;
   const long long row = (long long)(kok ? key : a.Tk - 1) * a.ldkv + h * 64 + qd * 16;
-  const f16x8 k0 = *(const f16x8*)(a.k + row), k1 = *(const f16x8*)(a.k + row + 8);
-  const f16x8 v0 = *(const f16x8*)(a.v + row), v1 = *(const f16x8*)(a.v + row + 8);
-  const f16x8 q0 = *(const f16x8*)(a.q + h * 64 + qd * 16), q1 = *(const f16x8*)(a.q + h * 64 + qd * 16 + 8);
+  const f16x8 k0 = *(const f16x8*)(kb + row), k1 = *(const f16x8*)(kb + row + 8);
+  const f16x8 v0 = *(const f16x8*)(vb + row), v1 = *(const f16x8*)(vb + row + 8);
+  const f16* qr = a.q + (long long)r * a.ldq + h * 64 + qd * 16;
+  const f16x8 q0 = *(const f16x8*)qr, q1 = *(const f16x8*)(qr + 8);
   *(f16x8*)(Vs + kk * 64 + qd * 16) = v0;
   *(f16x8*)(Vs + kk * 64 + qd * 16 + 8) = v1;
   float sc = 0.f;
@@ -372,8 +379,9 @@ __global__ __launch_bounds__(256) void k_xattn_partial1(XAttnArgs a) {
   pv[wid][lane] = acc;
   __syncthreads();
   if (tid < 64) {
-    a.part_o[((long long)c * a.n_head + h) * 64 + tid] = pv[0][tid] + pv[1][tid] + pv[2][tid] + pv[3][tid];
-    if (tid == 0) a.part_ml[(long long)c * a.n_head + h] = make_float2(mx, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+    const long long cr = (long long)c * (ROWS ? a.R : 1) + r;
+    a.part_o[(cr * a.n_head + h) * 64 + tid] = pv[0][tid] + pv[1][tid] + pv[2][tid] + pv[3][tid];
+    if (tid == 0) a.part_ml[cr * a.n_head + h] = make_float2(mx, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
   }
 }
 
@@ -398,9 +406,12 @@ void launch_xattn(const XAttnArgs& a, hipStream_t s) {
   WDR_CHECK(a.R >= 1 && a.R <= XA_RMAX, "cross-attention decode: R out of range");
   const int nsplit = cdiv(a.Tk, XA_KC);
   WDR_CHECK(nsplit == 24, "cross-attention decode expects 1500 keys");
-  if (a.R == 1) {
-    wdr_launch(PROF_XATTN, (double)a.Tk * a.n_head * 64 * 2 * 2, (double)a.Tk * a.n_head * 64 * 4, k_xattn_partial1,
-               dim3(nsplit, a.n_head), dim3(256), 0, s, a);
+  if (a.row_k) {
+    wdr_launch(PROF_XATTN, (double)a.R * a.Tk * a.n_head * 64 * 2 * 2, (double)a.R * a.Tk * a.n_head * 64 * 4,
+               k_xattn_partial1<true>, dim3(nsplit, a.n_head, a.R), dim3(256), 0, s, a);
+  } else if (a.R == 1) {
+    wdr_launch(PROF_XATTN, (double)a.Tk * a.n_head * 64 * 2 * 2, (double)a.Tk * a.n_head * 64 * 4,
+               k_xattn_partial1<false>, dim3(nsplit, a.n_head), dim3(256), 0, s, a);
   } else {
     wdr_launch(PROF_XATTN, (double)a.Tk * a.n_head * 64 * 2 * 2, (double)a.R * a.Tk * a.n_head * 64 * 4,
                k_xattn_partial, dim3(nsplit, a.n_head), dim3(256), 0, s, a);

@@ -110,6 +110,10 @@ struct XAttnArgs {
   float* part_o;
   float2* part_ml;
   f16* o; int ldo;
+  // per-row cross K/V (rows from different speech segments): row r's K at row_k[r] + layer_off
+  // (device array of slot bases), its V d columns further; k / v unused then
+  const f16* const* row_k = nullptr;
+  long long layer_off = 0;
 };
 void launch_xattn(const XAttnArgs& a, hipStream_t s);
 struct CaptureArgs {

@@ -89,6 +89,12 @@ class Context {
   DevMem aheads_dev;                              // per-layer head lists (device)
   std::vector<int> aheads_dev_off;
   hipStream_t stream = nullptr;
+  // self-attention KV caches of every decode chain (State), one pool so that the step
+  // batcher can address rows of several chains: [L][max_chains * NSLOT][n_text_ctx][d] f16
+  int max_chains = 1;
+  DevMem kv_k, kv_v;
+  std::unique_ptr<class StepBatcher> batcher;     // multi-chain greedy steps (created on demand)
+  StepBatcher& step_batcher();
 };
 
 struct FullParams {
@@ -126,6 +132,46 @@ struct StageTimes {   // host wall-clock per phase (seconds), accumulated
   double lang = 0, prompt_gpu = 0;   // language-detect wall time; GPU time of the prompt prefills
 };
 
+// one decode step's working set (rows of one speech segment, or of several: row_xkv)
+struct StepIO {
+  float* xd; f16* qkvd; f16* attd; f16* qx; f16* mlpd;
+  float* logits; int ldlogits;
+  float* part_o; float2* part_ml;
+  const int* rows_tok; const int* rows_pos; const int* rows_seq;
+  f16* kc; f16* vc; long long layer_stride, seq_stride;   // KV pool (layer 0) and its strides
+  const f16* xkv;                  // one cross-K/V slot for every row, or
+  const f16* const* row_xkv;       // per-row slot bases (device array)
+};
+void decode_step_layers(const Context& ctx, const StepIO& io, int R, hipStream_t s);
+
+// Multi-chain greedy decoding: several States ("chains", each decoding its own contiguous
+// block of speech segments on its own host thread) hand their single-row greedy steps to
+// this batcher, which runs them as ONE R-row step (weights streamed once for all rows; each
+// row with its own KV-pool sequence and cross-K/V slot) on its own stream.  Lockstep: a
+// batch launches once every chain inside a greedy decode loop has submitted its row.
+class StepBatcher {
+ public:
+  explicit StepBatcher(Context& ctx);
+  ~StepBatcher();
+  struct Req {
+    int tok, seq, pos;         // seq: absolute KV-pool sequence
+    const f16* xkv;            // the row's cross-K/V slot
+    LogitsCtl ctl;
+    VocabIds vids;
+    TokenData out;
+  };
+  void enter();
+  void leave();
+  void step(Req& r);           // blocks until the batch holding r has run
+  long long launches = 0, rows = 0;
+  struct Impl;
+
+ private:
+  Context& ctx_;
+  std::unique_ptr<Impl> m_;
+  void launch(std::vector<Req*>& batch);
+};
+
 struct Seq;           // one decoder's sequence (whisper_ctx.cpp)
 struct PrefillBufs;   // a prefill's working set (whisper_ctx.cpp)
 
@@ -138,7 +184,7 @@ struct DtwTicket {
 
 class State {
  public:
-  explicit State(Context& ctx);
+  explicit State(Context& ctx, int chain = 0);
   ~State();
   // whisper_full_with_state on host f32 samples. Returns 0 on success.
   // job >= 0: segment `job` of the current plan (samples / n come from the plan).
@@ -155,6 +201,12 @@ class State {
   StageTimes times;
   long long t_beg = 0, t_last = 0, tid_last = 0;
   std::vector<float> energy;
+  int chain = 0;                // decode chain (KV pool sequences chain*NSLOT ..)
+  bool batched = false;         // greedy steps go through ctx.step_batcher() (multi-chain run)
+  bool sampled = false;         // the last full() drew random numbers (t > 0 decoders)
+  void reset_rng();             // decoder 0's std::mt19937 back to its per-state seed
+  std::string rng_state() const;
+  void set_rng_state(const std::string& s);
 
   // test seams
   void compute_mel(const float* x_host, int n);

@@ -11,6 +11,10 @@
 #include <cstdlib>
 #include <map>
 #include <random>
+#include <exception>
+#include <condition_variable>
+#include <mutex>
+#include <sstream>
 
 namespace wdr {
 
@@ -302,9 +306,18 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
     if (!flat.empty()) WDR_HIP(hipMemcpyAsync(aheads_dev.p, flat.data(), flat.size() * 4, hipMemcpyHostToDevice, s));
   }
   WDR_HIP(hipStreamSynchronize(s));
+  {
+    // KV pool for the decode chains of every State of this context (multi-chain pipeline)
+    const char* e = getenv("WDR_DECODE_CHAINS");
+    max_chains = std::max(1, std::min(8, e ? atoi(e) : 4));
+    const size_t per = (size_t)hp.n_text_layer * 18 * hp.n_text_ctx * hp.n_text_state;   // NSLOT = 18
+    kv_k = DevMem(per * max_chains * 2);
+    kv_v = DevMem(per * max_chains * 2);
+  }
 }
 
 Context::~Context() {
+  batcher.reset();
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -374,8 +387,11 @@ struct State::Impl {
   std::mt19937 rng[NSEQ];      // whisper_decoder::rng
   int* h_pairs = nullptr;
   DevMem fpart_o, fpart_ml;   // split flash-attention partials (prefill cross-attention)
-  DevMem kc, vc;
+  f16* kc = nullptr;          // this chain's sequences in the context's KV pool (layer 0)
+  f16* vc = nullptr;
+  int nslot_tot = 0;          // sequences per layer in the pool (layer stride / seq_stride)
   long long seq_stride = 0;   // elements per (layer, seq)
+  hipStream_t own = nullptr;  // this state's decode stream
   // dtw
   DevMem nrm, xdtw, times;
   PrefillBufs pb_main{}, pb_dtw{}, pb_lang{};
@@ -430,10 +446,19 @@ static void alloc_enc(State::Impl::EncBufs& e, int nb, int d, int kp1) {
   e.emlp = DevMem((size_t)nb * 1500 * 4 * d * 2);
 }
 
-State::State(Context& ctx) : ctx_(ctx), s_(ctx.stream), m_(new Impl) {
+State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
   WDR_HIP(hipSetDevice(ctx.cp.gpu_device));
   const HParams& hp = ctx.model.hp;
   Impl& m = *m_;
+  chain = chain_;
+  WDR_CHECK(chain >= 0 && chain < ctx.max_chains, "decode chain index out of range");
+  {
+    // every state has its own highest-priority decode stream (chains run concurrently)
+    int lo = 0, hi = 0;
+    WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    WDR_HIP(hipStreamCreateWithPriority(&m.own, hipStreamNonBlocking, hi));
+    s_ = m.own;
+  }
   m.d = hp.n_text_state;
   m.L = hp.n_text_layer;
   m.H = hp.n_text_head;
@@ -486,8 +511,9 @@ State::State(Context& ctx) : ctx_(ctx), s_(ctx.stream), m_(new Impl) {
   m.rows_pos = DevMem(RMAX * 4);
   m.rows_seq = DevMem(RMAX * 4);
   m.seq_stride = (long long)hp.n_text_ctx * d;
-  m.kc = DevMem((size_t)m.L * NSLOT * m.seq_stride * 2);
-  m.vc = DevMem((size_t)m.L * NSLOT * m.seq_stride * 2);
+  m.nslot_tot = ctx.max_chains * NSLOT;
+  m.kc = ctx.kv_k.as<f16>() + (size_t)chain * NSLOT * m.seq_stride;
+  m.vc = ctx.kv_v.as<f16>() + (size_t)chain * NSLOT * m.seq_stride;
   m.nrm = DevMem((size_t)A * RMAX * 1500 * 4);
   m.xdtw = DevMem((size_t)RMAX * 1500 * 4);
   m.times = DevMem((RMAX + 8) * 4);
@@ -607,6 +633,10 @@ State::~State() {
     if (m_->sd) {
       (void)hipStreamSynchronize(m_->sd);
       (void)hipStreamDestroy(m_->sd);
+    }
+    if (m_->own) {
+      (void)hipStreamSynchronize(m_->own);
+      (void)hipStreamDestroy(m_->own);
     }
     for (auto& j : m_->jobs) {
       if (j.blk) m_->blk_pool.push_back(j.blk);
@@ -845,8 +875,8 @@ void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool c
   const int ldxkv = L * 2 * d;
   for (int l = 0; l < L; ++l) {
     const DecLayer& e = md.dec[l];
-    f16* kc = m.kc.as<f16>() + (size_t)l * NSLOT * m.seq_stride;
-    f16* vc = m.vc.as<f16>() + (size_t)l * NSLOT * m.seq_stride;
+    f16* kc = m.kc + (size_t)l * m.nslot_tot * m.seq_stride;
+    f16* vc = m.vc + (size_t)l * m.nslot_tot * m.seq_stride;
     launch_layernorm(b.xd, d, e.ln1_g, e.ln1_b, b.hd, d, n, d, st);
     // Q to qkvd, K / V straight into this sequence's cache rows 0..n-1 (the epilogue scatter)
     ProjArgs qa{b.hd, d, e.w_qkv, d, e.b_qkv, b.qkvd, 3 * d, nullptr, 0, n, 3 * d, d, EPI_QKV_CACHE};
@@ -907,13 +937,12 @@ void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool c
 void State::decoder_step_body(int R) {
   Impl& m = *m_;
   const Model& md = ctx_.model;
-  const HParams& hp = md.hp;
   const int d = m.d, L = m.L;
   launch_embed(md.tok_emb, md.dec_pos, m.rows_tok.as<int>(), m.rows_pos.as<int>(), R, d, m.xd.as<float>(), s_);
   const float scale = 1.0f / 8.0f;
   if (R == 1 && m.st_on) {
     StepArgs a{m.st_layers.as<StepLayer>(), L, d, m.H, m.V, md.tok_emb, md.ln_g, md.ln_b, m.rows_seq.as<int>(),
-               m.rows_pos.as<int>(), m.kc.as<f16>(), m.vc.as<f16>(), (long long)NSLOT * m.seq_stride, m.seq_stride,
+               m.rows_pos.as<int>(), m.kc, m.vc, (long long)m.nslot_tot * m.seq_stride, m.seq_stride,
                m.xkv(), L * 2 * d, m.xd.as<float>(), m.st_q.as<f16>(), m.st_att.as<f16>(), m.st_qx.as<f16>(),
                m.st_xatt.as<f16>(), m.st_mlp.as<f16>(), m.part_o.as<float>(), m.part_ml.as<float2>(),
                m.logits.as<float>(), m.st_ctr.as<unsigned>(), m.d_err, scale};
@@ -921,12 +950,28 @@ void State::decoder_step_body(int R) {
     launch_step(a, m.st_wg, s_);
     return;
   }
+  StepIO io{m.xd.as<float>(), m.qkvd.as<f16>(), m.attd.as<f16>(), m.qx.as<f16>(), m.mlpd.as<f16>(),
+            m.logits.as<float>(), m.V, m.part_o.as<float>(), m.part_ml.as<float2>(), m.rows_tok.as<int>(),
+            m.rows_pos.as<int>(), m.rows_seq.as<int>(), m.kc, m.vc, (long long)m.nslot_tot * m.seq_stride,
+            m.seq_stride, m.xkv(), nullptr};
+  decode_step_layers(ctx_, io, R, s_);
+}
+
+// The per-kernel decode step after the embedding: for every layer QKV (LN fused, K/V into the
+// cache), self-attention, O, cross-Q (LN fused), cross-attention (2), cross-O, FC1 (LN fused),
+// FC2; then the final LN + logits.  Rows may come from different speech segments (per-row
+// cross-K/V slots, StepBatcher) or from one (beams / best_of decoders, State).
+void decode_step_layers(const Context& ctx, const StepIO& io, int R, hipStream_t s) {
+  const Model& md = ctx.model;
+  const HParams& hp = md.hp;
+  const int d = hp.n_text_state, L = hp.n_text_layer;
+  const float scale = 1.0f / 8.0f;
   const int ldxkv = L * 2 * d;
   auto P = [&](const f16* A, int lda, const f16* W, const float* b, void* out, int ldo, int N, int K, int epi,
                const float* lng = nullptr, const float* lnb = nullptr) {
     ProjArgs a{A, lda, W, K, b, out, ldo, nullptr, 0, R, N, K, epi};
     if (lng) {
-      a.ln_x = m.xd.as<float>();
+      a.ln_x = io.xd;
       a.ldln = d;
       a.ln_g = lng;
       a.ln_b = lnb;
@@ -935,30 +980,34 @@ void State::decoder_step_body(int R) {
   };
   for (int l = 0; l < L; ++l) {
     const DecLayer& e = md.dec[l];
-    f16* kc = m.kc.as<f16>() + (size_t)l * NSLOT * m.seq_stride;
-    f16* vc = m.vc.as<f16>() + (size_t)l * NSLOT * m.seq_stride;
-    ProjArgs q = P(nullptr, d, e.w_qkv, e.b_qkv, m.qkvd.p, 3 * d, 3 * d, d, EPI_QKV_CACHE, e.ln1_g, e.ln1_b);
+    f16* kc = io.kc + (size_t)l * io.layer_stride;
+    f16* vc = io.vc + (size_t)l * io.layer_stride;
+    ProjArgs q = P(nullptr, d, e.w_qkv, e.b_qkv, io.qkvd, 3 * d, 3 * d, d, EPI_QKV_CACHE, e.ln1_g, e.ln1_b);
     q.kc = kc;
     q.vc = vc;
-    q.seq_stride = m.seq_stride;
-    q.row_seq = m.rows_seq.as<int>();
-    q.row_pos = m.rows_pos.as<int>();
+    q.seq_stride = io.seq_stride;
+    q.row_seq = io.rows_seq;
+    q.row_pos = io.rows_pos;
     q.d = d;
-    launch_proj(q, s_);
-    DecSelfArgs sa{m.qkvd.as<f16>(), 3 * d, kc, vc, m.seq_stride, d, m.rows_seq.as<int>(), m.rows_pos.as<int>(),
-                   m.attd.as<f16>(), d, scale};
-    launch_dec_self_attn(sa, R, hp.n_text_head, s_);
-    launch_proj(P(m.attd.as<f16>(), d, e.w_o, e.b_o, m.xd.p, d, d, d, EPI_F32_RESID), s_);
-    launch_proj(P(nullptr, d, e.w_xq, e.b_xq, m.qx.p, d, d, d, EPI_F16, e.ln2_g, e.ln2_b), s_);
-    const f16* xk = m.xkv() + (size_t)l * 2 * d;
-    XAttnArgs xa{m.qx.as<f16>(), d, xk, xk + d, ldxkv, 1500, R, hp.n_text_head, scale, m.part_o.as<float>(),
-                 m.part_ml.as<float2>(), m.attd.as<f16>(), d};
-    launch_xattn(xa, s_);
-    launch_proj(P(m.attd.as<f16>(), d, e.w_xo, e.b_xo, m.xd.p, d, d, d, EPI_F32_RESID), s_);
-    launch_proj(P(nullptr, d, e.w_fc1, e.b_fc1, m.mlpd.p, 4 * d, 4 * d, d, EPI_F16_GELU, e.ln3_g, e.ln3_b), s_);
-    launch_proj(P(m.mlpd.as<f16>(), 4 * d, e.w_fc2, e.b_fc2, m.xd.p, d, d, 4 * d, EPI_F32_RESID), s_);
+    launch_proj(q, s);
+    DecSelfArgs sa{io.qkvd, 3 * d, kc, vc, io.seq_stride, d, io.rows_seq, io.rows_pos, io.attd, d, scale};
+    launch_dec_self_attn(sa, R, hp.n_text_head, s);
+    launch_proj(P(io.attd, d, e.w_o, e.b_o, io.xd, d, d, d, EPI_F32_RESID), s);
+    launch_proj(P(nullptr, d, e.w_xq, e.b_xq, io.qx, d, d, d, EPI_F16, e.ln2_g, e.ln2_b), s);
+    XAttnArgs xa{io.qx, d, nullptr, nullptr, ldxkv, 1500, R, hp.n_text_head, scale, io.part_o, io.part_ml, io.attd, d};
+    if (io.row_xkv) {
+      xa.row_k = io.row_xkv;
+      xa.layer_off = (long long)l * 2 * d;
+    } else {
+      xa.k = io.xkv + (size_t)l * 2 * d;
+      xa.v = xa.k + d;
+    }
+    launch_xattn(xa, s);
+    launch_proj(P(io.attd, d, e.w_xo, e.b_xo, io.xd, d, d, d, EPI_F32_RESID), s);
+    launch_proj(P(nullptr, d, e.w_fc1, e.b_fc1, io.mlpd, 4 * d, 4 * d, d, EPI_F16_GELU, e.ln3_g, e.ln3_b), s);
+    launch_proj(P(io.mlpd, 4 * d, e.w_fc2, e.b_fc2, io.xd, d, d, 4 * d, EPI_F32_RESID), s);
   }
-  launch_proj(P(nullptr, d, md.tok_emb, nullptr, m.logits.p, m.V, m.V, d, EPI_F32, md.ln_g, md.ln_b), s_);
+  launch_proj(P(nullptr, d, md.tok_emb, nullptr, io.logits, io.ldlogits, hp.n_vocab, d, EPI_F32, md.ln_g, md.ln_b), s);
 }
 
 // after a synchronised step: a persistent-step wait that gave up leaves counters behind
@@ -1105,8 +1154,8 @@ void State::kv_reorder(const std::vector<std::pair<int, int>>& moves, int n_rows
     m.h_pairs[2 * NSEQ + 2 * i + 1] = moves[i].second;
   }
   WDR_HIP(hipMemcpyAsync(m.kvpairs.p, m.h_pairs, 4 * NSEQ * 4, hipMemcpyHostToDevice, s_));
-  launch_kv_copy(m.kc.as<f16>(), m.vc.as<f16>(), m.seq_stride, NSLOT, m.L, m.kvpairs.as<int>(), n, n_rows, m.d, s_);
-  launch_kv_copy(m.kc.as<f16>(), m.vc.as<f16>(), m.seq_stride, NSLOT, m.L, m.kvpairs.as<int>() + 2 * NSEQ, n, n_rows,
+  launch_kv_copy(m.kc, m.vc, m.seq_stride, m.nslot_tot, m.L, m.kvpairs.as<int>(), n, n_rows, m.d, s_);
+  launch_kv_copy(m.kc, m.vc, m.seq_stride, m.nslot_tot, m.L, m.kvpairs.as<int>() + 2 * NSEQ, n, n_rows,
                  m.d, s_);
   WDR_HIP(hipStreamSynchronize(s_));   // the pinned pair table is rewritten by the next reorder
 }
@@ -1133,6 +1182,17 @@ void State::dbg_step(const int* toks, int n, bool classic, float* logits_out) {
 }
 
 bool State::persistent_step() const { return m_->st_on; }
+
+void State::reset_rng() { m_->rng[0] = std::mt19937(0); }
+std::string State::rng_state() const {
+  std::ostringstream o;
+  o << m_->rng[0];
+  return o.str();
+}
+void State::set_rng_state(const std::string& st) {
+  std::istringstream i(st);
+  i >> m_->rng[0];
+}
 
 int State::step_trace(uint64_t* out, int cap) {
   Impl& m = *m_;
@@ -1563,6 +1623,7 @@ Seq State::decode_beam(const std::vector<int>& prompt, const FullParams& params,
 Seq State::decode_sample(const std::vector<int>& prompt, const FullParams& params, float t_cur, int seek, int seek_end,
                          int Lf, int window, float* nosp) {
   Impl& m = *m_;
+  sampled = true;
   const Vocab& v = ctx_.vocab;
   const int K = std::max(1, std::min(params.best_of, NSEQ));
   const int n_max = ctx_.model.hp.n_text_ctx / 2 - 4;
@@ -1717,6 +1778,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
     for (auto& t : stale) resolve_dtw(t, none);
   }
   for (int j = 1; j < NSEQ; ++j) m.rng[j] = std::mt19937(0);   // WHISPER_DECODER_INIT, every call
+  sampled = false;
   double t_start = now_s();
   const bool planned = job >= 0 && job < (int)m.plan.pcm.size();
   // the slot goes back to the encode-ahead ring once this segment's last kernel has run
@@ -1854,6 +1916,13 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
       } else if (!params.greedy) {
         sq = decode_beam(prompt, params, t_cur, seek, seek_end, Lf, window, &nosp);
       }
+      // multi-chain run: from the second token on, this chain's row joins the batched step
+      struct Lockstep {
+        StepBatcher* b = nullptr;
+        ~Lockstep() {
+          if (b) b->leave();
+        }
+      } lockstep;
       for (int i = 0; i < n_max && single; ++i) {
         LogitsCtl c{};
         c.n_tokens = (int)sq.tokens.size();
@@ -1877,7 +1946,18 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
           const int pos = (int)prompt.size() + i - 1;
           const int seq0 = 0;
           const int prev_id = sq.tokens.back().id;
-          step_and_sample(&prev_id, &seq0, &pos, &c, 1, &tok);
+          if (batched) {
+            if (!lockstep.b) {
+              lockstep.b = &ctx_.step_batcher();
+              lockstep.b->enter();
+            }
+            StepBatcher::Req rq{prev_id, chain * NSLOT + seq0, pos, m.xkv(), c, m.vids, {}};
+            lockstep.b->step(rq);
+            tok = rq.out;
+            times.decode_steps++;
+          } else {
+            step_and_sample(&prev_id, &seq0, &pos, &c, 1, &tok);
+          }
         }
         sq.tokens.push_back(tok);
         if (tok.id > v.beg) {
@@ -1968,6 +2048,213 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
     for (auto& t : tk) resolve_dtw(t, result_all);
   }
   return 0;
+}
+
+}  // namespace wdr
+
+// ------------------------------------------------------------------ multi-chain step batcher
+namespace wdr {
+
+static constexpr int RB = NSEQ;   // rows per batched step (chains)
+
+struct StepBatcher::Impl {
+  std::mutex mu;
+  std::condition_variable cv;
+  int active = 0;                 // chains inside a greedy decode loop
+  std::vector<Req*> pend;         // requests of the batch being collected
+  long long round = 0;            // completed launches
+  bool running = false;           // a batch is on the GPU (new requests wait for the next)
+  std::exception_ptr err;         // failure of the last launch (rethrown to its requesters)
+  hipStream_t s = nullptr;
+  int d = 0, V = 0, H = 0;
+  DevMem xd, qkvd, attd, qx, mlpd, logits, work, tokout, ctl, rows_tok, rows_pos, rows_seq, row_xkv, part_o, part_ml;
+  int* h_rows = nullptr;          // [3][RB]
+  LogitsCtl* h_ctl = nullptr;
+  const f16** h_xkv = nullptr;
+  TokOut* h_tok = nullptr;
+  struct G {
+    hipGraphExec_t exec = nullptr;
+    VocabIds vids{};
+  };
+  std::map<int, G> graphs;        // by row count
+};
+
+StepBatcher::StepBatcher(Context& ctx) : ctx_(ctx), m_(new Impl) {
+  WDR_HIP(hipSetDevice(ctx.cp.gpu_device));
+  Impl& m = *m_;
+  const HParams& hp = ctx.model.hp;
+  m.d = hp.n_text_state;
+  m.V = hp.n_vocab;
+  m.H = hp.n_text_head;
+  int lo = 0, hi = 0;
+  WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  WDR_HIP(hipStreamCreateWithPriority(&m.s, hipStreamNonBlocking, hi));
+  const int d = m.d;
+  m.xd = DevMem((size_t)RB * d * 4);
+  m.qkvd = DevMem((size_t)RB * 3 * d * 2);
+  m.attd = DevMem((size_t)RB * d * 2);
+  m.qx = DevMem((size_t)RB * d * 2);
+  m.mlpd = DevMem((size_t)RB * 4 * d * 2);
+  m.logits = DevMem((size_t)RB * m.V * 4);
+  m.work = DevMem((size_t)RB * m.V * 4);
+  m.tokout = DevMem(RB * sizeof(TokOut));
+  m.ctl = DevMem(RB * sizeof(LogitsCtl));
+  m.rows_tok = DevMem(RB * 4);
+  m.rows_pos = DevMem(RB * 4);
+  m.rows_seq = DevMem(RB * 4);
+  m.row_xkv = DevMem(RB * sizeof(void*));
+  m.part_o = DevMem((size_t)NSPLIT * RB * m.H * 64 * 4);
+  m.part_ml = DevMem((size_t)NSPLIT * RB * m.H * sizeof(float2));
+  WDR_HIP(hipHostMalloc((void**)&m.h_rows, 3 * RB * 4, hipHostMallocDefault));
+  WDR_HIP(hipHostMalloc((void**)&m.h_ctl, RB * sizeof(LogitsCtl), hipHostMallocDefault));
+  WDR_HIP(hipHostMalloc((void**)&m.h_xkv, RB * sizeof(void*), hipHostMallocDefault));
+  WDR_HIP(hipHostMalloc((void**)&m.h_tok, RB * sizeof(TokOut), hipHostMallocDefault));
+}
+
+StepBatcher::~StepBatcher() {
+  if (!m_) return;
+  for (auto& g : m_->graphs)
+    if (g.second.exec) (void)hipGraphExecDestroy(g.second.exec);
+  if (m_->s) {
+    (void)hipStreamSynchronize(m_->s);
+    (void)hipStreamDestroy(m_->s);
+  }
+  (void)hipHostFree(m_->h_rows);
+  (void)hipHostFree(m_->h_ctl);
+  (void)hipHostFree(m_->h_xkv);
+  (void)hipHostFree(m_->h_tok);
+}
+
+StepBatcher& Context::step_batcher() {
+  static std::mutex mu;
+  std::lock_guard<std::mutex> g(mu);
+  if (!batcher) batcher = std::make_unique<StepBatcher>(*this);
+  return *batcher;
+}
+
+void StepBatcher::enter() {
+  std::lock_guard<std::mutex> g(m_->mu);
+  m_->active++;
+}
+
+void StepBatcher::leave() {
+  Impl& m = *m_;
+  std::unique_lock<std::mutex> lk(m.mu);
+  m.active--;
+  if (!m.running && !m.pend.empty() && (int)m.pend.size() >= m.active) {
+    std::vector<Req*> batch;
+    batch.swap(m.pend);
+    m.running = true;
+    lk.unlock();
+    std::exception_ptr e;
+    try {
+      launch(batch);
+    } catch (...) {
+      e = std::current_exception();
+    }
+    lk.lock();
+    m.err = e;
+    m.running = false;
+    m.round++;
+    m.cv.notify_all();
+  }
+}
+
+void StepBatcher::step(Req& r) {
+  Impl& m = *m_;
+  std::unique_lock<std::mutex> lk(m.mu);
+  m.cv.wait(lk, [&] { return !m.running; });
+  m.pend.push_back(&r);
+  const long long my = m.round;
+  if ((int)m.pend.size() >= m.active) {
+    std::vector<Req*> batch;
+    batch.swap(m.pend);
+    m.running = true;
+    lk.unlock();
+    std::exception_ptr e;
+    try {
+      launch(batch);
+    } catch (...) {
+      e = std::current_exception();
+    }
+    lk.lock();
+    m.err = e;
+    m.running = false;
+    m.round++;
+    m.cv.notify_all();
+    if (e) std::rethrow_exception(e);
+    return;
+  }
+  m.cv.wait(lk, [&] { return m.round != my; });
+  if (m.err) std::rethrow_exception(m.err);
+}
+
+// one R-row greedy step: embed, the layer chain with per-row cross-K/V, logit rules + pick
+void StepBatcher::launch(std::vector<Req*>& batch) {
+  Impl& m = *m_;
+  const int R = (int)batch.size();
+  WDR_CHECK(R >= 1 && R <= RB, "step batcher: row count out of range");
+  WDR_HIP(hipSetDevice(ctx_.cp.gpu_device));
+  for (int i = 0; i < R; ++i) {
+    m.h_rows[i] = batch[i]->tok;
+    m.h_rows[RB + i] = batch[i]->pos;
+    m.h_rows[2 * RB + i] = batch[i]->seq;
+    m.h_ctl[i] = batch[i]->ctl;
+    m.h_xkv[i] = batch[i]->xkv;
+  }
+  const VocabIds& vids = batch[0]->vids;
+  const HParams& hp = ctx_.model.hp;
+  const long long seq_stride = (long long)hp.n_text_ctx * m.d;
+  StepIO io{m.xd.as<float>(), m.qkvd.as<f16>(), m.attd.as<f16>(), m.qx.as<f16>(), m.mlpd.as<f16>(),
+            m.logits.as<float>(), m.V, m.part_o.as<float>(), m.part_ml.as<float2>(), m.rows_tok.as<int>(),
+            m.rows_pos.as<int>(), m.rows_seq.as<int>(), ctx_.kv_k.as<f16>(), ctx_.kv_v.as<f16>(),
+            (long long)ctx_.max_chains * NSLOT * seq_stride, seq_stride, nullptr, m.row_xkv.as<const f16*>()};
+  auto body = [&]() {
+    WDR_HIP(hipMemcpyAsync(m.rows_tok.p, m.h_rows, R * 4, hipMemcpyHostToDevice, m.s));
+    WDR_HIP(hipMemcpyAsync(m.rows_pos.p, m.h_rows + RB, R * 4, hipMemcpyHostToDevice, m.s));
+    WDR_HIP(hipMemcpyAsync(m.rows_seq.p, m.h_rows + 2 * RB, R * 4, hipMemcpyHostToDevice, m.s));
+    WDR_HIP(hipMemcpyAsync(m.ctl.p, m.h_ctl, R * sizeof(LogitsCtl), hipMemcpyHostToDevice, m.s));
+    WDR_HIP(hipMemcpyAsync(m.row_xkv.p, m.h_xkv, R * sizeof(void*), hipMemcpyHostToDevice, m.s));
+    launch_embed(ctx_.model.tok_emb, ctx_.model.dec_pos, m.rows_tok.as<int>(), m.rows_pos.as<int>(), R, m.d,
+                 m.xd.as<float>(), m.s);
+    decode_step_layers(ctx_, io, R, m.s);
+    launch_logits_process(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), vids, R, m.work.as<float>(),
+                          m.tokout.as<TokOut>(), m.s);
+    WDR_HIP(hipMemcpyAsync(m.h_tok, m.tokout.p, R * sizeof(TokOut), hipMemcpyDeviceToHost, m.s));
+  };
+  if (prof_class() != PROF_NONE || getenv("WDR_NO_GRAPH")) {
+    body();
+  } else {
+    Impl::G& g = m.graphs[R];
+    if (g.exec && memcmp(&g.vids, &vids, sizeof(VocabIds)) != 0) {
+      (void)hipGraphExecDestroy(g.exec);
+      g.exec = nullptr;
+    }
+    if (!g.exec) {
+      hipGraph_t graph;
+      WDR_HIP(hipStreamBeginCapture(m.s, hipStreamCaptureModeThreadLocal));
+      body();
+      WDR_HIP(hipStreamEndCapture(m.s, &graph));
+      WDR_HIP(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
+      WDR_HIP(hipGraphDestroy(graph));
+      g.vids = vids;
+    }
+    WDR_HIP(hipGraphLaunch(g.exec, m.s));
+  }
+  WDR_HIP(hipStreamSynchronize(m.s));
+  for (int i = 0; i < R; ++i) {
+    const TokOut& o = m.h_tok[i];
+    TokenData& t = batch[i]->out;
+    t = TokenData{};
+    t.id = o.id;
+    t.tid = o.tid;
+    t.p = o.p;
+    t.plog = o.plog;
+    t.pt = o.pt;
+    t.ptsum = o.ptsum;
+  }
+  launches++;
+  rows += R;
 }
 
 }  // namespace wdr

@@ -538,6 +538,11 @@ class WhisperContext:
         segs, lang, index = _segments(out, True)
         return segs, lang, index or []
 
+    def set_chains(self, n: int):
+        """Decode chains for greedy run_pipeline calls (wdr_context_set_chains): n blocks of the
+        speech segments decoded concurrently with batched steps, exact prompt fix-up."""
+        L.check(self._lib.wdr_context_set_chains(self.h, int(n)))
+
     def stage_times(self) -> dict:
         t = L.StageTimes()
         L.check(self._lib.wdr_context_stage_times(self.h, C.byref(t)))

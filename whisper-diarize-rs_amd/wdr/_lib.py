@@ -130,6 +130,7 @@ _SIGS = {
     "wdr_run_pipeline": (C.c_int, [vp, P(SpeechSegment), sz, P(TranscribeOptions), P(Synthetic), P(Callbacks),
                                    P(P(SegmentList))]),
     "wdr_segment_list_free": (None, [P(SegmentList)]),
+    "wdr_context_set_chains": (C.c_int, [vp, i32]),
     "wdr_context_stage_times": (C.c_int, [vp, P(StageTimes)]),
     "wdr_context_hparams": (C.c_int, [vp, P(i32)]),
     "wdr_prof_set": (C.c_int, [i32]),

@@ -212,10 +212,19 @@ def _raw_block(ctx, options: TranscribeOptions):
     return run
 
 
+# per-call statistics of the last transcribe_block on this rank (bench / probes)
+last_stats: dict = {}
+
+
 def transcribe_block(block_fn, segs: List[SpeechSegment], spec_prompt: Optional[str], rank: int, G: int):
     """Speculative decode of this rank's block, then the rank-ordered prompt fix-up.
     Returns (groups per speech segment, detected_lang of the block's first segment)."""
+    import time
+    t0 = time.perf_counter()
     groups, lang = block_fn(segs, spec_prompt) if segs else ([], None)
+    t1 = time.perf_counter()
+    last_stats.clear()
+    last_stats.update(segments=len(segs), spec_s=t1 - t0, fixups=0)
     # prompt entering each segment of the speculative run
     spec_in = [spec_prompt]
     for g in groups:
@@ -223,9 +232,12 @@ def transcribe_block(block_fn, segs: List[SpeechSegment], spec_prompt: Optional[
     e_in = spec_prompt
     if rank > 0:
         e_in = _recv_prompt(rank - 1)
+    t2 = time.perf_counter()
+    last_stats.update(wait_s=t2 - t1)
     if e_in != spec_prompt:
         e = e_in
         for j in range(len(segs)):
+            last_stats["fixups"] += 1
             gj, lj = block_fn([segs[j]], e)
             groups[j] = gj[0]
             if j == 0:
@@ -233,6 +245,7 @@ def transcribe_block(block_fn, segs: List[SpeechSegment], spec_prompt: Optional[
             e = next_prompt(e, gj[0])
             if e == spec_in[j + 1]:
                 break
+    last_stats.update(fixup_s=time.perf_counter() - t2)
     e_out = e_in
     for g in groups:
         e_out = next_prompt(e_out, g)
