@@ -141,6 +141,11 @@ typedef struct {
   double mel, encode, decode, dtw, vad, total;
   int64_t windows, decode_steps, prefills;
   double lang, prompt_gpu, embed;   /* language detect wall, prompt-prefill GPU time, speaker embeddings */
+  /* multi-chain decoding (wdr_context_set_chains): chains used, batched steps launched and
+   * the rows they carried, segments re-decoded by the prompt fix-up / the sampled-tail
+   * replay, wall time of the speculative and the fix-up phases */
+  int64_t chains, batch_launches, batch_rows, fixup_segments, replay_segments;
+  double spec_s, fixup_s;
 } wdr_stage_times;
 
 const char* wdr_last_error(void);
@@ -268,6 +273,10 @@ int wdr_dbg_decode(wdr_context* c, const int32_t* tokens, size_t n, float* logit
 int wdr_dbg_step(wdr_context* c, const int32_t* tokens, size_t n, int32_t mode, float* logits_out /* [n_vocab] */);
 /* timeline of the last persistent step (WDR_STEP_TRACE=1 at context creation): wall_clock64
  * stamps [67][n_wg] (layer < 4: 16 events per layer; 64 start, 65 logits ready, 66 end) */
+/* multi-chain batched step (StepBatcher) with `rows` rows on the last encoded window, `iters`
+ * times after prefilling tokens[0..n-2]: host milliseconds per step (probe seam) */
+int wdr_dbg_batch_step(wdr_context* c, const int32_t* tokens, size_t n, int32_t rows, int32_t iters,
+                       double* ms_per_step);
 int wdr_dbg_step_trace(wdr_context* c, uint64_t* out, int32_t cap, int32_t* n_wg);
 int wdr_dbg_capture(wdr_context* c, const int32_t* tokens, size_t n, float* cap_out /* [n_aheads][n][1500] */);
 int wdr_dbg_dtw(const float* cap, int32_t n_heads, int32_t n_tok, int32_t n_audio, int32_t sot_len, int32_t seek,

@@ -222,6 +222,10 @@ struct wdr_context {
   std::unique_ptr<State> st;
   std::vector<std::unique_ptr<State>> chain_st;   // decode chains 1.. (multi-chain pipeline)
   int chains = 1;                                 // decode chains per run_pipeline call
+  struct ChainStats {
+    long long chains = 1, launches = 0, rows = 0, fixups = 0, replays = 0;
+    double spec_s = 0, fixup_s = 0;
+  } cs;                                           // the last run_pipeline's multi-chain figures
   std::unique_ptr<CamModel> cam;   // EmbeddingExtractor, created on the first diarized run
   double load_s = 0;
   double embed_s = 0;              // wall time the decode chain waited on speaker embeddings
@@ -593,6 +597,10 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
   const Prompt e0{params.has_initial_prompt, params.initial_prompt};
   std::atomic<bool> stop{false};
   std::vector<std::exception_ptr> errs(C);
+  c->cs.chains = C;
+  StepBatcher& sb = c->ctx->step_batcher();
+  const long long l0 = sb.launches, r0 = sb.rows;
+  const double t_spec = now_s();
   auto worker = [&](int k) {
     State& st = state(k);
     try {
@@ -657,6 +665,8 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
       if (e) std::rethrow_exception(e);
     if (stop) throw std::runtime_error("failed to transcribe");
   }
+  c->cs.spec_s = now_s() - t_spec;
+  const double t_fix = now_s();
   // fix-ups in chain order (unplanned single-segment decodes, decoder 0's RNG fresh: no
   // segment before a fixed-up one drew, or the sampled tail below redoes it anyway)
   Prompt e_true = spec_out[cut[1] - 1];
@@ -670,6 +680,7 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
         if (cb && cb->is_cancelled && cb->is_cancelled(cb->user)) throw std::runtime_error("failed to transcribe");
         const std::vector<float> x = seg_f32(segs[j]);
         st.reset_rng();
+        c->cs.fixups++;
         if (st.full(with_prompt(params, e), x.data(), (int)x.size(), -1, false) != 0)
           throw std::runtime_error("failed to transcribe");
         out[j].res = st.result_all;
@@ -700,6 +711,7 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
     for (size_t i = f + 1; i < N; ++i) {
       if (cb && cb->is_cancelled && cb->is_cancelled(cb->user)) throw std::runtime_error("failed to transcribe");
       const std::vector<float> x = seg_f32(segs[i]);
+      c->cs.replays++;
       if (st.full(with_prompt(params, e), x.data(), (int)x.size(), -1, false) != 0)
         throw std::runtime_error("failed to transcribe");
       out[i].res = st.result_all;
@@ -707,6 +719,9 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
       e = next_prompt(e, out[i].res);
     }
   }
+  c->cs.fixup_s = now_s() - t_fix;
+  c->cs.launches = sb.launches - l0;
+  c->cs.rows = sb.rows - r0;
   // stage accounting: chains' times summed into the context's state
   for (int k = 1; k < C; ++k) {
     const StageTimes& t = state(k).times;
@@ -1314,6 +1329,7 @@ int wdr_run_pipeline(wdr_context* c, const wdr_speech_segment* segs, size_t n_se
     bool has_lang = false;
     const double t = now_s();
     c->st->times = StageTimes{};
+    c->cs = wdr_context::ChainStats{};
     std::vector<Seg> res = run_pipeline(c, v, o, syn_of(syn), cb, &lang, &has_lang);
     c->st->times.glue = now_s() - t;   // total wall for this pipeline call
     *out = to_list(res, has_lang ? &lang : nullptr);
@@ -1329,6 +1345,7 @@ int wdr_run_pipeline_raw(wdr_context* c, const wdr_speech_segment* segs, size_t 
     bool has_lang = false;
     const double t = now_s();
     c->st->times = StageTimes{};
+    c->cs = wdr_context::ChainStats{};
     std::vector<Seg> res = run_pipeline(c, v, o, syn_of(syn), nullptr, &lang, &has_lang, true);
     c->st->times.glue = now_s() - t;
     *out = to_list(res, has_lang ? &lang : nullptr);
@@ -1365,6 +1382,13 @@ int wdr_context_stage_times(wdr_context* c, wdr_stage_times* o) {
     const StageTimes& t = c->st->times;
     *o = wdr_stage_times{t.mel,          t.encode,   t.decode,  t.dtw,        0.0,  t.glue, t.windows,
                          t.decode_steps, t.prefills, t.lang,    t.prompt_gpu, c->embed_s};
+    o->chains = c->cs.chains;
+    o->batch_launches = c->cs.launches;
+    o->batch_rows = c->cs.rows;
+    o->fixup_segments = c->cs.fixups;
+    o->replay_segments = c->cs.replays;
+    o->spec_s = c->cs.spec_s;
+    o->fixup_s = c->cs.fixup_s;
     return 0;
   })
 }
@@ -1456,6 +1480,14 @@ int wdr_dbg_step(wdr_context* c, const int32_t* tokens, size_t n, int32_t mode, 
   WDR_GUARD({
     if (mode == 0 && !c->st->persistent_step()) return fail("persistent step not available for this model");
     c->st->dbg_step(tokens, (int)n, mode != 0, logits_out);
+    return 0;
+  })
+}
+
+int wdr_dbg_batch_step(wdr_context* c, const int32_t* tokens, size_t n, int32_t rows, int32_t iters,
+                       double* ms_per_step) {
+  WDR_GUARD({
+    *ms_per_step = c->st->dbg_batch_step(tokens, (int)n, rows, iters);
     return 0;
   })
 }

@@ -363,6 +363,168 @@ __global__ __launch_bounds__(256) void k_dgemv(ProjArgs a) {
   }
 }
 
+// Decode GEMV for 2 < M <= 8 rows (the multi-chain batched step, whisper_ctx.cpp StepBatcher):
+// k_dgemv's weight stream (each wave owns R weight rows, every load issued up front) with the
+// activation rows shared through LDS instead of registers.  With the LayerNorm prologue, wave w
+// normalises rows w, w+4 (the same arithmetic as k_dgemv, so every row's result is bit-identical
+// to the 1-row step's: multi-chain decoding equals one chain exactly) into LDS; without it the
+// rows are read per 512-wide chunk from L2.  Per (weight row, activation row) the dot product
+// runs over the chunks in the same order as k_dgemv, then the same wave reduction.
+template <int EPI, int MR, int R, int NCH, bool LN>
+__global__ __launch_bounds__(256) void k_mgemv(ProjArgs a) {
+  constexpr int KP = NCH * 512;
+  constexpr int LR = LN ? (MR + 3) / 4 : 1;   // LayerNorm rows per wave
+  extern __shared__ __attribute__((aligned(16))) f16 xsh[];   // LN: [MR][KP] normalised rows
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int n0 = (blockIdx.x * 4 + wid) * R;
+  const int K = a.K, M = a.M;
+  int kc[NCH];
+  bool kin[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int k = c * 512 + lane * 8;
+    kin[c] = k < K;
+    kc[c] = kin[c] ? k : K - 8;
+  }
+  // 1. this wave's LayerNorm rows (+ gamma / beta) first, then the weight stream
+  float xf[LR][LN ? NCH : 1][8];
+  float gv[LN ? NCH : 1][8], bv[LN ? NCH : 1][8];
+  if constexpr (LN) {
+#pragma unroll
+    for (int j = 0; j < LR; ++j) {
+      const int m = wid + 4 * j;
+      const int mm = m < M ? m : M - 1;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const float* xs = a.ln_x + (size_t)mm * a.ldln + kc[c];
+        const float4 p0 = *(const float4*)xs, p1 = *(const float4*)(xs + 4);
+        xf[j][c][0] = p0.x; xf[j][c][1] = p0.y; xf[j][c][2] = p0.z; xf[j][c][3] = p0.w;
+        xf[j][c][4] = p1.x; xf[j][c][5] = p1.y; xf[j][c][6] = p1.z; xf[j][c][7] = p1.w;
+        if (!kin[c])
+#pragma unroll
+          for (int e = 0; e < 8; ++e) xf[j][c][e] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const float4 g0 = *(const float4*)(a.ln_g + kc[c]), g1 = *(const float4*)(a.ln_g + kc[c] + 4);
+      const float4 b0 = *(const float4*)(a.ln_b + kc[c]), b1 = *(const float4*)(a.ln_b + kc[c] + 4);
+      gv[c][0] = g0.x; gv[c][1] = g0.y; gv[c][2] = g0.z; gv[c][3] = g0.w;
+      gv[c][4] = g1.x; gv[c][5] = g1.y; gv[c][6] = g1.z; gv[c][7] = g1.w;
+      bv[c][0] = b0.x; bv[c][1] = b0.y; bv[c][2] = b0.z; bv[c][3] = b0.w;
+      bv[c][4] = b1.x; bv[c][5] = b1.y; bv[c][6] = b1.z; bv[c][7] = b1.w;
+    }
+  }
+  f16x8 wv[R][NCH];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int n = n0 + r < a.N ? n0 + r : a.N - 1;
+    const f16* w = a.B + (size_t)n * a.ldb;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const f16x8 t = *(const f16x8*)(w + kc[c]);
+      wv[r][c] = kin[c] ? t : (f16x8){};
+    }
+  }
+  const int mrow = lane < M ? lane : 0;   // lane m stores output row m
+  float pbias[R], pold[R];
+  long long cdst = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int n = n0 + r < a.N ? n0 + r : a.N - 1;
+    pbias[r] = a.bias ? a.bias[n] : 0.f;
+    pold[r] = 0.f;
+    if constexpr (EPI == EPI_F32_RESID) pold[r] = ((const float*)a.out)[(size_t)mrow * a.ldo + n];
+  }
+  if constexpr (EPI == EPI_QKV_CACHE) cdst = a.row_seq[mrow] * a.seq_stride + (long long)a.row_pos[mrow] * a.d;
+  // 2. LayerNorm (ggml_norm, eps 1e-5; k_dgemv's arithmetic) into LDS
+  if constexpr (LN) {
+#pragma unroll
+    for (int j = 0; j < LR; ++j) {
+      const int m = wid + 4 * j;
+      float sm = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sm += xf[j][c][e];
+      sm = wave_sum(sm);
+      const float mean = sm / a.K;
+      float s2 = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float t = xf[j][c][e] - mean;
+          s2 += kin[c] ? t * t : 0.f;
+        }
+      s2 = wave_sum(s2);
+      const float scale = 1.0f / sqrtf(s2 / a.K + 1e-5f);
+      if (m < MR) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          f16x8 o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = (f16)((xf[j][c][e] - mean) * scale * gv[c][e] + bv[c][e]);
+          *(f16x8*)(xsh + m * KP + c * 512 + lane * 8) = o;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // 3. dot products chunk by chunk (activation rows from LDS / L2), reductions, epilogue
+  float acc[R][MR];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int m = 0; m < MR; ++m) acc[r][m] = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    f16x8 xv[MR];
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      if constexpr (LN) {
+        xv[m] = *(const f16x8*)(xsh + m * KP + c * 512 + lane * 8);
+      } else {
+        const int mm = m < M ? m : M - 1;
+        const f16x8 t = *(const f16x8*)(a.A + (size_t)mm * a.lda + kc[c]);
+        xv[m] = kin[c] ? t : (f16x8){};
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int m = 0; m < MR; ++m) acc[r][m] = dot8(wv[r][c], xv[m], acc[r][m]);
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int n = n0 + r;
+#pragma unroll
+    for (int m = 0; m < MR; ++m) acc[r][m] = wave_sum(acc[r][m]);
+    if (n >= a.N || lane >= MR || lane >= a.M) continue;
+    float v = acc[r][0];
+#pragma unroll
+    for (int m = 1; m < MR; ++m)
+      if (lane == m) v = acc[r][m];
+    v += pbias[r];
+    const size_t o = (size_t)lane * a.ldo + n;
+    if constexpr (EPI == EPI_F16) {
+      ((f16*)a.out)[o] = (f16)v;
+    } else if constexpr (EPI == EPI_F16_GELU) {
+      ((f16*)a.out)[o] = (f16)gelu_tanh(v);
+    } else if constexpr (EPI == EPI_F32_RESID) {
+      ((float*)a.out)[o] = pold[r] + v;
+    } else if constexpr (EPI == EPI_F32) {
+      ((float*)a.out)[o] = v;
+    } else if constexpr (EPI == EPI_QKV_CACHE) {
+      if (n < a.d) ((f16*)a.out)[o] = (f16)v;
+      else if (n < 2 * a.d) a.kc[cdst + n - a.d] = (f16)v;
+      else a.vc[cdst + n - 2 * a.d] = (f16)v;
+    } else {
+      epi_store<EPI>(a, lane, n, v - pbias[r]);
+    }
+  }
+}
+
 // General GEMV (optional LN prologue through LDS for 2 < M <= 8).
 template <int EPI, int MR, bool LN>
 __global__ __launch_bounds__(256) void k_gemv(ProjArgs a) {
@@ -508,6 +670,32 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
       }
 #undef WDR_DG_N
 #undef WDR_DG
+    } else if ((ln && a.K <= 1536) || (!ln && a.K <= 5120 && (a.K % 512 == 0 || a.K <= 1536))) {
+      // 3..8 rows (multi-chain batched steps): weight stream as k_dgemv, rows through LDS / L2
+      const int R = a.N >= 1024 ? 2 : 1;
+      dim3 g2(cdiv(a.N, 4 * R));
+      const bool m4 = a.M <= 4;
+      const uint32_t lds = ln ? (uint32_t)(m4 ? 4 : 8) * nch * 512 * 2 : 0;
+#define WDR_MG(MR, RR, NCH)                                                                                  \
+  if (ln) wdr_launch(PROF_GEMV, bytes, flops, k_mgemv<EPI, MR, RR, NCH, true>, g2, blk, lds, s, a);         \
+  else wdr_launch(PROF_GEMV, bytes, flops, k_mgemv<EPI, MR, RR, NCH, false>, g2, blk, 0, s, a);
+#define WDR_MG_N(MR, RR)                                                                                     \
+  switch (nch) {                                                                                             \
+    case 1: WDR_MG(MR, RR, 1) break;                                                                         \
+    case 2: WDR_MG(MR, RR, 2) break;                                                                         \
+    case 3: WDR_MG(MR, RR, 3) break;                                                                         \
+    case 4: if (!ln) { wdr_launch(PROF_GEMV, bytes, flops, k_mgemv<EPI, MR, RR, 4, false>, g2, blk, 0, s, a); } break; \
+    case 6: if (!ln) { wdr_launch(PROF_GEMV, bytes, flops, k_mgemv<EPI, MR, RR, 6, false>, g2, blk, 0, s, a); } break; \
+    case 8: if (!ln) { wdr_launch(PROF_GEMV, bytes, flops, k_mgemv<EPI, MR, RR, 8, false>, g2, blk, 0, s, a); } break; \
+    default: if (!ln) { wdr_launch(PROF_GEMV, bytes, flops, k_mgemv<EPI, MR, RR, 10, false>, g2, blk, 0, s, a); } break; \
+  }
+      if (m4) {
+        if (R == 2) { WDR_MG_N(4, 2) } else { WDR_MG_N(4, 1) }
+      } else {
+        if (R == 2) { WDR_MG_N(8, 2) } else { WDR_MG_N(8, 1) }
+      }
+#undef WDR_MG_N
+#undef WDR_MG
     } else {
       const uint32_t lds = ln ? (uint32_t)a.M * a.K * 2 : 0;
 #define WDR_GEMV(MR)                                                                          \

@@ -1,5 +1,7 @@
 #include "prof.h"
 
+#include <atomic>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -14,7 +16,7 @@ struct Rec {
 std::mutex g_mu;
 int g_cls = PROF_NONE;
 bool g_broken = false;
-unsigned g_tick = 0;
+std::atomic<unsigned> g_tick{0};
 constexpr unsigned kEvery = 8;
 std::vector<Rec> g_pending;
 std::vector<hipEvent_t> g_pool;
@@ -41,6 +43,15 @@ bool prof_on(int cls) {
   return (g_tick++ % kEvery) == 0;
 }
 int prof_class() { return g_cls; }
+
+std::mutex* launch_lock() {
+  static std::mutex mu;
+  static const bool on = [] {
+    const char* e = getenv("WDR_LAUNCH_LOCK");
+    return e && atoi(e) != 0;
+  }();
+  return on ? &mu : nullptr;
+}
 
 hipEvent_t prof_event() {
   std::lock_guard<std::mutex> l(g_mu);

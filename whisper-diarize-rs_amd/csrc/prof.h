@@ -5,6 +5,7 @@
 #pragma once
 #include <hip/hip_ext.h>
 
+#include <mutex>
 #include <vector>
 
 #include "common.h"
@@ -17,10 +18,15 @@ bool prof_on(int cls);
 int prof_class();
 hipEvent_t prof_event();
 void prof_push(hipEvent_t a, hipEvent_t b, double bytes, double flops);
+// WDR_LAUNCH_LOCK=1: kernel launches from the decode-chain threads go through one process-wide
+// mutex (profiling runs: rocprofv3's kernel tracing faults on concurrent multi-thread launches)
+std::mutex* launch_lock();
 
 template <typename F, typename... Args>
 inline void wdr_launch(int cls, double bytes, double flops, F kernel, dim3 grid, dim3 block, uint32_t shmem,
                        hipStream_t s, Args... args) {
+  std::mutex* mu = launch_lock();
+  if (mu) mu->lock();
   if (prof_on(cls)) {
     hipEvent_t a = prof_event(), b = prof_event();
     hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, a, b, 0, args...);
@@ -28,6 +34,7 @@ inline void wdr_launch(int cls, double bytes, double flops, F kernel, dim3 grid,
   } else {
     hipLaunchKernelGGL(kernel, grid, block, shmem, s, args...);
   }
+  if (mu) mu->unlock();
 }
 
 }  // namespace wdr

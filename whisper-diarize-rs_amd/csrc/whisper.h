@@ -163,6 +163,7 @@ class StepBatcher {
   void enter();
   void leave();
   void step(Req& r);           // blocks until the batch holding r has run
+  void run(std::vector<Req*>& batch) { launch(batch); }   // one batch, caller's thread (test seam)
   long long launches = 0, rows = 0;
   struct Impl;
 
@@ -210,6 +211,8 @@ class State {
 
   // test seams
   void compute_mel(const float* x_host, int n);
+  // R-row batched step (StepBatcher) on this state's window, `iters` times: host ms per step
+  double dbg_batch_step(const int* toks, int n, int R, int iters);
   void read_mel_window(int seek, float* out);              // [n_mels][3000] normalised
   void encode_window(int seek);
   void encode_from_mel_window(const float* mel_window);    // [n_mels][3000] normalised, host

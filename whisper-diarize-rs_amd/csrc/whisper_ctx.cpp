@@ -1181,6 +1181,29 @@ void State::dbg_step(const int* toks, int n, bool classic, float* logits_out) {
   step_err_check();
 }
 
+double State::dbg_batch_step(const int* toks, int n, int R, int iters) {
+  Impl& m = *m_;
+  WDR_CHECK(n >= 2 && n <= 448 && R >= 1 && R <= NSEQ && iters >= 1, "dbg_batch_step: bad shape");
+  decoder_prefill(toks, n - 1, 0, false, false);
+  WDR_HIP(hipStreamSynchronize(s_));
+  StepBatcher& b = ctx_.step_batcher();
+  std::vector<StepBatcher::Req> rq(R);
+  std::vector<StepBatcher::Req*> batch(R);
+  for (int r = 0; r < R; ++r) {
+    LogitsCtl c{};
+    c.n_tokens = 1;
+    c.pen_ts = 1;
+    c.force_kind = 2;
+    // every row reads this window's cross-K/V; rows 1.. attend over an uninitialised cache
+    rq[r] = StepBatcher::Req{toks[n - 1], chain * NSLOT + r, n - 1, m.xkv(), c, m.vids, {}};
+    batch[r] = &rq[r];
+  }
+  b.run(batch);
+  const double t = now_s();
+  for (int i = 0; i < iters; ++i) b.run(batch);
+  return (now_s() - t) * 1e3 / iters;
+}
+
 bool State::persistent_step() const { return m_->st_on; }
 
 void State::reset_rng() { m_->rng[0] = std::mt19937(0); }

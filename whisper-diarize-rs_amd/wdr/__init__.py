@@ -599,6 +599,15 @@ class WhisperContext:
                                        out.ctypes.data_as(C.POINTER(C.c_float))))
         return out
 
+    def batch_step_ms(self, tokens, rows: int, iters: int = 50) -> float:
+        """Host ms per multi-chain batched step of `rows` rows on the last encoded window
+        (wdr_dbg_batch_step probe seam)."""
+        t = np.ascontiguousarray(tokens, np.int32)
+        ms = C.c_double()
+        L.check(self._lib.wdr_dbg_batch_step(self.h, t.ctypes.data_as(C.POINTER(C.c_int32)), t.size, int(rows),
+                                             int(iters), C.byref(ms)))
+        return ms.value
+
     def capture(self, tokens, n_aheads: int) -> np.ndarray:
         t = np.ascontiguousarray(tokens, np.int32)
         out = np.zeros((n_aheads, t.size, 1500), np.float32)

@@ -79,7 +79,8 @@ class Callbacks(C.Structure):
 class StageTimes(C.Structure):
     _fields_ = [("mel", f64), ("encode", f64), ("decode", f64), ("dtw", f64), ("vad", f64), ("total", f64),
                 ("windows", i64), ("decode_steps", i64), ("prefills", i64), ("lang", f64), ("prompt_gpu", f64),
-                ("embed", f64)]
+                ("embed", f64), ("chains", i64), ("batch_launches", i64), ("batch_rows", i64),
+                ("fixup_segments", i64), ("replay_segments", i64), ("spec_s", f64), ("fixup_s", f64)]
 
 
 class Token(C.Structure):
@@ -131,6 +132,7 @@ _SIGS = {
                                    P(P(SegmentList))]),
     "wdr_segment_list_free": (None, [P(SegmentList)]),
     "wdr_context_set_chains": (C.c_int, [vp, i32]),
+    "wdr_dbg_batch_step": (C.c_int, [vp, P(i32), sz, i32, i32, P(f64)]),
     "wdr_context_stage_times": (C.c_int, [vp, P(StageTimes)]),
     "wdr_context_hparams": (C.c_int, [vp, P(i32)]),
     "wdr_prof_set": (C.c_int, [i32]),
