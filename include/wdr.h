@@ -212,6 +212,10 @@ int wdr_diarize_segments_from_classes(const int32_t* cls, size_t n_windows, cons
  * the 512-d embedding; ok = 0 where the reference's ONNX call fails (fewer than 400 samples) */
 int wdr_diarize_fbank(wdr_diarizer* d, const int16_t* samples, size_t n, float* feats_out, size_t* n_frames);
 int wdr_diarize_embedding(wdr_diarizer* d, const int16_t* samples, size_t n, float* emb_out, int8_t* ok);
+/* B utterances in one batched CAM++ forward (what the pipeline's embedding worker runs):
+ * emb_out [B][512], ok[b] as wdr_diarize_embedding's; bit-identical per utterance to it */
+int wdr_diarize_embedding_batch(wdr_diarizer* d, const int16_t* const* samples, const size_t* n, int32_t B,
+                                float* emb_out, int8_t* ok);
 /* GPU time of the last segmentation / embedding call (ms) */
 int wdr_diarize_stats(wdr_diarizer* d, double* seg_ms, double* emb_ms);
 /* EmbeddingManager + the reference's choice of get_best_speaker_match / search_speaker

@@ -75,6 +75,24 @@ def test_fbank_and_embedding(dz, audio, n):
     assert dz.stats()[1] > 0
 
 
+def test_embedding_batch_equals_single(dz, audio):
+    """The pipeline's embedding worker runs CamModel::embed_batch over many utterances at once;
+    per utterance it must be bit-identical to the one-utterance forward (ragged lengths, a
+    too-short utterance with no frames, a 1-frame utterance)."""
+    pcm, spurts = audio
+    segs = [pcm[int(a * 16000):int(b * 16000)] for a, b, _ in spurts]
+    segs = segs[:6] + [pcm[:399], pcm[5000:5400], pcm[7000:7000 + 16000 * 11 + 3]] + segs[6:9]
+    got = dz.embedding_batch(segs)
+    assert len(got) == len(segs)
+    for x, g in zip(segs, got):
+        e = dz.embedding(x)
+        if e is None:
+            assert g is None
+            continue
+        np.testing.assert_array_equal(g, e)
+    assert dz.embedding_batch([]) == []
+
+
 SYN = wdr.Synthetic(weight_std=0.02, emb_std=0.5, force_len_rate=3.3, disable_fallback=True)
 
 

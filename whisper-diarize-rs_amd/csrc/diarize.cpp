@@ -285,6 +285,11 @@ struct CamModel::W {
   const float *outs, *outb, *dense, *dens, *denb;
   // activations
   DevMem pcm, x, fb, a, b, r, col, XA, XB, h, y, ctx, c1buf, m, st, emb;
+  DevMem tab;                 // batched runs: utterance row tables (SegRows) + context offsets
+  int* h_tab = nullptr;       // pinned staging of tab
+  int tab_cap = 0;            // utterances
+  int B_cap = 0;              // st / emb rows
+  size_t pcm_cap = 0;         // samples
 };
 
 static double mel_k(double f) { return 1127.0 * std::log(1.0 + f / 700.0); }
@@ -412,17 +417,22 @@ CamModel::CamModel(int dev) : device(dev) {
 }
 
 CamModel::~CamModel() {
+  if (s_) (void)hipStreamSynchronize(s_);
+  if (w_ && w_->h_tab) (void)hipHostFree(w_->h_tab);
   delete w_;
   if (e0_) (void)hipEventDestroy(e0_);
   if (e1_) (void)hipEventDestroy(e1_);
   if (s_) (void)hipStreamDestroy(s_);
 }
 
-void CamModel::ensure(int T) {
-  if (T <= T_cap_) return;
+void CamModel::ensure(int T, int T2tot, int nsegtot) {
+  if (T <= T_cap_ && T2tot <= T2_cap_ && nsegtot <= nseg_cap_) return;
+  T = std::max(T, T_cap_);
+  T2tot = std::max(T2tot, T2_cap_);
+  nsegtot = std::max(nsegtot, nseg_cap_);
   W& w = *w_;
   const size_t t = (size_t)T;
-  const size_t t2 = t / 2 + 2;
+  const size_t t2 = (size_t)T2tot + 2;
   w.fb = DevMem(t * 80 * 4);
   w.a = DevMem(t * 80 * 32 * 4);
   w.b = DevMem(t * 80 * 32 * 4);
@@ -432,18 +442,20 @@ void CamModel::ensure(int T) {
   w.XB = DevMem(t2 * 1024 * 4);
   w.h = DevMem(t2 * 128 * 4);
   w.y = DevMem(t2 * 32 * 4);
-  const size_t nseg = (t2 + 99) / 100 + 1;
+  const size_t nseg = (size_t)nsegtot + 1;
   w.ctx = DevMem(nseg * 128 * 4);
   w.c1buf = DevMem(nseg * 64 * 4);
   w.m = DevMem(nseg * 32 * 4);
   T_cap_ = T;
+  T2_cap_ = T2tot;
+  nseg_cap_ = nsegtot;
 }
 
 int CamModel::run_fbank(const int16_t* pcm, size_t n) {
   W& w = *w_;
   const int T = n < 400 ? 0 : (int)(1 + (n - 400) / 160);
   if (T == 0) return 0;
-  ensure(T);
+  ensure(T, (T - 1) / 2 + 1, ((T - 1) / 2 + 1 + 99) / 100);
   if (w.pcm.bytes < n * 2) {
     w.pcm = DevMem(n * 2);
     w.x = DevMem(n * 4);
@@ -465,15 +477,94 @@ std::vector<float> CamModel::feats(const int16_t* pcm, size_t n) {
 }
 
 bool CamModel::embed(const int16_t* pcm, size_t n, float* emb_out) {
+  char ok = 0;
+  embed_batch(&pcm, &n, 1, emb_out, &ok);
+  return ok != 0;
+}
+
+// Several utterances in one forward: their fbank rows are concatenated, every GEMM runs over
+// all utterances' rows at once (the per-utterance convs, CMN, CAM context and stats pooling use
+// the batched kernels' row tables).  Per utterance the arithmetic is exactly the one-utterance
+// forward's, so each embedding is bit-identical to embed() of that utterance alone.
+void CamModel::embed_batch(const int16_t* const* pcm, const size_t* n, int B, float* emb_out, char* ok) {
   WDR_HIP(hipSetDevice(device));
   W& w = *w_;
   WDR_HIP(hipEventRecord(e0_, s_));
-  const int T = run_fbank(pcm, n);
-  if (T == 0) return false;
+  // utterances with frames (fewer than 400 samples: the reference's ORT call fails -> no embedding)
+  std::vector<int> idx, T, T2, ns;
+  size_t nsamp = 0;
+  for (int i = 0; i < B; ++i) {
+    ok[i] = 0;
+    const int t = n[i] < 400 ? 0 : (int)(1 + (n[i] - 400) / 160);
+    if (t == 0) continue;
+    idx.push_back(i);
+    T.push_back(t);
+    T2.push_back((t + 4 - 5) / 2 + 1);
+    ns.push_back((T2.back() + 99) / 100);
+    nsamp += n[i];
+  }
+  const int Bv = (int)idx.size();
+  if (Bv == 0) return;
+  // row tables: offT[Bv+1] lenT[Bv] offT2[Bv+1] lenT2[Bv] ctxoff[Bv+1]
+  const int tab_n = 5 * Bv + 3;
+  if (w.tab_cap < Bv) {
+    if (w.h_tab) (void)hipHostFree(w.h_tab);
+    WDR_HIP(hipHostMalloc((void**)&w.h_tab, (size_t)tab_n * 4, hipHostMallocDefault));
+    w.tab = DevMem((size_t)tab_n * 4);
+    w.tab_cap = Bv;
+  }
+  WDR_HIP(hipStreamSynchronize(s_));   // the pinned table may still feed the previous batch's copy
+  int* offT = w.h_tab;
+  int* lenT = offT + Bv + 1;
+  int* offT2 = lenT + Bv;
+  int* lenT2 = offT2 + Bv + 1;
+  int* ctxoff = lenT2 + Bv;
+  offT[0] = offT2[0] = ctxoff[0] = 0;
+  for (int b = 0; b < Bv; ++b) {
+    lenT[b] = T[b];
+    lenT2[b] = T2[b];
+    offT[b + 1] = offT[b] + T[b];
+    offT2[b + 1] = offT2[b] + T2[b];
+    ctxoff[b + 1] = ctxoff[b] + ns[b];
+  }
+  const int Tt = offT[Bv], T2t = offT2[Bv], nst = ctxoff[Bv];
+  ensure(Tt, T2t, nst);
+  if (w.B_cap < Bv) {
+    w.st = DevMem((size_t)Bv * 1024 * 4);
+    w.emb = DevMem((size_t)Bv * 512 * 4);
+    w.B_cap = Bv;
+  }
+  if (w.pcm_cap < nsamp) {
+    w.pcm = DevMem(nsamp * 2);
+    w.x = DevMem(nsamp * 4);
+    w.pcm_cap = nsamp;
+  }
+  WDR_HIP(hipMemcpyAsync(w.tab.p, w.h_tab, (size_t)tab_n * 4, hipMemcpyHostToDevice, s_));
+  const int* d = w.tab.as<int>();
+  const SegRows sT{d, d + Bv + 1, Bv};
+  const SegRows sT2{d + 2 * Bv + 1, d + 3 * Bv + 2, Bv};
+  const int* dctx = d + 4 * Bv + 2;
+  // i16 -> /32768 -> fbank per utterance into its rows, then CMN per utterance
+  {
+    size_t so = 0;
+    for (int b = 0; b < Bv; ++b) {
+      const int i = idx[b];
+      WDR_HIP(hipMemcpyAsync(w.pcm.as<int16_t>() + so, pcm[i], n[i] * 2, hipMemcpyHostToDevice, s_));
+      so += n[i];
+    }
+    launch_i16_scale(w.pcm.as<int16_t>(), (long long)nsamp, 1.0f / 32768.0f, w.x.as<float>(), s_);
+    so = 0;
+    for (int b = 0; b < Bv; ++b) {
+      launch_fbank(w.x.as<float>() + so, T[b], w.povey, w.cos_t, w.sin_t, w.banks, w.fb.as<float>() + (size_t)offT[b] * 80,
+                   s_);
+      so += n[idx[b]];
+    }
+    launch_colstats_b(w.fb.as<float>(), 80, sT, 80, 0, nullptr, s_);
+  }
   float* col = w.col.as<float>();
   // ---- FCM over [T][F][C]
-  launch_im2col_2d(w.fb.as<float>(), T, 80, 1, 3, 3, 1, 80, col, s_);
-  gemm(s_, col, 9, w.c1, 9, w.a.as<float>(), 32, T * 80, 32, 9, nullptr, ACT_RELU, w.bn1s, w.bn1b);
+  launch_im2col_2d_b(w.fb.as<float>(), sT, Tt, 80, 1, 3, 3, 1, 80, col, s_);
+  gemm(s_, col, 9, w.c1, 9, w.a.as<float>(), 32, Tt * 80, 32, 9, nullptr, ACT_RELU, w.bn1s, w.bn1b);
   float* cur = w.a.as<float>();
   float* tmp = w.b.as<float>();
   float* res = w.r.as<float>();
@@ -483,73 +574,75 @@ bool CamModel::embed(const int16_t* pcm, size_t n, float* emb_out) {
     const int sf = (i % 2 == 0) ? 2 : 1;
     const int Fo = sf == 2 ? (F + 2 - 3) / 2 + 1 : F;
     // y = relu(bn1(conv1(x)))
-    launch_im2col_2d(cur, T, F, 32, 3, 3, sf, Fo, col, s_);
-    gemm(s_, col, 288, R.w1, 288, tmp, 32, T * Fo, 32, 288, nullptr, ACT_RELU, R.s1, R.b1);
+    launch_im2col_2d_b(cur, sT, Tt, F, 32, 3, 3, sf, Fo, col, s_);
+    gemm(s_, col, 288, R.w1, 288, tmp, 32, Tt * Fo, 32, 288, nullptr, ACT_RELU, R.s1, R.b1);
     // shortcut into res
     if (R.sc) {
-      launch_im2col_2d(cur, T, F, 32, 1, 1, 2, Fo, col, s_);
-      gemm(s_, col, 32, R.sc, 32, res, 32, T * Fo, 32, 32, nullptr, ACT_NONE, R.scs, R.scb);
+      launch_im2col_2d_b(cur, sT, Tt, F, 32, 1, 1, 2, Fo, col, s_);
+      gemm(s_, col, 32, R.sc, 32, res, 32, Tt * Fo, 32, 32, nullptr, ACT_NONE, R.scs, R.scb);
     } else {
-      WDR_HIP(hipMemcpyAsync(res, cur, (size_t)T * Fo * 32 * 4, hipMemcpyDeviceToDevice, s_));
+      WDR_HIP(hipMemcpyAsync(res, cur, (size_t)Tt * Fo * 32 * 4, hipMemcpyDeviceToDevice, s_));
     }
     // out = relu(bn2(conv2(y)) + shortcut)
-    launch_im2col_2d(tmp, T, Fo, 32, 3, 3, 1, Fo, col, s_);
-    gemm(s_, col, 288, R.w2, 288, res, 32, T * Fo, 32, 288, nullptr, ACT_RELU, R.s2, R.b2, nullptr, nullptr, 1);
+    launch_im2col_2d_b(tmp, sT, Tt, Fo, 32, 3, 3, 1, Fo, col, s_);
+    gemm(s_, col, 288, R.w2, 288, res, 32, Tt * Fo, 32, 288, nullptr, ACT_RELU, R.s2, R.b2, nullptr, nullptr, 1);
     std::swap(cur, res);
     F = Fo;
   }
   // conv2 (stride 2 in frequency) + bn2 + relu: [T][10][32] == [T][320] (column f*32 + c)
-  launch_im2col_2d(cur, T, F, 32, 3, 3, 2, 10, col, s_);
-  gemm(s_, col, 288, w.c2, 288, tmp, 32, T * 10, 32, 288, nullptr, ACT_RELU, w.bn2s, w.bn2b);
+  launch_im2col_2d_b(cur, sT, Tt, F, 32, 3, 3, 2, 10, col, s_);
+  gemm(s_, col, 288, w.c2, 288, tmp, 32, Tt * 10, 32, 288, nullptr, ACT_RELU, w.bn2s, w.bn2b);
   // ---- TDNN k5 s2 p2 -> X [T2][1024] (ld 1024)
-  const int T2 = (T + 4 - 5) / 2 + 1;
-  launch_im2col_1d(tmp, 320, T, 320, 5, 2, 1, 2, T2, col, s_);
+  launch_im2col_1d_b(tmp, 320, sT, sT2, T2t, 320, 5, 2, 1, 2, col, s_);
   float* X = w.XA.as<float>();
   float* Y = w.XB.as<float>();
-  gemm(s_, col, 1600, w.tdnn, 1600, X, 1024, T2, 128, 1600, nullptr, ACT_RELU, w.tds, w.tdb);
+  gemm(s_, col, 1600, w.tdnn, 1600, X, 1024, T2t, 128, 1600, nullptr, ACT_RELU, w.tds, w.tdb);
   int ch = 128;
-  const int nseg = (T2 + 99) / 100;
   for (int bi = 0; bi < 3; ++bi) {
     const int nl = kCamBlocks[bi][0], k = kCamBlocks[bi][1], dil = kCamBlocks[bi][2];
     for (int li = 0; li < nl; ++li) {
       const W::Layer& Lr = w.layers[bi][li];
       const int cin = ch + li * 32;
       // h = relu(bn2(linear1(relu(bn1(x)))))
-      gemm(s_, X, 1024, Lr.lin1, cin, w.h.as<float>(), 128, T2, 128, cin, nullptr, ACT_RELU, Lr.s2, Lr.b2, Lr.s1,
+      gemm(s_, X, 1024, Lr.lin1, cin, w.h.as<float>(), 128, T2t, 128, cin, nullptr, ACT_RELU, Lr.s2, Lr.b2, Lr.s1,
            Lr.b1);
       // y = local conv (k3, dilation)
-      launch_im2col_1d(w.h.as<float>(), 128, T2, 128, k, 1, dil, (k - 1) / 2 * dil, T2, col, s_);
-      gemm(s_, col, 128 * k, Lr.local, 128 * k, w.y.as<float>(), 32, T2, 32, 128 * k, nullptr, ACT_NONE);
+      launch_im2col_1d_b(w.h.as<float>(), 128, sT2, sT2, T2t, 128, k, 1, dil, (k - 1) / 2 * dil, col, s_);
+      gemm(s_, col, 128 * k, Lr.local, 128 * k, w.y.as<float>(), 32, T2t, 32, 128 * k, nullptr, ACT_NONE);
       // m = sigmoid(W2 relu(W1 (mean + segment mean) + b1) + b2), one row per 100-frame segment
-      launch_cam_context(w.h.as<float>(), 128, T2, 128, w.ctx.as<float>(), s_);
-      gemm(s_, w.ctx.as<float>(), 128, Lr.cam1w, 128, w.c1buf.as<float>(), 64, nseg, 64, 128, Lr.cam1b, ACT_RELU);
-      gemm(s_, w.c1buf.as<float>(), 64, Lr.cam2w, 64, w.m.as<float>(), 32, nseg, 32, 64, Lr.cam2b, ACT_SIGMOID);
-      launch_cam_gate(w.y.as<float>(), 32, w.m.as<float>(), T2, 32, X + cin, 1024, s_);
+      launch_cam_context_b(w.h.as<float>(), 128, sT2, dctx, 128, w.ctx.as<float>(), s_);
+      gemm(s_, w.ctx.as<float>(), 128, Lr.cam1w, 128, w.c1buf.as<float>(), 64, nst, 64, 128, Lr.cam1b, ACT_RELU);
+      gemm(s_, w.c1buf.as<float>(), 64, Lr.cam2w, 64, w.m.as<float>(), 32, nst, 32, 64, Lr.cam2b, ACT_SIGMOID);
+      launch_cam_gate_b(w.y.as<float>(), 32, w.m.as<float>(), sT2, dctx, T2t, 32, X + cin, 1024, s_);
     }
     ch += nl * 32;
     // transit: linear(relu(bn(x))) -> ch/2 channels; after the last block, out_nonlinear
     // (BN + ReLU) is fused into the epilogue
     if (bi < 2) {
-      gemm(s_, X, 1024, w.trw[bi], ch, Y, 1024, T2, ch / 2, ch, nullptr, ACT_NONE, nullptr, nullptr, w.trs[bi],
+      gemm(s_, X, 1024, w.trw[bi], ch, Y, 1024, T2t, ch / 2, ch, nullptr, ACT_NONE, nullptr, nullptr, w.trs[bi],
            w.trb[bi]);
     } else {
-      gemm(s_, X, 1024, w.trw[bi], ch, Y, 1024, T2, ch / 2, ch, nullptr, ACT_RELU, w.outs, w.outb, w.trs[bi],
+      gemm(s_, X, 1024, w.trw[bi], ch, Y, 1024, T2t, ch / 2, ch, nullptr, ACT_RELU, w.outs, w.outb, w.trs[bi],
            w.trb[bi]);
     }
     std::swap(X, Y);
     ch /= 2;
   }
-  // stats pooling + dense + BN
-  launch_colstats(X, 1024, T2, ch, 1, w.st.as<float>(), s_);
-  gemm(s_, w.st.as<float>(), 2 * ch, w.dense, 2 * ch, w.emb.as<float>(), 512, 1, 512, 2 * ch, nullptr, ACT_NONE, w.dens,
-       w.denb);
-  WDR_HIP(hipMemcpyAsync(emb_out, w.emb.p, 512 * 4, hipMemcpyDeviceToHost, s_));
+  // stats pooling + dense + BN (one row per utterance)
+  launch_colstats_b(X, 1024, sT2, ch, 1, w.st.as<float>(), s_);
+  gemm(s_, w.st.as<float>(), 2 * ch, w.dense, 2 * ch, w.emb.as<float>(), 512, Bv, 512, 2 * ch, nullptr, ACT_NONE,
+       w.dens, w.denb);
+  std::vector<float> e((size_t)Bv * 512);
+  WDR_HIP(hipMemcpyAsync(e.data(), w.emb.p, e.size() * 4, hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipEventRecord(e1_, s_));
   WDR_HIP(hipStreamSynchronize(s_));
+  for (int b = 0; b < Bv; ++b) {
+    memcpy(emb_out + (size_t)idx[b] * 512, e.data() + (size_t)b * 512, 512 * 4);
+    ok[idx[b]] = 1;
+  }
   float ms = 0.f;
   WDR_HIP(hipEventElapsedTime(&ms, e0_, e1_));
   last_ms = ms;
-  return true;
 }
 
 // ================================================================== speakers

@@ -48,6 +48,9 @@ class CamModel {
   // EmbeddingExtractor::compute: i16 -> /32768 -> fbank -> CMN -> CAM++ -> [512].
   // Returns false where the reference's ORT call fails (fewer than 400 samples: no frames).
   bool embed(const int16_t* pcm, size_t n, float* emb_out);
+  // B utterances in one batched forward: emb_out[b * 512 ..], ok[b] = embed()'s return value
+  // (bit-identical per utterance to embed())
+  void embed_batch(const int16_t* const* pcm, const size_t* n, int B, float* emb_out, char* ok);
   // fbank after CMN, [T][80] (test seam)
   std::vector<float> feats(const int16_t* pcm, size_t n);
   double last_ms = 0.0;
@@ -58,8 +61,8 @@ class CamModel {
   W* w_ = nullptr;
   hipStream_t s_ = nullptr;
   hipEvent_t e0_ = nullptr, e1_ = nullptr;
-  int T_cap_ = 0;
-  void ensure(int T);
+  int T_cap_ = 0, T2_cap_ = 0, nseg_cap_ = 0;
+  void ensure(int T, int T2tot, int nsegtot);
   int run_fbank(const int16_t* pcm, size_t n);
 };
 

@@ -241,13 +241,28 @@ class EmbedAhead {
       : emb_(segs.size() * 512), ok_(segs.size(), 0) {
     th_ = std::thread([this, &cam, &segs] {
       try {
-        for (size_t i = 0; i < segs.size(); ++i) {
-          if (stop_) break;
-          const bool ok = cam.embed(segs[i].samples, segs[i].n_samples, emb_.data() + i * 512);
+        // batches of consecutive segments (CamModel::embed_batch: one forward over all their
+        // frames); the first batch is small so that segment 0's embedding is ready early
+        size_t i = 0;
+        long long cap = 2000;
+        while (i < segs.size() && !stop_) {
+          std::vector<const int16_t*> p;
+          std::vector<size_t> n;
+          long long frames = 0;
+          for (size_t j = i; j < segs.size() && (p.empty() || (frames < cap && p.size() < 64)); ++j) {
+            p.push_back(segs[j].samples);
+            n.push_back(segs[j].n_samples);
+            frames += (long long)segs[j].n_samples / 160;
+          }
+          const int B = (int)p.size();
+          std::vector<char> ok(B);
+          cam.embed_batch(p.data(), n.data(), B, emb_.data() + i * 512, ok.data());
           std::lock_guard<std::mutex> g(mu_);
-          ok_[i] = ok;
-          done_ = i + 1;
+          for (int b = 0; b < B; ++b) ok_[i + b] = ok[b];
+          i += B;
+          done_ = i;
           cv_.notify_all();
+          cap = 16000;
         }
       } catch (...) {
         std::lock_guard<std::mutex> g(mu_);
@@ -1180,6 +1195,17 @@ int wdr_diarize_fbank(wdr_diarizer* d, const int16_t* samples, size_t n, float* 
 int wdr_diarize_embedding(wdr_diarizer* d, const int16_t* samples, size_t n, float* emb_out, int8_t* ok) {
   WDR_GUARD({
     *ok = d->E().embed(samples, n, emb_out) ? 1 : 0;
+    return 0;
+  })
+}
+
+int wdr_diarize_embedding_batch(wdr_diarizer* d, const int16_t* const* samples, const size_t* n, int32_t B,
+                                float* emb_out, int8_t* ok) {
+  WDR_GUARD({
+    if (B < 0) return fail("embedding batch: negative count");
+    std::vector<char> k(B);
+    if (B) d->E().embed_batch(samples, n, B, emb_out, k.data());
+    for (int b = 0; b < B; ++b) ok[b] = k[b];
     return 0;
   })
 }

@@ -446,6 +446,161 @@ void launch_cam_gate(const float* y, int ldy, const float* m, int T, int G, floa
   WDR_HIP(hipGetLastError());
 }
 
+
+// ---------------------------------------------------------------- batched CAM++ (several utterances)
+// Utterance b's rows are [off[b], off[b] + len[b]) of a concatenated [rows][...] buffer (CamModel
+// embed_batch).  Each kernel below does, per utterance, exactly the arithmetic of its
+// single-utterance form above, so every embedding is bit-identical to a one-utterance run.
+__device__ __forceinline__ int seg_of(const int* off, int B, int r) {
+  int lo = 0, hi = B - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= r) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ void k_im2col_2d_b(const float* X, SegRows sr, int Ttot, int F, int C, int kf, int kt, int sf, int Fo,
+                              float* col) {
+  const int pf = (kf - 1) / 2, pt = (kt - 1) / 2;
+  const int K = C * kf * kt;
+  const long long total = (long long)Ttot * Fo * K;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const long long row = i / K;
+    const int r = (int)(i - row * K);
+    const int tg = (int)(row / Fo), f = (int)(row - (long long)tg * Fo);
+    const int b = seg_of(sr.off, sr.B, tg);
+    const int t = tg - sr.off[b], T = sr.len[b];
+    const int c = r / (kf * kt), q = r - c * kf * kt;
+    const int aa = q / kt, bb = q - aa * kt;
+    const int tt = t + bb - pt, ff = f * sf + aa - pf;
+    col[i] = (tt >= 0 && tt < T && ff >= 0 && ff < F) ? X[((long long)(sr.off[b] + tt) * F + ff) * C + c] : 0.f;
+  }
+}
+
+void launch_im2col_2d_b(const float* X, const SegRows& sr, int Ttot, int F, int C, int kf, int kt, int sf, int Fo,
+                        float* col, hipStream_t s) {
+  const long long total = (long long)Ttot * Fo * C * kf * kt;
+  if (total <= 0) return;
+  const int grid = (int)std::min<long long>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_im2col_2d_b, dim3(grid), dim3(256), 0, s, X, sr, Ttot, F, C, kf, kt, sf, Fo, col);
+  WDR_HIP(hipGetLastError());
+}
+
+// col[u][c*k + j] = X[in.off[b] + u_local*stride + j*dil - pad][c] within utterance b's input rows
+__global__ void k_im2col_1d_b(const float* X, int ldx, SegRows in, SegRows out, int Ttot_out, int C, int k, int stride,
+                              int dil, int pad, float* col) {
+  const long long total = (long long)Ttot_out * C * k;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int tg = (int)(i / (C * k));
+    const int r = (int)(i - (long long)tg * C * k);
+    const int c = r / k, j = r - c * k;
+    const int b = seg_of(out.off, out.B, tg);
+    const int t = tg - out.off[b];
+    const int u = t * stride + j * dil - pad;
+    col[i] = (u >= 0 && u < in.len[b]) ? X[(long long)(in.off[b] + u) * ldx + c] : 0.f;
+  }
+}
+
+void launch_im2col_1d_b(const float* X, int ldx, const SegRows& in, const SegRows& out, int Ttot_out, int C, int k,
+                        int stride, int dil, int pad, float* col, hipStream_t s) {
+  const long long total = (long long)Ttot_out * C * k;
+  if (total <= 0) return;
+  const int grid = (int)std::min<long long>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_im2col_1d_b, dim3(grid), dim3(256), 0, s, X, ldx, in, out, Ttot_out, C, k, stride, dil, pad,
+                     col);
+  WDR_HIP(hipGetLastError());
+}
+
+// k_colstats per utterance (blockIdx.y): CMN in place, or stats pooling into out[b][2C]
+__global__ __launch_bounds__(256) void k_colstats_b(float* xall, int ld, SegRows sr, int C, int mode, float* outall) {
+  const int c = blockIdx.x, b = blockIdx.y;
+  const int T = sr.len[b];
+  float* x = xall + (long long)sr.off[b] * ld;
+  float* out = outall ? outall + (long long)b * 2 * C : nullptr;
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int t = threadIdx.x; t < T; t += 256) s += x[(long long)t * ld + c];
+  s = wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  const double mean = (red[0] + red[1] + red[2] + red[3]) / T;
+  if (mode == 0) {
+    const float mf = (float)mean;
+    for (int t = threadIdx.x; t < T; t += 256) x[(long long)t * ld + c] -= mf;
+    return;
+  }
+  __syncthreads();
+  double v = 0.0;
+  for (int t = threadIdx.x; t < T; t += 256) {
+    const double d = x[(long long)t * ld + c] - mean;
+    v += d * d;
+  }
+  v = wave_sum_d(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out[c] = (float)mean;
+    out[C + c] = T > 1 ? (float)sqrt((red[0] + red[1] + red[2] + red[3]) / (T - 1)) : __builtin_nanf("");
+  }
+}
+
+void launch_colstats_b(float* x, int ld, const SegRows& sr, int C, int mode, float* out, hipStream_t s) {
+  if (sr.B <= 0 || C <= 0) return;
+  hipLaunchKernelGGL(k_colstats_b, dim3(C, sr.B), dim3(256), 0, s, x, ld, sr, C, mode, out);
+  WDR_HIP(hipGetLastError());
+}
+
+// k_cam_context per utterance (blockIdx.y); its context rows start at ctx_off[b]
+__global__ __launch_bounds__(256) void k_cam_context_b(const float* hall, int ldh, SegRows sr, const int* ctx_off, int C,
+                                                       float* outall) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, b = blockIdx.y;
+  if (c >= C) return;
+  const int T = sr.len[b];
+  const float* h = hall + (long long)sr.off[b] * ldh;
+  float* out = outall + (long long)ctx_off[b] * C;
+  double tot = 0.0;
+  for (int t = lane; t < T; t += 64) tot += h[(long long)t * ldh + c];
+  tot = wave_sum_d(tot);
+  const float gm = (float)(tot / T);
+  const int nseg = (T + 99) / 100;
+  for (int sgi = 0; sgi < nseg; ++sgi) {
+    const int t0 = sgi * 100, t1 = min(T, t0 + 100);
+    double s = 0.0;
+    for (int t = t0 + lane; t < t1; t += 64) s += h[(long long)t * ldh + c];
+    s = wave_sum_d(s);
+    if (lane == 0) out[(long long)sgi * C + c] = gm + (float)(s / (t1 - t0));
+  }
+}
+
+void launch_cam_context_b(const float* h, int ldh, const SegRows& sr, const int* ctx_off, int C, float* out,
+                          hipStream_t s) {
+  if (sr.B <= 0) return;
+  hipLaunchKernelGGL(k_cam_context_b, dim3(cdiv(C, 4), sr.B), dim3(256), 0, s, h, ldh, sr, ctx_off, C, out);
+  WDR_HIP(hipGetLastError());
+}
+
+__global__ void k_cam_gate_b(const float* y, int ldy, const float* m, SegRows sr, const int* ctx_off, int Ttot, int G,
+                             float* out, int ldo) {
+  const long long total = (long long)Ttot * G;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int tg = (int)(i / G), j = (int)(i - (long long)tg * G);
+    const int b = seg_of(sr.off, sr.B, tg);
+    const int t = tg - sr.off[b];
+    out[(long long)tg * ldo + j] = y[(long long)tg * ldy + j] * m[(long long)(ctx_off[b] + t / 100) * G + j];
+  }
+}
+
+void launch_cam_gate_b(const float* y, int ldy, const float* m, const SegRows& sr, const int* ctx_off, int Ttot, int G,
+                       float* out, int ldo, hipStream_t s) {
+  const long long total = (long long)Ttot * G;
+  if (total <= 0) return;
+  hipLaunchKernelGGL(k_cam_gate_b, dim3((unsigned)std::min<long long>((total + 255) / 256, 8192)), dim3(256), 0, s, y,
+                     ldy, m, sr, ctx_off, Ttot, G, out, ldo);
+  WDR_HIP(hipGetLastError());
+}
 }  // namespace wdr
 
 namespace wdr {

@@ -200,5 +200,20 @@ void launch_colstats(float* x, int ld, int T, int C, int mode, float* out, hipSt
 void launch_cam_context(const float* h, int ldh, int T, int C, float* out, hipStream_t s);
 void launch_i16_scale(const int16_t* in, long long n, float scale, float* out, hipStream_t s);
 void launch_cam_gate(const float* y, int ldy, const float* m, int T, int G, float* out, int ldo, hipStream_t s);
+// batched CAM++: utterance b owns rows [off[b], off[b] + len[b]) (device arrays, off[B] = total)
+struct SegRows {
+  const int* off;
+  const int* len;
+  int B;
+};
+void launch_im2col_2d_b(const float* X, const SegRows& sr, int Ttot, int F, int C, int kf, int kt, int sf, int Fo,
+                        float* col, hipStream_t s);
+void launch_im2col_1d_b(const float* X, int ldx, const SegRows& in, const SegRows& out, int Ttot_out, int C, int k,
+                        int stride, int dil, int pad, float* col, hipStream_t s);
+void launch_colstats_b(float* x, int ld, const SegRows& sr, int C, int mode, float* out, hipStream_t s);
+void launch_cam_context_b(const float* h, int ldh, const SegRows& sr, const int* ctx_off, int C, float* out,
+                          hipStream_t s);
+void launch_cam_gate_b(const float* y, int ldy, const float* m, const SegRows& sr, const int* ctx_off, int Ttot, int G,
+                       float* out, int ldo, hipStream_t s);
 
 }  // namespace wdr

@@ -460,6 +460,18 @@ class Diarizer:
                                                 out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(ok)))
         return out if ok.value else None
 
+    def embedding_batch(self, segments):
+        """Embeddings of several utterances in one batched forward (wdr_diarize_embedding_batch):
+        a list with None where embedding() would return None."""
+        smp = [np.ascontiguousarray(x, np.int16) for x in segments]
+        B = len(smp)
+        ptrs = (C.POINTER(C.c_int16) * max(B, 1))(*[x.ctypes.data_as(C.POINTER(C.c_int16)) for x in smp])
+        ns = (C.c_size_t * max(B, 1))(*[x.size for x in smp])
+        out = np.zeros((max(B, 1), 512), np.float32)
+        ok = (C.c_int8 * max(B, 1))()
+        L.check(self._lib.wdr_diarize_embedding_batch(self.h, ptrs, ns, B, out.ctypes.data_as(C.POINTER(C.c_float)), ok))
+        return [out[b].copy() if ok[b] else None for b in range(B)]
+
     def stats(self):
         a, b = C.c_double(), C.c_double()
         L.check(self._lib.wdr_diarize_stats(self.h, C.byref(a), C.byref(b)))

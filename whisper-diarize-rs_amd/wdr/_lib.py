@@ -120,6 +120,7 @@ _SIGS = {
     "wdr_diarize_segments_from_classes": (C.c_int, [P(i32), sz, P(C.c_int16), sz, P(P(SpeechSegment)), P(sz)]),
     "wdr_diarize_fbank": (C.c_int, [vp, P(C.c_int16), sz, P(f32), P(sz)]),
     "wdr_diarize_embedding": (C.c_int, [vp, P(C.c_int16), sz, P(f32), P(i8)]),
+    "wdr_diarize_embedding_batch": (C.c_int, [vp, P(P(C.c_int16)), P(sz), i32, P(f32), P(i8)]),
     "wdr_diarize_stats": (C.c_int, [vp, P(f64), P(f64)]),
     "wdr_speakers_new": (C.c_int, [i8, u64, P(vp)]),
     "wdr_speakers_free": (None, [vp]),
