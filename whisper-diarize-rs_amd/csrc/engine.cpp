@@ -682,34 +682,74 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
   }
   c->cs.spec_s = now_s() - t_spec;
   const double t_fix = now_s();
-  // fix-ups in chain order (unplanned single-segment decodes, decoder 0's RNG fresh: no
-  // segment before a fixed-up one drew, or the sampled tail below redoes it anyway)
-  Prompt e_true = spec_out[cut[1] - 1];
-  for (int k = 1; k < C; ++k) {
-    const size_t a = cut[k], b = cut[k + 1];
-    if (e_true != e0) {
-      State& st = state(k);
-      Prompt e = e_true;
-      size_t j = a;
-      for (; j < b; ++j) {
-        if (cb && cb->is_cancelled && cb->is_cancelled(cb->user)) throw std::runtime_error("failed to transcribe");
-        const std::vector<float> x = seg_f32(segs[j]);
-        st.reset_rng();
-        c->cs.fixups++;
-        if (st.full(with_prompt(params, e), x.data(), (int)x.size(), -1, false) != 0)
-          throw std::runtime_error("failed to transcribe");
-        out[j].res = st.result_all;
-        out[j].lang_id = st.lang_id;
-        out[j].sampled = st.sampled;
-        out[j].rng_after = st.sampled ? st.rng_state() : std::string();
-        e = next_prompt(e, out[j].res);
-        if (e == spec_out[j]) break;
-      }
-      e_true = j < b ? spec_out[b - 1] : e;
-    } else {
-      e_true = spec_out[b - 1];
+  // Fix-up rounds.  dec_in[k] is the prompt chain k's first segment was decoded from (e0 in
+  // the speculative run); the true one is the prompt leaving block k-1 as it now stands.  Every
+  // chain whose two differ re-decodes its block from the true prompt -- all such chains at once,
+  // their greedy steps batched as in the speculative phase -- segment by segment until the
+  // prompt leaving a segment equals the one its successor was decoded from.  A chain that ran
+  // through its whole block changes its successor's true prompt: the next round redoes that
+  // one.  Chain 0 is always exact, so every round fixes at least one more chain.  Each redone
+  // segment starts from decoder 0's initial RNG state: no segment before it drew (or the
+  // sampled tail below redoes it anyway).
+  std::vector<Prompt> dec_in(C, e0);
+  std::atomic<long long> fixups{0};
+  for (;;) {
+    std::vector<int> redo;
+    std::vector<Prompt> e_true(C);
+    for (int k = 1; k < C; ++k) {
+      e_true[k] = spec_out[cut[k] - 1];
+      if (e_true[k] != dec_in[k]) redo.push_back(k);
     }
+    if (redo.empty()) break;
+    const bool batch = redo.size() > 1;
+    auto fix = [&](int k) {
+      State& st = state(k);
+      try {
+        const size_t a = cut[k], b = cut[k + 1];
+        st.batched = batch;
+        struct Guard {
+          State& st;
+          ~Guard() { st.batched = false; }
+        } guard{st};
+        Prompt e = e_true[k];
+        for (size_t j = a; j < b && !stop; ++j) {
+          const std::vector<float> x = seg_f32(segs[j]);
+          st.reset_rng();
+          if (st.full(with_prompt(params, e), x.data(), (int)x.size(), -1, false) != 0)
+            throw std::runtime_error("failed to transcribe");
+          out[j].res = st.result_all;
+          out[j].lang_id = st.lang_id;
+          out[j].sampled = st.sampled;
+          out[j].rng_after = st.sampled ? st.rng_state() : std::string();
+          e = next_prompt(e, out[j].res);
+          const bool converged = e == spec_out[j];
+          spec_out[j] = e;
+          fixups++;
+          if (converged) break;
+        }
+      } catch (...) {
+        errs[k] = std::current_exception();
+        stop = true;
+      }
+    };
+    std::atomic<int> live{(int)redo.size()};
+    std::vector<std::thread> th;
+    for (int k : redo)
+      th.emplace_back([&, k] {
+        fix(k);
+        live--;
+      });
+    while (live > 0) {
+      if (!stop && cb && cb->is_cancelled && cb->is_cancelled(cb->user)) stop = true;
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+      if (e) std::rethrow_exception(e);
+    if (stop) throw std::runtime_error("failed to transcribe");
+    for (int k : redo) dec_in[k] = e_true[k];
   }
+  c->cs.fixups = fixups;
   // random draws: the first segment (file order) that drew is exact; every later one is
   // re-decoded in order from its RNG state
   size_t f = N;
@@ -781,6 +821,9 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
                     : 1;
   // every segment's PCM goes to the encode-ahead ring up front (int16 -> f32 on the GPU,
   // the same x / 32768 as src/transcribe.rs's conversion); multi-chain: per chain block
+  // the reference creates a fresh whisper state per pipeline call (src/transcribe.rs:335):
+  // decoder 0's RNG starts from its initial seed
+  c->st->reset_rng();
   if (C == 1) {
     std::vector<const int16_t*> pcm(segs.size());
     std::vector<int> ns(segs.size());

@@ -309,7 +309,7 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
   {
     // KV pool for the decode chains of every State of this context (multi-chain pipeline)
     const char* e = getenv("WDR_DECODE_CHAINS");
-    max_chains = std::max(1, std::min(8, e ? atoi(e) : 4));
+    max_chains = std::max(1, std::min(8, e ? atoi(e) : 8));
     const size_t per = (size_t)hp.n_text_layer * 18 * hp.n_text_ctx * hp.n_text_state;   // NSLOT = 18
     kv_k = DevMem(per * max_chains * 2);
     kv_v = DevMem(per * max_chains * 2);
