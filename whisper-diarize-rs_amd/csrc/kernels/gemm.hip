@@ -14,6 +14,7 @@
 #include "../prof.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace wdr {
 
@@ -567,9 +568,9 @@ __global__ __launch_bounds__(256) void k_gemv(ProjArgs a) {
 // its 4 waves split K (interleaved 32-wide steps), stream the weight fragments straight from
 // HBM into v_mfma_f32_16x16x32_f16 (B operand = 16 contiguous bytes of one weight row per
 // lane) and reduce through LDS.  N/16 workgroups instead of N/128 keep every CU streaming.
-template <int EPI, int MT, int NT>
-__global__ __launch_bounds__(256) void k_skinny(ProjArgs a) {
-  __shared__ float red[4][MT][NT][4][64];
+template <int EPI, int MT, int NT, int W = 4>
+__global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
+  __shared__ float red[W][MT][NT][4][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 16 * NT;
   const int fr = lane & 15, fk = 8 * (lane >> 4);
@@ -595,11 +596,11 @@ __global__ __launch_bounds__(256) void k_skinny(ProjArgs a) {
   // U k-steps per batch: all of a batch's fragment loads are issued before its MFMAs, so each
   // wave keeps U*(NT+MT) 16-B loads in flight instead of one dependent round trip per step
   constexpr int U = (MT + NT) <= 3 ? 8 : 4;
-  for (int k0 = wid * 32; k0 < a.K; k0 += 128 * U) {
+  for (int k0 = wid * 32; k0 < a.K; k0 += 32 * W * U) {
     f16x8 bf[U][NT], af[U][MT];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int k = k0 + u * 128;
+      const int k = k0 + u * 32 * W;
       const bool ok = k < a.K;
       const int kk = ok ? k : 0;
 #pragma unroll
@@ -628,13 +629,16 @@ __global__ __launch_bounds__(256) void k_skinny(ProjArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[wid][i][j][r][lane] = acc[i][j][r];
   __syncthreads();
-  for (int e = threadIdx.x; e < MT * NT * 4 * 64; e += 256) {
+  for (int e = threadIdx.x; e < MT * NT * 4 * 64; e += W * 64) {
     const int l = e & 63, r = (e >> 6) & 3, j = (e >> 8) % NT, i = (e >> 8) / NT;
-    const float v = red[0][i][j][r][l] + red[1][i][j][r][l] + red[2][i][j][r][l] + red[3][i][j][r][l];
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < W; ++w) v += red[w][i][j][r][l];
     const int row = i * 16 + (l >> 4) * 4 + r, col = n0 + j * 16 + (l & 15);
     epi_store<EPI>(a, row, col, v);
   }
 }
+
 
 template <int EPI>
 static void launch_epi(const ProjArgs& a, hipStream_t s) {
@@ -708,12 +712,13 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
 #undef WDR_GEMV
     }
   } else if (a.M <= 64) {
+    // 8 waves per workgroup split K (tools/skinny_bench: 5-12 % faster than 4 at M 24-64)
     const bool wide = a.N >= 4096;
-    dim3 grid(cdiv(a.N, wide ? 32 : 16)), blk(256);
     const int mt = cdiv(a.M, 16);
-#define WDR_SK(MTV)                                                                            \
-  if (wide) wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, MTV, 2>, grid, blk, 0, s, a);  \
-  else wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, MTV, 1>, grid, blk, 0, s, a);
+    dim3 grid(cdiv(a.N, wide ? 32 : 16)), blk(512);
+#define WDR_SK(MTV)                                                                                   \
+  if (wide) wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, MTV, 2, 8>, grid, blk, 0, s, a);      \
+  else wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, MTV, 1, 8>, grid, blk, 0, s, a);
     if (mt == 1) { WDR_SK(1) }
     else if (mt == 2) { WDR_SK(2) }
     else if (mt == 3) { WDR_SK(3) }

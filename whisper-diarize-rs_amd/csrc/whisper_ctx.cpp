@@ -873,7 +873,14 @@ void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool c
   launch_embed(md.tok_emb, md.dec_pos, b.rows_tok, b.rows_pos, n, d, b.xd, st);
   const float scale = 1.0f / 8.0f;
   const int ldxkv = L * 2 * d;
-  for (int l = 0; l < L; ++l) {
+  // a capture-only pass (the DTW re-forward) needs nothing past the last alignment-head layer's
+  // cross-attention: the layers after it cannot change any captured probability
+  int l_end = L;
+  if (capture && !want_logits)
+    for (l_end = L; l_end > 0 && ctx_.aheads_per_layer.size() == (size_t)L && ctx_.aheads_per_layer[l_end - 1].empty();)
+      --l_end;
+  if (l_end == 0) l_end = L;
+  for (int l = 0; l < l_end; ++l) {
     const DecLayer& e = md.dec[l];
     f16* kc = m.kc + (size_t)l * m.nslot_tot * m.seq_stride;
     f16* vc = m.vc + (size_t)l * m.nslot_tot * m.seq_stride;
@@ -918,6 +925,7 @@ void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool c
                    b.part_ml, b.attd, d};
         launch_xattn(xa, st);
     }
+    if (l_end < L && l == l_end - 1) break;   // capture-only pass: done after the last head layer
     proj(st, b.attd, d, e.w_xo, d, e.b_xo, b.xd, d, n, d, d, EPI_F32_RESID);
     launch_layernorm(b.xd, d, e.ln3_g, e.ln3_b, b.hd, d, n, d, st);
     proj(st, b.hd, d, e.w_fc1, d, e.b_fc1, b.mlpd, 4 * d, n, 4 * d, d, EPI_F16_GELU);
