@@ -33,7 +33,7 @@ sys.path.insert(0, os.path.join(ROOT, "whisper-diarize-rs_amd"))
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_F16_PEAK_TFS = 2500.0  # dense f16/bf16 MFMA
-PROF_SAMPLE = 8             # csrc/prof.cpp kEvery
+PROF_SAMPLE = 8             # csrc/prof.cpp kEvery (launches) and kStepEvery (steps)
 
 
 def parse():
@@ -195,10 +195,9 @@ def main():
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                     "launches": nl.value, "avg_launch_us": round(ms.value * 1e3 / nl.value, 3),
                     "bytes_per_launch": by.value / nl.value}
-        # 1 in PROF_SAMPLE launches of the class carries events (csrc/prof.h): scale the sampled
-        # kernel time back up for the class's share of the timed region
-        roof["sampled_1_in"] = PROF_SAMPLE
-        roof["kernel_share_of_step"] = round(PROF_SAMPLE * ms.value * 1e-3 / dt, 4)
+        # csrc/prof.h: decode steps replay hipGraphs; 1 in 8 steps runs eagerly and 1 in 8 of its
+        # launches of the class carries HIP start/stop events on its own stream
+        roof["sampling"] = "1 in %d decode steps eager, 1 in %d of their launches timed" % (PROF_SAMPLE, PROF_SAMPLE)
         tr, src = pmc_traffic(args.prof)
         if tr is not None:
             roof["traffic"] = round(tr)

@@ -16,7 +16,7 @@ import os
 from collections import defaultdict
 
 CLASSES = {
-    "gemv": ("k_gemv", "k_dgemv"),
+    "gemv": ("k_gemv", "k_dgemv", "k_mgemv"),
     "gemm": ("k_gemm<", "k_gemm(", "wdr::k_gemm"),
     "flash": ("k_flash_attn",),
     "xattn": ("k_xattn_partial", "k_xattn_combine"),

@@ -38,10 +38,25 @@ void drain_locked() {
 }
 }  // namespace
 
+std::atomic<unsigned> g_step{0}, g_tick_out{0};
+constexpr unsigned kStepEvery = 8;
+thread_local bool t_capture = false;
+thread_local bool t_step = false;   // inside a sampled (eager) decode step
+
+// every launch of the class is timed with probability 1 / (kEvery * kStepEvery): 1 in kEvery
+// inside the sampled steps, 1 in kEvery * kStepEvery elsewhere (prefill, language detection),
+// so the average is over a uniform sample of the class's launches
 bool prof_on(int cls) {
-  if (g_cls == PROF_NONE || g_cls != cls) return false;
-  return (g_tick++ % kEvery) == 0;
+  if (g_cls == PROF_NONE || g_cls != cls || t_capture) return false;
+  if (t_step) return (g_tick++ % kEvery) == 0;
+  return (g_tick_out++ % (kEvery * kStepEvery)) == 0;
 }
+bool prof_step() {
+  if (g_cls == PROF_NONE) return false;
+  return (g_step++ % kStepEvery) == 0;
+}
+void prof_capture(bool on) { t_capture = on; }
+void prof_in_step(bool on) { t_step = on; }
 int prof_class() { return g_cls; }
 
 std::mutex* launch_lock() {
@@ -83,6 +98,8 @@ int wdr_prof_set(int32_t cls) {
   wdr::g_cls = cls;
   wdr::g_broken = false;
   wdr::g_tick = 0;
+  wdr::g_step = 0;
+  wdr::g_tick_out = 0;
   wdr::g_ms = wdr::g_bytes = wdr::g_flops = 0;
   wdr::g_n = 0;
   return 0;

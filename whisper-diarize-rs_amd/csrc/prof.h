@@ -16,6 +16,13 @@ enum ProfClass : int { PROF_NONE = 0, PROF_GEMM = 1, PROF_GEMV = 2, PROF_FLASH =
 
 bool prof_on(int cls);
 int prof_class();
+// decode steps replay hipGraphs; while a class is enabled, 1 in kStepEvery steps runs its
+// kernels eagerly instead (events recorded inside a graph cannot be read on this ROCm), and
+// those launches are sampled 1 in kEvery.  prof_capture(true) around a stream capture keeps
+// event launches out of the graph.
+bool prof_step();
+void prof_capture(bool on);
+void prof_in_step(bool on);   // around the eager launches of a step prof_step() picked
 hipEvent_t prof_event();
 void prof_push(hipEvent_t a, hipEvent_t b, double bytes, double flops);
 // WDR_LAUNCH_LOCK=1: kernel launches from the decode-chain threads go through one process-wide

@@ -310,7 +310,7 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
     // KV pool for the decode chains of every State of this context (multi-chain pipeline)
     const char* e = getenv("WDR_DECODE_CHAINS");
     max_chains = std::max(1, std::min(8, e ? atoi(e) : 8));
-    const size_t per = (size_t)hp.n_text_layer * 18 * hp.n_text_ctx * hp.n_text_state;   // NSLOT = 18
+    const size_t per = (size_t)hp.n_text_layer * 21 * hp.n_text_ctx * hp.n_text_state;   // NSLOT = 21
     kv_k = DevMem(per * max_chains * 2);
     kv_v = DevMem(per * max_chains * 2);
   }
@@ -324,9 +324,9 @@ Context::~Context() {
 // ------------------------------------------------------------------ state buffers
 static constexpr int RMAX = 448;   // max decoder rows in one forward (n_text_ctx)
 static constexpr int NSEQ = 8;     // max decoder rows in one step
-static constexpr int NSLOT = 18;   // self-attention KV-cache sequences (beams + reorder scratch + DTW + lang)
+static constexpr int NSLOT = 21;   // self-attention KV-cache sequences (beams + reorder scratch + DTW + lang)
 static constexpr int DTW_SEQ = 16;  // the DTW re-forward's own sequence (runs on its own stream)
-static constexpr int LANG_SEQ = 17; // encode-ahead language detection's sequence (encode stream)
+static constexpr int LANG_SEQ = 17; // encode-ahead language detection: sequences 17..20, one per window of a batch
 static constexpr int NSPLIT = 24;  // cross-attention key chunks (1500 / 64)
 
 // Working set of a prefill: the decode stream's own (pointing at the buffers above) and the
@@ -372,7 +372,8 @@ struct State::Impl {
   // encode-ahead language detection: its own prefill working set and the 100 language
   // logits of each slot's window 0 (pinned, written by the encode stream before `ready`)
   struct LangSet {
-    DevMem xd, hd, qkvd, attd, qx, mlpd, rows_tok, rows_pos, rows_seq, part_o, part_ml, logits;
+    DevMem xd, hd, qkvd, attd, qx, mlpd, rows_tok, rows_pos, rows_seq, part_o, part_ml, logits, row_xkv;
+    const f16** h_xkv = nullptr;   // pinned [(S + 1)][kBatch] row cross-K/V bases, by first slot
   } lset;
   float* h_lang = nullptr;      // [(S + 1)][100]
   DevMem energy_d; int energy_cap = 0;
@@ -394,7 +395,7 @@ struct State::Impl {
   hipStream_t own = nullptr;  // this state's decode stream
   // dtw
   DevMem nrm, xdtw, times;
-  PrefillBufs pb_main{}, pb_dtw{}, pb_lang{};
+  PrefillBufs pb_main{}, pb_dtw{};
   struct DtwSet {
     DevMem xd, hd, qkvd, attd, qx, mlpd, rows_tok, rows_pos, rows_seq, fpart_o, fpart_ml, ml, cap, part_o, part_ml,
         nrm, xdtw, times;
@@ -419,7 +420,6 @@ struct State::Impl {
   VocabIds vids;
   struct StepGraph {
     hipGraphExec_t exec = nullptr;
-    int prof_cls = -1;
     VocabIds vids{};
   };
   std::map<int, StepGraph> graphs;   // key: R * 256 + slot (the cross-K/V pointer is baked in)
@@ -541,25 +541,34 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
                         D.mlpd.as<f16>(), D.rows_tok.as<int>(), D.rows_pos.as<int>(), D.rows_seq.as<int>(),
                         D.fpart_o.as<float>(), D.fpart_ml.as<float2>(), D.ml.as<float2>(), D.cap.as<float>(),
                         D.part_o.as<float>(), D.part_ml.as<float2>(), nullptr, nullptr};
+    // language detection: one kBatch-row step (SOT at position 0, one KV sequence and one
+    // cross-K/V slot per window) per encode-ahead batch
     Impl::LangSet& G = m.lset;
-    G.xd = DevMem((size_t)d * 4);
-    G.hd = DevMem((size_t)d * 2);
-    G.qkvd = DevMem((size_t)3 * d * 2);
-    G.attd = DevMem((size_t)d * 2);
-    G.qx = DevMem((size_t)d * 2);
-    G.mlpd = DevMem((size_t)4 * d * 2);
-    G.rows_tok = DevMem(64);
-    G.rows_pos = DevMem(64);
-    G.rows_seq = DevMem(64);
-    G.part_o = DevMem((size_t)NSPLIT * m.H * 64 * 4);
-    G.part_ml = DevMem((size_t)NSPLIT * m.H * sizeof(float2));
-    G.logits = DevMem((size_t)m.V * 4);
-    int* lrows = nullptr;
-    WDR_HIP(hipHostMalloc((void**)&lrows, 3 * RMAX * 4, hipHostMallocDefault));
-    m.pb_lang = PrefillBufs{G.xd.as<float>(), G.hd.as<f16>(), G.qkvd.as<f16>(), G.attd.as<f16>(), G.qx.as<f16>(),
-                            G.mlpd.as<f16>(), G.rows_tok.as<int>(), G.rows_pos.as<int>(), G.rows_seq.as<int>(),
-                            nullptr, nullptr, nullptr, nullptr, G.part_o.as<float>(), G.part_ml.as<float2>(),
-                            G.logits.as<float>(), lrows};
+    const int LB = kBatch;
+    G.xd = DevMem((size_t)LB * d * 4);
+    G.qkvd = DevMem((size_t)LB * 3 * d * 2);
+    G.attd = DevMem((size_t)LB * d * 2);
+    G.qx = DevMem((size_t)LB * d * 2);
+    G.mlpd = DevMem((size_t)LB * 4 * d * 2);
+    G.rows_tok = DevMem(LB * 4);
+    G.rows_pos = DevMem(LB * 4);
+    G.rows_seq = DevMem(LB * 4);
+    G.part_o = DevMem((size_t)NSPLIT * LB * m.H * 64 * 4);
+    G.part_ml = DevMem((size_t)NSPLIT * LB * m.H * sizeof(float2));
+    G.logits = DevMem((size_t)LB * m.V * 4);
+    G.row_xkv = DevMem(LB * sizeof(void*));
+    WDR_HIP(hipHostMalloc((void**)&G.h_xkv, (size_t)(kSlots + 1) * LB * sizeof(void*), hipHostMallocDefault));
+    {
+      std::vector<int> rows(3 * LB);
+      for (int r = 0; r < LB; ++r) {
+        rows[r] = ctx.vocab.sot;
+        rows[LB + r] = 0;
+        rows[2 * LB + r] = LANG_SEQ + r;
+      }
+      WDR_HIP(hipMemcpy(G.rows_tok.p, rows.data(), LB * 4, hipMemcpyHostToDevice));
+      WDR_HIP(hipMemcpy(G.rows_pos.p, rows.data() + LB, LB * 4, hipMemcpyHostToDevice));
+      WDR_HIP(hipMemcpy(G.rows_seq.p, rows.data() + 2 * LB, LB * 4, hipMemcpyHostToDevice));
+    }
     WDR_HIP(hipHostMalloc((void**)&m.h_lang, (size_t)(kSlots + 1) * 100 * 4, hipHostMallocDefault));
     int lo = 0, hi = 0;
     WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -645,7 +654,7 @@ State::~State() {
     for (int* b : m_->blk_pool) (void)hipHostFree(b);
     for (hipEvent_t e : m_->ev_pool) (void)hipEventDestroy(e);
     if (m_->ev_sync) (void)hipEventDestroy(m_->ev_sync);
-    if (m_->pb_lang.h_rows) (void)hipHostFree(m_->pb_lang.h_rows);
+    if (m_->lset.h_xkv) (void)hipHostFree(m_->lset.h_xkv);
     if (m_->h_lang) (void)hipHostFree(m_->h_lang);
     if (m_->ev_dtw) (void)hipEventDestroy(m_->ev_dtw);
     for (auto& sl : m_->slots) {
@@ -830,19 +839,28 @@ void State::top_up(int j) {
       launch_im2col_mel(ia, m.es);
     }
     encoder_body(ctx_, m, m.eb, g1 - g0, m.xkv_ring.as<f16>() + (size_t)slot0 * m.xkv_slot_elems, m.es);
-    for (int k = g0; k < g1; ++k) {
-      const int slot = k % m.S;
-      if (m.plan.detect_lang) {
-        // whisper.cpp's language detection (one SOT pass over window 0, argmax of the language
-        // logits) depends on nothing decoded, so it runs here, off the decode chain
-        const int sot = ctx_.vocab.sot;
-        prefill_on(&sot, 1, LANG_SEQ, true, false, m.pb_lang, m.es,
-                   m.xkv_ring.as<f16>() + (size_t)slot * m.xkv_slot_elems);
-        WDR_HIP(hipMemcpyAsync(m.h_lang + (size_t)slot * 100, m.pb_lang.logits + ctx_.vocab.sot + 1, 100 * 4,
+    if (m.plan.detect_lang) {
+      // whisper.cpp's language detection (one SOT pass over window 0, argmax of the language
+      // logits) depends on nothing decoded, so it runs here, off the decode chain: the batch's
+      // windows as the rows of ONE decode step, each with its own cross-K/V slot and sequence
+      Impl::LangSet& G = m.lset;
+      const int R = g1 - g0;
+      const f16** hx = G.h_xkv + (size_t)(g0 % m.S) * kBatch;   // reused >= S segments later
+      for (int r = 0; r < R; ++r) hx[r] = m.xkv_ring.as<f16>() + (size_t)((g0 + r) % m.S) * m.xkv_slot_elems;
+      WDR_HIP(hipMemcpyAsync(G.row_xkv.p, hx, R * sizeof(void*), hipMemcpyHostToDevice, m.es));
+      launch_embed(ctx_.model.tok_emb, ctx_.model.dec_pos, G.rows_tok.as<int>(), G.rows_pos.as<int>(), R, m.d,
+                   G.xd.as<float>(), m.es);
+      StepIO io{G.xd.as<float>(), G.qkvd.as<f16>(), G.attd.as<f16>(), G.qx.as<f16>(), G.mlpd.as<f16>(),
+                G.logits.as<float>(), m.V, G.part_o.as<float>(), G.part_ml.as<float2>(), G.rows_tok.as<int>(),
+                G.rows_pos.as<int>(), G.rows_seq.as<int>(), m.kc, m.vc, (long long)m.nslot_tot * m.seq_stride,
+                m.seq_stride, nullptr, G.row_xkv.as<const f16*>()};
+      decode_step_layers(ctx_, io, R, m.es);
+      for (int r = 0; r < R; ++r)
+        WDR_HIP(hipMemcpyAsync(m.h_lang + (size_t)((g0 + r) % m.S) * 100,
+                               G.logits.as<float>() + (size_t)r * m.V + ctx_.vocab.sot + 1, 100 * 4,
                                hipMemcpyDeviceToHost, m.es));
-      }
-      WDR_HIP(hipEventRecord(m.slots[slot].ready, m.es));
     }
+    for (int k = g0; k < g1; ++k) WDR_HIP(hipEventRecord(m.slots[k % m.S].ready, m.es));
     m.plan.next_enq = g1;
     times.windows += g1 - g0;
   }
@@ -1055,22 +1073,26 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
     m.h_rows[2 * RMAX + i] = seqs[i];
   }
   memcpy(m.h_ctl, ctl, R * sizeof(LogitsCtl));
-  if (prof_class() != PROF_NONE || getenv("WDR_NO_GRAPH")) {
+  const bool sampled = prof_step();
+  if (sampled || getenv("WDR_NO_GRAPH")) {
     // live per-kernel HIP-event timing cannot read events recorded inside a graph on this
-    // ROCm: run the same kernels eagerly while a profiling class is active
-    decoder_step(toks, seqs, pos, R);
+    // ROCm: a sampled step runs the same kernels eagerly (prof.h)
+    prof_in_step(sampled);
+    try {
+      decoder_step(toks, seqs, pos, R);
+    } catch (...) {
+      prof_in_step(false);
+      throw;
+    }
+    prof_in_step(false);
     run_logits(R, ctl, out, nullptr);
     if (K > 0) logits_topk(R, K, cands);
     return;
   }
   Impl::StepGraph& g = m.graphs[(K << 16) + R * 256 + m.cur];
-  if (!g.exec || g.prof_cls != prof_class()) {
-    if (g.exec) {
-      (void)hipGraphExecDestroy(g.exec);
-      g.exec = nullptr;
-    }
-    g.prof_cls = prof_class();
+  if (!g.exec) {
     hipGraph_t graph;
+    prof_capture(true);
     WDR_HIP(hipStreamBeginCapture(s_, hipStreamCaptureModeThreadLocal));
     WDR_HIP(hipMemcpyAsync(m.rows_tok.p, m.h_rows, R * 4, hipMemcpyHostToDevice, s_));
     WDR_HIP(hipMemcpyAsync(m.rows_pos.p, m.h_rows + RMAX, R * 4, hipMemcpyHostToDevice, s_));
@@ -1085,6 +1107,7 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
                          m.beamc.as<BeamCand>(), s_);
       WDR_HIP(hipMemcpyAsync(m.h_beam, m.beamc.p, (size_t)R * K * sizeof(BeamCand), hipMemcpyDeviceToHost, s_));
     }
+    prof_capture(false);
     WDR_HIP(hipStreamEndCapture(s_, &graph));
     WDR_HIP(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
     WDR_HIP(hipGraphDestroy(graph));
@@ -2253,8 +2276,17 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
                           m.tokout.as<TokOut>(), m.s);
     WDR_HIP(hipMemcpyAsync(m.h_tok, m.tokout.p, R * sizeof(TokOut), hipMemcpyDeviceToHost, m.s));
   };
-  if (prof_class() != PROF_NONE || getenv("WDR_NO_GRAPH")) {
-    body();
+  const bool sampled = prof_step();
+  if (sampled || getenv("WDR_NO_GRAPH")) {
+    // sampled step for live kernel timing (prof.h), or graphs disabled
+    prof_in_step(sampled);
+    try {
+      body();
+    } catch (...) {
+      prof_in_step(false);
+      throw;
+    }
+    prof_in_step(false);
   } else {
     Impl::G& g = m.graphs[R];
     if (g.exec && memcmp(&g.vids, &vids, sizeof(VocabIds)) != 0) {
@@ -2263,8 +2295,10 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
     }
     if (!g.exec) {
       hipGraph_t graph;
+      prof_capture(true);
       WDR_HIP(hipStreamBeginCapture(m.s, hipStreamCaptureModeThreadLocal));
       body();
+      prof_capture(false);
       WDR_HIP(hipStreamEndCapture(m.s, &graph));
       WDR_HIP(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
       WDR_HIP(hipGraphDestroy(graph));
