@@ -1,0 +1,119 @@
+// Encoder GEMM microbenchmark (large-v3, 4 windows batched: M = 6000 rows): per-launch time and
+// TFLOP/s of the production launch_proj path at the encoder / cross-K/V shapes, uniform random
+// f16 operands (MI355X_MICROARCH.md: zero-filled operands read high).
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/gemm_bench.cpp -Lwhisper-diarize-rs_amd -lwdr
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <cmath>
+
+#include "../whisper-diarize-rs_amd/csrc/common.h"
+#include "../whisper-diarize-rs_amd/csrc/kernels/kernels.h"
+
+using namespace wdr;
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e = (x);                                                        \
+    if (e != hipSuccess) {                                                     \
+      printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__);          \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+__global__ void k_rand(f16* p, long long n, unsigned seed) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    unsigned x = (unsigned)i * 2654435761u + seed;
+    x ^= x >> 13;
+    x *= 0x5bd1e995u;
+    x ^= x >> 15;
+    p[i] = (f16)(((x & 0xffff) / 65536.0f - 0.5f) * 0.2f);
+  }
+}
+
+int main(int argc, char** argv) {
+  const int M = argc > 1 ? atoi(argv[1]) : 6000;
+  struct Shape {
+    const char* name;
+    int N, K, epi;
+  } shapes[] = {{"qkv   3d x d", 3840, 1280, EPI_F16},        {"o      d x d resid", 1280, 1280, EPI_F32_RESID},
+                {"fc1  4d x d gelu", 5120, 1280, EPI_F16_GELU}, {"fc2   d x 4d resid", 1280, 5120, EPI_F32_RESID},
+                {"xkv  64d x d", 81920, 1280, EPI_F16}};
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  f16 *A, *W;
+  float *out, *bias;
+  CK(hipMalloc(&A, (size_t)M * 5120 * 2));
+  CK(hipMalloc(&W, (size_t)81920 * 1280 * 2));
+  CK(hipMalloc(&out, (size_t)M * 81920 * 4 / 2 + (size_t)M * 5120 * 4));
+  CK(hipMalloc(&bias, 81920 * 4));
+  CK(hipMemset(bias, 0, 81920 * 4));
+  hipLaunchKernelGGL(k_rand, dim3(4096), dim3(256), 0, s, A, (long long)M * 5120, 1u);
+  hipLaunchKernelGGL(k_rand, dim3(4096), dim3(256), 0, s, W, (long long)81920 * 1280, 2u);
+  CK(hipMemsetAsync(out, 0, (size_t)M * 5120 * 4, s));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  std::vector<float> r1, r2;
+  for (const Shape& sh : shapes) {
+    for (int variant = 0; variant < 2; ++variant) {
+      // variant 0: k_gemm (register staging, WDR_GEMM1), 1: k_gemm2 (LDS-DMA staging)
+      if (variant == 0) setenv("WDR_GEMM1", "1", 1);
+      else unsetenv("WDR_GEMM1");
+      // EPI_F32 into a zeroed buffer for the cross-check (the timed runs use the real epilogue)
+      const size_t on = (size_t)M * sh.N;
+      if (sh.N <= 5120) {
+        CK(hipMemsetAsync(out, 0, on * 4, s));
+        ProjArgs c{A, sh.K, W, sh.K, bias, out, sh.N, nullptr, 0, M, sh.N, sh.K, EPI_F32};
+        launch_proj(c, s);
+        std::vector<float>& r = variant == 0 ? r1 : r2;
+        r.resize(on);
+        CK(hipMemcpyAsync(r.data(), out, on * 4, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+      }
+      ProjArgs p{A, sh.K, W, sh.K, bias, out, sh.N, nullptr, 0, M, sh.N, sh.K, sh.epi};
+      for (int i = 0; i < 3; ++i) launch_proj(p, s);
+      const int reps = 20;
+      CK(hipEventRecord(a, s));
+      for (int i = 0; i < reps; ++i) launch_proj(p, s);
+      CK(hipEventRecord(b, s));
+      CK(hipEventSynchronize(b));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, a, b));
+      const double us = ms * 1e3 / reps, tf = 2.0 * M * sh.N * sh.K / (us * 1e-6) / 1e12;
+      printf("%-20s %s M=%d N=%5d K=%4d  %9.1f us  %7.1f TFLOP/s\n", sh.name, variant ? "gemm2" : "gemm ", M, sh.N,
+             sh.K, us, tf);
+    }
+    if (sh.N <= 5120) {
+      size_t nd = 0;
+      double md = 0;
+      for (size_t i = 0; i < r1.size(); ++i) {
+        const double dd = std::fabs((double)r1[i] - r2[i]);
+        if (dd > 0) ++nd;
+        if (dd > md) md = dd;
+      }
+      printf("   cross-check: %zu of %zu differ, max |diff| %.3g\n", nd, r1.size(), md);
+    }
+  }
+  {
+    // encoder self-attention of the same batch: nb = M / 1500 windows x 20 heads x 1500^2
+    const int nb = M / 1500, d = 1280;
+    f16* att;
+    CK(hipMalloc(&att, (size_t)M * d * 2));
+    const long long bs = 1500ll * 3 * d, obs = 1500ll * d;
+    FlashArgs fa{A, 3 * d, bs, A + d, 3 * d, bs, A + 2 * d, 3 * d, bs, att, d, obs, nullptr, 1500, 1500, 20, 0, 0.125f};
+    for (int i = 0; i < 3; ++i) launch_flash_attn(fa, nb, s);
+    const int reps = 20;
+    CK(hipEventRecord(a, s));
+    for (int i = 0; i < reps; ++i) launch_flash_attn(fa, nb, s);
+    CK(hipEventRecord(b, s));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    const double us = ms * 1e3 / reps, tf = 4.0 * nb * 20 * 1500.0 * 1500.0 * 64 / (us * 1e-6) / 1e12;
+    printf("%-20s       nb=%d T=1500 H=20      %9.1f us  %7.1f TFLOP/s\n", "flash attention", nb, us, tf);
+  }
+  return 0;
+}

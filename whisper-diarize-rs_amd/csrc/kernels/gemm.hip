@@ -145,6 +145,106 @@ __global__ __launch_bounds__(256, 2) void k_gemm(ProjArgs a) {
       }
 }
 
+
+// ---------------------------------------------------------------- MFMA GEMM, LDS-DMA staged
+// The encoder / cross-K/V GEMM (M > 64): 128x128 block tile, BK = 64, 4 waves of 64x64
+// (2x2 v_mfma_f32_32x32x16_f16 per 16-deep k-step, the same k order as k_gemm), operand tiles
+// staged global -> LDS by global_load_lds (16 B per lane, no VGPR round trip) into two buffers:
+// the loads of tile k+1 fly while tile k is multiplied.  LDS images are lane-linear (what the
+// DMA writes: 1 KB per wave-instruction = 8 rows x 128 B); bank conflicts of the fragment reads
+// are removed by an XOR swizzle applied on the global SOURCE address: logical 16-B chunk c of
+// row r sits at chunk c ^ ((r >> 1) & 7).  Workgroups are remapped so that each XCD owns a
+// contiguous run of tiles (row-major over N tiles): the A rows and B columns a tile reuses stay
+// in that XCD's L2.
+constexpr int G2_BK = 64;
+__device__ __forceinline__ int g2_swz(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void k_gemm2(ProjArgs a) {
+  __shared__ __attribute__((aligned(16))) f16 lds[2][2][GB_M * G2_BK];   // [buf][A,B][128 x 64]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // XCD-aware tile order (bijective for any tile count)
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+  const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int ntn = a.N / GB_N;
+  const int bm = id / ntn, bn = id % ntn;
+  const int wr = wid >> 1, wc = wid & 1;
+  // this wave's 4 DMA blocks per operand: block j = wid*4 + jj covers rows 8*j .. 8*j + 7
+  const f16* ga[4];
+  const f16* gb[4];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    const int row = (wid * 4 + jj) * 8 + (lane >> 3);
+    const int c = g2_swz(row, lane & 7);
+    int gm = bm * GB_M + row;
+    gm = gm < a.M ? gm : a.M - 1;
+    ga[jj] = a.A + (size_t)gm * a.lda + c * 8;
+    gb[jj] = a.B + (size_t)(bn * GB_N + row) * a.ldb + c * 8;
+  }
+  auto stage = [&](int buf, int k0) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      __builtin_amdgcn_global_load_lds((const void*)(ga[jj] + k0), (void*)&lds[buf][0][(wid * 4 + jj) * 512], 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(gb[jj] + k0), (void*)&lds[buf][1][(wid * 4 + jj) * 512], 16, 0, 0);
+    }
+  };
+  const int nk = a.K / G2_BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int fr = lane & 31, fh = lane >> 5;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * G2_BK);
+    const f16* As = lds[cur][0];
+    const f16* Bs = lds[cur][1];
+#pragma unroll
+    for (int ks = 0; ks < G2_BK / 16; ++ks) {
+      const int c = 2 * ks + fh;   // logical 16-B chunk of this lane's 8 k values
+      f16x8 af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = wr * 64 + i * 32 + fr;
+        af[i] = *(const f16x8*)(As + r * G2_BK + g2_swz(r, c) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wc * 64 + j * 32 + fr;
+        bf[j] = *(const f16x8*)(Bs + r * G2_BK + g2_swz(r, c) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  const int h = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = bm * GB_M + wr * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int col = bn * GB_N + wc * 64 + j * 32 + fr;
+        epi_store<EPI>(a, row, col, acc[i][j][r]);
+      }
+}
+
 // ---------------------------------------------------------------- GEMV (M <= 8)
 // Grid-stride over output rows (one weight row per wave per iteration), 16-B weight loads,
 // v_dot2_f32_f16.  With the fused LayerNorm prologue (LN, K <= 1536) every wave normalises
@@ -640,6 +740,12 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
 }
 
 
+// WDR_GEMM1=1: every M > 64 projection on k_gemm (A/B runs of tools/gemm_bench); read per call
+static bool gemm1_forced() {
+  const char* e = getenv("WDR_GEMM1");
+  return e && atoi(e) != 0;
+}
+
 template <int EPI>
 static void launch_epi(const ProjArgs& a, hipStream_t s) {
   const int ob = (EPI == EPI_F32_RESID || EPI == EPI_F32 || EPI == EPI_F32_GELU_POS) ? 4 : 2;
@@ -724,6 +830,11 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
     else if (mt == 3) { WDR_SK(3) }
     else { WDR_SK(4) }
 #undef WDR_SK
+  } else if (a.K % G2_BK == 0 && a.N <= 4096 && !gemm1_forced()) {
+    // LDS-DMA GEMM where it measured faster (tools/gemm_bench, M = 6000: qkv -5 %, o -11 %,
+    // fc2 -23 %; fc1 and the 82k-column cross-K/V GEMM stay on k_gemm, +8 % / +7 % there)
+    dim3 grid((a.N / GB_N) * cdiv(a.M, GB_M));
+    wdr_launch(PROF_GEMM, bytes, flops, k_gemm2<EPI>, grid, dim3(256), 0, s, a);
   } else {
     dim3 grid(a.N / GB_N, cdiv(a.M, GB_M));
     wdr_launch(PROF_GEMM, bytes, flops, k_gemm<EPI>, grid, dim3(256), 0, s, a);
