@@ -67,6 +67,34 @@ def pmc_traffic(cls):
         os.path.relpath(files[-1], ROOT)
 
 
+# BASELINE.md §3 units of work: encoder + cross-K/V per 30-s window (MFMA flops) and the decode
+# step's bytes split into the decoder weights (streamed once per launched step, shared by its
+# rows) and one row's cross-K/V (read per row).
+WORK = {"large-v3": {"enc_flops": 2.589e12, "dec_weight_bytes": 1.601e9, "xkv_row_bytes": 0.246e9},
+        "base.en": {"enc_flops": 96.8e9, "dec_weight_bytes": 97.1e6, "xkv_row_bytes": 18.4e6}}
+
+
+def pipeline_roofline(model, times, t_wall):
+    """Whole-pipeline roofline of one step (BASELINE.md §3 'roofline.achieved = T_roof / T_wall'
+    with the schedule actually used): encoder windows at the dense f16 MFMA peak; decode steps
+    (each launched step streams the decoder weights once, each row its cross-K/V), prompt
+    prefills and DTW re-forwards (one decode step of bytes each) at the HBM peak."""
+    w = WORK.get(model)
+    if w is None:
+        return None
+    windows, steps, prefills = times["windows"], times["decode_steps"], times["prefills"]
+    launches = times.get("batch_launches", 0) + (steps - times.get("batch_rows", 0))
+    t_enc = windows * w["enc_flops"] / (MFMA_F16_PEAK_TFS * 1e12)
+    t_dec = (launches * w["dec_weight_bytes"] + steps * w["xkv_row_bytes"]) / (HBM_PEAK_GBS * 1e9)
+    step_bytes = w["dec_weight_bytes"] + w["xkv_row_bytes"]
+    t_pre = (prefills + windows) * step_bytes / (HBM_PEAK_GBS * 1e9)   # prompt prefills + DTW re-forwards
+    t_roof = t_enc + t_dec + t_pre
+    return {"t_roof_s": round(t_roof, 4), "t_wall_s": round(t_wall, 4), "frac": round(t_roof / t_wall, 4),
+            "terms_s": {"encoder_mfma": round(t_enc, 4), "decode_steps_hbm": round(t_dec, 4),
+                        "prefill_dtw_hbm": round(t_pre, 4)},
+            "step_launches": launches}
+
+
 def cpu_baseline(model, segs, budget_s):
     """The CPU restatement (oracle/, numpy f32 with f16-rounded weights/activations as ggml)
     on a bounded prefix of the same workload.  Returns (xRT, sample description, threads)."""
@@ -203,6 +231,8 @@ def main():
             roof["traffic"] = round(tr)
             roof["traffic_source"] = src
 
+    pipe = pipeline_roofline(args.model, times, dt / args.steps)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ctx.close()
@@ -225,7 +255,7 @@ def main():
                                     "downstream (synthetic pin)") % (args.model, shard_s, len(segs), audio_s),
                        "model": args.model, "global_batch": len(segs) * world, "seq_len": 1500,
                        "parallelism": "dp%d (segment shards per rank)" % world},
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "pipeline_roofline": pipe, "cpu_baseline": cpu,
             "stages_s": {k: round(v, 3) for k, v in times.items() if isinstance(v, float)},
             "counts": {k: v for k, v in times.items() if isinstance(v, int)},
             "segmentation": ({"stage": "pyannote", "s_per_step": round(vad_t[0] / args.steps, 4), "segments": vad_t[1],
