@@ -114,6 +114,15 @@ int main() {
         }
       }, s, 20);
       printf("   M=%2d launch_proj      %8.2f us  %7.2f TB/s\n", M, t * 1e3 / L, mb / (t * 1e3 / L) / 1e3);
+      setenv("WDR_SKINNY_MSPLIT", "0", 1);
+      const float t0 = time_graph([&] {
+        for (int l = 0; l < L; ++l) {
+          ProjArgs a{x16, sh.K, W[l], sh.K, bias, out, sh.N, nullptr, 0, M, sh.N, sh.K, sh.epi};
+          launch_proj(a, s);
+        }
+      }, s, 20);
+      unsetenv("WDR_SKINNY_MSPLIT");
+      printf("   M=%2d no row split     %8.2f us\n", M, t0 * 1e3 / L);
     }
     for (int l = 0; l < L; ++l) CK(hipFree(W[l]));
   }

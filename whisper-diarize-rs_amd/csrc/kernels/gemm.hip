@@ -673,6 +673,7 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
   __shared__ float red[W][MT][NT][4][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 16 * NT;
+  const int m0 = blockIdx.y * 16 * MT;   // row tiles split over gridDim.y workgroups (narrow N)
   const int fr = lane & 15, fk = 8 * (lane >> 4);
   f32x4 acc[MT][NT];
 #pragma unroll
@@ -682,7 +683,7 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
   const f16* arow[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
-    int m = i * 16 + fr;
+    int m = m0 + i * 16 + fr;
     m = m < a.M ? m : a.M - 1;
     arow[i] = a.A + (size_t)m * a.lda + fk;
   }
@@ -734,11 +735,17 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < W; ++w) v += red[w][i][j][r][l];
-    const int row = i * 16 + (l >> 4) * 4 + r, col = n0 + j * 16 + (l & 15);
+    const int row = m0 + i * 16 + (l >> 4) * 4 + r, col = n0 + j * 16 + (l & 15);
     epi_store<EPI>(a, row, col, v);
   }
 }
 
+
+// WDR_SKINNY_MSPLIT=0: narrow skinny GEMMs keep all row tiles in one workgroup (A/B runs)
+static bool skinny_msplit_off() {
+  const char* e = getenv("WDR_SKINNY_MSPLIT");
+  return e && atoi(e) == 0;
+}
 
 // WDR_GEMM1=1: every M > 64 projection on k_gemm (A/B runs of tools/gemm_bench); read per call
 static bool gemm1_forced() {
@@ -817,6 +824,12 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
       else { WDR_GEMV(8) }
 #undef WDR_GEMV
     }
+  } else if (a.M <= 64 && a.N <= 2048 && !skinny_msplit_off()) {
+    // narrow N (o / xq / xo / fc2: 80 column tiles): one 16-row tile per workgroup, the row
+    // tiles of a column tile on one XCD (gridDim.x % 8 == 0 there) so its weights hit that L2
+    const int mt = cdiv(a.M, 16);
+    dim3 grid(cdiv(a.N, 16), mt), blk(512);
+    wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, 1, 1, 8>, grid, blk, 0, s, a);
   } else if (a.M <= 64) {
     // 8 waves per workgroup split K (tools/skinny_bench: 5-12 % faster than 4 at M 24-64)
     const bool wide = a.N >= 4096;
