@@ -668,9 +668,14 @@ __global__ __launch_bounds__(256) void k_gemv(ProjArgs a) {
 // its 4 waves split K (interleaved 32-wide steps), stream the weight fragments straight from
 // HBM into v_mfma_f32_16x16x32_f16 (B operand = 16 contiguous bytes of one weight row per
 // lane) and reduce through LDS.  N/16 workgroups instead of N/128 keep every CU streaming.
-template <int EPI, int MT, int NT, int W = 4>
+// LN: the A rows are LayerNorm(ln_x rows) -- each workgroup normalises its 16*MT rows into LDS
+// first (k_layernorm's arithmetic, so the f16 operands are bit-identical to the unfused path;
+// row stride K + 8 halfs keeps the 16-row fragment reads conflict-free) -- which removes the
+// separate LayerNorm launch and its f16 round trip from the prefill / DTW passes.
+template <int EPI, int MT, int NT, int W = 4, bool LN = false>
 __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
   __shared__ float red[W][MT][NT][4][64];
+  extern __shared__ __attribute__((aligned(16))) f16 xln[];   // LN: [16*MT][K + 8]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 16 * NT;
   const int m0 = blockIdx.y * 16 * MT;   // row tiles split over gridDim.y workgroups (narrow N)
@@ -680,12 +685,59 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int lds_ld = a.K + 8;
+  if constexpr (LN) {
+    const int d = a.K;
+    for (int rr = wid; rr < 16 * MT; rr += W) {
+      int row = m0 + rr;
+      row = row < a.M ? row : a.M - 1;
+      const float* xr = a.ln_x + (long long)row * a.ldln;
+      float v[5][4], gg[5][4], bb[5][4];
+      float sm = 0.f;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const int c = lane * 4 + j * 256;
+        const bool ok = c < d;
+        const int cc = ok ? c : 0;
+        const float4 q = *(const float4*)(xr + cc);
+        const float4 g4 = *(const float4*)(a.ln_g + cc);
+        const float4 b4 = *(const float4*)(a.ln_b + cc);
+        v[j][0] = ok ? q.x : 0.f; v[j][1] = ok ? q.y : 0.f; v[j][2] = ok ? q.z : 0.f; v[j][3] = ok ? q.w : 0.f;
+        gg[j][0] = g4.x; gg[j][1] = g4.y; gg[j][2] = g4.z; gg[j][3] = g4.w;
+        bb[j][0] = b4.x; bb[j][1] = b4.y; bb[j][2] = b4.z; bb[j][3] = b4.w;
+        sm += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+      }
+      sm = wave_sum(sm);
+      const float mean = sm / d;
+      float s2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+        if (lane * 4 + j * 256 < d)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float t = v[j][e] - mean;
+            s2 += t * t;
+          }
+      s2 = wave_sum(s2);
+      const float scale = 1.0f / sqrtf(s2 / d + 1e-5f);
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const int c = lane * 4 + j * 256;
+        if (c >= d) continue;
+        f16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (f16)((v[j][e] - mean) * scale * gg[j][e] + bb[j][e]);
+        *(f16x4*)(xln + rr * lds_ld + c) = o;
+      }
+    }
+    __syncthreads();
+  }
   const f16* arow[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
     int m = m0 + i * 16 + fr;
     m = m < a.M ? m : a.M - 1;
-    arow[i] = a.A + (size_t)m * a.lda + fk;
+    arow[i] = LN ? xln + (i * 16 + fr) * lds_ld + fk : a.A + (size_t)m * a.lda + fk;
   }
   const f16* brow[NT];
 #pragma unroll
@@ -829,14 +881,20 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
     // tiles of a column tile on one XCD (gridDim.x % 8 == 0 there) so its weights hit that L2
     const int mt = cdiv(a.M, 16);
     dim3 grid(cdiv(a.N, 16), mt), blk(512);
-    wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, 1, 1, 8>, grid, blk, 0, s, a);
+    if (a.ln_x) wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, 1, 1, 8, true>, grid, blk,
+                           (uint32_t)16 * (a.K + 8) * 2, s, a);
+    else wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, 1, 1, 8>, grid, blk, 0, s, a);
   } else if (a.M <= 64) {
     // 8 waves per workgroup split K (tools/skinny_bench: 5-12 % faster than 4 at M 24-64)
     const bool wide = a.N >= 4096;
     const int mt = cdiv(a.M, 16);
     dim3 grid(cdiv(a.N, wide ? 32 : 16)), blk(512);
-#define WDR_SK(MTV)                                                                                   \
-  if (wide) wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, MTV, 2, 8>, grid, blk, 0, s, a);      \
+    const uint32_t lds = a.ln_x ? (uint32_t)16 * mt * (a.K + 8) * 2 : 0;
+#define WDR_SK(MTV)                                                                                             \
+  if (a.ln_x) {                                                                                                 \
+    if (wide) wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, MTV, 2, 8, true>, grid, blk, lds, s, a);      \
+    else wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, MTV, 1, 8, true>, grid, blk, lds, s, a);           \
+  } else if (wide) wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, MTV, 2, 8>, grid, blk, 0, s, a);         \
   else wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, MTV, 1, 8>, grid, blk, 0, s, a);
     if (mt == 1) { WDR_SK(1) }
     else if (mt == 2) { WDR_SK(2) }
@@ -862,6 +920,7 @@ void launch_proj(const ProjArgs& a, hipStream_t s) {
     WDR_CHECK(a.K % GB_K == 0, "gemm: K must be a multiple of 32");
   } else if (a.M > 8) {
     WDR_CHECK(a.K % 32 == 0, "skinny gemm: K must be a multiple of 32");
+    WDR_CHECK(!a.ln_x || (a.K <= 1280 && a.K % 4 == 0 && a.M <= 32), "skinny LN prologue: K <= 1280, M <= 32");
   } else if (a.ln_x) {
     WDR_CHECK(a.K <= 1536 && a.K % 8 == 0, "gemv LN prologue: K must be <= 1536");
   }

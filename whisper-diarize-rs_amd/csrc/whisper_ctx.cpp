@@ -891,6 +891,18 @@ void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool c
   launch_embed(md.tok_emb, md.dec_pos, b.rows_tok, b.rows_pos, n, d, b.xd, st);
   const float scale = 1.0f / 8.0f;
   const int ldxkv = L * 2 * d;
+  // the projection's input rows are LayerNorm(x): fused into the skinny GEMM for 8 < n <= 32
+  // rows (bit-identical to k_layernorm + GEMM), else the separate LayerNorm into b.hd
+  auto ln_into = [&](ProjArgs& p, const float* x, const float* g, const float* bb) {
+    if (n > NSEQ && n <= 32 && d <= 1280) {
+      p.ln_x = x;
+      p.ldln = d;
+      p.ln_g = g;
+      p.ln_b = bb;
+    } else {
+      launch_layernorm(x, d, g, bb, b.hd, d, n, d, st);
+    }
+  };
   // a capture-only pass (the DTW re-forward) needs nothing past the last alignment-head layer's
   // cross-attention: the layers after it cannot change any captured probability
   int l_end = L;
@@ -902,9 +914,10 @@ void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool c
     const DecLayer& e = md.dec[l];
     f16* kc = m.kc + (size_t)l * m.nslot_tot * m.seq_stride;
     f16* vc = m.vc + (size_t)l * m.nslot_tot * m.seq_stride;
-    launch_layernorm(b.xd, d, e.ln1_g, e.ln1_b, b.hd, d, n, d, st);
-    // Q to qkvd, K / V straight into this sequence's cache rows 0..n-1 (the epilogue scatter)
+    // Q to qkvd, K / V straight into this sequence's cache rows 0..n-1 (the epilogue scatter);
+    // 8 < n <= 32 rows: the LayerNorm runs inside the skinny GEMM (fused prologue)
     ProjArgs qa{b.hd, d, e.w_qkv, d, e.b_qkv, b.qkvd, 3 * d, nullptr, 0, n, 3 * d, d, EPI_QKV_CACHE};
+    ln_into(qa, b.xd, e.ln1_g, e.ln1_b);
     qa.kc = kc;
     qa.vc = vc;
     qa.seq_stride = m.seq_stride;
@@ -917,8 +930,11 @@ void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool c
     FlashArgs sa{b.qkvd, 3 * d, 0, ks, d, 0, vs, d, 0, b.attd, d, 0, nullptr, n, n, hp.n_text_head, 1, scale};
     launch_flash_attn(sa, 1, st);
     proj(st, b.attd, d, e.w_o, d, e.b_o, b.xd, d, n, d, d, EPI_F32_RESID);
-    launch_layernorm(b.xd, d, e.ln2_g, e.ln2_b, b.hd, d, n, d, st);
-    proj(st, b.hd, d, e.w_xq, d, e.b_xq, b.qx, d, n, d, d, EPI_F16);
+    {
+      ProjArgs xq{b.hd, d, e.w_xq, d, e.b_xq, b.qx, d, nullptr, 0, n, d, d, EPI_F16};
+      ln_into(xq, b.xd, e.ln2_g, e.ln2_b);
+      launch_proj(xq, st);
+    }
     const f16* xk = xkv_base + (size_t)l * 2 * d;
     const f16* xv = xk + d;
     const bool cap_layer = capture && !ctx_.aheads_per_layer.empty() && !ctx_.aheads_per_layer[l].empty();
@@ -945,8 +961,11 @@ void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool c
     }
     if (l_end < L && l == l_end - 1) break;   // capture-only pass: done after the last head layer
     proj(st, b.attd, d, e.w_xo, d, e.b_xo, b.xd, d, n, d, d, EPI_F32_RESID);
-    launch_layernorm(b.xd, d, e.ln3_g, e.ln3_b, b.hd, d, n, d, st);
-    proj(st, b.hd, d, e.w_fc1, d, e.b_fc1, b.mlpd, 4 * d, n, 4 * d, d, EPI_F16_GELU);
+    {
+      ProjArgs f1{b.hd, d, e.w_fc1, d, e.b_fc1, b.mlpd, 4 * d, nullptr, 0, n, 4 * d, d, EPI_F16_GELU};
+      ln_into(f1, b.xd, e.ln3_g, e.ln3_b);
+      launch_proj(f1, st);
+    }
     proj(st, b.mlpd, 4 * d, e.w_fc2, 4 * d, e.b_fc2, b.xd, d, n, d, 4 * d, EPI_F32_RESID);
   }
   if (want_logits) {
