@@ -46,3 +46,22 @@ def test_chains_equal_single_chain(name, seconds, fallback, diarize):
         assert [s["text"] for s in got] == [s["text"] for s in ref], chains
         assert got == ref, chains
     ctx.close()
+
+
+@pytest.mark.parametrize("name,seconds", [("tiny-test", 120.0), ("large-v3", 110.0)])
+def test_sixteen_chains_equal_single_chain(name, seconds, monkeypatch):
+    """16 decode chains: batched steps of 9..16 rows (k_mgemv 16-row shapes, the fc2 step split
+    into two 8-row launches) must still give the one-chain result exactly."""
+    monkeypatch.setenv("WDR_DECODE_CHAINS", "16")   # KV pool sized for 16 chains at creation
+    syn = wdr.Synthetic(weight_std=0.02, emb_std=0.5, force_len_rate=3.3, disable_fallback=True)
+    ctx = wdr.WhisperContext(name, synthetic=syn)
+    pcm, spurts = synth_speech(seconds, seed=5, n_speakers=2)
+    segs = _segs(pcm, spurts)
+    assert len(segs) >= 16
+    opts = wdr.TranscribeOptions(lang="auto", advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    ref, lang1 = _run(ctx, segs, opts, 1)
+    got, lang = _run(ctx, segs, opts, 16)
+    assert ctx.stage_times()["chains"] == 16
+    assert lang == lang1
+    assert got == ref
+    ctx.close()

@@ -80,6 +80,9 @@ struct ProjArgs {
   // EPI_QKV_CACHE
   f16* kc = nullptr; f16* vc = nullptr; long long seq_stride = 0; const int* row_seq = nullptr;
   const int* row_pos = nullptr; int d = 0;
+  // decode-step rows (up to 16, the multi-chain batched step): stay on the GEMV kernels, whose
+  // per-row arithmetic does not depend on the row count
+  int step_rows = 0;
 };
 void launch_proj(const ProjArgs& a, hipStream_t s);   // picks GEMV (M<=8) or MFMA GEMM
 

@@ -403,7 +403,7 @@ __global__ __launch_bounds__(64) void k_xattn_combine(XAttnArgs a) {
 }
 
 void launch_xattn(const XAttnArgs& a, hipStream_t s) {
-  WDR_CHECK(a.R >= 1 && a.R <= XA_RMAX, "cross-attention decode: R out of range");
+  WDR_CHECK(a.R >= 1 && a.R <= (a.row_k ? 64 : XA_RMAX), "cross-attention decode: R out of range");
   const int nsplit = cdiv(a.Tk, XA_KC);
   WDR_CHECK(nsplit == 24, "cross-attention decode expects 1500 keys");
   if (a.row_k) {

@@ -810,7 +810,22 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
   const int ob = (EPI == EPI_F32_RESID || EPI == EPI_F32 || EPI == EPI_F32_GELU_POS) ? 4 : 2;
   const double bytes = (double)a.N * a.K * 2 + (double)a.M * a.K * 2 + (double)a.M * a.N * ob;
   const double flops = 2.0 * a.M * a.N * a.K;
-  if (a.M <= 8) {
+  if (a.step_rows && a.M > 8 && !a.ln_x && a.K > 3072) {
+    // 9..16 step rows through a K > 3072 projection (fc2): two 8-row launches -- the 16-row
+    // shape would spill its activation registers; per-row results are unchanged
+    ProjArgs lo = a, hi = a;
+    lo.M = 8;
+    hi.M = a.M - 8;
+    hi.A = a.A + (size_t)8 * a.lda;
+    const int ob = (EPI == EPI_F32_RESID || EPI == EPI_F32 || EPI == EPI_F32_GELU_POS) ? 4 : 2;
+    hi.out = (char*)a.out + (size_t)8 * a.ldo * ob;
+    if (a.row_seq) hi.row_seq = a.row_seq + 8;
+    if (a.row_pos) hi.row_pos = a.row_pos + 8;
+    launch_epi<EPI>(lo, s);
+    launch_epi<EPI>(hi, s);
+    return;
+  }
+  if (a.M <= 8 || (a.step_rows && a.M <= 16)) {
     const int nwg = std::min(cdiv(a.N, 4), 1024);
     dim3 grid(nwg), blk(256);
     const bool ln = a.ln_x != nullptr;
@@ -844,7 +859,7 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
       const int R = a.N >= 1024 ? 2 : 1;
       dim3 g2(cdiv(a.N, 4 * R));
       const bool m4 = a.M <= 4;
-      const uint32_t lds = ln ? (uint32_t)(m4 ? 4 : 8) * nch * 512 * 2 : 0;
+      const uint32_t lds = ln ? (uint32_t)(m4 ? 4 : a.M <= 8 ? 8 : 16) * nch * 512 * 2 : 0;
 #define WDR_MG(MR, RR, NCH)                                                                                  \
   if (ln) wdr_launch(PROF_GEMV, bytes, flops, k_mgemv<EPI, MR, RR, NCH, true>, g2, blk, lds, s, a);         \
   else wdr_launch(PROF_GEMV, bytes, flops, k_mgemv<EPI, MR, RR, NCH, false>, g2, blk, 0, s, a);
@@ -860,12 +875,15 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
   }
       if (m4) {
         if (R == 2) { WDR_MG_N(4, 2) } else { WDR_MG_N(4, 1) }
-      } else {
+      } else if (a.M <= 8) {
         if (R == 2) { WDR_MG_N(8, 2) } else { WDR_MG_N(8, 1) }
+      } else {
+        if (R == 2) { WDR_MG_N(16, 2) } else { WDR_MG_N(16, 1) }
       }
 #undef WDR_MG_N
 #undef WDR_MG
     } else {
+      WDR_CHECK(a.M <= 8, "gemv: more than 8 rows need the k_mgemv shapes");
       const uint32_t lds = ln ? (uint32_t)a.M * a.K * 2 : 0;
 #define WDR_GEMV(MR)                                                                          \
   if (ln) wdr_launch(PROF_GEMV, bytes, flops, k_gemv<EPI, MR, true>, grid, blk, lds, s, a);  \
@@ -918,6 +936,8 @@ void launch_proj(const ProjArgs& a, hipStream_t s) {
   if (a.M > 64) {
     WDR_CHECK(a.N % GB_N == 0, "gemm: N must be a multiple of 128");
     WDR_CHECK(a.K % GB_K == 0, "gemm: K must be a multiple of 32");
+  } else if (a.step_rows && a.M <= 16) {
+    WDR_CHECK(!a.ln_x || a.K <= 1536, "gemv LN prologue: K must be <= 1536");
   } else if (a.M > 8) {
     WDR_CHECK(a.K % 32 == 0, "skinny gemm: K must be a multiple of 32");
     WDR_CHECK(!a.ln_x || (a.K <= 1280 && a.K % 4 == 0 && a.M <= 32), "skinny LN prologue: K <= 1280, M <= 32");

@@ -309,7 +309,7 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
   {
     // KV pool for the decode chains of every State of this context (multi-chain pipeline)
     const char* e = getenv("WDR_DECODE_CHAINS");
-    max_chains = std::max(1, std::min(8, e ? atoi(e) : 8));
+    max_chains = std::max(1, std::min(16, e ? atoi(e) : 16));
     const size_t per = (size_t)hp.n_text_layer * 21 * hp.n_text_ctx * hp.n_text_state;   // NSLOT = 21
     kv_k = DevMem(per * max_chains * 2);
     kv_v = DevMem(per * max_chains * 2);
@@ -1015,6 +1015,7 @@ void decode_step_layers(const Context& ctx, const StepIO& io, int R, hipStream_t
   auto P = [&](const f16* A, int lda, const f16* W, const float* b, void* out, int ldo, int N, int K, int epi,
                const float* lng = nullptr, const float* lnb = nullptr) {
     ProjArgs a{A, lda, W, K, b, out, ldo, nullptr, 0, R, N, K, epi};
+    a.step_rows = 1;
     if (lng) {
       a.ln_x = io.xd;
       a.ldln = d;
@@ -1233,7 +1234,7 @@ void State::dbg_step(const int* toks, int n, bool classic, float* logits_out) {
 
 double State::dbg_batch_step(const int* toks, int n, int R, int iters) {
   Impl& m = *m_;
-  WDR_CHECK(n >= 2 && n <= 448 && R >= 1 && R <= NSEQ && iters >= 1, "dbg_batch_step: bad shape");
+  WDR_CHECK(n >= 2 && n <= 448 && R >= 1 && R <= 16 && iters >= 1, "dbg_batch_step: bad shape");
   decoder_prefill(toks, n - 1, 0, false, false);
   WDR_HIP(hipStreamSynchronize(s_));
   StepBatcher& b = ctx_.step_batcher();
@@ -2128,7 +2129,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
 // ------------------------------------------------------------------ multi-chain step batcher
 namespace wdr {
 
-static constexpr int RB = NSEQ;   // rows per batched step (chains)
+static constexpr int RB = 16;     // rows per batched step (chains)
 
 struct StepBatcher::Impl {
   std::mutex mu;
