@@ -245,6 +245,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(ProjArgs a) {
       }
 }
 
+
 // ---------------------------------------------------------------- GEMV (M <= 8)
 // Grid-stride over output rows (one weight row per wave per iteration), 16-B weight loads,
 // v_dot2_f32_f16.  With the fused LayerNorm prologue (LN, K <= 1536) every wave normalises
