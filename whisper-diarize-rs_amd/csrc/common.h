@@ -85,5 +85,8 @@ struct ProjArgs {
   int step_rows = 0;
 };
 void launch_proj(const ProjArgs& a, hipStream_t s);   // picks GEMV (M<=8) or MFMA GEMM
+// the LayerNorm prologue of a decode-step projection as its own launch (k_dgemv's arithmetic):
+// rows ln_x -> y [M][ldy] f16
+void launch_ln_rows(const ProjArgs& a, f16* y, int ldy, hipStream_t s);
 
 }  // namespace wdr

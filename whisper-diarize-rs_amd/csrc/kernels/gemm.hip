@@ -627,6 +627,76 @@ __global__ __launch_bounds__(256) void k_mgemv(ProjArgs a) {
   }
 }
 
+
+// LayerNorm of decode-step rows into f16 with k_dgemv's in-register arithmetic (same per-lane
+// chunk order, sums and masks), so a GEMV over these rows gives exactly what the fused-LN GEMV
+// gives.  One wave per row.  Used for 9..16-row steps, where recomputing the LayerNorm of every
+// row in every GEMV workgroup (k_mgemv's LN prologue) costs more L2 traffic than the weights.
+template <int NCH>
+__global__ __launch_bounds__(64) void k_ln_rows(ProjArgs a, f16* y, int ldy) {
+  const int lane = threadIdx.x, row = blockIdx.x;
+  const int K = a.K;
+  int kc[NCH];
+  bool kin[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int k = c * 512 + lane * 8;
+    kin[c] = k < K;
+    kc[c] = kin[c] ? k : K - 8;
+  }
+  float xf[NCH][8], gv[NCH][8], bv[NCH][8];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const float* xs = a.ln_x + (size_t)row * a.ldln + kc[c];
+    const float4 p0 = *(const float4*)xs, p1 = *(const float4*)(xs + 4);
+    xf[c][0] = p0.x; xf[c][1] = p0.y; xf[c][2] = p0.z; xf[c][3] = p0.w;
+    xf[c][4] = p1.x; xf[c][5] = p1.y; xf[c][6] = p1.z; xf[c][7] = p1.w;
+    if (!kin[c])
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xf[c][e] = 0.f;
+    const float4 g0 = *(const float4*)(a.ln_g + kc[c]), g1 = *(const float4*)(a.ln_g + kc[c] + 4);
+    const float4 b0 = *(const float4*)(a.ln_b + kc[c]), b1 = *(const float4*)(a.ln_b + kc[c] + 4);
+    gv[c][0] = g0.x; gv[c][1] = g0.y; gv[c][2] = g0.z; gv[c][3] = g0.w;
+    gv[c][4] = g1.x; gv[c][5] = g1.y; gv[c][6] = g1.z; gv[c][7] = g1.w;
+    bv[c][0] = b0.x; bv[c][1] = b0.y; bv[c][2] = b0.z; bv[c][3] = b0.w;
+    bv[c][4] = b1.x; bv[c][5] = b1.y; bv[c][6] = b1.z; bv[c][7] = b1.w;
+  }
+  float sm = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sm += xf[c][e];
+  sm = wave_sum(sm);
+  const float mean = sm / a.K;
+  float s2 = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float t = xf[c][e] - mean;
+      s2 += kin[c] ? t * t : 0.f;
+    }
+  s2 = wave_sum(s2);
+  const float scale = 1.0f / sqrtf(s2 / a.K + 1e-5f);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    if (!kin[c]) continue;
+    f16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (f16)((xf[c][e] - mean) * scale * gv[c][e] + bv[c][e]);
+    *(f16x8*)(y + (size_t)row * ldy + kc[c]) = o;
+  }
+}
+
+void launch_ln_rows(const ProjArgs& a, f16* y, int ldy, hipStream_t s) {
+  WDR_CHECK(a.ln_x && a.K % 8 == 0 && a.K <= 1536, "step LayerNorm rows: K must be <= 1536");
+  const int nch = cdiv(a.K, 512);
+  if (nch == 1) hipLaunchKernelGGL(k_ln_rows<1>, dim3(a.M), dim3(64), 0, s, a, y, ldy);
+  else if (nch == 2) hipLaunchKernelGGL(k_ln_rows<2>, dim3(a.M), dim3(64), 0, s, a, y, ldy);
+  else hipLaunchKernelGGL(k_ln_rows<3>, dim3(a.M), dim3(64), 0, s, a, y, ldy);
+  WDR_HIP(hipGetLastError());
+}
+
 // General GEMV (optional LN prologue through LDS for 2 < M <= 8).
 template <int EPI, int MR, bool LN>
 __global__ __launch_bounds__(256) void k_gemv(ProjArgs a) {

@@ -1012,6 +1012,9 @@ void decode_step_layers(const Context& ctx, const StepIO& io, int R, hipStream_t
   const int d = hp.n_text_state, L = hp.n_text_layer;
   const float scale = 1.0f / 8.0f;
   const int ldxkv = L * 2 * d;
+  // more than ln_split rows: the LayerNorm of the rows runs once into io.attd (free at every
+  // LN point of the layer) instead of in every GEMV workgroup
+  static const int ln_split = getenv("WDR_STEP_LN_SPLIT") ? atoi(getenv("WDR_STEP_LN_SPLIT")) : 8;
   auto P = [&](const f16* A, int lda, const f16* W, const float* b, void* out, int ldo, int N, int K, int epi,
                const float* lng = nullptr, const float* lnb = nullptr) {
     ProjArgs a{A, lda, W, K, b, out, ldo, nullptr, 0, R, N, K, epi};
@@ -1021,6 +1024,12 @@ void decode_step_layers(const Context& ctx, const StepIO& io, int R, hipStream_t
       a.ldln = d;
       a.ln_g = lng;
       a.ln_b = lnb;
+      if (R > ln_split) {
+        launch_ln_rows(a, io.attd, d, s);
+        a.ln_x = nullptr;
+        a.A = io.attd;
+        a.lda = d;
+      }
     }
     return a;
   };
