@@ -229,6 +229,10 @@ int wdr_context_create(const char* model_path, const char* model_name, int8_t ha
                        int8_t use_gpu, int8_t enable_dtw, int8_t enable_flash_attn, int8_t has_num_samples,
                        uint64_t num_samples, const wdr_synthetic* syn, wdr_context** out);
 void wdr_context_free(wdr_context* c);
+/* parse a whisper.cpp ggml model file without loading it (no GPU): hparams[11] = n_vocab,
+ * n_audio_ctx, n_audio_state, n_audio_head, n_audio_layer, n_text_ctx, n_text_state, n_text_head,
+ * n_text_layer, n_mels, ftype; wdr_context_create loads such a file when model_path is given */
+int wdr_ggml_info(const char* path, int32_t* hparams, int64_t* n_tensors, int64_t* n_vocab_tokens);
 int wdr_run_pipeline(wdr_context* c, const wdr_speech_segment* segs, size_t n_segs, const wdr_transcribe_options* opts,
                      const wdr_synthetic* syn, const wdr_callbacks* cb, wdr_segment_list** out);
 /* run_pipeline without the cross-segment overlap clip and without speaker assignment, with

@@ -116,3 +116,36 @@ def test_oracle_discrete_distribution_matches_libstdcxx(lib):
         rs = np.random.RandomState(seed)
         want = [WhisperState.discrete_draw(rs, w) for _ in range(64)]
         assert out.tolist() == want
+
+
+def test_ggml_info_reads_whisper_cpp_header(tmp_path):
+    """wdr_ggml_info parses a whisper.cpp ggml model file (the ggml-<model>.bin files
+    src/model_manager.rs:162 caches and whisper-rs loads at src/transcribe.rs:154) without a GPU:
+    header, mel filters, vocabulary and every tensor record."""
+    from tests.ggml_writer import write_ggml
+    p = str(tmp_path / "ggml-tiny-test.bin")
+    hp, n_tensors, n_words, _ = write_ggml(p, "tiny-test")
+    info = wdr.ggml_info(p)
+    assert info["n_vocab"] == hp.n_vocab and info["n_mels"] == hp.n_mels
+    assert (info["n_audio_state"], info["n_audio_layer"]) == (hp.n_audio_state, hp.n_audio_layer)
+    assert (info["n_text_state"], info["n_text_layer"]) == (hp.n_text_state, hp.n_text_layer)
+    assert info["ftype"] == 1
+    assert info["n_tensors"] == n_tensors and info["n_vocab_tokens"] == n_words
+    # f32 files parse too (ftype 0: every tensor f32)
+    p32 = str(tmp_path / "ggml-f32.bin")
+    write_ggml(p32, "tiny-test", ftype=0)
+    assert wdr.ggml_info(p32)["ftype"] == 0
+
+
+@pytest.mark.parametrize("kind,msg", [("magic", "bad magic"), ("trunc", "truncated"), ("missing", "doesn't exist")])
+def test_ggml_info_rejects_bad_files(tmp_path, kind, msg):
+    from tests.ggml_writer import write_ggml
+    p = str(tmp_path / "m.bin")
+    if kind == "magic":
+        write_ggml(p, "tiny-test", magic=0x12345678)
+    elif kind == "trunc":
+        write_ggml(p, "tiny-test", truncate=5000)
+    else:
+        p = str(tmp_path / "absent.bin")
+    with pytest.raises(wdr.WdrError, match=msg):
+        wdr.ggml_info(p)

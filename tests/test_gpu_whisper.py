@@ -180,3 +180,76 @@ def test_engine_transcribe_audio_with_vad(tmp_path):
     assert len(vsegs) > 0
     assert [(s.text, round(s.start, 6), round(s.end, 6)) for s in got] == \
         [(s.text, round(s.start, 6), round(s.end, 6)) for s in want]
+
+
+def _perturb_ln(W):
+    """LayerNorm gamma/beta away from 1/0 (synthetic mode has no LN tensors to read), so a
+    context that ignored the file's LN tensors would not match."""
+    rng = np.random.default_rng(5)
+    for k in list(W):
+        if k.endswith("ln.weight") or k.endswith("_ln.weight") or k.endswith("ln_post.weight"):
+            W[k] = (1.0 + 0.1 * rng.standard_normal(W[k].shape)).astype(np.float32)
+        elif k.endswith("ln.bias") or k.endswith("_ln.bias") or k.endswith("ln_post.bias"):
+            W[k] = (0.05 * rng.standard_normal(W[k].shape)).astype(np.float32)
+
+
+@pytest.fixture(scope="module")
+def ggml_model(tmp_path_factory):
+    from tests.ggml_writer import write_ggml
+    d = tmp_path_factory.mktemp("ggml")
+    path = str(d / "ggml-tiny-test.bin")
+    hp, _, _, W = write_ggml(path, "tiny-test", std=0.02, emb_std=EMB_STD, mutate=_perturb_ln)
+    return path, hp, W
+
+
+def test_ggml_file_context_matches_oracle(ggml_model, audio):
+    """wdr_context_create(model_path=<whisper.cpp ggml file>): weights (f16 matrices, f32
+    biases / LN / positional tables), mel filters and vocabulary come from the file
+    (src/transcribe.rs:154); encoder and full decode match the oracle on the same weights."""
+    path, hp, W = ggml_model
+    ctx = wdr.WhisperContext("tiny-test", model_path=path, synthetic=SYN)
+    assert ctx.hparams["n_vocab"] == hp.n_vocab and ctx.hparams["n_mels"] == hp.n_mels
+    rng = np.random.default_rng(11)
+    mel = (rng.standard_normal((hp.n_mels, 3000)) * 0.4).astype(np.float32)
+    got = ctx.encode(mel)
+    ref = Whisper(hp, W).encode(mel)
+    err = np.abs(got - ref)
+    assert err.max() < 5e-2 and err.mean() < 4e-3, (err.max(), err.mean())
+    syn_out = wdr.WhisperContext("tiny-test", synthetic=SYN).encode(mel)
+    assert np.abs(syn_out - ref).mean() > 10 * err.mean()   # the file's LN tensors were used
+    pcm, spurts = audio
+    st = _oracle_state("tiny-test", hp, W)
+    for a, b, _ in spurts[:2]:
+        x = pcm_i16_to_f32(pcm[int(a * 16000):int(b * 16000)])
+        g, lang_id = ctx.state_full(x, wdr.TranscribeOptions(
+            lang="auto", advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy")))
+        st.full(x, _params("auto"))
+        assert [[t["id"] for t in s["tokens"]] for s in g] == [[t.id for t in r.tokens] for r in st.result_all]
+        assert [s["text"] for s in g] == [r.text for r in st.result_all]
+        assert lang_id == st.lang_id
+
+
+def test_engine_loads_cached_ggml_file(ggml_model, tmp_path):
+    """Engine::transcribe_audio resolves ggml-<model>.bin in the hf-hub cache layout
+    (<cache>/models--ggerganov--whisper.cpp/snapshots/<rev>/, src/model_manager.rs:661-681)
+    and transcribes with the file's weights: same output as a context made from that file."""
+    import shutil
+    from oracle.pipeline import write_wav
+    path, hp, W = ggml_model
+    snap = tmp_path / "cache" / "models--ggerganov--whisper.cpp" / "snapshots" / "rev0"
+    snap.mkdir(parents=True)
+    shutil.copy(path, snap / "ggml-tiny-test.bin")
+    pcm, _ = synth_speech(25.0, seed=4)
+    wav = str(tmp_path / "a.wav")
+    write_wav(wav, pcm)
+    eng = wdr.Engine(wdr.EngineConfig(cache_dir=str(tmp_path / "cache")), synthetic=SYN)
+    opts = wdr.TranscribeOptions(model="tiny-test", lang="en", enable_vad=True,
+                                 advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    got = eng.transcribe_audio(wav, opts)
+    mask, vsegs = wdr.Vad().get_segments(pcm)
+    ctx = wdr.WhisperContext("tiny-test", model_path=path, synthetic=SYN)
+    want, lang = ctx.run_pipeline(vsegs, opts)
+    want = wdr.process_segments(want, lang or "en", None, mask)
+    assert len(got) > 0
+    assert [(s.text, round(s.start, 6), round(s.end, 6)) for s in got] == \
+        [(s.text, round(s.start, 6), round(s.end, 6)) for s in want]

@@ -20,6 +20,7 @@
 #include <random>
 #include <string>
 #include <sys/stat.h>
+#include <dirent.h>
 #include <condition_variable>
 #include <exception>
 #include <mutex>
@@ -31,6 +32,7 @@
 #include "formatting.h"
 #include "vad.h"
 #include "whisper.h"
+#include "ggml_file.h"
 
 using namespace wdr;
 
@@ -410,12 +412,51 @@ static bool file_exists(const char* p) {
   return p && stat(p, &st) == 0;
 }
 
-// src/transcribe.rs:89-166.  No ggml loader yet: the named model's
-// hparams are instantiated with synthetic weights.
+// The cached whisper.cpp model of `model` under the engine's cache dir, without network:
+// <cache>/ggml-<model>.bin, or the hf-hub layout the reference's model manager uses,
+// <cache>/models--ggerganov--whisper.cpp/snapshots/<rev>/ggml-<model>.bin
+// (src/model_manager.rs:162, 661-681).  Empty when absent (synthetic weights then).
+static std::string find_model_file(const std::string& cache_dir, const std::string& model) {
+  if (cache_dir.empty()) return std::string();
+  const std::string file = "ggml-" + model + ".bin";
+  const std::string direct = cache_dir + "/" + file;
+  if (file_exists(direct.c_str())) return direct;
+  const std::string snaps = cache_dir + "/models--ggerganov--whisper.cpp/snapshots";
+  std::string found;
+  if (DIR* d = opendir(snaps.c_str())) {
+    std::vector<std::string> revs;
+    while (dirent* ent = readdir(d))
+      if (ent->d_name[0] != '.') revs.push_back(ent->d_name);
+    closedir(d);
+    std::sort(revs.begin(), revs.end());
+    for (const std::string& r : revs) {
+      const std::string c = snaps + "/" + r + "/" + file;
+      if (file_exists(c.c_str())) {
+        found = c;
+        break;
+      }
+    }
+  }
+  return found;
+}
+
+// src/transcribe.rs:89-166.  model_path: a whisper.cpp ggml file (hparams, mel filters, vocabulary and weights from it;
+// model_name then only selects the DTW alignment-head preset, src/transcribe.rs:117-129);
+// empty: the named configuration with synthetic seeded weights
 static std::unique_ptr<wdr_context> make_context(const std::string& model_name, bool has_dev, int dev, int8_t use_gpu,
-                                                 int8_t enable_dtw, const SynCfg& syn) {
+                                                 int8_t enable_dtw, const SynCfg& syn,
+                                                 const std::string& model_path = std::string()) {
   HParams hp;
-  if (!hparams_for(model_name, &hp)) throw std::runtime_error("failed to open model: unknown model '" + model_name + "'");
+  std::unique_ptr<GgmlFile> gf;
+  if (!model_path.empty()) {
+    gf = std::make_unique<GgmlFile>(model_path);
+    const int32_t* h = gf->hp;
+    hp.n_vocab = h[0]; hp.n_audio_ctx = h[1]; hp.n_audio_state = h[2]; hp.n_audio_head = h[3];
+    hp.n_audio_layer = h[4]; hp.n_text_ctx = h[5]; hp.n_text_state = h[6]; hp.n_text_head = h[7];
+    hp.n_text_layer = h[8]; hp.n_mels = h[9];
+  } else if (!hparams_for(model_name, &hp)) {
+    throw std::runtime_error("failed to open model: unknown model '" + model_name + "'");
+  }
   ContextParams cp;
   if (use_gpu == 0) cp.use_gpu = false;
   if (has_dev) cp.gpu_device = dev;
@@ -426,9 +467,9 @@ static std::unique_ptr<wdr_context> make_context(const std::string& model_name, 
   auto c = std::make_unique<wdr_context>();
   const double t = now_s();
   try {
-    c->ctx = std::make_unique<Context>(model_name, hp, cp);
+    c->ctx = std::make_unique<Context>(model_name, hp, cp, gf.get());
     c->st = std::make_unique<State>(*c->ctx);
-    c->chains = c->ctx->max_chains;   // WDR_DECODE_CHAINS (default 4), wdr_context_set_chains
+    c->chains = c->ctx->max_chains;   // WDR_DECODE_CHAINS (default 16), wdr_context_set_chains
   } catch (const std::exception& ex) {
     throw std::runtime_error(std::string("create whisper context crash: ") + ex.what());
   }
@@ -1110,7 +1151,8 @@ int wdr_transcribe_audio(wdr_engine* e, const char* audio_path, const wdr_transc
     auto it = e->contexts.find(model);
     if (it == e->contexts.end()) {
       it = e->contexts.emplace(model, make_context(model, e->cfg.has_gpu_device, e->cfg.gpu_device, e->cfg.use_gpu,
-                                                   e->cfg.enable_dtw, e->syn)).first;
+                                                   e->cfg.enable_dtw, e->syn, find_model_file(e->cache_dir, model)))
+               .first;
     }
     if (o && o->translate_target && !(o->whisper_to_english == 1))
       return fail("translate_target: network translation is out of scope for libwdr");
@@ -1382,13 +1424,24 @@ int wdr_context_create(const char* model_path, const char* model_name, int8_t ha
   WDR_GUARD({
     if (model_path && *model_path && !file_exists(model_path)) return fail("whisper file doesn't exist");
     *out = make_context(model_name ? model_name : "base", has_gpu_device == 1, gpu_device, use_gpu, enable_dtw,
-                        syn_of(syn))
+                        syn_of(syn), model_path ? std::string(model_path) : std::string())
                .release();
     return 0;
   })
 }
 
 void wdr_context_free(wdr_context* c) { delete c; }
+
+int wdr_ggml_info(const char* path, int32_t* hparams, int64_t* n_tensors, int64_t* n_vocab_tokens) {
+  WDR_GUARD({
+    if (!path || !file_exists(path)) return fail("whisper file doesn't exist");
+    const GgmlFile f(path);
+    memcpy(hparams, f.hp, sizeof f.hp);
+    *n_tensors = (int64_t)f.tensors.size();
+    *n_vocab_tokens = (int64_t)f.vocab.size();
+    return 0;
+  })
+}
 
 int wdr_run_pipeline(wdr_context* c, const wdr_speech_segment* segs, size_t n_segs, const wdr_transcribe_options* o,
                      const wdr_synthetic* syn, const wdr_callbacks* cb, wdr_segment_list** out) {

@@ -78,7 +78,9 @@ struct ContextParams {
 
 class Context {
  public:
-  Context(const std::string& model_name, const HParams& hp, const ContextParams& cp);
+  // gf: weights, mel filters and vocabulary from a whisper.cpp ggml file; null: synthetic
+  Context(const std::string& model_name, const HParams& hp, const ContextParams& cp,
+          const class GgmlFile* gf = nullptr);
   ~Context();
   std::string name;
   ContextParams cp;

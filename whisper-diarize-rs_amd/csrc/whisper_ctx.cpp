@@ -2,6 +2,7 @@
 // whisper_full_with_state decode loop as the reference drives it
 // (src/transcribe.rs:20-87 params, :389 state.full).  Mirrors oracle/whisper_full.py.
 #include "whisper.h"
+#include "ggml_file.h"
 #include "prof.h"
 
 #include <algorithm>
@@ -152,7 +153,7 @@ struct Alloc {
 };
 }  // namespace
 
-Context::Context(const std::string& model_name, const HParams& hp, const ContextParams& p)
+Context::Context(const std::string& model_name, const HParams& hp, const ContextParams& p, const GgmlFile* gf)
     : name(model_name), cp(p), vocab(hp.n_vocab) {
   WDR_CHECK(cp.use_gpu, "libwdr has no CPU backend: use_gpu=false is not supported (the CPU restatement is test-only)");
   WDR_HIP(hipSetDevice(cp.gpu_device));
@@ -215,13 +216,36 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
   m.ln_g = f32(o_lng); m.ln_b = f32(o_lnb);
   m.mel_filters = f32(o_filt); m.hann = f32(o_hann); m.cos_tab = f32(o_cos); m.sin_tab = f32(o_sin);
 
-  // ---- synthetic weights (oracle/weights.py naming + hash)
+  // ---- weights: from a whisper.cpp ggml file (gf), else synthetic (oracle/weights.py naming +
+  // hash).  Both paths name every tensor as whisper.cpp does.
   hipStream_t s = stream;
   const double sq3 = std::sqrt(3.0);
   auto fill = [&](void* dst, const std::string& nm, long long rows, int src_cols, int dst_cols, bool is16, double sd) {
-    launch_synth_fill(dst, rows, src_cols, dst_cols, fnv1a64(nm), (float)(sd * sq3), is16, 0, 0.f, s);
+    if (!gf) {
+      launch_synth_fill(dst, rows, src_cols, dst_cols, fnv1a64(nm), (float)(sd * sq3), is16, 0, 0.f, s);
+      return;
+    }
+    const int64_t n = rows * (int64_t)src_cols;
+    if (is16) {
+      std::vector<uint16_t> v = gf->as_f16(nm, n), padded;
+      if (dst_cols != src_cols) {
+        padded.assign((size_t)rows * dst_cols, 0);
+        for (long long r = 0; r < rows; ++r) memcpy(&padded[r * dst_cols], &v[r * src_cols], (size_t)src_cols * 2);
+        v.swap(padded);
+      }
+      WDR_HIP(hipMemcpy(dst, v.data(), v.size() * 2, hipMemcpyHostToDevice));
+    } else {
+      WDR_CHECK(dst_cols == src_cols, "ggml load: padded f32 tensor");
+      const std::vector<float> v = gf->as_f32(nm, n);
+      WDR_HIP(hipMemcpy(dst, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+    }
   };
   auto cfill = [&](float* dst, long long n, float v) { launch_synth_fill(dst, 1, (int)n, (int)n, 0, 0.f, false, 1, v, s); };
+  // LayerNorm parameters: gamma 1 / beta 0 in synthetic mode, the named tensor from a file
+  auto lnfill = [&](float* dst, const std::string& nm, long long n, float v) {
+    if (gf) fill(dst, nm, 1, (int)n, (int)n, false, 0.0);
+    else cfill(dst, n, v);
+  };
   const double sd = cp.weight_std;
   fill(m.conv1_w, "encoder.conv1.weight", d, hp.n_mels * 3, m.kp1, true, sd);
   fill(m.conv1_b, "encoder.conv1.bias", 1, d, d, false, sd);
@@ -243,10 +267,11 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
     fill(e.b_fc1, p + "mlp.0.bias", 1, 4 * d, 4 * d, false, sd);
     fill(e.w_fc2, p + "mlp.2.weight", d, 4 * d, 4 * d, true, sd);
     fill(e.b_fc2, p + "mlp.2.bias", 1, d, d, false, sd);
-    cfill(e.ln1_g, d, 1.f); cfill(e.ln1_b, d, 0.f); cfill(e.ln2_g, d, 1.f); cfill(e.ln2_b, d, 0.f);
+    lnfill(e.ln1_g, p + "attn_ln.weight", d, 1.f); lnfill(e.ln1_b, p + "attn_ln.bias", d, 0.f);
+    lnfill(e.ln2_g, p + "mlp_ln.weight", d, 1.f); lnfill(e.ln2_b, p + "mlp_ln.bias", d, 0.f);
   }
-  cfill(m.ln_post_g, d, 1.f);
-  cfill(m.ln_post_b, d, 0.f);
+  lnfill(m.ln_post_g, "encoder.ln_post.weight", d, 1.f);
+  lnfill(m.ln_post_b, "encoder.ln_post.bias", d, 0.f);
   fill(m.tok_emb, "decoder.token_embedding.weight", hp.n_vocab, dt, dt, true, cp.emb_std);
   fill(m.dec_pos, "decoder.positional_embedding", hp.n_text_ctx, dt, dt, false, sd);
   for (int i = 0; i < L; ++i) {
@@ -272,13 +297,23 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
     fill(e.b_fc1, p + "mlp.0.bias", 1, 4 * dt, 4 * dt, false, sd);
     fill(e.w_fc2, p + "mlp.2.weight", dt, 4 * dt, 4 * dt, true, sd);
     fill(e.b_fc2, p + "mlp.2.bias", 1, dt, dt, false, sd);
-    cfill(e.ln1_g, dt, 1.f); cfill(e.ln1_b, dt, 0.f); cfill(e.ln2_g, dt, 1.f); cfill(e.ln2_b, dt, 0.f);
-    cfill(e.ln3_g, dt, 1.f); cfill(e.ln3_b, dt, 0.f);
+    lnfill(e.ln1_g, p + "attn_ln.weight", dt, 1.f); lnfill(e.ln1_b, p + "attn_ln.bias", dt, 0.f);
+    lnfill(e.ln2_g, p + "cross_attn_ln.weight", dt, 1.f); lnfill(e.ln2_b, p + "cross_attn_ln.bias", dt, 0.f);
+    lnfill(e.ln3_g, p + "mlp_ln.weight", dt, 1.f); lnfill(e.ln3_b, p + "mlp_ln.bias", dt, 0.f);
   }
-  cfill(m.ln_g, dt, 1.f);
-  cfill(m.ln_b, dt, 0.f);
+  lnfill(m.ln_g, "decoder.ln.weight", dt, 1.f);
+  lnfill(m.ln_b, "decoder.ln.bias", dt, 0.f);
   // mel front-end constants
   std::vector<float> filt = mel_filters_host(hp.n_mels), hann(400), cs(400), sn(400);
+  if (gf) {   // the file's own filter bank (whisper.cpp uses it as stored)
+    WDR_CHECK(gf->n_mel == hp.n_mels && gf->n_fft == 201, "ggml load: mel filter bank shape");
+    filt = gf->filters;
+    // the file's vocabulary replaces the synthetic token texts (special tokens past the file's
+    // list keep whisper.cpp's generated names); token_to_id rebuilt in id order, last wins
+    for (size_t i = 0; i < gf->vocab.size() && (int)i < vocab.n_vocab; ++i) vocab.id_to_token[i] = gf->vocab[i];
+    vocab.token_to_id.clear();
+    for (int i = 0; i < vocab.n_vocab; ++i) vocab.token_to_id[vocab.id_to_token[i]] = i;
+  }
   for (int i = 0; i < 400; ++i) {
     hann[i] = (float)(0.5 * (1.0 - std::cos(2.0 * M_PI * i / 400.0)));
     cs[i] = (float)std::cos(2.0 * M_PI * i / 400.0);

@@ -484,6 +484,17 @@ class Diarizer:
             pass
 
 
+def ggml_info(path: str) -> dict:
+    """Header of a whisper.cpp ggml model file (wdr_ggml_info; parses the whole file, no GPU)."""
+    lib = L.load()
+    hp = (C.c_int32 * 11)()
+    nt, nv = C.c_int64(), C.c_int64()
+    L.check(lib.wdr_ggml_info(path.encode(), hp, C.byref(nt), C.byref(nv)))
+    keys = ["n_vocab", "n_audio_ctx", "n_audio_state", "n_audio_head", "n_audio_layer", "n_text_ctx",
+            "n_text_state", "n_text_head", "n_text_layer", "n_mels", "ftype"]
+    return {**dict(zip(keys, list(hp))), "n_tensors": nt.value, "n_vocab_tokens": nv.value}
+
+
 class WhisperContext:
     """transcribe::create_context (src/transcribe.rs:89-166) + its whisper_state."""
 
