@@ -146,6 +146,7 @@ typedef struct {
    * replay, wall time of the speculative and the fix-up phases */
   int64_t chains, batch_launches, batch_rows, fixup_segments, replay_segments;
   double spec_s, fixup_s;
+  double batch_step_s;   /* wall of the batched steps (submit -> tokens on the host), summed */
 } wdr_stage_times;
 
 const char* wdr_last_error(void);

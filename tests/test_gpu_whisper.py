@@ -133,19 +133,24 @@ def test_state_full_matches_oracle(model, audio, lang, strategy, temp):
         prompt = ref[-1].text.lstrip() if ref else prompt
 
 
-def test_pipeline_matches_oracle_glue(model, audio):
-    """run_transcription_pipeline: prompt chain, offsets, overlap clipping, callbacks order."""
+@pytest.mark.parametrize("translate", [False, True])
+def test_pipeline_matches_oracle_glue(model, audio, translate):
+    """run_transcription_pipeline: prompt chain, offsets, overlap clipping, callbacks order;
+    translate: whisper_to_english (translate task token, src/transcribe.rs:54-55) with the
+    interpolated word times of src/transcribe.rs:171-203."""
     name, ctx, hp, W = model
     pcm, spurts = audio
     segs = [wdr.SpeechSegment(a, b, pcm[int(a * 16000):int(b * 16000)]) for a, b, _ in spurts[:4]]
     events = []
     cb = wdr.Callbacks(progress=lambda p, t, l: events.append(("p", p, int(t), l)),
                        new_segment_callback=lambda s: events.append(("s", s.text)))
-    opts = wdr.TranscribeOptions(lang="auto", offset=1.5, advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    opts = wdr.TranscribeOptions(lang="auto", offset=1.5, whisper_to_english=translate,
+                                 advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
     got, lang = ctx.run_pipeline(segs, opts, cb)
     st = _oracle_state(name, hp, W)
     ref, rlang = run_transcription_pipeline(st, [OSeg(s.start, s.end, s.samples) for s in segs],
-                                            dict(lang="auto", offset=1.5, advanced=dict(sampling_strategy="greedy"),
+                                            dict(lang="auto", offset=1.5, whisper_to_english=translate,
+                                                 advanced=dict(sampling_strategy="greedy"),
                                                  synthetic=dict(force_len_rate=3.3, logprob_thold=-np.inf,
                                                                 entropy_thold=-1.0)))
     assert lang == rlang
@@ -253,3 +258,26 @@ def test_engine_loads_cached_ggml_file(ggml_model, tmp_path):
     assert len(got) > 0
     assert [(s.text, round(s.start, 6), round(s.end, 6)) for s in got] == \
         [(s.text, round(s.start, 6), round(s.end, 6)) for s in want]
+
+
+@pytest.mark.parametrize("translate", [False, True])
+def test_engine_whole_file_path(tmp_path, translate):
+    """Engine::transcribe_audio with neither VAD nor diarization: the whole file is one speech
+    segment (src/engine.rs:141-147), then process_segments without a VAD mask
+    (src/engine.rs:179-199); with whisper_to_english the words are interpolated."""
+    from oracle.pipeline import write_wav
+    pcm, _ = synth_speech(20.0, seed=7)
+    path = str(tmp_path / "w.wav")
+    write_wav(path, pcm)
+    eng = wdr.Engine(wdr.EngineConfig(), synthetic=SYN)
+    opts = wdr.TranscribeOptions(model="tiny-test-ml", lang="auto", whisper_to_english=translate, enable_vad=False,
+                                 advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    got = eng.transcribe_audio(path, opts)
+    ctx = wdr.WhisperContext("tiny-test-ml", synthetic=SYN)
+    want, lang = ctx.run_pipeline([wdr.SpeechSegment(0.0, len(pcm) / 16000.0, pcm)], opts)
+    want = wdr.process_segments(want, lang or "auto", None, None)
+    assert len(got) > 0
+    assert [(s.text, round(s.start, 6), round(s.end, 6)) for s in got] == \
+        [(s.text, round(s.start, 6), round(s.end, 6)) for s in want]
+    assert [[(w.text, round(w.start, 6), round(w.end, 6)) for w in s.words] for s in got] == \
+        [[(w.text, round(w.start, 6), round(w.end, 6)) for w in s.words] for s in want]

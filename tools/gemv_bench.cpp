@@ -168,6 +168,37 @@ int main() {
                          s, 50);
     printf("%-22s %8.2f us/launch\n", "null kernel 256 WGs", t * 1e3 / L);
   }
+  if (const char* gr = getenv("GB_ROWS")) {
+    // multi-row decode-step GEMVs (the batched step's projections after k_ln_rows): launch_proj
+    // with step_rows, M rows, no LN prologue; run under WDR_MGEMV_STAGED / WDR_MGEMV_R variants
+    const int M = atoi(gr);
+    f16* xa;
+    CK(hipMalloc(&xa, (size_t)16 * 4 * d * 2));
+    CK(hipMemset(xa, 0, (size_t)16 * 4 * d * 2));
+    float* o32;
+    CK(hipMalloc(&o32, (size_t)16 * 4 * d * 4));
+    CK(hipMemset(o32, 0, (size_t)16 * 4 * d * 4));
+    for (const Shape& sh : shapes) {
+      const size_t wel = (size_t)sh.N * sh.K;
+      std::vector<f16*> W(L);
+      for (int l = 0; l < L; ++l) {
+        CK(hipMalloc(&W[l], wel * 2));
+        CK(hipMemset(W[l], 0, wel * 2));
+      }
+      const double mb = wel * 2 / 1e6;
+      float t = time_graph([&] {
+        for (int l = 0; l < L; ++l) {
+          ProjArgs a{xa, sh.K, W[l], sh.K, bias, o32, sh.N, nullptr, 0, M, sh.N, sh.K,
+                     sh.epi == EPI_QKV_CACHE ? EPI_F16 : sh.epi};
+          a.step_rows = 1;
+          launch_proj(a, s);
+        }
+      }, s, 20);
+      printf("M=%-2d %-22s %8.2f us  %7.2f TB/s\n", M, sh.name, t * 1e3 / L, mb / (t * 1e3 / L));
+      for (int l = 0; l < L; ++l) CK(hipFree(W[l]));
+    }
+    return 0;
+  }
   for (const Shape& sh : shapes) {
     const size_t wel = (size_t)sh.N * sh.K;
     std::vector<f16*> W(L);
@@ -182,7 +213,7 @@ int main() {
         for (int l = 0; l < L; ++l)
           hipLaunchKernelGGL(k_stream, dim3(grid), dim3(256), 0, s, (const f16x8*)W[l], (long long)(wel / 8), out);
       }, s, 20);
-      printf("   stream grid %-5d   %8.2f us  %7.2f TB/s\n", grid, t * 1e3 / L, mb / (t * 1e3 / L) / 1e6);
+      printf("   stream grid %-5d   %8.2f us  %7.2f TB/s\n", grid, t * 1e3 / L, mb / (t * 1e3 / L));
     }
     {
       float t = time_graph([&] {
@@ -193,7 +224,7 @@ int main() {
           launch_proj(a, s);
         }
       }, s, 20);
-      printf("   launch_proj         %8.2f us  %7.2f TB/s\n", t * 1e3 / L, mb / (t * 1e3 / L) / 1e6);
+      printf("   launch_proj         %8.2f us  %7.2f TB/s\n", t * 1e3 / L, mb / (t * 1e3 / L));
     }
 #define ROWS(R, NCH)                                                                                              \
     {                                                                                                             \
@@ -202,7 +233,7 @@ int main() {
           hipLaunchKernelGGL((k_gemv_rows<R, NCH>), dim3((sh.N + 4 * R - 1) / (4 * R)), dim3(256), 0, s, W[l], sh.K, \
                              sh.N, x16, out);                                                                     \
       }, s, 20);                                                                                                  \
-      printf("   rows R=%d            %8.2f us  %7.2f TB/s\n", R, t * 1e3 / L, mb / (t * 1e3 / L) / 1e6);          \
+      printf("   rows R=%d            %8.2f us  %7.2f TB/s\n", R, t * 1e3 / L, mb / (t * 1e3 / L));          \
     }
     if (sh.K == d) {
       ROWS(1, 3) ROWS(2, 3) ROWS(4, 3)
@@ -216,7 +247,7 @@ int main() {
           hipLaunchKernelGGL((k_gemv_splitk<RW, KPW>), dim3((sh.N + RW - 1) / RW), dim3(256), 0, s, W[l], sh.K, \
                              sh.N, x16, out);                                                               \
       }, s, 20);                                                                                            \
-      printf("   splitk RW=%d KPW=%d     %8.2f us  %7.2f TB/s\n", RW, KPW, t * 1e3 / L, mb / (t * 1e3 / L) / 1e6); \
+      printf("   splitk RW=%d KPW=%d     %8.2f us  %7.2f TB/s\n", RW, KPW, t * 1e3 / L, mb / (t * 1e3 / L)); \
     }
     if (sh.K == d) {
       SPLITK(2, 1) SPLITK(4, 1) SPLITK(8, 1)

@@ -226,7 +226,7 @@ struct wdr_context {
   int chains = 1;                                 // decode chains per run_pipeline call
   struct ChainStats {
     long long chains = 1, launches = 0, rows = 0, fixups = 0, replays = 0;
-    double spec_s = 0, fixup_s = 0;
+    double spec_s = 0, fixup_s = 0, step_s = 0;
   } cs;                                           // the last run_pipeline's multi-chain figures
   std::unique_ptr<CamModel> cam;   // EmbeddingExtractor, created on the first diarized run
   double load_s = 0;
@@ -656,6 +656,7 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
   c->cs.chains = C;
   StepBatcher& sb = c->ctx->step_batcher();
   const long long l0 = sb.launches, r0 = sb.rows;
+  const double s0 = sb.step_s;
   const double t_spec = now_s();
   auto worker = [&](int k) {
     State& st = state(k);
@@ -818,6 +819,7 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
   c->cs.fixup_s = now_s() - t_fix;
   c->cs.launches = sb.launches - l0;
   c->cs.rows = sb.rows - r0;
+  c->cs.step_s = sb.step_s - s0;
   // stage accounting: chains' times summed into the context's state
   for (int k = 1; k < C; ++k) {
     const StageTimes& t = state(k).times;
@@ -1511,6 +1513,7 @@ int wdr_context_stage_times(wdr_context* c, wdr_stage_times* o) {
     o->replay_segments = c->cs.replays;
     o->spec_s = c->cs.spec_s;
     o->fixup_s = c->cs.fixup_s;
+    o->batch_step_s = c->cs.step_s;
     return 0;
   })
 }

@@ -697,6 +697,125 @@ void launch_ln_rows(const ProjArgs& a, f16* y, int ldy, hipStream_t s) {
   WDR_HIP(hipGetLastError());
 }
 
+// Decode GEMV for 3..16 step rows without a LayerNorm prologue (o / xo / fc2, and every
+// projection of a 9..16-row step after k_ln_rows): the workgroup stages its M activation rows
+// into LDS once (issued before the weight stream, so the L2 reads overlap the HBM latency)
+// instead of every wave re-reading all rows from L2, and the R x MR dot products of a wave
+// are reduced with one reduce-scatter butterfly (V - 1 + log2(64 / V) shuffles instead of
+// 6 V).  Per (weight row, activation row) the chunk order, dot8 order and the butterfly tree
+// are those of k_dgemv / k_mgemv (each butterfly step adds the partner lane's partial of the
+// same value), so every row's result is bit-identical to the 1-row step's.
+template <int V, int O, int CNT>
+__device__ __forceinline__ void reduce_scatter_step(float (&v)[V], int lane) {
+  if constexpr (CNT > 1) {
+    constexpr int H = CNT / 2;
+    const bool up = (lane & O) != 0;
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      const float keep = up ? v[i + H] : v[i];
+      const float send = up ? v[i] : v[i + H];
+      v[i] = keep + __shfl_xor(send, O, 64);
+    }
+  } else {
+    v[0] += __shfl_xor(v[0], O, 64);
+  }
+  if constexpr (O > 1) reduce_scatter_step<V, O / 2, (CNT > 1 ? CNT / 2 : 1)>(v, lane);
+}
+template <int V>
+__device__ __forceinline__ float reduce_scatter(float (&v)[V], int lane) {
+  static_assert(V >= 1 && V <= 64 && (V & (V - 1)) == 0, "V: power of two <= 64");
+  reduce_scatter_step<V, 32, V>(v, lane);
+  return v[0];   // the value index lane >> (6 - log2 V)
+}
+
+template <int EPI, int MR, int R, int NCH>
+__global__ __launch_bounds__(256) void k_mgemv_s(ProjArgs a) {
+  constexpr int KP = NCH * 512, V = R * MR;
+  constexpr int SH = V >= 64 ? 0 : V >= 32 ? 1 : V >= 16 ? 2 : V >= 8 ? 3 : V >= 4 ? 4 : V >= 2 ? 5 : 6;
+  extern __shared__ __attribute__((aligned(16))) f16 xsh[];   // [MR][KP] activation rows
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int n0 = (blockIdx.x * 4 + wid) * R;
+  const int K = a.K, M = a.M;
+  // 1. activation rows -> LDS (zero past K, rows >= M not staged: their results are dropped)
+  {
+    constexpr int NV = MR * KP / 8, PER = (NV + 255) / 256;
+    f16x8 t[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int v = i * 256 + threadIdx.x;
+      const int m = v / (KP / 8), k = (v % (KP / 8)) * 8;
+      t[i] = (v < NV && m < M && k < K) ? *(const f16x8*)(a.A + (size_t)m * a.lda + k) : (f16x8){};
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int v = i * 256 + threadIdx.x;
+      if (v < NV) *(f16x8*)(xsh + (size_t)v * 8) = t[i];
+    }
+  }
+  // 2. the weight stream, every load of the wave's R rows in flight at once
+  int kc[NCH];
+  bool kin[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int k = c * 512 + lane * 8;
+    kin[c] = k < K;
+    kc[c] = kin[c] ? k : K - 8;
+  }
+  f16x8 wv[R][NCH];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int n = n0 + r < a.N ? n0 + r : a.N - 1;
+    const f16* w = a.B + (size_t)n * a.ldb;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const f16x8 t = *(const f16x8*)(w + kc[c]);
+      wv[r][c] = kin[c] ? t : (f16x8){};
+    }
+  }
+  // epilogue operands of the (weight row, activation row) this lane stores
+  const int j = lane >> SH, jr = j / MR, jm = j % MR;
+  const bool st = (lane & ((1 << SH) - 1)) == 0 && n0 + jr < a.N && jm < M;
+  const int nst = n0 + jr < a.N ? n0 + jr : a.N - 1, mst = jm < M ? jm : 0;
+  const float pbias = a.bias ? a.bias[nst] : 0.f;
+  float pold = 0.f;
+  if constexpr (EPI == EPI_F32_RESID) pold = ((const float*)a.out)[(size_t)mst * a.ldo + nst];
+  long long cdst = 0;
+  if constexpr (EPI == EPI_QKV_CACHE) cdst = a.row_seq[mst] * a.seq_stride + (long long)a.row_pos[mst] * a.d;
+  __syncthreads();
+  // 3. dot products chunk by chunk (k_mgemv's order), one reduce-scatter, fused epilogue
+  float acc[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) acc[i] = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      const f16x8 xv = *(const f16x8*)(xsh + m * KP + c * 512 + lane * 8);
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r * MR + m] = dot8(wv[r][c], xv, acc[r * MR + m]);
+    }
+  }
+  float v = reduce_scatter<V>(acc, lane);
+  if (!st) return;
+  v += pbias;
+  const size_t o = (size_t)jm * a.ldo + nst;
+  if constexpr (EPI == EPI_F16) {
+    ((f16*)a.out)[o] = (f16)v;
+  } else if constexpr (EPI == EPI_F16_GELU) {
+    ((f16*)a.out)[o] = (f16)gelu_tanh(v);
+  } else if constexpr (EPI == EPI_F32_RESID) {
+    ((float*)a.out)[o] = pold + v;
+  } else if constexpr (EPI == EPI_F32) {
+    ((float*)a.out)[o] = v;
+  } else if constexpr (EPI == EPI_QKV_CACHE) {
+    if (nst < a.d) ((f16*)a.out)[o] = (f16)v;
+    else if (nst < 2 * a.d) a.kc[cdst + nst - a.d] = (f16)v;
+    else a.vc[cdst + nst - 2 * a.d] = (f16)v;
+  } else {
+    epi_store<EPI>(a, jm, nst, v - pbias);
+  }
+}
+
 // General GEMV (optional LN prologue through LDS for 2 < M <= 8).
 template <int EPI, int MR, bool LN>
 __global__ __launch_bounds__(256) void k_gemv(ProjArgs a) {
@@ -865,6 +984,23 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
 
 
 // WDR_SKINNY_MSPLIT=0: narrow skinny GEMMs keep all row tiles in one workgroup (A/B runs)
+// WDR_MGEMV_STAGED=0: 3..16-row GEMVs without LN on k_mgemv (rows re-read from L2 per wave)
+static bool mgemv_staged() {
+  static const bool on = [] {
+    const char* e = getenv("WDR_MGEMV_STAGED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+// WDR_MGEMV_R=1|2|4: weight rows per wave of k_mgemv_s (default 2 for N >= 1024, else 1)
+static int mgemv_rows() {
+  static const int r = [] {
+    const char* e = getenv("WDR_MGEMV_R");
+    const int v = e ? atoi(e) : 0;
+    return (v == 1 || v == 2 || v == 4) ? v : 0;
+  }();
+  return r;
+}
 static bool skinny_msplit_off() {
   const char* e = getenv("WDR_SKINNY_MSPLIT");
   return e && atoi(e) == 0;
@@ -925,6 +1061,42 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
       }
 #undef WDR_DG_N
 #undef WDR_DG
+    } else if (!ln && mgemv_staged() && a.K <= 5120 && (a.K % 512 == 0 || a.K <= 1536) &&
+               (a.M <= 8 || a.K <= 1536)) {
+      // 3..16 rows without LN: activation rows staged in LDS once per workgroup, one
+      // reduce-scatter per wave (k_mgemv_s)
+      const int rq = mgemv_rows();
+      // tools/gemv_bench GB_ROWS: one weight row per wave except the wide projections
+      // (qkv / fc1) of 9..16-row steps, where two halve the activation staging per weight byte
+      const int R = rq ? rq : (a.M > 8 && a.N >= 2048 ? 2 : 1);
+      dim3 g2(cdiv(a.N, 4 * R));
+      const int MRr = a.M <= 4 ? 4 : a.M <= 8 ? 8 : 16;
+      const uint32_t lds = (uint32_t)MRr * nch * 512 * 2;
+#define WDR_MS(MR, RR, NCH) wdr_launch(PROF_GEMV, bytes, flops, k_mgemv_s<EPI, MR, RR, NCH>, g2, blk, lds, s, a);
+#define WDR_MS_N(MR, RR)                         \
+  switch (nch) {                                 \
+    case 1: WDR_MS(MR, RR, 1) break;             \
+    case 2: WDR_MS(MR, RR, 2) break;             \
+    case 3: WDR_MS(MR, RR, 3) break;             \
+    case 4: WDR_MS(MR, RR, 4) break;             \
+    case 6: WDR_MS(MR, RR, 6) break;             \
+    case 8: WDR_MS(MR, RR, 8) break;             \
+    default: WDR_MS(MR, RR, 10) break;           \
+  }
+#define WDR_MS_R(MR)                                                        \
+  if (R == 1) { WDR_MS_N(MR, 1) } else if (R == 2) { WDR_MS_N(MR, 2) } else { WDR_MS_N(MR, 4) }
+      if (MRr == 4) { WDR_MS_R(4) }
+      else if (MRr == 8) { WDR_MS_R(8) }
+      else {
+        switch (nch) {
+          case 1: if (R == 1) { WDR_MS(16, 1, 1) } else if (R == 2) { WDR_MS(16, 2, 1) } else { WDR_MS(16, 4, 1) } break;
+          case 2: if (R == 1) { WDR_MS(16, 1, 2) } else if (R == 2) { WDR_MS(16, 2, 2) } else { WDR_MS(16, 4, 2) } break;
+          default: if (R == 1) { WDR_MS(16, 1, 3) } else if (R == 2) { WDR_MS(16, 2, 3) } else { WDR_MS(16, 4, 3) } break;
+        }
+      }
+#undef WDR_MS_R
+#undef WDR_MS_N
+#undef WDR_MS
     } else if ((ln && a.K <= 1536) || (!ln && a.K <= 5120 && (a.K % 512 == 0 || a.K <= 1536))) {
       // 3..8 rows (multi-chain batched steps): weight stream as k_dgemv, rows through LDS / L2
       const int R = a.N >= 1024 ? 2 : 1;

@@ -167,6 +167,7 @@ class StepBatcher {
   void step(Req& r);           // blocks until the batch holding r has run
   void run(std::vector<Req*>& batch) { launch(batch); }   // one batch, caller's thread (test seam)
   long long launches = 0, rows = 0;
+  double step_s = 0;           // wall of the launches (submit -> results on the host)
   struct Impl;
 
  private:

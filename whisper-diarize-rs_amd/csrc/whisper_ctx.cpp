@@ -1049,7 +1049,7 @@ void decode_step_layers(const Context& ctx, const StepIO& io, int R, hipStream_t
   const int ldxkv = L * 2 * d;
   // more than ln_split rows: the LayerNorm of the rows runs once into io.attd (free at every
   // LN point of the layer) instead of in every GEMV workgroup
-  static const int ln_split = getenv("WDR_STEP_LN_SPLIT") ? atoi(getenv("WDR_STEP_LN_SPLIT")) : 8;
+  static const int ln_split = getenv("WDR_STEP_LN_SPLIT") ? atoi(getenv("WDR_STEP_LN_SPLIT")) : 2;
   auto P = [&](const f16* A, int lda, const f16* W, const float* b, void* out, int ldo, int N, int K, int epi,
                const float* lng = nullptr, const float* lnb = nullptr) {
     ProjArgs a{A, lda, W, K, b, out, ldo, nullptr, 0, R, N, K, epi};
@@ -2340,6 +2340,7 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
                           m.tokout.as<TokOut>(), m.s);
     WDR_HIP(hipMemcpyAsync(m.h_tok, m.tokout.p, R * sizeof(TokOut), hipMemcpyDeviceToHost, m.s));
   };
+  const double t_step = now_s();
   const bool sampled = prof_step();
   if (sampled || getenv("WDR_NO_GRAPH")) {
     // sampled step for live kernel timing (prof.h), or graphs disabled
@@ -2384,6 +2385,7 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
   }
   launches++;
   rows += R;
+  step_s += now_s() - t_step;
 }
 
 }  // namespace wdr

@@ -80,7 +80,8 @@ class StageTimes(C.Structure):
     _fields_ = [("mel", f64), ("encode", f64), ("decode", f64), ("dtw", f64), ("vad", f64), ("total", f64),
                 ("windows", i64), ("decode_steps", i64), ("prefills", i64), ("lang", f64), ("prompt_gpu", f64),
                 ("embed", f64), ("chains", i64), ("batch_launches", i64), ("batch_rows", i64),
-                ("fixup_segments", i64), ("replay_segments", i64), ("spec_s", f64), ("fixup_s", f64)]
+                ("fixup_segments", i64), ("replay_segments", i64), ("spec_s", f64), ("fixup_s", f64),
+                ("batch_step_s", f64)]
 
 
 class Token(C.Structure):
