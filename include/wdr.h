@@ -294,6 +294,8 @@ int wdr_dbg_discrete(const float* w, size_t n, uint32_t seed, int32_t n_draws, i
 int wdr_dbg_dtw_dp(const float* x, int32_t rows, int32_t cols, int32_t seek, int32_t* times_out, int32_t* n_times);
 int wdr_dbg_proj(const uint16_t* a_f16, const uint16_t* w_f16, const float* bias, int32_t M, int32_t N, int32_t K,
                  int32_t epi, float* out /* [M][N] f32 (f16 epilogues are widened) */);
+/* epi | WDR_DBG_PROJ_STEP selects the decode-step GEMV schedule (M <= 16 rows) */
+#define WDR_DBG_PROJ_STEP 0x100
 int wdr_dbg_attn(const uint16_t* q, const uint16_t* k, const uint16_t* v, int32_t Tq, int32_t Tk, int32_t n_head,
                  int32_t causal, float* out /* [Tq][n_head*64] */);
 

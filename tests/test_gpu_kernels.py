@@ -53,6 +53,32 @@ def test_projection_matches_fp32_reference(lib, M):
     np.testing.assert_allclose(_proj(lib, a, w, bias, 2, base), base + ref, rtol=0, atol=2e-4)
 
 
+STEP = 0x100   # include/wdr.h WDR_DBG_PROJ_STEP
+
+
+@pytest.mark.parametrize("N,K,epi", [(1280, 5120, 2), (1280, 4096, 2), (1280, 1280, 2), (3840, 1280, 0),
+                                     (5120, 1280, 1)])
+def test_step_projection_rows_bit_identical(lib, N, K, epi):
+    """Decode-step GEMV schedule (ProjArgs::step_rows): every row of an M-row step (M = 1..16:
+    k_dgemv, k_mgemv_s 4/8/16-row images, the K > 3072 two-pass 8-row image) must equal the
+    1-row step's result for that row bit for bit -- batched chains depend on it -- and match
+    the fp64 product within f16-operand accumulation error."""
+    rng = np.random.default_rng(N + K + epi)
+    a = rng.standard_normal((16, K)).astype(np.float16).astype(np.float32)
+    w = (rng.standard_normal((N, K)) * 0.03).astype(np.float16).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32) * 0.1
+    base = rng.standard_normal((16, N)).astype(np.float32)
+    ref = a.astype(np.float64) @ w.T.astype(np.float64) + bias
+    one = np.concatenate([_proj(lib, a[i:i + 1], w, bias, epi | STEP, base[i:i + 1] if epi == 2 else None)
+                          for i in range(16)])
+    want = {0: ref, 1: _gelu(ref), 2: base + ref}[epi]
+    tol = dict(rtol=0, atol=2e-4) if epi == 2 else dict(rtol=2e-3, atol=2e-3)
+    np.testing.assert_allclose(one, want, **tol)
+    for M in (2, 3, 5, 8, 9, 12, 16):
+        got = _proj(lib, a[:M], w, bias, epi | STEP, base[:M] if epi == 2 else None)
+        np.testing.assert_array_equal(got, one[:M], err_msg="M=%d" % M)
+
+
 def test_projection_logits_shape(lib):
     """decoder logits: N not a multiple of the tile (51866 x d), M = 1 (GEMV path)."""
     rng = np.random.default_rng(7)

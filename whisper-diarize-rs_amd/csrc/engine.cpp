@@ -1670,10 +1670,14 @@ int wdr_dbg_proj(const uint16_t* a16, const uint16_t* w16, const float* bias, in
     WDR_HIP(hipMemcpy(da.p, a16, da.bytes, hipMemcpyHostToDevice));
     WDR_HIP(hipMemcpy(dw.p, w16, dw.bytes, hipMemcpyHostToDevice));
     if (bias) WDR_HIP(hipMemcpy(db.p, bias, db.bytes, hipMemcpyHostToDevice));
+    // epi | WDR_DBG_PROJ_STEP: the decode-step schedule (ProjArgs::step_rows, 9..16-row shapes)
+    const bool step = (epi & 0x100) != 0;
+    epi &= 0xff;
     const bool f16out = epi == EPI_F16 || epi == EPI_F16_GELU;
     std::vector<f16> h16;
     if (!f16out) WDR_HIP(hipMemcpy(dout.p, out, dout.bytes, hipMemcpyHostToDevice));
     ProjArgs a{da.as<f16>(), K, dw.as<f16>(), K, bias ? db.as<float>() : nullptr, dout.p, N, nullptr, 0, M, N, K, epi};
+    a.step_rows = step ? 1 : 0;
     launch_proj(a, nullptr);
     WDR_HIP(hipDeviceSynchronize());
     if (f16out) {

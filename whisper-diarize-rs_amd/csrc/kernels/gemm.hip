@@ -728,30 +728,38 @@ __device__ __forceinline__ float reduce_scatter(float (&v)[V], int lane) {
   return v[0];   // the value index lane >> (6 - log2 V)
 }
 
-template <int EPI, int MR, int R, int NCH>
+// NP > 1: the M <= MR * NP rows go through the LDS image MR at a time (pass p covers rows
+// p*MR .. p*MR + MR - 1) with the wave's weight rows held in registers across the passes, so a
+// K = 5120 projection (fc2) of a 9..16-row step streams its weights once from one launch
+// within an 8-row LDS image; the next pass's rows are loaded while the current one is
+// multiplied.  Per row, the arithmetic is that of the NP = 1 kernel.
+template <int EPI, int MR, int R, int NCH, int NP = 1>
 __global__ __launch_bounds__(256) void k_mgemv_s(ProjArgs a) {
   constexpr int KP = NCH * 512, V = R * MR;
   constexpr int SH = V >= 64 ? 0 : V >= 32 ? 1 : V >= 16 ? 2 : V >= 8 ? 3 : V >= 4 ? 4 : V >= 2 ? 5 : 6;
+  constexpr int NV = MR * KP / 8, PER = (NV + 255) / 256;
   extern __shared__ __attribute__((aligned(16))) f16 xsh[];   // [MR][KP] activation rows
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int n0 = (blockIdx.x * 4 + wid) * R;
   const int K = a.K, M = a.M;
-  // 1. activation rows -> LDS (zero past K, rows >= M not staged: their results are dropped)
-  {
-    constexpr int NV = MR * KP / 8, PER = (NV + 255) / 256;
-    f16x8 t[PER];
+  // 1. activation rows -> registers (zero past K, rows >= M not staged: their results are dropped)
+  f16x8 t[PER];
+  auto fetch = [&](int p) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int v = i * 256 + threadIdx.x;
-      const int m = v / (KP / 8), k = (v % (KP / 8)) * 8;
+      const int m = v / (KP / 8) + p * MR, k = (v % (KP / 8)) * 8;
       t[i] = (v < NV && m < M && k < K) ? *(const f16x8*)(a.A + (size_t)m * a.lda + k) : (f16x8){};
     }
+  };
+  auto put = [&]() {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int v = i * 256 + threadIdx.x;
       if (v < NV) *(f16x8*)(xsh + (size_t)v * 8) = t[i];
     }
-  }
+  };
+  fetch(0);
   // 2. the weight stream, every load of the wave's R rows in flight at once
   int kc[NCH];
   bool kin[NCH];
@@ -768,51 +776,67 @@ __global__ __launch_bounds__(256) void k_mgemv_s(ProjArgs a) {
     const f16* w = a.B + (size_t)n * a.ldb;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      const f16x8 t = *(const f16x8*)(w + kc[c]);
-      wv[r][c] = kin[c] ? t : (f16x8){};
+      const f16x8 tw = *(const f16x8*)(w + kc[c]);
+      wv[r][c] = kin[c] ? tw : (f16x8){};
     }
   }
-  // epilogue operands of the (weight row, activation row) this lane stores
+  put();
+  // epilogue operands of the (weight row, activation row) this lane stores, per pass
   const int j = lane >> SH, jr = j / MR, jm = j % MR;
-  const bool st = (lane & ((1 << SH) - 1)) == 0 && n0 + jr < a.N && jm < M;
-  const int nst = n0 + jr < a.N ? n0 + jr : a.N - 1, mst = jm < M ? jm : 0;
+  const bool lead = (lane & ((1 << SH) - 1)) == 0 && n0 + jr < a.N;
+  const int nst = n0 + jr < a.N ? n0 + jr : a.N - 1;
   const float pbias = a.bias ? a.bias[nst] : 0.f;
-  float pold = 0.f;
-  if constexpr (EPI == EPI_F32_RESID) pold = ((const float*)a.out)[(size_t)mst * a.ldo + nst];
-  long long cdst = 0;
-  if constexpr (EPI == EPI_QKV_CACHE) cdst = a.row_seq[mst] * a.seq_stride + (long long)a.row_pos[mst] * a.d;
-  __syncthreads();
-  // 3. dot products chunk by chunk (k_mgemv's order), one reduce-scatter, fused epilogue
-  float acc[V];
+  float pold[NP];
+  long long cdst[NP];
 #pragma unroll
-  for (int i = 0; i < V; ++i) acc[i] = 0.f;
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-#pragma unroll
-    for (int m = 0; m < MR; ++m) {
-      const f16x8 xv = *(const f16x8*)(xsh + m * KP + c * 512 + lane * 8);
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[r * MR + m] = dot8(wv[r][c], xv, acc[r * MR + m]);
-    }
+  for (int p = 0; p < NP; ++p) {
+    const int mr = jm + p * MR, mst = mr < M ? mr : 0;
+    pold[p] = 0.f;
+    cdst[p] = 0;
+    if constexpr (EPI == EPI_F32_RESID) pold[p] = ((const float*)a.out)[(size_t)mst * a.ldo + nst];
+    if constexpr (EPI == EPI_QKV_CACHE) cdst[p] = a.row_seq[mst] * a.seq_stride + (long long)a.row_pos[mst] * a.d;
   }
-  float v = reduce_scatter<V>(acc, lane);
-  if (!st) return;
-  v += pbias;
-  const size_t o = (size_t)jm * a.ldo + nst;
-  if constexpr (EPI == EPI_F16) {
-    ((f16*)a.out)[o] = (f16)v;
-  } else if constexpr (EPI == EPI_F16_GELU) {
-    ((f16*)a.out)[o] = (f16)gelu_tanh(v);
-  } else if constexpr (EPI == EPI_F32_RESID) {
-    ((float*)a.out)[o] = pold + v;
-  } else if constexpr (EPI == EPI_F32) {
-    ((float*)a.out)[o] = v;
-  } else if constexpr (EPI == EPI_QKV_CACHE) {
-    if (nst < a.d) ((f16*)a.out)[o] = (f16)v;
-    else if (nst < 2 * a.d) a.kc[cdst + nst - a.d] = (f16)v;
-    else a.vc[cdst + nst - 2 * a.d] = (f16)v;
-  } else {
-    epi_store<EPI>(a, jm, nst, v - pbias);
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    if (p > 0) {
+      __syncthreads();   // every wave is done with the previous pass's rows
+      put();
+    }
+    if (p + 1 < NP) fetch(p + 1);   // in flight while this pass is multiplied
+    __syncthreads();
+    // 3. dot products chunk by chunk (k_mgemv's order), one reduce-scatter, fused epilogue
+    float acc[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+      for (int m = 0; m < MR; ++m) {
+        const f16x8 xv = *(const f16x8*)(xsh + m * KP + c * 512 + lane * 8);
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r * MR + m] = dot8(wv[r][c], xv, acc[r * MR + m]);
+      }
+    }
+    float v = reduce_scatter<V>(acc, lane);
+    const int mr = jm + p * MR;
+    if (!lead || mr >= M) continue;
+    v += pbias;
+    const size_t o = (size_t)mr * a.ldo + nst;
+    if constexpr (EPI == EPI_F16) {
+      ((f16*)a.out)[o] = (f16)v;
+    } else if constexpr (EPI == EPI_F16_GELU) {
+      ((f16*)a.out)[o] = (f16)gelu_tanh(v);
+    } else if constexpr (EPI == EPI_F32_RESID) {
+      ((float*)a.out)[o] = pold[p] + v;
+    } else if constexpr (EPI == EPI_F32) {
+      ((float*)a.out)[o] = v;
+    } else if constexpr (EPI == EPI_QKV_CACHE) {
+      if (nst < a.d) ((f16*)a.out)[o] = (f16)v;
+      else if (nst < 2 * a.d) a.kc[cdst[p] + nst - a.d] = (f16)v;
+      else a.vc[cdst[p] + nst - 2 * a.d] = (f16)v;
+    } else {
+      epi_store<EPI>(a, mr, nst, v - pbias);
+    }
   }
 }
 
@@ -1001,6 +1025,15 @@ static int mgemv_rows() {
   }();
   return r;
 }
+// WDR_MGEMV_NP2=0: K > 3072 projections of 9..16-row steps as two 8-row launches (the
+// previous schedule) instead of one two-pass launch
+static bool mgemv_np2() {
+  static const bool on = [] {
+    const char* e = getenv("WDR_MGEMV_NP2");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 static bool skinny_msplit_off() {
   const char* e = getenv("WDR_SKINNY_MSPLIT");
   return e && atoi(e) == 0;
@@ -1017,6 +1050,20 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
   const int ob = (EPI == EPI_F32_RESID || EPI == EPI_F32 || EPI == EPI_F32_GELU_POS) ? 4 : 2;
   const double bytes = (double)a.N * a.K * 2 + (double)a.M * a.K * 2 + (double)a.M * a.N * ob;
   const double flops = 2.0 * a.M * a.N * a.K;
+  if (a.step_rows && a.M > 8 && !a.ln_x && a.K > 3072 && mgemv_staged() && mgemv_np2() && a.K <= 5120 &&
+      a.K % 512 == 0) {
+    // 9..16 step rows through a K > 3072 projection (fc2): one launch, two 8-row passes through
+    // the LDS image, the weights streamed once
+    const int nch = a.K / 512;
+    const uint32_t lds = (uint32_t)8 * nch * 512 * 2;
+    dim3 g2(cdiv(a.N, 4)), blk(256);
+    switch (nch) {
+      case 8: wdr_launch(PROF_GEMV, bytes, flops, k_mgemv_s<EPI, 8, 1, 8, 2>, g2, blk, lds, s, a); break;
+      case 10: wdr_launch(PROF_GEMV, bytes, flops, k_mgemv_s<EPI, 8, 1, 10, 2>, g2, blk, lds, s, a); break;
+      default: WDR_CHECK(false, "step GEMV: two-pass staging needs K = 4096 or 5120");
+    }
+    return;
+  }
   if (a.step_rows && a.M > 8 && !a.ln_x && a.K > 3072) {
     // 9..16 step rows through a K > 3072 projection (fc2): two 8-row launches -- the 16-row
     // shape would spill its activation registers; per-row results are unchanged
