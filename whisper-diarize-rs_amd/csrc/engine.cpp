@@ -658,6 +658,39 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
   const long long l0 = sb.launches, r0 = sb.rows;
   const double s0 = sb.step_s;
   const double t_spec = now_s();
+  // dec_in[k]: the prompt chain k's first segment was last decoded from
+  std::vector<Prompt> dec_in(C, e0);
+  std::atomic<long long> fixups{0};
+  // re-decode block k from prompt e, segment by segment, until the prompt leaving a segment
+  // equals the one its successor was decoded from (used by the early and the round fix-ups)
+  auto redo_block = [&](int k, const Prompt& e_in, bool batched) {
+    State& st = state(k);
+    const size_t a = cut[k], b = cut[k + 1];
+    st.batched = batched;
+    struct Guard {
+      State& st;
+      ~Guard() { st.batched = false; }
+    } guard{st};
+    Prompt e = e_in;
+    for (size_t j = a; j < b && !stop; ++j) {
+      const std::vector<float> x = seg_f32(segs[j]);
+      st.reset_rng();
+      if (st.full(with_prompt(params, e), x.data(), (int)x.size(), -1, false) != 0)
+        throw std::runtime_error("failed to transcribe");
+      out[j].res = st.result_all;
+      out[j].lang_id = st.lang_id;
+      out[j].sampled = st.sampled;
+      out[j].rng_after = st.sampled ? st.rng_state() : std::string();
+      e = next_prompt(e, out[j].res);
+      const bool converged = e == spec_out[j];
+      spec_out[j] = e;
+      fixups++;
+      if (converged) break;
+    }
+  };
+  // done[k]: chain k finished its speculative block (and its early fix-up)
+  std::unique_ptr<std::atomic<int>[]> done(new std::atomic<int>[C]);
+  for (int k = 0; k < C; ++k) done[k] = 0;
   auto worker = [&](int k) {
     State& st = state(k);
     try {
@@ -703,6 +736,24 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
       errs[k] = std::current_exception();
       stop = true;
     }
+    // early fix-up: if chain k-1 has already finished, the prompt leaving its block is known
+    // now (as it stands) -- redo block k from it while the other chains' steps are still
+    // running, its rows joining their batches instead of a fix-up round after them.  The
+    // rounds below re-check it against the final prompt, so the result stays exact.
+    try {
+      static const bool early = !(getenv("WDR_EARLY_FIXUP") && getenv("WDR_EARLY_FIXUP")[0] == '0');
+      if (early && !errs[k] && !stop && k > 0 && done[k - 1].load()) {
+        const Prompt et = spec_out[cut[k] - 1];
+        if (et != dec_in[k]) {
+          redo_block(k, et, C > 1);
+          dec_in[k] = et;
+        }
+      }
+    } catch (...) {
+      errs[k] = std::current_exception();
+      stop = true;
+    }
+    done[k] = 1;
   };
   {
     std::atomic<int> live{C};
@@ -733,8 +784,6 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
   // one.  Chain 0 is always exact, so every round fixes at least one more chain.  Each redone
   // segment starts from decoder 0's initial RNG state: no segment before it drew (or the
   // sampled tail below redoes it anyway).
-  std::vector<Prompt> dec_in(C, e0);
-  std::atomic<long long> fixups{0};
   for (;;) {
     std::vector<int> redo;
     std::vector<Prompt> e_true(C);
@@ -745,30 +794,8 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
     if (redo.empty()) break;
     const bool batch = redo.size() > 1;
     auto fix = [&](int k) {
-      State& st = state(k);
       try {
-        const size_t a = cut[k], b = cut[k + 1];
-        st.batched = batch;
-        struct Guard {
-          State& st;
-          ~Guard() { st.batched = false; }
-        } guard{st};
-        Prompt e = e_true[k];
-        for (size_t j = a; j < b && !stop; ++j) {
-          const std::vector<float> x = seg_f32(segs[j]);
-          st.reset_rng();
-          if (st.full(with_prompt(params, e), x.data(), (int)x.size(), -1, false) != 0)
-            throw std::runtime_error("failed to transcribe");
-          out[j].res = st.result_all;
-          out[j].lang_id = st.lang_id;
-          out[j].sampled = st.sampled;
-          out[j].rng_after = st.sampled ? st.rng_state() : std::string();
-          e = next_prompt(e, out[j].res);
-          const bool converged = e == spec_out[j];
-          spec_out[j] = e;
-          fixups++;
-          if (converged) break;
-        }
+        redo_block(k, e_true[k], batch);
       } catch (...) {
         errs[k] = std::current_exception();
         stop = true;

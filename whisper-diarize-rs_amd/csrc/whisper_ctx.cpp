@@ -2385,7 +2385,14 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
   }
   launches++;
   rows += R;
-  step_s += now_s() - t_step;
+  const double t_end = now_s();
+  step_s += t_end - t_step;
+  // WDR_BATCH_LOG=<file>: one line per launch (start s, rows, wall ms) for schedule analysis
+  static FILE* blog = getenv("WDR_BATCH_LOG") ? fopen(getenv("WDR_BATCH_LOG"), "w") : nullptr;
+  if (blog) {
+    fprintf(blog, "%.6f %d %.3f\n", t_step, R, (t_end - t_step) * 1e3);
+    fflush(blog);
+  }
 }
 
 }  // namespace wdr
