@@ -633,11 +633,14 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
     c->chain_st.push_back(std::make_unique<State>(*c->ctx, (int)c->chain_st.size() + 1));
   auto state = [&](int k) -> State& { return k == 0 ? *c->st : *c->chain_st[k - 1]; };
   const bool auto_lang = !o || !o->lang || std::string(o->lang).empty() || std::string(o->lang) == "auto";
-  // contiguous blocks balanced by sample count (each chain at least one segment)
+  // contiguous blocks balanced by estimated decode cost (each chain at least one segment):
+  // tokens grow with the segment's duration, plus a per-segment overhead (prompt prefill,
+  // the SOT / timestamp / EOT steps, DTW re-forward) worth WDR_BALANCE_SEG_S seconds of audio
   std::vector<size_t> cut(C + 1, 0);
   {
+    static const double seg_s = getenv("WDR_BALANCE_SEG_S") ? atof(getenv("WDR_BALANCE_SEG_S")) : 0.0;
     std::vector<double> P(N + 1, 0.0);
-    for (size_t i = 0; i < N; ++i) P[i + 1] = P[i] + (double)segs[i].n_samples;
+    for (size_t i = 0; i < N; ++i) P[i + 1] = P[i] + (double)segs[i].n_samples + seg_s * 16000.0;
     for (int k = 1; k < C; ++k) {
       const double t = P[N] * k / C;
       size_t x = std::lower_bound(P.begin(), P.end(), t) - P.begin();
