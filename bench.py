@@ -164,6 +164,7 @@ def main():
     opts = wdr.TranscribeOptions(model=args.model, lang="auto", enable_vad=not diarize,
                                  enable_diarize=True if diarize else None,
                                  advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    dopts = wdr.DiarizeOptions.from_options(opts) if diarize else None   # src/engine.rs:101-111
     vad = None if diarize else wdr.Vad(gpu_device=local)
     dia = wdr.Diarizer(gpu_device=local) if diarize else None
     lib = wdr._lib.load()
@@ -180,7 +181,7 @@ def main():
             n_seg = len(vad.get_segments(pcm, materialize=False)[1])
         vad_t[0] += time.perf_counter() - t
         vad_t[1] = n_seg
-        return ctx.run_pipeline(segs, opts)
+        return ctx.run_pipeline(segs, opts, diarize_options=dopts)
 
     vad_t = [0.0, 0]
     for _ in range(args.warmup):

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define WDR_ABI_VERSION 1
+#define WDR_ABI_VERSION 2
 
 typedef struct wdr_engine wdr_engine;
 typedef struct wdr_context wdr_context;   /* ~ whisper_rs::WhisperContext (+ its state) */
@@ -73,6 +73,17 @@ typedef struct {
   int8_t has_max_speakers; uint64_t max_speakers;
   const wdr_advanced* advanced;           /* nullable */
 } wdr_transcribe_options;
+
+/* DiarizeOptions, src/types.rs:93-98: built by Engine::transcribe_audio (src/engine.rs:101-111) and
+ * passed to run_transcription_pipeline, whose speaker embeddings + assignment it switches on
+ * (src/transcribe.rs:339-345).  A NULL model path selects synthetic seeded weights (no model
+ * files exist offline); a non-NULL path is loaded or the call fails. */
+typedef struct {
+  const char* segment_model_path;         /* String (segmentation-3.0.onnx) */
+  const char* embedding_model_path;       /* String (wespeaker_en_voxceleb_CAM++.onnx) */
+  float threshold;                        /* f32, the Engine's default 0.5 */
+  uint64_t max_speakers;                  /* usize, the Engine maps None / Some(0) to usize::MAX */
+} wdr_diarize_options;
 
 /* Synthetic-weights / workload knobs (no checkpoints on this machine).
  * Not part of the reference API; NULL everywhere means defaults. */
@@ -147,6 +158,7 @@ typedef struct {
   int64_t chains, batch_launches, batch_rows, fixup_segments, replay_segments;
   double spec_s, fixup_s;
   double batch_step_s;   /* wall of the batched steps (submit -> tokens on the host), summed */
+  int64_t early_fixup_segments;   /* of fixup_segments: re-decoded by the early fix-up */
 } wdr_stage_times;
 
 const char* wdr_last_error(void);
@@ -156,6 +168,10 @@ int wdr_device_count(void);
 /* ---- Engine (whole-call drop-in) ---- */
 int wdr_engine_new(const wdr_engine_config* cfg, wdr_engine** out);
 void wdr_engine_free(wdr_engine* e);
+/* Synthetic mode (an explicit opt-in): models the Engine cannot find on disk (ggml-<model>.bin in
+ * the cache, the VAD / diarization model files) run on synthetic seeded weights.  Without it a
+ * missing whisper model fails with "whisper file doesn't exist" as the reference does
+ * (src/transcribe.rs:99-101), and a missing VAD / diarization model fails likewise. */
 int wdr_engine_set_synthetic(wdr_engine* e, const wdr_synthetic* syn);
 int wdr_transcribe_audio(wdr_engine* e, const char* audio_path, const wdr_transcribe_options* opts,
                          const wdr_formatting_overrides* fmt, const wdr_callbacks* cb, wdr_segment_list** out);
@@ -173,7 +189,8 @@ int wdr_vad_merge(const double* starts_cs, const double* ends_cs, size_t n_segs,
                   double* merged_out /* [2*n_segs] start,end seconds */, int64_t* merged_idx /* [2*n_segs] */,
                   size_t* n_merged);
 /* Silero VAD (src/vad.rs:6-85; whisper.cpp WhisperVadContext + segments_from_samples).
- * Weights are synthetic (seeded) until the ggml loader lands; model_path may be NULL. */
+ * model_path: whisper.cpp's ggml-silero-v5.1.2.bin (loaded, or the call fails); NULL selects
+ * synthetic seeded weights. */
 typedef struct wdr_vad wdr_vad;
 int wdr_vad_create(const char* model_path, int8_t has_gpu_device, int32_t gpu_device, wdr_vad** out);
 void wdr_vad_free(wdr_vad* v);
@@ -192,7 +209,9 @@ int wdr_vad_get_segments(wdr_vad* v, const int16_t* samples, size_t n, double** 
 
 /* pyannote diarization (src/engine.rs:89-122, src/transcribe.rs:339-345, 461-497):
  * segmentation-3.0 + get_segments stitching, Kaldi fbank + CMN, CAM++ embedding.
- * Weights are synthetic (seeded) until the ONNX initializer reader lands; paths may be NULL. */
+ * Paths: the ONNX files (segmentation-3.0.onnx, wespeaker_en_voxceleb_CAM++.onnx), whose
+ * initializers are read by libwdr's own protobuf reader (loaded, or the call fails); NULL selects
+ * synthetic seeded weights for that model. */
 typedef struct wdr_diarizer wdr_diarizer;
 int wdr_diarizer_create(const char* segment_model_path, const char* embedding_model_path, int8_t has_gpu_device,
                         int32_t gpu_device, wdr_diarizer** out);
@@ -226,6 +245,9 @@ int wdr_speakers_new(int8_t has_max_speakers, uint64_t max_speakers, wdr_speaker
 void wdr_speakers_free(wdr_speakers* m);
 int wdr_speakers_assign(wdr_speakers* m, const float* emb, int32_t dim, float threshold, char* id_out, size_t cap);
 
+/* model_path: a whisper.cpp ggml file (missing -> "whisper file doesn't exist").  NULL model_path
+ * with a non-NULL syn selects synthetic seeded weights of the named configuration; NULL with
+ * NULL syn fails like a missing file. */
 int wdr_context_create(const char* model_path, const char* model_name, int8_t has_gpu_device, int32_t gpu_device,
                        int8_t use_gpu, int8_t enable_dtw, int8_t enable_flash_attn, int8_t has_num_samples,
                        uint64_t num_samples, const wdr_synthetic* syn, wdr_context** out);
@@ -234,8 +256,11 @@ void wdr_context_free(wdr_context* c);
  * n_audio_ctx, n_audio_state, n_audio_head, n_audio_layer, n_text_ctx, n_text_state, n_text_head,
  * n_text_layer, n_mels, ftype; wdr_context_create loads such a file when model_path is given */
 int wdr_ggml_info(const char* path, int32_t* hparams, int64_t* n_tensors, int64_t* n_vocab_tokens);
+/* diarize: NULL = no speakers (the reference's `None`); else speaker embeddings of every speech
+ * segment + EmbeddingManager assignment per whisper segment */
 int wdr_run_pipeline(wdr_context* c, const wdr_speech_segment* segs, size_t n_segs, const wdr_transcribe_options* opts,
-                     const wdr_synthetic* syn, const wdr_callbacks* cb, wdr_segment_list** out);
+                     const wdr_diarize_options* diarize, const wdr_synthetic* syn, const wdr_callbacks* cb,
+                     wdr_segment_list** out);
 /* run_pipeline without the cross-segment overlap clip and without speaker assignment, with
  * speech_index set: building block of the multi-GPU one-file path (wdr/distributed.py), which
  * applies both over the merged, ordered blocks of every GPU */
@@ -247,6 +272,10 @@ void wdr_segment_list_free(wdr_segment_list* l);
  * prompt-chain fix-up (results identical to one chain).  Default WDR_DECODE_CHAINS or 16,
  * capped by the context's KV pool (max chains fixed at creation).  Not in the Rust API. */
 int wdr_context_set_chains(wdr_context* c, int32_t n);
+/* test seam: early prompt fix-up 0 off, 1 when the predecessor chain already finished (default),
+ * 2 always (chain k waits for chain k-1, then redoes its first segments from the known prompt);
+ * -1 restores the WDR_EARLY_FIXUP environment default */
+int wdr_dbg_set_early_fixup(wdr_context* c, int32_t mode);
 int wdr_context_stage_times(wdr_context* c, wdr_stage_times* out);
 int wdr_context_hparams(wdr_context* c, int32_t* out /* [10] */);
 

@@ -16,7 +16,7 @@ def test_library_exports_every_header_symbol(lib):
     assert len(syms) >= 25
     missing = [s for s in syms if not hasattr(lib, s)]
     assert not missing, missing
-    assert lib.wdr_abi_version() == 1
+    assert lib.wdr_abi_version() == 2
 
 
 def _wav(path, samples, ch=1, rate=16000, bits=16, fmt=1):
@@ -55,6 +55,34 @@ def test_transcribe_audio_missing_file_message():
     e = wdr.Engine(wdr.EngineConfig())
     with pytest.raises(wdr.WdrError, match="audio file doesn't exist"):
         e.transcribe_audio("/nonexistent/x.wav", wdr.TranscribeOptions())
+
+
+def test_missing_whisper_model_fails_like_the_reference(tmp_path):
+    """No ggml-<model>.bin in the cache and no explicit synthetic mode: transcribe_audio fails
+    with the reference's "whisper file doesn't exist" (src/transcribe.rs:99-101) before touching
+    the GPU -- it never falls back to random weights silently."""
+    from oracle.pipeline import write_wav
+    wav = str(tmp_path / "a.wav")
+    write_wav(wav, np.zeros(16000, np.int16))
+    e = wdr.Engine(wdr.EngineConfig(cache_dir=str(tmp_path / "empty_cache")))
+    for model in ("base.en", "large-v3", "tiny-test"):
+        with pytest.raises(wdr.WdrError, match="whisper file doesn't exist"):
+            e.transcribe_audio(wav, wdr.TranscribeOptions(model=model, enable_vad=False))
+    # create_context: a missing path, and no path without synthetic mode
+    with pytest.raises(wdr.WdrError, match="whisper file doesn't exist"):
+        wdr.WhisperContext("base.en", model_path=str(tmp_path / "ggml-base.en.bin"))
+    with pytest.raises(wdr.WdrError, match="whisper file doesn't exist"):
+        wdr.WhisperContext("base.en")
+
+
+def test_missing_vad_and_diarize_model_files_fail(tmp_path):
+    """A model path that does not exist is an error, never a silent synthetic fallback."""
+    with pytest.raises(wdr.WdrError, match="VAD model file doesn't exist"):
+        wdr.Vad(model_path=str(tmp_path / "ggml-silero-v5.1.2.bin"))
+    with pytest.raises(wdr.WdrError, match="diarization model file doesn't exist"):
+        wdr.Diarizer(segment_model_path=str(tmp_path / "segmentation-3.0.onnx"))
+    with pytest.raises(wdr.WdrError, match="diarization model file doesn't exist"):
+        wdr.Diarizer(embedding_model_path=str(tmp_path / "cam.onnx"))
 
 
 def test_vad_merge_matches_reference_glue():

@@ -18,9 +18,9 @@ def _segs(pcm, spurts):
     return [wdr.SpeechSegment(a, b, pcm[int(round(a * 16000)):int(round(b * 16000))]) for a, b, _ in spurts]
 
 
-def _run(ctx, segs, opts, chains):
+def _run(ctx, segs, opts, chains, dopts=None):
     ctx.set_chains(chains)
-    out, lang = ctx.run_pipeline(segs, opts)
+    out, lang = ctx.run_pipeline(segs, opts, diarize_options=dopts)
     return [dataclasses.asdict(s) for s in out], lang
 
 
@@ -39,9 +39,10 @@ def test_chains_equal_single_chain(name, seconds, fallback, diarize):
     assert len(segs) >= 6
     opts = wdr.TranscribeOptions(lang="auto", enable_diarize=True if diarize else None,
                                  advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
-    ref, lang1 = _run(ctx, segs, opts, 1)
+    dopts = wdr.DiarizeOptions.from_options(opts) if diarize else None
+    ref, lang1 = _run(ctx, segs, opts, 1, dopts)
     for chains in (2, 4):
-        got, lang = _run(ctx, segs, opts, chains)
+        got, lang = _run(ctx, segs, opts, chains, dopts)
         assert lang == lang1
         assert [s["text"] for s in got] == [s["text"] for s in ref], chains
         assert got == ref, chains
@@ -64,4 +65,30 @@ def test_sixteen_chains_equal_single_chain(name, seconds, monkeypatch):
     assert ctx.stage_times()["chains"] == 16
     assert lang == lang1
     assert got == ref
+    ctx.close()
+
+
+@pytest.mark.parametrize("fallback", [False, True])
+def test_forced_early_fixup_is_exact(fallback):
+    """The early prompt fix-up (a chain redoes its first segments from its predecessor's final
+    prompt while the others still decode) forced on through the wdr_dbg_set_early_fixup seam:
+    it must run (nonzero count) and give the one-chain result, as must the run with it off.
+    With fallback on, segments fall back to t > 0 sampling, so a redone segment's RNG state and
+    the sampled-tail replay are exercised too."""
+    syn = wdr.Synthetic(weight_std=0.02, emb_std=0.5, force_len_rate=0.0 if fallback else 3.3,
+                        disable_fallback=not fallback)
+    ctx = wdr.WhisperContext("tiny-test", synthetic=syn)
+    pcm, spurts = synth_speech(60.0, seed=13, n_speakers=2)
+    segs = _segs(pcm, spurts)
+    opts = wdr.TranscribeOptions(lang="auto", advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    ref, lang1 = _run(ctx, segs, opts, 1)
+    ctx.set_early_fixup(2)
+    got, lang = _run(ctx, segs, opts, 4)
+    st = ctx.stage_times()
+    assert st["early_fixup_segments"] > 0, st
+    assert lang == lang1 and got == ref
+    ctx.set_early_fixup(0)
+    got0, _ = _run(ctx, segs, opts, 4)
+    assert ctx.stage_times()["early_fixup_segments"] == 0
+    assert got0 == ref
     ctx.close()

@@ -103,7 +103,7 @@ def test_pipeline_assigns_speakers_like_the_reference_glue(dz, audio):
     for max_spk, thr in ((None, 0.5), (2, 0.9999)):
         opts = wdr.TranscribeOptions(lang="en", enable_diarize=True, max_speakers=max_spk,
                                      advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy", diarize_threshold=thr))
-        got, _ = ctx.run_pipeline(segs, opts)
+        got, _ = ctx.run_pipeline(segs, opts, diarize_options=wdr.DiarizeOptions.from_options(opts))
         plain, _ = ctx.run_pipeline(segs, wdr.TranscribeOptions(
             lang="en", advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy")))
         assert [s.text for s in got] == [s.text for s in plain]
@@ -123,7 +123,7 @@ def test_engine_transcribe_audio_with_diarize(tmp_path, dz):
     got = eng.transcribe_audio(path, opts)
     segs = dz.get_segments(pcm)
     ctx = wdr.WhisperContext("tiny-test", synthetic=SYN)
-    want, lang = ctx.run_pipeline(segs, opts)
+    want, lang = ctx.run_pipeline(segs, opts, diarize_options=wdr.DiarizeOptions.from_options(opts))
     want = wdr.process_segments(want, lang or "en")   # no VAD mask on the diarize branch
     assert [(s.text, s.speaker_id, round(s.start, 6)) for s in got] == \
         [(s.text, s.speaker_id, round(s.start, 6)) for s in want]

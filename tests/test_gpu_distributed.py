@@ -56,7 +56,8 @@ def test_two_ranks_match_one_process(tmp_path, seg):
     # synthetic workload pin (as bench.py): the segmentation kernels run on the ranks, the
     # speech segments handed downstream are the generator's talk spurts
     segs = [wdr.SpeechSegment(a, b, pcm[int(round(a * 16000)):int(round(b * 16000))]) for a, b in spurts]
-    ref, lang = ctx.run_pipeline(segs, opts)
+    ref, lang = ctx.run_pipeline(segs, opts, diarize_options=wdr.DiarizeOptions.from_options(opts)
+                                 if seg == "diarize" else None)
     ctx.close()
     assert len(ref) >= 4
     assert got["lang"] == lang

@@ -59,7 +59,8 @@ struct SegModel::W {
   DevMem pcm, x, col, s1, p1, s2, p2, s3, p3, xg, h0, h1, la, lb, z, cls;
 };
 
-SegModel::SegModel(int dev) : device(dev) {
+SegModel::SegModel(int dev, const std::string& path) : device(dev) {
+  if (!path.empty()) throw std::runtime_error("segmentation model file: ONNX loading not available yet: " + path);
   WDR_HIP(hipSetDevice(dev));
   WDR_HIP(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking));
   WDR_HIP(hipEventCreate(&e0_));
@@ -294,7 +295,8 @@ struct CamModel::W {
 
 static double mel_k(double f) { return 1127.0 * std::log(1.0 + f / 700.0); }
 
-CamModel::CamModel(int dev) : device(dev) {
+CamModel::CamModel(int dev, const std::string& path) : device(dev) {
+  if (!path.empty()) throw std::runtime_error("embedding model file: ONNX loading not available yet: " + path);
   WDR_HIP(hipSetDevice(dev));
   // lowest priority: embeddings run beside the latency-bound decode chain (EmbedAhead)
   int lo = 0, hi = 0;

@@ -24,7 +24,8 @@ std::vector<DiarSegment> diar_stitch(const std::vector<int>& cls, size_t n);
 
 class SegModel {
  public:
-  explicit SegModel(int device);
+  // path: segmentation-3.0.onnx (model_files.cpp); "" = synthetic seeded weights
+  explicit SegModel(int device, const std::string& path = std::string());
   ~SegModel();
   // per-window frame classes (argmax, last max on ties) of the zero-padded file:
   // [n_windows][589]; optionally the log-probabilities [n_windows][589][7]
@@ -43,7 +44,8 @@ class SegModel {
 
 class CamModel {
  public:
-  explicit CamModel(int device);
+  // path: wespeaker_en_voxceleb_CAM++.onnx (model_files.cpp); "" = synthetic seeded weights
+  explicit CamModel(int device, const std::string& path = std::string());
   ~CamModel();
   // EmbeddingExtractor::compute: i16 -> /32768 -> fbank -> CMN -> CAM++ -> [512].
   // Returns false where the reference's ORT call fails (fewer than 400 samples: no frames).

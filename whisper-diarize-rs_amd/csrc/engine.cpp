@@ -224,11 +224,15 @@ struct wdr_context {
   std::unique_ptr<State> st;
   std::vector<std::unique_ptr<State>> chain_st;   // decode chains 1.. (multi-chain pipeline)
   int chains = 1;                                 // decode chains per run_pipeline call
+  // early prompt fix-up: 0 off, 1 when the predecessor chain has already finished (default;
+  // WDR_EARLY_FIXUP=0 turns it off), 2 always (a chain waits for its predecessor: test seam)
+  int early_fixup = -1;
   struct ChainStats {
-    long long chains = 1, launches = 0, rows = 0, fixups = 0, replays = 0;
+    long long chains = 1, launches = 0, rows = 0, fixups = 0, replays = 0, early = 0;
     double spec_s = 0, fixup_s = 0, step_s = 0;
   } cs;                                           // the last run_pipeline's multi-chain figures
   std::unique_ptr<CamModel> cam;   // EmbeddingExtractor, created on the first diarized run
+  std::string cam_path;            // ... from this embedding model file ("" = synthetic weights)
   double load_s = 0;
   double embed_s = 0;              // wall time the decode chain waited on speaker embeddings
 };
@@ -318,14 +322,15 @@ struct wdr_vad {
 
 struct wdr_diarizer {
   int device = 0;
+  std::string seg_path, emb_path;   // "" = synthetic seeded weights
   std::unique_ptr<SegModel> seg;
   std::unique_ptr<CamModel> cam;
   SegModel& S() {
-    if (!seg) seg = std::make_unique<SegModel>(device);
+    if (!seg) seg = std::make_unique<SegModel>(device, seg_path);
     return *seg;
   }
   CamModel& E() {
-    if (!cam) cam = std::make_unique<CamModel>(device);
+    if (!cam) cam = std::make_unique<CamModel>(device, emb_path);
     return *cam;
   }
 };
@@ -334,19 +339,28 @@ struct wdr_speakers {
   std::unique_ptr<SpeakerManager> m;
 };
 
-// DiarizeOptions (src/engine.rs:103-111): threshold default 0.5, max_speakers None/0 -> usize::MAX
-static void diarize_options(const wdr_transcribe_options* o, float* thr, uint64_t* max_spk) {
-  *thr = (o && o->advanced && o->advanced->has_diarize_threshold) ? o->advanced->diarize_threshold : 0.5f;
-  *max_spk = (o && o->has_max_speakers && o->max_speakers != 0) ? o->max_speakers : UINT64_MAX;
+// DiarizeOptions as Engine::transcribe_audio builds it (src/engine.rs:101-111): threshold
+// default 0.5, max_speakers None / Some(0) -> usize::MAX
+static wdr_diarize_options diarize_options(const wdr_transcribe_options* o, const char* seg_path,
+                                           const char* emb_path) {
+  wdr_diarize_options d{};
+  d.segment_model_path = seg_path;
+  d.embedding_model_path = emb_path;
+  d.threshold = (o && o->advanced && o->advanced->has_diarize_threshold) ? o->advanced->diarize_threshold : 0.5f;
+  d.max_speakers = (o && o->has_max_speakers && o->max_speakers != 0) ? o->max_speakers : UINT64_MAX;
+  return d;
 }
 
 struct wdr_engine {
   wdr_engine_config cfg{};
   std::string cache_dir, vad_path, seg_path, emb_path;
   SynCfg syn;
+  bool syn_set = false;   // wdr_engine_set_synthetic: models missing on disk run on seeded weights
   std::map<std::string, std::unique_ptr<wdr_context>> contexts;
   std::unique_ptr<VadModel> vad;
+  std::string vad_loaded;   // model file the VAD was made from ("" = synthetic)
   std::unique_ptr<SegModel> seg;
+  std::string seg_loaded;
 };
 
 // src/vad.rs:6-85 on top of the GPU VAD: probabilities -> whisper.cpp segments (cs) -> the
@@ -412,16 +426,14 @@ static bool file_exists(const char* p) {
   return p && stat(p, &st) == 0;
 }
 
-// The cached whisper.cpp model of `model` under the engine's cache dir, without network:
-// <cache>/ggml-<model>.bin, or the hf-hub layout the reference's model manager uses,
-// <cache>/models--ggerganov--whisper.cpp/snapshots/<rev>/ggml-<model>.bin
-// (src/model_manager.rs:162, 661-681).  Empty when absent (synthetic weights then).
-static std::string find_model_file(const std::string& cache_dir, const std::string& model) {
+// A cached model file under the engine's cache dir, without network: <cache>/<file>, or the
+// hf-hub layout the reference's model manager uses, <cache>/models--<owner>--<repo>/snapshots/
+// <rev>/<file> (src/model_manager.rs:661-681).  Empty when absent.
+static std::string find_cached_file(const std::string& cache_dir, const std::string& hub_dir, const std::string& file) {
   if (cache_dir.empty()) return std::string();
-  const std::string file = "ggml-" + model + ".bin";
   const std::string direct = cache_dir + "/" + file;
   if (file_exists(direct.c_str())) return direct;
-  const std::string snaps = cache_dir + "/models--ggerganov--whisper.cpp/snapshots";
+  const std::string snaps = cache_dir + "/" + hub_dir + "/snapshots";
   std::string found;
   if (DIR* d = opendir(snaps.c_str())) {
     std::vector<std::string> revs;
@@ -438,6 +450,10 @@ static std::string find_model_file(const std::string& cache_dir, const std::stri
     }
   }
   return found;
+}
+// ggml-<model>.bin from ggerganov/whisper.cpp (src/model_manager.rs:148-162)
+static std::string find_model_file(const std::string& cache_dir, const std::string& model) {
+  return find_cached_file(cache_dir, "models--ggerganov--whisper.cpp", "ggml-" + model + ".bin");
 }
 
 // src/transcribe.rs:89-166.  model_path: a whisper.cpp ggml file (hparams, mel filters, vocabulary and weights from it;
@@ -589,6 +605,7 @@ struct SegOut {
   std::vector<ResultSeg> res;
   int lang_id = 0;
   bool sampled = false;            // a t > 0 decoder drew random numbers
+  bool rng_clean = true;           // decoded from decoder 0's initial RNG state (nothing drew before it)
   std::string rng_after;           // decoder 0's RNG right after this segment (when sampled)
 };
 struct Prompt {
@@ -663,10 +680,10 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
   const double t_spec = now_s();
   // dec_in[k]: the prompt chain k's first segment was last decoded from
   std::vector<Prompt> dec_in(C, e0);
-  std::atomic<long long> fixups{0};
+  std::atomic<long long> fixups{0}, early_n{0};
   // re-decode block k from prompt e, segment by segment, until the prompt leaving a segment
   // equals the one its successor was decoded from (used by the early and the round fix-ups)
-  auto redo_block = [&](int k, const Prompt& e_in, bool batched) {
+  auto redo_block = [&](int k, const Prompt& e_in, bool batched, std::atomic<long long>* count) {
     State& st = state(k);
     const size_t a = cut[k], b = cut[k + 1];
     st.batched = batched;
@@ -683,11 +700,12 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
       out[j].res = st.result_all;
       out[j].lang_id = st.lang_id;
       out[j].sampled = st.sampled;
+      out[j].rng_clean = true;   // reset_rng() above
       out[j].rng_after = st.sampled ? st.rng_state() : std::string();
       e = next_prompt(e, out[j].res);
       const bool converged = e == spec_out[j];
       spec_out[j] = e;
-      fixups++;
+      (*count)++;
       if (converged) break;
     }
   };
@@ -720,12 +738,15 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
       } guard{st};
       Prompt e = e0;
       std::vector<DtwTicket> prev_tk;
+      bool drew = false;   // a segment of this block drew before: decoder 0's RNG is no longer initial
       for (size_t i = a; i < b && !stop; ++i) {
         if (st.full(with_prompt(params, e), nullptr, 0, (int)(i - a), true) != 0)
           throw std::runtime_error("failed to transcribe");
         out[i].res = st.result_all;
         out[i].lang_id = st.lang_id;
         out[i].sampled = st.sampled;
+        out[i].rng_clean = !drew;
+        drew = drew || st.sampled;
         if (st.sampled) out[i].rng_after = st.rng_state();
         std::vector<DtwTicket> tk = st.take_dtw_jobs();
         if (i > a)
@@ -744,11 +765,14 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
     // running, its rows joining their batches instead of a fix-up round after them.  The
     // rounds below re-check it against the final prompt, so the result stays exact.
     try {
-      static const bool early = !(getenv("WDR_EARLY_FIXUP") && getenv("WDR_EARLY_FIXUP")[0] == '0');
-      if (early && !errs[k] && !stop && k > 0 && done[k - 1].load()) {
+      const int mode = c->early_fixup >= 0 ? c->early_fixup
+                                           : !(getenv("WDR_EARLY_FIXUP") && getenv("WDR_EARLY_FIXUP")[0] == '0');
+      if (mode == 2 && k > 0)
+        while (!done[k - 1].load() && !stop) std::this_thread::sleep_for(std::chrono::microseconds(200));
+      if (mode > 0 && !errs[k] && !stop && k > 0 && done[k - 1].load()) {
         const Prompt et = spec_out[cut[k] - 1];
         if (et != dec_in[k]) {
-          redo_block(k, et, C > 1);
+          redo_block(k, et, C > 1, &early_n);
           dec_in[k] = et;
         }
       }
@@ -798,7 +822,7 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
     const bool batch = redo.size() > 1;
     auto fix = [&](int k) {
       try {
-        redo_block(k, e_true[k], batch);
+        redo_block(k, e_true[k], batch, &fixups);
       } catch (...) {
         errs[k] = std::current_exception();
         stop = true;
@@ -821,21 +845,27 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
     if (stop) throw std::runtime_error("failed to transcribe");
     for (int k : redo) dec_in[k] = e_true[k];
   }
-  c->cs.fixups = fixups;
-  // random draws: the first segment (file order) that drew is exact; every later one is
-  // re-decoded in order from its RNG state
+  c->cs.fixups = fixups + early_n;
+  c->cs.early = early_n;
+  // random draws: no segment before the first one (file order) that drew did draw, so in the
+  // sequential loop it starts from decoder 0's initial RNG.  If its kept result was decoded from
+  // that state it is exact and the re-decode starts after it (from its RNG state); if not (a
+  // speculative segment before it in its block drew, and the fix-up stopped before redoing it),
+  // the re-decode starts at it, from the initial state.  Every later segment is re-decoded in order.
   size_t f = N;
   for (size_t i = 0; i < N; ++i)
     if (out[i].sampled) {
       f = i;
       break;
     }
-  if (f + 1 < N) {
+  const size_t rs = (f < N && !out[f].rng_clean) ? f : f + 1;
+  if (rs < N) {
     State& st = *c->st;
     Prompt e = e0;
-    for (size_t i = 0; i <= f; ++i) e = next_prompt(e, out[i].res);
-    st.set_rng_state(out[f].rng_after);
-    for (size_t i = f + 1; i < N; ++i) {
+    for (size_t i = 0; i < rs; ++i) e = next_prompt(e, out[i].res);
+    if (rs == f) st.reset_rng();
+    else st.set_rng_state(out[f].rng_after);
+    for (size_t i = rs; i < N; ++i) {
       if (cb && cb->is_cancelled && cb->is_cancelled(cb->user)) throw std::runtime_error("failed to transcribe");
       const std::vector<float> x = seg_f32(segs[i]);
       c->cs.replays++;
@@ -843,6 +873,7 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
         throw std::runtime_error("failed to transcribe");
       out[i].res = st.result_all;
       out[i].lang_id = st.lang_id;
+      out[i].sampled = st.sampled;
       e = next_prompt(e, out[i].res);
     }
   }
@@ -864,15 +895,24 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
 // src/transcribe.rs:323-535
 // raw: per-segment results only (no overlap clip against the next segment, no speakers): the
 // multi-GPU path (wdr/distributed.py) merges several GPUs' raw blocks and applies both in order.
+// dopts: DiarizeOptions (src/transcribe.rs:327, 339-345); its presence switches speakers on.
 static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speech_segment>& segs,
-                                     const wdr_transcribe_options* o, const SynCfg& syn, const wdr_callbacks* cb,
-                                     std::string* detected_lang, bool* has_lang, bool raw = false) {
-  const bool diarize = o && o->enable_diarize == 1 && !raw;
-  float dthr = 0.5f;
-  uint64_t dmax = UINT64_MAX;
-  diarize_options(o, &dthr, &dmax);
-  SpeakerManager speakers(dmax);
-  if (diarize && !c->cam) c->cam = std::make_unique<CamModel>(c->ctx->cp.gpu_device);
+                                     const wdr_transcribe_options* o, const wdr_diarize_options* dopts,
+                                     const SynCfg& syn, const wdr_callbacks* cb, std::string* detected_lang,
+                                     bool* has_lang, bool raw = false) {
+  const bool diarize = dopts != nullptr && !raw;
+  const float dthr = dopts ? dopts->threshold : 0.5f;
+  SpeakerManager speakers(dopts ? dopts->max_speakers : UINT64_MAX);
+  if (diarize) {
+    // EmbeddingExtractor::new(&diarize_options.embedding_model_path) (src/transcribe.rs:343)
+    const std::string path = dopts->embedding_model_path ? dopts->embedding_model_path : "";
+    if (!path.empty() && !file_exists(path.c_str())) throw std::runtime_error("embedding model file doesn't exist: " + path);
+    if (!c->cam || c->cam_path != path) {
+      c->cam.reset();
+      c->cam = std::make_unique<CamModel>(c->ctx->cp.gpu_device, path);
+      c->cam_path = path;
+    }
+  }
   std::unique_ptr<EmbedAhead> embeds;
   if (diarize) embeds = std::make_unique<EmbedAhead>(*c->cam, segs);
   FullParams params = setup_params(o, syn);
@@ -1149,6 +1189,7 @@ void wdr_engine_free(wdr_engine* e) { delete e; }
 int wdr_engine_set_synthetic(wdr_engine* e, const wdr_synthetic* syn) {
   WDR_GUARD({
     e->syn = syn_of(syn);
+    e->syn_set = true;
     e->contexts.clear();
     return 0;
   })
@@ -1159,38 +1200,77 @@ int wdr_transcribe_audio(wdr_engine* e, const char* audio_path, const wdr_transc
   WDR_GUARD({
     if (!audio_path || !file_exists(audio_path)) return fail("audio file doesn't exist");
     const std::string model = (o && o->model) ? o->model : "base";
+    // ModelManager::ensure_whisper_model (src/engine.rs:78-81): the cached ggml file, offline.
+    // No file: the reference's create_context fails "whisper file doesn't exist"
+    // (src/transcribe.rs:99-101) unless synthetic weights were asked for explicitly.
+    auto it = e->contexts.find(model);
+    std::string model_path;
+    if (it == e->contexts.end()) {
+      model_path = find_model_file(e->cache_dir, model);
+      if (model_path.empty() && !e->syn_set) return fail("whisper file doesn't exist");
+    }
+    if (o && o->translate_target && !(o->whisper_to_english == 1))
+      return fail("translate_target: network translation is out of scope for libwdr");
     std::vector<int16_t> pcm = read_wav_impl(audio_path);
     std::vector<wdr_speech_segment> segs;
     std::vector<int16_t> dpad;   // owns the samples of pyannote segments (they index the padded buffer)
     std::vector<std::pair<double, double>> vad_mask;   // VadMaskOracle input (VAD branch only)
     bool have_mask = false;
     const bool vad = !o || o->enable_vad == 1;   // `if let Some(true) = options.enable_vad` (src/engine.rs:123)
+    const int dev = e->cfg.has_gpu_device ? e->cfg.gpu_device : 0;
+    // a model file from the config, else the cache; absent -> synthetic (opt-in) or an error
+    auto resolve = [&](const std::string& cfg_path, const std::string& hub, const std::string& file,
+                       const char* what) -> std::string {
+      if (!cfg_path.empty()) {
+        if (!file_exists(cfg_path.c_str())) throw std::runtime_error(std::string(what) + " file doesn't exist: " + cfg_path);
+        return cfg_path;
+      }
+      const std::string f = find_cached_file(e->cache_dir, hub, file);
+      if (f.empty() && !e->syn_set) throw std::runtime_error(std::string(what) + " file doesn't exist");
+      return f;
+    };
+    bool diarize = false;
+    std::string seg_path, emb_path;
     if (o && o->enable_diarize == 1) {
-      // src/engine.rs:89-122: pyannote segmentation -> SpeechSegments
-      if (!e->seg) e->seg = std::make_unique<SegModel>(e->cfg.has_gpu_device ? e->cfg.gpu_device : 0);
+      // src/engine.rs:89-122: model paths from the config (both given) or the cache, then
+      // pyannote segmentation -> SpeechSegments
+      diarize = true;
+      const bool both = !e->seg_path.empty() && !e->emb_path.empty();
+      seg_path = resolve(both ? e->seg_path : "", "", "segmentation-3.0.onnx", "segmentation model");
+      emb_path = resolve(both ? e->emb_path : "", "", "wespeaker_en_voxceleb_CAM++.onnx", "embedding model");
+      if (!e->seg || e->seg_loaded != seg_path) {
+        e->seg.reset();
+        e->seg = std::make_unique<SegModel>(dev, seg_path);
+        e->seg_loaded = seg_path;
+      }
       const std::vector<DiarSegment> ds = e->seg->get_segments(pcm.data(), pcm.size());
       dpad.assign(pcm.begin(), pcm.end());
       dpad.resize(pcm.size() + (160000 - pcm.size() % 160000), 0);
       for (const DiarSegment& d : ds) segs.push_back({d.start, d.end, dpad.data() + d.start_idx, d.end_idx - d.start_idx});
     } else if (vad) {
-      if (!e->vad) e->vad = std::make_unique<VadModel>(e->cfg.has_gpu_device ? e->cfg.gpu_device : 0);
+      // src/engine.rs:123-139: cfg.vad_model_path, else ggml-silero-v5.1.2.bin from
+      // ggml-org/whisper-vad (src/model_manager.rs:303-319)
+      const std::string vp = resolve(e->vad_path, "models--ggml-org--whisper-vad", "ggml-silero-v5.1.2.bin", "VAD model");
+      if (!e->vad || e->vad_loaded != vp) {
+        e->vad.reset();
+        e->vad = std::make_unique<VadModel>(dev, vp);
+        e->vad_loaded = vp;
+      }
       vad_get_segments(*e->vad, pcm.data(), pcm.size(), &vad_mask, &segs);
       have_mask = true;
     } else {
       // whole file as one segment (src/engine.rs:141-147)
       segs.push_back({0.0, (double)pcm.size() / 16000.0, pcm.data(), pcm.size()});
     }
-    auto it = e->contexts.find(model);
-    if (it == e->contexts.end()) {
+    if (it == e->contexts.end())
       it = e->contexts.emplace(model, make_context(model, e->cfg.has_gpu_device, e->cfg.gpu_device, e->cfg.use_gpu,
-                                                   e->cfg.enable_dtw, e->syn, find_model_file(e->cache_dir, model)))
+                                                   e->cfg.enable_dtw, e->syn, model_path))
                .first;
-    }
-    if (o && o->translate_target && !(o->whisper_to_english == 1))
-      return fail("translate_target: network translation is out of scope for libwdr");
+    const wdr_diarize_options dopts = diarize_options(o, seg_path.c_str(), emb_path.c_str());
     std::string lang;
     bool has_lang = false;
-    std::vector<Seg> res = run_pipeline(it->second.get(), segs, o, e->syn, cb, &lang, &has_lang);
+    std::vector<Seg> res =
+        run_pipeline(it->second.get(), segs, o, diarize ? &dopts : nullptr, e->syn, cb, &lang, &has_lang);
     // src/engine.rs:179-199: preset of the detected (else requested) language + overrides,
     // then process_segments with the VAD mask oracle when VAD produced the segments
     const std::string eff = has_lang ? lang : ((o && o->lang) ? std::string(o->lang) : std::string("auto"));
@@ -1203,10 +1283,10 @@ int wdr_transcribe_audio(wdr_engine* e, const char* audio_path, const wdr_transc
 }
 
 int wdr_vad_create(const char* model_path, int8_t has_gpu_device, int32_t gpu_device, wdr_vad** out) {
-  (void)model_path;   // synthetic weights (the ggml loader is SURVEY §8(f) row 2)
   WDR_GUARD({
+    if (model_path && !file_exists(model_path)) return fail(std::string("VAD model file doesn't exist: ") + model_path);
     auto v = std::make_unique<wdr_vad>();
-    v->m = std::make_unique<VadModel>(has_gpu_device ? gpu_device : 0);
+    v->m = std::make_unique<VadModel>(has_gpu_device ? gpu_device : 0, model_path ? model_path : "");
     *out = v.release();
     return 0;
   })
@@ -1264,11 +1344,16 @@ int wdr_vad_get_segments(wdr_vad* v, const int16_t* samples, size_t n, double** 
 
 int wdr_diarizer_create(const char* segment_model_path, const char* embedding_model_path, int8_t has_gpu_device,
                         int32_t gpu_device, wdr_diarizer** out) {
-  (void)segment_model_path;   // synthetic weights (the ONNX initializer reader is SURVEY §8(f) row 3)
-  (void)embedding_model_path;
   WDR_GUARD({
+    for (const char* p : {segment_model_path, embedding_model_path})
+      if (p && !file_exists(p)) return fail(std::string("diarization model file doesn't exist: ") + p);
     auto d = std::make_unique<wdr_diarizer>();
     d->device = has_gpu_device ? gpu_device : 0;
+    d->seg_path = segment_model_path ? segment_model_path : "";
+    d->emb_path = embedding_model_path ? embedding_model_path : "";
+    // load eagerly: a bad file fails here, as ORT session creation does in the reference
+    if (!d->seg_path.empty()) d->S();
+    if (!d->emb_path.empty()) d->E();
     *out = d.release();
     return 0;
   })
@@ -1455,6 +1540,7 @@ int wdr_context_create(const char* model_path, const char* model_name, int8_t ha
   (void)num_samples;
   WDR_GUARD({
     if (model_path && *model_path && !file_exists(model_path)) return fail("whisper file doesn't exist");
+    if ((!model_path || !*model_path) && !syn) return fail("whisper file doesn't exist");
     *out = make_context(model_name ? model_name : "base", has_gpu_device == 1, gpu_device, use_gpu, enable_dtw,
                         syn_of(syn), model_path ? std::string(model_path) : std::string())
                .release();
@@ -1476,7 +1562,8 @@ int wdr_ggml_info(const char* path, int32_t* hparams, int64_t* n_tensors, int64_
 }
 
 int wdr_run_pipeline(wdr_context* c, const wdr_speech_segment* segs, size_t n_segs, const wdr_transcribe_options* o,
-                     const wdr_synthetic* syn, const wdr_callbacks* cb, wdr_segment_list** out) {
+                     const wdr_diarize_options* dopts, const wdr_synthetic* syn, const wdr_callbacks* cb,
+                     wdr_segment_list** out) {
   WDR_GUARD({
     std::vector<wdr_speech_segment> v(segs, segs + n_segs);
     std::string lang;
@@ -1484,7 +1571,7 @@ int wdr_run_pipeline(wdr_context* c, const wdr_speech_segment* segs, size_t n_se
     const double t = now_s();
     c->st->times = StageTimes{};
     c->cs = wdr_context::ChainStats{};
-    std::vector<Seg> res = run_pipeline(c, v, o, syn_of(syn), cb, &lang, &has_lang);
+    std::vector<Seg> res = run_pipeline(c, v, o, dopts, syn_of(syn), cb, &lang, &has_lang);
     c->st->times.glue = now_s() - t;   // total wall for this pipeline call
     *out = to_list(res, has_lang ? &lang : nullptr);
     return 0;
@@ -1500,7 +1587,7 @@ int wdr_run_pipeline_raw(wdr_context* c, const wdr_speech_segment* segs, size_t 
     const double t = now_s();
     c->st->times = StageTimes{};
     c->cs = wdr_context::ChainStats{};
-    std::vector<Seg> res = run_pipeline(c, v, o, syn_of(syn), nullptr, &lang, &has_lang, true);
+    std::vector<Seg> res = run_pipeline(c, v, o, nullptr, syn_of(syn), nullptr, &lang, &has_lang, true);
     c->st->times.glue = now_s() - t;
     *out = to_list(res, has_lang ? &lang : nullptr);
     if (!(*out)->speech_index && !res.empty()) return fail("raw pipeline: missing speech index");
@@ -1521,6 +1608,14 @@ void wdr_segment_list_free(wdr_segment_list* l) {
   free((void*)l->detected_lang);
   free((void*)l->speech_index);
   free(l);
+}
+
+int wdr_dbg_set_early_fixup(wdr_context* c, int32_t mode) {
+  WDR_GUARD({
+    if (mode < -1 || mode > 2) return fail("early fix-up mode: -1 (env default), 0, 1 or 2");
+    c->early_fixup = mode;
+    return 0;
+  })
 }
 
 int wdr_context_set_chains(wdr_context* c, int32_t n) {
@@ -1544,6 +1639,7 @@ int wdr_context_stage_times(wdr_context* c, wdr_stage_times* o) {
     o->spec_s = c->cs.spec_s;
     o->fixup_s = c->cs.fixup_s;
     o->batch_step_s = c->cs.step_s;
+    o->early_fixup_segments = c->cs.early;
     return 0;
   })
 }

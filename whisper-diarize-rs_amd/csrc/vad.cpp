@@ -28,7 +28,8 @@ VadLayout layout() {
 }
 }  // namespace
 
-VadModel::VadModel(int dev) : device(dev) {
+VadModel::VadModel(int dev, const std::string& path) : device(dev) {
+  if (!path.empty()) throw std::runtime_error("VAD model file: Silero ggml loading not available yet: " + path);
   WDR_HIP(hipSetDevice(dev));
   WDR_HIP(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking));
   WDR_HIP(hipEventCreate(&e0_));

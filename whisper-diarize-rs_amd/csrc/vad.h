@@ -1,6 +1,7 @@
 // Silero VAD model + whisper.cpp speech-segment state machine.
 #pragma once
 #include <cstdint>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -18,7 +19,8 @@ struct VadParams {   // whisper.cpp whisper_vad_default_params + src/vad.rs:22 (
 
 class VadModel {
  public:
-  explicit VadModel(int device);
+  // path: whisper.cpp's ggml-silero-v5.1.2.bin (model_files.cpp); "" = synthetic seeded weights
+  explicit VadModel(int device, const std::string& path = std::string());
   ~VadModel();
   // speech probability per 512-sample chunk of int16 PCM (x / 32768 as src/vad.rs:11-12)
   std::vector<float> probs(const int16_t* pcm, size_t n);

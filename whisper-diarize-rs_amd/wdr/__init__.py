@@ -16,7 +16,8 @@ import numpy as np
 
 from . import _lib as L
 
-__all__ = ["Engine", "EngineConfig", "TranscribeOptions", "AdvancedTranscribe", "Segment", "WordTimestamp",
+__all__ = ["Engine", "EngineConfig", "TranscribeOptions", "AdvancedTranscribe", "DiarizeOptions", "Segment",
+           "WordTimestamp",
            "ProgressType", "Callbacks", "Synthetic", "WhisperContext", "SpeechSegment", "read_wav", "vad_merge",
            "WdrError"]
 
@@ -94,6 +95,30 @@ class Callbacks:                           # src/engine.rs:35-40
     progress: Optional[Callable[[int, ProgressType, str], None]] = None
     new_segment_callback: Optional[Callable[[Segment], None]] = None
     is_cancelled: Optional[Callable[[], bool]] = None
+
+
+@dataclasses.dataclass
+class DiarizeOptions:                      # src/types.rs:93-98
+    """Passed to run_transcription_pipeline to switch speakers on (src/transcribe.rs:339-345).
+    A None model path selects synthetic seeded weights (no model files offline)."""
+    segment_model_path: Optional[str] = None
+    embedding_model_path: Optional[str] = None
+    threshold: float = 0.5
+    max_speakers: int = 2 ** 64 - 1      # usize::MAX, the Engine's mapping of None / Some(0)
+
+    @staticmethod
+    def from_options(o: "TranscribeOptions", segment_model_path=None, embedding_model_path=None):
+        """The DiarizeOptions Engine::transcribe_audio builds (src/engine.rs:101-111)."""
+        thr = o.advanced.diarize_threshold if (o.advanced and o.advanced.diarize_threshold is not None) else 0.5
+        mx = o.max_speakers if o.max_speakers else 2 ** 64 - 1
+        return DiarizeOptions(segment_model_path, embedding_model_path, thr, mx)
+
+
+def _dopts(d: Optional[DiarizeOptions], keep):
+    if d is None:
+        return None
+    return keep(L.DiarizeOptions(keep(_s(d.segment_model_path)), keep(_s(d.embedding_model_path)), d.threshold,
+                                 d.max_speakers))
 
 
 @dataclasses.dataclass
@@ -311,7 +336,8 @@ def vad_segments_from_probs(probs) -> list:
 
 
 class Vad:
-    """Silero VAD on the GPU (src/vad.rs:6-85).  Synthetic seeded weights."""
+    """Silero VAD on the GPU (src/vad.rs:6-85).  model_path: whisper.cpp's ggml-silero-v5.1.2.bin;
+    None = synthetic seeded weights."""
 
     def __init__(self, model_path: Optional[str] = None, gpu_device: Optional[int] = None):
         self._lib = L.load()
@@ -396,13 +422,14 @@ class SpeakerManager:
 
 class Diarizer:
     """pyannote segmentation-3.0 + CAM++ on the GPU (src/engine.rs:89-122,
-    src/transcribe.rs:461-497).  Synthetic seeded weights."""
+    src/transcribe.rs:461-497).  Model paths: the ONNX files; None = synthetic seeded weights."""
 
-    def __init__(self, gpu_device: Optional[int] = None):
+    def __init__(self, gpu_device: Optional[int] = None, segment_model_path: Optional[str] = None,
+                 embedding_model_path: Optional[str] = None):
         self._lib = L.load()
         h = C.c_void_p()
-        L.check(self._lib.wdr_diarizer_create(None, None, 0 if gpu_device is None else 1, gpu_device or 0,
-                                              C.byref(h)))
+        L.check(self._lib.wdr_diarizer_create(_s(segment_model_path), _s(embedding_model_path),
+                                              0 if gpu_device is None else 1, gpu_device or 0, C.byref(h)))
         self.h = h
 
     def frame_classes(self, samples: np.ndarray, logprobs: bool = False):
@@ -531,9 +558,12 @@ class WhisperContext:
 
     # -- run_transcription_pipeline (src/transcribe.rs:323-535)
     def run_pipeline(self, speech_segments, options: TranscribeOptions, callbacks: Optional[Callbacks] = None,
-                     synthetic: Optional[Synthetic] = None, with_index: bool = False):
-        """transcribe::run_transcription_pipeline -> (segments, detected_lang) [+ the input
-        SpeechSegment index of every output segment when with_index]."""
+                     synthetic: Optional[Synthetic] = None, with_index: bool = False,
+                     diarize_options: Optional[DiarizeOptions] = None):
+        """transcribe::run_transcription_pipeline(ctx, segments, options, diarize_options, ...)
+        -> (segments, detected_lang) [+ the input SpeechSegment index of every output segment
+        when with_index].  Speakers are assigned iff diarize_options is given (as the
+        reference's Option<DiarizeOptions>)."""
         keep = _Keep()
         arr = (L.SpeechSegment * max(1, len(speech_segments)))()
         for i, s in enumerate(speech_segments):
@@ -541,7 +571,9 @@ class WhisperContext:
             arr[i] = L.SpeechSegment(s.start, s.end, smp.ctypes.data_as(C.POINTER(C.c_int16)), smp.size)
         out = C.POINTER(L.SegmentList)()
         syn = _syn(synthetic or self.synthetic)
+        d = _dopts(diarize_options, keep)
         L.check(self._lib.wdr_run_pipeline(self.h, arr, len(speech_segments), _opts(options, keep),
+                                           C.byref(d) if d is not None else None,
                                            C.byref(syn) if syn else None, _callbacks(callbacks, keep),
                                            C.byref(out)))
         return _segments(out, with_index)
@@ -565,6 +597,10 @@ class WhisperContext:
         """Decode chains for greedy run_pipeline calls (wdr_context_set_chains): n blocks of the
         speech segments decoded concurrently with batched steps, exact prompt fix-up."""
         L.check(self._lib.wdr_context_set_chains(self.h, int(n)))
+
+    def set_early_fixup(self, mode: int):
+        """Test seam (wdr_dbg_set_early_fixup): 0 off, 1 default, 2 forced, -1 env default."""
+        L.check(self._lib.wdr_dbg_set_early_fixup(self.h, int(mode)))
 
     def stage_times(self) -> dict:
         t = L.StageTimes()

@@ -34,6 +34,11 @@ class TranscribeOptions(C.Structure):
                 ("max_speakers", u64), ("advanced", C.POINTER(Advanced))]
 
 
+class DiarizeOptions(C.Structure):
+    _fields_ = [("segment_model_path", cstr), ("embedding_model_path", cstr), ("threshold", f32),
+                ("max_speakers", u64)]
+
+
 class Synthetic(C.Structure):
     _fields_ = [("weight_std", f64), ("emb_std", f64), ("force_len_rate", f32), ("disable_fallback", i8)]
 
@@ -81,7 +86,7 @@ class StageTimes(C.Structure):
                 ("windows", i64), ("decode_steps", i64), ("prefills", i64), ("lang", f64), ("prompt_gpu", f64),
                 ("embed", f64), ("chains", i64), ("batch_launches", i64), ("batch_rows", i64),
                 ("fixup_segments", i64), ("replay_segments", i64), ("spec_s", f64), ("fixup_s", f64),
-                ("batch_step_s", f64)]
+                ("batch_step_s", f64), ("early_fixup_segments", i64)]
 
 
 class Token(C.Structure):
@@ -130,10 +135,11 @@ _SIGS = {
     "wdr_context_free": (None, [vp]),
     "wdr_run_pipeline_raw": (C.c_int, [vp, P(SpeechSegment), sz, P(TranscribeOptions), P(Synthetic),
                                        P(P(SegmentList))]),
-    "wdr_run_pipeline": (C.c_int, [vp, P(SpeechSegment), sz, P(TranscribeOptions), P(Synthetic), P(Callbacks),
-                                   P(P(SegmentList))]),
+    "wdr_run_pipeline": (C.c_int, [vp, P(SpeechSegment), sz, P(TranscribeOptions), P(DiarizeOptions), P(Synthetic),
+                                   P(Callbacks), P(P(SegmentList))]),
     "wdr_segment_list_free": (None, [P(SegmentList)]),
     "wdr_context_set_chains": (C.c_int, [vp, i32]),
+    "wdr_dbg_set_early_fixup": (C.c_int, [vp, i32]),
     "wdr_ggml_info": (C.c_int, [cstr, P(i32), P(i64), P(i64)]),
     "wdr_dbg_batch_step": (C.c_int, [vp, P(i32), sz, i32, i32, P(f64)]),
     "wdr_context_stage_times": (C.c_int, [vp, P(StageTimes)]),
