@@ -43,12 +43,14 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="large-v3")
     ap.add_argument("--seconds", type=float, default=3600.0, help="audio seconds per rank")
-    ap.add_argument("--prof", default="gemv", choices=["gemv", "gemm", "flash", "xattn", "none"],
-                    help="kernel class timed live with HIP events for the roofline figure")
+    ap.add_argument("--prof", default="gemm,gemv,flash,xattn",
+                    help="kernel classes timed live with HIP events (comma list of gemm, gemv, flash, xattn; "
+                         "'none'): the roofline figure is the one with the largest share of kernel time")
     ap.add_argument("--seg", default="diarize", choices=["diarize", "vad"],
                     help="segmentation stage: pyannote diarization (default) or Silero VAD")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU oracle work (rank 0, N=1)")
+    ap.add_argument("--cpu-audio", type=float, default=60.0,
+                    help="audio seconds of the workload the CPU baseline is extrapolated over (rank 0, N=1)")
     return ap.parse_args()
 
 
@@ -95,37 +97,84 @@ def pipeline_roofline(model, times, t_wall):
             "step_launches": launches}
 
 
-def cpu_baseline(model, segs, budget_s):
-    """The CPU restatement (oracle/, numpy f32 with f16-rounded weights/activations as ggml)
-    on a bounded prefix of the same workload.  Returns (xRT, sample description, threads)."""
+def cpu_baseline(model, segs, audio_target):
+    """The CPU restatement (oracle/, numpy f32 over f16-rounded weights/activations as ggml) timed
+    on this host at 4 threads (whisper.cpp's default min(4, hw), src/types.rs:19) and at the
+    process's BLAS thread count, per stage: one 30-s window through the encoder + cross K/V, a
+    prompt prefill, decode steps, a DTW re-forward with alignment-head capture, log-mel.  The
+    figures are combined over the first segments of the same shard covering >= audio_target
+    seconds of speech with the same schedule the GPU runs (windows, pinned decode lengths,
+    prompts, language-detection steps): xRT = the shard time they cover (to the last one's end,
+    silences included, the GPU figure's basis) / T_cpu.  Extrapolated, labelled so."""
     import numpy as np
-    from oracle.model import Whisper
-    from oracle.pipeline import SpeechSegment, run_transcription_pipeline
+    from threadpoolctl import threadpool_info, threadpool_limits
+    from oracle.mel import log_mel, pcm_i16_to_f32
+    from oracle.model import DecoderState, Whisper
     from oracle.vocab import Vocab
     from oracle.weights import hparams_for, synth_weights
-    from oracle.whisper_full import WhisperState
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    from oracle.whisper_full import aheads_for_model_name
     hp = hparams_for(model)
-    W = synth_weights(hp, std=0.02, emb_std=0.02)
-    st = WhisperState(Whisper(hp, W), Vocab(hp.n_vocab), model)
-    opts = dict(lang="auto", advanced=dict(sampling_strategy="greedy"),
-                synthetic=dict(force_len_rate=3.3, logprob_thold=-np.inf, entropy_thold=-1.0))
-    audio = 0.0
-    t0 = time.perf_counter()
-    n = 0
-    for s in segs:
-        run_transcription_pipeline(st, [SpeechSegment(s.start, s.end, s.samples)], opts)
-        audio += s.samples.size / 16000.0
-        n += 1
-        if time.perf_counter() - t0 > budget_s:
+    m = Whisper(hp, synth_weights(hp, std=0.02, emb_std=0.02))
+    v = Vocab(hp.n_vocab)
+    # the workload sample: segments in order until audio_target seconds
+    sel, audio = [], 0.0
+    for sg in segs:
+        sel.append(sg)
+        audio += sg.samples.size / 16000.0
+        if audio >= audio_target:
             break
-    wall = time.perf_counter() - t0
-    del W, st
-    return audio / wall, "first %d segments (%.1f s of audio) of rank 0's shard" % (n, audio), threads
+    n_win = n_steps = n_lang = 0
+    prefill_toks = dtw_toks = 0
+    prev_len = 0
+    for sg in sel:
+        n_len = sg.samples.size // 160
+        seek = 0
+        n_lang += 1                              # lang auto: one [SOT] step per segment
+        while seek + 100 < n_len:
+            win = min(3000, n_len - seek)
+            L = max(3, int(round(3.3 * win / 100.0)) + 3)
+            n_win += 1
+            n_steps += L
+            prefill_toks += (1 + min(224, prev_len) if prev_len else 0) + 3
+            dtw_toks += L + 2
+            prev_len = L - 3
+            seek += 3000
+    pcm0 = pcm_i16_to_f32(sel[0].samples)
+    threads_max = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    out = {}
+    for threads in sorted({4, threads_max}):
+        with threadpool_limits(limits=threads):
+            t = time.perf_counter()
+            mel = log_mel(pcm0, hp.n_mels)
+            t_mel_per_s = (time.perf_counter() - t) / (pcm0.size / 16000.0)
+            win = np.zeros((hp.n_mels, 3000), np.float32)
+            win[:, :min(3000, mel.shape[1])] = mel[:, :3000]
+            t = time.perf_counter()
+            cross = m.cross_kv(m.encode(win))
+            t_enc = time.perf_counter() - t
+            st = DecoderState(m)
+            prompt = [v.sot] + [int(x) for x in np.arange(30) * 97 % v.eot]
+            t = time.perf_counter()
+            st.forward(prompt, cross)
+            t_pre_tok = (time.perf_counter() - t) / len(prompt)
+            t = time.perf_counter()
+            for k in range(8):
+                st.forward([int(100 + k)], cross)
+            t_step = (time.perf_counter() - t) / 8
+            dt_toks = [v.sot, v.not_] + [int(x) for x in np.arange(40) * 31 % v.eot] + [v.eot]
+            t = time.perf_counter()
+            DecoderState(m).forward(dt_toks, cross, want_logits=None, aheads=aheads_for_model_name(model))
+            t_dtw_tok = (time.perf_counter() - t) / len(dt_toks)
+        T = (audio * t_mel_per_s + n_win * t_enc + (n_steps + n_lang) * t_step + prefill_toks * t_pre_tok
+             + dtw_toks * t_dtw_tok)
+        out[threads] = dict(xrt=float(sel[-1].end) / T, t_enc_s=round(t_enc, 3), t_step_ms=round(t_step * 1e3, 2),
+                            t_prefill_tok_ms=round(t_pre_tok * 1e3, 2), t_dtw_tok_ms=round(t_dtw_tok * 1e3, 2))
+    del m
+    sample = ("first %d segments (%.1f s of speech over %.1f s of audio: %d windows, %d decode steps, %d prompt + %d DTW tokens) of "
+              "rank 0's shard, extrapolated from per-stage timings (1 encoder window, 8 steps, a 31-token "
+              "prefill, a 43-token DTW re-forward) of the numpy oracle" % (len(sel), audio, sel[-1].end, n_win, n_steps,
+                                                                         prefill_toks, dtw_toks))
+    return out, sample, threads_max
 
 
 def main():
@@ -168,7 +217,9 @@ def main():
     vad = None if diarize else wdr.Vad(gpu_device=local)
     dia = wdr.Diarizer(gpu_device=local) if diarize else None
     lib = wdr._lib.load()
-    prof_cls = {"none": 0, "gemm": 1, "gemv": 2, "flash": 3, "xattn": 4}[args.prof]
+    CLS = {"gemm": 1, "gemv": 2, "flash": 3, "xattn": 4}
+    prof = [c for c in args.prof.split(",") if c in CLS]
+    prof_mask = sum(1 << CLS[c] for c in prof)
 
     def step():
         # the segmentation stage over the whole shard runs and is timed; in synthetic mode the
@@ -188,7 +239,7 @@ def main():
         step()
     vad_t = [0.0, 0]
     barrier()
-    lib.wdr_prof_set(prof_cls)
+    lib.wdr_prof_set_mask(prof_mask)
     t0 = time.perf_counter()
     n_out = 0
     for _ in range(args.steps):
@@ -197,10 +248,12 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     import ctypes as C
-    ms, nl, by, fl = C.c_double(), C.c_int64(), C.c_double(), C.c_double()
-    if lib.wdr_prof_read(C.byref(ms), C.byref(nl), C.byref(by), C.byref(fl)) != 0:
-        nl.value = 0
-    lib.wdr_prof_set(0)
+    live = {}
+    for c in prof:
+        ms, nl, by, fl = C.c_double(), C.c_int64(), C.c_double(), C.c_double()
+        if lib.wdr_prof_read_class(CLS[c], C.byref(ms), C.byref(nl), C.byref(by), C.byref(fl)) == 0 and nl.value:
+            live[c] = (ms.value, nl.value, by.value, fl.value)
+    lib.wdr_prof_set_mask(0)
     times = ctx.stage_times()
     t = torch.tensor([dt], dtype=torch.float64)
     if world > 1:
@@ -210,36 +263,45 @@ def main():
     dt_max = float(t.item())
     value = world * shard_s * args.steps / dt_max
 
-    roof = None
-    if prof_cls and nl.value > 0 and ms.value > 0:
-        if args.prof in ("gemm", "flash"):
-            ach = fl.value / (ms.value * 1e-3) / 1e12
-            roof = {"kernel": args.prof, "bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_F16_PEAK_TFS,
-                    "unit": "TFLOP/s", "frac": round(ach / MFMA_F16_PEAK_TFS, 4), "traffic": None,
-                    "launches": nl.value, "avg_launch_us": round(ms.value * 1e3 / nl.value, 3),
-                    "flops_per_launch": fl.value / nl.value}
+    # per class: algorithmic flops (MFMA classes) or bytes (HBM classes) per launch / the average
+    # duration of its HIP-event-timed launches; `roofline` is the class with the largest share
+    # of kernel time (every class is sampled at the same rate, csrc/prof.cpp)
+    classes = {}
+    for c, (ms, nl, by, fl) in live.items():
+        if ms <= 0:
+            continue
+        if c in ("gemm", "flash"):
+            ach = fl / (ms * 1e-3) / 1e12
+            r = {"kernel": c, "bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_F16_PEAK_TFS,
+                 "unit": "TFLOP/s", "frac": round(ach / MFMA_F16_PEAK_TFS, 4), "flops_per_launch": fl / nl}
         else:
-            ach = by.value / (ms.value * 1e-3) / 1e9
-            roof = {"kernel": args.prof, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                    "launches": nl.value, "avg_launch_us": round(ms.value * 1e3 / nl.value, 3),
-                    "bytes_per_launch": by.value / nl.value}
-        # csrc/prof.h: decode steps replay hipGraphs; 1 in 8 steps runs eagerly and 1 in 8 of its
-        # launches of the class carries HIP start/stop events on its own stream
-        roof["sampling"] = "1 in %d decode steps eager, 1 in %d of their launches timed" % (PROF_SAMPLE, PROF_SAMPLE)
-        tr, src = pmc_traffic(args.prof)
+            ach = by / (ms * 1e-3) / 1e9
+            r = {"kernel": c, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                 "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_launch": by / nl}
+        r.update({"traffic": None, "sampled_launches": nl, "avg_launch_us": round(ms * 1e3 / nl, 3),
+                  "sampled_ms": round(ms, 3)})
+        tr, src = pmc_traffic(c)
         if tr is not None:
-            roof["traffic"] = round(tr)
-            roof["traffic_source"] = src
+            r["traffic"] = round(tr)
+            r["traffic_source"] = src
+        # csrc/prof.h: decode steps replay hipGraphs; 1 in 8 steps runs eagerly and 1 in 8 of
+        # its launches carries HIP start/stop events on the launching stream; launches outside
+        # steps are timed 1 in 64
+        r["sampling"] = "1 in %d launches (decode steps: 1 in %d eager, 1 in %d of those)" % (
+            PROF_SAMPLE * PROF_SAMPLE, PROF_SAMPLE, PROF_SAMPLE)
+        classes[c] = r
+    roof = max(classes.values(), key=lambda r: r["sampled_ms"]) if classes else None
 
     pipe = pipeline_roofline(args.model, times, dt / args.steps)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ctx.close()
-        v, sample, threads = cpu_baseline(args.model, segs, args.cpu_budget)
-        cpu = {"value": round(v, 4), "unit": "audio-sec/wall-sec", "cores": threads, "kind": "port",
-               "sample": sample}
+        res, sample, tmax = cpu_baseline(args.model, segs, args.cpu_audio)
+        cpu = {"value": round(res[tmax]["xrt"], 5), "unit": "audio-sec/wall-sec", "cores": tmax, "kind": "port",
+               "sample": sample, "extrapolated": True, "host_cpus": os.cpu_count(),
+               "by_threads": {str(k): {kk: (round(vv, 5) if kk == "xrt" else vv) for kk, vv in r.items()}
+                              for k, r in res.items()}}
 
     if rank == 0:
         line = {
@@ -256,7 +318,7 @@ def main():
                                     "downstream (synthetic pin)") % (args.model, shard_s, len(segs), audio_s),
                        "model": args.model, "global_batch": len(segs) * world, "seq_len": 1500,
                        "parallelism": "dp%d (segment shards per rank)" % world},
-            "roofline": roof, "pipeline_roofline": pipe, "cpu_baseline": cpu,
+            "roofline": roof, "roofline_classes": classes, "pipeline_roofline": pipe, "cpu_baseline": cpu,
             "stages_s": {k: round(v, 3) for k, v in times.items() if isinstance(v, float)},
             "counts": {k: v for k, v in times.items() if isinstance(v, int)},
             "segmentation": ({"stage": "pyannote", "s_per_step": round(vad_t[0] / args.steps, 4), "segments": vad_t[1],

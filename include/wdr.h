@@ -283,6 +283,9 @@ int wdr_context_hparams(wdr_context* c, int32_t* out /* [10] */);
  * class 1 = MFMA GEMM (encoder / prefill / DTW projections), 2 = decoder GEMV, 3 = flash attention,
  * 4 = decoder cross-attention.  Setting a class resets the counters. */
 int wdr_prof_set(int32_t cls);
+/* several classes at once: bit (1 << cls) per class; read each with wdr_prof_read_class */
+int wdr_prof_set_mask(int32_t mask);
+int wdr_prof_read_class(int32_t cls, double* total_ms, int64_t* launches, double* algo_bytes, double* algo_flops);
 int wdr_prof_read(double* total_ms, int64_t* launches, double* algo_bytes, double* algo_flops);
 
 /* ---- whisper_full-level test seam: one state.full() call, raw token data ---- */
@@ -305,6 +308,8 @@ void wdr_result_free(wdr_result_seg* segs, size_t n);
 int wdr_dbg_log_mel(wdr_context* c, const float* x, size_t n, int32_t seek, float* window_out /* [n_mels][3000] */);
 int wdr_dbg_energy(const float* x, size_t n, float* out);
 int wdr_dbg_encode(wdr_context* c, const float* mel_window /* [n_mels][3000] */, float* enc_out /* [1500][d] */);
+/* cross K/V of the last wdr_dbg_encode window: [1500][n_text_layer][2 (K, V)][d] (f16 -> f32) */
+int wdr_dbg_cross_kv(wdr_context* c, float* out);
 int wdr_dbg_decode(wdr_context* c, const int32_t* tokens, size_t n, float* logits_out /* [n_vocab] */);
 /* prefill tokens[0..n-2], then one decode step of tokens[n-1]; mode 0 = the persistent
  * one-launch step (error if the model width has none), 1 = the per-kernel chain */

@@ -69,13 +69,14 @@ def softmax(s, axis=-1):
     return (e / e.sum(axis=axis, keepdims=True)).astype(np.float32)
 
 
-def attention(q, k, v, n_head, R, mask=None, want_probs=False):
-    """q [Tq][d], k/v [Tk][d] (already projected).  Returns [Tq][d] (and probs [H][Tq][Tk])."""
+def attention(q, k, v, n_head, R, mask=None, want_probs=False, kv_rounded=False):
+    """q [Tq][d], k/v [Tk][d] (already projected).  Returns [Tq][d] (and probs [H][Tq][Tk]).
+    kv_rounded: k and v already hold R-rounded values (caches), R is idempotent -- skipped."""
     Tq, d = q.shape
     dh = d // n_head
     qh = R(q).reshape(Tq, n_head, dh).transpose(1, 0, 2)
-    kh = R(k).reshape(-1, n_head, dh).transpose(1, 0, 2)
-    vh = R(v).reshape(-1, n_head, dh).transpose(1, 0, 2)
+    kh = (k if kv_rounded else R(k)).reshape(-1, n_head, dh).transpose(1, 0, 2)
+    vh = (v if kv_rounded else R(v)).reshape(-1, n_head, dh).transpose(1, 0, 2)
     s = (qh @ kh.transpose(0, 2, 1)) * np.float32(dh ** -0.5)
     if mask is not None:
         s = s + mask
@@ -177,12 +178,12 @@ class DecoderState:
             mask = np.zeros((n, T), np.float32)
             for r in range(n):
                 mask[r, pos0 + r + 1:] = -np.inf
-            a = attention(q, self.k[i], self.v[i], hp.n_text_head, R, mask=mask[None])
+            a = attention(q, self.k[i], self.v[i], hp.n_text_head, R, mask=mask[None], kv_rounded=True)
             x = x + linear(a, W[p + "attn.out.weight"], W[p + "attn.out.bias"], R)
             h = layer_norm(x, W[p + "cross_attn_ln.weight"], W[p + "cross_attn_ln.bias"])
             q = linear(h, W[p + "cross_attn.query.weight"], W[p + "cross_attn.query.bias"], R)
             ck, cv = cross[i]
-            a, probs = attention(q, ck, cv, hp.n_text_head, R, want_probs=True)
+            a, probs = attention(q, ck, cv, hp.n_text_head, R, want_probs=True, kv_rounded=True)
             if aheads:
                 for (l, hh) in aheads:
                     if l == i:

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 
 import numpy as np
 
@@ -89,19 +90,51 @@ def splitmix64(x: np.ndarray) -> np.ndarray:
     return z
 
 
+_CHUNK = 1 << 18
+_POOL = None
+
+
+def _pool():
+    """Threads for large tensors (numpy ufuncs release the GIL): BASELINE-size models
+    (large-v3, 1.55 B parameters) are generated in seconds instead of minutes."""
+    global _POOL
+    if _POOL is None:
+        import concurrent.futures
+        _POOL = concurrent.futures.ThreadPoolExecutor(max(1, min(16, os.cpu_count() or 1)))
+    return _POOL
+
+
+def _fill(seed: int, lo: int, hi: int, scale: np.float32, out: np.ndarray, round16: bool):
+    with np.errstate(over="ignore"):
+        idx = np.arange(lo, hi, dtype=np.uint64) + np.uint64(seed)
+    h = splitmix64(idx)
+    v = ((h >> np.uint64(40)).astype(np.float32) * np.float32(2.0 ** -23) - np.float32(1.0)) * scale
+    out[lo:hi] = v.astype(np.float16) if round16 else v
+
+
+def _synth(name: str, n: int, std: float, dtype, round16: bool = False) -> np.ndarray:
+    """dtype f16: the f16 tensor; f32 with round16: its values widened back to f32."""
+    seed = fnv1a64(name)
+    scale = np.float32(std * math.sqrt(3.0))
+    out = np.empty(n, dtype)
+    round16 = round16 or dtype == np.float16
+    if n <= _CHUNK:
+        _fill(seed, 0, n, scale, out, round16)
+        return out
+    futs = [_pool().submit(_fill, seed, lo, min(n, lo + _CHUNK), scale, out, round16) for lo in range(0, n, _CHUNK)]
+    for f in futs:
+        f.result()
+    return out
+
+
 def synth_uniform(name: str, n: int, std: float) -> np.ndarray:
     """f32 values (before the f16 cast) of a synthetic tensor with `n` elements."""
-    seed = np.uint64(fnv1a64(name))
-    with np.errstate(over="ignore"):
-        idx = np.arange(n, dtype=np.uint64) + seed
-    h = splitmix64(idx)
-    v = (h >> np.uint64(40)).astype(np.float32) * np.float32(2.0 ** -23) - np.float32(1.0)
-    return v * np.float32(std * math.sqrt(3.0))
+    return _synth(name, n, std, np.float32)
 
 
 def synth_f16(name: str, shape, std: float = 0.02) -> np.ndarray:
     n = int(np.prod(shape))
-    return synth_uniform(name, n, std).astype(np.float16).reshape(shape)
+    return _synth(name, n, std, np.float16).reshape(shape)
 
 
 def synth_f32(name: str, shape, std: float = 0.02) -> np.ndarray:
@@ -162,7 +195,7 @@ def synth_weights(hp: HParams, std: float = 0.02, emb_std: float | None = None) 
     for name, shape, kind in tensor_list(hp):
         if kind == "w16":
             s = emb_std if (emb_std is not None and name == "decoder.token_embedding.weight") else std
-            W[name] = synth_f16(name, shape, s).astype(np.float32)
+            W[name] = _synth(name, int(np.prod(shape)), s, np.float32, round16=True).reshape(shape)
         elif kind in ("b32", "p32"):
             W[name] = synth_f32(name, shape, std)
         elif kind == "ln_g":

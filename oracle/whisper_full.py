@@ -101,6 +101,7 @@ class Token:
     t1: int = -1
     t_dtw: int = -1
     vlen: float = 0.0
+    margin: float = float("inf")   # test diagnostics: logprob gap top-1 - top-2 at the greedy pick
 
 
 @dataclasses.dataclass
@@ -143,7 +144,8 @@ class WhisperState:
         self.tid_last = 0
         self.lang_id = 0
         self.result_all = []
-        self.stats = {"encode": 0, "decode_tokens": 0, "decode_calls": 0}
+        self.stats = {"encode": 0, "decode_tokens": 0, "decode_calls": 0, "no_speech_skips": 0, "fallbacks": 0}
+        self.lang_margin = float("inf")   # test diagnostics: language logit gap top-1 - top-2
         # whisper_decoder::rng (std::mt19937): decoder 0 seeded once per state, decoders >= 1
         # re-seeded with 0 on every whisper_full call (WHISPER_DECODER_INIT) -- parity unpinned
         self.rngs = [np.random.RandomState(0)] + [None] * 15
@@ -218,6 +220,10 @@ class WhisperState:
         idx = int(np.argmax(probs))
         if probs[idx] > 0:
             tok.id, tok.p, tok.plog = idx, float(probs[idx]), float(logprobs[idx])
+            fin = logprobs[logprobs > -np.inf]
+            if fin.size > 1:
+                top2 = np.partition(fin, -2)[-2:]
+                tok.margin = float(top2[1] - top2[0])
         if tok.id >= v.beg:
             tok.tid = tok.id
             tok.pt = tok.p
@@ -267,6 +273,8 @@ class WhisperState:
             lang_logits = [(float(logits[v.token_lang(i)]), i) for i in range(len(LANGS))]
             best = max(lang_logits, key=lambda t: t[0])     # sort descending, take first
             self.lang_id = best[1]
+            ll = sorted((x for x, _ in lang_logits), reverse=True)
+            self.lang_margin = ll[0] - ll[1]
             language = LANGS[self.lang_id]
         prompt_init = [v.sot]
         if v.multilingual:
@@ -374,6 +382,7 @@ class WhisperState:
                         success = False
                 if success:
                     break
+                self.stats["fallbacks"] += 1
             # ---------------- output
             seek_delta = best["seek_delta"]
             result_len = best["result_len"]
@@ -386,6 +395,8 @@ class WhisperState:
                 new_past = prompt[1:len(prompt) - len(prompt_init)]
             if not is_no_speech:
                 new_past += [t.id for t in tokens_cur[:result_len]]
+            else:
+                self.stats["no_speech_skips"] += 1
             prompt_past = new_past
             if tokens_cur and not is_no_speech:
                 t0 = seek + 2 * (tokens_cur[0].tid - v.beg)

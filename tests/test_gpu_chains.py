@@ -73,19 +73,32 @@ def test_forced_early_fixup_is_exact(fallback):
     """The early prompt fix-up (a chain redoes its first segments from its predecessor's final
     prompt while the others still decode) forced on through the wdr_dbg_set_early_fixup seam:
     it must run (nonzero count) and give the one-chain result, as must the run with it off.
-    With fallback on, segments fall back to t > 0 sampling, so a redone segment's RNG state and
-    the sampled-tail replay are exercised too."""
-    syn = wdr.Synthetic(weight_std=0.02, emb_std=0.5, force_len_rate=0.0 if fallback else 3.3,
-                        disable_fallback=not fallback)
+    fallback: whisper.cpp's thresholds active on ~12-s segments (consecutive talk spurts
+    merged), whose pinned decode repeats one token past 32 tokens -> entropy < 2.4 -> the
+    ladder samples at t = 0.2 .. 1.0; shorter segments pass at t = 0.  Random draws then make
+    every later segment depend on the RNG stream, so a redone segment's RNG state and the
+    sampled-tail replay (incl. a first sampled segment decoded from a stale RNG) are exercised."""
+    syn = wdr.Synthetic(weight_std=0.02, emb_std=0.5, force_len_rate=3.3, disable_fallback=not fallback)
     ctx = wdr.WhisperContext("tiny-test", synthetic=syn)
-    pcm, spurts = synth_speech(60.0, seed=13, n_speakers=2)
+    pcm, spurts = synth_speech(90.0, seed=13, n_speakers=2)
     segs = _segs(pcm, spurts)
+    if fallback:   # merge runs of spurts into ~12-s segments, keep every other one short
+        merged, cur = [], []
+        for k, sp in enumerate(spurts):
+            cur.append(sp)
+            if cur[-1][1] - cur[0][0] >= (12.0 if len(merged) % 2 == 0 else 0.0):
+                merged.append((cur[0][0], cur[-1][1], None))
+                cur = []
+        segs = _segs(pcm, merged)
+    assert len(segs) >= 6
     opts = wdr.TranscribeOptions(lang="auto", advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
     ref, lang1 = _run(ctx, segs, opts, 1)
     ctx.set_early_fixup(2)
     got, lang = _run(ctx, segs, opts, 4)
     st = ctx.stage_times()
     assert st["early_fixup_segments"] > 0, st
+    if fallback:
+        assert st["replay_segments"] > 0, st
     assert lang == lang1 and got == ref
     ctx.set_early_fixup(0)
     got0, _ = _run(ctx, segs, opts, 4)

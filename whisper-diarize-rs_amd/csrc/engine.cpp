@@ -1720,6 +1720,13 @@ int wdr_dbg_encode(wdr_context* c, const float* mel_window, float* enc_out) {
   })
 }
 
+int wdr_dbg_cross_kv(wdr_context* c, float* out) {
+  WDR_GUARD({
+    c->st->read_cross_kv(out);
+    return 0;
+  })
+}
+
 int wdr_dbg_decode(wdr_context* c, const int32_t* tokens, size_t n, float* logits_out) {
   WDR_GUARD({
     c->st->decode_logits(tokens, (int)n, logits_out);

@@ -1,6 +1,12 @@
 #include "prof.h"
 
+#include <execinfo.h>
+#include <signal.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <mutex>
 #include <vector>
@@ -12,16 +18,20 @@ namespace wdr {
 namespace {
 struct Rec {
   hipEvent_t a, b;
+  int cls;
 };
+constexpr int kClasses = 8;
 std::mutex g_mu;
-int g_cls = PROF_NONE;
+std::atomic<int> g_mask{0};   // enabled classes, bit (1 << cls)
 bool g_broken = false;
 std::atomic<unsigned> g_tick{0};
 constexpr unsigned kEvery = 8;
 std::vector<Rec> g_pending;
 std::vector<hipEvent_t> g_pool;
-double g_ms = 0, g_bytes = 0, g_flops = 0;
-long long g_n = 0;
+struct Acc {
+  double ms = 0, bytes = 0, flops = 0;
+  long long n = 0;
+} g_acc[kClasses];
 
 void drain_locked() {
   for (auto& r : g_pending) {
@@ -30,12 +40,40 @@ void drain_locked() {
       (void)hipGetLastError();
       g_broken = true;
     }
-    g_ms += ms;
+    g_acc[r.cls].ms += ms;
     g_pool.push_back(r.a);
     g_pool.push_back(r.b);
   }
   g_pending.clear();
 }
+}  // namespace
+
+// WDR_SEGV_TRACE=1: a fatal signal prints the faulting address, the thread and the native
+// backtrace to stderr before the default action (root-causing faults under rocprofv3)
+namespace {
+void fatal_handler(int sig, siginfo_t* si, void*) {
+  char buf[160];
+  const int n = snprintf(buf, sizeof buf, "\n[wdr] fatal signal %d at address %p in thread %ld\n", sig,
+                         si ? si->si_addr : nullptr, (long)syscall(SYS_gettid));
+  if (n > 0) (void)!write(2, buf, (size_t)n);
+  void* bt[64];
+  const int k = backtrace(bt, 64);
+  backtrace_symbols_fd(bt, k, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+struct FatalInit {
+  FatalInit() {
+    const char* e = getenv("WDR_SEGV_TRACE");
+    if (!e || atoi(e) == 0) return;
+    struct sigaction sa {};
+    sa.sa_sigaction = fatal_handler;
+    sa.sa_flags = SA_SIGINFO;
+    sigaction(SIGSEGV, &sa, nullptr);
+    sigaction(SIGBUS, &sa, nullptr);
+    sigaction(SIGABRT, &sa, nullptr);
+  }
+} g_fatal_init;
 }  // namespace
 
 std::atomic<unsigned> g_step{0}, g_tick_out{0};
@@ -47,17 +85,17 @@ thread_local bool t_step = false;   // inside a sampled (eager) decode step
 // inside the sampled steps, 1 in kEvery * kStepEvery elsewhere (prefill, language detection),
 // so the average is over a uniform sample of the class's launches
 bool prof_on(int cls) {
-  if (g_cls == PROF_NONE || g_cls != cls || t_capture) return false;
+  if (!(g_mask.load(std::memory_order_relaxed) & (1 << cls)) || t_capture) return false;
   if (t_step) return (g_tick++ % kEvery) == 0;
   return (g_tick_out++ % (kEvery * kStepEvery)) == 0;
 }
 bool prof_step() {
-  if (g_cls == PROF_NONE) return false;
+  if (!g_mask.load(std::memory_order_relaxed)) return false;
   return (g_step++ % kStepEvery) == 0;
 }
 void prof_capture(bool on) { t_capture = on; }
 void prof_in_step(bool on) { t_step = on; }
-int prof_class() { return g_cls; }
+int prof_class() { return g_mask.load(); }
 
 std::mutex* launch_lock() {
   static std::mutex mu;
@@ -80,38 +118,56 @@ hipEvent_t prof_event() {
   return e;
 }
 
-void prof_push(hipEvent_t a, hipEvent_t b, double bytes, double flops) {
+void prof_push(int cls, hipEvent_t a, hipEvent_t b, double bytes, double flops) {
   std::lock_guard<std::mutex> l(g_mu);
-  g_pending.push_back({a, b});
-  g_bytes += bytes;
-  g_flops += flops;
-  g_n++;
+  g_pending.push_back({a, b, cls});
+  g_acc[cls].bytes += bytes;
+  g_acc[cls].flops += flops;
+  g_acc[cls].n++;
   if (g_pending.size() > 4096) drain_locked();
 }
 
 }  // namespace wdr
 
 extern "C" {
-int wdr_prof_set(int32_t cls) {
+int wdr_prof_set_mask(int32_t mask) {
   std::lock_guard<std::mutex> l(wdr::g_mu);
   wdr::drain_locked();
-  wdr::g_cls = cls;
+  wdr::g_mask = mask & ((1 << wdr::kClasses) - 2);
   wdr::g_broken = false;
   wdr::g_tick = 0;
   wdr::g_step = 0;
   wdr::g_tick_out = 0;
-  wdr::g_ms = wdr::g_bytes = wdr::g_flops = 0;
-  wdr::g_n = 0;
+  for (auto& a : wdr::g_acc) a = wdr::Acc{};
   return 0;
 }
-int wdr_prof_read(double* total_ms, int64_t* launches, double* algo_bytes, double* algo_flops) {
+int wdr_prof_set(int32_t cls) { return wdr_prof_set_mask(cls > 0 && cls < wdr::kClasses ? (1 << cls) : 0); }
+int wdr_prof_read_class(int32_t cls, double* total_ms, int64_t* launches, double* algo_bytes, double* algo_flops) {
   std::lock_guard<std::mutex> l(wdr::g_mu);
   wdr::drain_locked();
   if (wdr::g_broken) return -2;
-  *total_ms = wdr::g_ms;
-  *launches = wdr::g_n;
-  *algo_bytes = wdr::g_bytes;
-  *algo_flops = wdr::g_flops;
+  if (cls <= 0 || cls >= wdr::kClasses) return -1;
+  *total_ms = wdr::g_acc[cls].ms;
+  *launches = wdr::g_acc[cls].n;
+  *algo_bytes = wdr::g_acc[cls].bytes;
+  *algo_flops = wdr::g_acc[cls].flops;
+  return 0;
+}
+int wdr_prof_read(double* total_ms, int64_t* launches, double* algo_bytes, double* algo_flops) {
+  // the sum over the enabled classes (one class: that class)
+  double ms = 0, by = 0, fl = 0;
+  int64_t n = 0;
+  for (int c = 1; c < wdr::kClasses; ++c) {
+    if (!(wdr::g_mask.load() & (1 << c))) continue;
+    double a, b, d;
+    int64_t k;
+    if (wdr_prof_read_class(c, &a, &k, &b, &d) != 0) return -2;
+    ms += a; n += k; by += b; fl += d;
+  }
+  *total_ms = ms;
+  *launches = n;
+  *algo_bytes = by;
+  *algo_flops = fl;
   return 0;
 }
 }

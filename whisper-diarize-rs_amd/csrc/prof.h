@@ -1,5 +1,5 @@
-// Live per-kernel-class timing for bench.py's roofline figure.  One class is enabled at a
-// time; 1 in 8 launches of that class is issued with hipExtLaunchKernelGGL start/stop events
+// Live per-kernel-class timing for bench.py's roofline figures.  Any set of classes can be
+// enabled at once (each accumulates separately); 1 in 8 launches of that class is issued with hipExtLaunchKernelGGL start/stop events
 // (timestamps of the dispatch itself, the same interval rocprofv3 reports), together with the
 // launch's algorithmic bytes and flops.  Graph replay is bypassed while a class is enabled.
 #pragma once
@@ -24,7 +24,7 @@ bool prof_step();
 void prof_capture(bool on);
 void prof_in_step(bool on);   // around the eager launches of a step prof_step() picked
 hipEvent_t prof_event();
-void prof_push(hipEvent_t a, hipEvent_t b, double bytes, double flops);
+void prof_push(int cls, hipEvent_t a, hipEvent_t b, double bytes, double flops);
 // WDR_LAUNCH_LOCK=1: kernel launches from the decode-chain threads go through one process-wide
 // mutex (profiling runs: rocprofv3's kernel tracing faults on concurrent multi-thread launches)
 std::mutex* launch_lock();
@@ -37,7 +37,7 @@ inline void wdr_launch(int cls, double bytes, double flops, F kernel, dim3 grid,
   if (prof_on(cls)) {
     hipEvent_t a = prof_event(), b = prof_event();
     hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, a, b, 0, args...);
-    prof_push(a, b, bytes, flops);
+    prof_push(cls, a, b, bytes, flops);
   } else {
     hipLaunchKernelGGL(kernel, grid, block, shmem, s, args...);
   }

@@ -220,6 +220,7 @@ class State {
   void encode_window(int seek);
   void encode_from_mel_window(const float* mel_window);    // [n_mels][3000] normalised, host
   void read_encoder_out(float* out);                       // [1500][d] (ln_post output, f16 -> f32)
+  void read_cross_kv(float* out);                          // [1500][L][2][d] of the last encoded window
   void decode_logits(const int* toks, int n, float* logits_out);   // prefill from an empty cache
   void dbg_step(const int* toks, int n, bool classic, float* logits_out);
   bool persistent_step() const;

@@ -810,6 +810,15 @@ void State::encode_from_mel_window(const float* w) {
   WDR_HIP(hipStreamSynchronize(s_));
 }
 
+void State::read_cross_kv(float* out) {
+  Impl& m = *m_;
+  const size_t n = (size_t)1500 * ctx_.model.hp.n_text_layer * 2 * ctx_.model.hp.n_text_state;
+  std::vector<f16> h(n);
+  WDR_HIP(hipMemcpyAsync(h.data(), m.xkv(), n * 2, hipMemcpyDeviceToHost, s_));
+  WDR_HIP(hipStreamSynchronize(s_));
+  for (size_t i = 0; i < n; ++i) out[i] = (float)h[i];
+}
+
 void State::read_encoder_out(float* out) {
   Impl& m = *m_;
   std::vector<f16> h((size_t)1500 * m.d);

@@ -642,6 +642,13 @@ class WhisperContext:
                                          out.ctypes.data_as(C.POINTER(C.c_float))))
         return out
 
+    def cross_kv(self) -> np.ndarray:
+        """Cross K/V of the last encode() window: [1500][n_text_layer][2][d]."""
+        h = self.hparams
+        out = np.zeros((1500, h["n_text_layer"], 2, h["n_text_state"]), np.float32)
+        L.check(self._lib.wdr_dbg_cross_kv(self.h, out.ctypes.data_as(C.POINTER(C.c_float))))
+        return out
+
     def decode(self, tokens) -> np.ndarray:
         t = np.ascontiguousarray(tokens, np.int32)
         out = np.zeros(self.hparams["n_vocab"], np.float32)

@@ -146,6 +146,8 @@ _SIGS = {
     "wdr_context_hparams": (C.c_int, [vp, P(i32)]),
     "wdr_prof_set": (C.c_int, [i32]),
     "wdr_prof_read": (C.c_int, [P(f64), P(i64), P(f64), P(f64)]),
+    "wdr_prof_set_mask": (C.c_int, [i32]),
+    "wdr_prof_read_class": (C.c_int, [i32, P(f64), P(i64), P(f64), P(f64)]),
     "wdr_state_full": (C.c_int, [vp, P(f32), sz, P(TranscribeOptions), P(Synthetic), cstr, P(P(ResultSeg)), P(sz),
                                  P(i32)]),
     "wdr_result_free": (None, [P(ResultSeg), sz]),
@@ -153,6 +155,7 @@ _SIGS = {
     "wdr_dbg_energy": (C.c_int, [P(f32), sz, P(f32)]),
     "wdr_dbg_encode": (C.c_int, [vp, P(f32), P(f32)]),
     "wdr_dbg_decode": (C.c_int, [vp, P(i32), sz, P(f32)]),
+    "wdr_dbg_cross_kv": (C.c_int, [vp, P(f32)]),
     "wdr_dbg_step": (C.c_int, [vp, P(i32), sz, i32, P(f32)]),
     "wdr_dbg_step_trace": (C.c_int, [vp, P(u64), i32, P(i32)]),
     "wdr_dbg_capture": (C.c_int, [vp, P(i32), sz, P(f32)]),
