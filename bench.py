@@ -248,11 +248,13 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     import ctypes as C
-    live = {}
+    live, live_ev = {}, {}
     for c in prof:
         ms, nl, by, fl = C.c_double(), C.c_int64(), C.c_double(), C.c_double()
-        if lib.wdr_prof_read_class(CLS[c], C.byref(ms), C.byref(nl), C.byref(by), C.byref(fl)) == 0 and nl.value:
+        if lib.wdr_prof_read_clock(CLS[c], C.byref(ms), C.byref(nl), C.byref(by), C.byref(fl)) == 0 and nl.value:
             live[c] = (ms.value, nl.value, by.value, fl.value)
+        if lib.wdr_prof_read_class(CLS[c], C.byref(ms), C.byref(nl), C.byref(by), C.byref(fl)) == 0 and nl.value:
+            live_ev[c] = (ms.value, nl.value)
     lib.wdr_prof_set_mask(0)
     times = ctx.stage_times()
     t = torch.tensor([dt], dtype=torch.float64)
@@ -264,8 +266,11 @@ def main():
     value = world * shard_s * args.steps / dt_max
 
     # per class: algorithmic flops (MFMA classes) or bytes (HBM classes) per launch / the average
-    # duration of its HIP-event-timed launches; `roofline` is the class with the largest share
-    # of kernel time (every class is sampled at the same rate, csrc/prof.cpp)
+    # duration of its sampled launches, timed by the kernels' own clock (first wave start -> last
+    # wave end: rocprofv3's dispatch span; csrc/common.h ProfClock); the same launches' HIP
+    # start/stop events are reported beside it (under the pipeline's multi-stream concurrency
+    # they also absorb the launch's wait for the GPU).  `roofline` is the class with the largest
+    # share of kernel time (every class is sampled at the same rate, csrc/prof.cpp)
     classes = {}
     for c, (ms, nl, by, fl) in live.items():
         if ms <= 0:
@@ -279,7 +284,9 @@ def main():
             r = {"kernel": c, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                  "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_launch": by / nl}
         r.update({"traffic": None, "sampled_launches": nl, "avg_launch_us": round(ms * 1e3 / nl, 3),
-                  "sampled_ms": round(ms, 3)})
+                  "sampled_ms": round(ms, 3), "timing": "kernel clock (wall_clock64, first wave -> last wave)"})
+        if c in live_ev:
+            r["hip_event_avg_launch_us"] = round(live_ev[c][0] * 1e3 / live_ev[c][1], 3)
         tr, src = pmc_traffic(c)
         if tr is not None:
             r["traffic"] = round(tr)

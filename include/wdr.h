@@ -286,6 +286,10 @@ int wdr_prof_set(int32_t cls);
 /* several classes at once: bit (1 << cls) per class; read each with wdr_prof_read_class */
 int wdr_prof_set_mask(int32_t mask);
 int wdr_prof_read_class(int32_t cls, double* total_ms, int64_t* launches, double* algo_bytes, double* algo_flops);
+/* the same sampled launches timed by the kernels' own clock (first wave start -> last wave end,
+ * wall_clock64; the span rocprofv3's dispatch timestamps measure) instead of HIP events, which
+ * under multi-stream concurrency also absorb the launch's wait for the GPU */
+int wdr_prof_read_clock(int32_t cls, double* total_ms, int64_t* launches, double* algo_bytes, double* algo_flops);
 int wdr_prof_read(double* total_ms, int64_t* launches, double* algo_bytes, double* algo_flops);
 
 /* ---- whisper_full-level test seam: one state.full() call, raw token data ---- */

@@ -83,7 +83,27 @@ struct ProjArgs {
   // decode-step rows (up to 16, the multi-chain batched step): stay on the GEMV kernels, whose
   // per-row arithmetic does not depend on the row count
   int step_rows = 0;
+  unsigned long long* ts = nullptr;   // live kernel clock of a sampled launch (ProfClock)
 };
+
+// Live kernel clock (csrc/prof.cpp): a launch the profiler samples carries ts -> {earliest wave
+// start, latest wave end} in wall_clock64() ticks (the constant-rate clock), i.e. the span
+// rocprofv3's dispatch timestamps measure, free of the queueing that HIP start/stop events of a
+// launch absorb under multi-stream concurrency.  Lane 0 of every wave stamps with vector
+// atomics; unsampled launches (ts null) skip it.
+struct ProfClock {
+  unsigned long long* ts;
+  __device__ __forceinline__ explicit ProfClock(unsigned long long* t) : ts(t) {
+    if (ts && (threadIdx.x & 63) == 0) atomicMin(ts, (unsigned long long)wall_clock64());
+  }
+  __device__ __forceinline__ ~ProfClock() {
+    if (ts && (threadIdx.x & 63) == 0) atomicMax(ts + 1, (unsigned long long)wall_clock64());
+  }
+};
+unsigned long long* prof_slot();   // next clock slot of the sampled-launch ring (null when full)
+template <typename A>
+inline unsigned long long* prof_attach(A&) { return nullptr; }
+inline unsigned long long* prof_attach(ProjArgs& a) { return a.ts = prof_slot(); }
 void launch_proj(const ProjArgs& a, hipStream_t s);   // picks GEMV (M<=8) or MFMA GEMM
 // the LayerNorm prologue of a decode-step projection as its own launch (k_dgemv's arithmetic):
 // rows ln_x -> y [M][ldy] f16

@@ -26,6 +26,7 @@ namespace wdr {
 constexpr int FA_KB = 64, FA_KS = 72, FA_VS = 68;
 
 __global__ __launch_bounds__(256) void k_flash_attn(FlashArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
   __shared__ __attribute__((aligned(16))) f16 Ks[FA_KB * FA_KS];
   __shared__ __attribute__((aligned(16))) f16 Vt[64 * FA_VS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -273,6 +274,7 @@ constexpr int XA_KC = 64, XA_RMAX = 8;
 // one workgroup per (64-key chunk, head): the chunk's K and V (8 KB each) are fetched with all
 // 16-B loads issued up front, staged in LDS and shared by every decoder row (beam) of the step.
 __global__ __launch_bounds__(256) void k_xattn_partial(XAttnArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
   __shared__ __attribute__((aligned(16))) f16 Ks[XA_KC * 72];
   __shared__ __attribute__((aligned(16))) f16 Vs[XA_KC * 64];
   __shared__ float qs[XA_RMAX][64];
@@ -339,6 +341,7 @@ __global__ __launch_bounds__(256) void k_xattn_partial(XAttnArgs a) {
 // segments batched into one step by the multi-chain decoder, whisper_ctx.cpp StepBatcher)
 template <bool ROWS>
 __global__ __launch_bounds__(256) void k_xattn_partial1(XAttnArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
   __shared__ __attribute__((aligned(16))) f16 Vs[XA_KC * 64];
   __shared__ float red[2][4];
   __shared__ float ps[XA_KC];

@@ -52,6 +52,7 @@ __device__ __forceinline__ void epi_store(const ProjArgs& a, int row, int col, f
 
 template <int EPI>
 __global__ __launch_bounds__(256, 2) void k_gemm(ProjArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
   __shared__ __attribute__((aligned(16))) f16 sA[2][GB_M * GLDS];
   __shared__ __attribute__((aligned(16))) f16 sB[2][GB_N * GLDS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -161,6 +162,7 @@ __device__ __forceinline__ int g2_swz(int r, int c) { return c ^ ((r >> 1) & 7);
 
 template <int EPI>
 __global__ __launch_bounds__(256, 2) void k_gemm2(ProjArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
   __shared__ __attribute__((aligned(16))) f16 lds[2][2][GB_M * G2_BK];   // [buf][A,B][128 x 64]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // XCD-aware tile order (bijective for any tile count)
@@ -330,6 +332,7 @@ __device__ __forceinline__ void gemv_store(const ProjArgs& a, float (&acc)[MR], 
 // grid = ceil(N / 4R), one pass, no grid-stride loop.
 template <int EPI, int MR, int R, int NCH, bool LN>
 __global__ __launch_bounds__(256) void k_dgemv(ProjArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int n0 = (blockIdx.x * 4 + wid) * R;
   const int K = a.K, M = a.M;
@@ -474,6 +477,7 @@ __global__ __launch_bounds__(256) void k_dgemv(ProjArgs a) {
 // runs over the chunks in the same order as k_dgemv, then the same wave reduction.
 template <int EPI, int MR, int R, int NCH, bool LN>
 __global__ __launch_bounds__(256) void k_mgemv(ProjArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
   constexpr int KP = NCH * 512;
   constexpr int LR = LN ? (MR + 3) / 4 : 1;   // LayerNorm rows per wave
   extern __shared__ __attribute__((aligned(16))) f16 xsh[];   // LN: [MR][KP] normalised rows
@@ -735,6 +739,7 @@ __device__ __forceinline__ float reduce_scatter(float (&v)[V], int lane) {
 // multiplied.  Per row, the arithmetic is that of the NP = 1 kernel.
 template <int EPI, int MR, int R, int NCH, int NP = 1>
 __global__ __launch_bounds__(256) void k_mgemv_s(ProjArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
   constexpr int KP = NCH * 512, V = R * MR;
   constexpr int SH = V >= 64 ? 0 : V >= 32 ? 1 : V >= 16 ? 2 : V >= 8 ? 3 : V >= 4 ? 4 : V >= 2 ? 5 : 6;
   constexpr int NV = MR * KP / 8, PER = (NV + 255) / 256;
@@ -843,6 +848,7 @@ __global__ __launch_bounds__(256) void k_mgemv_s(ProjArgs a) {
 // General GEMV (optional LN prologue through LDS for 2 < M <= 8).
 template <int EPI, int MR, bool LN>
 __global__ __launch_bounds__(256) void k_gemv(ProjArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
   extern __shared__ __attribute__((aligned(16))) f16 xs[];   // [MR][K] when LN
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   if constexpr (LN) {

@@ -91,7 +91,9 @@ struct FlashArgs {
   int nsplit = 1;
   float* part_o = nullptr;     // [nsplit][Tq][n_head][64]
   float2* part_ml = nullptr;   // [nsplit][n_head][Tq]
+  unsigned long long* ts = nullptr;   // live kernel clock (common.h ProfClock)
 };
+inline unsigned long long* prof_attach(FlashArgs& a) { return a.ts = prof_slot(); }
 void launch_flash_attn(const FlashArgs& a, int n_batch, hipStream_t s);
 struct DecSelfArgs {
   const f16* q; int ldq;
@@ -114,7 +116,9 @@ struct XAttnArgs {
   // (device array of slot bases), its V d columns further; k / v unused then
   const f16* const* row_k = nullptr;
   long long layer_off = 0;
+  unsigned long long* ts = nullptr;   // live kernel clock (common.h ProfClock)
 };
+inline unsigned long long* prof_attach(XAttnArgs& a) { return a.ts = prof_slot(); }
 void launch_xattn(const XAttnArgs& a, hipStream_t s);
 struct CaptureArgs {
   const f16* q; int ldq;

@@ -20,6 +20,12 @@ struct Rec {
   hipEvent_t a, b;
   int cls;
 };
+struct ClkRec {
+  long long slot;   // kernel-clock slot in the ring
+  int cls;
+  double bytes, flops;
+};
+std::vector<ClkRec> g_clk_pending;
 constexpr int kClasses = 8;
 std::mutex g_mu;
 std::atomic<int> g_mask{0};   // enabled classes, bit (1 << cls)
@@ -31,9 +37,41 @@ std::vector<hipEvent_t> g_pool;
 struct Acc {
   double ms = 0, bytes = 0, flops = 0;
   long long n = 0;
+  double clk_ms = 0, clk_bytes = 0, clk_flops = 0;   // launches whose kernel clock span was read
+  long long clk_n = 0;
 } g_acc[kClasses];
 
-void drain_locked() {
+// kernel-clock ring: {start, end} u64 pairs, initialised to {~0, 0}; slots are handed out in
+// order and read back (with a device synchronisation) only at drain time
+constexpr long long kRing = 1 << 20;
+unsigned long long* g_ring = nullptr;
+std::atomic<long long> g_next{0};
+double g_tick_ms = 0.0;   // wall_clock64 period in ms
+
+void ring_reset_locked() {
+  if (!g_ring) {
+    if (hipMalloc(&g_ring, (size_t)kRing * 16) != hipSuccess) {
+      (void)hipGetLastError();
+      g_ring = nullptr;
+      return;
+    }
+    int dev = 0, khz = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+    g_tick_ms = 1.0 / (double)khz;
+  }
+  std::vector<unsigned long long> init((size_t)kRing * 2);
+  for (long long i = 0; i < kRing; ++i) {
+    init[2 * i] = ~0ull;
+    init[2 * i + 1] = 0ull;
+  }
+  if (hipMemcpy(g_ring, init.data(), init.size() * 8, hipMemcpyHostToDevice) != hipSuccess) (void)hipGetLastError();
+  g_next = 0;
+}
+
+// events: waited for and folded in (batches during the run); kernel clocks (read_ring): read
+// back once, after a device synchronisation, at read time
+void drain_locked(bool read_ring = true) {
   for (auto& r : g_pending) {
     float ms = 0;
     if (hipEventSynchronize(r.b) != hipSuccess || hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) {
@@ -45,8 +83,33 @@ void drain_locked() {
     g_pool.push_back(r.b);
   }
   g_pending.clear();
+  if (!read_ring || g_clk_pending.empty() || !g_ring) return;
+  std::vector<unsigned long long> ring((size_t)std::min<long long>(g_next.load(), kRing) * 2);
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(ring.data(), g_ring, ring.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) {
+    (void)hipGetLastError();
+    g_broken = true;
+    return;
+  }
+  for (auto& r : g_clk_pending) {
+    if ((size_t)(2 * r.slot + 1) >= ring.size()) continue;
+    const unsigned long long t0 = ring[2 * r.slot], t1 = ring[2 * r.slot + 1];
+    if (t0 == ~0ull || t1 < t0) continue;
+    Acc& A = g_acc[r.cls];
+    A.clk_ms += (double)(t1 - t0) * g_tick_ms;
+    A.clk_n++;
+    A.clk_bytes += r.bytes;
+    A.clk_flops += r.flops;
+  }
+  g_clk_pending.clear();
 }
 }  // namespace
+
+unsigned long long* prof_slot() {
+  if (!g_ring) return nullptr;
+  const long long i = g_next++;
+  return i < kRing ? g_ring + 2 * i : nullptr;
+}
 
 // WDR_SEGV_TRACE=1: a fatal signal prints the faulting address, the thread and the native
 // backtrace to stderr before the default action (root-causing faults under rocprofv3)
@@ -118,13 +181,14 @@ hipEvent_t prof_event() {
   return e;
 }
 
-void prof_push(int cls, hipEvent_t a, hipEvent_t b, double bytes, double flops) {
+void prof_push(int cls, hipEvent_t a, hipEvent_t b, unsigned long long* ts, double bytes, double flops) {
   std::lock_guard<std::mutex> l(g_mu);
   g_pending.push_back({a, b, cls});
+  if (ts && g_ring) g_clk_pending.push_back({(long long)((ts - g_ring) / 2), cls, bytes, flops});
   g_acc[cls].bytes += bytes;
   g_acc[cls].flops += flops;
   g_acc[cls].n++;
-  if (g_pending.size() > 4096) drain_locked();
+  if (g_pending.size() > 4096) drain_locked(false);
 }
 
 }  // namespace wdr
@@ -134,6 +198,8 @@ int wdr_prof_set_mask(int32_t mask) {
   std::lock_guard<std::mutex> l(wdr::g_mu);
   wdr::drain_locked();
   wdr::g_mask = mask & ((1 << wdr::kClasses) - 2);
+  wdr::g_clk_pending.clear();
+  if (wdr::g_mask) wdr::ring_reset_locked();
   wdr::g_broken = false;
   wdr::g_tick = 0;
   wdr::g_step = 0;
@@ -151,6 +217,17 @@ int wdr_prof_read_class(int32_t cls, double* total_ms, int64_t* launches, double
   *launches = wdr::g_acc[cls].n;
   *algo_bytes = wdr::g_acc[cls].bytes;
   *algo_flops = wdr::g_acc[cls].flops;
+  return 0;
+}
+int wdr_prof_read_clock(int32_t cls, double* total_ms, int64_t* launches, double* algo_bytes, double* algo_flops) {
+  std::lock_guard<std::mutex> l(wdr::g_mu);
+  wdr::drain_locked();
+  if (wdr::g_broken) return -2;
+  if (cls <= 0 || cls >= wdr::kClasses) return -1;
+  *total_ms = wdr::g_acc[cls].clk_ms;
+  *launches = wdr::g_acc[cls].clk_n;
+  *algo_bytes = wdr::g_acc[cls].clk_bytes;
+  *algo_flops = wdr::g_acc[cls].clk_flops;
   return 0;
 }
 int wdr_prof_read(double* total_ms, int64_t* launches, double* algo_bytes, double* algo_flops) {

@@ -24,22 +24,26 @@ bool prof_step();
 void prof_capture(bool on);
 void prof_in_step(bool on);   // around the eager launches of a step prof_step() picked
 hipEvent_t prof_event();
-void prof_push(int cls, hipEvent_t a, hipEvent_t b, double bytes, double flops);
 // WDR_LAUNCH_LOCK=1: kernel launches from the decode-chain threads go through one process-wide
 // mutex (profiling runs: rocprofv3's kernel tracing faults on concurrent multi-thread launches)
 std::mutex* launch_lock();
 
-template <typename F, typename... Args>
+void prof_push(int cls, hipEvent_t a, hipEvent_t b, unsigned long long* ts, double bytes, double flops);
+
+// a sampled launch carries HIP start/stop events and, for argument structs with a ProfClock
+// slot (ProjArgs, FlashArgs, XAttnArgs: prof_attach), the kernel's own clock span
+template <typename F, typename A0, typename... Args>
 inline void wdr_launch(int cls, double bytes, double flops, F kernel, dim3 grid, dim3 block, uint32_t shmem,
-                       hipStream_t s, Args... args) {
+                       hipStream_t s, A0 a0, Args... args) {
   std::mutex* mu = launch_lock();
   if (mu) mu->lock();
   if (prof_on(cls)) {
     hipEvent_t a = prof_event(), b = prof_event();
-    hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, a, b, 0, args...);
-    prof_push(cls, a, b, bytes, flops);
+    unsigned long long* ts = prof_attach(a0);
+    hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, a, b, 0, a0, args...);
+    prof_push(cls, a, b, ts, bytes, flops);
   } else {
-    hipLaunchKernelGGL(kernel, grid, block, shmem, s, args...);
+    hipLaunchKernelGGL(kernel, grid, block, shmem, s, a0, args...);
   }
   if (mu) mu->unlock();
 }

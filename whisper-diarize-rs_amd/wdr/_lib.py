@@ -148,6 +148,7 @@ _SIGS = {
     "wdr_prof_read": (C.c_int, [P(f64), P(i64), P(f64), P(f64)]),
     "wdr_prof_set_mask": (C.c_int, [i32]),
     "wdr_prof_read_class": (C.c_int, [i32, P(f64), P(i64), P(f64), P(f64)]),
+    "wdr_prof_read_clock": (C.c_int, [i32, P(f64), P(i64), P(f64), P(f64)]),
     "wdr_state_full": (C.c_int, [vp, P(f32), sz, P(TranscribeOptions), P(Synthetic), cstr, P(P(ResultSeg)), P(sz),
                                  P(i32)]),
     "wdr_result_free": (None, [P(ResultSeg), sz]),
