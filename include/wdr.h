@@ -178,6 +178,11 @@ int wdr_transcribe_audio(wdr_engine* e, const char* audio_path, const wdr_transc
 
 /* ---- seams ---- */
 int wdr_read_wav(const char* path, int16_t** samples, size_t* n);
+/* test seam (host only, no GPU): parse a VAD / diarization model file the way the models load
+ * it -- kind 0 whisper.cpp Silero ggml, 1 segmentation-3.0 ONNX, 2 CAM++ ONNX -- and return its
+ * tensors under the oracle's names: names_out "name:count\n" per tensor (sorted), data_out the
+ * values concatenated in that order.  Free both with wdr_free. */
+int wdr_dbg_model_file(int32_t kind, const char* path, char** names_out, float** data_out, size_t* n_values);
 /* formatting::process_segments (src/formatting.rs:240-313) with PostProcessConfig::for_language(lang)
  * + overrides (nullable), and a VadMaskOracle over vad_mask (2 doubles per interval) when
  * has_mask (src/engine.rs:192-199).  Free the result with wdr_segment_list_free. */

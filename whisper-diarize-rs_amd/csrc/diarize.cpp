@@ -8,6 +8,8 @@
 #include <array>
 #include <cstring>
 
+#include "model_files.h"
+
 namespace wdr {
 
 static uint64_t splitmix64_host(uint64_t x) {
@@ -60,15 +62,22 @@ struct SegModel::W {
 };
 
 SegModel::SegModel(int dev, const std::string& path) : device(dev) {
-  if (!path.empty()) throw std::runtime_error("segmentation model file: ONNX loading not available yet: " + path);
+  // segmentation-3.0.onnx (model_files.cpp), or the seeded synthetic weights of oracle/diarize.py
+  const TensorMap file = path.empty() ? TensorMap() : load_segmentation_onnx(path);
+  auto get = [&](const std::string& n, size_t cnt, double sd, bool plus1) {
+    if (file.empty()) return plus1 ? plus_one(synth_f32_host("seg." + n, cnt, sd)) : synth_f32_host("seg." + n, cnt, sd);
+    const std::vector<float>& v = file.at(n);
+    WDR_CHECK(v.size() == cnt, "segmentation model: tensor " + n + " size mismatch");
+    return v;
+  };
   WDR_HIP(hipSetDevice(dev));
   WDR_HIP(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking));
   WDR_HIP(hipEventCreate(&e0_));
   WDR_HIP(hipEventCreate(&e1_));
   w_ = new W;
   Arena A;
-  auto f = [&](const std::string& n, size_t cnt, double sd) { return A.add(synth_f32_host("seg." + n, cnt, sd)); };
-  auto one = [&](const std::string& n, size_t cnt) { return A.add(plus_one(synth_f32_host("seg." + n, cnt, 0.1))); };
+  auto f = [&](const std::string& n, size_t cnt, double sd) { return A.add(get(n, cnt, sd, false)); };
+  auto one = [&](const std::string& n, size_t cnt) { return A.add(get(n, cnt, 0.1, true)); };
   size_t o_wng = one("wav_norm.weight", 1), o_wnb = f("wav_norm.bias", 1, 0.1);
   size_t o_sinc = f("sinc.weight", 80 * 251, 1.0 / std::sqrt(251.0));
   size_t o_ng[3], o_nb[3];
@@ -84,28 +93,28 @@ SegModel::SegModel(int dev, const std::string& path) : device(dev) {
     const int I = l == 0 ? 60 : 256;
     const std::string L = std::to_string(l);
     // both directions stacked: rows [0,512) forward, [512,1024) reverse
-    std::vector<float> wih = synth_f32_host("seg.lstm.weight_ih_l" + L, 512 * I, 1.0 / std::sqrt(128.0));
-    std::vector<float> wr = synth_f32_host("seg.lstm.weight_ih_l" + L + "_reverse", 512 * I, 1.0 / std::sqrt(128.0));
+    std::vector<float> wih = get("lstm.weight_ih_l" + L, 512 * I, 1.0 / std::sqrt(128.0), false);
+    std::vector<float> wr = get("lstm.weight_ih_l" + L + "_reverse", 512 * I, 1.0 / std::sqrt(128.0), false);
     wih.insert(wih.end(), wr.begin(), wr.end());
     o_wih[l] = A.add(wih);
-    std::vector<float> bih = synth_f32_host("seg.lstm.bias_ih_l" + L, 512, 0.05);
-    std::vector<float> br = synth_f32_host("seg.lstm.bias_ih_l" + L + "_reverse", 512, 0.05);
+    std::vector<float> bih = get("lstm.bias_ih_l" + L, 512, 0.05, false);
+    std::vector<float> br = get("lstm.bias_ih_l" + L + "_reverse", 512, 0.05, false);
     bih.insert(bih.end(), br.begin(), br.end());
     o_bih[l] = A.add(bih);
-    std::vector<float> whh = synth_f32_host("seg.lstm.weight_hh_l" + L, 512 * 128, 1.0 / std::sqrt(128.0));
-    std::vector<float> whr = synth_f32_host("seg.lstm.weight_hh_l" + L + "_reverse", 512 * 128, 1.0 / std::sqrt(128.0));
+    std::vector<float> whh = get("lstm.weight_hh_l" + L, 512 * 128, 1.0 / std::sqrt(128.0), false);
+    std::vector<float> whr = get("lstm.weight_hh_l" + L + "_reverse", 512 * 128, 1.0 / std::sqrt(128.0), false);
     whh.insert(whh.end(), whr.begin(), whr.end());
     o_whh[l] = A.add(whh);
-    std::vector<float> bhh = synth_f32_host("seg.lstm.bias_hh_l" + L, 512, 0.05);
-    std::vector<float> bhr = synth_f32_host("seg.lstm.bias_hh_l" + L + "_reverse", 512, 0.05);
+    std::vector<float> bhh = get("lstm.bias_hh_l" + L, 512, 0.05, false);
+    std::vector<float> bhr = get("lstm.bias_hh_l" + L + "_reverse", 512, 0.05, false);
     bhh.insert(bhh.end(), bhr.begin(), bhr.end());
     o_bhh[l] = A.add(bhh);
   }
   size_t o_l0w = f("linear0.weight", 128 * 256, 1.0 / std::sqrt(256.0)), o_l0b = f("linear0.bias", 128, 0.05);
   size_t o_l1w = f("linear1.weight", 128 * 128, 1.0 / std::sqrt(128.0)), o_l1b = f("linear1.bias", 128, 0.05);
   size_t o_cw = f("classifier.weight", 7 * 128, 8.0 / std::sqrt(128.0));
-  std::vector<float> cb = synth_f32_host("seg.classifier.bias", 7, 0.05);
-  cb[0] = cb[0] + kClass0Offset;
+  std::vector<float> cb = get("classifier.bias", 7, 0.05, false);
+  if (file.empty()) cb[0] = cb[0] + kClass0Offset;   // synthetic calibration only (oracle/diarize.py)
   size_t o_cb = A.add(cb);
   W& w = *w_;
   w.arena = DevMem(A.host.size() * 4);
@@ -296,7 +305,14 @@ struct CamModel::W {
 static double mel_k(double f) { return 1127.0 * std::log(1.0 + f / 700.0); }
 
 CamModel::CamModel(int dev, const std::string& path) : device(dev) {
-  if (!path.empty()) throw std::runtime_error("embedding model file: ONNX loading not available yet: " + path);
+  // wespeaker_en_voxceleb_CAM++.onnx (model_files.cpp), or the seeded synthetic weights
+  const TensorMap file = path.empty() ? TensorMap() : load_campplus_onnx(path);
+  auto get = [&](const std::string& n, size_t cnt, double sd, bool plus1) {
+    if (file.empty()) return plus1 ? plus_one(synth_f32_host("cam." + n, cnt, sd)) : synth_f32_host("cam." + n, cnt, sd);
+    const std::vector<float>& v = file.at(n);
+    WDR_CHECK(v.size() == cnt, "embedding model: tensor " + n + " size mismatch");
+    return v;
+  };
   WDR_HIP(hipSetDevice(dev));
   // lowest priority: embeddings run beside the latency-bound decode chain (EmbedAhead)
   int lo = 0, hi = 0;
@@ -326,10 +342,10 @@ CamModel::CamModel(int dev, const std::string& path) : device(dev) {
     }
   }
   size_t o_pov = A.add(pov), o_ct = A.add(ct), o_st = A.add(st), o_banks = A.add(banks);
-  auto f = [&](const std::string& n, size_t cnt, double sd) { return A.add(synth_f32_host("cam." + n, cnt, sd)); };
+  auto f = [&](const std::string& n, size_t cnt, double sd) { return A.add(get(n, cnt, sd, false)); };
   auto bn = [&](const std::string& n, size_t c, size_t* s, size_t* b) {
-    *s = A.add(plus_one(synth_f32_host("cam." + n + ".scale", c, 0.1)));
-    *b = A.add(synth_f32_host("cam." + n + ".shift", c, 0.1));
+    *s = A.add(get(n + ".scale", c, 0.1, true));
+    *b = A.add(get(n + ".shift", c, 0.1, false));
   };
   const int m = 32;
   size_t o_c1 = f("head.conv1", m * 9, 1.0 / 3.0), o_bn1s, o_bn1b;
@@ -355,7 +371,7 @@ CamModel::CamModel(int dev, const std::string& path) : device(dev) {
   // TDNN weight: torch input channel c*10 + f, ours (FCM output [T][F][C]) f*32 + c
   size_t o_tdnn;
   {
-    std::vector<float> wt = synth_f32_host("cam.tdnn.linear", 128 * 320 * 5, 1.0 / std::sqrt(320.0 * 5));
+    std::vector<float> wt = get("tdnn.linear", 128 * 320 * 5, 1.0 / std::sqrt(320.0 * 5), false);
     std::vector<float> wp(wt.size());
     for (int o = 0; o < 128; ++o)
       for (int c = 0; c < 32; ++c)

@@ -33,6 +33,7 @@
 #include "vad.h"
 #include "whisper.h"
 #include "ggml_file.h"
+#include "model_files.h"
 
 using namespace wdr;
 
@@ -1480,6 +1481,32 @@ int wdr_process_segments(const wdr_segment* segs, size_t n_segs, const char* lan
     for (size_t i = 0; has_mask && i < n_mask; ++i) mask.push_back({vad_mask[2 * i], vad_mask[2 * i + 1]});
     const std::vector<Seg> res = from_fmt(process_segments(to_fmt(in), cfg, has_mask ? &mask : nullptr));
     *out = to_list(res, nullptr);
+    return 0;
+  })
+}
+
+int wdr_dbg_model_file(int32_t kind, const char* path, char** names_out, float** data_out, size_t* n_values) {
+  WDR_GUARD({
+    if (!path || !file_exists(path)) return fail("model file doesn't exist");
+    TensorMap tm;
+    if (kind == 0) tm = load_silero_ggml(path);
+    else if (kind == 1) tm = load_segmentation_onnx(path);
+    else if (kind == 2) tm = load_campplus_onnx(path);
+    else return fail("model file kind: 0 Silero ggml, 1 segmentation ONNX, 2 CAM++ ONNX");
+    std::string names;
+    size_t tot = 0;
+    for (auto& kv : tm) {
+      names += kv.first + ":" + std::to_string(kv.second.size()) + "\n";
+      tot += kv.second.size();
+    }
+    *names_out = strdup(names.c_str());
+    *data_out = (float*)malloc(std::max<size_t>(1, tot) * 4);
+    size_t o = 0;
+    for (auto& kv : tm) {
+      if (!kv.second.empty()) memcpy(*data_out + o, kv.second.data(), kv.second.size() * 4);
+      o += kv.second.size();
+    }
+    *n_values = tot;
     return 0;
   })
 }

@@ -5,6 +5,8 @@
 #include <climits>
 #include <cmath>
 
+#include "model_files.h"
+
 namespace wdr {
 
 namespace {
@@ -29,7 +31,7 @@ VadLayout layout() {
 }  // namespace
 
 VadModel::VadModel(int dev, const std::string& path) : device(dev) {
-  if (!path.empty()) throw std::runtime_error("VAD model file: Silero ggml loading not available yet: " + path);
+  const TensorMap file = path.empty() ? TensorMap() : load_silero_ggml(path);   // before any GPU work
   WDR_HIP(hipSetDevice(dev));
   WDR_HIP(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking));
   WDR_HIP(hipEventCreate(&e0_));
@@ -48,10 +50,29 @@ VadModel::VadModel(int dev, const std::string& path) : device(dev) {
       basis[k * 256 + t] = (f16)(std::cos(ang) * hann);
       basis[(129 + k) * 256 + t] = (f16)(-std::sin(ang) * hann);
     }
+  std::vector<std::vector<f16>> staged16;   // file mode: host images kept alive until the sync below
+  std::vector<std::vector<float>> staged32;
+  if (!file.empty()) {
+    const std::vector<float>& b = file.at("stft");
+    for (size_t i = 0; i < basis.size(); ++i) basis[i] = (f16)b[i];
+  }
   WDR_HIP(hipMemcpyAsync(b16 + L.stft, basis.data(), basis.size() * 2, hipMemcpyHostToDevice, s_));
   const double sq3 = std::sqrt(3.0);
+  // synthetic: seeded on the GPU; file: the tensor of that name (f16 matrices, f32 biases)
   auto fill = [&](void* dst, const std::string& nm, int n, bool is16, double sd) {
-    launch_synth_fill(dst, 1, n, n, fnv1a64(nm), (float)(sd * sq3), is16, 0, 0.f, s_);
+    if (file.empty()) {
+      launch_synth_fill(dst, 1, n, n, fnv1a64(nm), (float)(sd * sq3), is16, 0, 0.f, s_);
+      return;
+    }
+    const std::vector<float>& v = file.at(nm);
+    WDR_CHECK((int)v.size() == n, "VAD model: tensor size mismatch");
+    if (is16) {
+      staged16.emplace_back(v.begin(), v.end());
+      WDR_HIP(hipMemcpyAsync(dst, staged16.back().data(), (size_t)n * 2, hipMemcpyHostToDevice, s_));
+    } else {
+      staged32.push_back(v);
+      WDR_HIP(hipMemcpyAsync(dst, staged32.back().data(), (size_t)n * 4, hipMemcpyHostToDevice, s_));
+    }
   };
   const char* cn[4] = {"_model.encoder.0.reparam_conv", "_model.encoder.1.reparam_conv",
                        "_model.encoder.2.reparam_conv", "_model.encoder.3.reparam_conv"};

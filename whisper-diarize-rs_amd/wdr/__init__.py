@@ -511,6 +511,27 @@ class Diarizer:
             pass
 
 
+def model_file_tensors(kind: str, path: str) -> dict:
+    """Tensors of a VAD / diarization model file as libwdr's loader maps them (oracle names):
+    kind 'silero' (whisper.cpp ggml), 'segmentation' / 'campplus' (ONNX).  Host only."""
+    lib = L.load()
+    k = {"silero": 0, "segmentation": 1, "campplus": 2}[kind]
+    names, data, n = C.c_void_p(), C.POINTER(C.c_float)(), C.c_size_t()
+    L.check(lib.wdr_dbg_model_file(k, path.encode(), C.byref(names), C.byref(data), C.byref(n)))
+    try:
+        txt = C.cast(names, C.c_char_p).value.decode()
+        flat = np.ctypeslib.as_array(data, (max(1, n.value),))[:n.value].copy()
+    finally:
+        lib.wdr_free(names)
+        lib.wdr_free(C.cast(data, C.c_void_p))
+    out, o = {}, 0
+    for line in txt.splitlines():
+        name, cnt = line.rsplit(":", 1)
+        out[name] = flat[o:o + int(cnt)]
+        o += int(cnt)
+    return out
+
+
 def ggml_info(path: str) -> dict:
     """Header of a whisper.cpp ggml model file (wdr_ggml_info; parses the whole file, no GPU)."""
     lib = L.load()

@@ -109,6 +109,7 @@ _SIGS = {
     "wdr_transcribe_audio": (C.c_int, [vp, cstr, P(TranscribeOptions), P(FormattingOverrides), P(Callbacks),
                                        P(P(SegmentList))]),
     "wdr_read_wav": (C.c_int, [cstr, P(P(C.c_int16)), P(sz)]),
+    "wdr_dbg_model_file": (C.c_int, [i32, cstr, P(C.c_void_p), P(P(f32)), P(sz)]),
     "wdr_process_segments": (C.c_int, [P(Segment), sz, cstr, P(FormattingOverrides), i8, P(f64), sz,
                                        P(P(SegmentList))]),
     "wdr_free": (None, [vp]),
