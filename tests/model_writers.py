@@ -122,10 +122,10 @@ def _mutate(W, seed, keys=None):
 
 
 def write_segmentation_onnx(path, seed=1, gemm=False):
-    """PyanNet (segmentation-3.0) with the oracle's seg_weights(), mutated.  gemm: linear
-    layers as Gemm(transB=1) instead of MatMul + Add."""
+    """PyanNet (segmentation-3.0) with the oracle's seg_weights(), mutated (seed None: as
+    they are).  gemm: linear layers as Gemm(transB=1) instead of MatMul + Add."""
     from oracle import diarize as D
-    W = _mutate(D.seg_weights(), seed)
+    W = D.seg_weights() if seed is None else _mutate(D.seg_weights(), seed)
     g = Graph()
     x = "input_values"
     x = g.node("InstanceNormalization", [x, g.init(W["wav_norm.weight"]), g.init(W["wav_norm.bias"])], epsilon=1e-5)

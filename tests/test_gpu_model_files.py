@@ -73,7 +73,7 @@ def test_engine_uses_cached_model_files(tmp_path):
     vad_path = str(snap / "ggml-silero-v5.1.2.bin")
     write_silero_ggml(vad_path)
     seg_path, emb_path = str(cache / "segmentation-3.0.onnx"), str(cache / "wespeaker_en_voxceleb_CAM++.onnx")
-    write_segmentation_onnx(seg_path)
+    write_segmentation_onnx(seg_path, seed=None)   # the synthetic calibration: frames split speech / silence
     write_campplus_onnx(emb_path)
     pcm, _ = synth_speech(25.0, seed=8, n_speakers=2)
     wav = str(tmp_path / "a.wav")
@@ -93,6 +93,7 @@ def test_engine_uses_cached_model_files(tmp_path):
                                  advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
     got = eng.transcribe_audio(wav, opts)
     dsegs = wdr.Diarizer(segment_model_path=seg_path).get_segments(pcm)
+    assert len(dsegs) > 0
     want, lang = ctx.run_pipeline(dsegs, opts, diarize_options=wdr.DiarizeOptions.from_options(opts, seg_path, emb_path))
     want = wdr.process_segments(want, lang or "en")
     assert len(got) > 0
