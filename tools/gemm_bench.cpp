@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <vector>
 #include <cmath>
+#include <algorithm>
 
 #include "../whisper-diarize-rs_amd/csrc/common.h"
 #include "../whisper-diarize-rs_amd/csrc/kernels/kernels.h"
@@ -56,22 +57,38 @@ int main(int argc, char** argv) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  std::vector<float> r1, r2;
+  std::vector<float> ref, r;
+  const char* vname[3] = {"gemm ", "gemm2", "gemm3"};
   for (const Shape& sh : shapes) {
-    for (int variant = 0; variant < 2; ++variant) {
-      // variant 0: k_gemm (register staging, WDR_GEMM1), 1: the production choice (k_gemm2 for N <= 4096)
+    for (int variant = 0; variant < 3; ++variant) {
+      // 0: k_gemm (register staging, WDR_GEMM1=1); 1: k_gemm2 / k_gemm (WDR_GEMM3=0);
+      // 2: the production choice (k_gemm3, 256 x 256 tiles, where the shape allows)
+      unsetenv("WDR_GEMM1");
+      unsetenv("WDR_GEMM3");
       if (variant == 0) setenv("WDR_GEMM1", "1", 1);
-      else unsetenv("WDR_GEMM1");
+      if (variant == 1) setenv("WDR_GEMM3", "0", 1);
       // EPI_F32 into a zeroed buffer for the cross-check (the timed runs use the real epilogue)
       const size_t on = (size_t)M * sh.N;
       if (sh.N <= 5120) {
         CK(hipMemsetAsync(out, 0, on * 4, s));
         ProjArgs c{A, sh.K, W, sh.K, bias, out, sh.N, nullptr, 0, M, sh.N, sh.K, EPI_F32};
         launch_proj(c, s);
-        std::vector<float>& r = variant == 0 ? r1 : r2;
-        r.resize(on);
-        CK(hipMemcpyAsync(r.data(), out, on * 4, hipMemcpyDeviceToHost, s));
+        std::vector<float>& rr = variant == 0 ? ref : r;
+        rr.resize(on);
+        CK(hipMemcpyAsync(rr.data(), out, on * 4, hipMemcpyDeviceToHost, s));
         CK(hipStreamSynchronize(s));
+        if (variant > 0) {
+          size_t nd = 0;
+          double md = 0, mr = 0;
+          for (size_t i = 0; i < ref.size(); ++i) {
+            const double dd = std::fabs((double)ref[i] - r[i]);
+            if (dd > 0) ++nd;
+            md = std::max(md, dd);
+            mr = std::max(mr, std::fabs((double)ref[i]));
+          }
+          printf("   %s vs k_gemm: %zu of %zu differ, max |diff| %.3g (max |ref| %.3g)\n", vname[variant], nd, ref.size(),
+                 md, mr);
+        }
       }
       ProjArgs p{A, sh.K, W, sh.K, bias, out, sh.N, nullptr, 0, M, sh.N, sh.K, sh.epi};
       for (int i = 0; i < 3; ++i) launch_proj(p, s);
@@ -83,20 +100,7 @@ int main(int argc, char** argv) {
       float ms = 0;
       CK(hipEventElapsedTime(&ms, a, b));
       const double us = ms * 1e3 / reps, tf = 2.0 * M * sh.N * sh.K / (us * 1e-6) / 1e12;
-      printf("%-20s %s M=%d N=%5d K=%4d  %9.1f us  %7.1f TFLOP/s\n", sh.name, variant == 0 ? "gemm " : "prod ", M, sh.N,
-             sh.K, us, tf);
-    }
-    if (sh.N <= 5120) {
-      for (const std::vector<float>* rx : {&r2}) {
-        size_t nd = 0;
-        double md = 0;
-        for (size_t i = 0; i < r1.size(); ++i) {
-          const double dd = std::fabs((double)r1[i] - (*rx)[i]);
-          if (dd > 0) ++nd;
-          if (dd > md) md = dd;
-        }
-        printf("   cross-check vs k_gemm: %zu of %zu differ, max |diff| %.3g\n", nd, r1.size(), md);
-      }
+      printf("%-20s %s M=%d N=%5d K=%4d  %9.1f us  %7.1f TFLOP/s\n", sh.name, vname[variant], M, sh.N, sh.K, us, tf);
     }
   }
   {

@@ -248,6 +248,105 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(ProjArgs a) {
 }
 
 
+// ---------------------------------------------------------------- MFMA GEMM, 256 x 256 tile
+// The big encoder GEMMs (M = windows x 1500 > 2048, N % 256 == 0): 256 x 256 block tile, BK 64,
+// 8 waves (2 along M x 4 along N) of 128 x 64 outputs, v_mfma_f32_16x16x32_f16 (8 x 4
+// accumulator tiles per wave: 128 acc registers), one workgroup per CU.  Operand tiles are
+// staged by global_load_lds into two LDS buffers (2 x (32 + 32) KB = 128 KB, one dynamic LDS
+// array); lane-linear images (8 rows x 128 B per wave-instruction) with the g2_swz XOR applied to
+// the global source address, so the 16-row fragment reads (ds_read_b128) are conflict-free.
+// The loads of tile k+1 are issued before tile k's MFMAs and retired once per K-tile by a
+// counted wait + a raw s_barrier (no __syncthreads fence that would drain them early).
+// Twice the output per staged byte of k_gemm2 (128 x 128) and 4x the MFMAs per barrier.
+constexpr int G3_M = 256, G3_N = 256, G3_BK = 64;
+constexpr uint32_t G3_LDS = 2u * 2u * G3_M * G3_BK * 2u;   // bytes
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm3(ProjArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
+  extern __shared__ __attribute__((aligned(16))) f16 lds3[];   // [buf][A, B][256 x 64]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+  const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int ntn = a.N / G3_N;
+  const int bm = id / ntn, bn = id % ntn;
+  const int wm = wid >> 2, wn = wid & 3;
+  // DMA blocks of this wave: block j = wid * 4 + jj holds rows 8 j .. 8 j + 7 of each operand
+  const f16* ga[4];
+  const f16* gb[4];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    const int row = (wid * 4 + jj) * 8 + (lane >> 3);
+    const int c = g2_swz(row, lane & 7);
+    int gm = bm * G3_M + row;
+    gm = gm < a.M ? gm : a.M - 1;
+    ga[jj] = a.A + (size_t)gm * a.lda + c * 8;
+    gb[jj] = a.B + (size_t)(bn * G3_N + row) * a.ldb + c * 8;
+  }
+  constexpr int OP = G3_M * G3_BK;   // halfs per operand image
+  auto stage = [&](int buf, int k0) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      __builtin_amdgcn_global_load_lds((const void*)(ga[jj] + k0), (void*)(lds3 + (buf * 2 + 0) * OP + (wid * 4 + jj) * 512),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(gb[jj] + k0), (void*)(lds3 + (buf * 2 + 1) * OP + (wid * 4 + jj) * 512),
+                                       16, 0, 0);
+    }
+  };
+  const int nk = a.K / G3_BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * G3_BK);
+    const f16* As = lds3 + (cur * 2 + 0) * OP;
+    const f16* Bs = lds3 + (cur * 2 + 1) * OP;
+#pragma unroll
+    for (int ks = 0; ks < G3_BK / 32; ++ks) {
+      const int c = ks * 4 + fq;   // logical 16-B chunk: k = 8 fq .. 8 fq + 7 of this 32-deep step
+      f16x8 bf[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = wn * 64 + j * 16 + fr;
+        bf[j] = *(const f16x8*)(Bs + r * G3_BK + g2_swz(r, c) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = wm * 128 + i * 16 + fr;
+        const f16x8 af = *(const f16x8*)(As + r * G3_BK + g2_swz(r, c) * 8);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    // own loads of tile k+1 landed and own reads of tile k retired; the barrier then publishes
+    // every wave's loads and frees buffer `cur` for the next stage
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = bm * G3_M + wm * 128 + i * 16 + fq * 4 + r;
+        const int col = bn * G3_N + wn * 64 + j * 16 + fr;
+        epi_store<EPI>(a, row, col, acc[i][j][r]);
+      }
+}
+
+
 // ---------------------------------------------------------------- GEMV (M <= 8)
 // Grid-stride over output rows (one weight row per wave per iteration), 16-B weight loads,
 // v_dot2_f32_f16.  With the fused LayerNorm prologue (LN, K <= 1536) every wave normalises
@@ -1050,6 +1149,11 @@ static bool gemm1_forced() {
   const char* e = getenv("WDR_GEMM1");
   return e && atoi(e) != 0;
 }
+// WDR_GEMM3=0: keep the big encoder GEMMs on k_gemm2 / k_gemm (A/B runs); read per call
+static bool gemm3_enabled() {
+  const char* e = getenv("WDR_GEMM3");
+  return !(e && atoi(e) == 0) && !gemm1_forced();
+}
 
 template <int EPI>
 static void launch_epi(const ProjArgs& a, hipStream_t s) {
@@ -1215,6 +1319,18 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
     else if (mt == 3) { WDR_SK(3) }
     else { WDR_SK(4) }
 #undef WDR_SK
+  } else if ((a.N >= 5120 || a.M >= 9000) && a.M > 2048 && a.N % G3_N == 0 && a.K % G3_BK == 0 && gemm3_enabled()) {
+    // 256 x 256 tiles where they measured faster (tools/gemm_bench, large-v3 shapes): M = 6000
+    // fc1 574 vs 509 TFLOP/s, cross-K/V 743 vs 641; at M = 12000 every encoder shape (qkv 667 vs
+    // 520, o 387 vs 335, fc1 550 vs 527, fc2 746 vs 620).  Below that the 120..360 tiles of the
+    // N <= 3840 shapes leave CUs idle and k_gemm2's 128 x 128 tiles win.
+    static bool attr = [] {
+      WDR_HIP(hipFuncSetAttribute((const void*)k_gemm3<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G3_LDS));
+      return true;
+    }();
+    (void)attr;
+    dim3 grid((a.N / G3_N) * cdiv(a.M, G3_M));
+    wdr_launch(PROF_GEMM, bytes, flops, k_gemm3<EPI>, grid, dim3(512), G3_LDS, s, a);
   } else if (a.K % G2_BK == 0 && a.N <= 4096 && !gemm1_forced()) {
     // LDS-DMA GEMM where it measured faster (tools/gemm_bench, M = 6000: qkv -5 %, o -11 %,
     // fc2 -23 %; fc1 and the 82k-column cross-K/V GEMM stay on k_gemm, +8 % / +7 % there)
