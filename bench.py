@@ -17,6 +17,14 @@ detection, prompt prefill, greedy decode, heuristic timestamps, DTW re-forward +
 CAM++ speaker embeddings + speaker assignment, reference glue).  Inputs (PCM) are
 host-resident as in the reference API; the PCIe share is negligible (115 MB/h) and included.
 
+N > 1 (wdr/distributed.py): ONE file of N x --seconds of audio (4 h at N = 4:
+configs[3]) is transcribed across the N GPUs, one process each over RCCL: pyannote windows
+sharded (PCM scattered, frame classes gathered to rank 0), speech segments in N contiguous
+blocks (PCM scattered), each rank decodes its block speculatively with its decode chains, the
+parallel prompt fix-up rounds (prompts all-gathered) make the text equal to one GPU's, raw
+results + speaker embeddings are gathered and merged in file order on rank 0 (overlap clip,
+speakers).  Weak scaling: every GPU holds ~--seconds of the file.
+
 Run:  python bench.py [--gpus N --steps K --warmup W]   (N>1 via torch.distributed.run)
 """
 from __future__ import annotations
@@ -189,10 +197,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # WDR_BENCH_BACKEND=gloo + WDR_BENCH_SHARE_GPU=1 rehearse N ranks on a 1-GPU box
+        backend = os.environ.get("WDR_BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        if os.environ.get("WDR_BENCH_SHARE_GPU") == "1":
+            local = 0
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
+    vad_t = [0.0, 0]
 
     def barrier():
         if world > 1:
@@ -201,11 +213,6 @@ def main():
             torch.cuda.synchronize()
 
     diarize = args.seg == "diarize"
-    pcm, spurts = synth_speech(args.seconds, seed=rank, n_speakers=3 if diarize else 1)
-    segs = [wdr.SpeechSegment(a, b, pcm[int(round(a * 16000)):int(round(b * 16000))]) for a, b, _ in spurts]
-    audio_s = float(sum(s.samples.size for s in segs)) / 16000.0   # speech seconds handed to the pipeline
-    shard_s = pcm.size / 16000.0                                  # wall-clock audio covered (xRT basis)
-
     syn = wdr.Synthetic(weight_std=0.02, emb_std=0.02, force_len_rate=3.3, disable_fallback=True)
     t_load = time.perf_counter()
     ctx = wdr.WhisperContext(args.model, gpu_device=local, enable_dtw=True, synthetic=syn)
@@ -221,18 +228,57 @@ def main():
     prof = [c for c in args.prof.split(",") if c in CLS]
     prof_mask = sum(1 << CLS[c] for c in prof)
 
-    def step():
-        # the segmentation stage over the whole shard runs and is timed; in synthetic mode the
-        # segment list handed downstream is the generator's ground-truth spurt table
-        # (BASELINE.md §2 pin)
-        t = time.perf_counter()
-        if diarize:
-            n_seg = len(dia.get_segments(pcm))
-        else:
-            n_seg = len(vad.get_segments(pcm, materialize=False)[1])
-        vad_t[0] += time.perf_counter() - t
-        vad_t[1] = n_seg
-        return ctx.run_pipeline(segs, opts, diarize_options=dopts)
+    if world > 1:
+        # ONE file of world x seconds: rank r synthesises hour r (seed r) in parallel, rank 0
+        # assembles the file (not timed); the timed step transcribes it across all ranks
+        from wdr import distributed as D
+        pcm_r, spurts_r = synth_speech(args.seconds, seed=rank, n_speakers=3 if diarize else 1)
+        parts = [None] * world if rank == 0 else None
+        dist.gather_object((pcm_r, [(a + rank * args.seconds, b + rank * args.seconds) for a, b, _ in spurts_r]),
+                           parts, dst=0)
+        del pcm_r
+        pcm, spurts = None, []
+        if rank == 0:
+            pcm = np.concatenate([p[0] for p in parts])
+            spurts = [sp for p in parts for sp in p[1]]
+        del parts
+        meta = [len(spurts), 0 if pcm is None else pcm.size, sum(b - a for a, b in spurts)]
+        obj = [meta]
+        dist.broadcast_object_list(obj, src=0)
+        segs_n, n_total, speech_total = obj[0]
+        shard_s = n_total / 16000.0 / world      # audio per GPU (the weak-scaling unit)
+        audio_s = speech_total / world
+
+        def pinned(*_):   # synthetic pin: the generator's talk spurts downstream
+            return [wdr.SpeechSegment(a, b, pcm[int(round(a * 16000)):int(round(b * 16000))]) for a, b in spurts]
+
+        def step():
+            t = time.perf_counter()
+            res = D.transcribe_file(pcm, opts, ctx=ctx, segmentation="diarize" if diarize else "vad",
+                                    diarizer=dia, vad=vad, speech_segments_fn=pinned)
+            vad_t[0] += time.perf_counter() - t
+            vad_t[1] = segs_n
+            return res if res is not None else ([], None)
+        segs = None
+    else:
+        pcm, spurts = synth_speech(args.seconds, seed=rank, n_speakers=3 if diarize else 1)
+        segs = [wdr.SpeechSegment(a, b, pcm[int(round(a * 16000)):int(round(b * 16000))]) for a, b, _ in spurts]
+        audio_s = float(sum(s.samples.size for s in segs)) / 16000.0   # speech seconds handed to the pipeline
+        shard_s = pcm.size / 16000.0                                  # wall-clock audio covered (xRT basis)
+        segs_n = len(segs)
+
+        def step():
+            # the segmentation stage over the whole shard runs and is timed; in synthetic mode the
+            # segment list handed downstream is the generator's ground-truth spurt table
+            # (BASELINE.md §2 pin)
+            t = time.perf_counter()
+            if diarize:
+                n_seg = len(dia.get_segments(pcm))
+            else:
+                n_seg = len(vad.get_segments(pcm, materialize=False)[1])
+            vad_t[0] += time.perf_counter() - t
+            vad_t[1] = n_seg
+            return ctx.run_pipeline(segs, opts, diarize_options=dopts)
 
     vad_t = [0.0, 0]
     for _ in range(args.warmup):
@@ -322,16 +368,19 @@ def main():
                                     "ground-truth spurt segments downstream (synthetic pin)" if diarize else
                                     "configs[2]: %s + DTW, Silero VAD run + timed, %.0f s synthetic audio per rank "
                                     "(%d segments, %.0f s speech), greedy, lang auto, ground-truth spurt segments "
-                                    "downstream (synthetic pin)") % (args.model, shard_s, len(segs), audio_s),
-                       "model": args.model, "global_batch": len(segs) * world, "seq_len": 1500,
-                       "parallelism": "dp%d (segment shards per rank)" % world},
+                                    "downstream (synthetic pin)") % (args.model, shard_s, segs_n // world, audio_s),
+                       "model": args.model, "global_batch": segs_n if world > 1 else segs_n * world, "seq_len": 1500,
+                       "parallelism": ("one file of %d x %.0f s over %d GPUs: pyannote windows + speech-segment blocks "
+                                       "sharded, parallel prompt fix-up rounds, results gathered (wdr/distributed.py)"
+                                       % (world, shard_s, world)) if world > 1 else "1 GPU"},
             "roofline": roof, "roofline_classes": classes, "pipeline_roofline": pipe, "cpu_baseline": cpu,
             "stages_s": {k: round(v, 3) for k, v in times.items() if isinstance(v, float)},
             "counts": {k: v for k, v in times.items() if isinstance(v, int)},
             "segmentation": ({"stage": "pyannote", "s_per_step": round(vad_t[0] / args.steps, 4), "segments": vad_t[1],
-                              "windows": pcm.size // 160000 + 1, "gpu_ms": round(dia.stats()[0], 2)} if diarize else
+                              "windows": n_total // 160000 + 1 if world > 1 else pcm.size // 160000 + 1, "gpu_ms": round(dia.stats()[0], 2)} if diarize else
                              {"stage": "silero", "s_per_step": round(vad_t[0] / args.steps, 4), "segments": vad_t[1],
-                              "chunks": (pcm.size + 511) // 512, "us_per_chunk": round(vad.last_us_per_step, 3)}),
+                              "chunks": ((n_total if world > 1 else pcm.size) + 511) // 512,
+                              "us_per_chunk": round(vad.last_us_per_step, 3)}),
             "load_s": round(t_load, 2), "segments_out": n_out // max(1, args.steps),
         }
         print(json.dumps(line), flush=True)

@@ -271,6 +271,14 @@ int wdr_run_pipeline(wdr_context* c, const wdr_speech_segment* segs, size_t n_se
  * applies both over the merged, ordered blocks of every GPU */
 int wdr_run_pipeline_raw(wdr_context* c, const wdr_speech_segment* segs, size_t n_segs,
                          const wdr_transcribe_options* opts, const wdr_synthetic* syn, wdr_segment_list** out);
+/* run_pipeline_raw continuing decoder 0's random-number stream (the multi-GPU one-file path,
+ * wdr/distributed.py: a GPU's block of the file starts from the RNG state the blocks before it
+ * left, as the reference's one state would, src/transcribe.rs:335): rng_in (NULL = the fresh
+ * state's) and rng_out (malloc'd; free with wdr_free) are decoder 0's std::mt19937 state as
+ * text; sampled_out[n_segs] = 1 where a segment drew random numbers (t > 0 decoders) */
+int wdr_run_pipeline_block(wdr_context* c, const wdr_speech_segment* segs, size_t n_segs,
+                           const wdr_transcribe_options* opts, const wdr_synthetic* syn, const char* rng_in,
+                           int8_t* sampled_out, char** rng_out, wdr_segment_list** out);
 void wdr_segment_list_free(wdr_segment_list* l);
 /* decode chains of run_pipeline (greedy decoding): n States decode n contiguous blocks of the
  * speech segments concurrently, their greedy steps batched into one n-row step, with an exact

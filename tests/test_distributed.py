@@ -180,7 +180,7 @@ def _chain_worker(rank, world, port, out_path):
         def counted(ss, p):
             calls.append(len(ss))
             return _fake_block(ss, p)
-        groups, _ = D.transcribe_block(counted, segs[a:b], None, rank, world)
+        groups, _ = D.transcribe_block(counted, segs[a:b], None, rank, world, seg0=a)
         gathered = [None] * world if rank == 0 else None
         torch.distributed.gather_object(([g[0].text for g in groups], calls), gathered, dst=0)
         if rank == 0:
@@ -200,6 +200,57 @@ def test_prompt_fixup_stops_at_convergence(tmp_path):
     # ranks 1..3 re-decode only until the prompt converges (a few single-segment calls)
     for calls in [g[1] for g in got][1:]:
         assert calls[0] == 10 and all(c == 1 for c in calls[1:]) and len(calls) - 1 <= 4, calls
+
+
+def _fake_block_rng(segs, prompt, rng):
+    """Like _fake_block, and every 7th segment "draws": its text depends on the RNG counter (a
+    string, as the mt19937 state is), which each draw advances.  rng None = the fresh state."""
+    groups, sampled = [], []
+    e = prompt
+    r = int(rng) if rng is not None else 0
+    for s in segs:
+        sid = int(s.samples[0])
+        if sid % 7 == 3:
+            r += 1 + len(e or "") % 3
+            text = "r%d|%d" % (r, sid)
+            sampled.append(True)
+        else:
+            text = ("p%s|%d" % ((e or "-")[:3], sid)) if sid % 3 == 0 else ("" if sid % 5 == 0 else "s%d" % sid)
+            sampled.append(False)
+        g = [wdr.Segment(s.start, s.end, text)]
+        groups.append(g)
+        e = D.next_prompt(e, g)
+    return groups, "en", sampled, str(r)
+
+
+def _rng_worker(rank, world, port, out_path, n):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        segs = [wdr.SpeechSegment(float(i), i + 0.5, np.full(10, i, np.int16)) for i in range(n)]
+        a, b = D.balance([1] * n, world)[rank]
+        groups, _ = D.transcribe_block(_fake_block_rng, segs[a:b], None, rank, world, seg0=a)
+        gathered = [None] * world if rank == 0 else None
+        torch.distributed.gather_object(([g[0].text for g in groups], dict(D.last_stats)), gathered, dst=0)
+        if rank == 0:
+            json.dump(gathered, open(out_path, "w"))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(3, 40), (4, 9), (4, 3)])
+def test_rng_replay_across_ranks(tmp_path, world, n):
+    """Sampled segments (temperature fallback) make every later result depend on decoder 0's
+    RNG stream: the multi-rank decode (parallel prompt rounds, then the in-order replay from the
+    first segment that drew, RNG state handed rank to rank) equals one sequential pass; also
+    with ranks that hold no segments (n < world)."""
+    out = str(tmp_path / "rng.json")
+    torch.multiprocessing.spawn(_rng_worker, args=(world, _port(), out, n), nprocs=world, join=True)
+    got = json.load(open(out))
+    texts = sum([g[0] for g in got], [])
+    segs = [wdr.SpeechSegment(float(i), i + 0.5, np.full(10, i, np.int16)) for i in range(n)]
+    ref = _fake_block_rng(segs, None, None)[0]
+    assert texts == [g[0].text for g in ref]
 
 
 def test_balance_partitions():

@@ -643,9 +643,11 @@ static std::vector<float> seg_f32(const wdr_speech_segment& s) {
 // result depend on every earlier draw (decoder 0's RNG lives in the state): from the first
 // segment that drew, the rest of the file is re-decoded sequentially from that segment's RNG
 // state.  The output equals the single-chain loop's exactly.
+// rng0: decoder 0's RNG entering the first segment (the fresh state's, or the state a previous
+// block of the same file left, multi-GPU one-file path); "clean" below means "equal to rng0".
 static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_speech_segment>& segs,
                                          const wdr_transcribe_options* o, const FullParams& params, int C,
-                                         const wdr_callbacks* cb) {
+                                         const wdr_callbacks* cb, const std::string& rng0) {
   const size_t N = segs.size();
   while ((int)c->chain_st.size() < C - 1)
     c->chain_st.push_back(std::make_unique<State>(*c->ctx, (int)c->chain_st.size() + 1));
@@ -695,13 +697,13 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
     Prompt e = e_in;
     for (size_t j = a; j < b && !stop; ++j) {
       const std::vector<float> x = seg_f32(segs[j]);
-      st.reset_rng();
+      st.set_rng_state(rng0);
       if (st.full(with_prompt(params, e), x.data(), (int)x.size(), -1, false) != 0)
         throw std::runtime_error("failed to transcribe");
       out[j].res = st.result_all;
       out[j].lang_id = st.lang_id;
       out[j].sampled = st.sampled;
-      out[j].rng_clean = true;   // reset_rng() above
+      out[j].rng_clean = true;   // rng0 above
       out[j].rng_after = st.sampled ? st.rng_state() : std::string();
       e = next_prompt(e, out[j].res);
       const bool converged = e == spec_out[j];
@@ -718,7 +720,7 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
     try {
       const size_t a = cut[k], b = cut[k + 1];
       st.times = StageTimes{};
-      st.reset_rng();
+      st.set_rng_state(rng0);
       st.batched = C > 1;
       std::vector<const int16_t*> pcm;
       std::vector<int> ns;
@@ -864,7 +866,7 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
     State& st = *c->st;
     Prompt e = e0;
     for (size_t i = 0; i < rs; ++i) e = next_prompt(e, out[i].res);
-    if (rs == f) st.reset_rng();
+    if (rs == f) st.set_rng_state(rng0);
     else st.set_rng_state(out[f].rng_after);
     for (size_t i = rs; i < N; ++i) {
       if (cb && cb->is_cancelled && cb->is_cancelled(cb->user)) throw std::runtime_error("failed to transcribe");
@@ -875,6 +877,7 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
       out[i].res = st.result_all;
       out[i].lang_id = st.lang_id;
       out[i].sampled = st.sampled;
+      out[i].rng_after = st.sampled ? st.rng_state() : std::string();
       e = next_prompt(e, out[i].res);
     }
   }
@@ -897,10 +900,18 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
 // raw: per-segment results only (no overlap clip against the next segment, no speakers): the
 // multi-GPU path (wdr/distributed.py) merges several GPUs' raw blocks and applies both in order.
 // dopts: DiarizeOptions (src/transcribe.rs:327, 339-345); its presence switches speakers on.
+// RNG carry (multi-GPU one-file path, wdr_run_pipeline_block): rng_in = decoder 0's RNG entering
+// the first segment (null: the fresh state's, src/transcribe.rs:335); rng_out = its state after
+// the last one; sampled[i] = segment i drew random numbers (t > 0 decoders)
+struct RngCarry {
+  const std::string* rng_in = nullptr;
+  std::string rng_out;
+  std::vector<char> sampled;
+};
 static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speech_segment>& segs,
                                      const wdr_transcribe_options* o, const wdr_diarize_options* dopts,
                                      const SynCfg& syn, const wdr_callbacks* cb, std::string* detected_lang,
-                                     bool* has_lang, bool raw = false) {
+                                     bool* has_lang, bool raw = false, RngCarry* carry = nullptr) {
   const bool diarize = dopts != nullptr && !raw;
   const float dthr = dopts ? dopts->threshold : 0.5f;
   SpeakerManager speakers(dopts ? dopts->max_speakers : UINT64_MAX);
@@ -936,8 +947,11 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
   // every segment's PCM goes to the encode-ahead ring up front (int16 -> f32 on the GPU,
   // the same x / 32768 as src/transcribe.rs's conversion); multi-chain: per chain block
   // the reference creates a fresh whisper state per pipeline call (src/transcribe.rs:335):
-  // decoder 0's RNG starts from its initial seed
+  // decoder 0's RNG starts from its initial seed (or from the state carried in)
   c->st->reset_rng();
+  if (carry && carry->rng_in) c->st->set_rng_state(*carry->rng_in);
+  const std::string rng0 = c->st->rng_state();
+  if (carry) carry->sampled.assign(segs.size(), 0);
   if (C == 1) {
     std::vector<const int16_t*> pcm(segs.size());
     std::vector<int> ns(segs.size());
@@ -1040,7 +1054,14 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
   if (C > 1) {
     // multi-chain: C States decode C contiguous blocks concurrently (batched greedy steps),
     // then the exact prompt fix-up; results come back DTW-resolved, finished here in order
-    std::vector<SegOut> res = decode_chains(c, segs, o, params, C, cb);
+    std::vector<SegOut> res = decode_chains(c, segs, o, params, C, cb, rng0);
+    if (carry) {
+      carry->rng_out = rng0;
+      for (size_t i = 0; i < segs.size(); ++i) {
+        carry->sampled[i] = res[i].sampled;
+        if (res[i].sampled) carry->rng_out = res[i].rng_after;
+      }
+    }
     for (size_t i = 0; i < segs.size(); ++i) {
       if (i == 0 && !*has_lang) {
         *detected_lang = kLangs[std::max(0, std::min(99, res[0].lang_id))];
@@ -1066,6 +1087,7 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
       throw std::runtime_error(std::string("failed to transcribe: ") + ex.what());
     }
     if (rc != 0) throw std::runtime_error("failed to transcribe");
+    if (carry) carry->sampled[i] = c->st->sampled;
     if (!*has_lang) {
       *detected_lang = kLangs[std::max(0, std::min(99, c->st->lang_id))];
       *has_lang = true;
@@ -1089,6 +1111,7 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
     finalize(pend[0]);
     pend.clear();
   }
+  if (carry) carry->rng_out = c->st->rng_state();
   return out;
 }
 
@@ -1618,6 +1641,28 @@ int wdr_run_pipeline_raw(wdr_context* c, const wdr_speech_segment* segs, size_t 
     c->st->times.glue = now_s() - t;
     *out = to_list(res, has_lang ? &lang : nullptr);
     if (!(*out)->speech_index && !res.empty()) return fail("raw pipeline: missing speech index");
+    return 0;
+  })
+}
+
+int wdr_run_pipeline_block(wdr_context* c, const wdr_speech_segment* segs, size_t n_segs,
+                           const wdr_transcribe_options* o, const wdr_synthetic* syn, const char* rng_in,
+                           int8_t* sampled_out, char** rng_out, wdr_segment_list** out) {
+  WDR_GUARD({
+    std::vector<wdr_speech_segment> v(segs, segs + n_segs);
+    std::string lang;
+    bool has_lang = false;
+    const double t = now_s();
+    c->st->times = StageTimes{};
+    c->cs = wdr_context::ChainStats{};
+    RngCarry carry;
+    const std::string in = rng_in ? std::string(rng_in) : std::string();
+    if (rng_in) carry.rng_in = &in;
+    std::vector<Seg> res = run_pipeline(c, v, o, nullptr, syn_of(syn), nullptr, &lang, &has_lang, true, &carry);
+    c->st->times.glue = now_s() - t;
+    for (size_t i = 0; i < n_segs; ++i) sampled_out[i] = carry.sampled[i];
+    *rng_out = strdup(carry.rng_out.c_str());
+    *out = to_list(res, has_lang ? &lang : nullptr);
     return 0;
   })
 }

@@ -614,6 +614,28 @@ class WhisperContext:
         segs, lang, index = _segments(out, True)
         return segs, lang, index or []
 
+    def run_pipeline_block(self, speech_segments, options: TranscribeOptions, rng_in: Optional[str] = None,
+                           synthetic: Optional[Synthetic] = None):
+        """run_pipeline_raw continuing decoder 0's RNG stream (wdr_run_pipeline_block):
+        (segments, detected_lang, speech index per segment, sampled flag per speech segment,
+        rng state after the block)."""
+        keep = _Keep()
+        arr = (L.SpeechSegment * max(1, len(speech_segments)))()
+        for i, s in enumerate(speech_segments):
+            smp = keep(np.ascontiguousarray(s.samples, np.int16))
+            arr[i] = L.SpeechSegment(s.start, s.end, smp.ctypes.data_as(C.POINTER(C.c_int16)), smp.size)
+        out = C.POINTER(L.SegmentList)()
+        syn = _syn(synthetic or self.synthetic)
+        sampled = (C.c_int8 * max(1, len(speech_segments)))()
+        rng = C.c_void_p()
+        L.check(self._lib.wdr_run_pipeline_block(self.h, arr, len(speech_segments), _opts(options, keep),
+                                                 C.byref(syn) if syn else None, _s(rng_in), sampled, C.byref(rng),
+                                                 C.byref(out)))
+        rng_out = C.cast(rng, C.c_char_p).value.decode()
+        self._lib.wdr_free(rng)
+        segs, lang, index = _segments(out, True)
+        return segs, lang, index or [], [bool(sampled[i]) for i in range(len(speech_segments))], rng_out
+
     def set_chains(self, n: int):
         """Decode chains for greedy run_pipeline calls (wdr_context_set_chains): n blocks of the
         speech segments decoded concurrently with batched steps, exact prompt fix-up."""

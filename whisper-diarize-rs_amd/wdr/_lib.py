@@ -138,6 +138,8 @@ _SIGS = {
                                        P(P(SegmentList))]),
     "wdr_run_pipeline": (C.c_int, [vp, P(SpeechSegment), sz, P(TranscribeOptions), P(DiarizeOptions), P(Synthetic),
                                    P(Callbacks), P(P(SegmentList))]),
+    "wdr_run_pipeline_block": (C.c_int, [vp, P(SpeechSegment), sz, P(TranscribeOptions), P(Synthetic), cstr, P(i8),
+                                         P(C.c_void_p), P(P(SegmentList))]),
     "wdr_segment_list_free": (None, [P(SegmentList)]),
     "wdr_context_set_chains": (C.c_int, [vp, i32]),
     "wdr_dbg_set_early_fixup": (C.c_int, [vp, i32]),

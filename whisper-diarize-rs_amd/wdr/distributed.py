@@ -15,14 +15,18 @@ The reference transcribes a file on one device (src/engine.rs:65-200).  Here:
    thread computes the block's speaker embeddings (diarize).
 4. Prompt chain, exact.  Segment i's decode depends on the prompt E_i (src/transcribe.rs:384-386,
    502): E_{i+1} = the text of segment i's last result if that is non-empty, else E_i.  Every
-   rank first decodes its block speculatively from the file's initial prompt.  Then, in rank
-   order, rank r receives the true E entering its block from rank r-1 (point-to-point); if it
-   differs from the speculative one, rank r re-decodes its segments one at a time from the true
-   prompt until the prompt entering the next segment equals the speculative run's (from there
-   on the speculative results are the sequential ones), and passes its outgoing E on.  This
-   reproduces the single-GPU result exactly when decoding draws no random numbers (no
-   temperature > 0 sampling / fallback); whisper.cpp's sampling RNG state is per whisper
-   state and would have to be replayed across ranks.
+   rank first decodes its block speculatively from the file's initial prompt.  Then fix-up
+   rounds, all ranks at once: the prompts leaving every block are all-gathered; every rank whose
+   block was decoded from a prompt other than the one leaving its predecessor's block (as that
+   now stands) re-decodes its segments one at a time from it until the prompt entering the next
+   segment equals the previous run's (from there on the previous results are the sequential
+   ones).  A rank that ran through its block changes its successor's true prompt, which the next
+   round handles; rank 0 is always exact, so the rounds end.  Random draws (t > 0 decoders:
+   temperature fallback) make results depend on decoder 0's RNG stream, which in the reference
+   runs through the whole file in one state: from the first segment that drew in any decode,
+   the rest of the file is re-decoded in order, the RNG state and prompt handed from rank to
+   rank (wdr_run_pipeline_block carries the state in and out).  The result equals the
+   single-GPU run exactly.
 5. Raw per-segment results (no overlap clip, no speakers: wdr_run_pipeline_raw) and
    embeddings are gathered to rank 0, which merges them in file order and applies what the
    reference does sequentially: the overlap clip of each segment against its successor
@@ -195,20 +199,34 @@ def next_prompt(e_in: Optional[str], results: Sequence[Segment]) -> Optional[str
 
 
 def _raw_block(ctx, options: TranscribeOptions):
-    """Default block transcriber: wdr_run_pipeline_raw on this rank's GPU, results grouped per
-    speech segment."""
-    def run(segs: List[SpeechSegment], prompt: Optional[str]) -> tuple:
+    """Default block transcriber: wdr_run_pipeline_block on this rank's GPU (decode chains,
+    decoder 0's RNG carried in and out), results grouped per speech segment."""
+    def run(segs: List[SpeechSegment], prompt: Optional[str], rng: Optional[str] = None) -> tuple:
         adv = dataclasses.replace(options.advanced) if options.advanced else None
         if adv is None:
             from . import AdvancedTranscribe
             adv = AdvancedTranscribe()
         adv.init_prompt = prompt
         opts = dataclasses.replace(options, advanced=adv, enable_diarize=None)
-        out, lang, index = ctx.run_pipeline_raw(segs, opts)
+        out, lang, index, sampled, rng_out = ctx.run_pipeline_block(segs, opts, rng)
         groups: List[List[Segment]] = [[] for _ in segs]
         for s, i in zip(out, index):
             groups[i].append(s)
-        return groups, lang
+        return groups, lang, sampled, rng_out
+    return run
+
+
+def _as_block(fn):
+    """block_fn(segs, prompt, rng) -> (groups, lang, sampled flags, rng after); a 2-argument
+    function returning (groups, lang) is taken as one that never draws random numbers."""
+    def run(segs, prompt, rng):
+        try:
+            r = fn(segs, prompt, rng)
+        except TypeError:
+            r = fn(segs, prompt)
+        if len(r) == 2:
+            return r[0], r[1], [False] * len(segs), rng
+        return r
     return run
 
 
@@ -216,41 +234,95 @@ def _raw_block(ctx, options: TranscribeOptions):
 last_stats: dict = {}
 
 
-def transcribe_block(block_fn, segs: List[SpeechSegment], spec_prompt: Optional[str], rank: int, G: int):
-    """Speculative decode of this rank's block, then the rank-ordered prompt fix-up.
-    Returns (groups per speech segment, detected_lang of the block's first segment)."""
+def _prompts(e0, groups):
+    """Prompt entering each segment (and leaving the last): len(groups) + 1 entries."""
+    out = [e0]
+    for g in groups:
+        out.append(next_prompt(out[-1], g))
+    return out
+
+
+def transcribe_block(block_fn, segs: List[SpeechSegment], spec_prompt: Optional[str], rank: int, G: int,
+                     seg0: int = 0):
+    """Speculative decode of this rank's block (its first segment is segment seg0 of the file),
+    the parallel prompt fix-up rounds, then the in-order re-decode from the first segment that
+    drew random numbers.  Returns (groups per speech segment, detected_lang of the block's first
+    segment)."""
     import time
+    dist = _dist()
+    block = _as_block(block_fn)
     t0 = time.perf_counter()
-    groups, lang = block_fn(segs, spec_prompt) if segs else ([], None)
+    groups, lang, sampled, _ = block(segs, spec_prompt, None) if segs else ([], None, [], None)
+    drew = list(sampled)                      # drew in any decode of the segment
     t1 = time.perf_counter()
     last_stats.clear()
-    last_stats.update(segments=len(segs), spec_s=t1 - t0, fixups=0)
-    # prompt entering each segment of the speculative run
-    spec_in = [spec_prompt]
-    for g in groups:
-        spec_in.append(next_prompt(spec_in[-1], g))
-    e_in = spec_prompt
-    if rank > 0:
-        e_in = _recv_prompt(rank - 1)
+    last_stats.update(segments=len(segs), spec_s=t1 - t0, fixups=0, rounds=0, replayed=0)
+    dec_in = spec_prompt                      # the prompt this block's first segment was decoded from
+    while True:
+        states = [None] * G
+        dist.all_gather_object(states, (dec_in, _prompts(dec_in, groups)[-1]))
+        e_true = spec_prompt if rank == 0 else states[rank - 1][1]
+        # a rank with no segments passes its predecessor's prompt on unchanged
+        redo = bool(segs) and e_true != dec_in
+        if not segs:
+            dec_in = e_true
+        flags = [None] * G
+        dist.all_gather_object(flags, (redo, not segs and e_true != states[rank][0]))
+        if not any(f[0] or f[1] for f in flags):
+            break
+        last_stats["rounds"] += 1
+        if redo:
+            spec_in = _prompts(dec_in, groups)
+            e = e_true
+            for j in range(len(segs)):
+                last_stats["fixups"] += 1
+                gj, lj, sj, _ = block([segs[j]], e, None)
+                groups[j] = gj[0]
+                drew[j] = drew[j] or sj[0]
+                if j == 0:
+                    lang = lj
+                e = next_prompt(e, gj[0])
+                if e == spec_in[j + 1]:
+                    break
+            dec_in = e_true
     t2 = time.perf_counter()
-    last_stats.update(wait_s=t2 - t1)
-    if e_in != spec_prompt:
-        e = e_in
-        for j in range(len(segs)):
-            last_stats["fixups"] += 1
-            gj, lj = block_fn([segs[j]], e)
-            groups[j] = gj[0]
-            if j == 0:
-                lang = lj
-            e = next_prompt(e, gj[0])
-            if e == spec_in[j + 1]:
+    last_stats.update(fixup_s=t2 - t1)
+    # random draws: the first segment (file order) that drew in any decode is exact (nothing
+    # before it drew, so it started from the fresh RNG); everything after it is re-decoded in
+    # order with the RNG stream, block by block
+    every = [None] * G
+    dist.all_gather_object(every, (seg0, drew))
+    first = None
+    for s0, d in sorted(every, key=lambda x: x[0]):
+        for k, x in enumerate(d):
+            if x:
+                first = s0 + k
                 break
-    last_stats.update(fixup_s=time.perf_counter() - t2)
-    e_out = e_in
-    for g in groups:
-        e_out = next_prompt(e_out, g)
-    if rank < G - 1:
-        _send_prompt(e_out, rank + 1)
+        if first is not None:
+            break
+    if first is not None:
+        owner = next(r for r in range(G) if every[r][0] <= first < every[r][0] + len(every[r][1]))
+        if rank == owner:
+            k = first - seg0
+            e = _prompts(dec_in, groups)[k]
+            gk, lk, _, rng = block(segs[k:], e, None)
+            groups[k:] = gk
+            if k == 0:
+                lang = lk
+            last_stats["replayed"] += len(segs) - k
+        elif rank > owner and segs:
+            e = _recv_prompt(rank - 1)
+            rng = _recv_prompt(rank - 1)
+            groups, lang, _, rng = block(segs, e, rng)
+            last_stats["replayed"] += len(segs)
+        elif rank > owner:
+            e = _recv_prompt(rank - 1)
+            rng = _recv_prompt(rank - 1)
+        if rank >= owner and rank < G - 1:
+            e_out = _prompts(e, groups[k:] if rank == owner else groups)[-1]
+            _send_prompt(e_out, rank + 1)
+            _send_prompt(rng, rank + 1)
+    last_stats.update(replay_s=time.perf_counter() - t2)
     return groups, lang
 
 
@@ -298,8 +370,6 @@ def transcribe_file(pcm: Optional[np.ndarray], options: TranscribeOptions, *, ct
         block_fn = _raw_block(ctx, options)
     if classes_fn is None and segmentation == "diarize":
         classes_fn = diarizer.frame_classes
-    if embed_fn is None and segmentation == "diarize":
-        embed_fn = diarizer.embedding
     n = int(_bcast_i64([int(pcm.size)] if rank == 0 else None, 1)[0])
 
     # ---- segmentation -> speech segments on rank 0
@@ -347,13 +417,18 @@ def transcribe_file(pcm: Optional[np.ndarray], options: TranscribeOptions, *, ct
     th = None
     if segmentation == "diarize":
         def work():
+            batch = diarizer.embedding_batch if embed_fn is None else None
+            if batch is not None:   # one batched CAM++ forward per 64 utterances
+                for j in range(0, len(my_segs), 64):
+                    embs[j:j + 64] = batch([s.samples for s in my_segs[j:j + 64]])
+                return
             for j, s in enumerate(my_segs):
                 embs[j] = embed_fn(s.samples)
         th = threading.Thread(target=work)
         th.start()
     spec = options.advanced.init_prompt if options.advanced else None
     try:
-        groups, lang = transcribe_block(block_fn, my_segs, spec, rank, G)
+        groups, lang = transcribe_block(block_fn, my_segs, spec, rank, G, seg0=a)
     finally:
         if th is not None:
             th.join()
