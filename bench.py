@@ -56,6 +56,8 @@ def parse():
                          "'none'): the roofline figure is the one with the largest share of kernel time")
     ap.add_argument("--seg", default="diarize", choices=["diarize", "vad"],
                     help="segmentation stage: pyannote diarization (default) or Silero VAD")
+    ap.add_argument("--strategy", default="greedy", choices=["greedy", "beam"],
+                    help="greedy (configs[2]) or the reference's default beam search, 5 beams")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-audio", type=float, default=60.0,
                     help="audio seconds of the workload the CPU baseline is extrapolated over (rank 0, N=1)")
@@ -219,7 +221,8 @@ def main():
     t_load = time.perf_counter() - t_load
     opts = wdr.TranscribeOptions(model=args.model, lang="auto", enable_vad=not diarize,
                                  enable_diarize=True if diarize else None,
-                                 advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+                                 advanced=wdr.AdvancedTranscribe(
+                                     sampling_strategy="greedy" if args.strategy == "greedy" else None))
     dopts = wdr.DiarizeOptions.from_options(opts) if diarize else None   # src/engine.rs:101-111
     vad = None if diarize else wdr.Vad(gpu_device=local)
     dia = wdr.Diarizer(gpu_device=local) if diarize else None
@@ -362,12 +365,13 @@ def main():
             "value": round(value, 3), "unit": "audio-sec/wall-sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt_max * 1e3 / args.steps, 1), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f16 (f32 accumulate)", "data": "synthetic",
-            "config": {"workload": ("configs[3] per-GPU shard with configs[2]'s greedy decode: %s + DTW + diarize "
+            "config": {"strategy": "greedy" if args.strategy == "greedy" else "beam search, 5 beams (reference default)",
+                       "workload": ("configs[3] per-GPU shard with configs[2]'s greedy decode: %s + DTW + diarize "
                                     "(pyannote segmentation-3.0 run + timed, CAM++ embeddings + speaker assignment), "
                                     "%.0f s synthetic audio per rank (%d segments, %.0f s speech, 3 speakers), lang auto, "
                                     "ground-truth spurt segments downstream (synthetic pin)" if diarize else
                                     "configs[2]: %s + DTW, Silero VAD run + timed, %.0f s synthetic audio per rank "
-                                    "(%d segments, %.0f s speech), greedy, lang auto, ground-truth spurt segments "
+                                    "(%d segments, %.0f s speech), lang auto, ground-truth spurt segments "
                                     "downstream (synthetic pin)") % (args.model, shard_s, segs_n // world, audio_s),
                        "model": args.model, "global_batch": segs_n if world > 1 else segs_n * world, "seq_len": 1500,
                        "parallelism": ("one file of %d x %.0f s over %d GPUs: pyannote windows + speech-segment blocks "

@@ -349,6 +349,9 @@ int wdr_dbg_proj(const uint16_t* a_f16, const uint16_t* w_f16, const float* bias
 #define WDR_DBG_PROJ_STEP 0x100
 int wdr_dbg_attn(const uint16_t* q, const uint16_t* k, const uint16_t* v, int32_t Tq, int32_t Tk, int32_t n_head,
                  int32_t causal, float* out /* [Tq][n_head*64] */);
+// decode-step cross-attention over 1500 keys (beam groups / per-row slots; see engine.cpp)
+int wdr_dbg_xattn(const uint16_t* q, const uint16_t* kv, const int32_t* row_slot, const int32_t* grp, int32_t R,
+                  int32_t S, int32_t H, int32_t iters, float* out);
 
 #ifdef __cplusplus
 }

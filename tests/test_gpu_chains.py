@@ -105,3 +105,26 @@ def test_forced_early_fixup_is_exact(fallback):
     assert ctx.stage_times()["early_fixup_segments"] == 0
     assert got0 == ref
     ctx.close()
+
+
+@pytest.mark.parametrize("name,seconds,chains", [("tiny-test", 80.0, 4), ("large-v3", 60.0, 8)])
+def test_beam_chains_equal_single_chain(name, seconds, chains, monkeypatch):
+    """The reference's default strategy (beam search, 5 beams: src/transcribe.rs:22-33) with
+    decode chains: every chain's live beams join one batched step (rows grouped by segment, the
+    segment's cross-K/V read once for its beams, top-5 candidates per row, steps above 16 rows
+    as 16-row launches).  The result must equal the one-chain beam search exactly."""
+    monkeypatch.setenv("WDR_DECODE_CHAINS", "16")
+    syn = wdr.Synthetic(weight_std=0.02, emb_std=0.5, force_len_rate=3.3, disable_fallback=True)
+    ctx = wdr.WhisperContext(name, synthetic=syn)
+    pcm, spurts = synth_speech(seconds, seed=3, n_speakers=2)
+    segs = _segs(pcm, spurts)
+    assert len(segs) >= chains
+    opts = wdr.TranscribeOptions(lang="auto")   # sampling_strategy unset: beam search, 5 beams
+    ref, lang1 = _run(ctx, segs, opts, 1)
+    got, lang = _run(ctx, segs, opts, chains)
+    st = ctx.stage_times()
+    assert st["chains"] == chains
+    assert st["batch_rows"] > st["batch_launches"] * 2   # beams batched across chains
+    assert lang == lang1
+    assert got == ref
+    ctx.close()

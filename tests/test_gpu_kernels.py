@@ -117,6 +117,73 @@ def test_flash_attention_matches_fp32_reference(lib, Tq, Tk, H, causal):
     assert np.abs(out - ref).mean() < 1.5e-3
 
 
+def _xattn(lib, q, kv, H, row_slot=None, grp=None, iters=1):
+    R = q.shape[0]
+    out = np.zeros((R, H * 64), np.float32)
+    rs = None if row_slot is None else np.ascontiguousarray(row_slot, np.int32)
+    g = None if grp is None else np.ascontiguousarray(grp, np.int32)
+    _lib.check(lib.wdr_dbg_xattn(_f16bits(q).ctypes.data_as(U16), _f16bits(kv).ctypes.data_as(U16),
+                                 None if rs is None else rs.ctypes.data_as(I32),
+                                 None if g is None else g.ctypes.data_as(I32), R, kv.shape[0], H, iters,
+                                 out.ctypes.data_as(F32)))
+    return out
+
+
+def test_decode_cross_attention(lib):
+    """k_xattn_dec (one wave per key split, online softmax, splits merged in-launch by the last
+    arriving wave): per-row slots (batched greedy step), beam groups sharing a slot, the shared
+    form, and repeated launches on the same arrival counters.  Every row must equal the fp64
+    attention within the f16 P / output rounding, and a row's result must not depend on the
+    group it is computed in (batch composition varies with timing)."""
+    rng = np.random.default_rng(11)
+    H, S, R = 3, 6, 24
+    q = (rng.standard_normal((R, H * 64)) * 1.5).astype(np.float16).astype(np.float32)
+    kv = rng.standard_normal((S, 1500, 2 * H * 64)).astype(np.float16).astype(np.float32)
+    slot = rng.integers(0, S, R)
+    ref = np.concatenate([_attn_ref(q[r:r + 1], kv[slot[r], :, :H * 64], kv[slot[r], :, H * 64:], H, 0)
+                          for r in range(R)])
+    rows = _xattn(lib, q, kv, H, slot)
+    np.testing.assert_allclose(rows, ref, rtol=0, atol=1e-2)
+    assert np.abs(rows - ref).mean() < 1.5e-3
+    # groups: rows of a group share the leader's slot
+    sizes = [5, 1, 3, 8, 2, 5]
+    grp, gslot = np.zeros(R, np.int32), np.zeros(R, np.int64)
+    r0 = 0
+    for i, n in enumerate(sizes):
+        grp[r0] = n
+        gslot[r0:r0 + n] = i % S
+        r0 += n
+    assert r0 == R
+    gref = np.concatenate([_attn_ref(q[r:r + 1], kv[gslot[r], :, :H * 64], kv[gslot[r], :, H * 64:], H, 0)
+                           for r in range(R)])
+    grouped = _xattn(lib, q, kv, H, gslot, grp)
+    np.testing.assert_allclose(grouped, gref, rtol=0, atol=1e-2)
+    single = _xattn(lib, q, kv, H, gslot)   # same rows, every row its own group
+    np.testing.assert_array_equal(grouped, single)
+    np.testing.assert_array_equal(_xattn(lib, q, kv, H, gslot, grp, iters=3), grouped)
+    # shared K/V (one segment's beams on a State's own step), R <= 8
+    shared = _xattn(lib, q[:5], kv[:1], H)
+    np.testing.assert_array_equal(shared, _xattn(lib, q[:5], kv[:1], H, np.zeros(5), [5, 0, 0, 0, 0]))
+    np.testing.assert_allclose(shared, _attn_ref(q[:5], kv[0, :, :H * 64], kv[0, :, H * 64:], H, 0), rtol=0,
+                               atol=1e-2)
+
+
+@pytest.mark.parametrize("N,K,epi", [(1280, 5120, 2), (3840, 1280, 0)])
+def test_step_projection_wide_batches(lib, N, K, epi):
+    """Batched steps of more than 16 rows (beams of many segments) run as 16-row launches: every
+    row equals its one-row result bit for bit."""
+    rng = np.random.default_rng(N + K)
+    a = rng.standard_normal((80, K)).astype(np.float16).astype(np.float32)
+    w = (rng.standard_normal((N, K)) * 0.03).astype(np.float16).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32) * 0.1
+    base = rng.standard_normal((80, N)).astype(np.float32)
+    one = np.concatenate([_proj(lib, a[i:i + 1], w, bias, epi | STEP, base[i:i + 1] if epi == 2 else None)
+                          for i in range(0, 80, 7)])
+    for M in (17, 40, 80):
+        got = _proj(lib, a[:M], w, bias, epi | STEP, base[:M] if epi == 2 else None)
+        np.testing.assert_array_equal(got[0:M:7], one[:len(range(0, M, 7))], err_msg="M=%d" % M)
+
+
 def test_signal_energy_is_bit_exact(lib):
     rng = np.random.default_rng(0)
     for n in (1, 64, 65, 1000, 160000):

@@ -939,9 +939,9 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
     *has_lang = true;
   }
   const bool translated = o && o->whisper_to_english == 1;
-  // decode chains: greedy decoding only (its steps batch across chains; beam search and
-  // t > 0 decoders keep one chain)
-  const int C = (params.greedy && params.temperature <= 0.f)
+  // decode chains: greedy and beam search at t = 0 (their steps batch across chains; t > 0
+  // decoders from the first window on keep one chain)
+  const int C = (params.temperature <= 0.f)
                     ? std::max(1, std::min({c->chains, c->ctx->max_chains, (int)segs.size()}))
                     : 1;
   // every segment's PCM goes to the encode-ahead ring up front (int16 -> f32 on the GPU,
@@ -1916,6 +1916,52 @@ int wdr_dbg_attn(const uint16_t* q, const uint16_t* k, const uint16_t* v, int32_
     }
     launch_flash_attn(fa, 1, nullptr);
     std::vector<f16> h((size_t)Tq * d);
+    WDR_HIP(hipMemcpy(h.data(), dout.p, h.size() * 2, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < h.size(); ++i) out[i] = (float)h[i];
+    return 0;
+  })
+}
+
+// decode-step cross-attention (kernels/attn.hip k_xattn_dec) over 1500 keys: q [R][H*64],
+// kv [S][1500][2 * H * 64] (K then V per key), row_slot [R] (null: every row on slot 0 through
+// the shared-K/V form, R <= 8), grp [R] group sizes (XAttnArgs::grp, or null); run `iters`
+// times on the same arrival counters; out [R][H * 64]
+int wdr_dbg_xattn(const uint16_t* q, const uint16_t* kv, const int32_t* row_slot, const int32_t* grp, int32_t R,
+                  int32_t S, int32_t H, int32_t iters, float* out) {
+  WDR_GUARD({
+    WDR_CHECK(R >= 1 && R <= 128 && S >= 1 && H >= 1 && H <= 32 && iters >= 1, "dbg xattn: bad shape");
+    const int d = H * 64, T = 1500;
+    DevMem dq((size_t)R * d * 2), dkv((size_t)S * T * 2 * d * 2), dout((size_t)R * d * 2);
+    DevMem po((size_t)24 * R * H * 64 * 4), pml((size_t)24 * R * H * 8), ctr((size_t)XATTN_CTR_WORDS * 4);
+    DevMem drk(R * sizeof(void*)), dg(R * 4);
+    WDR_HIP(hipMemset(ctr.p, 0, ctr.bytes));
+    WDR_HIP(hipMemcpy(dq.p, q, dq.bytes, hipMemcpyHostToDevice));
+    WDR_HIP(hipMemcpy(dkv.p, kv, dkv.bytes, hipMemcpyHostToDevice));
+    XAttnArgs xa{dq.as<f16>(), d, dkv.as<f16>(), dkv.as<f16>() + d, 2 * d, T, R, H, 0.125f, po.as<float>(),
+                 pml.as<float2>(), dout.as<f16>(), d};
+    xa.ctr = ctr.as<unsigned>();
+    if (row_slot) {
+      std::vector<const f16*> rk(R);
+      for (int r = 0; r < R; ++r) {
+        WDR_CHECK(row_slot[r] >= 0 && row_slot[r] < S, "dbg xattn: slot out of range");
+        rk[r] = dkv.as<f16>() + (size_t)row_slot[r] * T * 2 * d;
+      }
+      WDR_HIP(hipMemcpy(drk.p, rk.data(), R * sizeof(void*), hipMemcpyHostToDevice));
+      xa.row_k = drk.as<const f16*>();
+      if (grp) {
+        int ng = 0;
+        for (int r = 0; r < R; ++r) {
+          WDR_CHECK(grp[r] >= 0 && grp[r] <= XATTN_GRP_MAX && r + grp[r] <= R, "dbg xattn: bad group");
+          ng += grp[r] > 0;
+        }
+        WDR_HIP(hipMemcpy(dg.p, grp, R * 4, hipMemcpyHostToDevice));
+        xa.grp = dg.as<int>();
+        xa.n_grp = ng;
+      }
+    }
+    for (int i = 0; i < iters; ++i) launch_xattn(xa, nullptr);
+    WDR_HIP(hipDeviceSynchronize());
+    std::vector<f16> h((size_t)R * d);
     WDR_HIP(hipMemcpy(h.data(), dout.p, h.size() * 2, hipMemcpyDeviceToHost));
     for (size_t i = 0; i < h.size(); ++i) out[i] = (float)h[i];
     return 0;

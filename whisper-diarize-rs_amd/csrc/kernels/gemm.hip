@@ -1344,6 +1344,23 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
 
 void launch_proj(const ProjArgs& a, hipStream_t s) {
   WDR_CHECK(a.M > 0 && a.K > 0 && a.N > 0, "projection: empty shape");
+  if (a.step_rows && a.M > 16) {
+    // a batched step of more than 16 rows (beams of several segments): 16-row GEMV launches,
+    // so every row's arithmetic stays that of a <= 16-row step whatever the batch holds
+    // (batch composition depends on timing; results must not)
+    const int ob = (a.epi == EPI_F32_RESID || a.epi == EPI_F32 || a.epi == EPI_F32_GELU_POS) ? 4 : 2;
+    for (int r0 = 0; r0 < a.M; r0 += 16) {
+      ProjArgs c = a;
+      c.M = std::min(16, a.M - r0);
+      if (a.A) c.A = a.A + (size_t)r0 * a.lda;
+      if (a.ln_x) c.ln_x = a.ln_x + (size_t)r0 * a.ldln;
+      c.out = (char*)a.out + (size_t)r0 * a.ldo * ob;
+      if (a.row_seq) c.row_seq = a.row_seq + r0;
+      if (a.row_pos) c.row_pos = a.row_pos + r0;
+      launch_proj(c, s);
+    }
+    return;
+  }
   WDR_CHECK(a.K % 8 == 0 && a.lda % 8 == 0 && a.ldb % 8 == 0, "projection: K/lda/ldb must be multiples of 8");
   if (a.M > 64) {
     WDR_CHECK(a.N % GB_N == 0, "gemm: N must be a multiple of 128");

@@ -117,7 +117,18 @@ struct XAttnArgs {
   const f16* const* row_k = nullptr;
   long long layer_off = 0;
   unsigned long long* ts = nullptr;   // live kernel clock (common.h ProfClock)
+  // row groups sharing one cross K/V (the beams of one segment in a batched step), row_k mode:
+  // grp[r] = the size of the group row r leads (rows r .. r + grp[r] - 1, <= XATTN_GRP_MAX, K/V
+  // at row_k[r]), 0 for the other rows of a group (device array [R]); n_grp = groups (for the
+  // byte count).  Null: every row its own group; without row_k one group of all R rows (k / v)
+  const int* grp = nullptr;
+  int n_grp = 0;
+  // split arrival counters of the in-launch combine, [groups][n_head] u32, zero at allocation
+  // (XATTN_CTR_WORDS per owner; every launch adds a multiple of the split count to each)
+  unsigned* ctr = nullptr;
 };
+constexpr int XATTN_GRP_MAX = 8;               // rows per group
+constexpr int XATTN_CTR_WORDS = 128 * 32;      // counters per owner: groups x heads
 inline unsigned long long* prof_attach(XAttnArgs& a) { return a.ts = prof_slot(); }
 void launch_xattn(const XAttnArgs& a, hipStream_t s);
 struct CaptureArgs {

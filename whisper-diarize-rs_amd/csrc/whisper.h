@@ -143,24 +143,33 @@ struct StepIO {
   f16* kc; f16* vc; long long layer_stride, seq_stride;   // KV pool (layer 0) and its strides
   const f16* xkv;                  // one cross-K/V slot for every row, or
   const f16* const* row_xkv;       // per-row slot bases (device array)
+  unsigned* xctr = nullptr;        // cross-attention arrival counters (XATTN_CTR_WORDS, zeroed)
+  const int* grp = nullptr;        // row groups sharing a slot (XAttnArgs::grp), or null
+  int n_grp = 0;
 };
 void decode_step_layers(const Context& ctx, const StepIO& io, int R, hipStream_t s);
 
-// Multi-chain greedy decoding: several States ("chains", each decoding its own contiguous
-// block of speech segments on its own host thread) hand their single-row greedy steps to
-// this batcher, which runs them as ONE R-row step (weights streamed once for all rows; each
-// row with its own KV-pool sequence and cross-K/V slot) on its own stream.  Lockstep: a
-// batch launches once every chain inside a greedy decode loop has submitted its row.
+// Multi-chain decoding: several States ("chains", each decoding its own contiguous block of
+// speech segments on its own host thread) hand their decode steps -- one row (greedy) or the
+// live beams of a segment (beam search, with top-K candidates per row) -- to this batcher,
+// which runs them as ONE R-row step (weights streamed once per 16 rows; each row with its own
+// KV-pool sequence, the rows of a request sharing their segment's cross-K/V slot, read once
+// for all of them) on its own stream.  Lockstep: a batch launches once every chain inside a
+// decode loop has submitted its request.
 class StepBatcher {
  public:
   explicit StepBatcher(Context& ctx);
   ~StepBatcher();
+  static constexpr int kRows = 8;   // rows of one request (the beams / decoders of a segment)
   struct Req {
-    int tok, seq, pos;         // seq: absolute KV-pool sequence
-    const f16* xkv;            // the row's cross-K/V slot
-    LogitsCtl ctl;
-    VocabIds vids;
-    TokenData out;
+    int n = 1;                 // rows
+    int tok[kRows], seq[kRows], pos[kRows];   // seq: absolute KV-pool sequence
+    LogitsCtl ctl[kRows];
+    const f16* xkv = nullptr;  // the segment's cross-K/V slot (all its rows)
+    VocabIds vids{};
+    int K = 0;                 // beam candidates per row (0: the greedy pick only)
+    TokenData out[kRows];
+    BeamCand cand[kRows * BEAM_KMAX];   // [row][K]
   };
   void enter();
   void leave();

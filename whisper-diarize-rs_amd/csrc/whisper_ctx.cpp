@@ -372,6 +372,7 @@ struct PrefillBufs {
   float* fpart_o; float2* fpart_ml; float2* ml; float* cap; float* part_o; float2* part_ml;
   float* logits;
   int* h_rows;
+  unsigned* xctr;
 };
 
 struct State::Impl {
@@ -407,14 +408,14 @@ struct State::Impl {
   // encode-ahead language detection: its own prefill working set and the 100 language
   // logits of each slot's window 0 (pinned, written by the encode stream before `ready`)
   struct LangSet {
-    DevMem xd, hd, qkvd, attd, qx, mlpd, rows_tok, rows_pos, rows_seq, part_o, part_ml, logits, row_xkv;
+    DevMem xd, hd, qkvd, attd, qx, mlpd, rows_tok, rows_pos, rows_seq, part_o, part_ml, logits, row_xkv, xctr;
     const f16** h_xkv = nullptr;   // pinned [(S + 1)][kBatch] row cross-K/V bases, by first slot
   } lset;
   float* h_lang = nullptr;      // [(S + 1)][100]
   DevMem energy_d; int energy_cap = 0;
   const f16* xkv() const { return xkv_ring.as<f16>() + (size_t)cur * xkv_slot_elems; }
   // decoder
-  DevMem xd, hd, qkvd, attd, qx, mlpd, logits, work, tokout, ctl, ml, cap, part_o, part_ml;
+  DevMem xd, hd, qkvd, attd, qx, mlpd, logits, work, tokout, ctl, ml, cap, part_o, part_ml, xctr;
   DevMem rows_tok, rows_pos, rows_seq;
   DevMem beamc, kvpairs;       // beam candidates [NSEQ][BEAM_KMAX], KV reorder (src, dst) pairs
   BeamCand* h_beam = nullptr;
@@ -433,7 +434,7 @@ struct State::Impl {
   PrefillBufs pb_main{}, pb_dtw{};
   struct DtwSet {
     DevMem xd, hd, qkvd, attd, qx, mlpd, rows_tok, rows_pos, rows_seq, fpart_o, fpart_ml, ml, cap, part_o, part_ml,
-        nrm, xdtw, times;
+        nrm, xdtw, times, xctr;
   } dset;
   hipStream_t sd = nullptr;        // DTW stream
   hipEvent_t ev_sync = nullptr;    // decode-stream point the DTW stream waits for
@@ -469,6 +470,13 @@ struct State::Impl {
 
 static constexpr int kBatch = 4;     // encoder windows per encode-ahead launch (M = 6000 rows)
 static constexpr int kSlots = 16;    // in-flight segments in the cross-K/V ring
+
+// cross-attention arrival counters of one working set (kernels/attn.hip k_xattn_dec)
+static DevMem zeroed_ctr() {
+  DevMem c((size_t)XATTN_CTR_WORDS * 4);
+  WDR_HIP(hipMemset(c.p, 0, c.bytes));
+  return c;
+}
 
 static void alloc_enc(State::Impl::EncBufs& e, int nb, int d, int kp1) {
   e.nb = nb;
@@ -533,6 +541,7 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
   m.cap = DevMem((size_t)A * RMAX * 1500 * 4);
   m.part_o = DevMem((size_t)NSPLIT * NSEQ * m.H * 64 * 4);
   m.part_ml = DevMem((size_t)NSPLIT * NSEQ * m.H * sizeof(float2));
+  m.xctr = zeroed_ctr();
   m.fpart_o = DevMem((size_t)12 * 256 * m.H * 64 * 4);
   m.fpart_ml = DevMem((size_t)12 * m.H * 256 * sizeof(float2));
   m.beamc = DevMem(NSEQ * BEAM_KMAX * sizeof(BeamCand));
@@ -569,13 +578,14 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
     D.cap = DevMem((size_t)A * RMAX * 1500 * 4);
     D.part_o = DevMem((size_t)NSPLIT * NSEQ * m.H * 64 * 4);
     D.part_ml = DevMem((size_t)NSPLIT * NSEQ * m.H * sizeof(float2));
+    D.xctr = zeroed_ctr();
     D.nrm = DevMem((size_t)A * RMAX * 1500 * 4);
     D.xdtw = DevMem((size_t)RMAX * 1500 * 4);
     D.times = DevMem((RMAX + 8) * 4);
     m.pb_dtw = PrefillBufs{D.xd.as<float>(), D.hd.as<f16>(), D.qkvd.as<f16>(), D.attd.as<f16>(), D.qx.as<f16>(),
                         D.mlpd.as<f16>(), D.rows_tok.as<int>(), D.rows_pos.as<int>(), D.rows_seq.as<int>(),
                         D.fpart_o.as<float>(), D.fpart_ml.as<float2>(), D.ml.as<float2>(), D.cap.as<float>(),
-                        D.part_o.as<float>(), D.part_ml.as<float2>(), nullptr, nullptr};
+                        D.part_o.as<float>(), D.part_ml.as<float2>(), nullptr, nullptr, D.xctr.as<unsigned>()};
     // language detection: one kBatch-row step (SOT at position 0, one KV sequence and one
     // cross-K/V slot per window) per encode-ahead batch
     Impl::LangSet& G = m.lset;
@@ -590,6 +600,7 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
     G.rows_seq = DevMem(LB * 4);
     G.part_o = DevMem((size_t)NSPLIT * LB * m.H * 64 * 4);
     G.part_ml = DevMem((size_t)NSPLIT * LB * m.H * sizeof(float2));
+    G.xctr = zeroed_ctr();
     G.logits = DevMem((size_t)LB * m.V * 4);
     G.row_xkv = DevMem(LB * sizeof(void*));
     WDR_HIP(hipHostMalloc((void**)&G.h_xkv, (size_t)(kSlots + 1) * LB * sizeof(void*), hipHostMallocDefault));
@@ -620,7 +631,8 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
   m.pb_main = PrefillBufs{m.xd.as<float>(), m.hd.as<f16>(), m.qkvd.as<f16>(), m.attd.as<f16>(), m.qx.as<f16>(),
                        m.mlpd.as<f16>(), m.rows_tok.as<int>(), m.rows_pos.as<int>(), m.rows_seq.as<int>(),
                        m.fpart_o.as<float>(), m.fpart_ml.as<float2>(), m.ml.as<float2>(), m.cap.as<float>(),
-                       m.part_o.as<float>(), m.part_ml.as<float2>(), m.logits.as<float>(), m.h_rows};
+                       m.part_o.as<float>(), m.part_ml.as<float2>(), m.logits.as<float>(), m.h_rows,
+                       m.xctr.as<unsigned>()};
   // The persistent one-launch step is measured SLOWER than the per-kernel chain on MI355X
   // (2.7 vs ~1.7 ms per large-v3 step: in-launch all-to-all hand-offs cost 2.5-7 us each, more
   // than the ~1.2 us kernel boundaries they replace), so it is opt-in.
@@ -909,7 +921,7 @@ void State::top_up(int j) {
       StepIO io{G.xd.as<float>(), G.qkvd.as<f16>(), G.attd.as<f16>(), G.qx.as<f16>(), G.mlpd.as<f16>(),
                 G.logits.as<float>(), m.V, G.part_o.as<float>(), G.part_ml.as<float2>(), G.rows_tok.as<int>(),
                 G.rows_pos.as<int>(), G.rows_seq.as<int>(), m.kc, m.vc, (long long)m.nslot_tot * m.seq_stride,
-                m.seq_stride, nullptr, G.row_xkv.as<const f16*>()};
+                m.seq_stride, nullptr, G.row_xkv.as<const f16*>(), G.xctr.as<unsigned>()};
       decode_step_layers(ctx_, io, R, m.es);
       for (int r = 0; r < R; ++r)
         WDR_HIP(hipMemcpyAsync(m.h_lang + (size_t)((g0 + r) % m.S) * 100,
@@ -1013,7 +1025,8 @@ void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool c
     } else {
       XAttnArgs xa{b.qx, d, xk, xv, ldxkv, 1500, n, hp.n_text_head, scale, b.part_o,
                    b.part_ml, b.attd, d};
-        launch_xattn(xa, st);
+      xa.ctr = b.xctr;
+      launch_xattn(xa, st);
     }
     if (l_end < L && l == l_end - 1) break;   // capture-only pass: done after the last head layer
     proj(st, b.attd, d, e.w_xo, d, e.b_xo, b.xd, d, n, d, d, EPI_F32_RESID);
@@ -1054,7 +1067,7 @@ void State::decoder_step_body(int R) {
   StepIO io{m.xd.as<float>(), m.qkvd.as<f16>(), m.attd.as<f16>(), m.qx.as<f16>(), m.mlpd.as<f16>(),
             m.logits.as<float>(), m.V, m.part_o.as<float>(), m.part_ml.as<float2>(), m.rows_tok.as<int>(),
             m.rows_pos.as<int>(), m.rows_seq.as<int>(), m.kc, m.vc, (long long)m.nslot_tot * m.seq_stride,
-            m.seq_stride, m.xkv(), nullptr};
+            m.seq_stride, m.xkv(), nullptr, m.xctr.as<unsigned>()};
   decode_step_layers(ctx_, io, R, s_);
 }
 
@@ -1106,6 +1119,9 @@ void decode_step_layers(const Context& ctx, const StepIO& io, int R, hipStream_t
     launch_proj(P(io.attd, d, e.w_o, e.b_o, io.xd, d, d, d, EPI_F32_RESID), s);
     launch_proj(P(nullptr, d, e.w_xq, e.b_xq, io.qx, d, d, d, EPI_F16, e.ln2_g, e.ln2_b), s);
     XAttnArgs xa{io.qx, d, nullptr, nullptr, ldxkv, 1500, R, hp.n_text_head, scale, io.part_o, io.part_ml, io.attd, d};
+    xa.ctr = io.xctr;
+    xa.grp = io.grp;
+    xa.n_grp = io.n_grp;
     if (io.row_xkv) {
       xa.row_k = io.row_xkv;
       xa.layer_off = (long long)l * 2 * d;
@@ -1297,6 +1313,19 @@ void State::dbg_step(const int* toks, int n, bool classic, float* logits_out) {
   step_err_check();
 }
 
+// a one-row (greedy) batcher request
+static StepBatcher::Req row_req(int tok, int seq, int pos, const f16* xkv, const LogitsCtl& c, const VocabIds& v) {
+  StepBatcher::Req q;
+  q.n = 1;
+  q.tok[0] = tok;
+  q.seq[0] = seq;
+  q.pos[0] = pos;
+  q.ctl[0] = c;
+  q.xkv = xkv;
+  q.vids = v;
+  return q;
+}
+
 double State::dbg_batch_step(const int* toks, int n, int R, int iters) {
   Impl& m = *m_;
   WDR_CHECK(n >= 2 && n <= 448 && R >= 1 && R <= 16 && iters >= 1, "dbg_batch_step: bad shape");
@@ -1311,7 +1340,7 @@ double State::dbg_batch_step(const int* toks, int n, int R, int iters) {
     c.pen_ts = 1;
     c.force_kind = 2;
     // every row reads this window's cross-K/V; rows 1.. attend over an uninitialised cache
-    rq[r] = StepBatcher::Req{toks[n - 1], chain * NSLOT + r, n - 1, m.xkv(), c, m.vids, {}};
+    rq[r] = row_req(toks[n - 1], chain * NSLOT + r, n - 1, m.xkv(), c, m.vids);
     batch[r] = &rq[r];
   }
   b.run(batch);
@@ -1608,6 +1637,13 @@ Seq State::decode_beam(const std::vector<int>& prompt, const FullParams& params,
   }
   std::vector<BeamCand> bc((size_t)NSEQ * K);
   std::vector<TokenData> td(NSEQ);
+  // multi-chain run: from the second token on, the live beams join the batched step
+  struct Seat {
+    StepBatcher* b = nullptr;
+    ~Seat() {
+      if (b) b->leave();
+    }
+  } seat;
   for (int i = 0; i < n_max; ++i) {
     std::vector<int> act;
     for (int j = 0; j < K; ++j)
@@ -1647,7 +1683,31 @@ Seq State::decode_beam(const std::vector<int>& prompt, const FullParams& params,
         toks[r] = dec[act[r]].tokens.back().id;
         seqs[r] = act[r];
       }
-      step_and_sample(toks.data(), seqs.data(), pos.data(), ctl.data(), (int)act.size(), td.data(), K, bc.data());
+      if (batched) {
+        if (!seat.b) {
+          seat.b = &ctx_.step_batcher();
+          seat.b->enter();
+        }
+        StepBatcher::Req q;
+        q.n = (int)act.size();
+        for (int r = 0; r < q.n; ++r) {
+          q.tok[r] = toks[r];
+          q.seq[r] = chain * NSLOT + seqs[r];
+          q.pos[r] = pos[r];
+          q.ctl[r] = ctl[r];
+        }
+        q.xkv = m_->xkv();
+        q.vids = m_->vids;
+        q.K = K;
+        seat.b->step(q);
+        for (int r = 0; r < q.n; ++r) {
+          td[r] = q.out[r];
+          for (int k = 0; k < K; ++k) bc[(size_t)r * K + k] = q.cand[r * K + k];
+        }
+        times.decode_steps++;
+      } else {
+        step_and_sample(toks.data(), seqs.data(), pos.data(), ctl.data(), (int)act.size(), td.data(), K, bc.data());
+      }
     }
     struct Cand {
       int j;
@@ -2090,9 +2150,9 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
               lockstep.b = &ctx_.step_batcher();
               lockstep.b->enter();
             }
-            StepBatcher::Req rq{prev_id, chain * NSLOT + seq0, pos, m.xkv(), c, m.vids, {}};
+            StepBatcher::Req rq = row_req(prev_id, chain * NSLOT + seq0, pos, m.xkv(), c, m.vids);
             lockstep.b->step(rq);
-            tok = rq.out;
+            tok = rq.out[0];
             times.decode_steps++;
           } else {
             step_and_sample(&prev_id, &seq0, &pos, &c, 1, &tok);
@@ -2194,7 +2254,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
 // ------------------------------------------------------------------ multi-chain step batcher
 namespace wdr {
 
-static constexpr int RB = 16;     // rows per batched step (chains)
+static constexpr int RB = 128;    // rows per batched step (chains x beams)
 
 struct StepBatcher::Impl {
   std::mutex mu;
@@ -2207,15 +2267,17 @@ struct StepBatcher::Impl {
   hipStream_t s = nullptr;
   int d = 0, V = 0, H = 0;
   DevMem xd, qkvd, attd, qx, mlpd, logits, work, tokout, ctl, rows_tok, rows_pos, rows_seq, row_xkv, part_o, part_ml;
-  int* h_rows = nullptr;          // [3][RB]
+  DevMem xctr, grp, beamc;
+  int* h_rows = nullptr;          // [4][RB]: tokens, positions, sequences, group sizes
   LogitsCtl* h_ctl = nullptr;
   const f16** h_xkv = nullptr;
   TokOut* h_tok = nullptr;
+  BeamCand* h_beam = nullptr;     // [RB][BEAM_KMAX]
   struct G {
     hipGraphExec_t exec = nullptr;
     VocabIds vids{};
   };
-  std::map<int, G> graphs;        // by row count
+  std::map<int, G> graphs;        // by (K, grouped, row count)
 };
 
 StepBatcher::StepBatcher(Context& ctx) : ctx_(ctx), m_(new Impl) {
@@ -2244,7 +2306,11 @@ StepBatcher::StepBatcher(Context& ctx) : ctx_(ctx), m_(new Impl) {
   m.row_xkv = DevMem(RB * sizeof(void*));
   m.part_o = DevMem((size_t)NSPLIT * RB * m.H * 64 * 4);
   m.part_ml = DevMem((size_t)NSPLIT * RB * m.H * sizeof(float2));
-  WDR_HIP(hipHostMalloc((void**)&m.h_rows, 3 * RB * 4, hipHostMallocDefault));
+  m.xctr = zeroed_ctr();
+  m.grp = DevMem(RB * 4);
+  m.beamc = DevMem((size_t)RB * BEAM_KMAX * sizeof(BeamCand));
+  WDR_HIP(hipHostMalloc((void**)&m.h_beam, (size_t)RB * BEAM_KMAX * sizeof(BeamCand), hipHostMallocDefault));
+  WDR_HIP(hipHostMalloc((void**)&m.h_rows, 4 * RB * 4, hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_ctl, RB * sizeof(LogitsCtl), hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_xkv, RB * sizeof(void*), hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_tok, RB * sizeof(TokOut), hipHostMallocDefault));
@@ -2262,6 +2328,7 @@ StepBatcher::~StepBatcher() {
   (void)hipHostFree(m_->h_ctl);
   (void)hipHostFree(m_->h_xkv);
   (void)hipHostFree(m_->h_tok);
+  (void)hipHostFree(m_->h_beam);
 }
 
 StepBatcher& Context::step_batcher() {
@@ -2328,18 +2395,31 @@ void StepBatcher::step(Req& r) {
   if (m.err) std::rethrow_exception(m.err);
 }
 
-// one R-row greedy step: embed, the layer chain with per-row cross-K/V, logit rules + pick
+// one R-row step: embed, the layer chain with per-row cross-K/V (grouped by request), logit
+// rules + greedy pick, and the top-K candidates of every row when a request asks for them
 void StepBatcher::launch(std::vector<Req*>& batch) {
   Impl& m = *m_;
-  const int R = (int)batch.size();
+  int R = 0, K = 0;
+  bool grouped = false;
+  for (Req* q : batch) {
+    WDR_CHECK(q->n >= 1 && q->n <= kRows && q->K >= 0 && q->K <= BEAM_KMAX, "step batcher: bad request");
+    R += q->n;
+    K = std::max(K, q->K);
+    grouped = grouped || q->n > 1 || q->K > 0;
+  }
   WDR_CHECK(R >= 1 && R <= RB, "step batcher: row count out of range");
   WDR_HIP(hipSetDevice(ctx_.cp.gpu_device));
-  for (int i = 0; i < R; ++i) {
-    m.h_rows[i] = batch[i]->tok;
-    m.h_rows[RB + i] = batch[i]->pos;
-    m.h_rows[2 * RB + i] = batch[i]->seq;
-    m.h_ctl[i] = batch[i]->ctl;
-    m.h_xkv[i] = batch[i]->xkv;
+  {
+    int i = 0;
+    for (Req* q : batch)
+      for (int j = 0; j < q->n; ++j, ++i) {
+        m.h_rows[i] = q->tok[j];
+        m.h_rows[RB + i] = q->pos[j];
+        m.h_rows[2 * RB + i] = q->seq[j];
+        m.h_rows[3 * RB + i] = j == 0 ? q->n : 0;
+        m.h_ctl[i] = q->ctl[j];
+        m.h_xkv[i] = q->xkv;
+      }
   }
   const VocabIds& vids = batch[0]->vids;
   const HParams& hp = ctx_.model.hp;
@@ -2347,11 +2427,17 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
   StepIO io{m.xd.as<float>(), m.qkvd.as<f16>(), m.attd.as<f16>(), m.qx.as<f16>(), m.mlpd.as<f16>(),
             m.logits.as<float>(), m.V, m.part_o.as<float>(), m.part_ml.as<float2>(), m.rows_tok.as<int>(),
             m.rows_pos.as<int>(), m.rows_seq.as<int>(), ctx_.kv_k.as<f16>(), ctx_.kv_v.as<f16>(),
-            (long long)ctx_.max_chains * NSLOT * seq_stride, seq_stride, nullptr, m.row_xkv.as<const f16*>()};
+            (long long)ctx_.max_chains * NSLOT * seq_stride, seq_stride, nullptr, m.row_xkv.as<const f16*>(),
+            m.xctr.as<unsigned>()};
+  if (grouped) {
+    io.grp = m.grp.as<int>();
+    io.n_grp = (int)batch.size();
+  }
   auto body = [&]() {
     WDR_HIP(hipMemcpyAsync(m.rows_tok.p, m.h_rows, R * 4, hipMemcpyHostToDevice, m.s));
     WDR_HIP(hipMemcpyAsync(m.rows_pos.p, m.h_rows + RB, R * 4, hipMemcpyHostToDevice, m.s));
     WDR_HIP(hipMemcpyAsync(m.rows_seq.p, m.h_rows + 2 * RB, R * 4, hipMemcpyHostToDevice, m.s));
+    if (grouped) WDR_HIP(hipMemcpyAsync(m.grp.p, m.h_rows + 3 * RB, R * 4, hipMemcpyHostToDevice, m.s));
     WDR_HIP(hipMemcpyAsync(m.ctl.p, m.h_ctl, R * sizeof(LogitsCtl), hipMemcpyHostToDevice, m.s));
     WDR_HIP(hipMemcpyAsync(m.row_xkv.p, m.h_xkv, R * sizeof(void*), hipMemcpyHostToDevice, m.s));
     launch_embed(ctx_.model.tok_emb, ctx_.model.dec_pos, m.rows_tok.as<int>(), m.rows_pos.as<int>(), R, m.d,
@@ -2360,6 +2446,11 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
     launch_logits_process(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), vids, R, m.work.as<float>(),
                           m.tokout.as<TokOut>(), m.s);
     WDR_HIP(hipMemcpyAsync(m.h_tok, m.tokout.p, R * sizeof(TokOut), hipMemcpyDeviceToHost, m.s));
+    if (K > 0) {
+      launch_logits_topk(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), vids, R, K, m.work.as<float>(),
+                         m.beamc.as<BeamCand>(), m.s);
+      WDR_HIP(hipMemcpyAsync(m.h_beam, m.beamc.p, (size_t)R * K * sizeof(BeamCand), hipMemcpyDeviceToHost, m.s));
+    }
   };
   const double t_step = now_s();
   const bool sampled = prof_step();
@@ -2374,7 +2465,7 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
     }
     prof_in_step(false);
   } else {
-    Impl::G& g = m.graphs[R];
+    Impl::G& g = m.graphs[(K << 20) + (grouped ? 1 << 16 : 0) + R];
     if (g.exec && memcmp(&g.vids, &vids, sizeof(VocabIds)) != 0) {
       (void)hipGraphExecDestroy(g.exec);
       g.exec = nullptr;
@@ -2393,16 +2484,22 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
     WDR_HIP(hipGraphLaunch(g.exec, m.s));
   }
   WDR_HIP(hipStreamSynchronize(m.s));
-  for (int i = 0; i < R; ++i) {
-    const TokOut& o = m.h_tok[i];
-    TokenData& t = batch[i]->out;
-    t = TokenData{};
-    t.id = o.id;
-    t.tid = o.tid;
-    t.p = o.p;
-    t.plog = o.plog;
-    t.pt = o.pt;
-    t.ptsum = o.ptsum;
+  {
+    int i = 0;
+    for (Req* q : batch)
+      for (int j = 0; j < q->n; ++j, ++i) {
+        const TokOut& o = m.h_tok[i];
+        TokenData& t = q->out[j];
+        t = TokenData{};
+        t.id = o.id;
+        t.tid = o.tid;
+        t.p = o.p;
+        t.plog = o.plog;
+        t.pt = o.pt;
+        t.ptsum = o.ptsum;
+        if (q->K > 0)
+          for (int k = 0; k < q->K; ++k) q->cand[j * q->K + k] = m.h_beam[(size_t)i * K + k];
+      }
   }
   launches++;
   rows += R;

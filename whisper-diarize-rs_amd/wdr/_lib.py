@@ -168,6 +168,7 @@ _SIGS = {
     "wdr_dbg_dtw_dp": (C.c_int, [P(f32), i32, i32, i32, P(i32), P(i32)]),
     "wdr_dbg_proj": (C.c_int, [P(C.c_uint16), P(C.c_uint16), P(f32), i32, i32, i32, i32, P(f32)]),
     "wdr_dbg_attn": (C.c_int, [P(C.c_uint16), P(C.c_uint16), P(C.c_uint16), i32, i32, i32, i32, P(f32)]),
+    "wdr_dbg_xattn": (C.c_int, [P(C.c_uint16), P(C.c_uint16), P(i32), P(i32), i32, i32, i32, i32, P(f32)]),
 }
 
 _lib = None
