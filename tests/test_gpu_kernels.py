@@ -130,11 +130,11 @@ def _xattn(lib, q, kv, H, row_slot=None, grp=None, iters=1):
 
 
 def test_decode_cross_attention(lib):
-    """k_xattn_dec (one wave per key split, online softmax, splits merged in-launch by the last
-    arriving wave): per-row slots (batched greedy step), beam groups sharing a slot, the shared
-    form, and repeated launches on the same arrival counters.  Every row must equal the fp64
-    attention within the f16 P / output rounding, and a row's result must not depend on the
-    group it is computed in (batch composition varies with timing)."""
+    """k_xattn_partial + k_xattn_combine (64-key chunks, row groups sharing a chunk): per-row
+    slots (batched greedy step), beam groups sharing a slot, the shared form, and repeated
+    launches.  Every row must equal the fp64 attention within the f16 P / output rounding, and
+    a row's result must not depend on the group it is computed in (batch composition varies
+    with timing)."""
     rng = np.random.default_rng(11)
     H, S, R = 3, 6, 24
     q = (rng.standard_normal((R, H * 64)) * 1.5).astype(np.float16).astype(np.float32)

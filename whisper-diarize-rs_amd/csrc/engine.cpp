@@ -1932,14 +1932,12 @@ int wdr_dbg_xattn(const uint16_t* q, const uint16_t* kv, const int32_t* row_slot
     WDR_CHECK(R >= 1 && R <= 128 && S >= 1 && H >= 1 && H <= 32 && iters >= 1, "dbg xattn: bad shape");
     const int d = H * 64, T = 1500;
     DevMem dq((size_t)R * d * 2), dkv((size_t)S * T * 2 * d * 2), dout((size_t)R * d * 2);
-    DevMem po((size_t)24 * R * H * 64 * 4), pml((size_t)24 * R * H * 8), ctr((size_t)XATTN_CTR_WORDS * 4);
+    DevMem po((size_t)24 * R * H * 64 * 4), pml((size_t)24 * R * H * 8);
     DevMem drk(R * sizeof(void*)), dg(R * 4);
-    WDR_HIP(hipMemset(ctr.p, 0, ctr.bytes));
     WDR_HIP(hipMemcpy(dq.p, q, dq.bytes, hipMemcpyHostToDevice));
     WDR_HIP(hipMemcpy(dkv.p, kv, dkv.bytes, hipMemcpyHostToDevice));
     XAttnArgs xa{dq.as<f16>(), d, dkv.as<f16>(), dkv.as<f16>() + d, 2 * d, T, R, H, 0.125f, po.as<float>(),
                  pml.as<float2>(), dout.as<f16>(), d};
-    xa.ctr = ctr.as<unsigned>();
     if (row_slot) {
       std::vector<const f16*> rk(R);
       for (int r = 0; r < R; ++r) {

@@ -267,157 +267,105 @@ void launch_dec_self_attn(const DecSelfArgs& a, int R, int n_head, hipStream_t s
   WDR_HIP(hipGetLastError());
 }
 
-// ---------------------------------------------------------------- decoder cross-attention
+// ---------------------------------------------------------------- decoder cross-attention (split)
 //
-// One wave per workgroup, one (key split, head, row group) per wave: the wave streams XD_BPW
-// 64-key blocks of the group's cross K/V (lane = key: its 128-B K row straight into registers,
-// its V row through LDS), the next block's loads in flight while the current one is scored,
-// and keeps an online softmax for every row of the group -- the K/V bytes are read once for
-// all the group's rows (beams of one segment).  The XD_NS splits of a (group, head) are merged
-// in the same launch by the last-arriving wave (split-K arrival counter, agent-scope release /
-// acquire: cdna_hip_programming.md §6 Guideline 16), so the step has no combine launch.
-constexpr int XD_BPW = 3;                 // 64-key blocks per wave
-constexpr int XD_NS = 24 / XD_BPW;        // splits over the 1500 (24 x 64) keys; power of two
-static_assert((XD_NS & (XD_NS - 1)) == 0, "split count must divide 2^32 (ticket modulo)");
-constexpr int XD_VS = 72;                 // LDS row stride of V (halves)
+// One workgroup per (64-key chunk, head, row group): thread t takes key t/4 of the chunk and
+// dims 16*(t%4)..+16 (4 threads = one key's 128-B head row: coalesced 16-B loads, all issued up
+// front), V goes through LDS, and the four waves share the P.V (16 keys each).  A row group is
+// the rows sharing one cross K/V -- the beams of one segment -- whose chunk is fetched once and
+// scored row after row with exactly the arithmetic of a single row, so a row's result never
+// depends on the group (or batch) it runs in.  ROWS: each group its own cross K/V (row_k: the
+// multi-chain batched step), else one group of all R rows on k / v (a State's own step).  The
+// 24 chunk partials of each row are merged by k_xattn_combine.
+constexpr int XA_KC = 64, XA_NS = 24;
 
-template <int NR>
-__global__ __launch_bounds__(64) void k_xattn_dec(XAttnArgs a) {
+template <bool ROWS>
+__global__ __launch_bounds__(256) void k_xattn_partial(XAttnArgs a) {
   ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
-  __shared__ __attribute__((aligned(16))) float qs[NR][64];
-  __shared__ __attribute__((aligned(16))) float ps[NR][64];
-  __shared__ __attribute__((aligned(16))) f16 Vs[64 * XD_VS];
-  __shared__ int last;
-  const int c = blockIdx.x, h = blockIdx.y, g = blockIdx.z, lane = threadIdx.x;
-  const int H = a.n_head;
+  __shared__ __attribute__((aligned(16))) f16 Vs[XA_KC * 64];
+  __shared__ float red[2][4];
+  __shared__ float ps[XA_KC];
+  __shared__ float pv[4][64];
+  const int c = blockIdx.x, h = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   int r0 = 0, nr = a.R;
   const f16* kb = a.k;
   const f16* vb = a.v;
-  if (a.row_k) {
-    r0 = g;
-    nr = a.grp ? a.grp[g] : 1;
+  if (ROWS) {
+    r0 = blockIdx.z;
+    nr = a.grp ? a.grp[r0] : 1;
     if (nr == 0) return;   // a row of a group led by an earlier row
     kb = a.row_k[r0] + a.layer_off;
-    vb = kb + H * 64;
+    vb = kb + a.n_head * 64;
   }
-  // q pre-scaled by 1/8 (a power of two: exact), as the product ggml scales
+  const int key0 = c * XA_KC;
+  const int kk = tid >> 2, qd = tid & 3;
+  const int key = key0 + kk;
+  const bool kok = key < a.Tk;
+  const long long row = (long long)(kok ? key : a.Tk - 1) * a.ldkv + h * 64 + qd * 16;
+  const f16x8 k0 = *(const f16x8*)(kb + row), k1 = *(const f16x8*)(kb + row + 8);
+  const f16x8 v0 = *(const f16x8*)(vb + row), v1 = *(const f16x8*)(vb + row + 8);
+  *(f16x8*)(Vs + kk * 64 + qd * 16) = v0;
+  *(f16x8*)(Vs + kk * 64 + qd * 16 + 8) = v1;
+  for (int r = r0; r < r0 + nr; ++r) {
+    const f16* qr = a.q + (long long)r * a.ldq + h * 64 + qd * 16;
+    const f16x8 q0 = *(const f16x8*)qr, q1 = *(const f16x8*)(qr + 8);
+    float sc = 0.f;
 #pragma unroll
-  for (int r = 0; r < NR; ++r)
-    if (r < nr) qs[r][lane] = (float)a.q[(long long)(r0 + r) * a.ldq + h * 64 + lane] * a.scale;
-  float m[NR], l[NR], acc[NR];
-#pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    m[r] = -INFINITY;
-    l[r] = 0.f;
-    acc[r] = 0.f;
-  }
-  const int key0 = c * XD_BPW * 64;
-  f16x8 kr[8], vr[8];
-  auto load = [&](int b, f16x8* kd, f16x8* vd) {
-    int key = key0 + b * 64 + lane;
-    key = key < a.Tk ? key : a.Tk - 1;
-    const long long off = (long long)key * a.ldkv + h * 64;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      kd[e] = *(const f16x8*)(kb + off + e * 8);
-      vd[e] = *(const f16x8*)(vb + off + e * 8);
-    }
-  };
-  load(0, kr, vr);
-  for (int b = 0; b < XD_BPW; ++b) {
-    const bool kok = key0 + b * 64 + lane < a.Tk;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) *(f16x8*)(Vs + lane * XD_VS + e * 8) = vr[e];
-    f16x8 kn[8], vn[8];
-    if (b + 1 < XD_BPW) load(b + 1, kn, vn);
-    // scores of this lane's key for every row, online softmax per row
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      if (r >= nr) break;
-      float sc = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const f32x4 q0 = *(const f32x4*)&qs[r][e * 8];
-        const f32x4 q1 = *(const f32x4*)&qs[r][e * 8 + 4];
-        sc += q0[0] * (float)kr[e][0] + q0[1] * (float)kr[e][1] + q0[2] * (float)kr[e][2] + q0[3] * (float)kr[e][3];
-        sc += q1[0] * (float)kr[e][4] + q1[1] * (float)kr[e][5] + q1[2] * (float)kr[e][6] + q1[3] * (float)kr[e][7];
-      }
-      sc = kok ? sc : -INFINITY;
-      const float mx = fmaxf(m[r], wave_max(sc));
-      const float alpha = m[r] == -INFINITY ? 0.f : __expf(m[r] - mx);
-      const float p = sc == -INFINITY ? 0.f : __expf(sc - mx);
-      l[r] = l[r] * alpha + wave_sum(p);
-      m[r] = mx;
-      acc[r] *= alpha;
-      ps[r][lane] = (float)(f16)p;   // P in f16 for P.V, as the ggml graph
-    }
+    for (int e = 0; e < 8; ++e) sc += (float)q0[e] * (float)k0[e] + (float)q1[e] * (float)k1[e];
+    sc += __shfl_xor(sc, 1, 64);
+    sc += __shfl_xor(sc, 2, 64);
+    sc = kok ? sc * a.scale : -INFINITY;
+    const float wm = wave_max(sc);
+    if (lane == 0) red[0][wid] = wm;
     __syncthreads();
-    // P.V: lane = output dim
-#pragma unroll 4
-    for (int k = 0; k < 64; k += 4) {
-      const float v0 = (float)Vs[(k + 0) * XD_VS + lane], v1 = (float)Vs[(k + 1) * XD_VS + lane];
-      const float v2 = (float)Vs[(k + 2) * XD_VS + lane], v3 = (float)Vs[(k + 3) * XD_VS + lane];
-#pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        if (r >= nr) break;
-        const f32x4 p4 = *(const f32x4*)&ps[r][k];
-        acc[r] += p4[0] * v0 + p4[1] * v1 + p4[2] * v2 + p4[3] * v3;
-      }
-    }
+    const float mx = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+    const float p = sc == -INFINITY ? 0.f : __expf(sc - mx);
+    const float ws = wave_sum(qd == 0 ? p : 0.f);
+    if (qd == 0) ps[kk] = p;
+    if (lane == 0) red[1][wid] = ws;
     __syncthreads();
-    if (b + 1 < XD_BPW) {
+    float acc = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        kr[e] = kn[e];
-        vr[e] = vn[e];
-      }
+    for (int j = 0; j < 16; ++j) acc += (float)(f16)ps[wid * 16 + j] * (float)Vs[(wid * 16 + j) * 64 + lane];
+    pv[wid][lane] = acc;
+    __syncthreads();
+    if (tid < 64) {
+      const long long cr = (long long)c * a.R + r;
+      a.part_o[(cr * a.n_head + h) * 64 + tid] = pv[0][tid] + pv[1][tid] + pv[2][tid] + pv[3][tid];
+      if (tid == 0) a.part_ml[cr * a.n_head + h] = make_float2(mx, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
     }
-  }
-  // this split's partial (unnormalised O, max, sum) per row, then the arrival ticket
-  for (int r = 0; r < nr; ++r) {
-    const long long cr = (long long)c * a.R + r0 + r;
-    a.part_o[(cr * H + h) * 64 + lane] = acc[r];
-    if (lane == 0) a.part_ml[cr * H + h] = make_float2(m[r], l[r]);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(a.ctr + (long long)g * H + h, 1u, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-    last = (t % XD_NS) == XD_NS - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  if (lane == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int r = 0; r < nr; ++r) {
-    float2 ml = make_float2(-INFINITY, 0.f);
-    if (lane < XD_NS) ml = a.part_ml[((long long)lane * a.R + r0 + r) * H + h];
-    const float M = wave_max(ml.x);
-    const float w = (lane < XD_NS && ml.x != -INFINITY) ? __expf(ml.x - M) : 0.f;
-    const float L = wave_sum(ml.y * w);
-    float o = 0.f;
-#pragma unroll
-    for (int s = 0; s < XD_NS; ++s) o += a.part_o[(((long long)s * a.R + r0 + r) * H + h) * 64 + lane] * __shfl(w, s, 64);
-    a.o[(long long)(r0 + r) * a.ldo + h * 64 + lane] = (f16)(o / L);
+    __syncthreads();   // red / ps / pv are rewritten by the next row
   }
 }
 
+template <int NS>
+__global__ __launch_bounds__(64) void k_xattn_combine(XAttnArgs a) {
+  const int r = blockIdx.x, h = blockIdx.y, d = threadIdx.x;
+  float po[NS];
+#pragma unroll
+  for (int c = 0; c < NS; ++c) po[c] = a.part_o[(((long long)c * a.R + r) * a.n_head + h) * 64 + d];
+  float2 ml = make_float2(-INFINITY, 0.f);
+  if (d < NS) ml = a.part_ml[((long long)d * a.R + r) * a.n_head + h];
+  const float M = wave_max(ml.x);
+  const float w = (d < NS && ml.x != -INFINITY) ? __expf(ml.x - M) : 0.f;
+  const float L = wave_sum(ml.y * w);
+  float acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < NS; ++c) acc += po[c] * __shfl(w, c, 64);
+  a.o[(long long)r * a.ldo + h * 64 + d] = (f16)(acc / L);
+}
+
 void launch_xattn(const XAttnArgs& a, hipStream_t s) {
-  WDR_CHECK(a.Tk > (XD_NS * XD_BPW - 1) * 64 && a.Tk <= XD_NS * XD_BPW * 64, "cross-attention decode expects 1500 keys");
-  WDR_CHECK(a.ctr, "cross-attention decode: no arrival counters");
-  const int G = a.row_k ? a.R : 1;   // workgroup z: one per row (rows that do not lead a group exit)
-  WDR_CHECK(a.R >= 1 && G * a.n_head <= XATTN_CTR_WORDS, "cross-attention decode: too many rows");
-  WDR_CHECK(a.row_k || a.R <= XATTN_GRP_MAX, "cross-attention decode: more than 8 rows on one K/V");
-  const bool one = a.row_k ? !a.grp : a.R == 1;   // every group a single row
-  // algorithmic bytes: every group's K/V once (n_grp groups; one per row without grp)
+  WDR_CHECK(cdiv(a.Tk, XA_KC) == XA_NS, "cross-attention decode expects 1500 keys");
+  WDR_CHECK(a.R >= 1 && (a.row_k || a.R <= XATTN_GRP_MAX), "cross-attention decode: R out of range");
+  // algorithmic bytes: every group's K/V once
   const int ng = a.row_k ? (a.grp ? a.n_grp : a.R) : 1;
   const double bytes = (double)ng * a.Tk * a.n_head * 64 * 2 * 2, flops = (double)a.R * a.Tk * a.n_head * 64 * 4;
-  const dim3 grid(XD_NS, a.n_head, G);
-  if (one) wdr_launch(PROF_XATTN, bytes, flops, k_xattn_dec<1>, grid, dim3(64), 0, s, a);
-  else wdr_launch(PROF_XATTN, bytes, flops, k_xattn_dec<XATTN_GRP_MAX>, grid, dim3(64), 0, s, a);
+  if (a.row_k)
+    wdr_launch(PROF_XATTN, bytes, flops, k_xattn_partial<true>, dim3(XA_NS, a.n_head, a.R), dim3(256), 0, s, a);
+  else
+    wdr_launch(PROF_XATTN, bytes, flops, k_xattn_partial<false>, dim3(XA_NS, a.n_head), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_xattn_combine<XA_NS>, dim3(a.R, a.n_head), dim3(64), 0, s, a);
   WDR_HIP(hipGetLastError());
 }
 

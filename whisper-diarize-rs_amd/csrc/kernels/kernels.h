@@ -123,12 +123,8 @@ struct XAttnArgs {
   // byte count).  Null: every row its own group; without row_k one group of all R rows (k / v)
   const int* grp = nullptr;
   int n_grp = 0;
-  // split arrival counters of the in-launch combine, [groups][n_head] u32, zero at allocation
-  // (XATTN_CTR_WORDS per owner; every launch adds a multiple of the split count to each)
-  unsigned* ctr = nullptr;
 };
-constexpr int XATTN_GRP_MAX = 8;               // rows per group
-constexpr int XATTN_CTR_WORDS = 128 * 32;      // counters per owner: groups x heads
+constexpr int XATTN_GRP_MAX = 8;   // rows sharing one K/V without row_k
 inline unsigned long long* prof_attach(XAttnArgs& a) { return a.ts = prof_slot(); }
 void launch_xattn(const XAttnArgs& a, hipStream_t s);
 struct CaptureArgs {

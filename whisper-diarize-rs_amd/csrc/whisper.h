@@ -143,7 +143,6 @@ struct StepIO {
   f16* kc; f16* vc; long long layer_stride, seq_stride;   // KV pool (layer 0) and its strides
   const f16* xkv;                  // one cross-K/V slot for every row, or
   const f16* const* row_xkv;       // per-row slot bases (device array)
-  unsigned* xctr = nullptr;        // cross-attention arrival counters (XATTN_CTR_WORDS, zeroed)
   const int* grp = nullptr;        // row groups sharing a slot (XAttnArgs::grp), or null
   int n_grp = 0;
 };

@@ -372,7 +372,6 @@ struct PrefillBufs {
   float* fpart_o; float2* fpart_ml; float2* ml; float* cap; float* part_o; float2* part_ml;
   float* logits;
   int* h_rows;
-  unsigned* xctr;
 };
 
 struct State::Impl {
@@ -408,14 +407,14 @@ struct State::Impl {
   // encode-ahead language detection: its own prefill working set and the 100 language
   // logits of each slot's window 0 (pinned, written by the encode stream before `ready`)
   struct LangSet {
-    DevMem xd, hd, qkvd, attd, qx, mlpd, rows_tok, rows_pos, rows_seq, part_o, part_ml, logits, row_xkv, xctr;
+    DevMem xd, hd, qkvd, attd, qx, mlpd, rows_tok, rows_pos, rows_seq, part_o, part_ml, logits, row_xkv;
     const f16** h_xkv = nullptr;   // pinned [(S + 1)][kBatch] row cross-K/V bases, by first slot
   } lset;
   float* h_lang = nullptr;      // [(S + 1)][100]
   DevMem energy_d; int energy_cap = 0;
   const f16* xkv() const { return xkv_ring.as<f16>() + (size_t)cur * xkv_slot_elems; }
   // decoder
-  DevMem xd, hd, qkvd, attd, qx, mlpd, logits, work, tokout, ctl, ml, cap, part_o, part_ml, xctr;
+  DevMem xd, hd, qkvd, attd, qx, mlpd, logits, work, tokout, ctl, ml, cap, part_o, part_ml;
   DevMem rows_tok, rows_pos, rows_seq;
   DevMem beamc, kvpairs;       // beam candidates [NSEQ][BEAM_KMAX], KV reorder (src, dst) pairs
   BeamCand* h_beam = nullptr;
@@ -434,7 +433,7 @@ struct State::Impl {
   PrefillBufs pb_main{}, pb_dtw{};
   struct DtwSet {
     DevMem xd, hd, qkvd, attd, qx, mlpd, rows_tok, rows_pos, rows_seq, fpart_o, fpart_ml, ml, cap, part_o, part_ml,
-        nrm, xdtw, times, xctr;
+        nrm, xdtw, times;
   } dset;
   hipStream_t sd = nullptr;        // DTW stream
   hipEvent_t ev_sync = nullptr;    // decode-stream point the DTW stream waits for
@@ -470,13 +469,6 @@ struct State::Impl {
 
 static constexpr int kBatch = 4;     // encoder windows per encode-ahead launch (M = 6000 rows)
 static constexpr int kSlots = 16;    // in-flight segments in the cross-K/V ring
-
-// cross-attention arrival counters of one working set (kernels/attn.hip k_xattn_dec)
-static DevMem zeroed_ctr() {
-  DevMem c((size_t)XATTN_CTR_WORDS * 4);
-  WDR_HIP(hipMemset(c.p, 0, c.bytes));
-  return c;
-}
 
 static void alloc_enc(State::Impl::EncBufs& e, int nb, int d, int kp1) {
   e.nb = nb;
@@ -541,7 +533,6 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
   m.cap = DevMem((size_t)A * RMAX * 1500 * 4);
   m.part_o = DevMem((size_t)NSPLIT * NSEQ * m.H * 64 * 4);
   m.part_ml = DevMem((size_t)NSPLIT * NSEQ * m.H * sizeof(float2));
-  m.xctr = zeroed_ctr();
   m.fpart_o = DevMem((size_t)12 * 256 * m.H * 64 * 4);
   m.fpart_ml = DevMem((size_t)12 * m.H * 256 * sizeof(float2));
   m.beamc = DevMem(NSEQ * BEAM_KMAX * sizeof(BeamCand));
@@ -578,14 +569,13 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
     D.cap = DevMem((size_t)A * RMAX * 1500 * 4);
     D.part_o = DevMem((size_t)NSPLIT * NSEQ * m.H * 64 * 4);
     D.part_ml = DevMem((size_t)NSPLIT * NSEQ * m.H * sizeof(float2));
-    D.xctr = zeroed_ctr();
     D.nrm = DevMem((size_t)A * RMAX * 1500 * 4);
     D.xdtw = DevMem((size_t)RMAX * 1500 * 4);
     D.times = DevMem((RMAX + 8) * 4);
     m.pb_dtw = PrefillBufs{D.xd.as<float>(), D.hd.as<f16>(), D.qkvd.as<f16>(), D.attd.as<f16>(), D.qx.as<f16>(),
                         D.mlpd.as<f16>(), D.rows_tok.as<int>(), D.rows_pos.as<int>(), D.rows_seq.as<int>(),
                         D.fpart_o.as<float>(), D.fpart_ml.as<float2>(), D.ml.as<float2>(), D.cap.as<float>(),
-                        D.part_o.as<float>(), D.part_ml.as<float2>(), nullptr, nullptr, D.xctr.as<unsigned>()};
+                        D.part_o.as<float>(), D.part_ml.as<float2>(), nullptr, nullptr};
     // language detection: one kBatch-row step (SOT at position 0, one KV sequence and one
     // cross-K/V slot per window) per encode-ahead batch
     Impl::LangSet& G = m.lset;
@@ -600,7 +590,6 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
     G.rows_seq = DevMem(LB * 4);
     G.part_o = DevMem((size_t)NSPLIT * LB * m.H * 64 * 4);
     G.part_ml = DevMem((size_t)NSPLIT * LB * m.H * sizeof(float2));
-    G.xctr = zeroed_ctr();
     G.logits = DevMem((size_t)LB * m.V * 4);
     G.row_xkv = DevMem(LB * sizeof(void*));
     WDR_HIP(hipHostMalloc((void**)&G.h_xkv, (size_t)(kSlots + 1) * LB * sizeof(void*), hipHostMallocDefault));
@@ -631,8 +620,7 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
   m.pb_main = PrefillBufs{m.xd.as<float>(), m.hd.as<f16>(), m.qkvd.as<f16>(), m.attd.as<f16>(), m.qx.as<f16>(),
                        m.mlpd.as<f16>(), m.rows_tok.as<int>(), m.rows_pos.as<int>(), m.rows_seq.as<int>(),
                        m.fpart_o.as<float>(), m.fpart_ml.as<float2>(), m.ml.as<float2>(), m.cap.as<float>(),
-                       m.part_o.as<float>(), m.part_ml.as<float2>(), m.logits.as<float>(), m.h_rows,
-                       m.xctr.as<unsigned>()};
+                       m.part_o.as<float>(), m.part_ml.as<float2>(), m.logits.as<float>(), m.h_rows};
   // The persistent one-launch step is measured SLOWER than the per-kernel chain on MI355X
   // (2.7 vs ~1.7 ms per large-v3 step: in-launch all-to-all hand-offs cost 2.5-7 us each, more
   // than the ~1.2 us kernel boundaries they replace), so it is opt-in.
@@ -921,7 +909,7 @@ void State::top_up(int j) {
       StepIO io{G.xd.as<float>(), G.qkvd.as<f16>(), G.attd.as<f16>(), G.qx.as<f16>(), G.mlpd.as<f16>(),
                 G.logits.as<float>(), m.V, G.part_o.as<float>(), G.part_ml.as<float2>(), G.rows_tok.as<int>(),
                 G.rows_pos.as<int>(), G.rows_seq.as<int>(), m.kc, m.vc, (long long)m.nslot_tot * m.seq_stride,
-                m.seq_stride, nullptr, G.row_xkv.as<const f16*>(), G.xctr.as<unsigned>()};
+                m.seq_stride, nullptr, G.row_xkv.as<const f16*>()};
       decode_step_layers(ctx_, io, R, m.es);
       for (int r = 0; r < R; ++r)
         WDR_HIP(hipMemcpyAsync(m.h_lang + (size_t)((g0 + r) % m.S) * 100,
@@ -1025,7 +1013,6 @@ void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool c
     } else {
       XAttnArgs xa{b.qx, d, xk, xv, ldxkv, 1500, n, hp.n_text_head, scale, b.part_o,
                    b.part_ml, b.attd, d};
-      xa.ctr = b.xctr;
       launch_xattn(xa, st);
     }
     if (l_end < L && l == l_end - 1) break;   // capture-only pass: done after the last head layer
@@ -1067,7 +1054,7 @@ void State::decoder_step_body(int R) {
   StepIO io{m.xd.as<float>(), m.qkvd.as<f16>(), m.attd.as<f16>(), m.qx.as<f16>(), m.mlpd.as<f16>(),
             m.logits.as<float>(), m.V, m.part_o.as<float>(), m.part_ml.as<float2>(), m.rows_tok.as<int>(),
             m.rows_pos.as<int>(), m.rows_seq.as<int>(), m.kc, m.vc, (long long)m.nslot_tot * m.seq_stride,
-            m.seq_stride, m.xkv(), nullptr, m.xctr.as<unsigned>()};
+            m.seq_stride, m.xkv(), nullptr};
   decode_step_layers(ctx_, io, R, s_);
 }
 
@@ -1119,7 +1106,6 @@ void decode_step_layers(const Context& ctx, const StepIO& io, int R, hipStream_t
     launch_proj(P(io.attd, d, e.w_o, e.b_o, io.xd, d, d, d, EPI_F32_RESID), s);
     launch_proj(P(nullptr, d, e.w_xq, e.b_xq, io.qx, d, d, d, EPI_F16, e.ln2_g, e.ln2_b), s);
     XAttnArgs xa{io.qx, d, nullptr, nullptr, ldxkv, 1500, R, hp.n_text_head, scale, io.part_o, io.part_ml, io.attd, d};
-    xa.ctr = io.xctr;
     xa.grp = io.grp;
     xa.n_grp = io.n_grp;
     if (io.row_xkv) {
@@ -2267,7 +2253,7 @@ struct StepBatcher::Impl {
   hipStream_t s = nullptr;
   int d = 0, V = 0, H = 0;
   DevMem xd, qkvd, attd, qx, mlpd, logits, work, tokout, ctl, rows_tok, rows_pos, rows_seq, row_xkv, part_o, part_ml;
-  DevMem xctr, grp, beamc;
+  DevMem grp, beamc;
   int* h_rows = nullptr;          // [4][RB]: tokens, positions, sequences, group sizes
   LogitsCtl* h_ctl = nullptr;
   const f16** h_xkv = nullptr;
@@ -2306,7 +2292,6 @@ StepBatcher::StepBatcher(Context& ctx) : ctx_(ctx), m_(new Impl) {
   m.row_xkv = DevMem(RB * sizeof(void*));
   m.part_o = DevMem((size_t)NSPLIT * RB * m.H * 64 * 4);
   m.part_ml = DevMem((size_t)NSPLIT * RB * m.H * sizeof(float2));
-  m.xctr = zeroed_ctr();
   m.grp = DevMem(RB * 4);
   m.beamc = DevMem((size_t)RB * BEAM_KMAX * sizeof(BeamCand));
   WDR_HIP(hipHostMalloc((void**)&m.h_beam, (size_t)RB * BEAM_KMAX * sizeof(BeamCand), hipHostMallocDefault));
@@ -2427,8 +2412,7 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
   StepIO io{m.xd.as<float>(), m.qkvd.as<f16>(), m.attd.as<f16>(), m.qx.as<f16>(), m.mlpd.as<f16>(),
             m.logits.as<float>(), m.V, m.part_o.as<float>(), m.part_ml.as<float2>(), m.rows_tok.as<int>(),
             m.rows_pos.as<int>(), m.rows_seq.as<int>(), ctx_.kv_k.as<f16>(), ctx_.kv_v.as<f16>(),
-            (long long)ctx_.max_chains * NSLOT * seq_stride, seq_stride, nullptr, m.row_xkv.as<const f16*>(),
-            m.xctr.as<unsigned>()};
+            (long long)ctx_.max_chains * NSLOT * seq_stride, seq_stride, nullptr, m.row_xkv.as<const f16*>()};
   if (grouped) {
     io.grp = m.grp.as<int>();
     io.n_grp = (int)batch.size();
