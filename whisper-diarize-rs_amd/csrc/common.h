@@ -89,15 +89,21 @@ struct ProjArgs {
 // Live kernel clock (csrc/prof.cpp): a launch the profiler samples carries ts -> {earliest wave
 // start, latest wave end} in wall_clock64() ticks (the constant-rate clock), i.e. the span
 // rocprofv3's dispatch timestamps measure, free of the queueing that HIP start/stop events of a
-// launch absorb under multi-stream concurrency.  Lane 0 of every wave stamps with vector
-// atomics; unsampled launches (ts null) skip it.
+// launch absorb under multi-stream concurrency.  The first wave of every workgroup stamps the
+// start, lane 0 of every wave the end, with vector atomics spread over PROF_CLK_LANES words;
+// unsampled launches (ts null) skip it.
+constexpr int PROF_CLK_LANES = 32;   // stamp addresses per sampled launch (csrc/prof.cpp ring)
 struct ProfClock {
   unsigned long long* ts;
   __device__ __forceinline__ explicit ProfClock(unsigned long long* t) : ts(t) {
-    if (ts && (threadIdx.x & 63) == 0) atomicMin(ts, (unsigned long long)wall_clock64());
+    // a workgroup's waves start together: its first wave stamps the start
+    if (ts && threadIdx.x == 0) atomicMin(ts + lane_of_block(), (unsigned long long)wall_clock64());
   }
   __device__ __forceinline__ ~ProfClock() {
-    if (ts && (threadIdx.x & 63) == 0) atomicMax(ts + 1, (unsigned long long)wall_clock64());
+    if (ts && (threadIdx.x & 63) == 0) atomicMax(ts + PROF_CLK_LANES + lane_of_block(), (unsigned long long)wall_clock64());
+  }
+  __device__ __forceinline__ static int lane_of_block() {
+    return (int)((blockIdx.x + blockIdx.y * 7u + blockIdx.z * 13u) % PROF_CLK_LANES);
   }
 };
 unsigned long long* prof_slot();   // next clock slot of the sampled-launch ring (null when full)

@@ -41,16 +41,20 @@ struct Acc {
   long long clk_n = 0;
 } g_acc[kClasses];
 
-// kernel-clock ring: {start, end} u64 pairs, initialised to {~0, 0}; slots are handed out in
-// order and read back (with a device synchronisation) only at drain time
-constexpr long long kRing = 1 << 20;
+// kernel-clock ring: per slot PROF_CLK_LANES start words (init ~0) then PROF_CLK_LANES end words
+// (init 0) -- workgroups stamp lane (block id % PROF_CLK_LANES), so the atomics of a
+// many-workgroup launch spread over that many addresses instead of serialising on one (which
+// inflated a 7680-workgroup launch by hundreds of us); slots are handed out in order and read
+// back (with a device synchronisation) only at drain time
+constexpr long long kSlotWords = 2 * PROF_CLK_LANES;
+constexpr long long kRing = 1 << 16;
 unsigned long long* g_ring = nullptr;
 std::atomic<long long> g_next{0};
 double g_tick_ms = 0.0;   // wall_clock64 period in ms
 
 void ring_reset_locked() {
   if (!g_ring) {
-    if (hipMalloc(&g_ring, (size_t)kRing * 16) != hipSuccess) {
+    if (hipMalloc(&g_ring, (size_t)kRing * kSlotWords * 8) != hipSuccess) {
       (void)hipGetLastError();
       g_ring = nullptr;
       return;
@@ -60,11 +64,12 @@ void ring_reset_locked() {
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
     g_tick_ms = 1.0 / (double)khz;
   }
-  std::vector<unsigned long long> init((size_t)kRing * 2);
-  for (long long i = 0; i < kRing; ++i) {
-    init[2 * i] = ~0ull;
-    init[2 * i + 1] = 0ull;
-  }
+  std::vector<unsigned long long> init((size_t)kRing * kSlotWords);
+  for (long long i = 0; i < kRing; ++i)
+    for (int j = 0; j < PROF_CLK_LANES; ++j) {
+      init[i * kSlotWords + j] = ~0ull;
+      init[i * kSlotWords + PROF_CLK_LANES + j] = 0ull;
+    }
   if (hipMemcpy(g_ring, init.data(), init.size() * 8, hipMemcpyHostToDevice) != hipSuccess) (void)hipGetLastError();
   g_next = 0;
 }
@@ -84,7 +89,7 @@ void drain_locked(bool read_ring = true) {
   }
   g_pending.clear();
   if (!read_ring || g_clk_pending.empty() || !g_ring) return;
-  std::vector<unsigned long long> ring((size_t)std::min<long long>(g_next.load(), kRing) * 2);
+  std::vector<unsigned long long> ring((size_t)std::min<long long>(g_next.load(), kRing) * kSlotWords);
   if (hipDeviceSynchronize() != hipSuccess ||
       hipMemcpy(ring.data(), g_ring, ring.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) {
     (void)hipGetLastError();
@@ -92,8 +97,12 @@ void drain_locked(bool read_ring = true) {
     return;
   }
   for (auto& r : g_clk_pending) {
-    if ((size_t)(2 * r.slot + 1) >= ring.size()) continue;
-    const unsigned long long t0 = ring[2 * r.slot], t1 = ring[2 * r.slot + 1];
+    if ((size_t)((r.slot + 1) * kSlotWords) > ring.size()) continue;
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (int j = 0; j < PROF_CLK_LANES; ++j) {
+      t0 = std::min(t0, ring[r.slot * kSlotWords + j]);
+      t1 = std::max(t1, ring[r.slot * kSlotWords + PROF_CLK_LANES + j]);
+    }
     if (t0 == ~0ull || t1 < t0) continue;
     Acc& A = g_acc[r.cls];
     A.clk_ms += (double)(t1 - t0) * g_tick_ms;
@@ -108,7 +117,7 @@ void drain_locked(bool read_ring = true) {
 unsigned long long* prof_slot() {
   if (!g_ring) return nullptr;
   const long long i = g_next++;
-  return i < kRing ? g_ring + 2 * i : nullptr;
+  return i < kRing ? g_ring + kSlotWords * i : nullptr;
 }
 
 // WDR_SEGV_TRACE=1: a fatal signal prints the faulting address, the thread and the native
@@ -184,7 +193,7 @@ hipEvent_t prof_event() {
 void prof_push(int cls, hipEvent_t a, hipEvent_t b, unsigned long long* ts, double bytes, double flops) {
   std::lock_guard<std::mutex> l(g_mu);
   g_pending.push_back({a, b, cls});
-  if (ts && g_ring) g_clk_pending.push_back({(long long)((ts - g_ring) / 2), cls, bytes, flops});
+  if (ts && g_ring) g_clk_pending.push_back({(long long)((ts - g_ring) / kSlotWords), cls, bytes, flops});
   g_acc[cls].bytes += bytes;
   g_acc[cls].flops += flops;
   g_acc[cls].n++;
