@@ -285,6 +285,11 @@ void wdr_segment_list_free(wdr_segment_list* l);
  * prompt-chain fix-up (results identical to one chain).  Default WDR_DECODE_CHAINS or 16,
  * capped by the context's KV pool (max chains fixed at creation).  Not in the Rust API. */
 int wdr_context_set_chains(wdr_context* c, int32_t n);
+/* GPUs the context runs on: gpu_device Some(d) -> 1 (device d); None -> every visible GPU (up to
+ * 8; WDR_DEVICES="a,b,.." lists them), each holding the model, the decode chains spread over
+ * them (chain k on GPU k % n) with the same exact prompt fix-up; device_ids (nullable) receives
+ * the ordinals, at most `cap` */
+int wdr_context_devices(const wdr_context* c, int32_t* n, int32_t* device_ids, int32_t cap);
 /* test seam: early prompt fix-up 0 off, 1 when the predecessor chain already finished (default),
  * 2 always (chain k waits for chain k-1, then redoes its first segments from the known prompt);
  * -1 restores the WDR_EARLY_FIXUP environment default */

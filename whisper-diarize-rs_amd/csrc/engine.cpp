@@ -223,8 +223,12 @@ static std::vector<Word> interpolate_word_timestamps(const std::string& line, do
 struct wdr_context {
   std::unique_ptr<Context> ctx;
   std::unique_ptr<State> st;
-  std::vector<std::unique_ptr<State>> chain_st;   // decode chains 1.. (multi-chain pipeline)
-  int chains = 1;                                 // decode chains per run_pipeline call
+  // gpu_device None (src/engine.rs:14): every visible GPU.  peers[g - 1] is the
+  // model on device devices[g]; decode chain k runs on GPU k % G (chain k / G of its pool)
+  std::vector<int> devices;
+  std::vector<std::unique_ptr<Context>> peers;
+  std::map<int, std::unique_ptr<State>> chain_st; // decode chains 1.. (multi-chain pipeline)
+  int chains = 1;                                 // decode chains per GPU and run_pipeline call
   // early prompt fix-up: 0 off, 1 when the predecessor chain has already finished (default;
   // WDR_EARLY_FIXUP=0 turns it off), 2 always (a chain waits for its predecessor: test seam)
   int early_fixup = -1;
@@ -482,10 +486,32 @@ static std::unique_ptr<wdr_context> make_context(const std::string& model_name, 
   cp.weight_std = syn.weight_std;
   cp.emb_std = syn.emb_std;
   auto c = std::make_unique<wdr_context>();
+  // the GPUs: the one named, or (None) every visible one -- WDR_DEVICES="0,0" lists them
+  // explicitly (two models on one GPU exercise the multi-GPU path on a one-GPU machine)
+  if (has_dev) {
+    c->devices = {dev};
+  } else if (const char* e = getenv("WDR_DEVICES")) {
+    for (const char* q = e; *q;) {
+      c->devices.push_back(atoi(q));
+      while (*q && *q != ',') ++q;
+      if (*q == ',') ++q;
+    }
+  } else {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n < 1) n = 1;
+    for (int g = 0; g < std::min(n, 8); ++g) c->devices.push_back(g);
+  }
+  WDR_CHECK(!c->devices.empty(), "no GPU device");
+  cp.gpu_device = c->devices[0];
   const double t = now_s();
   try {
     c->ctx = std::make_unique<Context>(model_name, hp, cp, gf.get());
     c->st = std::make_unique<State>(*c->ctx);
+    for (size_t g = 1; g < c->devices.size(); ++g) {
+      ContextParams pc = cp;
+      pc.gpu_device = c->devices[g];
+      c->peers.push_back(std::make_unique<Context>(model_name, hp, pc, gf.get()));
+    }
     c->chains = c->ctx->max_chains;   // WDR_DECODE_CHAINS (default 16), wdr_context_set_chains
   } catch (const std::exception& ex) {
     throw std::runtime_error(std::string("create whisper context crash: ") + ex.what());
@@ -649,9 +675,16 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
                                          const wdr_transcribe_options* o, const FullParams& params, int C,
                                          const wdr_callbacks* cb, const std::string& rng0) {
   const size_t N = segs.size();
-  while ((int)c->chain_st.size() < C - 1)
-    c->chain_st.push_back(std::make_unique<State>(*c->ctx, (int)c->chain_st.size() + 1));
-  auto state = [&](int k) -> State& { return k == 0 ? *c->st : *c->chain_st[k - 1]; };
+  const int G = (int)c->devices.size();
+  // chain k: GPU k % G, chain k / G of that GPU's KV pool (a fixed mapping, so states persist)
+  auto ctx_of = [&](int k) -> Context& { return k % G == 0 ? *c->ctx : *c->peers[k % G - 1]; };
+  for (int k = 1; k < C; ++k)
+    if (!c->chain_st.count(k)) {
+      WDR_HIP(hipSetDevice(c->devices[k % G]));
+      c->chain_st[k] = std::make_unique<State>(ctx_of(k), k / G);
+    }
+  auto state = [&](int k) -> State& { return k == 0 ? *c->st : *c->chain_st.at(k); };
+  auto on_gpu = [&](int k) { WDR_HIP(hipSetDevice(c->devices[k % G])); };
   const bool auto_lang = !o || !o->lang || std::string(o->lang).empty() || std::string(o->lang) == "auto";
   // contiguous blocks balanced by estimated decode cost (each chain at least one segment):
   // tokens grow with the segment's duration, plus a per-segment overhead (prompt prefill,
@@ -677,9 +710,18 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
   std::atomic<bool> stop{false};
   std::vector<std::exception_ptr> errs(C);
   c->cs.chains = C;
-  StepBatcher& sb = c->ctx->step_batcher();
-  const long long l0 = sb.launches, r0 = sb.rows;
-  const double s0 = sb.step_s;
+  auto batch_stats = [&](long long* l, long long* r, double* t) {
+    *l = 0, *r = 0, *t = 0;
+    for (int g = 0; g < std::min(G, C); ++g) {
+      StepBatcher& sb = (g == 0 ? *c->ctx : *c->peers[g - 1]).step_batcher();
+      *l += sb.launches;
+      *r += sb.rows;
+      *t = std::max(*t, sb.step_s);
+    }
+  };
+  long long l0, r0;
+  double s0;
+  batch_stats(&l0, &r0, &s0);
   const double t_spec = now_s();
   // dec_in[k]: the prompt chain k's first segment was last decoded from
   std::vector<Prompt> dec_in(C, e0);
@@ -687,6 +729,7 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
   // re-decode block k from prompt e, segment by segment, until the prompt leaving a segment
   // equals the one its successor was decoded from (used by the early and the round fix-ups)
   auto redo_block = [&](int k, const Prompt& e_in, bool batched, std::atomic<long long>* count) {
+    on_gpu(k);
     State& st = state(k);
     const size_t a = cut[k], b = cut[k + 1];
     st.batched = batched;
@@ -718,6 +761,7 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
   auto worker = [&](int k) {
     State& st = state(k);
     try {
+      on_gpu(k);
       const size_t a = cut[k], b = cut[k + 1];
       st.times = StageTimes{};
       st.set_rng_state(rng0);
@@ -863,6 +907,7 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
     }
   const size_t rs = (f < N && !out[f].rng_clean) ? f : f + 1;
   if (rs < N) {
+    on_gpu(0);
     State& st = *c->st;
     Prompt e = e0;
     for (size_t i = 0; i < rs; ++i) e = next_prompt(e, out[i].res);
@@ -882,9 +927,14 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
     }
   }
   c->cs.fixup_s = now_s() - t_fix;
-  c->cs.launches = sb.launches - l0;
-  c->cs.rows = sb.rows - r0;
-  c->cs.step_s = sb.step_s - s0;
+  {
+    long long l1, r1;
+    double s1;
+    batch_stats(&l1, &r1, &s1);
+    c->cs.launches = l1 - l0;
+    c->cs.rows = r1 - r0;
+    c->cs.step_s = s1 - s0;
+  }
   // stage accounting: chains' times summed into the context's state
   for (int k = 1; k < C; ++k) {
     const StageTimes& t = state(k).times;
@@ -942,8 +992,10 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
   // decode chains: greedy and beam search at t = 0 (their steps batch across chains; t > 0
   // decoders from the first window on keep one chain)
   const int C = (params.temperature <= 0.f)
-                    ? std::max(1, std::min({c->chains, c->ctx->max_chains, (int)segs.size()}))
+                    ? std::max(1, std::min({c->chains * (int)c->devices.size(),
+                                            c->ctx->max_chains * (int)c->devices.size(), (int)segs.size()}))
                     : 1;
+  WDR_HIP(hipSetDevice(c->devices[0]));
   // every segment's PCM goes to the encode-ahead ring up front (int16 -> f32 on the GPU,
   // the same x / 32768 as src/transcribe.rs's conversion); multi-chain: per chain block
   // the reference creates a fresh whisper state per pipeline call (src/transcribe.rs:335):
@@ -1686,6 +1738,14 @@ int wdr_dbg_set_early_fixup(wdr_context* c, int32_t mode) {
   WDR_GUARD({
     if (mode < -1 || mode > 2) return fail("early fix-up mode: -1 (env default), 0, 1 or 2");
     c->early_fixup = mode;
+    return 0;
+  })
+}
+
+int wdr_context_devices(const wdr_context* c, int32_t* n, int32_t* device_ids, int32_t cap) {
+  WDR_GUARD({
+    *n = (int32_t)c->devices.size();
+    for (int32_t i = 0; device_ids && i < cap && i < *n; ++i) device_ids[i] = c->devices[i];
     return 0;
   })
 }

@@ -636,9 +636,18 @@ class WhisperContext:
         segs, lang, index = _segments(out, True)
         return segs, lang, index or [], [bool(sampled[i]) for i in range(len(speech_segments))], rng_out
 
+    @property
+    def devices(self) -> List[int]:
+        """GPU ordinals this context runs on (wdr_context_devices): gpu_device=None -> every
+        visible GPU, the decode chains spread over them."""
+        n = C.c_int32()
+        ids = (C.c_int32 * 8)()
+        L.check(self._lib.wdr_context_devices(self.h, C.byref(n), ids, 8))
+        return [ids[i] for i in range(min(n.value, 8))]
+
     def set_chains(self, n: int):
-        """Decode chains for greedy run_pipeline calls (wdr_context_set_chains): n blocks of the
-        speech segments decoded concurrently with batched steps, exact prompt fix-up."""
+        """Decode chains per GPU for run_pipeline calls (wdr_context_set_chains): n blocks of the
+        speech segments per GPU decoded concurrently with batched steps, exact prompt fix-up."""
         L.check(self._lib.wdr_context_set_chains(self.h, int(n)))
 
     def set_early_fixup(self, mode: int):

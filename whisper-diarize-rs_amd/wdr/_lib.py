@@ -142,6 +142,7 @@ _SIGS = {
                                          P(C.c_void_p), P(P(SegmentList))]),
     "wdr_segment_list_free": (None, [P(SegmentList)]),
     "wdr_context_set_chains": (C.c_int, [vp, i32]),
+    "wdr_context_devices": (C.c_int, [vp, P(i32), P(i32), i32]),
     "wdr_dbg_set_early_fixup": (C.c_int, [vp, i32]),
     "wdr_ggml_info": (C.c_int, [cstr, P(i32), P(i64), P(i64)]),
     "wdr_dbg_batch_step": (C.c_int, [vp, P(i32), sz, i32, i32, P(f64)]),
