@@ -41,6 +41,7 @@ sys.path.insert(0, os.path.join(ROOT, "whisper-diarize-rs_amd"))
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_F16_PEAK_TFS = 2500.0  # dense f16/bf16 MFMA
+MFMA_FP8_PEAK_TFS = 5000.0  # dense block-scaled fp8 MFMA (MI355X_MICROARCH.md, matrix cores)
 PROF_SAMPLE = 8             # csrc/prof.cpp kEvery (launches) and kStepEvery (steps)
 
 
@@ -58,6 +59,7 @@ def parse():
                     help="segmentation stage: pyannote diarization (default) or Silero VAD")
     ap.add_argument("--strategy", default="greedy", choices=["greedy", "beam"],
                     help="greedy (configs[2]) or the reference's default beam search, 5 beams")
+    ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3) encoder GEMMs (configs[4])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-audio", type=float, default=60.0,
                     help="audio seconds of the workload the CPU baseline is extrapolated over (rank 0, N=1)")
@@ -218,6 +220,8 @@ def main():
     syn = wdr.Synthetic(weight_std=0.02, emb_std=0.02, force_len_rate=3.3, disable_fallback=True)
     t_load = time.perf_counter()
     ctx = wdr.WhisperContext(args.model, gpu_device=local, enable_dtw=True, synthetic=syn)
+    if args.fp8:
+        ctx.set_encoder_fp8(True)
     t_load = time.perf_counter() - t_load
     opts = wdr.TranscribeOptions(model=args.model, lang="auto", enable_vad=not diarize,
                                  enable_diarize=True if diarize else None,
@@ -326,8 +330,10 @@ def main():
             continue
         if c in ("gemm", "flash"):
             ach = fl / (ms * 1e-3) / 1e12
-            r = {"kernel": c, "bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_F16_PEAK_TFS,
-                 "unit": "TFLOP/s", "frac": round(ach / MFMA_F16_PEAK_TFS, 4), "flops_per_launch": fl / nl}
+            # --fp8: the encoder GEMMs run the block-scaled fp8 MFMA, dense peak 5 PF/s
+            pk = MFMA_FP8_PEAK_TFS if (args.fp8 and c == "gemm") else MFMA_F16_PEAK_TFS
+            r = {"kernel": c, "bound": "mfma", "achieved": round(ach, 2), "peak": pk,
+                 "unit": "TFLOP/s", "frac": round(ach / pk, 4), "flops_per_launch": fl / nl}
         else:
             ach = by / (ms * 1e-3) / 1e9
             r = {"kernel": c, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
@@ -364,8 +370,9 @@ def main():
             "metric": "audio-sec/wall-sec (xRT), large-v3 + DTW + diarize, 1/2/4/8 MI355X",
             "value": round(value, 3), "unit": "audio-sec/wall-sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt_max * 1e3 / args.steps, 1), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f16 (f32 accumulate)", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": ("fp8 e4m3 encoder GEMMs, f16 elsewhere (f32 accumulate)" if args.fp8 else "f16 (f32 accumulate)"), "data": "synthetic",
             "config": {"strategy": "greedy" if args.strategy == "greedy" else "beam search, 5 beams (reference default)",
+                       "encoder_gemms": "fp8 e4m3 (configs[4])" if args.fp8 else "f16",
                        "workload": ("configs[3] per-GPU shard with configs[2]'s greedy decode: %s + DTW + diarize "
                                     "(pyannote segmentation-3.0 run + timed, CAM++ embeddings + speaker assignment), "
                                     "%.0f s synthetic audio per rank (%d segments, %.0f s speech, 3 speakers), lang auto, "

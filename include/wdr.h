@@ -290,6 +290,11 @@ int wdr_context_set_chains(wdr_context* c, int32_t n);
  * them (chain k on GPU k % n) with the same exact prompt fix-up; device_ids (nullable) receives
  * the ordinals, at most `cap` */
 int wdr_context_devices(const wdr_context* c, int32_t* n, int32_t* device_ids, int32_t cap);
+/* fp8 (OCP e4m3) encoder GEMMs (BASELINE configs[4]): projections and cross-K/V on the block-scaled
+ * fp8 MFMA, activations quantised per row and weights per output channel (made on first use);
+ * LayerNorm, attention, residuals and the decoder stay f16/f32.  Default off (WDR_FP8_ENCODER=1
+ * turns it on at creation).  Not in the Rust API. */
+int wdr_context_set_encoder_fp8(wdr_context* c, int8_t on);
 /* test seam: early prompt fix-up 0 off, 1 when the predecessor chain already finished (default),
  * 2 always (chain k waits for chain k-1, then redoes its first segments from the known prompt);
  * -1 restores the WDR_EARLY_FIXUP environment default */
@@ -348,6 +353,12 @@ int wdr_dbg_dtw(const float* cap, int32_t n_heads, int32_t n_tok, int32_t n_audi
                 float* x_out /* [n_tok-sot_len-1][n_audio] */, int32_t* times_out, int32_t* n_times);
 int wdr_dbg_discrete(const float* w, size_t n, uint32_t seed, int32_t n_draws, int32_t* out);
 int wdr_dbg_dtw_dp(const float* x, int32_t rows, int32_t cols, int32_t seek, int32_t* times_out, int32_t* n_times);
+/* fp8 (e4m3) encoder projection (BASELINE configs[4]): per-row quantisation of a [M][K] and
+ * w [N][K] on the GPU, the block-scaled fp8 MFMA GEMM, epilogue as wdr_dbg_proj; the quantised
+ * bytes / scales are returned (nullable) for the reference product */
+int wdr_dbg_proj_fp8(const uint16_t* a_f16, const uint16_t* w_f16, const float* bias, int32_t M, int32_t N, int32_t K,
+                     int32_t epi, float* out, uint8_t* a8_out, float* a_scale_out, uint8_t* w8_out,
+                     float* w_scale_out);
 int wdr_dbg_proj(const uint16_t* a_f16, const uint16_t* w_f16, const float* bias, int32_t M, int32_t N, int32_t K,
                  int32_t epi, float* out /* [M][N] f32 (f16 epilogues are widened) */);
 /* epi | WDR_DBG_PROJ_STEP selects the decode-step GEMV schedule (M <= 16 rows) */

@@ -240,3 +240,64 @@ def test_dtw_preprocessing_bit_exact(lib):
     xr = odtw.alignment_matrix(cap, 2 * n_audio, sot_len)
     np.testing.assert_array_equal(x, xr)
     assert list(t[:nt.value]) == odtw.token_times(xr, 200)
+
+
+def _e4m3_decode(b):
+    """OCP e4m3fn byte -> float (sign, 4-bit exponent bias 7, 3-bit mantissa, no infinities)."""
+    b = np.asarray(b, np.uint8).astype(np.int32)
+    s = np.where(b & 0x80, -1.0, 1.0)
+    e = (b >> 3) & 0xF
+    m = (b & 7).astype(np.float64)
+    v = np.where(e == 0, m / 8.0 * 2.0 ** -6, (1 + m / 8.0) * 2.0 ** (e - 7))
+    v = np.where((e == 15) & ((b & 7) == 7), np.nan, v)
+    return s * v
+
+
+def _e4m3_grid():
+    g = _e4m3_decode(np.arange(256))
+    return np.unique(g[np.isfinite(g)])
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(300, 256, 256, 3), (1500, 1280, 1280, 2), (777, 3840, 1280, 0),
+                                       (600, 1280, 5120, 2), (256, 5120, 1280, 1)])
+def test_fp8_projection(lib, M, N, K, epi):
+    """fp8 encoder GEMM (BASELINE configs[4]): the per-row e4m3 quantisation is round-to-nearest
+    onto the e4m3 grid at scale max|row| / 448, and the GEMM output equals the fp64 product of
+    the dequantised operands (scales applied in the epilogue) within f32 accumulation error,
+    for both tile widths (N = 1280: 128-column tiles) and every epilogue."""
+    rng = np.random.default_rng(M + N + K)
+    a = (rng.standard_normal((M, K)) * rng.uniform(0.1, 3.0, (M, 1))).astype(np.float16)
+    w = (rng.standard_normal((N, K)) * 0.05).astype(np.float16)
+    bias = (rng.standard_normal(N) * 0.1).astype(np.float32)
+    base = rng.standard_normal((M, N)).astype(np.float32)
+    out = base.copy() if epi == 2 else np.zeros((M, N), np.float32)
+    a8, w8 = np.zeros((M, K), np.uint8), np.zeros((N, K), np.uint8)
+    asc, wsc = np.zeros(M, np.float32), np.zeros(N, np.float32)
+    U8 = C.POINTER(C.c_uint8)
+    _lib.check(lib.wdr_dbg_proj_fp8(a.view(np.uint16).ctypes.data_as(U16), w.view(np.uint16).ctypes.data_as(U16),
+                                    bias.ctypes.data_as(F32), M, N, K, epi, out.ctypes.data_as(F32),
+                                    a8.ctypes.data_as(U8), asc.ctypes.data_as(F32), w8.ctypes.data_as(U8),
+                                    wsc.ctypes.data_as(F32)))
+    # quantisation: scale and nearest grid point (ties may go either way: within half a step)
+    np.testing.assert_allclose(asc, np.abs(a.astype(np.float32)).max(1) / 448, rtol=1e-6)
+    grid = _e4m3_grid()
+    x = a.astype(np.float64) / asc[:, None].astype(np.float64)
+    q = _e4m3_decode(a8)
+    idx = np.clip(np.searchsorted(grid, x), 1, len(grid) - 1)
+    nearest = np.minimum(np.abs(grid[idx] - x), np.abs(grid[idx - 1] - x))
+    # x is computed here in f64 (the kernel multiplies by 448 / amax in f32): near-ties may round
+    # to the other neighbour
+    excess = np.abs(q - x) - nearest
+    bad = excess > 1e-5 * np.maximum(np.abs(x), 1.0)
+    assert not bad.any(), (int(bad.sum()), float(excess.max()), x[bad][:5], q[bad][:5])
+    # GEMM on the dequantised operands
+    A = _e4m3_decode(a8) * asc[:, None]
+    W = _e4m3_decode(w8) * wsc[:, None]
+    ref = A @ W.T + bias
+    want = {0: ref, 1: _gelu(ref), 2: base + ref, 3: ref}[epi]
+    tol = dict(rtol=2e-3, atol=2e-3) if epi in (0, 1) else dict(rtol=0, atol=1e-4 * np.abs(A).max() * np.abs(W).max() * K ** 0.5 + 1e-4)
+    np.testing.assert_allclose(out, want, **tol)
+    # and close to the f16 product (the quantisation error, e4m3 has 3 mantissa bits)
+    f16ref = a.astype(np.float64) @ w.T.astype(np.float64) + bias
+    rel = np.linalg.norm(ref - f16ref) / np.linalg.norm(f16ref)
+    assert rel < 0.06, rel

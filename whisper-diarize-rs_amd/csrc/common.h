@@ -84,6 +84,10 @@ struct ProjArgs {
   // per-row arithmetic does not depend on the row count
   int step_rows = 0;
   unsigned long long* ts = nullptr;   // live kernel clock of a sampled launch (ProfClock)
+  // fp8 (OCP e4m3) operands (launch_proj_fp8): A8 [M][lda] and B8 [N][ldb] bytes, dequantised
+  // in the epilogue by a_scale[row] * b_scale[col] (per-row / per-output-channel scales)
+  const uint8_t* A8 = nullptr; const uint8_t* B8 = nullptr;
+  const float* a_scale = nullptr; const float* b_scale = nullptr;
 };
 
 // Live kernel clock (csrc/prof.cpp): a launch the profiler samples carries ts -> {earliest wave
@@ -111,6 +115,11 @@ template <typename A>
 inline unsigned long long* prof_attach(A&) { return nullptr; }
 inline unsigned long long* prof_attach(ProjArgs& a) { return a.ts = prof_slot(); }
 void launch_proj(const ProjArgs& a, hipStream_t s);   // picks GEMV (M<=8) or MFMA GEMM
+// fp8 encoder GEMM (BASELINE configs[4]): ProjArgs::A8 / B8 / a_scale / b_scale, M > 64,
+// N % 128 == 0, K % 128 == 0; epilogues as launch_proj
+void launch_proj_fp8(const ProjArgs& a, hipStream_t s);
+// per-row fp8 quantisation: y[r][0..K) = e4m3(x[r][k] / scale[r]), scale[r] = max_k |x[r][k]| / 448
+void launch_quant_rows(const f16* x, int ldx, int M, int K, uint8_t* y, int ldy, float* scale, hipStream_t s);
 // the LayerNorm prologue of a decode-step projection as its own launch (k_dgemv's arithmetic):
 // rows ln_x -> y [M][ldy] f16
 void launch_ln_rows(const ProjArgs& a, f16* y, int ldy, hipStream_t s);

@@ -1742,6 +1742,14 @@ int wdr_dbg_set_early_fixup(wdr_context* c, int32_t mode) {
   })
 }
 
+int wdr_context_set_encoder_fp8(wdr_context* c, int8_t on) {
+  WDR_GUARD({
+    c->ctx->fp8_encoder = on != 0;
+    for (auto& p : c->peers) p->fp8_encoder = on != 0;
+    return 0;
+  })
+}
+
 int wdr_context_devices(const wdr_context* c, int32_t* n, int32_t* device_ids, int32_t cap) {
   WDR_GUARD({
     *n = (int32_t)c->devices.size();
@@ -1924,6 +1932,43 @@ int wdr_dbg_dtw_dp(const float* x, int32_t rows, int32_t cols, int32_t seek, int
     WDR_HIP(hipMemcpy(t.data(), dt.p, t.size() * 4, hipMemcpyDeviceToHost));
     *n_times = t[rows + 4];
     for (int i = 0; i < *n_times; ++i) times_out[i] = t[i];
+    return 0;
+  })
+}
+
+// fp8 encoder projection: a, w quantised per row on the GPU (launch_quant_rows), the fp8 GEMM
+// with the epilogue `epi` (out f32 in / out, as wdr_dbg_proj); the quantised bytes and scales
+// come back for the reference product
+int wdr_dbg_proj_fp8(const uint16_t* a16, const uint16_t* w16, const float* bias, int32_t M, int32_t N, int32_t K,
+                     int32_t epi, float* out, uint8_t* a8_out, float* a_scale_out, uint8_t* w8_out, float* w_scale_out) {
+  WDR_GUARD({
+    DevMem da((size_t)M * K * 2), dw((size_t)N * K * 2), db(bias ? (size_t)N * 4 : 0), dout((size_t)M * N * 4);
+    DevMem a8((size_t)M * K), w8((size_t)N * K), as((size_t)M * 4), ws((size_t)N * 4);
+    WDR_HIP(hipMemcpy(da.p, a16, da.bytes, hipMemcpyHostToDevice));
+    WDR_HIP(hipMemcpy(dw.p, w16, dw.bytes, hipMemcpyHostToDevice));
+    if (bias) WDR_HIP(hipMemcpy(db.p, bias, db.bytes, hipMemcpyHostToDevice));
+    launch_quant_rows(da.as<f16>(), K, M, K, a8.as<uint8_t>(), K, as.as<float>(), nullptr);
+    launch_quant_rows(dw.as<f16>(), K, N, K, w8.as<uint8_t>(), K, ws.as<float>(), nullptr);
+    const bool f16out = epi == EPI_F16 || epi == EPI_F16_GELU;
+    if (!f16out) WDR_HIP(hipMemcpy(dout.p, out, dout.bytes, hipMemcpyHostToDevice));
+    ProjArgs p{nullptr, K, nullptr, K, bias ? db.as<float>() : nullptr, dout.p, N, nullptr, 0, M, N, K, epi};
+    p.A8 = a8.as<uint8_t>();
+    p.B8 = w8.as<uint8_t>();
+    p.a_scale = as.as<float>();
+    p.b_scale = ws.as<float>();
+    launch_proj_fp8(p, nullptr);
+    WDR_HIP(hipDeviceSynchronize());
+    if (f16out) {
+      std::vector<f16> h((size_t)M * N);
+      WDR_HIP(hipMemcpy(h.data(), dout.p, h.size() * 2, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < h.size(); ++i) out[i] = (float)h[i];
+    } else {
+      WDR_HIP(hipMemcpy(out, dout.p, dout.bytes, hipMemcpyDeviceToHost));
+    }
+    if (a8_out) WDR_HIP(hipMemcpy(a8_out, a8.p, a8.bytes, hipMemcpyDeviceToHost));
+    if (a_scale_out) WDR_HIP(hipMemcpy(a_scale_out, as.p, as.bytes, hipMemcpyDeviceToHost));
+    if (w8_out) WDR_HIP(hipMemcpy(w8_out, w8.p, w8.bytes, hipMemcpyDeviceToHost));
+    if (w_scale_out) WDR_HIP(hipMemcpy(w_scale_out, ws.p, ws.bytes, hipMemcpyDeviceToHost));
     return 0;
   })
 }

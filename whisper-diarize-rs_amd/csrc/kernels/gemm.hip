@@ -347,6 +347,187 @@ __global__ __launch_bounds__(512, 1) void k_gemm3(ProjArgs a) {
 }
 
 
+// ---------------------------------------------------------------- fp8 (e4m3) MFMA GEMM
+// The encoder GEMMs of BASELINE configs[4]: k_gemm3's structure (8 waves of 128 x BN/4, operand
+// tiles staged by global_load_lds into two LDS buffers, g2_swz source swizzle, XCD-aware tile
+// order) on fp8 operands: a K-tile is 128 k = 128 B per row (the bytes of k_gemm3's f16 BK = 64
+// tile), one v_mfma_scale_f32_16x16x128_f8f6f4 per 16 x 16 output tile and K-tile -- the
+// block-scaled form runs twice the f16 MFMA rate (MI355X_MICROARCH.md, matrix cores); its
+// block scales are all 1 (E8M0 127) and the per-row / per-channel scales of the quantisation
+// are applied in the epilogue.  Lane l holds bytes 32 (l >> 4) .. +32 of row (l & 15) of both
+// operands: the same k for A and B, so the dot product is that of the rows whatever k order the
+// hardware sums them in.  BN = 128 for the N = d projections (o, fc2), so M = 6000 fills 240
+// tiles, BN = 256 otherwise.
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+constexpr int G8_M = 256, G8_BK = 128;
+
+template <int EPI, int BN>
+__global__ __launch_bounds__(512, 1) void k_gemm8(ProjArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];   // [buf][A 256 x 128 B, B BN x 128 B]
+  constexpr int NJ = BN / 64;          // 16-column tiles per wave
+  constexpr int BI = BN / 64;          // B DMA instructions (8 rows each) per wave
+  constexpr int BUF = (G8_M + BN) * G8_BK;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+  const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int ntn = a.N / BN;
+  const int bm = id / ntn, bn = id % ntn;
+  const int wm = wid >> 2, wn = wid & 3;
+  const uint8_t* ga[4];
+  const uint8_t* gb[BI];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    const int row = (wid * 4 + jj) * 8 + (lane >> 3);
+    const int c = g2_swz(row, lane & 7);
+    int gm = bm * G8_M + row;
+    gm = gm < a.M ? gm : a.M - 1;
+    ga[jj] = a.A8 + (size_t)gm * a.lda + c * 16;
+  }
+#pragma unroll
+  for (int jj = 0; jj < BI; ++jj) {
+    const int row = (wid * BI + jj) * 8 + (lane >> 3);
+    const int c = g2_swz(row, lane & 7);
+    gb[jj] = a.B8 + (size_t)(bn * BN + row) * a.ldb + c * 16;
+  }
+  auto stage = [&](int buf, int k0) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+      __builtin_amdgcn_global_load_lds((const void*)(ga[jj] + k0), (void*)(lds8 + buf * BUF + (wid * 4 + jj) * 1024),
+                                       16, 0, 0);
+#pragma unroll
+    for (int jj = 0; jj < BI; ++jj)
+      __builtin_amdgcn_global_load_lds((const void*)(gb[jj] + k0),
+                                       (void*)(lds8 + buf * BUF + G8_M * G8_BK + (wid * BI + jj) * 1024), 16, 0, 0);
+  };
+  const int nk = a.K / G8_BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  f32x4 acc[8][NJ];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * G8_BK);
+    const uint8_t* As = lds8 + cur * BUF;
+    const uint8_t* Bs = As + G8_M * G8_BK;
+    i32x8 bf[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int r = wn * (BN / 4) + j * 16 + fr;
+      const int4 lo = *(const int4*)(Bs + r * G8_BK + g2_swz(r, 2 * fq) * 16);
+      const int4 hi = *(const int4*)(Bs + r * G8_BK + g2_swz(r, 2 * fq + 1) * 16);
+      bf[j] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = wm * 128 + i * 16 + fr;
+      const int4 lo = *(const int4*)(As + r * G8_BK + g2_swz(r, 2 * fq) * 16);
+      const int4 hi = *(const int4*)(As + r * G8_BK + g2_swz(r, 2 * fq + 1) * 16);
+      const i32x8 af = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bf[j], acc[i][j], 0, 0, 0, 0x7f7f7f7f, 0,
+                                                                      0x7f7f7f7f);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = bm * G8_M + wm * 128 + i * 16 + fq * 4 + r;
+      const float xs = row < a.M ? a.a_scale[row] : 0.f;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int col = bn * BN + wn * (BN / 4) + j * 16 + fr;
+        epi_store<EPI>(a, row, col, acc[i][j][r] * xs * a.b_scale[col]);
+      }
+    }
+}
+
+template <int EPI>
+static void launch_epi8(const ProjArgs& a, hipStream_t s) {
+  const double bytes = (double)a.N * a.K + (double)a.M * a.K + (double)a.M * a.N * 2;
+  const double flops = 2.0 * a.M * a.N * a.K;
+  const bool narrow = a.N % 256 != 0 || a.N <= 2048;
+  const uint32_t lds = 2u * (G8_M + (narrow ? 128u : 256u)) * G8_BK;
+  static bool attr = [] {
+    WDR_HIP(hipFuncSetAttribute((const void*)k_gemm8<EPI, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * (G8_M + 128) * G8_BK));
+    WDR_HIP(hipFuncSetAttribute((const void*)k_gemm8<EPI, 256>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * (G8_M + 256) * G8_BK));
+    return true;
+  }();
+  (void)attr;
+  if (narrow) {
+    dim3 grid((a.N / 128) * cdiv(a.M, G8_M));
+    wdr_launch(PROF_GEMM, bytes, flops, k_gemm8<EPI, 128>, grid, dim3(512), lds, s, a);
+  } else {
+    dim3 grid((a.N / 256) * cdiv(a.M, G8_M));
+    wdr_launch(PROF_GEMM, bytes, flops, k_gemm8<EPI, 256>, grid, dim3(512), lds, s, a);
+  }
+}
+
+void launch_proj_fp8(const ProjArgs& a, hipStream_t s) {
+  WDR_CHECK(a.A8 && a.B8 && a.a_scale && a.b_scale, "fp8 projection: operands / scales missing");
+  WDR_CHECK(a.M > 64 && a.N % 128 == 0 && a.K % G8_BK == 0 && a.lda % 16 == 0 && a.ldb % 16 == 0,
+            "fp8 projection: M > 64, N % 128 == 0, K % 128 == 0 required");
+  switch (a.epi) {
+    case EPI_F16: launch_epi8<EPI_F16>(a, s); break;
+    case EPI_F16_GELU: launch_epi8<EPI_F16_GELU>(a, s); break;
+    case EPI_F32_RESID: launch_epi8<EPI_F32_RESID>(a, s); break;
+    case EPI_F32: launch_epi8<EPI_F32>(a, s); break;
+    default: throw std::runtime_error("fp8 projection: unsupported epilogue");
+  }
+  WDR_HIP(hipGetLastError());
+}
+
+// one workgroup per row: max |x| -> scale = amax / 448 (e4m3's largest finite value), then
+// the row scaled by 448 / amax, rounded to nearest-even e4m3 (v_cvt_pk_fp8_f32, OCP e4m3fn)
+__global__ __launch_bounds__(256) void k_quant_rows(const f16* x, int ldx, int K, uint8_t* y, int ldy, float* scale) {
+  __shared__ float red[4];
+  const int r = blockIdx.x, tid = threadIdx.x;
+  const f16* xr = x + (size_t)r * ldx;
+  float am = 0.f;
+  for (int c = tid * 8; c < K; c += 2048) {
+    const f16x8 v = *(const f16x8*)(xr + c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf((float)v[e]));
+  }
+  am = wave_max(am);
+  if ((tid & 63) == 0) red[tid >> 6] = am;
+  __syncthreads();
+  am = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float inv = am > 0.f ? 448.f / am : 1.f;
+  if (tid == 0) scale[r] = am > 0.f ? am / 448.f : 1.f;
+  uint8_t* yr = y + (size_t)r * ldy;
+  for (int c = tid * 8; c < K; c += 2048) {
+    const f16x8 v = *(const f16x8*)(xr + c);
+    unsigned lo = 0, hi = 0;
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[0] * inv, (float)v[1] * inv, lo, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[2] * inv, (float)v[3] * inv, lo, true);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[4] * inv, (float)v[5] * inv, hi, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[6] * inv, (float)v[7] * inv, hi, true);
+    *(uint2*)(yr + c) = make_uint2(lo, hi);
+  }
+}
+
+void launch_quant_rows(const f16* x, int ldx, int M, int K, uint8_t* y, int ldy, float* scale, hipStream_t s) {
+  WDR_CHECK(M >= 1 && K % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0, "fp8 quantisation: K, ld must be multiples of 8");
+  hipLaunchKernelGGL(k_quant_rows, dim3(M), dim3(256), 0, s, x, ldx, K, y, ldy, scale);
+  WDR_HIP(hipGetLastError());
+}
+
 // ---------------------------------------------------------------- GEMV (M <= 8)
 // Grid-stride over output rows (one weight row per wave per iteration), 16-B weight loads,
 // v_dot2_f32_f16.  With the fused LayerNorm prologue (LN, K <= 1536) every wave normalises

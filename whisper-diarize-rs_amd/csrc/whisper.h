@@ -7,7 +7,9 @@
 //            device work buffers, KV caches, streams, and the host-side decode loop
 //            `full()` = whisper_full_with_state as the reference drives it.
 #pragma once
+#include <atomic>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -97,6 +99,24 @@ class Context {
   DevMem kv_k, kv_v;
   std::unique_ptr<class StepBatcher> batcher;     // multi-chain greedy steps (created on demand)
   StepBatcher& step_batcher();
+  // fp8 (e4m3) encoder GEMMs (BASELINE configs[4]; wdr_context_set_encoder_fp8, WDR_FP8_ENCODER):
+  // the encoder's projection and cross-K/V weights quantised per output channel, made once on
+  // first use; activations are quantised per row in the encoder
+  std::atomic<bool> fp8_encoder{false};
+  struct Fp8W {
+    DevMem w, s;   // [N][K] e4m3, [N] f32 scales
+  };
+  struct Fp8Layer {
+    Fp8W qkv, o, fc1, fc2;
+  };
+  const std::vector<Fp8Layer>& fp8_layers();   // thread-safe lazy quantisation
+  const Fp8W& fp8_xkv();
+
+ private:
+  std::mutex fp8_mu_;
+  std::vector<Fp8Layer> fp8_layers_;
+  Fp8W fp8_xkv_;
+  void fp8_build();
 };
 
 struct FullParams {

@@ -345,6 +345,7 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
     // KV pool for the decode chains of every State of this context (multi-chain pipeline)
     const char* e = getenv("WDR_DECODE_CHAINS");
     max_chains = std::max(1, std::min(16, e ? atoi(e) : 16));
+    fp8_encoder = getenv("WDR_FP8_ENCODER") && atoi(getenv("WDR_FP8_ENCODER")) != 0;
     const size_t per = (size_t)hp.n_text_layer * 21 * hp.n_text_ctx * hp.n_text_state;   // NSLOT = 21
     kv_k = DevMem(per * max_chains * 2);
     kv_v = DevMem(per * max_chains * 2);
@@ -381,6 +382,7 @@ struct State::Impl {
   struct EncBufs {
     int nb = 0;
     DevMem im2col, c1, ex, eh, eqkv, eatt, emlp;
+    DevMem q8, qs;   // fp8 encoder: the GEMM input quantised per row, its row scales
   };
   EncBufs eb, e1;
   // cross-K/V ring: one slot per in-flight speech segment, [slot][1500][L*2d] f16, plus a
@@ -467,6 +469,40 @@ struct State::Impl {
   int* d_err = nullptr;
 };
 
+// ------------------------------------------------------------------ fp8 encoder weights
+void Context::fp8_build() {
+  WDR_HIP(hipSetDevice(cp.gpu_device));
+  const HParams& hp = model.hp;
+  const int d = hp.n_audio_state;
+  auto quant = [&](const f16* w, int N, int K) {
+    Fp8W q;
+    q.w = DevMem((size_t)N * K);
+    q.s = DevMem((size_t)N * 4);
+    launch_quant_rows(w, K, N, K, q.w.as<uint8_t>(), K, q.s.as<float>(), stream);
+    return q;
+  };
+  std::vector<Fp8Layer> L(hp.n_audio_layer);
+  for (int l = 0; l < hp.n_audio_layer; ++l) {
+    const EncLayer& e = model.enc[l];
+    L[l].qkv = quant(e.w_qkv, 3 * d, d);
+    L[l].o = quant(e.w_o, d, d);
+    L[l].fc1 = quant(e.w_fc1, 4 * d, d);
+    L[l].fc2 = quant(e.w_fc2, d, 4 * d);
+  }
+  fp8_xkv_ = quant(model.w_xkv, hp.n_text_layer * 2 * hp.n_text_state, d);
+  WDR_HIP(hipStreamSynchronize(stream));
+  fp8_layers_ = std::move(L);
+}
+const std::vector<Context::Fp8Layer>& Context::fp8_layers() {
+  std::lock_guard<std::mutex> g(fp8_mu_);
+  if (fp8_layers_.empty()) fp8_build();
+  return fp8_layers_;
+}
+const Context::Fp8W& Context::fp8_xkv() {
+  fp8_layers();
+  return fp8_xkv_;
+}
+
 static constexpr int kBatch = 4;     // encoder windows per encode-ahead launch (M = 6000 rows)
 static constexpr int kSlots = 16;    // in-flight segments in the cross-K/V ring
 
@@ -479,6 +515,8 @@ static void alloc_enc(State::Impl::EncBufs& e, int nb, int d, int kp1) {
   e.eqkv = DevMem((size_t)nb * 1500 * 3 * d * 2);
   e.eatt = DevMem((size_t)nb * 1500 * d * 2);
   e.emlp = DevMem((size_t)nb * 1500 * 4 * d * 2);
+  e.q8 = DevMem((size_t)nb * 1500 * 4 * d);
+  e.qs = DevMem((size_t)nb * 1500 * 4);
 }
 
 State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
@@ -768,22 +806,43 @@ static void encoder_body(Context& ctx, State::Impl& m, State::Impl::EncBufs& e, 
        md.enc_pos, hp.n_audio_ctx);
   const float scale = 1.0f / 8.0f;   // d_head^-1/2
   const long long bs = 1500ll * 3 * d, obs = 1500ll * d;
+  // fp8 encoder (BASELINE configs[4]): every projection's input quantised per row into e.q8,
+  // the weights per output channel (Context::fp8_layers), the block-scaled fp8 MFMA GEMM with
+  // the same epilogues; LayerNorm, attention and the residual stream stay f16 / f32
+  const bool f8 = ctx.fp8_encoder.load() && d % 128 == 0;
+  const std::vector<Context::Fp8Layer>* F8 = f8 ? &ctx.fp8_layers() : nullptr;
+  auto gemm = [&](const f16* A, int lda, const f16* W, const Context::Fp8W* W8, const float* bias, void* out, int ldo,
+                  int N, int K, int epi) {
+    if (!W8) {
+      proj(s, A, lda, W, K, bias, out, ldo, M, N, K, epi);
+      return;
+    }
+    launch_quant_rows(A, lda, M, K, e.q8.as<uint8_t>(), K, e.qs.as<float>(), s);
+    ProjArgs p{nullptr, K, nullptr, K, bias, out, ldo, nullptr, 0, M, N, K, epi};
+    p.A8 = e.q8.as<uint8_t>();
+    p.B8 = W8->w.as<uint8_t>();
+    p.a_scale = e.qs.as<float>();
+    p.b_scale = W8->s.as<float>();
+    launch_proj_fp8(p, s);
+  };
   for (int l = 0; l < hp.n_audio_layer; ++l) {
     const EncLayer& w = md.enc[l];
+    const Context::Fp8Layer* w8 = F8 ? &(*F8)[l] : nullptr;
     launch_layernorm(e.ex.as<float>(), d, w.ln1_g, w.ln1_b, e.eh.as<f16>(), d, M, d, s);
-    proj(s, e.eh.as<f16>(), d, w.w_qkv, d, w.b_qkv, e.eqkv.p, 3 * d, M, 3 * d, d, EPI_F16);
+    gemm(e.eh.as<f16>(), d, w.w_qkv, w8 ? &w8->qkv : nullptr, w.b_qkv, e.eqkv.p, 3 * d, 3 * d, d, EPI_F16);
     FlashArgs fa{e.eqkv.as<f16>(), 3 * d, bs, e.eqkv.as<f16>() + d, 3 * d, bs, e.eqkv.as<f16>() + 2 * d, 3 * d, bs,
                  e.eatt.as<f16>(), d, obs, nullptr, 1500, 1500, hp.n_audio_head, 0, scale};
     launch_flash_attn(fa, nb, s);
-    proj(s, e.eatt.as<f16>(), d, w.w_o, d, w.b_o, e.ex.p, d, M, d, d, EPI_F32_RESID);
+    gemm(e.eatt.as<f16>(), d, w.w_o, w8 ? &w8->o : nullptr, w.b_o, e.ex.p, d, d, d, EPI_F32_RESID);
     launch_layernorm(e.ex.as<float>(), d, w.ln2_g, w.ln2_b, e.eh.as<f16>(), d, M, d, s);
-    proj(s, e.eh.as<f16>(), d, w.w_fc1, d, w.b_fc1, e.emlp.p, 4 * d, M, 4 * d, d, EPI_F16_GELU);
-    proj(s, e.emlp.as<f16>(), 4 * d, w.w_fc2, 4 * d, w.b_fc2, e.ex.p, d, M, d, 4 * d, EPI_F32_RESID);
+    gemm(e.eh.as<f16>(), d, w.w_fc1, w8 ? &w8->fc1 : nullptr, w.b_fc1, e.emlp.p, 4 * d, 4 * d, d, EPI_F16_GELU);
+    gemm(e.emlp.as<f16>(), 4 * d, w.w_fc2, w8 ? &w8->fc2 : nullptr, w.b_fc2, e.ex.p, d, d, 4 * d, EPI_F32_RESID);
   }
   launch_layernorm(e.ex.as<float>(), d, md.ln_post_g, md.ln_post_b, e.eh.as<f16>(), d, M, d, s);
   // cross K/V for every decoder layer in one GEMM: [nb*1500][L*2d] (slots are contiguous)
   const int L = hp.n_text_layer;
-  proj(s, e.eh.as<f16>(), d, md.w_xkv, d, md.b_xkv, xkv_out, L * 2 * d, M, L * 2 * d, d, EPI_F16);
+  gemm(e.eh.as<f16>(), d, md.w_xkv, f8 ? &ctx.fp8_xkv() : nullptr, md.b_xkv, xkv_out, L * 2 * d, L * 2 * d, d,
+       EPI_F16);
 }
 
 // one window of the current slot's segment on the decode stream (on-demand path)

@@ -645,6 +645,10 @@ class WhisperContext:
         L.check(self._lib.wdr_context_devices(self.h, C.byref(n), ids, 8))
         return [ids[i] for i in range(min(n.value, 8))]
 
+    def set_encoder_fp8(self, on: bool):
+        """fp8 (e4m3) encoder GEMMs, BASELINE configs[4] (wdr_context_set_encoder_fp8)."""
+        L.check(self._lib.wdr_context_set_encoder_fp8(self.h, 1 if on else 0))
+
     def set_chains(self, n: int):
         """Decode chains per GPU for run_pipeline calls (wdr_context_set_chains): n blocks of the
         speech segments per GPU decoded concurrently with batched steps, exact prompt fix-up."""

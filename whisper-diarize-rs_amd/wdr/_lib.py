@@ -143,6 +143,7 @@ _SIGS = {
     "wdr_segment_list_free": (None, [P(SegmentList)]),
     "wdr_context_set_chains": (C.c_int, [vp, i32]),
     "wdr_context_devices": (C.c_int, [vp, P(i32), P(i32), i32]),
+    "wdr_context_set_encoder_fp8": (C.c_int, [vp, C.c_int8]),
     "wdr_dbg_set_early_fixup": (C.c_int, [vp, i32]),
     "wdr_ggml_info": (C.c_int, [cstr, P(i32), P(i64), P(i64)]),
     "wdr_dbg_batch_step": (C.c_int, [vp, P(i32), sz, i32, i32, P(f64)]),
@@ -168,6 +169,8 @@ _SIGS = {
     "wdr_dbg_discrete": (C.c_int, [P(f32), sz, C.c_uint32, i32, P(i32)]),
     "wdr_dbg_dtw_dp": (C.c_int, [P(f32), i32, i32, i32, P(i32), P(i32)]),
     "wdr_dbg_proj": (C.c_int, [P(C.c_uint16), P(C.c_uint16), P(f32), i32, i32, i32, i32, P(f32)]),
+    "wdr_dbg_proj_fp8": (C.c_int, [P(C.c_uint16), P(C.c_uint16), P(f32), i32, i32, i32, i32, P(f32), P(C.c_uint8),
+                                   P(f32), P(C.c_uint8), P(f32)]),
     "wdr_dbg_attn": (C.c_int, [P(C.c_uint16), P(C.c_uint16), P(C.c_uint16), i32, i32, i32, i32, P(f32)]),
     "wdr_dbg_xattn": (C.c_int, [P(C.c_uint16), P(C.c_uint16), P(i32), P(i32), i32, i32, i32, i32, P(f32)]),
 }
