@@ -41,8 +41,20 @@ enum Epi : int {
   EPI_F32_RESID = 2,    // out32 += acc + bias          (pre-LN residual stream update)
   EPI_F32 = 3,          // out32 = acc + bias
   EPI_F32_GELU_POS = 4, // out32 = gelu_tanh(acc + bias) + pos[row % pos_rows]  (conv2 + positional)
-  EPI_QKV_CACHE = 5     // cols [0,d) -> out16 (Q); [d,2d) / [2d,3d) -> K / V self-attention cache rows
+  EPI_QKV_CACHE = 5,    // cols [0,d) -> out16 (Q); [d,2d) / [2d,3d) -> K / V self-attention cache rows
+  EPI_XKV = 6           // cross K/V of all layers (N = L*2d) into head-major slots (XKV_* below):
+                        // row = window*1500 + key -> slot out + window*seq_stride
 };
+
+// Cross-K/V slot layout (one per encoded 30-s window): head-major [L][2][H][1500][64] f16, so
+// one head's keys (or values) of one layer are 192 KB contiguous -- a cross-attention chunk of
+// 64 keys is one 8-KB run.  Layer l, head h: K at xkv_k_off(l, H) + h * XKV_HS, V at
+// xkv_v_off(l, H) + h * XKV_HS, key stride 64.  GEMM column c of the N = L*2d projection is
+// (layer, K|V, head, dim) = (c / 2d, c / d % 2, c / 64 % H, c % 64): its block is c / 64.
+constexpr int XKV_T = 1500;
+constexpr long long XKV_HS = (long long)XKV_T * 64;   // head stride (elements)
+__host__ __device__ inline long long xkv_k_off(int l, int H) { return (long long)(2 * l) * H * XKV_HS; }
+__host__ __device__ inline long long xkv_v_off(int l, int H) { return (long long)(2 * l + 1) * H * XKV_HS; }
 
 __host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
@@ -88,6 +100,8 @@ struct ProjArgs {
   // in the epilogue by a_scale[row] * b_scale[col] (per-row / per-output-channel scales)
   const uint8_t* A8 = nullptr; const uint8_t* B8 = nullptr;
   const float* a_scale = nullptr; const float* b_scale = nullptr;
+  // k_gemm4 tile order: groups of tile_gm row tiles walked column by column (0: row-major)
+  int tile_gm = 0;
 };
 
 // Live kernel clock (csrc/prof.cpp): a launch the profiler samples carries ts -> {earliest wave

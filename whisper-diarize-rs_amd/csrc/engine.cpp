@@ -2051,6 +2051,7 @@ int wdr_dbg_xattn(const uint16_t* q, const uint16_t* kv, const int32_t* row_slot
       }
       WDR_HIP(hipMemcpy(drk.p, rk.data(), R * sizeof(void*), hipMemcpyHostToDevice));
       xa.row_k = drk.as<const f16*>();
+      xa.v_off = d;   // this probe's K/V: [S][1500][2d], K then V per key
       if (grp) {
         int ng = 0;
         for (int r = 0; r < R; ++r) {

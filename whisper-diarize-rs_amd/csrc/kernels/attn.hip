@@ -32,8 +32,8 @@ __global__ __launch_bounds__(256) void k_flash_attn(FlashArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const f16* Q = a.q + b * a.q_bs + h * 64;
-  const f16* K = a.k + b * a.k_bs + h * 64;
-  const f16* V = a.v + b * a.v_bs + h * 64;
+  const f16* K = a.k + b * a.k_bs + h * a.k_hs;
+  const f16* V = a.v + b * a.v_bs + h * a.v_hs;
   if (a.nsplit > 1) Q = a.q + h * 64;
   const int fr = lane & 31, hh = lane >> 5;
   const int qrow = qb * 128 + wid * 32 + fr;
@@ -53,8 +53,8 @@ __global__ __launch_bounds__(256) void k_flash_attn(FlashArgs a) {
     kbeg = b * ks;
     kmax = min(a.Tk, kbeg + ks);
     Q = a.q + h * 64;
-    K = a.k + h * 64;
-    V = a.v + h * 64;
+    K = a.k + h * a.k_hs;
+    V = a.v + h * a.v_hs;
   }
   if (a.causal) {
     const int last_q = qb * 128 + 127;
@@ -295,13 +295,13 @@ __global__ __launch_bounds__(256) void k_xattn_partial(XAttnArgs a) {
     nr = a.grp ? a.grp[r0] : 1;
     if (nr == 0) return;   // a row of a group led by an earlier row
     kb = a.row_k[r0] + a.layer_off;
-    vb = kb + a.n_head * 64;
+    vb = kb + a.v_off;
   }
   const int key0 = c * XA_KC;
   const int kk = tid >> 2, qd = tid & 3;
   const int key = key0 + kk;
   const bool kok = key < a.Tk;
-  const long long row = (long long)(kok ? key : a.Tk - 1) * a.ldkv + h * 64 + qd * 16;
+  const long long row = (long long)(kok ? key : a.Tk - 1) * a.ldkv + h * a.hs + qd * 16;
   const f16x8 k0 = *(const f16x8*)(kb + row), k1 = *(const f16x8*)(kb + row + 8);
   const f16x8 v0 = *(const f16x8*)(vb + row), v1 = *(const f16x8*)(vb + row + 8);
   *(f16x8*)(Vs + kk * 64 + qd * 16) = v0;
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(256) void k_aheads_capture(CaptureArgs a) {
   const float inv = 1.f / ml.y;
   float* out = a.out + ((long long)(a.slot0 + i) * a.R + r) * a.Tk;
   for (int key = tid; key < a.Tk; key += 256) {
-    const f16* kr = a.k + (long long)key * a.ldk + h * 64;
+    const f16* kr = a.k + (long long)key * a.ldk + h * a.hs;
     float s = 0.f;
 #pragma unroll
     for (int c = 0; c < 64; c += 8) {

@@ -39,6 +39,9 @@ __device__ __forceinline__ void epi_store(const ProjArgs& a, int row, int col, f
   } else if constexpr (EPI == EPI_F32_GELU_POS) {
     ((float*)a.out)[(size_t)row * a.ldo + col] =
         gelu_tanh(v) + a.pos[(size_t)(row % a.pos_rows) * a.N + col];
+  } else if constexpr (EPI == EPI_XKV) {
+    const int w = row / XKV_T, t = row - w * XKV_T;
+    ((f16*)a.out)[w * a.seq_stride + (long long)(col >> 6) * XKV_HS + t * 64 + (col & 63)] = (f16)v;
   } else {  // EPI_QKV_CACHE
     if (col < a.d) {
       ((f16*)a.out)[(size_t)row * a.ldo + col] = (f16)v;
@@ -347,6 +350,192 @@ __global__ __launch_bounds__(512, 1) void k_gemm3(ProjArgs a) {
 }
 
 
+// ---------------------------------------------------------------- MFMA GEMM, 256 x 256 ping-pong
+// k_gemm3's tile and wave layout (8 waves: 2 along M x 4 along N, 128 x 64 outputs each,
+// v_mfma_f32_16x16x32_f16, the same k order, so bit-identical to k_gemm) in a phased schedule:
+//  * a K-tile (BK 64) is four phases, one output quadrant each -- Q(a, b) = the wave's rows
+//    64a..64a+63 x columns 32b..32b+31, 16 MFMAs over the tile's 64 k -- in the order Q00, Q01,
+//    Q11, Q10, so a phase reads 12, 4, 8 or 4 fragments (A kept from Q00 to Q01, B1 from Q01 to
+//    Q11; B0 re-read for Q10);
+//  * a phase is {LDS fragment reads + one half-tile of LDS-DMA staging} barrier {16 MFMAs}
+//    barrier, and waves 4-7 run one barrier behind waves 0-3: the two waves of every SIMD
+//    alternate, one multiplying while the other reads and stages (a ping-pong on the matrix pipe);
+//  * the LDS tile of each operand is cut into the halves the quadrants read -- AH[a] = rows
+//    64a..64a+63 of both wave groups, BH[b] = columns 32b..32b+31 of every wave -- so a half is
+//    restaged one phase after its last read: BH0 of tile t+1 in phase 1 of tile t, AH0 / BH1 /
+//    AH1 of tile t+2 in phases 2 / 3 / 4 (two LDS buffers, two tiles in flight);
+//  * one counted wait per tile (vmcnt(6): the three half-tiles staged after BH0 of tile t+1 stay
+//    in flight across the barriers), raw s_barrier, all LDS in one dynamic array.
+// Image: 128 rows x 128 B per half, lane-linear LDS-DMA pieces of 8 rows, g2_swz on the source.
+constexpr int G4_HALF = 128 * 64;                   // halfs per half-tile image
+constexpr uint32_t G4_LDS = 2u * 4u * G4_HALF * 2u;   // 2 buffers x {AH0, AH1, BH0, BH1}: 128 KB
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm4(ProjArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
+  extern __shared__ __attribute__((aligned(16))) f16 lds4[];   // [buf][AH0, AH1, BH0, BH1][128 x 64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+  const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int ntn = a.N / G3_N;
+  int bm = id / ntn, bn = id % ntn;
+  if (a.tile_gm > 1) {
+    // grouped order: consecutive ids (one XCD's concurrent workgroups) cover tile_gm row tiles
+    // x a few column tiles, so the K-slices they stage are shared through that XCD's L2
+    const int ntm = cdiv(a.M, G3_M), gsz = a.tile_gm * ntn, g = id / gsz, m0 = g * a.tile_gm;
+    const int gm = min(a.tile_gm, ntm - m0), l = id - g * gsz;
+    bm = m0 + l % gm;
+    bn = l / gm;
+  }
+  const int grp = wid >> 2, wn = wid & 3;
+  // staging: wave w writes pieces 2w, 2w+1 (8 image rows each) of every half-tile
+  //   AH[h] image row q -> A row bm*256 + (q >> 6)*128 + 64h + (q & 63)
+  //   BH[h] image row q -> B row bn*256 + (q >> 5)*64 + 32h + (q & 31)
+  const f16* ga[2][2];   // [half][piece]; rows past M read row M - 1
+  const f16* gb[2];      // [piece]; BH1 = BH0 + 32 rows
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int qa = (2 * wid + jj) * 8 + (lane >> 3);
+    const int ca = g2_swz(qa, lane & 7);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      int gm = bm * G3_M + (qa >> 6) * 128 + 64 * h + (qa & 63);
+      gm = gm < a.M ? gm : a.M - 1;
+      ga[h][jj] = a.A + (size_t)gm * a.lda + ca * 8;
+    }
+    const int gn = bn * G3_N + (qa >> 5) * 64 + (qa & 31);
+    gb[jj] = a.B + (size_t)gn * a.ldb + ca * 8;
+  }
+  const size_t b_half = (size_t)32 * a.ldb;
+  auto stage = [&](int buf, int half, int k0) {   // half: 0 AH0, 1 AH1, 2 BH0, 3 BH1
+    f16* dst = lds4 + (buf * 4 + half) * G4_HALF + (2 * wid) * 512;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const f16* src = half < 2 ? ga[half][jj] + k0 : gb[jj] + (half - 2) * b_half + k0;
+      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(dst + jj * 512), 16, 0, 0);
+    }
+  };
+  const int nk = a.K / G3_BK;
+  // prologue: tile 0 and the halves of tile 1 staged ahead of the loop (AH0, BH1, AH1)
+  stage(0, 0, 0);
+  stage(0, 2, 0);
+  stage(0, 3, 0);
+  stage(0, 1, 0);
+  if (nk > 1) {
+    stage(1, 0, G3_BK);
+    stage(1, 3, G3_BK);
+    stage(1, 1, G3_BK);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();   // waves 4-7 run one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  f16x8 af[2][4], bf[2][2];   // [ks][row tile], [ks][column tile] of the current quadrant
+  auto read_a = [&](const f16* img) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = grp * 64 + i * 16 + fr;
+        af[ks][i] = *(const f16x8*)(img + r * 64 + g2_swz(r, ks * 4 + fq) * 8);
+      }
+  };
+  auto read_b = [&](const f16* img) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wn * 32 + j * 16 + fr;
+        bf[ks][j] = *(const f16x8*)(img + r * 64 + g2_swz(r, ks * 4 + fq) * 8);
+      }
+  };
+  auto mfma_q = [&](int qa, int qb) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[qa * 4 + i][qb * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_f16(af[ks][i], bf[ks][j], acc[qa * 4 + i][qb * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // end of a load section: fragments in registers, then the barrier into the MFMA section
+  auto sync_in = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto sync_out = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const f16* img = lds4 + cur * 4 * G4_HALF;
+    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+    // phase 1: Q00 -- read AH0 + BH0; stage BH0 of tile kt+1
+    read_b(img + 2 * G4_HALF);
+    read_a(img);
+    if (n1) stage(cur ^ 1, 2, (kt + 1) * G3_BK);
+    sync_in();
+    mfma_q(0, 0);
+    sync_out();
+    // phase 2: Q01 -- read BH1; stage AH0 of tile kt+2
+    read_b(img + 3 * G4_HALF);
+    if (n2) stage(cur, 0, (kt + 2) * G3_BK);
+    sync_in();
+    mfma_q(0, 1);
+    sync_out();
+    // phase 3: Q11 -- read AH1; stage BH1 of tile kt+2
+    read_a(img + G4_HALF);
+    if (n2) stage(cur, 3, (kt + 2) * G3_BK);
+    sync_in();
+    mfma_q(1, 1);
+    sync_out();
+    // phase 4: Q10 -- read BH0; stage AH1 of tile kt+2; retire everything up to BH0 of tile kt+1
+    read_b(img + 2 * G4_HALF);
+    if (n2) {
+      stage(cur, 1, (kt + 2) * G3_BK);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    sync_in();
+    mfma_q(1, 0);
+    sync_out();
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();   // matches the stagger barrier of waves 4-7
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = bm * G3_M + grp * 128 + i * 16 + fq * 4 + r;
+        const int col = bn * G3_N + wn * 64 + j * 16 + fr;
+        epi_store<EPI>(a, row, col, acc[i][j][r]);
+      }
+}
+
+
 // ---------------------------------------------------------------- fp8 (e4m3) MFMA GEMM
 // The encoder GEMMs of BASELINE configs[4]: k_gemm3's structure (8 waves of 128 x BN/4, operand
 // tiles staged by global_load_lds into two LDS buffers, g2_swz source swizzle, XCD-aware tile
@@ -487,6 +676,7 @@ void launch_proj_fp8(const ProjArgs& a, hipStream_t s) {
     case EPI_F16_GELU: launch_epi8<EPI_F16_GELU>(a, s); break;
     case EPI_F32_RESID: launch_epi8<EPI_F32_RESID>(a, s); break;
     case EPI_F32: launch_epi8<EPI_F32>(a, s); break;
+    case EPI_XKV: launch_epi8<EPI_XKV>(a, s); break;
     default: throw std::runtime_error("fp8 projection: unsupported epilogue");
   }
   WDR_HIP(hipGetLastError());
@@ -1336,6 +1526,13 @@ static bool gemm3_enabled() {
   return !(e && atoi(e) == 0) && !gemm1_forced();
 }
 
+// WDR_GEMM4=0|1: the ping-pong 256 x 256 GEMM (k_gemm4) off / forced on for every M > 64 shape
+// it takes (A/B runs of tools/gemm_bench); unset: the measured dispatch rule; read per call
+static int gemm4_mode() {
+  const char* e = getenv("WDR_GEMM4");
+  return e ? atoi(e) : -1;
+}
+
 template <int EPI>
 static void launch_epi(const ProjArgs& a, hipStream_t s) {
   const int ob = (EPI == EPI_F32_RESID || EPI == EPI_F32 || EPI == EPI_F32_GELU_POS) ? 4 : 2;
@@ -1500,6 +1697,23 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
     else if (mt == 3) { WDR_SK(3) }
     else { WDR_SK(4) }
 #undef WDR_SK
+  } else if (a.N % G3_N == 0 && a.K % G3_BK == 0 && !gemm1_forced() &&
+             (gemm4_mode() == 1 ||
+              (gemm4_mode() != 0 && ((a.M >= 4096 && a.N >= 3840) || a.M >= 9000 || a.N >= 16384)))) {
+    // ping-pong 256 x 256 tiles where they measured fastest (tools/gemm_bench, large-v3): M = 6000
+    // qkv 600 vs 557 (k_gemm2), fc1 616 vs 574 (k_gemm3), cross-K/V 818 vs 742 TFLOP/s; M = 12000
+    // every shape (o 394 vs 382, fc2 811 vs 743); M = 1500 cross-K/V 773 vs 616.  The N = 1280
+    // shapes at M = 6000 fill only 120 of 256 CUs with 256 x 256 tiles and stay on k_gemm2.
+    static bool attr4 = [] {
+      WDR_HIP(hipFuncSetAttribute((const void*)k_gemm4<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G4_LDS));
+      return true;
+    }();
+    (void)attr4;
+    dim3 grid((a.N / G3_N) * cdiv(a.M, G3_M));
+    ProjArgs g = a;
+    const char* e = getenv("WDR_GEMM4_GM");
+    g.tile_gm = e ? atoi(e) : 4;   // grouped order: qkv, cross-K/V 1 % faster (gemm_bench)
+    wdr_launch(PROF_GEMM, bytes, flops, k_gemm4<EPI>, grid, dim3(512), G4_LDS, s, g);
   } else if ((a.N >= 5120 || a.M >= 9000) && a.M > 2048 && a.N % G3_N == 0 && a.K % G3_BK == 0 && gemm3_enabled()) {
     // 256 x 256 tiles where they measured faster (tools/gemm_bench, large-v3 shapes): M = 6000
     // fc1 574 vs 509 TFLOP/s, cross-K/V 743 vs 641; at M = 12000 every encoder shape (qkv 667 vs
@@ -1562,6 +1776,10 @@ void launch_proj(const ProjArgs& a, hipStream_t s) {
     case EPI_F32: launch_epi<EPI_F32>(a, s); break;
     case EPI_F32_GELU_POS: launch_epi<EPI_F32_GELU_POS>(a, s); break;
     case EPI_QKV_CACHE: launch_epi<EPI_QKV_CACHE>(a, s); break;
+    case EPI_XKV:
+      WDR_CHECK(a.M > 64 && a.seq_stride > 0, "cross-K/V epilogue: encoder GEMM rows and a slot stride");
+      launch_epi<EPI_XKV>(a, s);
+      break;
     default: throw std::runtime_error("projection: bad epilogue");
   }
   WDR_HIP(hipGetLastError());

@@ -86,6 +86,7 @@ struct FlashArgs {
   int Tq, Tk, n_head;
   int causal;
   float scale;
+  long long k_hs = 64, v_hs = 64;   // head stride of K / V (elements): 64 interleaved, XKV_HS cross K/V
   // split-K over keys (few query rows against 1500 cross keys): partial O (unnormalised, f32)
   // and (max, sum) per split, merged by a combine kernel.  nsplit <= 64, n_batch must be 1.
   int nsplit = 1;
@@ -113,9 +114,11 @@ struct XAttnArgs {
   float2* part_ml;
   f16* o; int ldo;
   // per-row cross K/V (rows from different speech segments): row r's K at row_k[r] + layer_off
-  // (device array of slot bases), its V d columns further; k / v unused then
+  // (device array of slot bases), its V v_off elements further; k / v unused then
   const f16* const* row_k = nullptr;
   long long layer_off = 0;
+  long long v_off = 0;
+  long long hs = 64;                  // head stride of K / V (elements; XKV_HS for the slots)
   unsigned long long* ts = nullptr;   // live kernel clock (common.h ProfClock)
   // row groups sharing one cross K/V (the beams of one segment in a batched step), row_k mode:
   // grp[r] = the size of the group row r leads (rows r .. r + grp[r] - 1, <= XATTN_GRP_MAX, K/V
@@ -135,6 +138,7 @@ struct CaptureArgs {
   float* out;
   int slot0, R, Tk;
   float scale;
+  long long hs = 64;                  // head stride of K (elements)
 };
 void launch_aheads_capture(const CaptureArgs& a, int n_sel, hipStream_t s);
 
@@ -152,7 +156,7 @@ struct StepArgs {
   const int* row_seq; const int* row_pos;
   f16* kc; f16* vc;                 // self-attention caches; layer l at + l * layer_stride
   long long layer_stride, seq_stride;
-  const f16* xkv; int ldxkv;        // cross K/V slot [1500][L*2d]
+  const f16* xkv; int ldxkv;        // cross K/V slot, head-major (common.h XKV_*); ldxkv unused
   float* x;                         // [d] residual row (token + positional embedding on entry)
   f16 *q, *att, *qx, *xatt, *mlp;   // [d] x4, [4d]
   float* part_o; float2* part_ml;   // [24][n_head][64], [24][n_head]

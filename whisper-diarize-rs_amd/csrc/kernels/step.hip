@@ -362,8 +362,8 @@ __global__ __launch_bounds__(256) void k_step(StepArgs a) {
     }
     // ---------------- XATT: (head, 64-key chunk) items; cross K/V loaded before the wait
     {
-      const f16* xk = a.xkv + (size_t)l * 2 * d;
-      const f16* xv = xk + d;
+      const f16* xk = a.xkv + xkv_k_off(l, a.n_head);   // head-major slot (common.h)
+      const f16* xv = a.xkv + xkv_v_off(l, a.n_head);
       const int kk = tid >> 2, qd = tid & 3;
       f16x8 kr[2][2], vr[2][2];
 #pragma unroll
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(256) void k_step(StepArgs a) {
         if (it < n_xa) {
           const int c = it % 24, h = it / 24;
           const int key = c * 64 + kk;
-          const size_t row = (size_t)(key < 1500 ? key : 1499) * a.ldxkv + h * 64 + qd * 16;
+          const size_t row = (size_t)(key < 1500 ? key : 1499) * 64 + h * XKV_HS + qd * 16;
           kr[u][0] = __builtin_nontemporal_load((const f16x8*)(xk + row));
           kr[u][1] = __builtin_nontemporal_load((const f16x8*)(xk + row + 8));
           vr[u][0] = __builtin_nontemporal_load((const f16x8*)(xv + row));

@@ -814,11 +814,14 @@ static void encoder_body(Context& ctx, State::Impl& m, State::Impl::EncBufs& e, 
   auto gemm = [&](const f16* A, int lda, const f16* W, const Context::Fp8W* W8, const float* bias, void* out, int ldo,
                   int N, int K, int epi) {
     if (!W8) {
-      proj(s, A, lda, W, K, bias, out, ldo, M, N, K, epi);
+      ProjArgs p{A, lda, W, K, bias, out, ldo, nullptr, 0, M, N, K, epi};
+      if (epi == EPI_XKV) p.seq_stride = (long long)m.xkv_slot_elems;   // window b -> slot b
+      launch_proj(p, s);
       return;
     }
     launch_quant_rows(A, lda, M, K, e.q8.as<uint8_t>(), K, e.qs.as<float>(), s);
     ProjArgs p{nullptr, K, nullptr, K, bias, out, ldo, nullptr, 0, M, N, K, epi};
+    if (epi == EPI_XKV) p.seq_stride = (long long)m.xkv_slot_elems;
     p.A8 = e.q8.as<uint8_t>();
     p.B8 = W8->w.as<uint8_t>();
     p.a_scale = e.qs.as<float>();
@@ -839,10 +842,11 @@ static void encoder_body(Context& ctx, State::Impl& m, State::Impl::EncBufs& e, 
     gemm(e.emlp.as<f16>(), 4 * d, w.w_fc2, w8 ? &w8->fc2 : nullptr, w.b_fc2, e.ex.p, d, d, 4 * d, EPI_F32_RESID);
   }
   launch_layernorm(e.ex.as<float>(), d, md.ln_post_g, md.ln_post_b, e.eh.as<f16>(), d, M, d, s);
-  // cross K/V for every decoder layer in one GEMM: [nb*1500][L*2d] (slots are contiguous)
+  // cross K/V for every decoder layer in one GEMM (N = L*2d), scattered by the epilogue into the
+  // windows' head-major slots (common.h XKV_*; the batch's slots are contiguous)
   const int L = hp.n_text_layer;
   gemm(e.eh.as<f16>(), d, md.w_xkv, f8 ? &ctx.fp8_xkv() : nullptr, md.b_xkv, xkv_out, L * 2 * d, L * 2 * d, d,
-       EPI_F16);
+       EPI_XKV);
 }
 
 // one window of the current slot's segment on the decode stream (on-demand path)
@@ -869,13 +873,17 @@ void State::encode_from_mel_window(const float* w) {
   WDR_HIP(hipStreamSynchronize(s_));
 }
 
+// the current slot's cross K/V as [1500][L*2d] (key-major, K then V of every layer: the
+// reference's per-layer cross-attention K / V projections side by side) from the head-major slot
 void State::read_cross_kv(float* out) {
   Impl& m = *m_;
-  const size_t n = (size_t)1500 * ctx_.model.hp.n_text_layer * 2 * ctx_.model.hp.n_text_state;
+  const int L = ctx_.model.hp.n_text_layer, d = ctx_.model.hp.n_text_state, N = L * 2 * d;
+  const size_t n = (size_t)XKV_T * N;
   std::vector<f16> h(n);
   WDR_HIP(hipMemcpyAsync(h.data(), m.xkv(), n * 2, hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
-  for (size_t i = 0; i < n; ++i) out[i] = (float)h[i];
+  for (int c = 0; c < N; ++c)
+    for (int t = 0; t < XKV_T; ++t) out[(size_t)t * N + c] = (float)h[(size_t)(c >> 6) * XKV_HS + t * 64 + (c & 63)];
 }
 
 void State::read_encoder_out(float* out) {
@@ -1005,7 +1013,7 @@ void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool c
   WDR_HIP(hipMemcpyAsync(b.rows_seq, b.h_rows + 2 * RMAX, n * 4, hipMemcpyHostToDevice, st));
   launch_embed(md.tok_emb, md.dec_pos, b.rows_tok, b.rows_pos, n, d, b.xd, st);
   const float scale = 1.0f / 8.0f;
-  const int ldxkv = L * 2 * d;
+  const int H = hp.n_text_head;
   // the projection's input rows are LayerNorm(x): fused into the skinny GEMM for 8 < n <= 32
   // rows (bit-identical to k_layernorm + GEMM), else the separate LayerNorm into b.hd
   auto ln_into = [&](ProjArgs& p, const float* x, const float* g, const float* bb) {
@@ -1050,12 +1058,14 @@ void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool c
       ln_into(xq, b.xd, e.ln2_g, e.ln2_b);
       launch_proj(xq, st);
     }
-    const f16* xk = xkv_base + (size_t)l * 2 * d;
-    const f16* xv = xk + d;
+    // head-major cross K/V (common.h XKV_*): key stride 64, head stride XKV_HS
+    const f16* xk = xkv_base + xkv_k_off(l, H);
+    const f16* xv = xkv_base + xkv_v_off(l, H);
     const bool cap_layer = capture && !ctx_.aheads_per_layer.empty() && !ctx_.aheads_per_layer[l].empty();
     if (n > NSEQ || cap_layer) {
-      FlashArgs xa{b.qx, d, 0, xk, ldxkv, 0, xv, ldxkv, 0, b.attd, d, 0,
+      FlashArgs xa{b.qx, d, 0, xk, 64, 0, xv, 64, 0, b.attd, d, 0,
                    cap_layer ? b.ml : nullptr, n, 1500, hp.n_text_head, 0, scale};
+      xa.k_hs = xa.v_hs = XKV_HS;
       if (n <= 256) {   // few queries: split the 1500 keys so every CU streams part of the cross K/V
         xa.nsplit = 12;
         xa.part_o = b.fpart_o;
@@ -1065,13 +1075,15 @@ void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool c
       if (cap_layer) {
         int slot0 = 0;
         for (int q = 0; q < l; ++q) slot0 += (int)ctx_.aheads_per_layer[q].size();
-        CaptureArgs ca{b.qx, d, xk, ldxkv, b.ml, ctx_.aheads_dev.as<int>() + ctx_.aheads_dev_off[l],
+        CaptureArgs ca{b.qx, d, xk, 64, b.ml, ctx_.aheads_dev.as<int>() + ctx_.aheads_dev_off[l],
                        b.cap, slot0, n, 1500, scale};
+        ca.hs = XKV_HS;
         launch_aheads_capture(ca, (int)ctx_.aheads_per_layer[l].size(), st);
       }
     } else {
-      XAttnArgs xa{b.qx, d, xk, xv, ldxkv, 1500, n, hp.n_text_head, scale, b.part_o,
+      XAttnArgs xa{b.qx, d, xk, xv, 64, 1500, n, hp.n_text_head, scale, b.part_o,
                    b.part_ml, b.attd, d};
+      xa.hs = XKV_HS;
       launch_xattn(xa, st);
     }
     if (l_end < L && l == l_end - 1) break;   // capture-only pass: done after the last head layer
@@ -1126,7 +1138,7 @@ void decode_step_layers(const Context& ctx, const StepIO& io, int R, hipStream_t
   const HParams& hp = md.hp;
   const int d = hp.n_text_state, L = hp.n_text_layer;
   const float scale = 1.0f / 8.0f;
-  const int ldxkv = L * 2 * d;
+  const int H = hp.n_text_head;
   // more than ln_split rows: the LayerNorm of the rows runs once into io.attd (free at every
   // LN point of the layer) instead of in every GEMV workgroup
   static const int ln_split = getenv("WDR_STEP_LN_SPLIT") ? atoi(getenv("WDR_STEP_LN_SPLIT")) : 2;
@@ -1164,15 +1176,18 @@ void decode_step_layers(const Context& ctx, const StepIO& io, int R, hipStream_t
     launch_dec_self_attn(sa, R, hp.n_text_head, s);
     launch_proj(P(io.attd, d, e.w_o, e.b_o, io.xd, d, d, d, EPI_F32_RESID), s);
     launch_proj(P(nullptr, d, e.w_xq, e.b_xq, io.qx, d, d, d, EPI_F16, e.ln2_g, e.ln2_b), s);
-    XAttnArgs xa{io.qx, d, nullptr, nullptr, ldxkv, 1500, R, hp.n_text_head, scale, io.part_o, io.part_ml, io.attd, d};
+    // head-major cross K/V slots (common.h XKV_*): key stride 64, head stride XKV_HS
+    XAttnArgs xa{io.qx, d, nullptr, nullptr, 64, 1500, R, hp.n_text_head, scale, io.part_o, io.part_ml, io.attd, d};
     xa.grp = io.grp;
     xa.n_grp = io.n_grp;
+    xa.hs = XKV_HS;
     if (io.row_xkv) {
       xa.row_k = io.row_xkv;
-      xa.layer_off = (long long)l * 2 * d;
+      xa.layer_off = xkv_k_off(l, H);
+      xa.v_off = xkv_v_off(l, H) - xkv_k_off(l, H);
     } else {
-      xa.k = io.xkv + (size_t)l * 2 * d;
-      xa.v = xa.k + d;
+      xa.k = io.xkv + xkv_k_off(l, H);
+      xa.v = io.xkv + xkv_v_off(l, H);
     }
     launch_xattn(xa, s);
     launch_proj(P(io.attd, d, e.w_xo, e.b_xo, io.xd, d, d, d, EPI_F32_RESID), s);
