@@ -60,21 +60,34 @@ __global__ __launch_bounds__(256) void k_flash_attn(FlashArgs a) {
     const int last_q = qb * 128 + 127;
     kmax = kmax < last_q + 1 ? kmax : last_q + 1;
   }
+  // K / V tiles are register-staged one tile ahead: the loads of tile k0 + 64 are issued right
+  // after tile k0 is published to LDS and land while tile k0 is multiplied; they are written to
+  // LDS after the next barrier
+  f16x8 kreg[2], vreg[2];
+  auto load_tile = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      const int r = c >> 3, col = (c & 7) * 8;
+      int key = kt + r;
+      key = key < kmax ? key : kmax - 1;
+      kreg[i] = *(const f16x8*)(K + (long long)key * a.ldk + col);
+      vreg[i] = *(const f16x8*)(V + (long long)key * a.ldv + col);
+    }
+  };
+  if (kbeg < kmax) load_tile(kbeg);
   for (int k0 = kbeg; k0 < kmax; k0 += FA_KB) {
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int c = tid + 256 * i;
       const int r = c >> 3, col = (c & 7) * 8;
-      int key = k0 + r;
-      key = key < kmax ? key : kmax - 1;
-      const f16x8 kv = *(const f16x8*)(K + (long long)key * a.ldk + col);
-      *(f16x8*)(Ks + r * FA_KS + col) = kv;
-      const f16x8 vv = *(const f16x8*)(V + (long long)key * a.ldv + col);
+      *(f16x8*)(Ks + r * FA_KS + col) = kreg[i];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) Vt[(col + e) * FA_VS + r] = vv[e];
+      for (int e = 0; e < 8; ++e) Vt[(col + e) * FA_VS + r] = vreg[i][e];
     }
     __syncthreads();
+    if (k0 + FA_KB < kmax) load_tile(k0 + FA_KB);
     f32x16 st[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {

@@ -371,12 +371,9 @@ constexpr int G4_HALF = 128 * 64;                   // halfs per half-tile image
 constexpr uint32_t G4_LDS = 2u * 4u * G4_HALF * 2u;   // 2 buffers x {AH0, AH1, BH0, BH1}: 128 KB
 
 template <int EPI>
-__global__ __launch_bounds__(512, 1) void k_gemm4(ProjArgs a) {
-  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
-  extern __shared__ __attribute__((aligned(16))) f16 lds4[];   // [buf][AH0, AH1, BH0, BH1][128 x 64]
+__device__ __forceinline__ void gemm4_tile(const ProjArgs& a, f16* lds4, int orig, int nwg) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nwg = gridDim.x, orig = blockIdx.x;
   const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
   const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
   const int ntn = a.N / G3_N;
@@ -533,6 +530,21 @@ __global__ __launch_bounds__(512, 1) void k_gemm4(ProjArgs a) {
         const int col = bn * G3_N + wn * 64 + j * 16 + fr;
         epi_store<EPI>(a, row, col, acc[i][j][r]);
       }
+}
+
+// Persistent form: gridDim.x workgroups (a multiple of 8, <= the tile count) walk the tiles
+// blockIdx.x, blockIdx.x + gridDim.x, ... -- every tile of a workgroup keeps its XCD, so the
+// XCD-grouped order holds.  Fewer workgroups than CUs leave CUs to the decode-step kernels that
+// run beside the encoder (WDR_GEMM_CUS).
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm4(ProjArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
+  extern __shared__ __attribute__((aligned(16))) f16 lds4[];   // [buf][AH0, AH1, BH0, BH1][128 x 64]
+  const int ntiles = (a.N / G3_N) * cdiv(a.M, G3_M);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    gemm4_tile<EPI>(a, lds4, t, ntiles);
+    __builtin_amdgcn_s_barrier();   // every wave's last LDS reads done before the next prologue
+  }
 }
 
 
@@ -1699,17 +1711,24 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
 #undef WDR_SK
   } else if (a.N % G3_N == 0 && a.K % G3_BK == 0 && !gemm1_forced() &&
              (gemm4_mode() == 1 ||
-              (gemm4_mode() != 0 && ((a.M >= 4096 && a.N >= 3840) || a.M >= 9000 || a.N >= 16384)))) {
-    // ping-pong 256 x 256 tiles where they measured fastest (tools/gemm_bench, large-v3): M = 6000
-    // qkv 600 vs 557 (k_gemm2), fc1 616 vs 574 (k_gemm3), cross-K/V 818 vs 742 TFLOP/s; M = 12000
-    // every shape (o 394 vs 382, fc2 811 vs 743); M = 1500 cross-K/V 773 vs 616.  The N = 1280
-    // shapes at M = 6000 fill only 120 of 256 CUs with 256 x 256 tiles and stay on k_gemm2.
+              (gemm4_mode() != 0 && (a.M >= 4096 || a.N >= 16384)))) {
+    // ping-pong 256 x 256 tiles (tools/gemm_bench, large-v3, alone on the GPU): M = 6000 qkv 600
+    // vs 557 (k_gemm2), fc1 616 vs 574 (k_gemm3), cross-K/V 818 vs 742 TFLOP/s; M = 12000 every
+    // shape (o 394 vs 382, fc2 811 vs 743); M = 1500 cross-K/V 773 vs 616.  The N = 1280 shapes
+    // at M = 6000 fill only 120 of 256 CUs (alone: 209 / 478 vs 314 / 618 TFLOP/s on k_gemm2),
+    // but inside the pipeline the CUs they leave run decode steps: 1-h bench 480 vs 476 xRT.
     static bool attr4 = [] {
       WDR_HIP(hipFuncSetAttribute((const void*)k_gemm4<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G4_LDS));
       return true;
     }();
     (void)attr4;
-    dim3 grid((a.N / G3_N) * cdiv(a.M, G3_M));
+    // WDR_GEMM_CUS: persistent workgroups (multiple of 8; default one per tile)
+    const int ntiles = (a.N / G3_N) * cdiv(a.M, G3_M);
+    static const int cus = [] {
+      const char* e = getenv("WDR_GEMM_CUS");
+      return e ? atoi(e) / 8 * 8 : 0;
+    }();
+    dim3 grid(cus > 0 && cus < ntiles ? cus : ntiles);
     ProjArgs g = a;
     const char* e = getenv("WDR_GEMM4_GM");
     g.tile_gm = e ? atoi(e) : 4;   // grouped order: qkv, cross-K/V 1 % faster (gemm_bench)
