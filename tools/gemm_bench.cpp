@@ -92,7 +92,10 @@ int main(int argc, char** argv) {
                  md, mr);
         }
       }
-      ProjArgs p{A, sh.K, W, sh.K, bias, out, sh.N, nullptr, 0, M, sh.N, sh.K, sh.epi};
+      // GB_HOT=1: every row of A and B is the same K-vector (lda = ldb = 0), so every operand
+      // load hits in cache: the launch time without the memory latency (a diagnostic only)
+      const int ldz = getenv("GB_HOT") ? 0 : sh.K;
+      ProjArgs p{A, ldz, W, ldz, bias, out, sh.N, nullptr, 0, M, sh.N, sh.K, sh.epi};
       for (int i = 0; i < 3; ++i) launch_proj(p, s);
       const int reps = 20;
       CK(hipEventRecord(a, s));

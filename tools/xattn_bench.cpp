@@ -89,5 +89,51 @@ int main(int argc, char** argv) {
              layout == 0 ? "head-major" : "key-major ", R, us, bytes / us / 1e3, us * L / 1e3);
     }
   }
+  // beam groups: 16 segments x 5 beams (80 rows), each group's rows share its slot
+  {
+    const int G = 5, R = S * G;
+    f16 *qg, *og;
+    float* pog;
+    float2* pmlg;
+    CK(hipMalloc(&qg, (size_t)R * d * 2));
+    CK(hipMalloc(&og, (size_t)R * d * 2));
+    CK(hipMalloc(&pog, (size_t)24 * R * H * 64 * 4));
+    CK(hipMalloc(&pmlg, (size_t)24 * R * H * 8));
+    hipLaunchKernelGGL(k_rand, dim3(64), dim3(256), 0, nullptr, qg, (long long)R * d, 5u);
+    const f16** rkg;
+    int* grp;
+    CK(hipMalloc(&rkg, R * sizeof(void*)));
+    CK(hipMalloc(&grp, R * 4));
+    std::vector<const f16*> hk(R);
+    std::vector<int> hg(R, 0);
+    for (int r = 0; r < R; ++r) hk[r] = xkv + (size_t)(r / G) * slot;
+    for (int g = 0; g < S; ++g) hg[g * G] = G;
+    CK(hipMemcpy(rkg, hk.data(), R * sizeof(void*), hipMemcpyHostToDevice));
+    CK(hipMemcpy(grp, hg.data(), R * 4, hipMemcpyHostToDevice));
+    for (int grouped = 0; grouped < 2; ++grouped) {
+      auto run = [&](int l) {
+        XAttnArgs xa{qg, d, nullptr, nullptr, 64, T, R, H, 0.125f, pog, pmlg, og, d};
+        xa.row_k = rkg;
+        xa.hs = XKV_HS;
+        xa.layer_off = xkv_k_off(l, H);
+        xa.v_off = xkv_v_off(l, H) - xkv_k_off(l, H);
+        if (grouped) {
+          xa.grp = grp;
+          xa.n_grp = S;
+        }
+        launch_xattn(xa, nullptr);
+      };
+      for (int l = 0; l < L; ++l) run(l);
+      CK(hipEventRecord(a, nullptr));
+      for (int i = 0; i < 5; ++i)
+        for (int l = 0; l < L; ++l) run(l);
+      CK(hipEventRecord(b, nullptr));
+      CK(hipEventSynchronize(b));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, a, b));
+      const double us = ms * 1e3 / (5 * L);
+      printf("beams %s R=%d (16 x 5)  %8.2f us per layer\n", grouped ? "grouped  " : "ungrouped", R, us);
+    }
+  }
   return 0;
 }

@@ -295,10 +295,11 @@ constexpr int XA_KC = 64, XA_NS = 24;
 template <bool ROWS>
 __global__ __launch_bounds__(256) void k_xattn_partial(XAttnArgs a) {
   ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
+  constexpr int G = XATTN_GRP_MAX;
   __shared__ __attribute__((aligned(16))) f16 Vs[XA_KC * 64];
-  __shared__ float red[2][4];
-  __shared__ float ps[XA_KC];
-  __shared__ float pv[4][64];
+  __shared__ float red[2][G][4];
+  __shared__ float ps[G][XA_KC];
+  __shared__ float pv[G][4][64];
   const int c = blockIdx.x, h = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   int r0 = 0, nr = a.R;
   const f16* kb = a.k;
@@ -319,35 +320,51 @@ __global__ __launch_bounds__(256) void k_xattn_partial(XAttnArgs a) {
   const f16x8 v0 = *(const f16x8*)(vb + row), v1 = *(const f16x8*)(vb + row + 8);
   *(f16x8*)(Vs + kk * 64 + qd * 16) = v0;
   *(f16x8*)(Vs + kk * 64 + qd * 16 + 8) = v1;
-  for (int r = r0; r < r0 + nr; ++r) {
-    const f16* qr = a.q + (long long)r * a.ldq + h * 64 + qd * 16;
-    const f16x8 q0 = *(const f16x8*)qr, q1 = *(const f16x8*)(qr + 8);
-    float sc = 0.f;
+  // every row of the group is scored with exactly the arithmetic of a single row (the same
+  // per-thread partial dot, shuffles and wave reductions), all rows between the same three
+  // barriers: a row's result never depends on the group (or batch) it runs in
+  float sc[G];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) sc += (float)q0[e] * (float)k0[e] + (float)q1[e] * (float)k1[e];
-    sc += __shfl_xor(sc, 1, 64);
-    sc += __shfl_xor(sc, 2, 64);
-    sc = kok ? sc * a.scale : -INFINITY;
-    const float wm = wave_max(sc);
-    if (lane == 0) red[0][wid] = wm;
-    __syncthreads();
-    const float mx = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
-    const float p = sc == -INFINITY ? 0.f : __expf(sc - mx);
+  for (int j = 0; j < G; ++j) {
+    if (j >= nr) break;
+    const f16* qr = a.q + (long long)(r0 + j) * a.ldq + h * 64 + qd * 16;
+    const f16x8 q0 = *(const f16x8*)qr, q1 = *(const f16x8*)(qr + 8);
+    float t = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t += (float)q0[e] * (float)k0[e] + (float)q1[e] * (float)k1[e];
+    t += __shfl_xor(t, 1, 64);
+    t += __shfl_xor(t, 2, 64);
+    sc[j] = kok ? t * a.scale : -INFINITY;
+    const float wm = wave_max(sc[j]);
+    if (lane == 0) red[0][j][wid] = wm;
+  }
+  __syncthreads();
+  float mx[G];
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    if (j >= nr) break;
+    mx[j] = fmaxf(fmaxf(red[0][j][0], red[0][j][1]), fmaxf(red[0][j][2], red[0][j][3]));
+    const float p = sc[j] == -INFINITY ? 0.f : __expf(sc[j] - mx[j]);
     const float ws = wave_sum(qd == 0 ? p : 0.f);
-    if (qd == 0) ps[kk] = p;
-    if (lane == 0) red[1][wid] = ws;
-    __syncthreads();
+    if (qd == 0) ps[j][kk] = p;
+    if (lane == 0) red[1][j][wid] = ws;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    if (j >= nr) break;
     float acc = 0.f;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc += (float)(f16)ps[wid * 16 + j] * (float)Vs[(wid * 16 + j) * 64 + lane];
-    pv[wid][lane] = acc;
-    __syncthreads();
-    if (tid < 64) {
-      const long long cr = (long long)c * a.R + r;
-      a.part_o[(cr * a.n_head + h) * 64 + tid] = pv[0][tid] + pv[1][tid] + pv[2][tid] + pv[3][tid];
-      if (tid == 0) a.part_ml[cr * a.n_head + h] = make_float2(mx, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
-    }
-    __syncthreads();   // red / ps / pv are rewritten by the next row
+    for (int i = 0; i < 16; ++i) acc += (float)(f16)ps[j][wid * 16 + i] * (float)Vs[(wid * 16 + i) * 64 + lane];
+    pv[j][wid][lane] = acc;
+  }
+  __syncthreads();
+  for (int e = tid; e < nr * 64; e += 256) {
+    const int j = e >> 6, dd = e & 63;
+    const long long cr = (long long)c * a.R + r0 + j;
+    a.part_o[(cr * a.n_head + h) * 64 + dd] = pv[j][0][dd] + pv[j][1][dd] + pv[j][2][dd] + pv[j][3][dd];
+    if (dd == 0)
+      a.part_ml[cr * a.n_head + h] = make_float2(mx[j], red[1][j][0] + red[1][j][1] + red[1][j][2] + red[1][j][3]);
   }
 }
 
