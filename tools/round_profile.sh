@@ -1,13 +1,17 @@
 #!/bin/bash
 # Round profile of the BENCHED configuration on the GPU box: rocprofv3 kernel trace + stats of
-# the default bench command (1 h of audio, hipGraph replays on, concurrent launches from the
-# decode-chain threads), then the stage grouping.  Every GPU step has its own time limit and
-# the chain stops at the first failure.
+# the default bench command (1 h of audio, hipGraph replays on, the GPU streams of all decode
+# chains concurrent), then the stage grouping.  WDR_LAUNCH_LOCK=1 serialises only the host-side
+# launch CALLS of the chain threads: rocprofv3's kernel-trace interception of hipLaunchKernel
+# faults (SIGSEGV inside the tool) when several threads launch eagerly at once
+# (tools/prof_crash_ab.sh: eager + unlocked faults, every locked or graph-replayed run is clean).
+# Every GPU step has its own time limit and the chain stops at the first failure.
 #   tools/round_profile.sh TAG [SECONDS]
 set -e -o pipefail
 TAG=${1:-r02}
 SECS=${2:-3600}
 export TMPDIR=/tmp
+export WDR_LAUNCH_LOCK=1
 mkdir -p gpurun_out
 O=gpurun_out/prof_$TAG
 rm -rf $O && mkdir -p $O

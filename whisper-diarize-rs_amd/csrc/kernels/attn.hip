@@ -200,7 +200,7 @@ void launch_flash_attn(const FlashArgs& a, int n_batch, hipStream_t s) {
     WDR_CHECK(n_batch == 1 && !a.causal && a.nsplit <= 64 && a.part_o && a.part_ml, "flash split: bad args");
     wdr_launch(PROF_FLASH, (double)a.n_head * 64 * 2 * (2.0 * a.Tq + 2.0 * a.Tk), (double)a.n_head * a.Tq * a.Tk * 64 * 4,
                k_flash_attn, dim3(cdiv(a.Tq, 128), a.n_head, a.nsplit), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_flash_combine, dim3(a.Tq, a.n_head), dim3(64), 0, s, a);
+    WDR_KLAUNCH(k_flash_combine, dim3(a.Tq, a.n_head), dim3(64), 0, s, a);
     WDR_HIP(hipGetLastError());
     return;
   }
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecSelfArgs a) {
 }
 
 void launch_dec_self_attn(const DecSelfArgs& a, int R, int n_head, hipStream_t s) {
-  hipLaunchKernelGGL(k_dec_self_attn, dim3(R, n_head), dim3(256), 0, s, a);
+  WDR_KLAUNCH(k_dec_self_attn, dim3(R, n_head), dim3(256), 0, s, a);
   WDR_HIP(hipGetLastError());
 }
 
@@ -395,7 +395,7 @@ void launch_xattn(const XAttnArgs& a, hipStream_t s) {
     wdr_launch(PROF_XATTN, bytes, flops, k_xattn_partial<true>, dim3(XA_NS, a.n_head, a.R), dim3(256), 0, s, a);
   else
     wdr_launch(PROF_XATTN, bytes, flops, k_xattn_partial<false>, dim3(XA_NS, a.n_head), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_xattn_combine<XA_NS>, dim3(a.R, a.n_head), dim3(64), 0, s, a);
+  WDR_KLAUNCH(k_xattn_combine<XA_NS>, dim3(a.R, a.n_head), dim3(64), 0, s, a);
   WDR_HIP(hipGetLastError());
 }
 
@@ -426,7 +426,7 @@ __global__ __launch_bounds__(256) void k_aheads_capture(CaptureArgs a) {
 }
 
 void launch_aheads_capture(const CaptureArgs& a, int n_sel, hipStream_t s) {
-  hipLaunchKernelGGL(k_aheads_capture, dim3(a.R, n_sel), dim3(256), 0, s, a);
+  WDR_KLAUNCH(k_aheads_capture, dim3(a.R, n_sel), dim3(256), 0, s, a);
   WDR_HIP(hipGetLastError());
 }
 

@@ -22,6 +22,7 @@
 //  k_cam_gate      out = y * m[segment] into the dense block's column range.
 #include "../common.h"
 #include "kernels.h"
+#include "../prof.h"
 
 namespace wdr {
 
@@ -94,7 +95,7 @@ __global__ __launch_bounds__(256) void k_gemm32(Gemm32Args a) {
 
 void launch_gemm32(const Gemm32Args& a, hipStream_t s) {
   if (a.M <= 0 || a.N <= 0) return;
-  hipLaunchKernelGGL(k_gemm32, dim3(cdiv(a.N, G_BN), cdiv(a.M, G_BM)), dim3(256), 0, s, a);
+  WDR_KLAUNCH(k_gemm32, dim3(cdiv(a.N, G_BN), cdiv(a.M, G_BM)), dim3(256), 0, s, a);
   WDR_HIP(hipGetLastError());
 }
 
@@ -117,7 +118,7 @@ void launch_im2col_1d(const float* X, int ldx, int T, int C, int k, int stride, 
   const long long total = (long long)To * C * k;
   if (total <= 0) return;
   const int grid = (int)std::min<long long>(cdiv((int)std::min<long long>(total, 1ll << 30), 256), 8192);
-  hipLaunchKernelGGL(k_im2col_1d, dim3(grid), dim3(256), 0, s, X, ldx, T, C, k, stride, dil, pad, To, col);
+  WDR_KLAUNCH(k_im2col_1d, dim3(grid), dim3(256), 0, s, X, ldx, T, C, k, stride, dil, pad, To, col);
   WDR_HIP(hipGetLastError());
 }
 
@@ -141,7 +142,7 @@ void launch_im2col_2d(const float* X, int T, int F, int C, int kf, int kt, int s
   const long long total = (long long)T * Fo * C * kf * kt;
   if (total <= 0) return;
   const int grid = (int)std::min<long long>((total + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_im2col_2d, dim3(grid), dim3(256), 0, s, X, T, F, C, kf, kt, sf, Fo, col);
+  WDR_KLAUNCH(k_im2col_2d, dim3(grid), dim3(256), 0, s, X, T, F, C, kf, kt, sf, Fo, col);
   WDR_HIP(hipGetLastError());
 }
 
@@ -191,7 +192,7 @@ __global__ __launch_bounds__(256) void k_inorm(float* y, long long bs, int T, in
 void launch_maxpool3(const float* x, long long bs, int T, int C, int B, float* y, long long ybs, hipStream_t s) {
   const long long total = (long long)(T / 3) * C;
   if (total <= 0 || B <= 0) return;
-  hipLaunchKernelGGL(k_maxpool3, dim3((unsigned)std::min<long long>((total + 255) / 256, 2048), B), dim3(256), 0, s, x,
+  WDR_KLAUNCH(k_maxpool3, dim3((unsigned)std::min<long long>((total + 255) / 256, 2048), B), dim3(256), 0, s, x,
                      bs, T, C, y, ybs);
   WDR_HIP(hipGetLastError());
 }
@@ -199,7 +200,7 @@ void launch_maxpool3(const float* x, long long bs, int T, int C, int B, float* y
 void launch_inorm(float* y, long long bs, int T, int C, int B, const float* g, const float* beta, int act,
                   hipStream_t s) {
   if (B <= 0 || C <= 0) return;
-  hipLaunchKernelGGL(k_inorm, dim3(C, B), dim3(256), 0, s, y, bs, T, C, g, beta, act);
+  WDR_KLAUNCH(k_inorm, dim3(C, B), dim3(256), 0, s, y, bs, T, C, g, beta, act);
   WDR_HIP(hipGetLastError());
 }
 
@@ -276,7 +277,7 @@ __global__ __launch_bounds__(512) void k_lstm_scan(const float* __restrict__ xg,
 void launch_lstm_scan(const float* xg, long long xbs, int ldxg, int T, int B, const float* whh, const float* bhh,
                       float* out, long long obs, int ldo, hipStream_t s) {
   if (B <= 0) return;
-  hipLaunchKernelGGL(k_lstm_scan, dim3(B, 2), dim3(128 * kLP), 0, s, xg, xbs, ldxg, T, whh, bhh, out, obs, ldo);
+  WDR_KLAUNCH(k_lstm_scan, dim3(B, 2), dim3(128 * kLP), 0, s, xg, xbs, ldxg, T, whh, bhh, out, obs, ldo);
   WDR_HIP(hipGetLastError());
 }
 
@@ -307,7 +308,7 @@ __global__ void k_logsoftmax7(float* z, int rows, int* cls) {
 
 void launch_logsoftmax7(float* z, int rows, int* cls, hipStream_t s) {
   if (rows <= 0) return;
-  hipLaunchKernelGGL(k_logsoftmax7, dim3(cdiv(rows, 256)), dim3(256), 0, s, z, rows, cls);
+  WDR_KLAUNCH(k_logsoftmax7, dim3(cdiv(rows, 256)), dim3(256), 0, s, z, rows, cls);
   WDR_HIP(hipGetLastError());
 }
 
@@ -363,7 +364,7 @@ __global__ __launch_bounds__(256) void k_fbank(const float* x, int T, const floa
 void launch_fbank(const float* x, int T, const float* povey, const float* cos_t, const float* sin_t, const float* banks,
                   float* out, hipStream_t s) {
   if (T <= 0) return;
-  hipLaunchKernelGGL(k_fbank, dim3(T), dim3(256), 0, s, x, T, povey, cos_t, sin_t, banks, out);
+  WDR_KLAUNCH(k_fbank, dim3(T), dim3(256), 0, s, x, T, povey, cos_t, sin_t, banks, out);
   WDR_HIP(hipGetLastError());
 }
 
@@ -400,7 +401,7 @@ __global__ __launch_bounds__(256) void k_colstats(float* x, int ld, int T, int C
 
 void launch_colstats(float* x, int ld, int T, int C, int mode, float* out, hipStream_t s) {
   if (T <= 0 || C <= 0) return;
-  hipLaunchKernelGGL(k_colstats, dim3(C), dim3(256), 0, s, x, ld, T, C, mode, out);
+  WDR_KLAUNCH(k_colstats, dim3(C), dim3(256), 0, s, x, ld, T, C, mode, out);
   WDR_HIP(hipGetLastError());
 }
 
@@ -434,14 +435,14 @@ __global__ void k_cam_gate(const float* y, int ldy, const float* m, int T, int G
 
 void launch_cam_context(const float* h, int ldh, int T, int C, float* out, hipStream_t s) {
   if (T <= 0) return;
-  hipLaunchKernelGGL(k_cam_context, dim3(cdiv(C, 4)), dim3(256), 0, s, h, ldh, T, C, out);
+  WDR_KLAUNCH(k_cam_context, dim3(cdiv(C, 4)), dim3(256), 0, s, h, ldh, T, C, out);
   WDR_HIP(hipGetLastError());
 }
 
 void launch_cam_gate(const float* y, int ldy, const float* m, int T, int G, float* out, int ldo, hipStream_t s) {
   const long long total = (long long)T * G;
   if (total <= 0) return;
-  hipLaunchKernelGGL(k_cam_gate, dim3((unsigned)std::min<long long>((total + 255) / 256, 4096)), dim3(256), 0, s, y, ldy,
+  WDR_KLAUNCH(k_cam_gate, dim3((unsigned)std::min<long long>((total + 255) / 256, 4096)), dim3(256), 0, s, y, ldy,
                      m, T, G, out, ldo);
   WDR_HIP(hipGetLastError());
 }
@@ -484,7 +485,7 @@ void launch_im2col_2d_b(const float* X, const SegRows& sr, int Ttot, int F, int 
   const long long total = (long long)Ttot * Fo * C * kf * kt;
   if (total <= 0) return;
   const int grid = (int)std::min<long long>((total + 255) / 256, 16384);
-  hipLaunchKernelGGL(k_im2col_2d_b, dim3(grid), dim3(256), 0, s, X, sr, Ttot, F, C, kf, kt, sf, Fo, col);
+  WDR_KLAUNCH(k_im2col_2d_b, dim3(grid), dim3(256), 0, s, X, sr, Ttot, F, C, kf, kt, sf, Fo, col);
   WDR_HIP(hipGetLastError());
 }
 
@@ -508,7 +509,7 @@ void launch_im2col_1d_b(const float* X, int ldx, const SegRows& in, const SegRow
   const long long total = (long long)Ttot_out * C * k;
   if (total <= 0) return;
   const int grid = (int)std::min<long long>((total + 255) / 256, 16384);
-  hipLaunchKernelGGL(k_im2col_1d_b, dim3(grid), dim3(256), 0, s, X, ldx, in, out, Ttot_out, C, k, stride, dil, pad,
+  WDR_KLAUNCH(k_im2col_1d_b, dim3(grid), dim3(256), 0, s, X, ldx, in, out, Ttot_out, C, k, stride, dil, pad,
                      col);
   WDR_HIP(hipGetLastError());
 }
@@ -548,7 +549,7 @@ __global__ __launch_bounds__(256) void k_colstats_b(float* xall, int ld, SegRows
 
 void launch_colstats_b(float* x, int ld, const SegRows& sr, int C, int mode, float* out, hipStream_t s) {
   if (sr.B <= 0 || C <= 0) return;
-  hipLaunchKernelGGL(k_colstats_b, dim3(C, sr.B), dim3(256), 0, s, x, ld, sr, C, mode, out);
+  WDR_KLAUNCH(k_colstats_b, dim3(C, sr.B), dim3(256), 0, s, x, ld, sr, C, mode, out);
   WDR_HIP(hipGetLastError());
 }
 
@@ -578,7 +579,7 @@ __global__ __launch_bounds__(256) void k_cam_context_b(const float* hall, int ld
 void launch_cam_context_b(const float* h, int ldh, const SegRows& sr, const int* ctx_off, int C, float* out,
                           hipStream_t s) {
   if (sr.B <= 0) return;
-  hipLaunchKernelGGL(k_cam_context_b, dim3(cdiv(C, 4), sr.B), dim3(256), 0, s, h, ldh, sr, ctx_off, C, out);
+  WDR_KLAUNCH(k_cam_context_b, dim3(cdiv(C, 4), sr.B), dim3(256), 0, s, h, ldh, sr, ctx_off, C, out);
   WDR_HIP(hipGetLastError());
 }
 
@@ -597,7 +598,7 @@ void launch_cam_gate_b(const float* y, int ldy, const float* m, const SegRows& s
                        float* out, int ldo, hipStream_t s) {
   const long long total = (long long)Ttot * G;
   if (total <= 0) return;
-  hipLaunchKernelGGL(k_cam_gate_b, dim3((unsigned)std::min<long long>((total + 255) / 256, 8192)), dim3(256), 0, s, y,
+  WDR_KLAUNCH(k_cam_gate_b, dim3((unsigned)std::min<long long>((total + 255) / 256, 8192)), dim3(256), 0, s, y,
                      ldy, m, sr, ctx_off, Ttot, G, out, ldo);
   WDR_HIP(hipGetLastError());
 }
@@ -612,7 +613,7 @@ __global__ void k_i16_scale(const int16_t* in, long long n, float scale, float* 
 
 void launch_i16_scale(const int16_t* in, long long n, float scale, float* out, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_i16_scale, dim3((unsigned)std::min<long long>((n + 255) / 256, 8192)), dim3(256), 0, s, in, n,
+  WDR_KLAUNCH(k_i16_scale, dim3((unsigned)std::min<long long>((n + 255) / 256, 8192)), dim3(256), 0, s, in, n,
                      scale, out);
   WDR_HIP(hipGetLastError());
 }

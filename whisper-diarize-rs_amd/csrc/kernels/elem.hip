@@ -16,6 +16,7 @@
 //  k_synth_fill      synthetic seeded weights (oracle/weights.py hash, bit-identical).
 #include "../common.h"
 #include "kernels.h"
+#include "../prof.h"
 
 namespace wdr {
 
@@ -58,7 +59,7 @@ void launch_synth_fill(void* dst, long long rows, int src_cols, int dst_cols, ui
   long long blocks = (n + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(k_synth_fill, dim3((unsigned)blocks), dim3(256), 0, s, dst, rows, src_cols, dst_cols, seed, scale,
+  WDR_KLAUNCH(k_synth_fill, dim3((unsigned)blocks), dim3(256), 0, s, dst, rows, src_cols, dst_cols, seed, scale,
                      f16out ? 1 : 0, cval, mode);
   WDR_HIP(hipGetLastError());
 }
@@ -138,7 +139,7 @@ __global__ __launch_bounds__(256) void k_mel_frames(MelArgs a) {
 
 void launch_mel(const MelArgs& a, hipStream_t s) {
   if (a.n_frames > 0) {
-    hipLaunchKernelGGL(k_mel_frames, dim3(cdiv(a.n_frames, MEL_FB)), dim3(256), 0, s, a);
+    WDR_KLAUNCH(k_mel_frames, dim3(cdiv(a.n_frames, MEL_FB)), dim3(256), 0, s, a);
     WDR_HIP(hipGetLastError());
   }
 }
@@ -172,7 +173,7 @@ __global__ void k_im2col_mel(Im2colMelArgs a) {
 }
 
 void launch_im2col_mel(const Im2colMelArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_im2col_mel, dim3(2048), dim3(256), 0, s, a);
+  WDR_KLAUNCH(k_im2col_mel, dim3(2048), dim3(256), 0, s, a);
   WDR_HIP(hipGetLastError());
 }
 
@@ -188,7 +189,7 @@ __global__ void k_im2col_conv2(const f16* x, int d, f16* out) {
 }
 
 void launch_im2col_conv2(const f16* x, int d, f16* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_im2col_conv2, dim3(4096), dim3(256), 0, s, x, d, out);
+  WDR_KLAUNCH(k_im2col_conv2, dim3(4096), dim3(256), 0, s, x, d, out);
   WDR_HIP(hipGetLastError());
 }
 
@@ -205,7 +206,7 @@ __global__ void k_mel_window(const float* mel, int n_mels, int n_fft_frames, con
 
 void launch_mel_window(const float* mel, int n_mels, int n_fft_frames, const int* gmax, int seek, float* out,
                        hipStream_t s) {
-  hipLaunchKernelGGL(k_mel_window, dim3(512), dim3(256), 0, s, mel, n_mels, n_fft_frames, gmax, seek, out);
+  WDR_KLAUNCH(k_mel_window, dim3(512), dim3(256), 0, s, mel, n_mels, n_fft_frames, gmax, seek, out);
   WDR_HIP(hipGetLastError());
 }
 
@@ -214,7 +215,7 @@ void launch_gmax_init(int* gmax, hipStream_t s) {
   // the zero-padded tail always exists (n_len > n_fft_frames), so the max starts at -10
   union { float f; int i; } u;
   u.f = -10.f;
-  hipLaunchKernelGGL(k_set_int, dim3(1), dim3(1), 0, s, gmax, u.i);
+  WDR_KLAUNCH(k_set_int, dim3(1), dim3(1), 0, s, gmax, u.i);
   WDR_HIP(hipGetLastError());
 }
 
@@ -232,7 +233,7 @@ __global__ void k_energy(const float* x, int n, float* e) {
 
 void launch_energy(const float* x, int n, float* e, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_energy, dim3(cdiv(n, 256)), dim3(256), 0, s, x, n, e);
+  WDR_KLAUNCH(k_energy, dim3(cdiv(n, 256)), dim3(256), 0, s, x, n, e);
   WDR_HIP(hipGetLastError());
 }
 
@@ -242,7 +243,7 @@ __global__ void k_i16_to_f32(const int16_t* in, int n, float* out) {
 }
 void launch_i16_to_f32(const int16_t* in, int n, float* out, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_i16_to_f32, dim3(cdiv(n, 256)), dim3(256), 0, s, in, n, out);
+  WDR_KLAUNCH(k_i16_to_f32, dim3(cdiv(n, 256)), dim3(256), 0, s, in, n, out);
   WDR_HIP(hipGetLastError());
 }
 
@@ -298,7 +299,7 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* x, int ldx, cons
 void launch_layernorm(const float* x, int ldx, const float* g, const float* b, f16* y, int ldy, int rows, int d,
                       hipStream_t s) {
   WDR_CHECK(d % 4 == 0 && d <= 1280 && ldx % 4 == 0 && ldy % 4 == 0, "layernorm: unsupported width");
-  hipLaunchKernelGGL(k_layernorm, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, g, b, y, ldy, rows, d);
+  WDR_KLAUNCH(k_layernorm, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, g, b, y, ldy, rows, d);
   WDR_HIP(hipGetLastError());
 }
 
@@ -310,7 +311,7 @@ __global__ void k_embed(const f16* E, const float* P, const int* tok, const int*
 }
 
 void launch_embed(const f16* E, const float* P, const int* tok, const int* pos, int R, int d, float* x, hipStream_t s) {
-  hipLaunchKernelGGL(k_embed, dim3(R), dim3(256), 0, s, E, P, tok, pos, d, x);
+  WDR_KLAUNCH(k_embed, dim3(R), dim3(256), 0, s, E, P, tok, pos, d, x);
   WDR_HIP(hipGetLastError());
 }
 
@@ -326,7 +327,7 @@ __global__ void k_kv_scatter(const f16* qkv, int ldqkv, int d, const int* row_se
 
 void launch_kv_scatter(const f16* qkv, int ldqkv, int d, const int* row_seq, const int* row_pos, int R, f16* kc, f16* vc,
                        long long seq_stride, hipStream_t s) {
-  hipLaunchKernelGGL(k_kv_scatter, dim3(R), dim3(64), 0, s, qkv, ldqkv, d, row_seq, row_pos, kc, vc, seq_stride);
+  WDR_KLAUNCH(k_kv_scatter, dim3(R), dim3(64), 0, s, qkv, ldqkv, d, row_seq, row_pos, kc, vc, seq_stride);
   WDR_HIP(hipGetLastError());
 }
 
@@ -679,8 +680,8 @@ void launch_logits_topk(const float* logits, int ld, const LogitsCtl* ctls, cons
   WDR_CHECK(K >= 1 && K <= BEAM_KMAX, "beam size out of range");
   const LgStats* st = (const LgStats*)work;   // written by launch_logits_process
   LgTop* part = (LgTop*)(work + (size_t)R * LG_NB * 8 + (size_t)R * LG_NB * 8);
-  hipLaunchKernelGGL(k_logits_topk, dim3(LG_NB, R), dim3(256), 0, s, logits, ld, ctls, v, st, K, part);
-  hipLaunchKernelGGL(k_logits_topk_final, dim3(R), dim3(64), 0, s, st, part, K, out);
+  WDR_KLAUNCH(k_logits_topk, dim3(LG_NB, R), dim3(256), 0, s, logits, ld, ctls, v, st, K, part);
+  WDR_KLAUNCH(k_logits_topk_final, dim3(R), dim3(64), 0, s, st, part, K, out);
   WDR_HIP(hipGetLastError());
 }
 
@@ -710,7 +711,7 @@ __global__ __launch_bounds__(256) void k_logits_probs(const float* logits, int l
 void launch_logits_probs(const float* logits, int ld, const LogitsCtl* ctls, const VocabIds& v, int R, float* work,
                          float* probs, float* logprobs, hipStream_t s) {
   const LgStats* st = (const LgStats*)work;   // written by launch_logits_process
-  hipLaunchKernelGGL(k_logits_probs, dim3(LG_NB, R), dim3(256), 0, s, logits, ld, ctls, v, st, probs, logprobs);
+  WDR_KLAUNCH(k_logits_probs, dim3(LG_NB, R), dim3(256), 0, s, logits, ld, ctls, v, st, probs, logprobs);
   WDR_HIP(hipGetLastError());
 }
 
@@ -734,7 +735,7 @@ void launch_kv_copy(f16* kc, f16* vc, long long seq_stride, int nslot, int L, co
                     int n_rows, int d, hipStream_t s) {
   if (n_pairs <= 0 || n_rows <= 0) return;
   WDR_CHECK(d % 8 == 0, "kv copy: d must be a multiple of 8");
-  hipLaunchKernelGGL(k_kv_copy, dim3(std::max(1, std::min(64, n_rows * d / 8 / 256 + 1)), L, n_pairs), dim3(256), 0, s,
+  WDR_KLAUNCH(k_kv_copy, dim3(std::max(1, std::min(64, n_rows * d / 8 / 256 + 1)), L, n_pairs), dim3(256), 0, s,
                      kc, vc, seq_stride, nslot, pairs_dev, n_rows, d);
   WDR_HIP(hipGetLastError());
 }
@@ -743,9 +744,9 @@ void launch_logits_process(const float* logits, int ld, const LogitsCtl* ctls, c
                            TokOut* out, hipStream_t s) {
   LgStats* st = (LgStats*)work;
   LgPick* pk = (LgPick*)(work + (size_t)R * LG_NB * 8);
-  hipLaunchKernelGGL(k_logits_stats, dim3(LG_NB, R), dim3(256), 0, s, logits, ld, ctls, v, st);
-  hipLaunchKernelGGL(k_logits_pick, dim3(LG_NB, R), dim3(256), 0, s, logits, ld, ctls, v, st, pk);
-  hipLaunchKernelGGL(k_logits_final, dim3(R), dim3(64), 0, s, logits, ld, ctls, v, st, pk, out);
+  WDR_KLAUNCH(k_logits_stats, dim3(LG_NB, R), dim3(256), 0, s, logits, ld, ctls, v, st);
+  WDR_KLAUNCH(k_logits_pick, dim3(LG_NB, R), dim3(256), 0, s, logits, ld, ctls, v, st, pk);
+  WDR_KLAUNCH(k_logits_final, dim3(R), dim3(64), 0, s, logits, ld, ctls, v, st, pk, out);
   WDR_HIP(hipGetLastError());
 }
 
@@ -892,15 +893,15 @@ void launch_dtw(const float* cap, int A, int N_tok, int Tk, int n_audio, int sot
   const int rows = N_tok - sot_len - 1;
   WDR_CHECK(rows >= 1 && rows <= DTW_NMAX, "DTW: token count out of range");
   WDR_CHECK(M >= 1 && M <= 1500, "DTW: frame count out of range");
-  hipLaunchKernelGGL(k_dtw_norm, dim3(cdiv(A * M, 256)), dim3(256), 0, s, cap, A, N_tok, Tk, M, nrm);
-  hipLaunchKernelGGL(k_dtw_medmean, dim3(cdiv(rows * M, 256)), dim3(256), 0, s, nrm, A, N_tok, M, sot_len, x);
-  hipLaunchKernelGGL(k_dtw_dp, dim3(1), dim3(256), 0, s, x, rows, M, seek, times, n_times);
+  WDR_KLAUNCH(k_dtw_norm, dim3(cdiv(A * M, 256)), dim3(256), 0, s, cap, A, N_tok, Tk, M, nrm);
+  WDR_KLAUNCH(k_dtw_medmean, dim3(cdiv(rows * M, 256)), dim3(256), 0, s, nrm, A, N_tok, M, sot_len, x);
+  WDR_KLAUNCH(k_dtw_dp, dim3(1), dim3(256), 0, s, x, rows, M, seek, times, n_times);
   WDR_HIP(hipGetLastError());
 }
 
 void launch_dtw_dp_only(const float* x, int rows, int M, int seek, int* times, int* n_times, hipStream_t s) {
   WDR_CHECK(rows >= 1 && rows <= DTW_NMAX && M >= 1 && M <= 1500, "DTW: shape out of range");
-  hipLaunchKernelGGL(k_dtw_dp, dim3(1), dim3(256), 0, s, x, rows, M, seek, times, n_times);
+  WDR_KLAUNCH(k_dtw_dp, dim3(1), dim3(256), 0, s, x, rows, M, seek, times, n_times);
   WDR_HIP(hipGetLastError());
 }
 

@@ -726,7 +726,7 @@ __global__ __launch_bounds__(256) void k_quant_rows(const f16* x, int ldx, int K
 
 void launch_quant_rows(const f16* x, int ldx, int M, int K, uint8_t* y, int ldy, float* scale, hipStream_t s) {
   WDR_CHECK(M >= 1 && K % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0, "fp8 quantisation: K, ld must be multiples of 8");
-  hipLaunchKernelGGL(k_quant_rows, dim3(M), dim3(256), 0, s, x, ldx, K, y, ldy, scale);
+  WDR_KLAUNCH(k_quant_rows, dim3(M), dim3(256), 0, s, x, ldx, K, y, ldy, scale);
   WDR_HIP(hipGetLastError());
 }
 
@@ -1177,9 +1177,9 @@ __global__ __launch_bounds__(64) void k_ln_rows(ProjArgs a, f16* y, int ldy) {
 void launch_ln_rows(const ProjArgs& a, f16* y, int ldy, hipStream_t s) {
   WDR_CHECK(a.ln_x && a.K % 8 == 0 && a.K <= 1536, "step LayerNorm rows: K must be <= 1536");
   const int nch = cdiv(a.K, 512);
-  if (nch == 1) hipLaunchKernelGGL(k_ln_rows<1>, dim3(a.M), dim3(64), 0, s, a, y, ldy);
-  else if (nch == 2) hipLaunchKernelGGL(k_ln_rows<2>, dim3(a.M), dim3(64), 0, s, a, y, ldy);
-  else hipLaunchKernelGGL(k_ln_rows<3>, dim3(a.M), dim3(64), 0, s, a, y, ldy);
+  if (nch == 1) WDR_KLAUNCH(k_ln_rows<1>, dim3(a.M), dim3(64), 0, s, a, y, ldy);
+  else if (nch == 2) WDR_KLAUNCH(k_ln_rows<2>, dim3(a.M), dim3(64), 0, s, a, y, ldy);
+  else WDR_KLAUNCH(k_ln_rows<3>, dim3(a.M), dim3(64), 0, s, a, y, ldy);
   WDR_HIP(hipGetLastError());
 }
 

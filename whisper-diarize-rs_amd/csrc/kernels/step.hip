@@ -27,6 +27,7 @@
 // leaves, and the host resets the counters and raises.  Co-residency is not required for
 // progress (items only wait on lower phases, which never wait on later ones).
 #include "kernels.h"
+#include "../prof.h"
 
 namespace wdr {
 
@@ -587,7 +588,7 @@ void launch_step(const StepArgs& a, int n_wg, hipStream_t s) {
   dim3 g(n_wg), b(256);
 #define WDR_ST(ND, NF)                                   \
   if (nd == ND && nf == NF) {                            \
-    hipLaunchKernelGGL((k_step<ND, NF>), g, b, 0, s, a); \
+    WDR_KLAUNCH((k_step<ND, NF>), g, b, 0, s, a); \
     WDR_HIP(hipGetLastError());                          \
     return;                                              \
   }

@@ -15,6 +15,7 @@
 //  k_vad_head    p = sigmoid(w_o . f16(relu(h)) + b_o), one wave per chunk.
 #include "../common.h"
 #include "kernels.h"
+#include "../prof.h"
 
 namespace wdr {
 
@@ -207,11 +208,11 @@ void launch_vad(const float* x, long long n, const VadWeights& w, float* xg, flo
   const long long nc = (n + 511) / 512;
   if (nc <= 0) return;
   WDR_CHECK(nc < (1ll << 31), "VAD: input too long");
-  hipLaunchKernelGGL(k_vad_front, dim3((unsigned)nc), dim3(256), 0, s, x, n, w, xg);
+  WDR_KLAUNCH(k_vad_front, dim3((unsigned)nc), dim3(256), 0, s, x, n, w, xg);
   WDR_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_vad_lstm, dim3(1), dim3(256), 0, s, xg, nc, w, hout);
+  WDR_KLAUNCH(k_vad_lstm, dim3(1), dim3(256), 0, s, xg, nc, w, hout);
   WDR_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_vad_head, dim3((unsigned)((nc + 3) / 4)), dim3(256), 0, s, hout, nc, w, probs);
+  WDR_KLAUNCH(k_vad_head, dim3((unsigned)((nc + 3) / 4)), dim3(256), 0, s, hout, nc, w, probs);
   WDR_HIP(hipGetLastError());
 }
 

@@ -24,11 +24,22 @@ bool prof_step();
 void prof_capture(bool on);
 void prof_in_step(bool on);   // around the eager launches of a step prof_step() picked
 hipEvent_t prof_event();
-// WDR_LAUNCH_LOCK=1: kernel launches from the decode-chain threads go through one process-wide
-// mutex (profiling runs: rocprofv3's kernel tracing faults on concurrent multi-thread launches)
+// WDR_LAUNCH_LOCK=1: kernel launches and graph replays from all host threads go through one
+// process-wide mutex (profiling runs: rocprofv3's kernel-trace interception of a launch faults
+// inside the tool when several threads launch at once -- tools/prof_crash_ab.sh)
 std::mutex* launch_lock();
 
 void prof_push(int cls, hipEvent_t a, hipEvent_t b, unsigned long long* ts, double bytes, double flops);
+
+// a plain kernel launch under WDR_LAUNCH_LOCK (every launch site of libwdr goes through it or
+// wdr_launch, the graph replays through launch_lock() too)
+#define WDR_KLAUNCH(...)                                    \
+  do {                                                      \
+    std::mutex* mu_ = ::wdr::launch_lock();                 \
+    if (mu_) mu_->lock();                                   \
+    hipLaunchKernelGGL(__VA_ARGS__);                        \
+    if (mu_) mu_->unlock();                                 \
+  } while (0)
 
 // a sampled launch carries HIP start/stop events and, for argument structs with a ProfClock
 // slot (ProjArgs, FlashArgs, XAttnArgs: prof_attach), the kernel's own clock span

@@ -1280,7 +1280,13 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
     step_and_sample(toks, seqs, pos, ctl, R, out, K, cands);
     return;
   }
-  WDR_HIP(hipGraphLaunch(g.exec, s_));
+  {
+    std::mutex* mu = launch_lock();   // WDR_LAUNCH_LOCK (prof.h)
+    if (mu) mu->lock();
+    const hipError_t ge = hipGraphLaunch(g.exec, s_);
+    if (mu) mu->unlock();
+    WDR_HIP(ge);
+  }
   WDR_HIP(hipStreamSynchronize(s_));
   step_err_check();
   if (K > 0) memcpy(cands, m.h_beam, (size_t)R * K * sizeof(BeamCand));
@@ -2539,7 +2545,13 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
       WDR_HIP(hipGraphDestroy(graph));
       g.vids = vids;
     }
-    WDR_HIP(hipGraphLaunch(g.exec, m.s));
+    {
+      std::mutex* mu = launch_lock();   // WDR_LAUNCH_LOCK (prof.h)
+      if (mu) mu->lock();
+      const hipError_t ge = hipGraphLaunch(g.exec, m.s);
+      if (mu) mu->unlock();
+      WDR_HIP(ge);
+    }
   }
   WDR_HIP(hipStreamSynchronize(m.s));
   {
