@@ -170,8 +170,9 @@ def test_decode_cross_attention(lib):
 
 @pytest.mark.parametrize("N,K,epi", [(1280, 5120, 2), (3840, 1280, 0)])
 def test_step_projection_wide_batches(lib, N, K, epi):
-    """Batched steps of more than 16 rows (beams of many segments) run as 16-row launches: every
-    row equals its one-row result bit for bit."""
+    """Batched steps of more than 16 rows (beams of many segments) run as one multi-pass launch
+    (k_mgemv_sp: 16 or 8 rows per pass, the weights streamed once): every row equals its one-row
+    result bit for bit."""
     rng = np.random.default_rng(N + K)
     a = rng.standard_normal((80, K)).astype(np.float16).astype(np.float32)
     w = (rng.standard_normal((N, K)) * 0.03).astype(np.float16).astype(np.float32)

@@ -2038,7 +2038,7 @@ int wdr_dbg_xattn(const uint16_t* q, const uint16_t* kv, const int32_t* row_slot
     const int d = H * 64, T = 1500;
     DevMem dq((size_t)R * d * 2), dkv((size_t)S * T * 2 * d * 2), dout((size_t)R * d * 2);
     DevMem po((size_t)24 * R * H * 64 * 4), pml((size_t)24 * R * H * 8);
-    DevMem drk(R * sizeof(void*)), dg(R * 4);
+    DevMem drk(R * sizeof(void*)), dg(R * 4), dl(R * 4);
     WDR_HIP(hipMemcpy(dq.p, q, dq.bytes, hipMemcpyHostToDevice));
     WDR_HIP(hipMemcpy(dkv.p, kv, dkv.bytes, hipMemcpyHostToDevice));
     XAttnArgs xa{dq.as<f16>(), d, dkv.as<f16>(), dkv.as<f16>() + d, 2 * d, T, R, H, 0.125f, po.as<float>(),
@@ -2061,6 +2061,12 @@ int wdr_dbg_xattn(const uint16_t* q, const uint16_t* kv, const int32_t* row_slot
         WDR_HIP(hipMemcpy(dg.p, grp, R * 4, hipMemcpyHostToDevice));
         xa.grp = dg.as<int>();
         xa.n_grp = ng;
+        // one workgroup row per group, as the step batcher launches it
+        std::vector<int> lead;
+        for (int r = 0; r < R; ++r)
+          if (grp[r] > 0) lead.push_back(r);
+        WDR_HIP(hipMemcpy(dl.p, lead.data(), lead.size() * 4, hipMemcpyHostToDevice));
+        xa.lead = dl.as<int>();
       }
     }
     for (int i = 0; i < iters; ++i) launch_xattn(xa, nullptr);

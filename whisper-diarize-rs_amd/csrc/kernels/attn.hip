@@ -305,7 +305,7 @@ __global__ __launch_bounds__(256) void k_xattn_partial(XAttnArgs a) {
   const f16* kb = a.k;
   const f16* vb = a.v;
   if (ROWS) {
-    r0 = blockIdx.z;
+    r0 = a.lead ? a.lead[blockIdx.z] : blockIdx.z;
     nr = a.grp ? a.grp[r0] : 1;
     if (nr == 0) return;   // a row of a group led by an earlier row
     kb = a.row_k[r0] + a.layer_off;
@@ -391,8 +391,10 @@ void launch_xattn(const XAttnArgs& a, hipStream_t s) {
   // algorithmic bytes: every group's K/V once
   const int ng = a.row_k ? (a.grp ? a.n_grp : a.R) : 1;
   const double bytes = (double)ng * a.Tk * a.n_head * 64 * 2 * 2, flops = (double)a.R * a.Tk * a.n_head * 64 * 4;
+  WDR_CHECK(!a.lead || (a.grp && a.n_grp >= 1 && a.n_grp <= a.R), "cross-attention decode: leaders need groups");
   if (a.row_k)
-    wdr_launch(PROF_XATTN, bytes, flops, k_xattn_partial<true>, dim3(XA_NS, a.n_head, a.R), dim3(256), 0, s, a);
+    wdr_launch(PROF_XATTN, bytes, flops, k_xattn_partial<true>, dim3(XA_NS, a.n_head, a.lead ? a.n_grp : a.R),
+               dim3(256), 0, s, a);
   else
     wdr_launch(PROF_XATTN, bytes, flops, k_xattn_partial<false>, dim3(XA_NS, a.n_head), dim3(256), 0, s, a);
   WDR_KLAUNCH(k_xattn_combine<XA_NS>, dim3(a.R, a.n_head), dim3(64), 0, s, a);

@@ -1328,6 +1328,106 @@ __global__ __launch_bounds__(256) void k_mgemv_s(ProjArgs a) {
 }
 
 // General GEMV (optional LN prologue through LDS for 2 < M <= 8).
+// A decode step of more than 16 rows (the beams of several segments, StepBatcher): k_mgemv_s's
+// arithmetic with the pass count a runtime value -- ceil(M / MR) passes of MR rows through the
+// LDS image, the wave's weight rows held in registers across them -- so the weights stream once
+// for every row of the step (16-row launches streamed them once per 16 rows).  MR is the row
+// count of the <= 16-row kernel for the same K (16, or 8 for K > 3072), so each row's result is
+// bit-identical to the one it gets in a smaller step.
+template <int EPI, int MR, int R, int NCH>
+__global__ __launch_bounds__(256) void k_mgemv_sp(ProjArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
+  constexpr int KP = NCH * 512, V = R * MR;
+  constexpr int SH = V >= 64 ? 0 : V >= 32 ? 1 : V >= 16 ? 2 : V >= 8 ? 3 : V >= 4 ? 4 : V >= 2 ? 5 : 6;
+  constexpr int NV = MR * KP / 8, PER = (NV + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) f16 xsh[];   // [MR][KP] activation rows
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int n0 = (blockIdx.x * 4 + wid) * R;
+  const int K = a.K, M = a.M, np = (M + MR - 1) / MR;
+  f16x8 t[PER];
+  auto fetch = [&](int p) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int v = i * 256 + threadIdx.x;
+      const int m = v / (KP / 8) + p * MR, k = (v % (KP / 8)) * 8;
+      t[i] = (v < NV && m < M && k < K) ? *(const f16x8*)(a.A + (size_t)m * a.lda + k) : (f16x8){};
+    }
+  };
+  auto put = [&]() {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int v = i * 256 + threadIdx.x;
+      if (v < NV) *(f16x8*)(xsh + (size_t)v * 8) = t[i];
+    }
+  };
+  fetch(0);
+  int kc[NCH];
+  bool kin[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int k = c * 512 + lane * 8;
+    kin[c] = k < K;
+    kc[c] = kin[c] ? k : K - 8;
+  }
+  f16x8 wv[R][NCH];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int n = n0 + r < a.N ? n0 + r : a.N - 1;
+    const f16* w = a.B + (size_t)n * a.ldb;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const f16x8 tw = *(const f16x8*)(w + kc[c]);
+      wv[r][c] = kin[c] ? tw : (f16x8){};
+    }
+  }
+  put();
+  const int j = lane >> SH, jr = j / MR, jm = j % MR;
+  const bool lead = (lane & ((1 << SH) - 1)) == 0 && n0 + jr < a.N;
+  const int nst = n0 + jr < a.N ? n0 + jr : a.N - 1;
+  const float pbias = a.bias ? a.bias[nst] : 0.f;
+  for (int p = 0; p < np; ++p) {
+    if (p > 0) {
+      __syncthreads();   // every wave is done with the previous pass's rows
+      put();
+    }
+    if (p + 1 < np) fetch(p + 1);   // in flight while this pass is multiplied
+    __syncthreads();
+    float acc[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+      for (int m = 0; m < MR; ++m) {
+        const f16x8 xv = *(const f16x8*)(xsh + m * KP + c * 512 + lane * 8);
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r * MR + m] = dot8(wv[r][c], xv, acc[r * MR + m]);
+      }
+    }
+    float v = reduce_scatter<V>(acc, lane);
+    const int mr = jm + p * MR;
+    if (!lead || mr >= M) continue;
+    v += pbias;
+    const size_t o = (size_t)mr * a.ldo + nst;
+    if constexpr (EPI == EPI_F16) {
+      ((f16*)a.out)[o] = (f16)v;
+    } else if constexpr (EPI == EPI_F16_GELU) {
+      ((f16*)a.out)[o] = (f16)gelu_tanh(v);
+    } else if constexpr (EPI == EPI_F32_RESID) {
+      ((float*)a.out)[o] += v;
+    } else if constexpr (EPI == EPI_F32) {
+      ((float*)a.out)[o] = v;
+    } else if constexpr (EPI == EPI_QKV_CACHE) {
+      const long long cdst = a.row_seq[mr] * a.seq_stride + (long long)a.row_pos[mr] * a.d;
+      if (nst < a.d) ((f16*)a.out)[o] = (f16)v;
+      else if (nst < 2 * a.d) a.kc[cdst + nst - a.d] = (f16)v;
+      else a.vc[cdst + nst - 2 * a.d] = (f16)v;
+    } else {
+      epi_store<EPI>(a, mr, nst, v - pbias);
+    }
+  }
+}
+
 template <int EPI, int MR, bool LN>
 __global__ __launch_bounds__(256) void k_gemv(ProjArgs a) {
   ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
@@ -1756,8 +1856,62 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
   }
 }
 
+// > 16 step rows through k_mgemv_sp: one launch, ceil(M / MR) passes, the weights streamed once.
+// MR / R / NCH as the <= 16-row dispatch of launch_epi picks them for the same N, K (16 rows per
+// pass up to K = 1536 -- 8 above K = 3072 with the two-pass fc2's shapes), so the per-row
+// arithmetic is unchanged.  False: the shape has no multi-pass form (the caller chunks it).
+template <int EPI>
+static bool launch_mgemv_passes_epi(const ProjArgs& a, hipStream_t s) {
+  const int ob = (EPI == EPI_F32_RESID || EPI == EPI_F32 || EPI == EPI_F32_GELU_POS) ? 4 : 2;
+  const double bytes = (double)a.N * a.K * 2 + (double)a.M * a.K * 2 + (double)a.M * a.N * ob;
+  const double flops = 2.0 * a.M * a.N * a.K;
+  dim3 blk(256);
+  if (a.K <= 1536) {
+    // the 9..16-row k_mgemv_s shape: MR 16, R = 2 for N >= 2048 (unless WDR_MGEMV_R)
+    const int rq = mgemv_rows();
+    const int R = rq ? rq : (a.N >= 2048 ? 2 : 1);
+    const int nch = cdiv(a.K, 512);
+    const uint32_t lds = (uint32_t)16 * nch * 512 * 2;
+    dim3 g(cdiv(a.N, 4 * R));
+#define WDR_SP(RR, NCHV) wdr_launch(PROF_GEMV, bytes, flops, k_mgemv_sp<EPI, 16, RR, NCHV>, g, blk, lds, s, a)
+    if (R == 1) {
+      if (nch == 1) WDR_SP(1, 1); else if (nch == 2) WDR_SP(1, 2); else WDR_SP(1, 3);
+    } else if (R == 2) {
+      if (nch == 1) WDR_SP(2, 1); else if (nch == 2) WDR_SP(2, 2); else WDR_SP(2, 3);
+    } else {
+      return false;
+    }
+#undef WDR_SP
+    return true;
+  }
+  if (a.K > 3072 && a.K <= 5120 && a.K % 512 == 0 && mgemv_np2()) {
+    // the two-pass fc2 shape (MR 8, R 1): 8 rows per pass
+    const int nch = a.K / 512;
+    const uint32_t lds = (uint32_t)8 * nch * 512 * 2;
+    dim3 g(cdiv(a.N, 4));
+    if (nch == 8) wdr_launch(PROF_GEMV, bytes, flops, k_mgemv_sp<EPI, 8, 1, 8>, g, blk, lds, s, a);
+    else if (nch == 10) wdr_launch(PROF_GEMV, bytes, flops, k_mgemv_sp<EPI, 8, 1, 10>, g, blk, lds, s, a);
+    else return false;
+    return true;
+  }
+  return false;
+}
+
+static bool launch_mgemv_passes(const ProjArgs& a, hipStream_t s) {
+  if (getenv("WDR_MGEMV_PASSES") && atoi(getenv("WDR_MGEMV_PASSES")) == 0) return false;
+  switch (a.epi) {
+    case EPI_F16: return launch_mgemv_passes_epi<EPI_F16>(a, s);
+    case EPI_F16_GELU: return launch_mgemv_passes_epi<EPI_F16_GELU>(a, s);
+    case EPI_F32_RESID: return launch_mgemv_passes_epi<EPI_F32_RESID>(a, s);
+    case EPI_F32: return launch_mgemv_passes_epi<EPI_F32>(a, s);
+    case EPI_QKV_CACHE: return launch_mgemv_passes_epi<EPI_QKV_CACHE>(a, s);
+    default: return false;
+  }
+}
+
 void launch_proj(const ProjArgs& a, hipStream_t s) {
   WDR_CHECK(a.M > 0 && a.K > 0 && a.N > 0, "projection: empty shape");
+  if (a.step_rows && a.M > 16 && !a.ln_x && mgemv_staged() && launch_mgemv_passes(a, s)) return;
   if (a.step_rows && a.M > 16) {
     // a batched step of more than 16 rows (beams of several segments): 16-row GEMV launches,
     // so every row's arithmetic stays that of a <= 16-row step whatever the batch holds

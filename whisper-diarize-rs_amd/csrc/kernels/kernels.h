@@ -126,6 +126,9 @@ struct XAttnArgs {
   // byte count).  Null: every row its own group; without row_k one group of all R rows (k / v)
   const int* grp = nullptr;
   int n_grp = 0;
+  // with grp: the n_grp leading rows (device array), so the launch has one workgroup per group
+  // and chunk instead of one per row (the other rows' workgroups would only exit)
+  const int* lead = nullptr;
 };
 constexpr int XATTN_GRP_MAX = 8;   // rows sharing one K/V without row_k
 inline unsigned long long* prof_attach(XAttnArgs& a) { return a.ts = prof_slot(); }

@@ -165,6 +165,7 @@ struct StepIO {
   const f16* const* row_xkv;       // per-row slot bases (device array)
   const int* grp = nullptr;        // row groups sharing a slot (XAttnArgs::grp), or null
   int n_grp = 0;
+  const int* lead = nullptr;       // the groups' first rows (XAttnArgs::lead), or null
 };
 void decode_step_layers(const Context& ctx, const StepIO& io, int R, hipStream_t s);
 

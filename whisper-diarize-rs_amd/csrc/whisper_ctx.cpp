@@ -1180,6 +1180,7 @@ void decode_step_layers(const Context& ctx, const StepIO& io, int R, hipStream_t
     XAttnArgs xa{io.qx, d, nullptr, nullptr, 64, 1500, R, hp.n_text_head, scale, io.part_o, io.part_ml, io.attd, d};
     xa.grp = io.grp;
     xa.n_grp = io.n_grp;
+    xa.lead = io.lead;
     xa.hs = XKV_HS;
     if (io.row_xkv) {
       xa.row_k = io.row_xkv;
@@ -2333,7 +2334,7 @@ struct StepBatcher::Impl {
   hipStream_t s = nullptr;
   int d = 0, V = 0, H = 0;
   DevMem xd, qkvd, attd, qx, mlpd, logits, work, tokout, ctl, rows_tok, rows_pos, rows_seq, row_xkv, part_o, part_ml;
-  DevMem grp, beamc;
+  DevMem grp, lead, beamc;
   int* h_rows = nullptr;          // [4][RB]: tokens, positions, sequences, group sizes
   LogitsCtl* h_ctl = nullptr;
   const f16** h_xkv = nullptr;
@@ -2343,7 +2344,7 @@ struct StepBatcher::Impl {
     hipGraphExec_t exec = nullptr;
     VocabIds vids{};
   };
-  std::map<int, G> graphs;        // by (K, grouped, row count)
+  std::map<int, G> graphs;        // by (K, grouped, groups, row count)
 };
 
 StepBatcher::StepBatcher(Context& ctx) : ctx_(ctx), m_(new Impl) {
@@ -2373,9 +2374,10 @@ StepBatcher::StepBatcher(Context& ctx) : ctx_(ctx), m_(new Impl) {
   m.part_o = DevMem((size_t)NSPLIT * RB * m.H * 64 * 4);
   m.part_ml = DevMem((size_t)NSPLIT * RB * m.H * sizeof(float2));
   m.grp = DevMem(RB * 4);
+  m.lead = DevMem(RB * 4);
   m.beamc = DevMem((size_t)RB * BEAM_KMAX * sizeof(BeamCand));
   WDR_HIP(hipHostMalloc((void**)&m.h_beam, (size_t)RB * BEAM_KMAX * sizeof(BeamCand), hipHostMallocDefault));
-  WDR_HIP(hipHostMalloc((void**)&m.h_rows, 4 * RB * 4, hipHostMallocDefault));
+  WDR_HIP(hipHostMalloc((void**)&m.h_rows, 5 * RB * 4, hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_ctl, RB * sizeof(LogitsCtl), hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_xkv, RB * sizeof(void*), hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_tok, RB * sizeof(TokOut), hipHostMallocDefault));
@@ -2475,8 +2477,9 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
   WDR_CHECK(R >= 1 && R <= RB, "step batcher: row count out of range");
   WDR_HIP(hipSetDevice(ctx_.cp.gpu_device));
   {
-    int i = 0;
-    for (Req* q : batch)
+    int i = 0, g = 0;
+    for (Req* q : batch) {
+      m.h_rows[4 * RB + g++] = i;   // the group's first row
       for (int j = 0; j < q->n; ++j, ++i) {
         m.h_rows[i] = q->tok[j];
         m.h_rows[RB + i] = q->pos[j];
@@ -2485,6 +2488,7 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
         m.h_ctl[i] = q->ctl[j];
         m.h_xkv[i] = q->xkv;
       }
+    }
   }
   const VocabIds& vids = batch[0]->vids;
   const HParams& hp = ctx_.model.hp;
@@ -2496,12 +2500,16 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
   if (grouped) {
     io.grp = m.grp.as<int>();
     io.n_grp = (int)batch.size();
+    io.lead = m.lead.as<int>();
   }
   auto body = [&]() {
     WDR_HIP(hipMemcpyAsync(m.rows_tok.p, m.h_rows, R * 4, hipMemcpyHostToDevice, m.s));
     WDR_HIP(hipMemcpyAsync(m.rows_pos.p, m.h_rows + RB, R * 4, hipMemcpyHostToDevice, m.s));
     WDR_HIP(hipMemcpyAsync(m.rows_seq.p, m.h_rows + 2 * RB, R * 4, hipMemcpyHostToDevice, m.s));
-    if (grouped) WDR_HIP(hipMemcpyAsync(m.grp.p, m.h_rows + 3 * RB, R * 4, hipMemcpyHostToDevice, m.s));
+    if (grouped) {
+      WDR_HIP(hipMemcpyAsync(m.grp.p, m.h_rows + 3 * RB, R * 4, hipMemcpyHostToDevice, m.s));
+      WDR_HIP(hipMemcpyAsync(m.lead.p, m.h_rows + 4 * RB, io.n_grp * 4, hipMemcpyHostToDevice, m.s));
+    }
     WDR_HIP(hipMemcpyAsync(m.ctl.p, m.h_ctl, R * sizeof(LogitsCtl), hipMemcpyHostToDevice, m.s));
     WDR_HIP(hipMemcpyAsync(m.row_xkv.p, m.h_xkv, R * sizeof(void*), hipMemcpyHostToDevice, m.s));
     launch_embed(ctx_.model.tok_emb, ctx_.model.dec_pos, m.rows_tok.as<int>(), m.rows_pos.as<int>(), R, m.d,
@@ -2529,7 +2537,8 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
     }
     prof_in_step(false);
   } else {
-    Impl::G& g = m.graphs[(K << 20) + (grouped ? 1 << 16 : 0) + R];
+    // the cross-attention grid has one workgroup row per group: the group count is in the key
+    Impl::G& g = m.graphs[(K << 24) + (grouped ? 1 << 23 : 0) + ((grouped ? io.n_grp : 0) << 8) + R];
     if (g.exec && memcmp(&g.vids, &vids, sizeof(VocabIds)) != 0) {
       (void)hipGraphExecDestroy(g.exec);
       g.exec = nullptr;
