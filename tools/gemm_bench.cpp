@@ -58,15 +58,17 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   std::vector<float> ref, r;
-  const char* vname[6] = {"gemm ", "gemm2", "gemm3", "gemm4", "g4gm4", "g4gm8"};
+  const char* vname[6] = {"gemm ", "gemm2", "gemm3", "gemm4", "gemm5", "g4gm8"};
   for (const Shape& sh : shapes) {
     for (int variant = 0; variant < 6; ++variant) {
       // 0: k_gemm (register staging, WDR_GEMM1=1); 1: k_gemm2 / k_gemm (WDR_GEMM3=0);
       // 2: k_gemm3 / k_gemm2 (256 x 256 tiles where the shape allows); 3: k_gemm4 (ping-pong)
       unsetenv("WDR_GEMM1");
       unsetenv("WDR_GEMM3");
-      setenv("WDR_GEMM4", variant >= 3 ? "1" : "0", 1);
-      setenv("WDR_GEMM4_GM", variant == 4 ? "4" : variant == 5 ? "8" : "0", 1);
+      // 3: k_gemm4 forced on every shape; 4: the default dispatch (k_gemm5 on the narrow shapes)
+      setenv("WDR_GEMM4", variant == 3 || variant == 5 ? "1" : variant == 4 ? "-1" : "0", 1);
+      setenv("WDR_GEMM5", variant == 3 ? "0" : "1", 1);
+      setenv("WDR_GEMM4_GM", variant == 5 ? "8" : "4", 1);
       if (variant == 0) setenv("WDR_GEMM1", "1", 1);
       if (variant == 1) setenv("WDR_GEMM3", "0", 1);
       // EPI_F32 into a zeroed buffer for the cross-check (the timed runs use the real epilogue)

@@ -548,6 +548,179 @@ __global__ __launch_bounds__(512, 1) void k_gemm4(ProjArgs a) {
 }
 
 
+// ---------------------------------------------------------------- MFMA GEMM, 256 x 128 ping-pong
+// k_gemm4's schedule on a 256 x 128 tile for the narrow encoder projections (o, fc2: N = d =
+// 1280), which fill only 120 of 256 CUs with 256 x 256 tiles at M = 6000 (240 with these).
+// 8 waves, 2 along M x 4 along N, 128 x 32 outputs each; a K-tile (BK 64) is two phases, one per
+// 64-row half of the wave's rows (16 MFMAs each: 4 row x 2 column tiles x 2 k-steps); the B
+// fragments are read in phase 1 and kept for phase 2.  LDS per buffer: AH0 / AH1 (the two row
+// halves of both wave groups) and BT (the 128 B rows), 16 KB each, two buffers (96 KB); a half is
+// restaged one phase after its last read -- AH1 of tile t+1 in phase 1 of tile t, AH0 and BT of
+// tile t+2 in phase 2 -- and every phase ends its load section with a counted wait (vmcnt(6):
+// three half-tiles in flight across the barriers).  Same k order as k_gemm: bit-identical.
+constexpr uint32_t G5_LDS = 2u * 3u * G4_HALF * 2u;   // 96 KB
+
+template <int EPI>
+__device__ __forceinline__ void gemm5_tile(const ProjArgs& a, f16* lds5, int orig, int nwg) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+  const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int ntn = a.N / 128;
+  int bm = id / ntn, bn = id % ntn;
+  if (a.tile_gm > 1) {
+    const int ntm = cdiv(a.M, G3_M), gsz = a.tile_gm * ntn, g = id / gsz, m0 = g * a.tile_gm;
+    const int gm = min(a.tile_gm, ntm - m0), l = id - g * gsz;
+    bm = m0 + l % gm;
+    bn = l / gm;
+  }
+  const int grp = wid >> 2, wn = wid & 3;
+  // staging: wave w writes pieces 2w, 2w+1 (8 image rows each) of every half
+  //   AH[h] image row q -> A row bm*256 + (q >> 6)*128 + 64h + (q & 63);  BT row q -> B row bn*128 + q
+  const f16* ga[2][2];
+  const f16* gb[2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int qa = (2 * wid + jj) * 8 + (lane >> 3);
+    const int ca = g2_swz(qa, lane & 7);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      int gm = bm * G3_M + (qa >> 6) * 128 + 64 * h + (qa & 63);
+      gm = gm < a.M ? gm : a.M - 1;
+      ga[h][jj] = a.A + (size_t)gm * a.lda + ca * 8;
+    }
+    gb[jj] = a.B + (size_t)(bn * 128 + qa) * a.ldb + ca * 8;
+  }
+  auto stage = [&](int buf, int half, int k0) {   // half: 0 AH0, 1 AH1, 2 BT
+    f16* dst = lds5 + (buf * 3 + half) * G4_HALF + (2 * wid) * 512;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const f16* src = half < 2 ? ga[half][jj] + k0 : gb[jj] + k0;
+      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(dst + jj * 512), 16, 0, 0);
+    }
+  };
+  const int nk = a.K / G3_BK;
+  stage(0, 0, 0);
+  stage(0, 2, 0);
+  stage(0, 1, 0);
+  if (nk > 1) {
+    stage(1, 0, G3_BK);
+    stage(1, 2, G3_BK);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();   // waves 4-7 run one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  f32x4 acc[8][2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  f16x8 af[2][4], bf[2][2];
+  auto read_a = [&](const f16* img) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = grp * 64 + i * 16 + fr;
+        af[ks][i] = *(const f16x8*)(img + r * 64 + g2_swz(r, ks * 4 + fq) * 8);
+      }
+  };
+  auto read_b = [&](const f16* img) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wn * 32 + j * 16 + fr;
+        bf[ks][j] = *(const f16x8*)(img + r * 64 + g2_swz(r, ks * 4 + fq) * 8);
+      }
+  };
+  auto mfma_h = [&](int qa) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[qa * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[ks][i], bf[ks][j], acc[qa * 4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto sync_in = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto sync_out = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const f16* img = lds5 + cur * 3 * G4_HALF;
+    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+    // phase 1: rows 0..63 of the wave's half -- read AH0 + BT; stage AH1 of tile kt+1; retire AH1
+    // of tile kt (read in phase 2)
+    read_b(img + 2 * G4_HALF);
+    read_a(img);
+    if (n1) {
+      stage(cur ^ 1, 1, (kt + 1) * G3_BK);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    sync_in();
+    mfma_h(0);
+    sync_out();
+    // phase 2: rows 64..127 -- read AH1; stage AH0 + BT of tile kt+2; retire AH0 / BT of tile kt+1
+    read_a(img + G4_HALF);
+    if (n2) {
+      stage(cur, 0, (kt + 2) * G3_BK);
+      stage(cur, 2, (kt + 2) * G3_BK);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else if (n1) {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    sync_in();
+    mfma_h(1);
+    sync_out();
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();   // matches the stagger barrier of waves 4-7
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = bm * G3_M + grp * 128 + i * 16 + fq * 4 + r;
+        const int col = bn * 128 + wn * 32 + j * 16 + fr;
+        epi_store<EPI>(a, row, col, acc[i][j][r]);
+      }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm5(ProjArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
+  extern __shared__ __attribute__((aligned(16))) f16 lds5[];   // [buf][AH0, AH1, BT][128 x 64]
+  const int ntiles = (a.N / 128) * cdiv(a.M, G3_M);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    gemm5_tile<EPI>(a, lds5, t, ntiles);
+    __builtin_amdgcn_s_barrier();   // every wave's last LDS reads done before the next prologue
+  }
+}
+
+
 // ---------------------------------------------------------------- fp8 (e4m3) MFMA GEMM
 // The encoder GEMMs of BASELINE configs[4]: k_gemm3's structure (8 waves of 128 x BN/4, operand
 // tiles staged by global_load_lds into two LDS buffers, g2_swz source swizzle, XCD-aware tile
@@ -1645,6 +1818,12 @@ static int gemm4_mode() {
   return e ? atoi(e) : -1;
 }
 
+// WDR_GEMM5=0: the narrow encoder projections on k_gemm4's 256 x 256 tiles (A/B); read per call
+static bool gemm5_on() {
+  const char* e = getenv("WDR_GEMM5");
+  return !(e && atoi(e) == 0);
+}
+
 template <int EPI>
 static void launch_epi(const ProjArgs& a, hipStream_t s) {
   const int ob = (EPI == EPI_F32_RESID || EPI == EPI_F32 || EPI == EPI_F32_GELU_POS) ? 4 : 2;
@@ -1809,6 +1988,21 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
     else if (mt == 3) { WDR_SK(3) }
     else { WDR_SK(4) }
 #undef WDR_SK
+  } else if (a.N % 128 == 0 && a.N < 2048 && a.K % G3_BK == 0 && a.M >= 4096 && !gemm1_forced() && gemm5_on() &&
+             gemm4_mode() != 0 && (a.N / G3_N) * cdiv(a.M, G3_M) < 192) {
+    // the narrow encoder projections (o, fc2) where 256 x 256 tiles would leave CUs idle: 256 x
+    // 128 tiles fill 240 of 256 CUs at M = 6000 (tools/gemm_bench: o 53 vs 62 us on k_gemm2, fc2
+    // 107 vs 126 us; at M = 12000 k_gemm4's 235 tiles are faster: fc2 194 vs 216 us)
+    static bool attr5 = [] {
+      WDR_HIP(hipFuncSetAttribute((const void*)k_gemm5<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G5_LDS));
+      return true;
+    }();
+    (void)attr5;
+    ProjArgs g = a;
+    const char* e = getenv("WDR_GEMM4_GM");
+    g.tile_gm = e ? atoi(e) : 4;
+    dim3 grid((a.N / 128) * cdiv(a.M, G3_M));
+    wdr_launch(PROF_GEMM, bytes, flops, k_gemm5<EPI>, grid, dim3(512), G5_LDS, s, g);
   } else if (a.N % G3_N == 0 && a.K % G3_BK == 0 && !gemm1_forced() &&
              (gemm4_mode() == 1 ||
               (gemm4_mode() != 0 && (a.M >= 4096 || a.N >= 16384)))) {

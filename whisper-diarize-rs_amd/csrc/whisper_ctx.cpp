@@ -344,7 +344,7 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
   {
     // KV pool for the decode chains of every State of this context (multi-chain pipeline)
     const char* e = getenv("WDR_DECODE_CHAINS");
-    max_chains = std::max(1, std::min(16, e ? atoi(e) : 16));
+    max_chains = std::max(1, std::min(32, e ? atoi(e) : 16));
     fp8_encoder = getenv("WDR_FP8_ENCODER") && atoi(getenv("WDR_FP8_ENCODER")) != 0;
     const size_t per = (size_t)hp.n_text_layer * 21 * hp.n_text_ctx * hp.n_text_state;   // NSLOT = 21
     kv_k = DevMem(per * max_chains * 2);
@@ -2321,7 +2321,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
 // ------------------------------------------------------------------ multi-chain step batcher
 namespace wdr {
 
-static constexpr int RB = 128;    // rows per batched step (chains x beams)
+static constexpr int RB = 256;    // rows per batched step (chains x beams: 32 x 8)
 
 struct StepBatcher::Impl {
   std::mutex mu;
@@ -2344,7 +2344,7 @@ struct StepBatcher::Impl {
     hipGraphExec_t exec = nullptr;
     VocabIds vids{};
   };
-  std::map<int, G> graphs;        // by (K, grouped, groups, row count)
+  std::map<long long, G> graphs;  // by (K, grouped, groups, row count)
 };
 
 StepBatcher::StepBatcher(Context& ctx) : ctx_(ctx), m_(new Impl) {
@@ -2538,7 +2538,7 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
     prof_in_step(false);
   } else {
     // the cross-attention grid has one workgroup row per group: the group count is in the key
-    Impl::G& g = m.graphs[(K << 24) + (grouped ? 1 << 23 : 0) + ((grouped ? io.n_grp : 0) << 8) + R];
+    Impl::G& g = m.graphs[((long long)K << 40) + (grouped ? 1ll << 39 : 0ll) + ((long long)(grouped ? io.n_grp : 0) << 16) + R];
     if (g.exec && memcmp(&g.vids, &vids, sizeof(VocabIds)) != 0) {
       (void)hipGraphExecDestroy(g.exec);
       g.exec = nullptr;
