@@ -552,9 +552,13 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
   m.xkv_ring = DevMem((m.S + 1) * m.xkv_slot_elems * 2);
   m.cur = m.S;
   {
+    // the encode-ahead stream at the lowest priority (WDR_ENC_PRIO=1: the middle of the range,
+    // 2: the highest; A/B runs)
     int lo = 0, hi = 0;
     WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    WDR_HIP(hipStreamCreateWithPriority(&m.es, hipStreamNonBlocking, lo));
+    static const int ep = getenv("WDR_ENC_PRIO") ? atoi(getenv("WDR_ENC_PRIO")) : 0;
+    const int prio = ep == 2 ? hi : ep == 1 ? (lo + hi) / 2 : lo;
+    WDR_HIP(hipStreamCreateWithPriority(&m.es, hipStreamNonBlocking, prio));
   }
   m.xd = DevMem((size_t)RMAX * d * 4);
   m.hd = DevMem((size_t)RMAX * d * 2);
