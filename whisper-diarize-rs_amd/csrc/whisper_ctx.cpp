@@ -938,9 +938,19 @@ static int enc_ahead(int S) {
 void State::top_up(int j) {
   Impl& m = *m_;
   const int N = (int)m.plan.pcm.size();
+  // WDR_ENC_FIRST: windows in the first batch of a plan (A/B: 1 / 2 / 4 measured 491-493 /
+  // 495 / 496 xRT on the 1-h bench, so a full batch stays the default); a batch never wraps
+  // around the ring (its slots stay contiguous for the cross-K/V GEMM).  Encoder results do not
+  // depend on the batch.
+  static const int first = [] {
+    const char* e = getenv("WDR_ENC_FIRST");
+    const int v = e ? atoi(e) : kBatch;
+    return std::max(1, std::min(kBatch, v));
+  }();
   while ((int)m.plan.next_enq < N) {
     const int g0 = (int)m.plan.next_enq;
-    const int g1 = std::min(N, g0 + kBatch);
+    int g1 = std::min(N, g0 + (g0 == 0 ? first : kBatch));
+    g1 = std::min(g1, (g0 / m.S + 1) * m.S);
     if (g1 - 1 > j + enc_ahead(m.S) - 1) break;
     const int slot0 = g0 % m.S;
     for (int k = g0; k < g1; ++k) {
