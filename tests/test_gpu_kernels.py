@@ -53,6 +53,29 @@ def test_projection_matches_fp32_reference(lib, M):
     np.testing.assert_allclose(_proj(lib, a, w, bias, 2, base), base + ref, rtol=0, atol=2e-4)
 
 
+@pytest.mark.parametrize("N", [1280, 2560])
+def test_encoder_gemm_tiles(lib, N, monkeypatch):
+    """The encoder-batch GEMMs (M >= 4096): k_gemm5 (256 x 128 ping-pong, N = 1280) and k_gemm4
+    (256 x 256 ping-pong, N = 2560), a ragged last row tile (M = 4200): against the fp64 product
+    within the f32 / f16 output rounding, and bit for bit equal to the register-staged k_gemm
+    (WDR_GEMM1=1), whose per-row arithmetic every other GEMM path shares."""
+    rng = np.random.default_rng(N)
+    M, K = 4200, 256
+    a = rng.standard_normal((M, K)).astype(np.float16).astype(np.float32)
+    w = (rng.standard_normal((N, K)) * 0.05).astype(np.float16).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32) * 0.1
+    ref = a.astype(np.float64) @ w.T.astype(np.float64) + bias
+    got = _proj(lib, a, w, bias, 3)
+    np.testing.assert_allclose(got, ref, rtol=0, atol=2e-4)
+    np.testing.assert_allclose(_proj(lib, a, w, bias, 1), _gelu(ref), rtol=2e-3, atol=2e-3)
+    base = rng.standard_normal((M, N)).astype(np.float32)
+    resid = _proj(lib, a, w, bias, 2, base)
+    np.testing.assert_allclose(resid, base + ref, rtol=0, atol=2e-4)
+    monkeypatch.setenv("WDR_GEMM1", "1")
+    np.testing.assert_array_equal(_proj(lib, a, w, bias, 3), got)
+    np.testing.assert_array_equal(_proj(lib, a, w, bias, 2, base), resid)
+
+
 STEP = 0x100   # include/wdr.h WDR_DBG_PROJ_STEP
 
 

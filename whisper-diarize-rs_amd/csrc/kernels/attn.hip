@@ -292,10 +292,12 @@ void launch_dec_self_attn(const DecSelfArgs& a, int R, int n_head, hipStream_t s
 // 24 chunk partials of each row are merged by k_xattn_combine.
 constexpr int XA_KC = 64, XA_NS = 24;
 
-template <bool ROWS>
+// G: the largest group a launch holds -- 1 for the greedy batched step (every row its own
+// group), which keeps the kernel at <= 64 VGPRs so a workgroup still fits on a CU beside an
+// encoder GEMM tile (k_gemm4: 2 x 224 of the SIMD's 512)
+template <bool ROWS, int G>
 __global__ __launch_bounds__(256) void k_xattn_partial(XAttnArgs a) {
   ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
-  constexpr int G = XATTN_GRP_MAX;
   __shared__ __attribute__((aligned(16))) f16 Vs[XA_KC * 64];
   __shared__ float red[2][G][4];
   __shared__ float ps[G][XA_KC];
@@ -392,11 +394,14 @@ void launch_xattn(const XAttnArgs& a, hipStream_t s) {
   const int ng = a.row_k ? (a.grp ? a.n_grp : a.R) : 1;
   const double bytes = (double)ng * a.Tk * a.n_head * 64 * 2 * 2, flops = (double)a.R * a.Tk * a.n_head * 64 * 4;
   WDR_CHECK(!a.lead || (a.grp && a.n_grp >= 1 && a.n_grp <= a.R), "cross-attention decode: leaders need groups");
-  if (a.row_k)
-    wdr_launch(PROF_XATTN, bytes, flops, k_xattn_partial<true>, dim3(XA_NS, a.n_head, a.lead ? a.n_grp : a.R),
-               dim3(256), 0, s, a);
+  if (a.row_k && !a.grp)
+    wdr_launch(PROF_XATTN, bytes, flops, k_xattn_partial<true, 1>, dim3(XA_NS, a.n_head, a.R), dim3(256), 0, s, a);
+  else if (a.row_k)
+    wdr_launch(PROF_XATTN, bytes, flops, k_xattn_partial<true, XATTN_GRP_MAX>,
+               dim3(XA_NS, a.n_head, a.lead ? a.n_grp : a.R), dim3(256), 0, s, a);
   else
-    wdr_launch(PROF_XATTN, bytes, flops, k_xattn_partial<false>, dim3(XA_NS, a.n_head), dim3(256), 0, s, a);
+    wdr_launch(PROF_XATTN, bytes, flops, k_xattn_partial<false, XATTN_GRP_MAX>, dim3(XA_NS, a.n_head), dim3(256), 0,
+               s, a);
   WDR_KLAUNCH(k_xattn_combine<XA_NS>, dim3(a.R, a.n_head), dim3(64), 0, s, a);
   WDR_HIP(hipGetLastError());
 }
