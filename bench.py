@@ -42,7 +42,7 @@ sys.path.insert(0, os.path.join(ROOT, "whisper-diarize-rs_amd"))
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_F16_PEAK_TFS = 2500.0  # dense f16/bf16 MFMA
 MFMA_FP8_PEAK_TFS = 5000.0  # dense block-scaled fp8 MFMA (MI355X_MICROARCH.md, matrix cores)
-PROF_SAMPLE = 8             # csrc/prof.cpp kEvery (launches) and kStepEvery (steps)
+PROF_EVERY, PROF_STEP_EVERY = 2, 32   # csrc/prof.cpp kEvery (launches in a sampled step), kStepEvery
 
 
 def parse():
@@ -346,11 +346,11 @@ def main():
         if tr is not None:
             r["traffic"] = round(tr)
             r["traffic_source"] = src
-        # csrc/prof.h: decode steps replay hipGraphs; 1 in 8 steps runs eagerly and 1 in 8 of
+        # csrc/prof.h: decode steps replay hipGraphs; 1 in 32 steps runs eagerly and 1 in 2 of
         # its launches carries HIP start/stop events on the launching stream; launches outside
         # steps are timed 1 in 64
         r["sampling"] = "1 in %d launches (decode steps: 1 in %d eager, 1 in %d of those)" % (
-            PROF_SAMPLE * PROF_SAMPLE, PROF_SAMPLE, PROF_SAMPLE)
+            PROF_EVERY * PROF_STEP_EVERY, PROF_STEP_EVERY, PROF_EVERY)
         classes[c] = r
     # `roofline` = the encoder GEMM class: the largest share of kernel time in the rocprofv3 trace
     # of this benched configuration (profiles/r02/prof_graph/summary.txt: gemm 27.8 %, gemv 17.1 %,

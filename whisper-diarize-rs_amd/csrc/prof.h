@@ -1,5 +1,5 @@
 // Live per-kernel-class timing for bench.py's roofline figures.  Any set of classes can be
-// enabled at once (each accumulates separately); 1 in 8 launches of that class is issued with hipExtLaunchKernelGGL start/stop events
+// enabled at once (each accumulates separately); 1 in 64 launches of that class is issued with hipExtLaunchKernelGGL start/stop events
 // (timestamps of the dispatch itself, the same interval rocprofv3 reports), together with the
 // launch's algorithmic bytes and flops.  Graph replay is bypassed while a class is enabled.
 #pragma once
