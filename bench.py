@@ -353,10 +353,10 @@ def main():
             PROF_EVERY * PROF_STEP_EVERY, PROF_STEP_EVERY, PROF_EVERY)
         classes[c] = r
     # `roofline` = the encoder GEMM class: the largest share of kernel time in the rocprofv3 trace
-    # of this benched configuration (profiles/r02/prof_graph/summary.txt: gemm 27.8 %, gemv 17.1 %,
-    # flash 10.5 %, xattn 6.6 % -- 1 h, graphs on).  The live sampler's own shares are not used
+    # of this benched configuration (profiles/r02/prof_graph/summary.txt: gemm 25.1 %, gemv 17.6 %,
+    # flash 11.0 %, xattn 6.6 % -- 1 h, graphs on).  The live sampler's own shares are not used
     # for the pick: its sampled decode steps run eagerly (csrc/prof.h), which lengthens the GEMV
-    # launches it times (11-19 us live vs 7.9 us traced).
+    # launches it times (11-19 us live vs 7.4 us traced).
     roof = classes.get("gemm") or (max(classes.values(), key=lambda r: r["sampled_ms"]) if classes else None)
     if roof is not None:
         roof = dict(roof, dominant_by="rocprofv3 kernel-time share of the benched configuration "

@@ -9,6 +9,7 @@
 #include <cstring>
 
 #include "model_files.h"
+#include "prof.h"
 
 namespace wdr {
 
@@ -176,10 +177,10 @@ std::vector<int> SegModel::frame_classes(const int16_t* pcm, size_t n, std::vect
   for (int w0 = 0; w0 < nw; w0 += kSegBatch) {
     const int B = std::min(kSegBatch, nw - w0);
     // windows of the zero-padded buffer: raw int16 values as f32 (no 1/32768)
-    WDR_HIP(hipMemsetAsync(w.pcm.p, 0, (size_t)B * kWin * 2, s_));
+    WDR_HIP(wdr_memset_async(w.pcm.p, 0, (size_t)B * kWin * 2, s_));
     const size_t s0 = (size_t)w0 * kWin;
     const size_t avail = s0 < n ? std::min(n - s0, (size_t)B * kWin) : 0;
-    if (avail) WDR_HIP(hipMemcpyAsync(w.pcm.p, pcm + s0, avail * 2, hipMemcpyHostToDevice, s_));
+    if (avail) WDR_HIP(wdr_memcpy_async(w.pcm.p, pcm + s0, avail * 2, hipMemcpyHostToDevice, s_));
     launch_i16_scale(w.pcm.as<int16_t>(), (long long)B * kWin, 1.0f, w.x.as<float>(), s_);
     launch_inorm(w.x.as<float>(), kWin, kWin, 1, B, w.wn_g, w.wn_b, ACT_NONE, s_);
     // SincNet
@@ -216,10 +217,10 @@ std::vector<int> SegModel::frame_classes(const int16_t* pcm, size_t n, std::vect
     gemm(s_, w.la.as<float>(), 128, w.l1w, 128, w.lb.as<float>(), 128, B * kFrames, 128, 128, w.l1b, ACT_LRELU);
     gemm(s_, w.lb.as<float>(), 128, w.cw, 128, w.z.as<float>(), 7, B * kFrames, 7, 128, w.cb, ACT_NONE);
     launch_logsoftmax7(w.z.as<float>(), B * kFrames, w.cls.as<int>(), s_);
-    WDR_HIP(hipMemcpyAsync(cls.data() + (size_t)w0 * kFrames, w.cls.p, (size_t)B * kFrames * 4, hipMemcpyDeviceToHost,
+    WDR_HIP(wdr_memcpy_async(cls.data() + (size_t)w0 * kFrames, w.cls.p, (size_t)B * kFrames * 4, hipMemcpyDeviceToHost,
                            s_));
     if (logprobs)
-      WDR_HIP(hipMemcpyAsync(logprobs->data() + (size_t)w0 * kFrames * 7, w.z.p, (size_t)B * kFrames * 7 * 4,
+      WDR_HIP(wdr_memcpy_async(logprobs->data() + (size_t)w0 * kFrames * 7, w.z.p, (size_t)B * kFrames * 7 * 4,
                              hipMemcpyDeviceToHost, s_));
     WDR_HIP(hipStreamSynchronize(s_));   // host staging of the next batch reuses the buffers
   }
@@ -478,7 +479,7 @@ int CamModel::run_fbank(const int16_t* pcm, size_t n) {
     w.pcm = DevMem(n * 2);
     w.x = DevMem(n * 4);
   }
-  WDR_HIP(hipMemcpyAsync(w.pcm.p, pcm, n * 2, hipMemcpyHostToDevice, s_));
+  WDR_HIP(wdr_memcpy_async(w.pcm.p, pcm, n * 2, hipMemcpyHostToDevice, s_));
   launch_i16_scale(w.pcm.as<int16_t>(), (long long)n, 1.0f / 32768.0f, w.x.as<float>(), s_);
   launch_fbank(w.x.as<float>(), T, w.povey, w.cos_t, w.sin_t, w.banks, w.fb.as<float>(), s_);
   launch_colstats(w.fb.as<float>(), 80, T, 80, 0, nullptr, s_);   // CMN
@@ -489,7 +490,7 @@ std::vector<float> CamModel::feats(const int16_t* pcm, size_t n) {
   WDR_HIP(hipSetDevice(device));
   const int T = run_fbank(pcm, n);
   std::vector<float> out((size_t)T * 80);
-  if (T) WDR_HIP(hipMemcpyAsync(out.data(), w_->fb.p, out.size() * 4, hipMemcpyDeviceToHost, s_));
+  if (T) WDR_HIP(wdr_memcpy_async(out.data(), w_->fb.p, out.size() * 4, hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
   return out;
 }
@@ -557,7 +558,7 @@ void CamModel::embed_batch(const int16_t* const* pcm, const size_t* n, int B, fl
     w.x = DevMem(nsamp * 4);
     w.pcm_cap = nsamp;
   }
-  WDR_HIP(hipMemcpyAsync(w.tab.p, w.h_tab, (size_t)tab_n * 4, hipMemcpyHostToDevice, s_));
+  WDR_HIP(wdr_memcpy_async(w.tab.p, w.h_tab, (size_t)tab_n * 4, hipMemcpyHostToDevice, s_));
   const int* d = w.tab.as<int>();
   const SegRows sT{d, d + Bv + 1, Bv};
   const SegRows sT2{d + 2 * Bv + 1, d + 3 * Bv + 2, Bv};
@@ -567,7 +568,7 @@ void CamModel::embed_batch(const int16_t* const* pcm, const size_t* n, int B, fl
     size_t so = 0;
     for (int b = 0; b < Bv; ++b) {
       const int i = idx[b];
-      WDR_HIP(hipMemcpyAsync(w.pcm.as<int16_t>() + so, pcm[i], n[i] * 2, hipMemcpyHostToDevice, s_));
+      WDR_HIP(wdr_memcpy_async(w.pcm.as<int16_t>() + so, pcm[i], n[i] * 2, hipMemcpyHostToDevice, s_));
       so += n[i];
     }
     launch_i16_scale(w.pcm.as<int16_t>(), (long long)nsamp, 1.0f / 32768.0f, w.x.as<float>(), s_);
@@ -599,7 +600,7 @@ void CamModel::embed_batch(const int16_t* const* pcm, const size_t* n, int B, fl
       launch_im2col_2d_b(cur, sT, Tt, F, 32, 1, 1, 2, Fo, col, s_);
       gemm(s_, col, 32, R.sc, 32, res, 32, Tt * Fo, 32, 32, nullptr, ACT_NONE, R.scs, R.scb);
     } else {
-      WDR_HIP(hipMemcpyAsync(res, cur, (size_t)Tt * Fo * 32 * 4, hipMemcpyDeviceToDevice, s_));
+      WDR_HIP(wdr_memcpy_async(res, cur, (size_t)Tt * Fo * 32 * 4, hipMemcpyDeviceToDevice, s_));
     }
     // out = relu(bn2(conv2(y)) + shortcut)
     launch_im2col_2d_b(tmp, sT, Tt, Fo, 32, 3, 3, 1, Fo, col, s_);
@@ -651,7 +652,7 @@ void CamModel::embed_batch(const int16_t* const* pcm, const size_t* n, int B, fl
   gemm(s_, w.st.as<float>(), 2 * ch, w.dense, 2 * ch, w.emb.as<float>(), 512, Bv, 512, 2 * ch, nullptr, ACT_NONE,
        w.dens, w.denb);
   std::vector<float> e((size_t)Bv * 512);
-  WDR_HIP(hipMemcpyAsync(e.data(), w.emb.p, e.size() * 4, hipMemcpyDeviceToHost, s_));
+  WDR_HIP(wdr_memcpy_async(e.data(), w.emb.p, e.size() * 4, hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipEventRecord(e1_, s_));
   WDR_HIP(hipStreamSynchronize(s_));
   for (int b = 0; b < Bv; ++b) {

@@ -31,6 +31,23 @@ std::mutex* launch_lock();
 
 void prof_push(int cls, hipEvent_t a, hipEvent_t b, unsigned long long* ts, double bytes, double flops);
 
+// async copies / fills under WDR_LAUNCH_LOCK too: HIP runs them as blit kernels, whose
+// dispatches the profiler intercepts like any launch
+inline hipError_t wdr_memcpy_async(void* dst, const void* src, size_t n, hipMemcpyKind kind, hipStream_t s) {
+  std::mutex* mu = launch_lock();
+  if (mu) mu->lock();
+  const hipError_t e = hipMemcpyAsync(dst, src, n, kind, s);
+  if (mu) mu->unlock();
+  return e;
+}
+inline hipError_t wdr_memset_async(void* dst, int v, size_t n, hipStream_t s) {
+  std::mutex* mu = launch_lock();
+  if (mu) mu->lock();
+  const hipError_t e = hipMemsetAsync(dst, v, n, s);
+  if (mu) mu->unlock();
+  return e;
+}
+
 // a plain kernel launch under WDR_LAUNCH_LOCK (every launch site of libwdr goes through it or
 // wdr_launch, the graph replays through launch_lock() too)
 #define WDR_KLAUNCH(...)                                    \

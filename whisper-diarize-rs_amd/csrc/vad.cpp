@@ -6,6 +6,7 @@
 #include <cmath>
 
 #include "model_files.h"
+#include "prof.h"
 
 namespace wdr {
 
@@ -56,7 +57,7 @@ VadModel::VadModel(int dev, const std::string& path) : device(dev) {
     const std::vector<float>& b = file.at("stft");
     for (size_t i = 0; i < basis.size(); ++i) basis[i] = (f16)b[i];
   }
-  WDR_HIP(hipMemcpyAsync(b16 + L.stft, basis.data(), basis.size() * 2, hipMemcpyHostToDevice, s_));
+  WDR_HIP(wdr_memcpy_async(b16 + L.stft, basis.data(), basis.size() * 2, hipMemcpyHostToDevice, s_));
   const double sq3 = std::sqrt(3.0);
   // synthetic: seeded on the GPU; file: the tensor of that name (f16 matrices, f32 biases)
   auto fill = [&](void* dst, const std::string& nm, int n, bool is16, double sd) {
@@ -68,10 +69,10 @@ VadModel::VadModel(int dev, const std::string& path) : device(dev) {
     WDR_CHECK((int)v.size() == n, "VAD model: tensor size mismatch");
     if (is16) {
       staged16.emplace_back(v.begin(), v.end());
-      WDR_HIP(hipMemcpyAsync(dst, staged16.back().data(), (size_t)n * 2, hipMemcpyHostToDevice, s_));
+      WDR_HIP(wdr_memcpy_async(dst, staged16.back().data(), (size_t)n * 2, hipMemcpyHostToDevice, s_));
     } else {
       staged32.push_back(v);
-      WDR_HIP(hipMemcpyAsync(dst, staged32.back().data(), (size_t)n * 4, hipMemcpyHostToDevice, s_));
+      WDR_HIP(wdr_memcpy_async(dst, staged32.back().data(), (size_t)n * 4, hipMemcpyHostToDevice, s_));
     }
   };
   const char* cn[4] = {"_model.encoder.0.reparam_conv", "_model.encoder.1.reparam_conv",
@@ -114,12 +115,12 @@ std::vector<float> VadModel::probs(const int16_t* pcm, size_t n) {
     cap_ = n;
   }
   WDR_CHECK(n < (size_t)INT_MAX, "VAD: input too long");
-  WDR_HIP(hipMemcpyAsync(pcm_.p, pcm, n * 2, hipMemcpyHostToDevice, s_));
+  WDR_HIP(wdr_memcpy_async(pcm_.p, pcm, n * 2, hipMemcpyHostToDevice, s_));
   launch_i16_to_f32(pcm_.as<int16_t>(), (int)n, x_.as<float>(), s_);
   WDR_HIP(hipEventRecord(e0_, s_));
   launch_vad(x_.as<float>(), (long long)n, vw_, xg_.as<float>(), hout_.as<float>(), probs_.as<float>(), s_);
   WDR_HIP(hipEventRecord(e1_, s_));
-  WDR_HIP(hipMemcpyAsync(out.data(), probs_.p, nc * 4, hipMemcpyDeviceToHost, s_));
+  WDR_HIP(wdr_memcpy_async(out.data(), probs_.p, nc * 4, hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
   float ms = 0.f;
   WDR_HIP(hipEventElapsedTime(&ms, e0_, e1_));

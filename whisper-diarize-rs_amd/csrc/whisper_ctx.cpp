@@ -319,10 +319,10 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
     cs[i] = (float)std::cos(2.0 * M_PI * i / 400.0);
     sn[i] = (float)(-std::sin(2.0 * M_PI * i / 400.0));
   }
-  WDR_HIP(hipMemcpyAsync(m.mel_filters, filt.data(), filt.size() * 4, hipMemcpyHostToDevice, s));
-  WDR_HIP(hipMemcpyAsync(m.hann, hann.data(), 1600, hipMemcpyHostToDevice, s));
-  WDR_HIP(hipMemcpyAsync(m.cos_tab, cs.data(), 1600, hipMemcpyHostToDevice, s));
-  WDR_HIP(hipMemcpyAsync(m.sin_tab, sn.data(), 1600, hipMemcpyHostToDevice, s));
+  WDR_HIP(wdr_memcpy_async(m.mel_filters, filt.data(), filt.size() * 4, hipMemcpyHostToDevice, s));
+  WDR_HIP(wdr_memcpy_async(m.hann, hann.data(), 1600, hipMemcpyHostToDevice, s));
+  WDR_HIP(wdr_memcpy_async(m.cos_tab, cs.data(), 1600, hipMemcpyHostToDevice, s));
+  WDR_HIP(wdr_memcpy_async(m.sin_tab, sn.data(), 1600, hipMemcpyHostToDevice, s));
 
   // ---- DTW preset
   if (cp.dtw) {
@@ -338,7 +338,7 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
       for (int h : aheads_per_layer[l]) flat.push_back(h);
     }
     aheads_dev = DevMem(std::max<size_t>(4, flat.size() * 4));
-    if (!flat.empty()) WDR_HIP(hipMemcpyAsync(aheads_dev.p, flat.data(), flat.size() * 4, hipMemcpyHostToDevice, s));
+    if (!flat.empty()) WDR_HIP(wdr_memcpy_async(aheads_dev.p, flat.data(), flat.size() * 4, hipMemcpyHostToDevice, s));
   }
   WDR_HIP(hipStreamSynchronize(s));
   {
@@ -773,7 +773,7 @@ void State::compute_mel(const float* x_host, int n) {
   WDR_HIP(hipStreamWaitEvent(s_, m.ev_dtw, 0));   // the scratch slot may still feed a DTW job
   Impl::Slot& sl = m.slots[m.S];
   slot_reserve_x(sl, n);
-  if (n > 0) WDR_HIP(hipMemcpyAsync(sl.x.p, x_host, (size_t)n * 4, hipMemcpyHostToDevice, s_));
+  if (n > 0) WDR_HIP(wdr_memcpy_async(sl.x.p, x_host, (size_t)n * 4, hipMemcpyHostToDevice, s_));
   slot_mel(ctx_, m, sl, n, s_);
 }
 
@@ -782,7 +782,7 @@ void State::read_mel_window(int seek, float* out) {
   Impl::Slot& sl = m.slots[m.cur];
   DevMem tmp((size_t)m.n_mels * 3000 * 4);
   launch_mel_window(sl.mel.as<float>(), m.n_mels, sl.n_fft_frames, sl.gmax.as<int>(), seek, tmp.as<float>(), s_);
-  WDR_HIP(hipMemcpyAsync(out, tmp.p, tmp.bytes, hipMemcpyDeviceToHost, s_));
+  WDR_HIP(wdr_memcpy_async(out, tmp.p, tmp.bytes, hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
 }
 
@@ -872,7 +872,7 @@ void State::encode_from_mel_window(const float* w) {
         const int u = t + k - 1;
         if (u >= 0 && u < 3000) col[(size_t)t * m.kp1 + ci * 3 + k] = (f16)w[(size_t)ci * 3000 + u];
       }
-  WDR_HIP(hipMemcpyAsync(m.e1.im2col.p, col.data(), col.size() * 2, hipMemcpyHostToDevice, s_));
+  WDR_HIP(wdr_memcpy_async(m.e1.im2col.p, col.data(), col.size() * 2, hipMemcpyHostToDevice, s_));
   encoder_body(ctx_, m, m.e1, 1, const_cast<f16*>(m.xkv()), s_);
   WDR_HIP(hipStreamSynchronize(s_));
 }
@@ -884,7 +884,7 @@ void State::read_cross_kv(float* out) {
   const int L = ctx_.model.hp.n_text_layer, d = ctx_.model.hp.n_text_state, N = L * 2 * d;
   const size_t n = (size_t)XKV_T * N;
   std::vector<f16> h(n);
-  WDR_HIP(hipMemcpyAsync(h.data(), m.xkv(), n * 2, hipMemcpyDeviceToHost, s_));
+  WDR_HIP(wdr_memcpy_async(h.data(), m.xkv(), n * 2, hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
   for (int c = 0; c < N; ++c)
     for (int t = 0; t < XKV_T; ++t) out[(size_t)t * N + c] = (float)h[(size_t)(c >> 6) * XKV_HS + t * 64 + (c & 63)];
@@ -893,7 +893,7 @@ void State::read_cross_kv(float* out) {
 void State::read_encoder_out(float* out) {
   Impl& m = *m_;
   std::vector<f16> h((size_t)1500 * m.d);
-  WDR_HIP(hipMemcpyAsync(h.data(), m.e1.eh.p, h.size() * 2, hipMemcpyDeviceToHost, s_));
+  WDR_HIP(wdr_memcpy_async(h.data(), m.e1.eh.p, h.size() * 2, hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
   for (size_t i = 0; i < h.size(); ++i) out[i] = (float)h[i];
 }
@@ -967,7 +967,7 @@ void State::top_up(int j) {
       if (nk > 0) {
         // the staging buffer's previous H2D copy (segment k - S) completed before its decode
         memcpy(sl.h_pcm, m.plan.pcm[k], (size_t)nk * 2);
-        WDR_HIP(hipMemcpyAsync(sl.pcm.p, sl.h_pcm, (size_t)nk * 2, hipMemcpyHostToDevice, m.es));
+        WDR_HIP(wdr_memcpy_async(sl.pcm.p, sl.h_pcm, (size_t)nk * 2, hipMemcpyHostToDevice, m.es));
         launch_i16_to_f32(sl.pcm.as<int16_t>(), nk, sl.x.as<float>(), m.es);
       }
       slot_mel(ctx_, m, sl, nk, m.es);
@@ -984,7 +984,7 @@ void State::top_up(int j) {
       const int R = g1 - g0;
       const f16** hx = G.h_xkv + (size_t)(g0 % m.S) * kBatch;   // reused >= S segments later
       for (int r = 0; r < R; ++r) hx[r] = m.xkv_ring.as<f16>() + (size_t)((g0 + r) % m.S) * m.xkv_slot_elems;
-      WDR_HIP(hipMemcpyAsync(G.row_xkv.p, hx, R * sizeof(void*), hipMemcpyHostToDevice, m.es));
+      WDR_HIP(wdr_memcpy_async(G.row_xkv.p, hx, R * sizeof(void*), hipMemcpyHostToDevice, m.es));
       launch_embed(ctx_.model.tok_emb, ctx_.model.dec_pos, G.rows_tok.as<int>(), G.rows_pos.as<int>(), R, m.d,
                    G.xd.as<float>(), m.es);
       StepIO io{G.xd.as<float>(), G.qkvd.as<f16>(), G.attd.as<f16>(), G.qx.as<f16>(), G.mlpd.as<f16>(),
@@ -993,7 +993,7 @@ void State::top_up(int j) {
                 m.seq_stride, nullptr, G.row_xkv.as<const f16*>()};
       decode_step_layers(ctx_, io, R, m.es);
       for (int r = 0; r < R; ++r)
-        WDR_HIP(hipMemcpyAsync(m.h_lang + (size_t)((g0 + r) % m.S) * 100,
+        WDR_HIP(wdr_memcpy_async(m.h_lang + (size_t)((g0 + r) % m.S) * 100,
                                G.logits.as<float>() + (size_t)r * m.V + ctx_.vocab.sot + 1, 100 * 4,
                                hipMemcpyDeviceToHost, m.es));
     }
@@ -1022,9 +1022,9 @@ void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool c
     b.h_rows[RMAX + i] = i;
     b.h_rows[2 * RMAX + i] = seq;
   }
-  WDR_HIP(hipMemcpyAsync(b.rows_tok, b.h_rows, n * 4, hipMemcpyHostToDevice, st));
-  WDR_HIP(hipMemcpyAsync(b.rows_pos, b.h_rows + RMAX, n * 4, hipMemcpyHostToDevice, st));
-  WDR_HIP(hipMemcpyAsync(b.rows_seq, b.h_rows + 2 * RMAX, n * 4, hipMemcpyHostToDevice, st));
+  WDR_HIP(wdr_memcpy_async(b.rows_tok, b.h_rows, n * 4, hipMemcpyHostToDevice, st));
+  WDR_HIP(wdr_memcpy_async(b.rows_pos, b.h_rows + RMAX, n * 4, hipMemcpyHostToDevice, st));
+  WDR_HIP(wdr_memcpy_async(b.rows_seq, b.h_rows + 2 * RMAX, n * 4, hipMemcpyHostToDevice, st));
   launch_embed(md.tok_emb, md.dec_pos, b.rows_tok, b.rows_pos, n, d, b.xd, st);
   const float scale = 1.0f / 8.0f;
   const int H = hp.n_text_head;
@@ -1216,7 +1216,7 @@ void decode_step_layers(const Context& ctx, const StepIO& io, int R, hipStream_t
 void State::step_err_check() {
   Impl& m = *m_;
   if (!m.h_err || !*(volatile int*)m.h_err) return;
-  WDR_HIP(hipMemsetAsync(m.st_ctr.p, 0, m.st_ctr.bytes, s_));
+  WDR_HIP(wdr_memset_async(m.st_ctr.p, 0, m.st_ctr.bytes, s_));
   WDR_HIP(hipStreamSynchronize(s_));
   *(volatile int*)m.h_err = 0;
   throw std::runtime_error("persistent decode step: a hand-off wait timed out");
@@ -1230,9 +1230,9 @@ void State::decoder_step(const int* toks, const int* seqs, const int* pos, int R
     m.h_rows[RMAX + i] = pos[i];
     m.h_rows[2 * RMAX + i] = seqs[i];
   }
-  WDR_HIP(hipMemcpyAsync(m.rows_tok.p, m.h_rows, R * 4, hipMemcpyHostToDevice, s_));
-  WDR_HIP(hipMemcpyAsync(m.rows_pos.p, m.h_rows + RMAX, R * 4, hipMemcpyHostToDevice, s_));
-  WDR_HIP(hipMemcpyAsync(m.rows_seq.p, m.h_rows + 2 * RMAX, R * 4, hipMemcpyHostToDevice, s_));
+  WDR_HIP(wdr_memcpy_async(m.rows_tok.p, m.h_rows, R * 4, hipMemcpyHostToDevice, s_));
+  WDR_HIP(wdr_memcpy_async(m.rows_pos.p, m.h_rows + RMAX, R * 4, hipMemcpyHostToDevice, s_));
+  WDR_HIP(wdr_memcpy_async(m.rows_seq.p, m.h_rows + 2 * RMAX, R * 4, hipMemcpyHostToDevice, s_));
   decoder_step_body(R);
   times.decode_steps++;
 }
@@ -1270,18 +1270,18 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
     hipGraph_t graph;
     prof_capture(true);
     WDR_HIP(hipStreamBeginCapture(s_, hipStreamCaptureModeThreadLocal));
-    WDR_HIP(hipMemcpyAsync(m.rows_tok.p, m.h_rows, R * 4, hipMemcpyHostToDevice, s_));
-    WDR_HIP(hipMemcpyAsync(m.rows_pos.p, m.h_rows + RMAX, R * 4, hipMemcpyHostToDevice, s_));
-    WDR_HIP(hipMemcpyAsync(m.rows_seq.p, m.h_rows + 2 * RMAX, R * 4, hipMemcpyHostToDevice, s_));
-    WDR_HIP(hipMemcpyAsync(m.ctl.p, m.h_ctl, R * sizeof(LogitsCtl), hipMemcpyHostToDevice, s_));
+    WDR_HIP(wdr_memcpy_async(m.rows_tok.p, m.h_rows, R * 4, hipMemcpyHostToDevice, s_));
+    WDR_HIP(wdr_memcpy_async(m.rows_pos.p, m.h_rows + RMAX, R * 4, hipMemcpyHostToDevice, s_));
+    WDR_HIP(wdr_memcpy_async(m.rows_seq.p, m.h_rows + 2 * RMAX, R * 4, hipMemcpyHostToDevice, s_));
+    WDR_HIP(wdr_memcpy_async(m.ctl.p, m.h_ctl, R * sizeof(LogitsCtl), hipMemcpyHostToDevice, s_));
     decoder_step_body(R);
     launch_logits_process(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, m.work.as<float>(),
                           m.tokout.as<TokOut>(), s_);
-    WDR_HIP(hipMemcpyAsync(m.h_tok, m.tokout.p, R * sizeof(TokOut), hipMemcpyDeviceToHost, s_));
+    WDR_HIP(wdr_memcpy_async(m.h_tok, m.tokout.p, R * sizeof(TokOut), hipMemcpyDeviceToHost, s_));
     if (K > 0) {
       launch_logits_topk(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, K, m.work.as<float>(),
                          m.beamc.as<BeamCand>(), s_);
-      WDR_HIP(hipMemcpyAsync(m.h_beam, m.beamc.p, (size_t)R * K * sizeof(BeamCand), hipMemcpyDeviceToHost, s_));
+      WDR_HIP(wdr_memcpy_async(m.h_beam, m.beamc.p, (size_t)R * K * sizeof(BeamCand), hipMemcpyDeviceToHost, s_));
     }
     prof_capture(false);
     WDR_HIP(hipStreamEndCapture(s_, &graph));
@@ -1322,10 +1322,10 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
 void State::run_logits(int R, const LogitsCtl* ctl, TokenData* out, float* nosp) {
   Impl& m = *m_;
   memcpy(m.h_ctl, ctl, R * sizeof(LogitsCtl));
-  WDR_HIP(hipMemcpyAsync(m.ctl.p, m.h_ctl, R * sizeof(LogitsCtl), hipMemcpyHostToDevice, s_));
+  WDR_HIP(wdr_memcpy_async(m.ctl.p, m.h_ctl, R * sizeof(LogitsCtl), hipMemcpyHostToDevice, s_));
   launch_logits_process(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, m.work.as<float>(),
                         m.tokout.as<TokOut>(), s_);
-  WDR_HIP(hipMemcpyAsync(m.h_tok, m.tokout.p, R * sizeof(TokOut), hipMemcpyDeviceToHost, s_));
+  WDR_HIP(wdr_memcpy_async(m.h_tok, m.tokout.p, R * sizeof(TokOut), hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
   step_err_check();
   for (int r = 0; r < R; ++r) {
@@ -1347,7 +1347,7 @@ void State::logits_topk(int R, int K, BeamCand* out) {
   Impl& m = *m_;
   launch_logits_topk(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, K, m.work.as<float>(),
                      m.beamc.as<BeamCand>(), s_);
-  WDR_HIP(hipMemcpyAsync(m.h_beam, m.beamc.p, (size_t)R * K * sizeof(BeamCand), hipMemcpyDeviceToHost, s_));
+  WDR_HIP(wdr_memcpy_async(m.h_beam, m.beamc.p, (size_t)R * K * sizeof(BeamCand), hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
   memcpy(out, m.h_beam, (size_t)R * K * sizeof(BeamCand));
 }
@@ -1366,7 +1366,7 @@ void State::kv_reorder(const std::vector<std::pair<int, int>>& moves, int n_rows
     m.h_pairs[2 * NSEQ + 2 * i] = NSEQ + moves[i].second;
     m.h_pairs[2 * NSEQ + 2 * i + 1] = moves[i].second;
   }
-  WDR_HIP(hipMemcpyAsync(m.kvpairs.p, m.h_pairs, 4 * NSEQ * 4, hipMemcpyHostToDevice, s_));
+  WDR_HIP(wdr_memcpy_async(m.kvpairs.p, m.h_pairs, 4 * NSEQ * 4, hipMemcpyHostToDevice, s_));
   launch_kv_copy(m.kc, m.vc, m.seq_stride, m.nslot_tot, m.L, m.kvpairs.as<int>(), n, n_rows, m.d, s_);
   launch_kv_copy(m.kc, m.vc, m.seq_stride, m.nslot_tot, m.L, m.kvpairs.as<int>() + 2 * NSEQ, n, n_rows,
                  m.d, s_);
@@ -1389,7 +1389,7 @@ void State::dbg_step(const int* toks, int n, bool classic, float* logits_out) {
     throw;
   }
   m.st_on = on;
-  WDR_HIP(hipMemcpyAsync(logits_out, m.logits.p, (size_t)m.V * 4, hipMemcpyDeviceToHost, s_));
+  WDR_HIP(wdr_memcpy_async(logits_out, m.logits.p, (size_t)m.V * 4, hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
   step_err_check();
 }
@@ -1453,14 +1453,14 @@ int State::step_trace(uint64_t* out, int cap) {
 
 void State::decode_logits(const int* toks, int n, float* logits_out) {
   decoder_prefill(toks, n, 0, true, false);
-  WDR_HIP(hipMemcpyAsync(logits_out, m_->logits.p, (size_t)m_->V * 4, hipMemcpyDeviceToHost, s_));
+  WDR_HIP(wdr_memcpy_async(logits_out, m_->logits.p, (size_t)m_->V * 4, hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
 }
 
 void State::dtw_capture(const int* toks, int n, float* cap_out) {
   decoder_prefill(toks, n, 0, false, true);
   const size_t A = ctx_.aheads.size();
-  WDR_HIP(hipMemcpyAsync(cap_out, m_->cap.p, A * n * 1500 * 4, hipMemcpyDeviceToHost, s_));
+  WDR_HIP(wdr_memcpy_async(cap_out, m_->cap.p, A * n * 1500 * 4, hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
 }
 
@@ -1631,7 +1631,7 @@ void State::dtw_timestamps(int i_segment, int n_segments, int seek, int n_frames
   Impl::DtwSet& D = m.dset;
   launch_dtw(D.cap.as<float>(), (int)ctx_.aheads.size(), N, 1500, n_audio, sot_len, seek, D.nrm.as<float>(),
              D.xdtw.as<float>(), D.times.as<int>(), D.times.as<int>() + RMAX + 4, m.sd);
-  WDR_HIP(hipMemcpyAsync(job.blk + 3 * RMAX, D.times.p, (RMAX + 8) * 4, hipMemcpyDeviceToHost, m.sd));
+  WDR_HIP(wdr_memcpy_async(job.blk + 3 * RMAX, D.times.p, (RMAX + 8) * 4, hipMemcpyDeviceToHost, m.sd));
   WDR_HIP(hipEventRecord(job.done, m.sd));
   WDR_HIP(hipEventRecord(m.ev_dtw, m.sd));
 }
@@ -1959,8 +1959,8 @@ Seq State::decode_sample(const std::vector<int>& prompt, const FullParams& param
     }
     launch_logits_probs(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, m.work.as<float>(),
                         m.sprobs.as<float>(), m.slogp.as<float>(), s_);
-    WDR_HIP(hipMemcpyAsync(m.hp_probs.data(), m.sprobs.p, (size_t)R * V * 4, hipMemcpyDeviceToHost, s_));
-    WDR_HIP(hipMemcpyAsync(m.hp_logp.data(), m.slogp.p, (size_t)R * V * 4, hipMemcpyDeviceToHost, s_));
+    WDR_HIP(wdr_memcpy_async(m.hp_probs.data(), m.sprobs.p, (size_t)R * V * 4, hipMemcpyDeviceToHost, s_));
+    WDR_HIP(wdr_memcpy_async(m.hp_logp.data(), m.slogp.p, (size_t)R * V * 4, hipMemcpyDeviceToHost, s_));
     WDR_HIP(hipStreamSynchronize(s_));
     for (size_t a = 0; a < act.size(); ++a) {
       const int j = act[a];
@@ -2097,7 +2097,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
         m.energy_cap = n;
       }
       launch_energy(m.slots[m.cur].x.as<float>(), n, m.energy_d.as<float>(), s_);
-      WDR_HIP(hipMemcpyAsync(energy.data(), m.energy_d.p, (size_t)n * 4, hipMemcpyDeviceToHost, s_));
+      WDR_HIP(wdr_memcpy_async(energy.data(), m.energy_d.p, (size_t)n * 4, hipMemcpyDeviceToHost, s_));
     }
   }
   WDR_HIP(hipStreamSynchronize(s_));
@@ -2132,7 +2132,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
     } else {
       const int sot = v.sot;
       decoder_prefill(&sot, 1, 0, true, false);
-      WDR_HIP(hipMemcpyAsync(ll.data(), m.logits.as<float>() + v.sot + 1, 100 * 4, hipMemcpyDeviceToHost, s_));
+      WDR_HIP(wdr_memcpy_async(ll.data(), m.logits.as<float>() + v.sot + 1, 100 * 4, hipMemcpyDeviceToHost, s_));
       WDR_HIP(hipStreamSynchronize(s_));
     }
     int best = 0;
@@ -2517,25 +2517,25 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
     io.lead = m.lead.as<int>();
   }
   auto body = [&]() {
-    WDR_HIP(hipMemcpyAsync(m.rows_tok.p, m.h_rows, R * 4, hipMemcpyHostToDevice, m.s));
-    WDR_HIP(hipMemcpyAsync(m.rows_pos.p, m.h_rows + RB, R * 4, hipMemcpyHostToDevice, m.s));
-    WDR_HIP(hipMemcpyAsync(m.rows_seq.p, m.h_rows + 2 * RB, R * 4, hipMemcpyHostToDevice, m.s));
+    WDR_HIP(wdr_memcpy_async(m.rows_tok.p, m.h_rows, R * 4, hipMemcpyHostToDevice, m.s));
+    WDR_HIP(wdr_memcpy_async(m.rows_pos.p, m.h_rows + RB, R * 4, hipMemcpyHostToDevice, m.s));
+    WDR_HIP(wdr_memcpy_async(m.rows_seq.p, m.h_rows + 2 * RB, R * 4, hipMemcpyHostToDevice, m.s));
     if (grouped) {
-      WDR_HIP(hipMemcpyAsync(m.grp.p, m.h_rows + 3 * RB, R * 4, hipMemcpyHostToDevice, m.s));
-      WDR_HIP(hipMemcpyAsync(m.lead.p, m.h_rows + 4 * RB, io.n_grp * 4, hipMemcpyHostToDevice, m.s));
+      WDR_HIP(wdr_memcpy_async(m.grp.p, m.h_rows + 3 * RB, R * 4, hipMemcpyHostToDevice, m.s));
+      WDR_HIP(wdr_memcpy_async(m.lead.p, m.h_rows + 4 * RB, io.n_grp * 4, hipMemcpyHostToDevice, m.s));
     }
-    WDR_HIP(hipMemcpyAsync(m.ctl.p, m.h_ctl, R * sizeof(LogitsCtl), hipMemcpyHostToDevice, m.s));
-    WDR_HIP(hipMemcpyAsync(m.row_xkv.p, m.h_xkv, R * sizeof(void*), hipMemcpyHostToDevice, m.s));
+    WDR_HIP(wdr_memcpy_async(m.ctl.p, m.h_ctl, R * sizeof(LogitsCtl), hipMemcpyHostToDevice, m.s));
+    WDR_HIP(wdr_memcpy_async(m.row_xkv.p, m.h_xkv, R * sizeof(void*), hipMemcpyHostToDevice, m.s));
     launch_embed(ctx_.model.tok_emb, ctx_.model.dec_pos, m.rows_tok.as<int>(), m.rows_pos.as<int>(), R, m.d,
                  m.xd.as<float>(), m.s);
     decode_step_layers(ctx_, io, R, m.s);
     launch_logits_process(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), vids, R, m.work.as<float>(),
                           m.tokout.as<TokOut>(), m.s);
-    WDR_HIP(hipMemcpyAsync(m.h_tok, m.tokout.p, R * sizeof(TokOut), hipMemcpyDeviceToHost, m.s));
+    WDR_HIP(wdr_memcpy_async(m.h_tok, m.tokout.p, R * sizeof(TokOut), hipMemcpyDeviceToHost, m.s));
     if (K > 0) {
       launch_logits_topk(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), vids, R, K, m.work.as<float>(),
                          m.beamc.as<BeamCand>(), m.s);
-      WDR_HIP(hipMemcpyAsync(m.h_beam, m.beamc.p, (size_t)R * K * sizeof(BeamCand), hipMemcpyDeviceToHost, m.s));
+      WDR_HIP(wdr_memcpy_async(m.h_beam, m.beamc.p, (size_t)R * K * sizeof(BeamCand), hipMemcpyDeviceToHost, m.s));
     }
   };
   const double t_step = now_s();
