@@ -1818,6 +1818,12 @@ static int gemm4_mode() {
   return e ? atoi(e) : -1;
 }
 
+// WDR_GEMM4_GM: row tiles per group of the k_gemm4 / k_gemm5 tile order (default 4: qkv and
+// cross-K/V 1 % faster than row-major in tools/gemm_bench); read per call (A/B runs)
+static int gemm_tile_gm() {
+  const char* e = getenv("WDR_GEMM4_GM");
+  return e ? atoi(e) : 4;
+}
 // WDR_GEMM5=0: the narrow encoder projections on k_gemm4's 256 x 256 tiles (A/B); read per call
 static bool gemm5_on() {
   const char* e = getenv("WDR_GEMM5");
@@ -1999,8 +2005,7 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
     }();
     (void)attr5;
     ProjArgs g = a;
-    const char* e = getenv("WDR_GEMM4_GM");
-    g.tile_gm = e ? atoi(e) : 4;
+    g.tile_gm = gemm_tile_gm();
     dim3 grid((a.N / 128) * cdiv(a.M, G3_M));
     wdr_launch(PROF_GEMM, bytes, flops, k_gemm5<EPI>, grid, dim3(512), G5_LDS, s, g);
   } else if (a.N % G3_N == 0 && a.K % G3_BK == 0 && !gemm1_forced() &&
@@ -2024,8 +2029,7 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
     }();
     dim3 grid(cus > 0 && cus < ntiles ? cus : ntiles);
     ProjArgs g = a;
-    const char* e = getenv("WDR_GEMM4_GM");
-    g.tile_gm = e ? atoi(e) : 4;   // grouped order: qkv, cross-K/V 1 % faster (gemm_bench)
+    g.tile_gm = gemm_tile_gm();
     wdr_launch(PROF_GEMM, bytes, flops, k_gemm4<EPI>, grid, dim3(512), G4_LDS, s, g);
   } else if ((a.N >= 5120 || a.M >= 9000) && a.M > 2048 && a.N % G3_N == 0 && a.K % G3_BK == 0 && gemm3_enabled()) {
     // 256 x 256 tiles where they measured faster (tools/gemm_bench, large-v3 shapes): M = 6000
@@ -2092,7 +2096,11 @@ static bool launch_mgemv_passes_epi(const ProjArgs& a, hipStream_t s) {
 }
 
 static bool launch_mgemv_passes(const ProjArgs& a, hipStream_t s) {
-  if (getenv("WDR_MGEMV_PASSES") && atoi(getenv("WDR_MGEMV_PASSES")) == 0) return false;
+  static const bool on = [] {
+    const char* e = getenv("WDR_MGEMV_PASSES");
+    return !(e && atoi(e) == 0);
+  }();
+  if (!on) return false;
   switch (a.epi) {
     case EPI_F16: return launch_mgemv_passes_epi<EPI_F16>(a, s);
     case EPI_F16_GELU: return launch_mgemv_passes_epi<EPI_F16_GELU>(a, s);
