@@ -338,16 +338,14 @@ int wdr_dbg_encode(wdr_context* c, const float* mel_window /* [n_mels][3000] */,
 /* cross K/V of the last wdr_dbg_encode window: [1500][n_text_layer][2 (K, V)][d] (f16 -> f32) */
 int wdr_dbg_cross_kv(wdr_context* c, float* out);
 int wdr_dbg_decode(wdr_context* c, const int32_t* tokens, size_t n, float* logits_out /* [n_vocab] */);
-/* prefill tokens[0..n-2], then one decode step of tokens[n-1]; mode 0 = the persistent
- * one-launch step (error if the model width has none), 1 = the per-kernel chain */
-int wdr_dbg_step(wdr_context* c, const int32_t* tokens, size_t n, int32_t mode, float* logits_out /* [n_vocab] */);
-/* timeline of the last persistent step (WDR_STEP_TRACE=1 at context creation): wall_clock64
- * stamps [67][n_wg] (layer < 4: 16 events per layer; 64 start, 65 logits ready, 66 end) */
+/* prefill tokens[0..n-2], then one decode step of tokens[n-1] (its logits); the decoder-rows
+ * contract makes them bit-identical to the n-token prefill's for n <= 8 (larger prefills run
+ * their cross-attention on the MFMA tile kernel) */
+int wdr_dbg_step(wdr_context* c, const int32_t* tokens, size_t n, float* logits_out /* [n_vocab] */);
 /* multi-chain batched step (StepBatcher) with `rows` rows on the last encoded window, `iters`
  * times after prefilling tokens[0..n-2]: host milliseconds per step (probe seam) */
 int wdr_dbg_batch_step(wdr_context* c, const int32_t* tokens, size_t n, int32_t rows, int32_t iters,
                        double* ms_per_step);
-int wdr_dbg_step_trace(wdr_context* c, uint64_t* out, int32_t cap, int32_t* n_wg);
 int wdr_dbg_capture(wdr_context* c, const int32_t* tokens, size_t n, float* cap_out /* [n_aheads][n][1500] */);
 int wdr_dbg_dtw(const float* cap, int32_t n_heads, int32_t n_tok, int32_t n_audio, int32_t sot_len, int32_t seek,
                 float* x_out /* [n_tok-sot_len-1][n_audio] */, int32_t* times_out, int32_t* n_times);

@@ -1,13 +1,12 @@
-"""The persistent one-launch decode step (kernels/step.hip) against the per-kernel chain it
-replaces and against the CPU oracle.
+"""The decoder-rows contract (csrc/rows.h) on the GPU: a decode step is a row like any other.
 
-Both HIP paths compute f16 operands with f32 accumulation but in different summation orders
-(the step's LayerNorm is a workgroup reduction, the chain's a per-wave one), so logits are
-compared relative to their spread: |err| <= 0.01 * std + 0.01, same argmax.  Widths cover
-every instantiation the bench and tests use: tiny-test (d 128), base.en (d 512) and large-v3
-(d 1280, 20 heads, 32 layers)."""
-import os
-
+A prefill of n tokens followed by nothing, and a prefill of n-1 tokens followed by ONE decode
+step of the n-th, compute the n-th row with the same kernels: bit-identical logits while the
+prefill's rows form a VALU cross-attention group (n <= 8); above that the prefill's
+cross-attention runs on the MFMA tile kernel (a different summation order), so the logits are
+compared relative to their spread (|err| <= 0.01 * std + 0.01, same argmax).  The step is also
+checked against the CPU oracle.  Widths: tiny-test (d 128), base.en (d 512), large-v3 (d 1280,
+20 heads, 32 layers)."""
 import numpy as np
 import pytest
 
@@ -19,16 +18,6 @@ from oracle.weights import hparams_for, synth_weights
 pytestmark = pytest.mark.gpu
 
 
-def _ctx(name, emb_std):
-    # the persistent step is opt-in (slower than the kernel chain on MI355X):
-    # enable it for the contexts of this module only
-    os.environ["WDR_PSTEP"] = "1"
-    try:
-        return wdr.WhisperContext(name, synthetic=wdr.Synthetic(weight_std=0.02, emb_std=emb_std))
-    finally:
-        del os.environ["WDR_PSTEP"]
-
-
 def _close(a, b):
     scale = float(b.std())
     err = float(np.abs(a - b).max())
@@ -36,33 +25,36 @@ def _close(a, b):
 
 
 @pytest.mark.parametrize("name", ["tiny-test", "base.en", "large-v3"])
-def test_persistent_step_matches_kernel_chain(name):
-    ctx = _ctx(name, 0.5)
+def test_step_row_equals_prefill_row(name):
+    ctx = wdr.WhisperContext(name, synthetic=wdr.Synthetic(weight_std=0.02, emb_std=0.5))
     hp = ctx.hparams
     rng = np.random.default_rng(3)
     mel = (rng.standard_normal((hp["n_mels"], 3000)) * 0.4).astype(np.float32)
     ctx.encode(mel)
     v = Vocab(hp["n_vocab"])
-    seqs = [[v.sot, v.beg], [v.sot, v.beg, 1234, 40000, 77],
+    seqs = [[v.sot, v.beg], [v.sot, v.beg, 1234, 40000, 77], list(rng.integers(0, 50000, 8)),
             list(rng.integers(0, 50000, 37)), list(rng.integers(0, 50000, 300)),
             list(rng.integers(0, 50000, 448))]
     for toks in seqs:
-        got = ctx.step(toks)
-        ref = ctx.step(toks, classic=True)
-        assert np.isfinite(got).all()
-        _close(got, ref)
-        assert int(np.argmax(got)) == int(np.argmax(ref))
-    # back-to-back launches: the counters are reset by the last workgroup of every launch
+        step = ctx.step(toks)
+        pre = ctx.decode(toks)
+        assert np.isfinite(step).all()
+        if len(toks) <= 8:
+            np.testing.assert_array_equal(step, pre)
+        else:
+            _close(step, pre)
+            assert int(np.argmax(step)) == int(np.argmax(pre))
+    # back-to-back: the same inputs give the same bits
     toks = [v.sot, v.beg, 500, 600]
     first = ctx.step(toks)
-    for _ in range(20):
+    for _ in range(10):
         np.testing.assert_array_equal(ctx.step(toks), first)
     ctx.close()
 
 
-def test_persistent_step_matches_oracle():
+def test_step_matches_oracle():
     name = "tiny-test"
-    ctx = _ctx(name, 0.5)
+    ctx = wdr.WhisperContext(name, synthetic=wdr.Synthetic(weight_std=0.02, emb_std=0.5))
     hp = hparams_for(name)
     W = synth_weights(hp, std=0.02, emb_std=0.5)
     rng = np.random.default_rng(12)

@@ -102,6 +102,12 @@ struct ProjArgs {
   const float* a_scale = nullptr; const float* b_scale = nullptr;
   // k_gemm4 tile order: groups of tile_gm row tiles walked column by column (0: row-major)
   int tile_gm = 0;
+  // decoder rows of any count (steps, prompt prefills, DTW re-forwards) on the row kernel
+  // (k_skinny's arithmetic: 8 waves split K, fixed k order, fixed wave order in the reduce), so
+  // a row's result never depends on how many rows share the launch; LN needs M <= 32
+  int rows_mma = 0;
+  // optional row map: A / ln_x row m is row_map[m] (logit rows gathered from the residual stream)
+  const int* row_map = nullptr;
 };
 
 // Live kernel clock (csrc/prof.cpp): a launch the profiler samples carries ts -> {earliest wave

@@ -491,10 +491,18 @@ static std::unique_ptr<wdr_context> make_context(const std::string& model_name, 
   if (has_dev) {
     c->devices = {dev};
   } else if (const char* e = getenv("WDR_DEVICES")) {
+    // validated here, not later as HIP errors: ordinals of visible GPUs, at most 8 entries
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n < 1) throw std::runtime_error("WDR_DEVICES: no visible GPU");
     for (const char* q = e; *q;) {
-      c->devices.push_back(atoi(q));
-      while (*q && *q != ',') ++q;
-      if (*q == ',') ++q;
+      char* end = nullptr;
+      const long g = strtol(q, &end, 10);
+      if (end == q || g < 0 || g >= n || (*end && *end != ','))
+        throw std::runtime_error(std::string("WDR_DEVICES: bad device list '") + e + "' (" + std::to_string(n) +
+                                 " visible GPUs)");
+      if (c->devices.size() >= 8) throw std::runtime_error("WDR_DEVICES: at most 8 devices");
+      c->devices.push_back((int)g);
+      q = *end == ',' ? end + 1 : end;
     }
   } else {
     int n = 0;
@@ -1874,10 +1882,9 @@ int wdr_dbg_decode(wdr_context* c, const int32_t* tokens, size_t n, float* logit
   })
 }
 
-int wdr_dbg_step(wdr_context* c, const int32_t* tokens, size_t n, int32_t mode, float* logits_out) {
+int wdr_dbg_step(wdr_context* c, const int32_t* tokens, size_t n, float* logits_out) {
   WDR_GUARD({
-    if (mode == 0 && !c->st->persistent_step()) return fail("persistent step not available for this model");
-    c->st->dbg_step(tokens, (int)n, mode != 0, logits_out);
+    c->st->dbg_step(tokens, (int)n, logits_out);
     return 0;
   })
 }
@@ -1886,13 +1893,6 @@ int wdr_dbg_batch_step(wdr_context* c, const int32_t* tokens, size_t n, int32_t 
                        double* ms_per_step) {
   WDR_GUARD({
     *ms_per_step = c->st->dbg_batch_step(tokens, (int)n, rows, iters);
-    return 0;
-  })
-}
-
-int wdr_dbg_step_trace(wdr_context* c, uint64_t* out, int32_t cap, int32_t* n_wg) {
-  WDR_GUARD({
-    *n_wg = c->st->step_trace(out, cap);
     return 0;
   })
 }

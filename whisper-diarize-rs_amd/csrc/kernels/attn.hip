@@ -310,6 +310,7 @@ __global__ __launch_bounds__(256) void k_xattn_partial(XAttnArgs a) {
     r0 = a.lead ? a.lead[blockIdx.z] : blockIdx.z;
     nr = a.grp ? a.grp[r0] : 1;
     if (nr == 0) return;   // a row of a group led by an earlier row
+    if (a.lend && a.layer >= a.lend[r0]) return;   // a DTW re-forward past its last head layer
     kb = a.row_k[r0] + a.layer_off;
     vb = kb + a.v_off;
   }
@@ -385,6 +386,126 @@ __global__ __launch_bounds__(64) void k_xattn_combine(XAttnArgs a) {
 #pragma unroll
   for (int c = 0; c < NS; ++c) acc += po[c] * __shfl(w, c, 64);
   a.o[(long long)r * a.ldo + h * 64 + d] = (f16)(acc / L);
+  if (a.ml_out && d == 0) a.ml_out[(long long)r * a.n_head + h] = make_float2(M, L);
+}
+
+// ---------------------------------------------------------------- cross-attention, MFMA row tiles
+// The rows of a prompt prefill or a DTW re-forward (more than XATTN_GRP_MAX rows sharing one
+// cross-K/V slot): one workgroup per (64-key chunk, head, tile of <= 128 rows); the chunk's K
+// and V^T are staged in LDS once and each wave scores 32 rows with k_flash_attn's swapped
+// product S^T = K.Q^T (v_mfma_f32_32x32x16_f16: a row's scores depend only on its own query),
+// takes the chunk's max / sum per row and P.V (P rounded to f16, as the VALU kernel) into the
+// same partial layout as k_xattn_partial, so k_xattn_combine merges both kinds.
+__global__ __launch_bounds__(256) void k_xattn_mma(XAttnArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
+  __shared__ __attribute__((aligned(16))) f16 Ks[FA_KB * FA_KS];
+  __shared__ __attribute__((aligned(16))) f16 Vt[64 * FA_VS];
+  const int c = blockIdx.x, h = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int4 t = a.tiles[blockIdx.z];
+  if (a.layer >= t.z) return;   // a DTW re-forward past its last head layer
+  const f16* kb = a.row_k[t.x] + a.layer_off + h * a.hs;
+  const f16* vb = kb + a.v_off;
+  const int key0 = c * FA_KB;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = tid + 256 * i;
+    const int r = e >> 3, col = (e & 7) * 8;
+    int key = key0 + r;
+    key = key < a.Tk ? key : a.Tk - 1;
+    const f16x8 kr = *(const f16x8*)(kb + (long long)key * a.ldkv + col);
+    const f16x8 vr = *(const f16x8*)(vb + (long long)key * a.ldkv + col);
+    *(f16x8*)(Ks + r * FA_KS + col) = kr;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Vt[(col + j) * FA_VS + r] = vr[j];
+  }
+  __syncthreads();
+  if (32 * wid >= t.y) return;   // no barrier below: idle waves leave
+  const int fr = lane & 31, hh = lane >> 5;
+  const int ql = 32 * wid + fr;
+  const int qrow = t.x + (ql < t.y ? ql : t.y - 1);
+  f16x8 qf[4];
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) qf[s4] = *(const f16x8*)(a.q + (long long)qrow * a.ldq + h * 64 + 16 * s4 + 8 * hh);
+  f32x16 st[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) st[u][r] = 0.f;
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const f16x8 af = *(const f16x8*)(Ks + (32 * u + fr) * FA_KS + 16 * s4 + 8 * hh);
+      st[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, qf[s4], st[u], 0, 0, 0);
+    }
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = key0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      const float sv = key < a.Tk ? st[u][r] * a.scale : -INFINITY;
+      st[u][r] = sv;
+      mx = fmaxf(mx, sv);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float rs = 0.f;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = st[u][r] == -INFINITY ? 0.f : __expf(st[u][r] - mx);
+      st[u][r] = p;
+      rs += p;
+    }
+  rs += __shfl_xor(rs, 32, 64);
+  f32x16 o0, o1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; }
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      f16x8 pb;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pb[j] = (f16)st[u][8 * s2 + j];
+      const int kc = 32 * u + 16 * s2 + 4 * hh;
+      const f16x4 lo0 = *(const f16x4*)(Vt + fr * FA_VS + kc), hi0 = *(const f16x4*)(Vt + fr * FA_VS + kc + 8);
+      const f16x4 lo1 = *(const f16x4*)(Vt + (32 + fr) * FA_VS + kc), hi1 = *(const f16x4*)(Vt + (32 + fr) * FA_VS + kc + 8);
+      const f16x8 va0 = {lo0[0], lo0[1], lo0[2], lo0[3], hi0[0], hi0[1], hi0[2], hi0[3]};
+      const f16x8 va1 = {lo1[0], lo1[1], lo1[2], lo1[3], hi1[0], hi1[1], hi1[2], hi1[3]};
+      o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(va0, pb, o0, 0, 0, 0);
+      o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(va1, pb, o1, 0, 0, 0);
+    }
+  if (ql >= t.y) return;
+  const long long cr = (long long)c * a.R + t.x + ql;
+  float* po = a.part_o + (cr * a.n_head + h) * 64;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    *(float4*)(po + 8 * g + 4 * hh) = make_float4(o0[4 * g], o0[4 * g + 1], o0[4 * g + 2], o0[4 * g + 3]);
+    *(float4*)(po + 32 + 8 * g + 4 * hh) = make_float4(o1[4 * g], o1[4 * g + 1], o1[4 * g + 2], o1[4 * g + 3]);
+  }
+  if (hh == 0) a.part_ml[cr * a.n_head + h] = make_float2(mx, rs);
+}
+
+void launch_xattn_rows(const XAttnArgs& a, hipStream_t s) {
+  WDR_CHECK(cdiv(a.Tk, XA_KC) == XA_NS && XA_KC == FA_KB, "cross-attention rows expect 1500 keys");
+  WDR_CHECK(a.row_k && a.R >= 1 && (a.n_vgrp == 0 || (a.grp && a.lead)) && (a.n_tiles == 0 || a.tiles),
+            "cross-attention rows: bad tables");
+  const double kv = (double)a.Tk * a.n_head * 64 * 2 * 2;
+  if (a.n_vgrp > 0) {
+    const double flops = (double)a.R * a.Tk * a.n_head * 64 * 4;
+    if (a.vgrp_max <= 1)
+      wdr_launch(PROF_XATTN, a.n_vgrp * kv, flops, k_xattn_partial<true, 1>, dim3(XA_NS, a.n_head, a.n_vgrp),
+                 dim3(256), 0, s, a);
+    else
+      wdr_launch(PROF_XATTN, a.n_vgrp * kv, flops, k_xattn_partial<true, XATTN_GRP_MAX>,
+                 dim3(XA_NS, a.n_head, a.n_vgrp), dim3(256), 0, s, a);
+  }
+  if (a.n_tiles > 0)
+    wdr_launch(PROF_XATTN, a.n_tiles * kv, (double)a.n_tiles * 128 * a.Tk * a.n_head * 64 * 4, k_xattn_mma,
+               dim3(XA_NS, a.n_head, a.n_tiles), dim3(256), 0, s, a);
+  WDR_KLAUNCH(k_xattn_combine<XA_NS>, dim3(a.R, a.n_head), dim3(64), 0, s, a);
+  WDR_HIP(hipGetLastError());
 }
 
 void launch_xattn(const XAttnArgs& a, hipStream_t s) {
@@ -434,6 +555,37 @@ __global__ __launch_bounds__(256) void k_aheads_capture(CaptureArgs a) {
 
 void launch_aheads_capture(const CaptureArgs& a, int n_sel, hipStream_t s) {
   WDR_KLAUNCH(k_aheads_capture, dim3(a.R, n_sel), dim3(256), 0, s, a);
+  WDR_HIP(hipGetLastError());
+}
+
+// k_aheads_capture for rows of several DTW re-forwards in one batch (rows_forward): each
+// capture row reads its own slot and writes its own request's buffer
+__global__ __launch_bounds__(256) void k_aheads_capture_rows(CaptureRowsArgs a) {
+  __shared__ float qs[64];
+  const int j = blockIdx.x, i = blockIdx.y, tid = threadIdx.x;
+  const int r = a.crow[j], h = a.heads[i];
+  if (tid < 64) qs[tid] = (float)a.q[(long long)r * a.ldq + h * 64 + tid];
+  __syncthreads();
+  const float2 ml = a.ml[(long long)r * a.n_head + h];
+  const float inv = 1.f / ml.y;
+  const f16* kb = a.row_k[r] + a.layer_off + h * a.hs;
+  float* out = a.cdst[j] + (long long)(a.slot0 + i) * a.cstride[j];
+  for (int key = tid; key < a.Tk; key += 256) {
+    const f16* kr = kb + (long long)key * 64;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 64; c += 8) {
+      const f16x8 kv = *(const f16x8*)(kr + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += qs[c + e] * (float)kv[e];
+    }
+    out[key] = __expf(s * a.scale - ml.x) * inv;
+  }
+}
+
+void launch_aheads_capture_rows(const CaptureRowsArgs& a, int n_sel, hipStream_t s) {
+  if (a.n_cap <= 0 || n_sel <= 0) return;
+  WDR_KLAUNCH(k_aheads_capture_rows, dim3(a.n_cap, n_sel), dim3(256), 0, s, a);
   WDR_HIP(hipGetLastError());
 }
 

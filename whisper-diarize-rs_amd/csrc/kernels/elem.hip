@@ -249,11 +249,11 @@ void launch_i16_to_f32(const int16_t* in, int n, float* out, hipStream_t s) {
 
 // ---------------------------------------------------------------- LayerNorm / embedding / KV
 __global__ __launch_bounds__(256) void k_layernorm(const float* x, int ldx, const float* g, const float* b, f16* y,
-                                                   int ldy, int rows, int d) {
+                                                   int ldy, int rows, int d, const int* row_map) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
-  const float* xr = x + (long long)row * ldx;
+  const float* xr = x + (long long)(row_map ? row_map[row] : row) * ldx;
   // d <= 1280: each lane keeps its <= 20 values in registers; fully unrolled (compile-time
   // indices keep them out of scratch) and gamma / beta are loaded together with x
   float v[5][4], gg[5][4], bb[5][4];
@@ -299,7 +299,15 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* x, int ldx, cons
 void launch_layernorm(const float* x, int ldx, const float* g, const float* b, f16* y, int ldy, int rows, int d,
                       hipStream_t s) {
   WDR_CHECK(d % 4 == 0 && d <= 1280 && ldx % 4 == 0 && ldy % 4 == 0, "layernorm: unsupported width");
-  WDR_KLAUNCH(k_layernorm, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, g, b, y, ldy, rows, d);
+  WDR_KLAUNCH(k_layernorm, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, g, b, y, ldy, rows, d, nullptr);
+  WDR_HIP(hipGetLastError());
+}
+
+// the rows row_map[0 .. rows) of x (the logit rows of a rows_forward batch), compacted into y
+void launch_layernorm_rows(const float* x, int ldx, const float* g, const float* b, f16* y, int ldy, int rows, int d,
+                           const int* row_map, hipStream_t s) {
+  WDR_CHECK(d % 4 == 0 && d <= 1280 && ldx % 4 == 0 && ldy % 4 == 0, "layernorm: unsupported width");
+  WDR_KLAUNCH(k_layernorm, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, g, b, y, ldy, rows, d, row_map);
   WDR_HIP(hipGetLastError());
 }
 

@@ -1647,7 +1647,7 @@ __global__ __launch_bounds__(256) void k_gemv(ProjArgs a) {
 // first (k_layernorm's arithmetic, so the f16 operands are bit-identical to the unfused path;
 // row stride K + 8 halfs keeps the 16-row fragment reads conflict-free) -- which removes the
 // separate LayerNorm launch and its f16 round trip from the prefill / DTW passes.
-template <int EPI, int MT, int NT, int W = 4, bool LN = false>
+template <int EPI, int MT, int NT, int W = 4, bool LN = false, int UU = 0>
 __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
   __shared__ float red[W][MT][NT][4][64];
   extern __shared__ __attribute__((aligned(16))) f16 xln[];   // LN: [16*MT][K + 8]
@@ -1663,9 +1663,12 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
   const int lds_ld = a.K + 8;
   if constexpr (LN) {
     const int d = a.K;
-    for (int rr = wid; rr < 16 * MT; rr += W) {
+    // rows past M are never stored (an MFMA output row depends on its own A row only): only
+    // the live rows are normalised, the rest of the tile stays whatever LDS holds
+    const int live = min(16 * MT, a.M - m0);
+    for (int rr = wid; rr < live; rr += W) {
       int row = m0 + rr;
-      row = row < a.M ? row : a.M - 1;
+      if (a.row_map) row = a.row_map[row];
       const float* xr = a.ln_x + (long long)row * a.ldln;
       float v[5][4], gg[5][4], bb[5][4];
       float sm = 0.f;
@@ -1712,6 +1715,7 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
   for (int i = 0; i < MT; ++i) {
     int m = m0 + i * 16 + fr;
     m = m < a.M ? m : a.M - 1;
+    if (!LN && a.row_map) m = a.row_map[m];
     arow[i] = LN ? xln + (i * 16 + fr) * lds_ld + fk : a.A + (size_t)m * a.lda + fk;
   }
   const f16* brow[NT];
@@ -1723,7 +1727,8 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
   }
   // U k-steps per batch: all of a batch's fragment loads are issued before its MFMAs, so each
   // wave keeps U*(NT+MT) 16-B loads in flight instead of one dependent round trip per step
-  constexpr int U = (MT + NT) <= 3 ? 8 : 4;
+  // (UU: a fixed batch, e.g. all of a wave's k-steps in one batch; the k order is the same)
+  constexpr int U = UU > 0 ? UU : (MT + NT) <= 3 ? 8 : 4;
   for (int k0 = wid * 32; k0 < a.K; k0 += 32 * W * U) {
     f16x8 bf[U][NT], af[U][MT];
 #pragma unroll
@@ -2111,8 +2116,88 @@ static bool launch_mgemv_passes(const ProjArgs& a, hipStream_t s) {
   }
 }
 
+// Decoder rows of any count on the row kernel (k_skinny, 8 waves splitting K): the k order of a
+// wave (k = 32 wid + 256 t, t = 0, 1, ...) and the wave order of the reduce do not depend on the
+// tile shape (MT, NT, U) or the row split, so every row's result is the same whatever the launch
+// holds -- a prompt prefill of n rows equals n one-row steps, bit for bit.
+// A/B knobs of the row kernel's wave count (microbenchmark only: the arithmetic of a shape must
+// not change within a run): WDR_ROWS_W16K=0 -> fc2 on 8 waves; WDR_ROWS_W16N=1 -> K <= 1280
+// narrow projections on 16 waves
+static bool rows_w16k() {
+  const char* e = getenv("WDR_ROWS_W16K");
+  return !(e && atoi(e) == 0);
+}
+static bool rows_w16n() {
+  const char* e = getenv("WDR_ROWS_W16N");
+  return e && atoi(e) != 0;
+}
+
+template <int EPI>
+static void launch_rows_epi(const ProjArgs& a, hipStream_t s) {
+  const int ob = (EPI == EPI_F32_RESID || EPI == EPI_F32 || EPI == EPI_F32_GELU_POS) ? 4 : 2;
+  const double bytes = (double)a.N * a.K * 2 + (double)a.M * a.K * 2 + (double)a.M * a.N * ob;
+  const double flops = 2.0 * a.M * a.N * a.K;
+  const int mt = cdiv(a.M, 16);
+  const bool ln = a.ln_x != nullptr;
+  const bool wide = a.N >= 4096;
+  const int prof = a.M <= 16 ? PROF_GEMV : PROF_SKINNY;
+  if (!wide) {
+    // one 16-row tile per workgroup: the row tiles of a column tile re-read its weights from L2.
+    // K > 2048 (fc2): 16 waves, each wave's 10 k-steps as ONE batch of loads (8 waves took three
+    // dependent batches: fc2 at 1 row 9.8 us against 5.4 us on the GEMV)
+    if (a.K > 2048) {
+      WDR_CHECK(!ln, "row projection: LN prologue needs K <= 1280");
+      dim3 grid(cdiv(a.N, 16), mt), blk(1024);
+      if (rows_w16k()) wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 16, false, 12>, grid, blk, 0, s, a);
+      else wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 8>, grid, dim3(512), 0, s, a);
+      return;
+    }
+    if (rows_w16n()) {
+      dim3 grid(cdiv(a.N, 16), mt), blk(1024);
+      if (ln) wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 16, true, 3>, grid, blk, (uint32_t)16 * (a.K + 8) * 2, s, a);
+      else wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 16, false, 3>, grid, blk, 0, s, a);
+      return;
+    }
+    dim3 grid(cdiv(a.N, 16), mt), blk(512);
+    if (ln) wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 8, true>, grid, blk, (uint32_t)16 * (a.K + 8) * 2, s, a);
+    else wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 8>, grid, blk, 0, s, a);
+    return;
+  }
+  // wide N (fc1, logits): 32 columns per workgroup, up to 4 row tiles per workgroup
+  const int mtw = std::min(mt, ln ? 2 : 4);
+  dim3 grid(cdiv(a.N, 32), cdiv(mt, mtw)), blk(512);
+  const uint32_t lds = ln ? (uint32_t)16 * mtw * (a.K + 8) * 2 : 0;
+#define WDR_RW(MTV)                                                                                        \
+  if (ln) wdr_launch(prof, bytes, flops, k_skinny<EPI, MTV, 2, 8, true>, grid, blk, lds, s, a);            \
+  else wdr_launch(prof, bytes, flops, k_skinny<EPI, MTV, 2, 8>, grid, blk, 0, s, a);
+  if (mtw == 1) { WDR_RW(1) }
+  else if (mtw == 2) { WDR_RW(2) }
+  else if (mtw == 3) { WDR_RW(3) }
+  else { WDR_RW(4) }
+#undef WDR_RW
+}
+
+static void launch_rows(const ProjArgs& a, hipStream_t s) {
+  WDR_CHECK(a.K % 32 == 0 && a.lda % 8 == 0 && a.ldb % 8 == 0, "row projection: K % 32, lda / ldb % 8");
+  WDR_CHECK(!a.ln_x || (a.K <= 1280 && a.K % 4 == 0 && a.M <= 32), "row projection LN prologue: K <= 1280, M <= 32");
+  WDR_CHECK(a.epi != EPI_QKV_CACHE || (a.kc && a.vc && a.row_seq && a.row_pos && a.d > 0), "qkv-cache epilogue args");
+  switch (a.epi) {
+    case EPI_F16: launch_rows_epi<EPI_F16>(a, s); break;
+    case EPI_F16_GELU: launch_rows_epi<EPI_F16_GELU>(a, s); break;
+    case EPI_F32_RESID: launch_rows_epi<EPI_F32_RESID>(a, s); break;
+    case EPI_F32: launch_rows_epi<EPI_F32>(a, s); break;
+    case EPI_QKV_CACHE: launch_rows_epi<EPI_QKV_CACHE>(a, s); break;
+    default: throw std::runtime_error("row projection: bad epilogue");
+  }
+  WDR_HIP(hipGetLastError());
+}
+
 void launch_proj(const ProjArgs& a, hipStream_t s) {
   WDR_CHECK(a.M > 0 && a.K > 0 && a.N > 0, "projection: empty shape");
+  if (a.rows_mma) {
+    launch_rows(a, s);
+    return;
+  }
   if (a.step_rows && a.M > 16 && !a.ln_x && mgemv_staged() && launch_mgemv_passes(a, s)) return;
   if (a.step_rows && a.M > 16) {
     // a batched step of more than 16 rows (beams of several segments): 16-row GEMV launches,

@@ -129,6 +129,17 @@ struct XAttnArgs {
   // with grp: the n_grp leading rows (device array), so the launch has one workgroup per group
   // and chunk instead of one per row (the other rows' workgroups would only exit)
   const int* lead = nullptr;
+  // decoder rows (rows_forward): the groups of a DTW re-forward stop after its last alignment-head
+  // layer -- lend[leader row] (VALU groups) / tiles[].z (MFMA tiles) is the first layer skipped
+  int layer = 0;
+  const int* lend = nullptr;
+  // MFMA row tiles (prompt prefills / DTW re-forwards of more than XATTN_GRP_MAX rows): tile t
+  // = rows tiles[t].x .. + tiles[t].y - 1 (<= 128) of one group, cross K/V at row_k[tiles[t].x]
+  const int4* tiles = nullptr;
+  int n_tiles = 0;
+  int n_vgrp = 0;                     // VALU groups (lead list length); 0 with tiles: none
+  int vgrp_max = 1;                   // largest VALU group (1: the 47-VGPR one-row kernel)
+  float2* ml_out = nullptr;           // combine: (max, sum) per (row, head) for the DTW capture
 };
 constexpr int XATTN_GRP_MAX = 8;   // rows sharing one K/V without row_k
 inline unsigned long long* prof_attach(XAttnArgs& a) { return a.ts = prof_slot(); }
@@ -144,34 +155,23 @@ struct CaptureArgs {
   long long hs = 64;                  // head stride of K (elements)
 };
 void launch_aheads_capture(const CaptureArgs& a, int n_sel, hipStream_t s);
-
-// persistent greedy decode step (kernels/step.hip): one decoder row through all layers + logits
-struct StepLayer {
-  const f16 *w_qkv, *w_o, *w_xq, *w_xo, *w_fc1, *w_fc2;
-  const float *b_qkv, *b_o, *b_xq, *b_xo, *b_fc1, *b_fc2;
-  const float *ln1_g, *ln1_b, *ln2_g, *ln2_b, *ln3_g, *ln3_b;
-};
-struct StepArgs {
-  const StepLayer* layers;          // device table [L]
-  int L, d, n_head, V;
-  const f16* tok_emb;               // [V][d] (tied logits weights)
-  const float* ln_g; const float* ln_b;
-  const int* row_seq; const int* row_pos;
-  f16* kc; f16* vc;                 // self-attention caches; layer l at + l * layer_stride
-  long long layer_stride, seq_stride;
-  const f16* xkv; int ldxkv;        // cross K/V slot, head-major (common.h XKV_*); ldxkv unused
-  float* x;                         // [d] residual row (token + positional embedding on entry)
-  f16 *q, *att, *qx, *xatt, *mlp;   // [d] x4, [4d]
-  float* part_o; float2* part_ml;   // [24][n_head][64], [24][n_head]
-  float* logits;                    // [V]
-  unsigned* ctr;                    // step_counters(L, n_head), all zero between launches
-  int* err;                         // set to 1 when a wait gives up
+// decoder rows (rows_forward): the cross-attention partials of the VALU groups and the MFMA
+// tiles of one layer, then the combine of every row
+void launch_xattn_rows(const XAttnArgs& a, hipStream_t s);
+// alignment-head capture of rows of several DTW re-forwards (rows_forward): capture row j is
+// batch row crow[j]; head-slot i of the layer lands at cdst[j] + (slot0 + i) * cstride[j]
+struct CaptureRowsArgs {
+  const f16* q; int ldq;
+  const f16* const* row_k; long long layer_off, hs;
+  const float2* ml;                   // [R][n_head] from the combine
+  const int* heads;                   // this layer's alignment heads
+  const int* crow; float* const* cdst; const int* cstride;
+  int n_cap, slot0, Tk, n_head;
   float scale;
-  unsigned long long* trace = nullptr;   // optional [67][G] wall_clock64 timeline
 };
-int step_counters(int L, int n_head);
-bool step_supported(int d, int n_head);
-void launch_step(const StepArgs& a, int n_wg, hipStream_t s);
+void launch_aheads_capture_rows(const CaptureRowsArgs& a, int n_sel, hipStream_t s);
+void launch_layernorm_rows(const float* x, int ldx, const float* g, const float* b, f16* y, int ldy, int rows, int d,
+                           const int* row_map, hipStream_t s);
 
 // Silero VAD (kernels/vad.hip); layouts [out][in*k] f16, biases f32
 struct VadWeights {

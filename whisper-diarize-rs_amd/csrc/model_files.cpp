@@ -426,8 +426,13 @@ TensorMap load_silero_ggml(const std::string& path) {
     std::vector<int64_t> ne;
     int64_t n = 1;
     for (int k = 0; k < nd; ++k) {
-      ne.push_back(i32());
-      n *= ne.back();
+      // untrusted dimensions: each in [1, 2^24] and the running product bounded by the file
+      // size before it is used (no sign games, no overflow)
+      const int32_t dk = i32();
+      if (dk < 1 || dk > (1 << 24)) bad(what, "bad tensor dimension " + std::to_string(dk));
+      ne.push_back(dk);
+      n *= dk;
+      if (n > (int64_t)buf.size()) bad(what, "tensor larger than the file");
     }
     if (e - p < nl) bad(what, "truncated file");
     const std::string name((const char*)p, (size_t)nl);

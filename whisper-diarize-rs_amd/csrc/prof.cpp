@@ -49,6 +49,7 @@ struct Acc {
 constexpr long long kSlotWords = 2 * PROF_CLK_LANES;
 constexpr long long kRing = 1 << 16;
 unsigned long long* g_ring = nullptr;
+int g_ring_dev = -1;   // the device the ring (and the pooled events) live on
 std::atomic<long long> g_next{0};
 double g_tick_ms = 0.0;   // wall_clock64 period in ms
 
@@ -61,6 +62,7 @@ void ring_reset_locked() {
     }
     int dev = 0, khz = 0;
     (void)hipGetDevice(&dev);
+    g_ring_dev = dev;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
     g_tick_ms = 1.0 / (double)khz;
   }
@@ -90,8 +92,12 @@ void drain_locked(bool read_ring = true) {
   g_pending.clear();
   if (!read_ring || g_clk_pending.empty() || !g_ring) return;
   std::vector<unsigned long long> ring((size_t)std::min<long long>(g_next.load(), kRing) * kSlotWords);
-  if (hipDeviceSynchronize() != hipSuccess ||
-      hipMemcpy(ring.data(), g_ring, ring.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const bool ok = hipSetDevice(g_ring_dev) == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+                  hipMemcpy(ring.data(), g_ring, ring.size() * 8, hipMemcpyDeviceToHost) == hipSuccess;
+  (void)hipSetDevice(dev);
+  if (!ok) {
     (void)hipGetLastError();
     g_broken = true;
     return;
@@ -114,8 +120,16 @@ void drain_locked(bool read_ring = true) {
 }
 }  // namespace
 
+// the profiler samples the launches of ONE device (the current one when the mask was set): a
+// multi-GPU context (gpu_device None) launches on peer devices too, whose kernels must not touch
+// this device's ring and whose streams must not record this device's pooled events
+static bool on_ring_device() {
+  int dev = -1;
+  return hipGetDevice(&dev) == hipSuccess && dev == g_ring_dev;
+}
+
 unsigned long long* prof_slot() {
-  if (!g_ring) return nullptr;
+  if (!g_ring || !on_ring_device()) return nullptr;
   const long long i = g_next++;
   return i < kRing ? g_ring + kSlotWords * i : nullptr;
 }
@@ -159,6 +173,7 @@ thread_local bool t_step = false;   // inside a sampled (eager) decode step
 // so the average is over a uniform sample of the class's launches
 bool prof_on(int cls) {
   if (!(g_mask.load(std::memory_order_relaxed) & (1 << cls)) || t_capture) return false;
+  if (!on_ring_device()) return false;
   if (t_step) return (g_tick++ % kEvery) == 0;
   return (g_tick_out++ % (kEvery * kStepEvery)) == 0;
 }

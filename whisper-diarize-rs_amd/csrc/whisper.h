@@ -97,6 +97,7 @@ class Context {
   // batcher can address rows of several chains: [L][max_chains * NSLOT][n_text_ctx][d] f16
   int max_chains = 1;
   DevMem kv_k, kv_v;
+  long long kv_seq_stride = 0, kv_layer_stride = 0;   // elements per (layer, sequence) / per layer
   std::unique_ptr<class StepBatcher> batcher;     // multi-chain greedy steps (created on demand)
   StepBatcher& step_batcher();
   // fp8 (e4m3) encoder GEMMs (BASELINE configs[4]; wdr_context_set_encoder_fp8, WDR_FP8_ENCODER):
@@ -154,35 +155,20 @@ struct StageTimes {   // host wall-clock per phase (seconds), accumulated
   double lang = 0, prompt_gpu = 0;   // language-detect wall time; GPU time of the prompt prefills
 };
 
-// one decode step's working set (rows of one speech segment, or of several: row_xkv)
-struct StepIO {
-  float* xd; f16* qkvd; f16* attd; f16* qx; f16* mlpd;
-  float* logits; int ldlogits;
-  float* part_o; float2* part_ml;
-  const int* rows_tok; const int* rows_pos; const int* rows_seq;
-  f16* kc; f16* vc; long long layer_stride, seq_stride;   // KV pool (layer 0) and its strides
-  const f16* xkv;                  // one cross-K/V slot for every row, or
-  const f16* const* row_xkv;       // per-row slot bases (device array)
-  const int* grp = nullptr;        // row groups sharing a slot (XAttnArgs::grp), or null
-  int n_grp = 0;
-  const int* lead = nullptr;       // the groups' first rows (XAttnArgs::lead), or null
-};
-void decode_step_layers(const Context& ctx, const StepIO& io, int R, hipStream_t s);
-
 // Multi-chain decoding: several States ("chains", each decoding its own contiguous block of
-// speech segments on its own host thread) hand their decode steps -- one row (greedy) or the
-// live beams of a segment (beam search, with top-K candidates per row) -- to this batcher,
-// which runs them as ONE R-row step (weights streamed once per 16 rows; each row with its own
-// KV-pool sequence, the rows of a request sharing their segment's cross-K/V slot, read once
-// for all of them) on its own stream.  Lockstep: a batch launches once every chain inside a
-// decode loop has submitted its request.
+// speech segments on its own host thread) hand their decoder work -- a decode step (one row,
+// or the live beams of a segment with top-K candidates per row), a segment's prompt prefill,
+// a window's DTW re-forward -- to this batcher, which runs everything submitted as ONE rows
+// forward (rows.h: the weights streamed once for all rows, each row with its own KV-pool
+// sequence, the rows of a request sharing their segment's cross-K/V slot) on its own stream.
+// Lockstep: a batch launches once every chain inside the batcher has submitted its request.
 class StepBatcher {
  public:
   explicit StepBatcher(Context& ctx);
   ~StepBatcher();
   static constexpr int kRows = 8;   // rows of one request (the beams / decoders of a segment)
   struct Req {
-    int n = 1;                 // rows
+    int n = 1;                 // decode rows (0: none)
     int tok[kRows], seq[kRows], pos[kRows];   // seq: absolute KV-pool sequence
     LogitsCtl ctl[kRows];
     const f16* xkv = nullptr;  // the segment's cross-K/V slot (all its rows)
@@ -190,12 +176,30 @@ class StepBatcher {
     int K = 0;                 // beam candidates per row (0: the greedy pick only)
     TokenData out[kRows];
     BeamCand cand[kRows * BEAM_KMAX];   // [row][K]
+    // prompt prefill (pn > 0): tokens ptok at positions 0.. of sequence pseq (absolute) on slot
+    // pxkv; its last row's logits go through the rules with pctl -> pout, pnosp
+    int pn = 0;
+    const int* ptok = nullptr;
+    int pseq = 0;
+    const f16* pxkv = nullptr;
+    LogitsCtl pctl{};
+    TokenData pout;
+    float pnosp = 0.f;
+    // DTW re-forward (dn > 0): tokens dtok at positions 0.. of sequence dseq on slot dxkv, the
+    // alignment heads' probabilities captured into dcap ([n_aheads][dn][1500], device); the
+    // cross-attention stops at layer dl_end
+    int dn = 0;
+    const int* dtok = nullptr;
+    int dseq = 0;
+    const f16* dxkv = nullptr;
+    float* dcap = nullptr;
+    int dl_end = 1 << 30;
   };
   void enter();
   void leave();
   void step(Req& r);           // blocks until the batch holding r has run
   void run(std::vector<Req*>& batch) { launch(batch); }   // one batch, caller's thread (test seam)
-  long long launches = 0, rows = 0;
+  long long launches = 0, rows = 0, prefill_rows = 0, dtw_rows = 0, mixed = 0;
   double step_s = 0;           // wall of the launches (submit -> results on the host)
   struct Impl;
 
@@ -206,7 +210,6 @@ class StepBatcher {
 };
 
 struct Seq;           // one decoder's sequence (whisper_ctx.cpp)
-struct PrefillBufs;   // a prefill's working set (whisper_ctx.cpp)
 
 // a window's DTW job in flight on the DTW stream (State::dtw_timestamps)
 struct DtwTicket {
@@ -251,9 +254,7 @@ class State {
   void read_encoder_out(float* out);                       // [1500][d] (ln_post output, f16 -> f32)
   void read_cross_kv(float* out);                          // [1500][L][2][d] of the last encoded window
   void decode_logits(const int* toks, int n, float* logits_out);   // prefill from an empty cache
-  void dbg_step(const int* toks, int n, bool classic, float* logits_out);
-  bool persistent_step() const;
-  int step_trace(uint64_t* out, int cap);   // timeline of the last persistent step; returns G
+  void dbg_step(const int* toks, int n, float* logits_out);
   void dtw_capture(const int* toks, int n, float* cap_out);        // [n_aheads][n][1500]
 
   struct Impl;
@@ -269,11 +270,9 @@ class State {
   Seq decode_beam(const std::vector<int>& prompt, const FullParams& params, float t_cur, int seek, int seek_end, int Lf,
                   int window, float* nosp);
   void decoder_prefill(const int* toks, int n, int seq, bool want_logits, bool capture);
-  void prefill_on(const int* toks, int n, int seq, bool want_logits, bool capture, const PrefillBufs& b,
-                  hipStream_t st, const f16* xkv_base);
+  void prefill_on(const int* toks, int n, int seq, bool want_logits, bool capture, bool dtw_set, hipStream_t st,
+                  const f16* xkv_base);
   void decoder_step(const int* toks, const int* seqs, const int* pos, int R);
-  void decoder_step_body(int R);
-  void step_err_check();
   void step_and_sample(const int* toks, const int* seqs, const int* pos, const LogitsCtl* ctl, int R, TokenData* out,
                        int K = 0, BeamCand* cands = nullptr);
   void logits_topk(int R, int K, BeamCand* out);

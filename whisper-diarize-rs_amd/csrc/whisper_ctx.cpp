@@ -2,6 +2,7 @@
 // whisper_full_with_state decode loop as the reference drives it
 // (src/transcribe.rs:20-87 params, :389 state.full).  Mirrors oracle/whisper_full.py.
 #include "whisper.h"
+#include "rows.h"
 #include "ggml_file.h"
 #include "prof.h"
 
@@ -349,6 +350,8 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
     const size_t per = (size_t)hp.n_text_layer * 21 * hp.n_text_ctx * hp.n_text_state;   // NSLOT = 21
     kv_k = DevMem(per * max_chains * 2);
     kv_v = DevMem(per * max_chains * 2);
+    kv_seq_stride = (long long)hp.n_text_ctx * hp.n_text_state;
+    kv_layer_stride = (long long)max_chains * 21 * kv_seq_stride;
   }
 }
 
@@ -363,17 +366,7 @@ static constexpr int NSEQ = 8;     // max decoder rows in one step
 static constexpr int NSLOT = 21;   // self-attention KV-cache sequences (beams + reorder scratch + DTW + lang)
 static constexpr int DTW_SEQ = 16;  // the DTW re-forward's own sequence (runs on its own stream)
 static constexpr int LANG_SEQ = 17; // encode-ahead language detection: sequences 17..20, one per window of a batch
-static constexpr int NSPLIT = 24;  // cross-attention key chunks (1500 / 64)
 
-// Working set of a prefill: the decode stream's own (pointing at the buffers above) and the
-// DTW stream's private copy, so a window's DTW re-forward overlaps the next decode.
-struct PrefillBufs {
-  float* xd; f16* hd; f16* qkvd; f16* attd; f16* qx; f16* mlpd;
-  int* rows_tok; int* rows_pos; int* rows_seq;
-  float* fpart_o; float2* fpart_ml; float2* ml; float* cap; float* part_o; float2* part_ml;
-  float* logits;
-  int* h_rows;
-};
 
 struct State::Impl {
   int d, L, H, V, n_mels, kp1;
@@ -408,23 +401,23 @@ struct State::Impl {
   } plan;
   // encode-ahead language detection: its own prefill working set and the 100 language
   // logits of each slot's window 0 (pinned, written by the encode stream before `ready`)
-  struct LangSet {
-    DevMem xd, hd, qkvd, attd, qx, mlpd, rows_tok, rows_pos, rows_seq, part_o, part_ml, logits, row_xkv;
-    const f16** h_xkv = nullptr;   // pinned [(S + 1)][kBatch] row cross-K/V bases, by first slot
-  } lset;
+  RowsBufs lb;                   // its rows forward (kBatch rows)
+  std::unique_ptr<RowBatch> tlb;
   float* h_lang = nullptr;      // [(S + 1)][100]
   DevMem energy_d; int energy_cap = 0;
   const f16* xkv() const { return xkv_ring.as<f16>() + (size_t)cur * xkv_slot_elems; }
-  // decoder
-  DevMem xd, hd, qkvd, attd, qx, mlpd, logits, work, tokout, ctl, ml, cap, part_o, part_ml;
-  DevMem rows_tok, rows_pos, rows_seq;
+  // decoder: this state's own rows forwards (prompt prefills, beam / sampling steps, test seams)
+  // on the decode stream, and the DTW re-forwards on the DTW stream, each with its own working
+  // set and row tables (rows.h)
+  RowsBufs mb, db;
+  std::unique_ptr<RowBatch> tb, tdb;
+  DevMem work, tokout, ctl, cap;
   DevMem beamc, kvpairs;       // beam candidates [NSEQ][BEAM_KMAX], KV reorder (src, dst) pairs
   BeamCand* h_beam = nullptr;
   DevMem sprobs, slogp;        // [NSEQ][V] sampled rows (t > 0)
   std::vector<float> hp_probs, hp_logp;
   std::mt19937 rng[NSEQ];      // whisper_decoder::rng
   int* h_pairs = nullptr;
-  DevMem fpart_o, fpart_ml;   // split flash-attention partials (prefill cross-attention)
   f16* kc = nullptr;          // this chain's sequences in the context's KV pool (layer 0)
   f16* vc = nullptr;
   int nslot_tot = 0;          // sequences per layer in the pool (layer stride / seq_stride)
@@ -432,10 +425,8 @@ struct State::Impl {
   hipStream_t own = nullptr;  // this state's decode stream
   // dtw
   DevMem nrm, xdtw, times;
-  PrefillBufs pb_main{}, pb_dtw{};
   struct DtwSet {
-    DevMem xd, hd, qkvd, attd, qx, mlpd, rows_tok, rows_pos, rows_seq, fpart_o, fpart_ml, ml, cap, part_o, part_ml,
-        nrm, xdtw, times;
+    DevMem cap, nrm, xdtw, times;
   } dset;
   hipStream_t sd = nullptr;        // DTW stream
   hipEvent_t ev_sync = nullptr;    // decode-stream point the DTW stream waits for
@@ -450,7 +441,6 @@ struct State::Impl {
   std::vector<int*> blk_pool;
   std::vector<hipEvent_t> ev_pool;
   // host pinned
-  int* h_rows = nullptr;       // 3 * RMAX
   TokOut* h_tok = nullptr;
   LogitsCtl* h_ctl = nullptr;
   int* h_times = nullptr;
@@ -459,14 +449,7 @@ struct State::Impl {
     hipGraphExec_t exec = nullptr;
     VocabIds vids{};
   };
-  std::map<int, StepGraph> graphs;   // key: R * 256 + slot (the cross-K/V pointer is baked in)
-  // persistent one-row step (kernels/step.hip): layer table, counters, hand-off rows
-  bool st_on = false;
-  int st_wg = 0;
-  DevMem st_layers, st_ctr, st_q, st_att, st_qx, st_xatt, st_mlp;
-  DevMem st_trace;             // optional timeline (WDR_STEP_TRACE=1), [67][st_wg]
-  int* h_err = nullptr;        // pinned, mapped: set by the kernel when a wait gives up
-  int* d_err = nullptr;
+  std::map<int, StepGraph> graphs;   // key: (K, R); the rows' slots are table entries
 };
 
 // ------------------------------------------------------------------ fp8 encoder weights
@@ -560,23 +543,19 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
     const int prio = ep == 2 ? hi : ep == 1 ? (lo + hi) / 2 : lo;
     WDR_HIP(hipStreamCreateWithPriority(&m.es, hipStreamNonBlocking, prio));
   }
-  m.xd = DevMem((size_t)RMAX * d * 4);
-  m.hd = DevMem((size_t)RMAX * d * 2);
-  m.qkvd = DevMem((size_t)RMAX * 3 * d * 2);
-  m.attd = DevMem((size_t)RMAX * d * 2);
-  m.qx = DevMem((size_t)RMAX * d * 2);
-  m.mlpd = DevMem((size_t)RMAX * 4 * d * 2);
-  m.logits = DevMem((size_t)NSEQ * m.V * 4);
+  // this state's rows forwards: prompt prefills / DTW re-forwards up to RMAX rows, steps of up
+  // to NSEQ logit rows; the DTW set captures; language detection kBatch rows
+  const int A = std::max<int>(1, (int)ctx.aheads.size());
+  m.mb.alloc(RMAX, NSEQ, d, m.H, m.V);
+  m.tb = std::make_unique<RowBatch>(RMAX, NSEQ, RMAX);
+  m.db.alloc(RMAX, 1, d, m.H, m.V);
+  m.tdb = std::make_unique<RowBatch>(RMAX, 1, RMAX);
+  m.lb.alloc(kBatch, kBatch, d, m.H, m.V);
+  m.tlb = std::make_unique<RowBatch>(kBatch, kBatch, 0);
   m.work = DevMem((size_t)NSEQ * m.V * 4);
   m.tokout = DevMem(NSEQ * sizeof(TokOut));
   m.ctl = DevMem(NSEQ * sizeof(LogitsCtl));
-  m.ml = DevMem((size_t)m.H * RMAX * sizeof(float2));
-  const int A = std::max<int>(1, (int)ctx.aheads.size());
   m.cap = DevMem((size_t)A * RMAX * 1500 * 4);
-  m.part_o = DevMem((size_t)NSPLIT * NSEQ * m.H * 64 * 4);
-  m.part_ml = DevMem((size_t)NSPLIT * NSEQ * m.H * sizeof(float2));
-  m.fpart_o = DevMem((size_t)12 * 256 * m.H * 64 * 4);
-  m.fpart_ml = DevMem((size_t)12 * m.H * 256 * sizeof(float2));
   m.beamc = DevMem(NSEQ * BEAM_KMAX * sizeof(BeamCand));
   m.sprobs = DevMem((size_t)NSEQ * m.V * 4);
   m.slogp = DevMem((size_t)NSEQ * m.V * 4);
@@ -584,68 +563,16 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
   m.kvpairs = DevMem(2 * 2 * NSEQ * 4);
   WDR_HIP(hipHostMalloc((void**)&m.h_beam, NSEQ * BEAM_KMAX * sizeof(BeamCand), hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_pairs, 2 * 2 * NSEQ * 4, hipHostMallocDefault));
-  m.rows_tok = DevMem(RMAX * 4);
-  m.rows_pos = DevMem(RMAX * 4);
-  m.rows_seq = DevMem(RMAX * 4);
   m.seq_stride = (long long)hp.n_text_ctx * d;
   m.nslot_tot = ctx.max_chains * NSLOT;
   m.kc = ctx.kv_k.as<f16>() + (size_t)chain * NSLOT * m.seq_stride;
   m.vc = ctx.kv_v.as<f16>() + (size_t)chain * NSLOT * m.seq_stride;
-  m.nrm = DevMem((size_t)A * RMAX * 1500 * 4);
-  m.xdtw = DevMem((size_t)RMAX * 1500 * 4);
-  m.times = DevMem((RMAX + 8) * 4);
   {
     Impl::DtwSet& D = m.dset;
-    D.xd = DevMem((size_t)RMAX * d * 4);
-    D.hd = DevMem((size_t)RMAX * d * 2);
-    D.qkvd = DevMem((size_t)RMAX * 3 * d * 2);
-    D.attd = DevMem((size_t)RMAX * d * 2);
-    D.qx = DevMem((size_t)RMAX * d * 2);
-    D.mlpd = DevMem((size_t)RMAX * 4 * d * 2);
-    D.rows_tok = DevMem(RMAX * 4);
-    D.rows_pos = DevMem(RMAX * 4);
-    D.rows_seq = DevMem(RMAX * 4);
-    D.fpart_o = DevMem((size_t)12 * 256 * m.H * 64 * 4);
-    D.fpart_ml = DevMem((size_t)12 * m.H * 256 * sizeof(float2));
-    D.ml = DevMem((size_t)m.H * RMAX * sizeof(float2));
     D.cap = DevMem((size_t)A * RMAX * 1500 * 4);
-    D.part_o = DevMem((size_t)NSPLIT * NSEQ * m.H * 64 * 4);
-    D.part_ml = DevMem((size_t)NSPLIT * NSEQ * m.H * sizeof(float2));
     D.nrm = DevMem((size_t)A * RMAX * 1500 * 4);
     D.xdtw = DevMem((size_t)RMAX * 1500 * 4);
     D.times = DevMem((RMAX + 8) * 4);
-    m.pb_dtw = PrefillBufs{D.xd.as<float>(), D.hd.as<f16>(), D.qkvd.as<f16>(), D.attd.as<f16>(), D.qx.as<f16>(),
-                        D.mlpd.as<f16>(), D.rows_tok.as<int>(), D.rows_pos.as<int>(), D.rows_seq.as<int>(),
-                        D.fpart_o.as<float>(), D.fpart_ml.as<float2>(), D.ml.as<float2>(), D.cap.as<float>(),
-                        D.part_o.as<float>(), D.part_ml.as<float2>(), nullptr, nullptr};
-    // language detection: one kBatch-row step (SOT at position 0, one KV sequence and one
-    // cross-K/V slot per window) per encode-ahead batch
-    Impl::LangSet& G = m.lset;
-    const int LB = kBatch;
-    G.xd = DevMem((size_t)LB * d * 4);
-    G.qkvd = DevMem((size_t)LB * 3 * d * 2);
-    G.attd = DevMem((size_t)LB * d * 2);
-    G.qx = DevMem((size_t)LB * d * 2);
-    G.mlpd = DevMem((size_t)LB * 4 * d * 2);
-    G.rows_tok = DevMem(LB * 4);
-    G.rows_pos = DevMem(LB * 4);
-    G.rows_seq = DevMem(LB * 4);
-    G.part_o = DevMem((size_t)NSPLIT * LB * m.H * 64 * 4);
-    G.part_ml = DevMem((size_t)NSPLIT * LB * m.H * sizeof(float2));
-    G.logits = DevMem((size_t)LB * m.V * 4);
-    G.row_xkv = DevMem(LB * sizeof(void*));
-    WDR_HIP(hipHostMalloc((void**)&G.h_xkv, (size_t)(kSlots + 1) * LB * sizeof(void*), hipHostMallocDefault));
-    {
-      std::vector<int> rows(3 * LB);
-      for (int r = 0; r < LB; ++r) {
-        rows[r] = ctx.vocab.sot;
-        rows[LB + r] = 0;
-        rows[2 * LB + r] = LANG_SEQ + r;
-      }
-      WDR_HIP(hipMemcpy(G.rows_tok.p, rows.data(), LB * 4, hipMemcpyHostToDevice));
-      WDR_HIP(hipMemcpy(G.rows_pos.p, rows.data() + LB, LB * 4, hipMemcpyHostToDevice));
-      WDR_HIP(hipMemcpy(G.rows_seq.p, rows.data() + 2 * LB, LB * 4, hipMemcpyHostToDevice));
-    }
     WDR_HIP(hipHostMalloc((void**)&m.h_lang, (size_t)(kSlots + 1) * 100 * 4, hipHostMallocDefault));
     int lo = 0, hi = 0;
     WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -655,47 +582,9 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
     WDR_HIP(hipEventCreate(&m.ev_p0));
     WDR_HIP(hipEventCreate(&m.ev_p1));
   }
-  WDR_HIP(hipHostMalloc((void**)&m.h_rows, 3 * RMAX * 4, hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_tok, NSEQ * sizeof(TokOut), hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_ctl, NSEQ * sizeof(LogitsCtl), hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_times, (RMAX + 8) * 4, hipHostMallocDefault));
-  m.pb_main = PrefillBufs{m.xd.as<float>(), m.hd.as<f16>(), m.qkvd.as<f16>(), m.attd.as<f16>(), m.qx.as<f16>(),
-                       m.mlpd.as<f16>(), m.rows_tok.as<int>(), m.rows_pos.as<int>(), m.rows_seq.as<int>(),
-                       m.fpart_o.as<float>(), m.fpart_ml.as<float2>(), m.ml.as<float2>(), m.cap.as<float>(),
-                       m.part_o.as<float>(), m.part_ml.as<float2>(), m.logits.as<float>(), m.h_rows};
-  // The persistent one-launch step is measured SLOWER than the per-kernel chain on MI355X
-  // (2.7 vs ~1.7 ms per large-v3 step: in-launch all-to-all hand-offs cost 2.5-7 us each, more
-  // than the ~1.2 us kernel boundaries they replace), so it is opt-in.
-  if (step_supported(d, m.H) && getenv("WDR_PSTEP") && atoi(getenv("WDR_PSTEP")) != 0) {
-    hipDeviceProp_t prop;
-    WDR_HIP(hipGetDeviceProperties(&prop, ctx.cp.gpu_device));
-    m.st_wg = prop.multiProcessorCount;   // one workgroup per CU
-    if (m.st_wg >= 12 * m.H && 2 * m.st_wg >= 24 * m.H && 2 * m.st_wg >= d / 4) {
-      std::vector<StepLayer> tab(m.L);
-      for (int l = 0; l < m.L; ++l) {
-        const DecLayer& e = ctx.model.dec[l];
-        tab[l] = StepLayer{e.w_qkv, e.w_o, e.w_xq, e.w_xo, e.w_fc1, e.w_fc2, e.b_qkv, e.b_o, e.b_xq, e.b_xo,
-                           e.b_fc1, e.b_fc2, e.ln1_g, e.ln1_b, e.ln2_g, e.ln2_b, e.ln3_g, e.ln3_b};
-      }
-      m.st_layers = DevMem(tab.size() * sizeof(StepLayer));
-      WDR_HIP(hipMemcpy(m.st_layers.p, tab.data(), tab.size() * sizeof(StepLayer), hipMemcpyHostToDevice));
-      m.st_ctr = DevMem((size_t)step_counters(m.L, m.H) * 4);
-      WDR_HIP(hipMemset(m.st_ctr.p, 0, m.st_ctr.bytes));
-      m.st_q = DevMem((size_t)d * 2);
-      m.st_att = DevMem((size_t)d * 2);
-      m.st_qx = DevMem((size_t)d * 2);
-      m.st_xatt = DevMem((size_t)d * 2);
-      m.st_mlp = DevMem((size_t)4 * d * 2);
-      WDR_HIP(hipHostMalloc((void**)&m.h_err, 64, hipHostMallocMapped | hipHostMallocCoherent));
-      *m.h_err = 0;
-      WDR_HIP(hipHostGetDevicePointer((void**)&m.d_err, m.h_err, 0));
-      if (getenv("WDR_STEP_TRACE")) {
-        m.st_trace = DevMem((size_t)67 * m.st_wg * 8);
-        WDR_HIP(hipMemset(m.st_trace.p, 0, m.st_trace.bytes));
-      }
-      m.st_on = true;
-    }
-  }
   const Vocab& v = ctx.vocab;
   m.vids = VocabIds{v.n_vocab, v.eot, v.sot, v.translate, v.transcribe, v.solm, v.prev, v.nosp, v.not_, v.beg,
                     v.token_to_id.at(" "), v.sot + 1, 100, -1, 1};
@@ -705,13 +594,11 @@ State::~State() {
   if (m_) {
     for (auto& g : m_->graphs)
       if (g.second.exec) (void)hipGraphExecDestroy(g.second.exec);
-    (void)hipHostFree(m_->h_rows);
     (void)hipHostFree(m_->h_tok);
     (void)hipHostFree(m_->h_ctl);
     (void)hipHostFree(m_->h_times);
     (void)hipHostFree(m_->h_beam);
     (void)hipHostFree(m_->h_pairs);
-    if (m_->h_err) (void)hipHostFree(m_->h_err);
     if (m_->es) {
       (void)hipStreamSynchronize(m_->es);
       (void)hipStreamDestroy(m_->es);
@@ -731,7 +618,6 @@ State::~State() {
     for (int* b : m_->blk_pool) (void)hipHostFree(b);
     for (hipEvent_t e : m_->ev_pool) (void)hipEventDestroy(e);
     if (m_->ev_sync) (void)hipEventDestroy(m_->ev_sync);
-    if (m_->lset.h_xkv) (void)hipHostFree(m_->lset.h_xkv);
     if (m_->h_lang) (void)hipHostFree(m_->h_lang);
     if (m_->ev_dtw) (void)hipEventDestroy(m_->ev_dtw);
     for (auto& sl : m_->slots) {
@@ -980,21 +866,26 @@ void State::top_up(int j) {
       // whisper.cpp's language detection (one SOT pass over window 0, argmax of the language
       // logits) depends on nothing decoded, so it runs here, off the decode chain: the batch's
       // windows as the rows of ONE decode step, each with its own cross-K/V slot and sequence
-      Impl::LangSet& G = m.lset;
+      // (every window a one-row group: the arithmetic of decoder_prefill(SOT) on the decode stream)
       const int R = g1 - g0;
-      const f16** hx = G.h_xkv + (size_t)(g0 % m.S) * kBatch;   // reused >= S segments later
-      for (int r = 0; r < R; ++r) hx[r] = m.xkv_ring.as<f16>() + (size_t)((g0 + r) % m.S) * m.xkv_slot_elems;
-      WDR_HIP(wdr_memcpy_async(G.row_xkv.p, hx, R * sizeof(void*), hipMemcpyHostToDevice, m.es));
-      launch_embed(ctx_.model.tok_emb, ctx_.model.dec_pos, G.rows_tok.as<int>(), G.rows_pos.as<int>(), R, m.d,
-                   G.xd.as<float>(), m.es);
-      StepIO io{G.xd.as<float>(), G.qkvd.as<f16>(), G.attd.as<f16>(), G.qx.as<f16>(), G.mlpd.as<f16>(),
-                G.logits.as<float>(), m.V, G.part_o.as<float>(), G.part_ml.as<float2>(), G.rows_tok.as<int>(),
-                G.rows_pos.as<int>(), G.rows_seq.as<int>(), m.kc, m.vc, (long long)m.nslot_tot * m.seq_stride,
-                m.seq_stride, nullptr, G.row_xkv.as<const f16*>()};
-      decode_step_layers(ctx_, io, R, m.es);
+      RowBatch& tl = *m.tlb;
+      tl.clear();   // waits for the previous batch's table copy
+      const int sot = ctx_.vocab.sot;
+      for (int r = 0; r < R; ++r) {
+        RowGroupDesc g;
+        g.n = 1;
+        g.tok = &sot;
+        g.seq0 = chain * NSLOT + LANG_SEQ + r;
+        g.xkv = m.xkv_ring.as<f16>() + (size_t)((g0 + r) % m.S) * m.xkv_slot_elems;
+        g.logits = 1;
+        tl.add(g);
+      }
+      RowsIO io = m.lb.io(ctx_, m.V);
+      tl.upload(io, m.es, true, true);
+      rows_forward(ctx_, io, R, m.es);
       for (int r = 0; r < R; ++r)
         WDR_HIP(wdr_memcpy_async(m.h_lang + (size_t)((g0 + r) % m.S) * 100,
-                               G.logits.as<float>() + (size_t)r * m.V + ctx_.vocab.sot + 1, 100 * 4,
+                               m.lb.logits.as<float>() + (size_t)r * m.V + sot + 1, 100 * 4,
                                hipMemcpyDeviceToHost, m.es));
     }
     for (int k = g0; k < g1; ++k) WDR_HIP(hipEventRecord(m.slots[k % m.S].ready, m.es));
@@ -1004,251 +895,80 @@ void State::top_up(int j) {
 }
 
 // ------------------------------------------------------------------ decoder
-// Prefill of `n` tokens into sequence `seq` from an empty cache (positions 0..n-1):
-// whisper.cpp clears the KV cache before the prompt decode and before the DTW pass.
-void State::decoder_prefill(const int* toks, int n, int seq, bool want_logits, bool capture) {
-  prefill_on(toks, n, seq, want_logits, capture, m_->pb_main, s_, m_->xkv());
+// Every decoder pass of a State is a rows forward (rows.h) -- the arithmetic every other pass
+// of the context uses too, so a prompt prefill, a DTW re-forward or a step gives the same result
+// here as inside the multi-chain batched step.
+
+// the first layer a capture-only pass (the DTW re-forward) can skip: nothing after the last
+// alignment-head layer's cross-attention changes a captured probability
+static int capture_l_end(const Context& ctx) {
+  const int L = ctx.model.hp.n_text_layer;
+  if (ctx.aheads_per_layer.size() != (size_t)L) return L;
+  int l = L;
+  while (l > 0 && ctx.aheads_per_layer[l - 1].empty()) --l;
+  return l == 0 ? L : l;
 }
 
-void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool capture, const PrefillBufs& b,
+// Prefill of `n` tokens into sequence `seq` (chain-local) from an empty cache (positions
+// 0..n-1): whisper.cpp clears the KV cache before the prompt decode and before the DTW pass.
+void State::decoder_prefill(const int* toks, int n, int seq, bool want_logits, bool capture) {
+  prefill_on(toks, n, seq, want_logits, capture, false, s_, m_->xkv());
+}
+
+void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool capture, bool dtw_set,
                        hipStream_t st, const f16* xkv_base) {
   Impl& m = *m_;
-  const Model& md = ctx_.model;
-  const HParams& hp = md.hp;
-  const int d = m.d, L = m.L;
   WDR_CHECK(n >= 1 && n <= RMAX, "decoder prefill: token count out of range");
-  for (int i = 0; i < n; ++i) {
-    b.h_rows[i] = toks[i];
-    b.h_rows[RMAX + i] = i;
-    b.h_rows[2 * RMAX + i] = seq;
+  RowBatch& tb = dtw_set ? *m.tdb : *m.tb;
+  const RowsBufs& B = dtw_set ? m.db : m.mb;
+  tb.clear();
+  RowGroupDesc g;
+  g.n = n;
+  g.tok = toks;
+  g.seq0 = chain * NSLOT + seq;
+  g.xkv = xkv_base;
+  g.logits = want_logits ? 1 : 0;
+  if (capture) {
+    g.cap = dtw_set ? m.dset.cap.as<float>() : m.cap.as<float>();
+    if (!want_logits) g.l_end = capture_l_end(ctx_);
   }
-  WDR_HIP(wdr_memcpy_async(b.rows_tok, b.h_rows, n * 4, hipMemcpyHostToDevice, st));
-  WDR_HIP(wdr_memcpy_async(b.rows_pos, b.h_rows + RMAX, n * 4, hipMemcpyHostToDevice, st));
-  WDR_HIP(wdr_memcpy_async(b.rows_seq, b.h_rows + 2 * RMAX, n * 4, hipMemcpyHostToDevice, st));
-  launch_embed(md.tok_emb, md.dec_pos, b.rows_tok, b.rows_pos, n, d, b.xd, st);
-  const float scale = 1.0f / 8.0f;
-  const int H = hp.n_text_head;
-  // the projection's input rows are LayerNorm(x): fused into the skinny GEMM for 8 < n <= 32
-  // rows (bit-identical to k_layernorm + GEMM), else the separate LayerNorm into b.hd
-  auto ln_into = [&](ProjArgs& p, const float* x, const float* g, const float* bb) {
-    if (n > NSEQ && n <= 32 && d <= 1280) {
-      p.ln_x = x;
-      p.ldln = d;
-      p.ln_g = g;
-      p.ln_b = bb;
-    } else {
-      launch_layernorm(x, d, g, bb, b.hd, d, n, d, st);
-    }
-  };
-  // a capture-only pass (the DTW re-forward) needs nothing past the last alignment-head layer's
-  // cross-attention: the layers after it cannot change any captured probability
-  int l_end = L;
-  if (capture && !want_logits)
-    for (l_end = L; l_end > 0 && ctx_.aheads_per_layer.size() == (size_t)L && ctx_.aheads_per_layer[l_end - 1].empty();)
-      --l_end;
-  if (l_end == 0) l_end = L;
-  for (int l = 0; l < l_end; ++l) {
-    const DecLayer& e = md.dec[l];
-    f16* kc = m.kc + (size_t)l * m.nslot_tot * m.seq_stride;
-    f16* vc = m.vc + (size_t)l * m.nslot_tot * m.seq_stride;
-    // Q to qkvd, K / V straight into this sequence's cache rows 0..n-1 (the epilogue scatter);
-    // 8 < n <= 32 rows: the LayerNorm runs inside the skinny GEMM (fused prologue)
-    ProjArgs qa{b.hd, d, e.w_qkv, d, e.b_qkv, b.qkvd, 3 * d, nullptr, 0, n, 3 * d, d, EPI_QKV_CACHE};
-    ln_into(qa, b.xd, e.ln1_g, e.ln1_b);
-    qa.kc = kc;
-    qa.vc = vc;
-    qa.seq_stride = m.seq_stride;
-    qa.row_seq = b.rows_seq;
-    qa.row_pos = b.rows_pos;
-    qa.d = d;
-    launch_proj(qa, st);
-    const f16* ks = kc + (size_t)seq * m.seq_stride;
-    const f16* vs = vc + (size_t)seq * m.seq_stride;
-    FlashArgs sa{b.qkvd, 3 * d, 0, ks, d, 0, vs, d, 0, b.attd, d, 0, nullptr, n, n, hp.n_text_head, 1, scale};
-    launch_flash_attn(sa, 1, st);
-    proj(st, b.attd, d, e.w_o, d, e.b_o, b.xd, d, n, d, d, EPI_F32_RESID);
-    {
-      ProjArgs xq{b.hd, d, e.w_xq, d, e.b_xq, b.qx, d, nullptr, 0, n, d, d, EPI_F16};
-      ln_into(xq, b.xd, e.ln2_g, e.ln2_b);
-      launch_proj(xq, st);
-    }
-    // head-major cross K/V (common.h XKV_*): key stride 64, head stride XKV_HS
-    const f16* xk = xkv_base + xkv_k_off(l, H);
-    const f16* xv = xkv_base + xkv_v_off(l, H);
-    const bool cap_layer = capture && !ctx_.aheads_per_layer.empty() && !ctx_.aheads_per_layer[l].empty();
-    if (n > NSEQ || cap_layer) {
-      FlashArgs xa{b.qx, d, 0, xk, 64, 0, xv, 64, 0, b.attd, d, 0,
-                   cap_layer ? b.ml : nullptr, n, 1500, hp.n_text_head, 0, scale};
-      xa.k_hs = xa.v_hs = XKV_HS;
-      if (n <= 256) {   // few queries: split the 1500 keys so every CU streams part of the cross K/V
-        xa.nsplit = 12;
-        xa.part_o = b.fpart_o;
-        xa.part_ml = b.fpart_ml;
-      }
-      launch_flash_attn(xa, 1, st);
-      if (cap_layer) {
-        int slot0 = 0;
-        for (int q = 0; q < l; ++q) slot0 += (int)ctx_.aheads_per_layer[q].size();
-        CaptureArgs ca{b.qx, d, xk, 64, b.ml, ctx_.aheads_dev.as<int>() + ctx_.aheads_dev_off[l],
-                       b.cap, slot0, n, 1500, scale};
-        ca.hs = XKV_HS;
-        launch_aheads_capture(ca, (int)ctx_.aheads_per_layer[l].size(), st);
-      }
-    } else {
-      XAttnArgs xa{b.qx, d, xk, xv, 64, 1500, n, hp.n_text_head, scale, b.part_o,
-                   b.part_ml, b.attd, d};
-      xa.hs = XKV_HS;
-      launch_xattn(xa, st);
-    }
-    if (l_end < L && l == l_end - 1) break;   // capture-only pass: done after the last head layer
-    proj(st, b.attd, d, e.w_xo, d, e.b_xo, b.xd, d, n, d, d, EPI_F32_RESID);
-    {
-      ProjArgs f1{b.hd, d, e.w_fc1, d, e.b_fc1, b.mlpd, 4 * d, nullptr, 0, n, 4 * d, d, EPI_F16_GELU};
-      ln_into(f1, b.xd, e.ln3_g, e.ln3_b);
-      launch_proj(f1, st);
-    }
-    proj(st, b.mlpd, 4 * d, e.w_fc2, 4 * d, e.b_fc2, b.xd, d, n, d, 4 * d, EPI_F32_RESID);
-  }
-  if (want_logits) {
-    launch_layernorm(b.xd + (size_t)(n - 1) * d, d, md.ln_g, md.ln_b, b.hd, d, 1, d, st);
-    proj(st, b.hd, d, md.tok_emb, d, nullptr, b.logits, m.V, 1, m.V, d, EPI_F32);
-  }
+  tb.add(g);
+  RowsIO io = B.io(ctx_, m.V);
+  tb.upload(io, st, true, true);
+  rows_forward(ctx_, io, n, st);
   if (st == s_) times.prefills++;
 }
 
-// One decode step for R rows: row r appends token rows_tok[r] at position rows_pos[r] of
-// sequence rows_seq[r] (device arrays, filled by the caller).  LayerNorms are fused into the
-// projections' prologue and K/V go straight into the cache from the QKV epilogue, so a layer
-// is 8 launches: QKV, self-attn, O, cross-Q, cross-attn (2), cross-O, FC1, FC2.
-void State::decoder_step_body(int R) {
-  Impl& m = *m_;
-  const Model& md = ctx_.model;
-  const int d = m.d, L = m.L;
-  launch_embed(md.tok_emb, md.dec_pos, m.rows_tok.as<int>(), m.rows_pos.as<int>(), R, d, m.xd.as<float>(), s_);
-  const float scale = 1.0f / 8.0f;
-  if (R == 1 && m.st_on) {
-    StepArgs a{m.st_layers.as<StepLayer>(), L, d, m.H, m.V, md.tok_emb, md.ln_g, md.ln_b, m.rows_seq.as<int>(),
-               m.rows_pos.as<int>(), m.kc, m.vc, (long long)m.nslot_tot * m.seq_stride, m.seq_stride,
-               m.xkv(), L * 2 * d, m.xd.as<float>(), m.st_q.as<f16>(), m.st_att.as<f16>(), m.st_qx.as<f16>(),
-               m.st_xatt.as<f16>(), m.st_mlp.as<f16>(), m.part_o.as<float>(), m.part_ml.as<float2>(),
-               m.logits.as<float>(), m.st_ctr.as<unsigned>(), m.d_err, scale};
-    a.trace = m.st_trace.p ? m.st_trace.as<unsigned long long>() : nullptr;
-    launch_step(a, m.st_wg, s_);
-    return;
-  }
-  StepIO io{m.xd.as<float>(), m.qkvd.as<f16>(), m.attd.as<f16>(), m.qx.as<f16>(), m.mlpd.as<f16>(),
-            m.logits.as<float>(), m.V, m.part_o.as<float>(), m.part_ml.as<float2>(), m.rows_tok.as<int>(),
-            m.rows_pos.as<int>(), m.rows_seq.as<int>(), m.kc, m.vc, (long long)m.nslot_tot * m.seq_stride,
-            m.seq_stride, m.xkv(), nullptr};
-  decode_step_layers(ctx_, io, R, s_);
-}
-
-// The per-kernel decode step after the embedding: for every layer QKV (LN fused, K/V into the
-// cache), self-attention, O, cross-Q (LN fused), cross-attention (2), cross-O, FC1 (LN fused),
-// FC2; then the final LN + logits.  Rows may come from different speech segments (per-row
-// cross-K/V slots, StepBatcher) or from one (beams / best_of decoders, State).
-void decode_step_layers(const Context& ctx, const StepIO& io, int R, hipStream_t s) {
-  const Model& md = ctx.model;
-  const HParams& hp = md.hp;
-  const int d = hp.n_text_state, L = hp.n_text_layer;
-  const float scale = 1.0f / 8.0f;
-  const int H = hp.n_text_head;
-  // more than ln_split rows: the LayerNorm of the rows runs once into io.attd (free at every
-  // LN point of the layer) instead of in every GEMV workgroup
-  static const int ln_split = getenv("WDR_STEP_LN_SPLIT") ? atoi(getenv("WDR_STEP_LN_SPLIT")) : 2;
-  auto P = [&](const f16* A, int lda, const f16* W, const float* b, void* out, int ldo, int N, int K, int epi,
-               const float* lng = nullptr, const float* lnb = nullptr) {
-    ProjArgs a{A, lda, W, K, b, out, ldo, nullptr, 0, R, N, K, epi};
-    a.step_rows = 1;
-    if (lng) {
-      a.ln_x = io.xd;
-      a.ldln = d;
-      a.ln_g = lng;
-      a.ln_b = lnb;
-      if (R > ln_split) {
-        launch_ln_rows(a, io.attd, d, s);
-        a.ln_x = nullptr;
-        a.A = io.attd;
-        a.lda = d;
-      }
-    }
-    return a;
-  };
-  for (int l = 0; l < L; ++l) {
-    const DecLayer& e = md.dec[l];
-    f16* kc = io.kc + (size_t)l * io.layer_stride;
-    f16* vc = io.vc + (size_t)l * io.layer_stride;
-    ProjArgs q = P(nullptr, d, e.w_qkv, e.b_qkv, io.qkvd, 3 * d, 3 * d, d, EPI_QKV_CACHE, e.ln1_g, e.ln1_b);
-    q.kc = kc;
-    q.vc = vc;
-    q.seq_stride = io.seq_stride;
-    q.row_seq = io.rows_seq;
-    q.row_pos = io.rows_pos;
-    q.d = d;
-    launch_proj(q, s);
-    DecSelfArgs sa{io.qkvd, 3 * d, kc, vc, io.seq_stride, d, io.rows_seq, io.rows_pos, io.attd, d, scale};
-    launch_dec_self_attn(sa, R, hp.n_text_head, s);
-    launch_proj(P(io.attd, d, e.w_o, e.b_o, io.xd, d, d, d, EPI_F32_RESID), s);
-    launch_proj(P(nullptr, d, e.w_xq, e.b_xq, io.qx, d, d, d, EPI_F16, e.ln2_g, e.ln2_b), s);
-    // head-major cross K/V slots (common.h XKV_*): key stride 64, head stride XKV_HS
-    XAttnArgs xa{io.qx, d, nullptr, nullptr, 64, 1500, R, hp.n_text_head, scale, io.part_o, io.part_ml, io.attd, d};
-    xa.grp = io.grp;
-    xa.n_grp = io.n_grp;
-    xa.lead = io.lead;
-    xa.hs = XKV_HS;
-    if (io.row_xkv) {
-      xa.row_k = io.row_xkv;
-      xa.layer_off = xkv_k_off(l, H);
-      xa.v_off = xkv_v_off(l, H) - xkv_k_off(l, H);
-    } else {
-      xa.k = io.xkv + xkv_k_off(l, H);
-      xa.v = io.xkv + xkv_v_off(l, H);
-    }
-    launch_xattn(xa, s);
-    launch_proj(P(io.attd, d, e.w_xo, e.b_xo, io.xd, d, d, d, EPI_F32_RESID), s);
-    launch_proj(P(nullptr, d, e.w_fc1, e.b_fc1, io.mlpd, 4 * d, 4 * d, d, EPI_F16_GELU, e.ln3_g, e.ln3_b), s);
-    launch_proj(P(io.mlpd, 4 * d, e.w_fc2, e.b_fc2, io.xd, d, d, 4 * d, EPI_F32_RESID), s);
-  }
-  launch_proj(P(nullptr, d, md.tok_emb, nullptr, io.logits, io.ldlogits, hp.n_vocab, d, EPI_F32, md.ln_g, md.ln_b), s);
-}
-
-// after a synchronised step: a persistent-step wait that gave up leaves counters behind
-void State::step_err_check() {
-  Impl& m = *m_;
-  if (!m.h_err || !*(volatile int*)m.h_err) return;
-  WDR_HIP(wdr_memset_async(m.st_ctr.p, 0, m.st_ctr.bytes, s_));
-  WDR_HIP(hipStreamSynchronize(s_));
-  *(volatile int*)m.h_err = 0;
-  throw std::runtime_error("persistent decode step: a hand-off wait timed out");
-}
-
+// R decoder rows of this state (beams / best_of decoders, chain-local sequences seqs[r]) reading
+// the current slot: one group sharing the slot, logits of every row into mb.logits
 void State::decoder_step(const int* toks, const int* seqs, const int* pos, int R) {
   Impl& m = *m_;
   WDR_CHECK(R >= 1 && R <= NSEQ, "decoder step: row count out of range");
-  for (int i = 0; i < R; ++i) {
-    m.h_rows[i] = toks[i];
-    m.h_rows[RMAX + i] = pos[i];
-    m.h_rows[2 * RMAX + i] = seqs[i];
-  }
-  WDR_HIP(wdr_memcpy_async(m.rows_tok.p, m.h_rows, R * 4, hipMemcpyHostToDevice, s_));
-  WDR_HIP(wdr_memcpy_async(m.rows_pos.p, m.h_rows + RMAX, R * 4, hipMemcpyHostToDevice, s_));
-  WDR_HIP(wdr_memcpy_async(m.rows_seq.p, m.h_rows + 2 * RMAX, R * 4, hipMemcpyHostToDevice, s_));
-  decoder_step_body(R);
+  RowBatch& tb = *m.tb;
+  tb.clear();
+  int sq[NSEQ];
+  for (int i = 0; i < R; ++i) sq[i] = chain * NSLOT + seqs[i];
+  RowGroupDesc g;
+  g.n = R;
+  g.tok = toks;
+  g.seq = sq;
+  g.pos = pos;
+  g.xkv = m.xkv();
+  g.logits = 2;
+  tb.add(g);
+  RowsIO io = m.mb.io(ctx_, m.V);
+  tb.upload(io, s_, true, true);
+  rows_forward(ctx_, io, R, s_);
   times.decode_steps++;
 }
 
 // decode step + logit rules + greedy pick as ONE hipGraph replay per token (captured once per
-// row count; the per-step inputs live in pinned host buffers the graph's copy nodes read).
+// (K, rows); the row tables and per-step inputs live in pinned host buffers the graph's copy
+// nodes read).
 void State::step_and_sample(const int* toks, const int* seqs, const int* pos, const LogitsCtl* ctl, int R,
                             TokenData* out, int K, BeamCand* cands) {
   Impl& m = *m_;
   WDR_CHECK(R >= 1 && R <= NSEQ, "decoder step: row count out of range");
-  for (int i = 0; i < R; ++i) {
-    m.h_rows[i] = toks[i];
-    m.h_rows[RMAX + i] = pos[i];
-    m.h_rows[2 * RMAX + i] = seqs[i];
-  }
-  memcpy(m.h_ctl, ctl, R * sizeof(LogitsCtl));
   const bool sampled = prof_step();
   if (sampled || getenv("WDR_NO_GRAPH")) {
     // live per-kernel HIP-event timing cannot read events recorded inside a graph on this
@@ -1265,21 +985,37 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
     if (K > 0) logits_topk(R, K, cands);
     return;
   }
-  Impl::StepGraph& g = m.graphs[(K << 16) + R * 256 + m.cur];
+  RowBatch& tb = *m.tb;
+  tb.clear();
+  int sq[NSEQ];
+  for (int i = 0; i < R; ++i) sq[i] = chain * NSLOT + seqs[i];
+  RowGroupDesc grp;
+  grp.n = R;
+  grp.tok = toks;
+  grp.seq = sq;
+  grp.pos = pos;
+  grp.xkv = m.xkv();
+  grp.logits = 2;
+  tb.add(grp);
+  memcpy(m.h_ctl, ctl, R * sizeof(LogitsCtl));
+  RowsIO io = m.mb.io(ctx_, m.V);
+  Impl::StepGraph& g = m.graphs[(K << 16) + R];
+  if (g.exec && memcmp(&g.vids, &m.vids, sizeof(VocabIds)) != 0) {   // rule constants changed: recapture
+    (void)hipGraphExecDestroy(g.exec);
+    g.exec = nullptr;
+  }
   if (!g.exec) {
     hipGraph_t graph;
     prof_capture(true);
     WDR_HIP(hipStreamBeginCapture(s_, hipStreamCaptureModeThreadLocal));
-    WDR_HIP(wdr_memcpy_async(m.rows_tok.p, m.h_rows, R * 4, hipMemcpyHostToDevice, s_));
-    WDR_HIP(wdr_memcpy_async(m.rows_pos.p, m.h_rows + RMAX, R * 4, hipMemcpyHostToDevice, s_));
-    WDR_HIP(wdr_memcpy_async(m.rows_seq.p, m.h_rows + 2 * RMAX, R * 4, hipMemcpyHostToDevice, s_));
+    tb.upload(io, s_, true, false);
     WDR_HIP(wdr_memcpy_async(m.ctl.p, m.h_ctl, R * sizeof(LogitsCtl), hipMemcpyHostToDevice, s_));
-    decoder_step_body(R);
-    launch_logits_process(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, m.work.as<float>(),
+    rows_forward(ctx_, io, R, s_);
+    launch_logits_process(m.mb.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, m.work.as<float>(),
                           m.tokout.as<TokOut>(), s_);
     WDR_HIP(wdr_memcpy_async(m.h_tok, m.tokout.p, R * sizeof(TokOut), hipMemcpyDeviceToHost, s_));
     if (K > 0) {
-      launch_logits_topk(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, K, m.work.as<float>(),
+      launch_logits_topk(m.mb.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, K, m.work.as<float>(),
                          m.beamc.as<BeamCand>(), s_);
       WDR_HIP(wdr_memcpy_async(m.h_beam, m.beamc.p, (size_t)R * K * sizeof(BeamCand), hipMemcpyDeviceToHost, s_));
     }
@@ -1288,12 +1024,8 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
     WDR_HIP(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
     WDR_HIP(hipGraphDestroy(graph));
     g.vids = m.vids;
-  }
-  if (memcmp(&g.vids, &m.vids, sizeof(VocabIds)) != 0) {   // rule constants changed: recapture
-    (void)hipGraphExecDestroy(g.exec);
-    g.exec = nullptr;
-    step_and_sample(toks, seqs, pos, ctl, R, out, K, cands);
-    return;
+  } else {
+    tb.upload(io, s_, false, false);   // the captured copy node reads the staging
   }
   {
     std::mutex* mu = launch_lock();   // WDR_LAUNCH_LOCK (prof.h)
@@ -1303,7 +1035,6 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
     WDR_HIP(ge);
   }
   WDR_HIP(hipStreamSynchronize(s_));
-  step_err_check();
   if (K > 0) memcpy(cands, m.h_beam, (size_t)R * K * sizeof(BeamCand));
   for (int r = 0; r < R; ++r) {
     const TokOut& o = m.h_tok[r];
@@ -1323,11 +1054,10 @@ void State::run_logits(int R, const LogitsCtl* ctl, TokenData* out, float* nosp)
   Impl& m = *m_;
   memcpy(m.h_ctl, ctl, R * sizeof(LogitsCtl));
   WDR_HIP(wdr_memcpy_async(m.ctl.p, m.h_ctl, R * sizeof(LogitsCtl), hipMemcpyHostToDevice, s_));
-  launch_logits_process(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, m.work.as<float>(),
+  launch_logits_process(m.mb.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, m.work.as<float>(),
                         m.tokout.as<TokOut>(), s_);
   WDR_HIP(wdr_memcpy_async(m.h_tok, m.tokout.p, R * sizeof(TokOut), hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
-  step_err_check();
   for (int r = 0; r < R; ++r) {
     const TokOut& o = m.h_tok[r];
     TokenData t;
@@ -1345,7 +1075,7 @@ void State::run_logits(int R, const LogitsCtl* ctl, TokenData* out, float* nosp)
 // top-K candidates of rows whose logits were just processed by run_logits (same ctl)
 void State::logits_topk(int R, int K, BeamCand* out) {
   Impl& m = *m_;
-  launch_logits_topk(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, K, m.work.as<float>(),
+  launch_logits_topk(m.mb.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, K, m.work.as<float>(),
                      m.beamc.as<BeamCand>(), s_);
   WDR_HIP(wdr_memcpy_async(m.h_beam, m.beamc.p, (size_t)R * K * sizeof(BeamCand), hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
@@ -1374,24 +1104,15 @@ void State::kv_reorder(const std::vector<std::pair<int, int>>& moves, int n_rows
 }
 
 // test seam: prefill toks[0..n-2] into sequence 0, then ONE decode step of toks[n-1] at
-// position n-1; classic = the per-kernel chain instead of the persistent step
-void State::dbg_step(const int* toks, int n, bool classic, float* logits_out) {
+// position n-1 (the step's logits; the rows contract makes them equal the n-token prefill's)
+void State::dbg_step(const int* toks, int n, float* logits_out) {
   Impl& m = *m_;
   WDR_CHECK(n >= 2 && n <= 448, "dbg_step: need 2..448 tokens");
   decoder_prefill(toks, n - 1, 0, false, false);
-  const bool on = m.st_on;
-  if (classic) m.st_on = false;
   const int tok = toks[n - 1], seq = 0, pos = n - 1;
-  try {
-    decoder_step(&tok, &seq, &pos, 1);
-  } catch (...) {
-    m.st_on = on;
-    throw;
-  }
-  m.st_on = on;
-  WDR_HIP(wdr_memcpy_async(logits_out, m.logits.p, (size_t)m.V * 4, hipMemcpyDeviceToHost, s_));
+  decoder_step(&tok, &seq, &pos, 1);
+  WDR_HIP(wdr_memcpy_async(logits_out, m.mb.logits.p, (size_t)m.V * 4, hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
-  step_err_check();
 }
 
 // a one-row (greedy) batcher request
@@ -1430,8 +1151,6 @@ double State::dbg_batch_step(const int* toks, int n, int R, int iters) {
   return (now_s() - t) * 1e3 / iters;
 }
 
-bool State::persistent_step() const { return m_->st_on; }
-
 void State::reset_rng() { m_->rng[0] = std::mt19937(0); }
 std::string State::rng_state() const {
   std::ostringstream o;
@@ -1443,17 +1162,9 @@ void State::set_rng_state(const std::string& st) {
   i >> m_->rng[0];
 }
 
-int State::step_trace(uint64_t* out, int cap) {
-  Impl& m = *m_;
-  if (!m.st_trace.p) return 0;
-  const int n = std::min(cap, 67 * m.st_wg);
-  WDR_HIP(hipMemcpy(out, m.st_trace.p, (size_t)n * 8, hipMemcpyDeviceToHost));
-  return m.st_wg;
-}
-
 void State::decode_logits(const int* toks, int n, float* logits_out) {
   decoder_prefill(toks, n, 0, true, false);
-  WDR_HIP(wdr_memcpy_async(logits_out, m_->logits.p, (size_t)m_->V * 4, hipMemcpyDeviceToHost, s_));
+  WDR_HIP(wdr_memcpy_async(logits_out, m_->mb.logits.p, (size_t)m_->V * 4, hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
 }
 
@@ -1621,14 +1332,38 @@ void State::dtw_timestamps(int i_segment, int n_segments, int seek, int n_frames
   job.done = m.ev_pool.back();
   m.ev_pool.pop_back();
   m.jobs.push_back(job);
-  // the window's cross-K/V (encoded ahead, or on demand on the decode stream) must be in place
-  WDR_HIP(hipEventRecord(m.ev_sync, s_));
-  WDR_HIP(hipStreamWaitEvent(m.sd, m.ev_sync, 0));
-  PrefillBufs pb = m.pb_dtw;
-  pb.h_rows = job.blk;
-  prefill_on(toks.data(), N, DTW_SEQ, false, true, pb, m.sd, m.xkv());
-  const int n_audio = n_frames / 2;
   Impl::DtwSet& D = m.dset;
+  if (batched) {
+    // multi-chain run: the re-forward's rows ride in the batched step (capture into this
+    // state's DTW buffer, which the previous job's DTW kernels must have finished reading); the
+    // DTW kernels then follow on the DTW stream
+    WDR_HIP(hipEventSynchronize(m.ev_dtw));
+    WDR_HIP(hipStreamSynchronize(s_));   // the window's cross-K/V (on-demand encodes) in place
+    StepBatcher& b = ctx_.step_batcher();
+    StepBatcher::Req q;
+    q.n = 0;
+    q.dn = N;
+    q.dtok = toks.data();
+    q.dseq = chain * NSLOT + DTW_SEQ;
+    q.dxkv = m.xkv();
+    q.dcap = D.cap.as<float>();
+    q.dl_end = capture_l_end(ctx_);
+    q.vids = m.vids;
+    b.enter();
+    try {
+      b.step(q);
+    } catch (...) {
+      b.leave();
+      throw;
+    }
+    b.leave();
+  } else {
+    // the window's cross-K/V (encoded ahead, or on demand on the decode stream) must be in place
+    WDR_HIP(hipEventRecord(m.ev_sync, s_));
+    WDR_HIP(hipStreamWaitEvent(m.sd, m.ev_sync, 0));
+    prefill_on(toks.data(), N, DTW_SEQ, false, true, true, m.sd, m.xkv());
+  }
+  const int n_audio = n_frames / 2;
   launch_dtw(D.cap.as<float>(), (int)ctx_.aheads.size(), N, 1500, n_audio, sot_len, seek, D.nrm.as<float>(),
              D.xdtw.as<float>(), D.times.as<int>(), D.times.as<int>() + RMAX + 4, m.sd);
   WDR_HIP(wdr_memcpy_async(job.blk + 3 * RMAX, D.times.p, (RMAX + 8) * 4, hipMemcpyDeviceToHost, m.sd));
@@ -1957,7 +1692,7 @@ Seq State::decode_sample(const std::vector<int>& prompt, const FullParams& param
       decoder_step(toks.data(), seqs.data(), pos.data(), R);
       run_logits(R, ctl.data(), td.data(), nullptr);
     }
-    launch_logits_probs(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, m.work.as<float>(),
+    launch_logits_probs(m.mb.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), m.vids, R, m.work.as<float>(),
                         m.sprobs.as<float>(), m.slogp.as<float>(), s_);
     WDR_HIP(wdr_memcpy_async(m.hp_probs.data(), m.sprobs.p, (size_t)R * V * 4, hipMemcpyDeviceToHost, s_));
     WDR_HIP(wdr_memcpy_async(m.hp_logp.data(), m.slogp.p, (size_t)R * V * 4, hipMemcpyDeviceToHost, s_));
@@ -2132,7 +1867,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
     } else {
       const int sot = v.sot;
       decoder_prefill(&sot, 1, 0, true, false);
-      WDR_HIP(wdr_memcpy_async(ll.data(), m.logits.as<float>() + v.sot + 1, 100 * 4, hipMemcpyDeviceToHost, s_));
+      WDR_HIP(wdr_memcpy_async(ll.data(), m.mb.logits.as<float>() + v.sot + 1, 100 * 4, hipMemcpyDeviceToHost, s_));
       WDR_HIP(hipStreamSynchronize(s_));
     }
     int best = 0;
@@ -2168,6 +1903,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
   std::vector<int> prompt;
   while (true) {
     if (seek + 100 >= seek_end) break;
+    bool prompt_timed = false;
     encode(seek);
     if (seek > seek_start && seek + 500 >= seek_end) prompt_past.clear();
     Seq best;
@@ -2181,16 +1917,22 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
         prompt.insert(prompt.end(), prompt_past.end() - n_take, prompt_past.end());
       }
       prompt.insert(prompt.end(), prompt_init.begin(), prompt_init.end());
-      WDR_HIP(hipEventRecord(m.ev_p0, s_));
-      decoder_prefill(prompt.data(), (int)prompt.size(), 0, true, false);
-      WDR_HIP(hipEventRecord(m.ev_p1, s_));
+      const bool single = params.greedy && t_cur <= 0.f;
+      // multi-chain greedy run: the prompt prefill rides in the batched step (its last row's
+      // logits give the first token), so the chain never leaves the batch
+      const bool pre_batched = batched && single;
+      if (!pre_batched) {
+        WDR_HIP(hipEventRecord(m.ev_p0, s_));
+        decoder_prefill(prompt.data(), (int)prompt.size(), 0, true, false);
+        WDR_HIP(hipEventRecord(m.ev_p1, s_));
+        prompt_timed = true;
+      }
       const int window = std::min(seek_end - seek, 3000);
       int Lf = 0;
       if (params.force_len_rate > 0.f) Lf = std::max(3, c_round(params.force_len_rate * window / 100.0) + 3);
       Seq sq;
       const int n_max = n_text_ctx / 2 - 4;
       float nosp = 0.f;
-      const bool single = params.greedy && t_cur <= 0.f;
       if (t_cur > 0.f) {
         sq = decode_sample(prompt, params, t_cur, seek, seek_end, Lf, window, &nosp);
       } else if (!params.greedy) {
@@ -2219,7 +1961,24 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
         }
         TokenData tok;
         float ns = 0.f;
-        if (i == 0) {
+        if (i == 0 && pre_batched) {
+          if (!lockstep.b) {
+            lockstep.b = &ctx_.step_batcher();
+            lockstep.b->enter();
+          }
+          StepBatcher::Req rq;
+          rq.n = 0;
+          rq.pn = (int)prompt.size();
+          rq.ptok = prompt.data();
+          rq.pseq = chain * NSLOT + 0;
+          rq.pxkv = m.xkv();
+          rq.pctl = c;
+          rq.vids = m.vids;
+          lockstep.b->step(rq);
+          tok = rq.pout;
+          nosp = rq.pnosp;
+          times.prefills++;
+        } else if (i == 0) {
           run_logits(1, &c, &tok, &ns);
           nosp = ns;
         } else {
@@ -2287,7 +2046,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
       if (success) break;
     }
     times.decode += now_s() - t_dec;
-    {
+    if (prompt_timed) {
       float ms = 0.f;
       if (hipEventElapsedTime(&ms, m.ev_p0, m.ev_p1) == hipSuccess) times.prompt_gpu += ms * 1e-3;
     }
@@ -2335,30 +2094,32 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
 // ------------------------------------------------------------------ multi-chain step batcher
 namespace wdr {
 
-static constexpr int RB = 256;    // rows per batched step (chains x beams: 32 x 8)
+// rows of one batched launch: decode rows, prompt prefills and DTW re-forwards of up to 32
+// chains (a prefill <= 228 rows, a DTW re-forward <= 229)
+static constexpr int RB = 16384;
+static constexpr int LB = 320;    // logit rows (32 chains x (8 beams + a prefill's last row))
 
 struct StepBatcher::Impl {
   std::mutex mu;
   std::condition_variable cv;
-  int active = 0;                 // chains inside a greedy decode loop
+  int active = 0;                 // chains inside the batcher
   std::vector<Req*> pend;         // requests of the batch being collected
   long long round = 0;            // completed launches
   bool running = false;           // a batch is on the GPU (new requests wait for the next)
   std::exception_ptr err;         // failure of the last launch (rethrown to its requesters)
   hipStream_t s = nullptr;
   int d = 0, V = 0, H = 0;
-  DevMem xd, qkvd, attd, qx, mlpd, logits, work, tokout, ctl, rows_tok, rows_pos, rows_seq, row_xkv, part_o, part_ml;
-  DevMem grp, lead, beamc;
-  int* h_rows = nullptr;          // [4][RB]: tokens, positions, sequences, group sizes
-  LogitsCtl* h_ctl = nullptr;
-  const f16** h_xkv = nullptr;
-  TokOut* h_tok = nullptr;
-  BeamCand* h_beam = nullptr;     // [RB][BEAM_KMAX]
+  RowsBufs bufs;
+  std::unique_ptr<RowBatch> tb;
+  DevMem work, tokout, ctl, beamc;
+  LogitsCtl* h_ctl = nullptr;     // [LB]
+  TokOut* h_tok = nullptr;        // [LB]
+  BeamCand* h_beam = nullptr;     // [LB][BEAM_KMAX]
   struct G {
     hipGraphExec_t exec = nullptr;
     VocabIds vids{};
   };
-  std::map<long long, G> graphs;  // by (K, grouped, groups, row count)
+  std::map<long long, G> graphs;  // decode-only batches, by (K, group kind, groups, rows)
 };
 
 StepBatcher::StepBatcher(Context& ctx) : ctx_(ctx), m_(new Impl) {
@@ -2371,30 +2132,15 @@ StepBatcher::StepBatcher(Context& ctx) : ctx_(ctx), m_(new Impl) {
   int lo = 0, hi = 0;
   WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
   WDR_HIP(hipStreamCreateWithPriority(&m.s, hipStreamNonBlocking, hi));
-  const int d = m.d;
-  m.xd = DevMem((size_t)RB * d * 4);
-  m.qkvd = DevMem((size_t)RB * 3 * d * 2);
-  m.attd = DevMem((size_t)RB * d * 2);
-  m.qx = DevMem((size_t)RB * d * 2);
-  m.mlpd = DevMem((size_t)RB * 4 * d * 2);
-  m.logits = DevMem((size_t)RB * m.V * 4);
-  m.work = DevMem((size_t)RB * m.V * 4);
-  m.tokout = DevMem(RB * sizeof(TokOut));
-  m.ctl = DevMem(RB * sizeof(LogitsCtl));
-  m.rows_tok = DevMem(RB * 4);
-  m.rows_pos = DevMem(RB * 4);
-  m.rows_seq = DevMem(RB * 4);
-  m.row_xkv = DevMem(RB * sizeof(void*));
-  m.part_o = DevMem((size_t)NSPLIT * RB * m.H * 64 * 4);
-  m.part_ml = DevMem((size_t)NSPLIT * RB * m.H * sizeof(float2));
-  m.grp = DevMem(RB * 4);
-  m.lead = DevMem(RB * 4);
-  m.beamc = DevMem((size_t)RB * BEAM_KMAX * sizeof(BeamCand));
-  WDR_HIP(hipHostMalloc((void**)&m.h_beam, (size_t)RB * BEAM_KMAX * sizeof(BeamCand), hipHostMallocDefault));
-  WDR_HIP(hipHostMalloc((void**)&m.h_rows, 5 * RB * 4, hipHostMallocDefault));
-  WDR_HIP(hipHostMalloc((void**)&m.h_ctl, RB * sizeof(LogitsCtl), hipHostMallocDefault));
-  WDR_HIP(hipHostMalloc((void**)&m.h_xkv, RB * sizeof(void*), hipHostMallocDefault));
-  WDR_HIP(hipHostMalloc((void**)&m.h_tok, RB * sizeof(TokOut), hipHostMallocDefault));
+  m.bufs.alloc(RB, LB, m.d, m.H, m.V);
+  m.tb = std::make_unique<RowBatch>(RB, LB, RB);
+  m.work = DevMem((size_t)LB * m.V * 4);
+  m.tokout = DevMem(LB * sizeof(TokOut));
+  m.ctl = DevMem(LB * sizeof(LogitsCtl));
+  m.beamc = DevMem((size_t)LB * BEAM_KMAX * sizeof(BeamCand));
+  WDR_HIP(hipHostMalloc((void**)&m.h_beam, (size_t)LB * BEAM_KMAX * sizeof(BeamCand), hipHostMallocDefault));
+  WDR_HIP(hipHostMalloc((void**)&m.h_ctl, LB * sizeof(LogitsCtl), hipHostMallocDefault));
+  WDR_HIP(hipHostMalloc((void**)&m.h_tok, LB * sizeof(TokOut), hipHostMallocDefault));
 }
 
 StepBatcher::~StepBatcher() {
@@ -2405,9 +2151,7 @@ StepBatcher::~StepBatcher() {
     (void)hipStreamSynchronize(m_->s);
     (void)hipStreamDestroy(m_->s);
   }
-  (void)hipHostFree(m_->h_rows);
   (void)hipHostFree(m_->h_ctl);
-  (void)hipHostFree(m_->h_xkv);
   (void)hipHostFree(m_->h_tok);
   (void)hipHostFree(m_->h_beam);
 }
@@ -2476,75 +2220,82 @@ void StepBatcher::step(Req& r) {
   if (m.err) std::rethrow_exception(m.err);
 }
 
-// one R-row step: embed, the layer chain with per-row cross-K/V (grouped by request), logit
-// rules + greedy pick, and the top-K candidates of every row when a request asks for them
+// one batch: every request's DTW rows, decode rows and prefill rows as ONE rows forward (rows.h),
+// then the logit rules + greedy pick of every logit row, and the top-K candidates when a request
+// asks for them.  Decode-only batches replay a graph captured per shape; batches holding a
+// prefill or a DTW re-forward (shapes vary with the prompt) launch eagerly.
 void StepBatcher::launch(std::vector<Req*>& batch) {
   Impl& m = *m_;
-  int R = 0, K = 0;
-  bool grouped = false;
-  for (Req* q : batch) {
-    WDR_CHECK(q->n >= 1 && q->n <= kRows && q->K >= 0 && q->K <= BEAM_KMAX, "step batcher: bad request");
-    R += q->n;
-    K = std::max(K, q->K);
-    grouped = grouped || q->n > 1 || q->K > 0;
-  }
-  WDR_CHECK(R >= 1 && R <= RB, "step batcher: row count out of range");
-  WDR_HIP(hipSetDevice(ctx_.cp.gpu_device));
-  {
-    int i = 0, g = 0;
-    for (Req* q : batch) {
-      m.h_rows[4 * RB + g++] = i;   // the group's first row
-      for (int j = 0; j < q->n; ++j, ++i) {
-        m.h_rows[i] = q->tok[j];
-        m.h_rows[RB + i] = q->pos[j];
-        m.h_rows[2 * RB + i] = q->seq[j];
-        m.h_rows[3 * RB + i] = j == 0 ? q->n : 0;
-        m.h_ctl[i] = q->ctl[j];
-        m.h_xkv[i] = q->xkv;
-      }
+  RowBatch& tb = *m.tb;
+  tb.clear();
+  int K = 0, n_pre = 0, n_dtw = 0;
+  std::vector<int> lidx(batch.size(), -1), lpre(batch.size(), -1);
+  for (size_t i = 0; i < batch.size(); ++i) {
+    Req* q = batch[i];
+    WDR_CHECK(q->n >= 0 && q->n <= kRows && q->K >= 0 && q->K <= BEAM_KMAX && q->pn >= 0 && q->dn >= 0 &&
+                  q->n + q->pn + q->dn > 0,
+              "step batcher: bad request");
+    if (q->dn > 0) {
+      RowGroupDesc g;
+      g.n = q->dn;
+      g.tok = q->dtok;
+      g.seq0 = q->dseq;
+      g.xkv = q->dxkv;
+      g.cap = q->dcap;
+      g.l_end = q->dl_end;
+      tb.add(g);
+      n_dtw += q->dn;
+    }
+    if (q->n > 0) {
+      RowGroupDesc g;
+      g.n = q->n;
+      g.tok = q->tok;
+      g.seq = q->seq;
+      g.pos = q->pos;
+      g.xkv = q->xkv;
+      g.logits = 2;
+      lidx[i] = tb.add(g);
+      for (int j = 0; j < q->n; ++j) m.h_ctl[lidx[i] + j] = q->ctl[j];
+      K = std::max(K, q->K);
+    }
+    if (q->pn > 0) {
+      RowGroupDesc g;
+      g.n = q->pn;
+      g.tok = q->ptok;
+      g.seq0 = q->pseq;
+      g.xkv = q->pxkv;
+      g.logits = 1;
+      lpre[i] = tb.add(g);
+      m.h_ctl[lpre[i]] = q->pctl;
+      n_pre += q->pn;
     }
   }
+  const int R = tb.R, NL = tb.n_logit;
   const VocabIds& vids = batch[0]->vids;
-  const HParams& hp = ctx_.model.hp;
-  const long long seq_stride = (long long)hp.n_text_ctx * m.d;
-  StepIO io{m.xd.as<float>(), m.qkvd.as<f16>(), m.attd.as<f16>(), m.qx.as<f16>(), m.mlpd.as<f16>(),
-            m.logits.as<float>(), m.V, m.part_o.as<float>(), m.part_ml.as<float2>(), m.rows_tok.as<int>(),
-            m.rows_pos.as<int>(), m.rows_seq.as<int>(), ctx_.kv_k.as<f16>(), ctx_.kv_v.as<f16>(),
-            (long long)ctx_.max_chains * NSLOT * seq_stride, seq_stride, nullptr, m.row_xkv.as<const f16*>()};
-  if (grouped) {
-    io.grp = m.grp.as<int>();
-    io.n_grp = (int)batch.size();
-    io.lead = m.lead.as<int>();
-  }
-  auto body = [&]() {
-    WDR_HIP(wdr_memcpy_async(m.rows_tok.p, m.h_rows, R * 4, hipMemcpyHostToDevice, m.s));
-    WDR_HIP(wdr_memcpy_async(m.rows_pos.p, m.h_rows + RB, R * 4, hipMemcpyHostToDevice, m.s));
-    WDR_HIP(wdr_memcpy_async(m.rows_seq.p, m.h_rows + 2 * RB, R * 4, hipMemcpyHostToDevice, m.s));
-    if (grouped) {
-      WDR_HIP(wdr_memcpy_async(m.grp.p, m.h_rows + 3 * RB, R * 4, hipMemcpyHostToDevice, m.s));
-      WDR_HIP(wdr_memcpy_async(m.lead.p, m.h_rows + 4 * RB, io.n_grp * 4, hipMemcpyHostToDevice, m.s));
-    }
-    WDR_HIP(wdr_memcpy_async(m.ctl.p, m.h_ctl, R * sizeof(LogitsCtl), hipMemcpyHostToDevice, m.s));
-    WDR_HIP(wdr_memcpy_async(m.row_xkv.p, m.h_xkv, R * sizeof(void*), hipMemcpyHostToDevice, m.s));
-    launch_embed(ctx_.model.tok_emb, ctx_.model.dec_pos, m.rows_tok.as<int>(), m.rows_pos.as<int>(), R, m.d,
-                 m.xd.as<float>(), m.s);
-    decode_step_layers(ctx_, io, R, m.s);
-    launch_logits_process(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), vids, R, m.work.as<float>(),
+  WDR_HIP(hipSetDevice(ctx_.cp.gpu_device));
+  RowsIO io = m.bufs.io(ctx_, m.V);
+  auto tail = [&]() {   // logit rules, greedy pick and top-K of the logit rows (after the forward)
+    if (NL == 0) return;
+    WDR_HIP(wdr_memcpy_async(m.ctl.p, m.h_ctl, NL * sizeof(LogitsCtl), hipMemcpyHostToDevice, m.s));
+    launch_logits_process(m.bufs.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), vids, NL, m.work.as<float>(),
                           m.tokout.as<TokOut>(), m.s);
-    WDR_HIP(wdr_memcpy_async(m.h_tok, m.tokout.p, R * sizeof(TokOut), hipMemcpyDeviceToHost, m.s));
+    WDR_HIP(wdr_memcpy_async(m.h_tok, m.tokout.p, NL * sizeof(TokOut), hipMemcpyDeviceToHost, m.s));
     if (K > 0) {
-      launch_logits_topk(m.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), vids, R, K, m.work.as<float>(),
+      launch_logits_topk(m.bufs.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), vids, NL, K, m.work.as<float>(),
                          m.beamc.as<BeamCand>(), m.s);
-      WDR_HIP(wdr_memcpy_async(m.h_beam, m.beamc.p, (size_t)R * K * sizeof(BeamCand), hipMemcpyDeviceToHost, m.s));
+      WDR_HIP(wdr_memcpy_async(m.h_beam, m.beamc.p, (size_t)NL * K * sizeof(BeamCand), hipMemcpyDeviceToHost, m.s));
     }
   };
   const double t_step = now_s();
   const bool sampled = prof_step();
-  if (sampled || getenv("WDR_NO_GRAPH")) {
-    // sampled step for live kernel timing (prof.h), or graphs disabled
+  const bool decode_only = n_pre == 0 && n_dtw == 0;
+  if (sampled || getenv("WDR_NO_GRAPH") || !decode_only) {
+    // sampled step for live kernel timing (prof.h), graphs disabled, or a mixed batch
     prof_in_step(sampled);
     try {
-      body();
+      tb.upload(io, m.s, true, false);
+      rows_forward(ctx_, io, R, m.s);
+      tail();
     } catch (...) {
       prof_in_step(false);
       throw;
@@ -2552,7 +2303,8 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
     prof_in_step(false);
   } else {
     // the cross-attention grid has one workgroup row per group: the group count is in the key
-    Impl::G& g = m.graphs[((long long)K << 40) + (grouped ? 1ll << 39 : 0ll) + ((long long)(grouped ? io.n_grp : 0) << 16) + R];
+    const bool grouped = tb.vgrp_max > 1;
+    Impl::G& g = m.graphs[((long long)K << 40) + (grouped ? 1ll << 39 : 0ll) + ((long long)tb.n_vgrp << 16) + R];
     if (g.exec && memcmp(&g.vids, &vids, sizeof(VocabIds)) != 0) {
       (void)hipGraphExecDestroy(g.exec);
       g.exec = nullptr;
@@ -2561,12 +2313,16 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
       hipGraph_t graph;
       prof_capture(true);
       WDR_HIP(hipStreamBeginCapture(m.s, hipStreamCaptureModeThreadLocal));
-      body();
+      tb.upload(io, m.s, true, false);
+      rows_forward(ctx_, io, R, m.s);
+      tail();
       prof_capture(false);
       WDR_HIP(hipStreamEndCapture(m.s, &graph));
       WDR_HIP(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
       WDR_HIP(hipGraphDestroy(graph));
       g.vids = vids;
+    } else {
+      tb.upload(io, m.s, false, false);   // the captured copy node reads the staging
     }
     {
       std::mutex* mu = launch_lock();   // WDR_LAUNCH_LOCK (prof.h)
@@ -2577,31 +2333,41 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
     }
   }
   WDR_HIP(hipStreamSynchronize(m.s));
-  {
-    int i = 0;
-    for (Req* q : batch)
-      for (int j = 0; j < q->n; ++j, ++i) {
-        const TokOut& o = m.h_tok[i];
-        TokenData& t = q->out[j];
-        t = TokenData{};
-        t.id = o.id;
-        t.tid = o.tid;
-        t.p = o.p;
-        t.plog = o.plog;
-        t.pt = o.pt;
-        t.ptsum = o.ptsum;
+  auto tok_of = [&](int i) {
+    const TokOut& o = m.h_tok[i];
+    TokenData t{};
+    t.id = o.id;
+    t.tid = o.tid;
+    t.p = o.p;
+    t.plog = o.plog;
+    t.pt = o.pt;
+    t.ptsum = o.ptsum;
+    return t;
+  };
+  for (size_t i = 0; i < batch.size(); ++i) {
+    Req* q = batch[i];
+    if (lidx[i] >= 0)
+      for (int j = 0; j < q->n; ++j) {
+        q->out[j] = tok_of(lidx[i] + j);
         if (q->K > 0)
-          for (int k = 0; k < q->K; ++k) q->cand[j * q->K + k] = m.h_beam[(size_t)i * K + k];
+          for (int k = 0; k < q->K; ++k) q->cand[j * q->K + k] = m.h_beam[(size_t)(lidx[i] + j) * K + k];
       }
+    if (lpre[i] >= 0) {
+      q->pout = tok_of(lpre[i]);
+      q->pnosp = m.h_tok[lpre[i]].nosp_prob;
+    }
   }
   launches++;
   rows += R;
+  prefill_rows += n_pre;
+  dtw_rows += n_dtw;
+  if (!decode_only) mixed++;
   const double t_end = now_s();
   step_s += t_end - t_step;
-  // WDR_BATCH_LOG=<file>: one line per launch (start s, rows, wall ms) for schedule analysis
+  // WDR_BATCH_LOG=<file>: one line per launch (start s, rows, wall ms, prefill rows, DTW rows)
   static FILE* blog = getenv("WDR_BATCH_LOG") ? fopen(getenv("WDR_BATCH_LOG"), "w") : nullptr;
   if (blog) {
-    fprintf(blog, "%.6f %d %.3f\n", t_step, R, (t_end - t_step) * 1e3);
+    fprintf(blog, "%.6f %d %.3f %d %d\n", t_step, R, (t_end - t_step) * 1e3, n_pre, n_dtw);
     fflush(blog);
   }
 }

@@ -712,12 +712,11 @@ class WhisperContext:
                                          out.ctypes.data_as(C.POINTER(C.c_float))))
         return out
 
-    def step(self, tokens, classic: bool = False) -> np.ndarray:
-        """Prefill tokens[:-1], then one decode step of tokens[-1] (persistent one-launch step,
-        or the per-kernel chain when classic)."""
+    def step(self, tokens) -> np.ndarray:
+        """Prefill tokens[:-1], then one decode step of tokens[-1]: the step's logits."""
         t = np.ascontiguousarray(tokens, np.int32)
         out = np.zeros(self.hparams["n_vocab"], np.float32)
-        L.check(self._lib.wdr_dbg_step(self.h, t.ctypes.data_as(C.POINTER(C.c_int32)), t.size, 1 if classic else 0,
+        L.check(self._lib.wdr_dbg_step(self.h, t.ctypes.data_as(C.POINTER(C.c_int32)), t.size,
                                        out.ctypes.data_as(C.POINTER(C.c_float))))
         return out
 

@@ -162,8 +162,7 @@ _SIGS = {
     "wdr_dbg_encode": (C.c_int, [vp, P(f32), P(f32)]),
     "wdr_dbg_decode": (C.c_int, [vp, P(i32), sz, P(f32)]),
     "wdr_dbg_cross_kv": (C.c_int, [vp, P(f32)]),
-    "wdr_dbg_step": (C.c_int, [vp, P(i32), sz, i32, P(f32)]),
-    "wdr_dbg_step_trace": (C.c_int, [vp, P(u64), i32, P(i32)]),
+    "wdr_dbg_step": (C.c_int, [vp, P(i32), sz, P(f32)]),
     "wdr_dbg_capture": (C.c_int, [vp, P(i32), sz, P(f32)]),
     "wdr_dbg_dtw": (C.c_int, [P(f32), i32, i32, i32, i32, i32, P(f32), P(i32), P(i32)]),
     "wdr_dbg_discrete": (C.c_int, [P(f32), sz, C.c_uint32, i32, P(i32)]),

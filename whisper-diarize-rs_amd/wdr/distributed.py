@@ -218,12 +218,19 @@ def _raw_block(ctx, options: TranscribeOptions):
 
 def _as_block(fn):
     """block_fn(segs, prompt, rng) -> (groups, lang, sampled flags, rng after); a 2-argument
-    function returning (groups, lang) is taken as one that never draws random numbers."""
+    function returning (groups, lang) is taken as one that never draws random numbers.  The
+    arity is decided once from the signature: an error raised inside the block is never retried
+    (a retry without the RNG state would silently change sampled results)."""
+    import inspect
+    try:
+        params = inspect.signature(fn).parameters.values()
+        positional = [p for p in params if p.kind in (p.POSITIONAL_ONLY, p.POSITIONAL_OR_KEYWORD)]
+        takes_rng = len(positional) >= 3 or any(p.kind == p.VAR_POSITIONAL for p in params)
+    except (TypeError, ValueError):   # builtins without a signature: the documented 3-argument form
+        takes_rng = True
+
     def run(segs, prompt, rng):
-        try:
-            r = fn(segs, prompt, rng)
-        except TypeError:
-            r = fn(segs, prompt)
+        r = fn(segs, prompt, rng) if takes_rng else fn(segs, prompt)
         if len(r) == 2:
             return r[0], r[1], [False] * len(segs), rng
         return r
