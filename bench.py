@@ -52,8 +52,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="large-v3")
     ap.add_argument("--seconds", type=float, default=3600.0, help="audio seconds per rank")
-    ap.add_argument("--prof", default="gemm,gemv,flash,xattn",
-                    help="kernel classes timed live with HIP events (comma list of gemm, gemv, flash, xattn; "
+    ap.add_argument("--prof", default="gemm,rows,flash,xattn",
+                    help="kernel classes timed live with HIP events (comma list of gemm, rows, flash, xattn; "
                          "'none'): the roofline figure is the one with the largest share of kernel time")
     ap.add_argument("--seg", default="diarize", choices=["diarize", "vad"],
                     help="segmentation stage: pyannote diarization (default) or Silero VAD")
@@ -81,32 +81,81 @@ def pmc_traffic(cls):
         os.path.relpath(files[-1], ROOT)
 
 
-# BASELINE.md §3 units of work: encoder + cross-K/V per 30-s window (MFMA flops) and the decode
-# step's bytes split into the decoder weights (streamed once per launched step, shared by its
-# rows) and one row's cross-K/V (read per row).
-WORK = {"large-v3": {"enc_flops": 2.589e12, "dec_weight_bytes": 1.601e9, "xkv_row_bytes": 0.246e9},
-        "base.en": {"enc_flops": 96.8e9, "dec_weight_bytes": 97.1e6, "xkv_row_bytes": 18.4e6}}
+# BASELINE.md §3 units of work: encoder + cross-K/V per 30-s window (MFMA flops: the GEMMs --
+# conv1, conv2, 32 x (qkv, o, fc1, fc2), the cross-K/V projection -- and the self-attention),
+# and a decoder pass's bytes: the decoder weights (streamed once per rows launch, shared by its
+# rows) and one slot's cross-K/V (read once per cross-attention group or MFMA row tile).
+WORK = {"large-v3": {"enc_flops": 2.589e12, "enc_gemm_flops": 2.221e12, "enc_attn_flops": 0.369e12,
+                     "dec_weight_bytes": 1.601e9, "xkv_row_bytes": 0.246e9},
+        "base.en": {"enc_flops": 96.8e9, "enc_gemm_flops": 87.6e9, "enc_attn_flops": 9.2e9,
+                    "dec_weight_bytes": 97.1e6, "xkv_row_bytes": 18.4e6}}
 
 
 def pipeline_roofline(model, times, t_wall):
     """Whole-pipeline roofline of one step (BASELINE.md §3 'roofline.achieved = T_roof / T_wall'
-    with the schedule actually used): encoder windows at the dense f16 MFMA peak; decode steps
-    (each launched step streams the decoder weights once, each row its cross-K/V), prompt
-    prefills and DTW re-forwards (one decode step of bytes each) at the HBM peak."""
+    with the schedule actually used): encoder windows at the dense f16 MFMA peak; the decoder
+    passes at the HBM peak -- every rows launch streams the decoder weights once for all its
+    rows (decode steps, prompt prefills, DTW re-forwards: csrc/rows.h), every cross-attention
+    group / MFMA row tile reads its slot's cross-K/V once.  Passes outside the batcher (one
+    chain: each step, prefill and DTW pass its own launch) count one launch and one slot each."""
     w = WORK.get(model)
     if w is None:
         return None
-    windows, steps, prefills = times["windows"], times["decode_steps"], times["prefills"]
-    launches = times.get("batch_launches", 0) + (steps - times.get("batch_rows", 0))
+    windows = times["windows"]
+    bl = times.get("batch_launches", 0)
+    if bl:
+        launches = bl
+        slot_reads = times.get("batch_xattn_groups", 0) + times.get("batch_xattn_tiles", 0)
+    else:
+        launches = times["decode_steps"] + times["prefills"] + windows
+        slot_reads = launches
     t_enc = windows * w["enc_flops"] / (MFMA_F16_PEAK_TFS * 1e12)
-    t_dec = (launches * w["dec_weight_bytes"] + steps * w["xkv_row_bytes"]) / (HBM_PEAK_GBS * 1e9)
-    step_bytes = w["dec_weight_bytes"] + w["xkv_row_bytes"]
-    t_pre = (prefills + windows) * step_bytes / (HBM_PEAK_GBS * 1e9)   # prompt prefills + DTW re-forwards
-    t_roof = t_enc + t_dec + t_pre
+    t_dec = (launches * w["dec_weight_bytes"] + slot_reads * w["xkv_row_bytes"]) / (HBM_PEAK_GBS * 1e9)
+    t_roof = t_enc + t_dec
     return {"t_roof_s": round(t_roof, 4), "t_wall_s": round(t_wall, 4), "frac": round(t_roof / t_wall, 4),
-            "terms_s": {"encoder_mfma": round(t_enc, 4), "decode_steps_hbm": round(t_dec, 4),
-                        "prefill_dtw_hbm": round(t_pre, 4)},
-            "step_launches": launches}
+            "terms_s": {"encoder_mfma": round(t_enc, 4), "decoder_rows_hbm": round(t_dec, 4)},
+            "rows_launches": launches, "slot_reads": slot_reads}
+
+
+def trace_roofline(model, fp8=False):
+    """The class-wide roofline fractions of the committed rocprofv3 trace of this benched
+    configuration (profiles/rNN/prof_graph/: classes.json from tools/prof_summary.py --json, the
+    traced run's own bench line for its work counts): achieved = the class's algorithmic work
+    over the traced runs / its summed kernel time.  Reproducible from profiles/ alone."""
+    import glob
+    w = WORK.get(model)
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "prof_graph", "classes.json")))
+    if not cands or w is None:
+        return None
+    d = os.path.dirname(cands[-1])
+    try:
+        cls = json.load(open(cands[-1]))
+        line = json.loads(open(os.path.join(d, "bench_trace.json")).read().splitlines()[0])
+    except (OSError, ValueError, IndexError):
+        return None
+    runs = line["warmup"] + line["steps"]          # the trace covers every run of the command
+    c = line["counts"]
+    out = {"source": os.path.relpath(d, ROOT), "traced_runs": runs}
+    pk = MFMA_FP8_PEAK_TFS if fp8 else MFMA_F16_PEAK_TFS
+    for k, work, unit in (("gemm", runs * c["windows"] * w["enc_gemm_flops"], "TFLOP/s"),
+                          ("flash", runs * c["windows"] * w["enc_attn_flops"], "TFLOP/s"),
+                          ("rows", runs * c.get("batch_launches", 0) * w["dec_weight_bytes"], "GB/s"),
+                          ("xattn", runs * (c.get("batch_xattn_groups", 0) + c.get("batch_xattn_tiles", 0))
+                           * w["xkv_row_bytes"], "GB/s")):
+            k_ms = cls["classes"].get(k, {}).get("total_ms")
+            if not k_ms or not work:
+                continue
+            if unit == "TFLOP/s":
+                ach = work / (k_ms * 1e-3) / 1e12
+                out[k] = {"achieved": round(ach, 2), "peak": pk if k == "gemm" else MFMA_F16_PEAK_TFS, "unit": unit}
+            else:
+                ach = work / (k_ms * 1e-3) / 1e9
+                out[k] = {"achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": unit}
+            out[k]["frac"] = round(ach / out[k]["peak"], 4)
+            out[k]["share"] = round(cls["classes"][k].get("share", 0.0), 4)
+            out[k]["launches"] = cls["classes"][k]["launches"]
+            out[k]["avg_us"] = round(cls["classes"][k]["avg_us"], 3)
+    return out
 
 
 def cpu_baseline(model, segs, audio_target):
@@ -152,10 +201,12 @@ def cpu_baseline(model, segs, audio_target):
             prev_len = L - 3
             seek += 3000
     pcm0 = pcm_i16_to_f32(sel[0].samples)
-    threads_max = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    # the host cores this process may run on (the box's share, not the machine's CPU count)
+    threads_max = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     out = {}
     for threads in sorted({4, threads_max}):
         with threadpool_limits(limits=threads):
+            threads_used = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
             t = time.perf_counter()
             mel = log_mel(pcm0, hp.n_mels)
             t_mel_per_s = (time.perf_counter() - t) / (pcm0.size / 16000.0)
@@ -179,7 +230,8 @@ def cpu_baseline(model, segs, audio_target):
             t_dtw_tok = (time.perf_counter() - t) / len(dt_toks)
         T = (audio * t_mel_per_s + n_win * t_enc + (n_steps + n_lang) * t_step + prefill_toks * t_pre_tok
              + dtw_toks * t_dtw_tok)
-        out[threads] = dict(xrt=float(sel[-1].end) / T, t_enc_s=round(t_enc, 3), t_step_ms=round(t_step * 1e3, 2),
+        out[threads] = dict(xrt=float(sel[-1].end) / T, blas_threads=threads_used, t_enc_s=round(t_enc, 3),
+                            t_step_ms=round(t_step * 1e3, 2),
                             t_prefill_tok_ms=round(t_pre_tok * 1e3, 2), t_dtw_tok_ms=round(t_dtw_tok * 1e3, 2))
     del m
     sample = ("first %d segments (%.1f s of speech over %.1f s of audio: %d windows, %d decode steps, %d prompt + %d DTW tokens) of "
@@ -231,7 +283,7 @@ def main():
     vad = None if diarize else wdr.Vad(gpu_device=local)
     dia = wdr.Diarizer(gpu_device=local) if diarize else None
     lib = wdr._lib.load()
-    CLS = {"gemm": 1, "gemv": 2, "flash": 3, "xattn": 4}
+    CLS = {"gemm": 1, "rows": 2, "flash": 3, "xattn": 4}
     prof = [c for c in args.prof.split(",") if c in CLS]
     prof_mask = sum(1 << CLS[c] for c in prof)
 
@@ -352,15 +404,22 @@ def main():
         r["sampling"] = "1 in %d launches (decode steps: 1 in %d eager, 1 in %d of those)" % (
             PROF_EVERY * PROF_STEP_EVERY, PROF_STEP_EVERY, PROF_EVERY)
         classes[c] = r
-    # `roofline` = the encoder GEMM class: the largest share of kernel time in the rocprofv3 trace
-    # of this benched configuration (profiles/r02/prof_graph/summary.txt: gemm 25.1 %, gemv 17.6 %,
-    # flash 11.0 %, xattn 6.6 % -- 1 h, graphs on).  The live sampler's own shares are not used
-    # for the pick: its sampled decode steps run eagerly (csrc/prof.h), which lengthens the GEMV
-    # launches it times (11-19 us live vs 7.4 us traced).
-    roof = classes.get("gemm") or (max(classes.values(), key=lambda r: r["sampled_ms"]) if classes else None)
+    # `roofline` = the class with the largest share of kernel time in the committed rocprofv3
+    # trace of this benched configuration (profiles/rNN/prof_graph/classes.json; r03: encoder
+    # GEMMs 30.7 %, decoder rows 27.3 %, cross-attention 11.2 %, encoder flash 8.7 %), the
+    # encoder GEMM class without one.  The live sampler's own shares are not used for the pick:
+    # its sampled decode steps run eagerly (csrc/prof.h).
+    trace = trace_roofline(args.model, args.fp8)
+    shares = {k: v.get("share", 0.0) for k, v in (trace or {}).items() if isinstance(v, dict) and k in classes}
+    pick = max(shares, key=shares.get) if shares else "gemm"
+    roof = classes.get(pick) or (max(classes.values(), key=lambda r: r["sampled_ms"]) if classes else None)
     if roof is not None:
-        roof = dict(roof, dominant_by="rocprofv3 kernel-time share of the benched configuration "
-                                      "(profiles/r02/prof_graph/summary.txt)")
+        roof = dict(roof, dominant_by="rocprofv3 kernel-time share of the benched configuration (%s)"
+                    % ((trace or {}).get("source", "no committed trace")))
+        if trace and roof["kernel"] in trace:
+            # the same class over the whole traced run (class-wide work / summed kernel time)
+            roof["trace_achieved"] = trace[roof["kernel"]]["achieved"]
+            roof["trace_frac"] = trace[roof["kernel"]]["frac"]
 
     pipe = pipeline_roofline(args.model, times, dt / args.steps)
 
@@ -368,7 +427,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ctx.close()
         res, sample, tmax = cpu_baseline(args.model, segs, args.cpu_audio)
-        cpu = {"value": round(res[tmax]["xrt"], 5), "unit": "audio-sec/wall-sec", "cores": tmax, "kind": "port",
+        cpu = {"value": round(res[tmax]["xrt"], 5), "unit": "audio-sec/wall-sec", "cores": res[tmax]["blas_threads"],
+               "kind": "port", "cores_available": tmax,
                "sample": sample, "extrapolated": True, "host_cpus": os.cpu_count(),
                "by_threads": {str(k): {kk: (round(vv, 5) if kk == "xrt" else vv) for kk, vv in r.items()}
                               for k, r in res.items()}}
@@ -392,7 +452,8 @@ def main():
                        "parallelism": ("one file of %d x %.0f s over %d GPUs: pyannote windows + speech-segment blocks "
                                        "sharded, parallel prompt fix-up rounds, results gathered (wdr/distributed.py)"
                                        % (world, shard_s, world)) if world > 1 else "1 GPU"},
-            "roofline": roof, "roofline_classes": classes, "pipeline_roofline": pipe, "cpu_baseline": cpu,
+            "roofline": roof, "roofline_classes": classes, "roofline_trace": trace, "pipeline_roofline": pipe,
+            "cpu_baseline": cpu,
             "stages_s": {k: round(v, 3) for k, v in times.items() if isinstance(v, float)},
             "counts": {k: v for k, v in times.items() if isinstance(v, int)},
             "segmentation": ({"stage": "pyannote", "s_per_step": round(vad_t[0] / args.steps, 4), "segments": vad_t[1],

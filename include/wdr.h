@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define WDR_ABI_VERSION 2
+#define WDR_ABI_VERSION 3
 
 typedef struct wdr_engine wdr_engine;
 typedef struct wdr_context wdr_context;   /* ~ whisper_rs::WhisperContext (+ its state) */
@@ -159,6 +159,11 @@ typedef struct {
   double spec_s, fixup_s;
   double batch_step_s;   /* wall of the batched steps (submit -> tokens on the host), summed */
   int64_t early_fixup_segments;   /* of fixup_segments: re-decoded by the early fix-up */
+  /* ABI 3: what the batched launches carried besides decode rows -- prompt-prefill rows and DTW
+   * re-forward rows (and how many of each), launches holding any (eager), and the cross-K/V
+   * reads: one-row / beam groups (VALU kernel) and MFMA row tiles, each one slot per layer */
+  int64_t batch_prefill_rows, batch_dtw_rows, batch_prefills, batch_dtws, batch_mixed;
+  int64_t batch_xattn_groups, batch_xattn_tiles;
 } wdr_stage_times;
 
 const char* wdr_last_error(void);
@@ -342,6 +347,13 @@ int wdr_dbg_decode(wdr_context* c, const int32_t* tokens, size_t n, float* logit
  * contract makes them bit-identical to the n-token prefill's for n <= 8 (larger prefills run
  * their cross-attention on the MFMA tile kernel) */
 int wdr_dbg_step(wdr_context* c, const int32_t* tokens, size_t n, float* logits_out /* [n_vocab] */);
+/* whisper.cpp's logit rules + greedy pick (k_logits_process) on given logits
+ * [R][n_vocab] (R <= 8); per row ctl[7] = {n_tokens, last_ts, pen_ts, has_ts, seek_delta, force_kind
+ * (0 none, 1 only force_tok, 2 text only), force_tok} and a temperature; max_initial_ts /
+ * suppress_blank as whisper_full_params.  Out: ids [R][2] = {id, tid}, f [R][5] = {p, log p, pt,
+ * ptsum, no-speech probability} */
+int wdr_dbg_logits(wdr_context* c, const float* logits, int32_t R, const int32_t* ctl, const float* temperature,
+                   float max_initial_ts, int32_t suppress_blank, int32_t* ids_out, float* f_out);
 /* multi-chain batched step (StepBatcher) with `rows` rows on the last encoded window, `iters`
  * times after prefilling tokens[0..n-2]: host milliseconds per step (probe seam) */
 int wdr_dbg_batch_step(wdr_context* c, const int32_t* tokens, size_t n, int32_t rows, int32_t iters,
@@ -359,11 +371,16 @@ int wdr_dbg_proj_fp8(const uint16_t* a_f16, const uint16_t* w_f16, const float* 
                      float* w_scale_out);
 int wdr_dbg_proj(const uint16_t* a_f16, const uint16_t* w_f16, const float* bias, int32_t M, int32_t N, int32_t K,
                  int32_t epi, float* out /* [M][N] f32 (f16 epilogues are widened) */);
-/* epi | WDR_DBG_PROJ_STEP selects the decode-step GEMV schedule (M <= 16 rows) */
+/* epi | WDR_DBG_PROJ_STEP selects the decode-step GEMV schedule (M <= 16 rows); epi |
+ * WDR_DBG_PROJ_ROWS the decoder-rows kernel (any M, per-row arithmetic independent of M) */
 #define WDR_DBG_PROJ_STEP 0x100
+#define WDR_DBG_PROJ_ROWS 0x200
 int wdr_dbg_attn(const uint16_t* q, const uint16_t* k, const uint16_t* v, int32_t Tq, int32_t Tk, int32_t n_head,
                  int32_t causal, float* out /* [Tq][n_head*64] */);
 // decode-step cross-attention over 1500 keys (beam groups / per-row slots; see engine.cpp)
+/* decode cross-attention probe: R rows (<= 1024) over S slots [S][1500][2 * 64 H] (K then V per key);
+ * grp[r] = size of the group row r leads (0 for followers): groups above 8 rows run the decoder-
+ * rows MFMA tile kernel (every row as rows_forward computes it), else the VALU split kernel */
 int wdr_dbg_xattn(const uint16_t* q, const uint16_t* kv, const int32_t* row_slot, const int32_t* grp, int32_t R,
                   int32_t S, int32_t H, int32_t iters, float* out);
 

@@ -190,6 +190,29 @@ def test_state_full_greedy_dtw_one_window(model, speech):
     assert n >= 3
 
 
+def test_state_full_beam5_dtw_one_window(model, speech):
+    """whisper_full with the reference's DEFAULT strategy -- beam search, 5 beams, patience -1
+    (src/transcribe.rs:22-33) -- on a ~8-s segment, lang auto, heuristic timestamps and DTW:
+    the beams' candidates (top-K per beam, ordered by cumulative log-prob, duplicates dropped,
+    KV caches following their parents) and the final ranking, token by token against the
+    oracle's WhisperState.decode_beam.  At large-v3 this runs the beam-group cross-attention
+    and the rows kernel at the full width."""
+    name, ctx, hp, W, m = model
+    pcm, spurts = speech
+    a = spurts[1][0]
+    x = pcm_i16_to_f32(pcm[int(a * 16000):int((a + 8.0) * 16000)])
+    opts = wdr.TranscribeOptions(lang="auto")          # advanced None: beam search, 5 beams
+    got, lang_id = ctx.state_full(x, opts)
+    st = WhisperState(m, Vocab(hp.n_vocab), name)
+    st.full(x, FullParams(strategy="beam", beam_size=5, language="auto", force_len_rate=3.3,
+                          logprob_thold=-np.inf, entropy_thold=-1.0))
+    if st.lang_margin > MARGIN[name]:
+        assert lang_id == st.lang_id
+    n = _compare_results(got, st.result_all, name, "beam5")
+    _report(test="state_full_beam5", model=name, tokens_compared=n, tokens=sum(len(r.tokens) for r in st.result_all))
+    assert n >= 3
+
+
 def test_state_full_seek_loop(model, speech):
     """A 45-s segment: two 30-s windows, seek advanced by the segment-end rules (whisper.cpp's
     seek loop; VAD-merged segments and the whole-file branch hit it, src/vad.rs:49-63,

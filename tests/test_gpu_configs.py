@@ -1,0 +1,123 @@
+"""BASELINE.json configs exercised end to end through the C ABI, against the CPU oracle where the
+oracle can follow, by properties where it cannot (VERDICT r2 "next round" item 1(b), 1(c)).
+
+  * configs[1] (C2): base.en, Silero VAD segmentation, DTW on, the reference's default decode
+    (beam 5, lang auto), 60 s of synthetic speech through Engine::transcribe_audio
+    (src/engine.rs:123-139, 169-199) against the oracle: oracle VAD + merge (src/vad.rs:6-84)
+    -> oracle run_transcription_pipeline (src/transcribe.rs:323-535) -> oracle formatting with
+    the VAD mask (src/engine.rs:192-199);
+  * configs[2] (C3): large-v3, VAD, DTW, greedy, 30 s, the same chain;
+  * configs[3]'s per-GPU shard at full size: 1 h of 3-speaker synthetic audio, large-v3 + DTW
+    + pyannote diarization + speaker assignment (the bench workload) -- the oracle cannot follow
+    an hour of large-v3 in a test, so its output is held to the properties the reference's glue
+    guarantees: one segment list in time order after the overlap clip (src/transcribe.rs:447-459),
+    word times inside their segment, speaker ids "1".."k" or "?" (src/transcribe.rs:478-497), no
+    control token or embedded marker left in any text (src/transcribe.rs:206-240).
+
+Synthetic weights on both sides (seeded, bit-identical), decode length pinned.
+Tolerances as tests/test_gpu_baseline_models.py: segment text equal; words within 20 ms
+(>= 90 %, the rest within 40 ms: a DTW anchor two frames off a near-tie of the random-weight
+alignment matrix moves a midpoint bound by 20-40 ms).
+"""
+import re
+
+import numpy as np
+import pytest
+
+import wdr
+from oracle import formatting as F
+from oracle.model import Whisper
+from oracle.pipeline import SpeechSegment as OSeg
+from oracle.pipeline import run_transcription_pipeline, write_wav
+from oracle.vad import get_segments as oracle_vad
+from oracle.vocab import Vocab
+from oracle.weights import hparams_for, synth_weights
+from oracle.whisper_full import WhisperState
+from wdr.synth import synth_speech
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(1200)]
+
+EMB_STD = 0.5
+
+
+def _vad_pipeline_vs_oracle(tmp_path, model, seconds, seed, greedy):
+    pcm, _ = synth_speech(seconds, seed=seed)
+    path = str(tmp_path / "a.wav")
+    write_wav(path, pcm)
+    syn = wdr.Synthetic(weight_std=0.02, emb_std=EMB_STD, force_len_rate=3.3, disable_fallback=True)
+    eng = wdr.Engine(wdr.EngineConfig(cache_dir=str(tmp_path / "cache")), synthetic=syn)
+    adv = wdr.AdvancedTranscribe(sampling_strategy="greedy") if greedy else None
+    opts = wdr.TranscribeOptions(model=model, enable_vad=True, advanced=adv)   # lang auto, DTW on
+    got = eng.transcribe_audio(path, opts)
+    # oracle: VAD + merge on the same (synthetic Silero) weights, then the pipeline + formatting
+    mask, vsegs = oracle_vad(pcm)
+    gmask, gsegs = wdr.Vad().get_segments(pcm)
+    assert [(round(a, 6), round(b, 6)) for a, b in gmask] == [(round(a, 6), round(b, 6)) for a, b in mask]
+    assert [(s.start, s.end) for s in gsegs] == [(s.start, s.end) for s in vsegs] and len(vsegs) >= 2
+    hp = hparams_for(model)
+    st = WhisperState(Whisper(hp, synth_weights(hp, std=0.02, emb_std=EMB_STD)), Vocab(hp.n_vocab), model)
+    o = dict(lang="auto", synthetic=dict(force_len_rate=3.3, logprob_thold=-np.inf, entropy_thold=-1.0))
+    if greedy:
+        o["advanced"] = dict(sampling_strategy="greedy")
+    raw, lang = run_transcription_pipeline(st, [OSeg(s.start, s.end, s.samples) for s in vsegs], o)
+    want = F.process_segments([F.Seg(s.start, s.end, s.text, None if s.words is None else
+                                     [F.Word(w.text, w.start, w.end, w.probability) for w in s.words], None)
+                               for s in raw], F.config_for_language(lang or "auto"), mask)
+    assert len(got) == len(want) >= 1, (len(got), len(want))
+    dts = []
+    for g, w in zip(got, want):
+        assert g.text == w.text, (g.text, w.text)
+        assert len(g.words or []) == len(w.words or [])
+        for a, b in zip(g.words or [], w.words or []):
+            assert a.text == b.text
+            dts += [abs(a.start - b.start), abs(a.end - b.end)]
+        dts += [abs(g.start - w.start), abs(g.end - w.end)]
+    within = sum(d <= 0.02 + 1e-9 for d in dts) / max(1, len(dts))
+    assert max(dts) <= 0.04 + 1e-9 and within >= 0.9, (max(dts), within)
+    return len(vsegs), len(got), max(dts), within
+
+
+def test_c2_base_en_vad_beam5_dtw(tmp_path):
+    n_vad, n_out, dw, within = _vad_pipeline_vs_oracle(tmp_path, "base.en", 60.0, 51, greedy=False)
+    print(dict(test="c2", vad_segments=n_vad, segments=n_out, word_max_dt=dw, within_20ms=within))
+
+
+def test_c3_large_v3_vad_greedy_dtw(tmp_path):
+    n_vad, n_out, dw, within = _vad_pipeline_vs_oracle(tmp_path, "large-v3", 30.0, 52, greedy=True)
+    print(dict(test="c3", vad_segments=n_vad, segments=n_out, word_max_dt=dw, within_20ms=within))
+
+
+_MARKER = re.compile(r"\[_|<\||\|>|_\]")
+
+
+def test_c4_shard_one_hour_large_v3_diarize_properties():
+    """The bench workload at full size (bench.py: configs[3]'s 1-h per-GPU shard, greedy):
+    every property the reference's glue guarantees, on every one of ~635 segments."""
+    pcm, spurts = synth_speech(3600.0, seed=0, n_speakers=3)
+    segs = [wdr.SpeechSegment(a, b, pcm[int(round(a * 16000)):int(round(b * 16000))]) for a, b, _ in spurts]
+    syn = wdr.Synthetic(weight_std=0.02, emb_std=0.02, force_len_rate=3.3, disable_fallback=True)
+    ctx = wdr.WhisperContext("large-v3", enable_dtw=True, synthetic=syn)
+    opts = wdr.TranscribeOptions(model="large-v3", lang="auto", enable_vad=False, enable_diarize=True,
+                                 advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    out, lang = ctx.run_pipeline(segs, opts, diarize_options=wdr.DiarizeOptions.from_options(opts))
+    ctx.close()
+    assert lang is not None
+    # one whisper segment per talk spurt (one window each, single_segment, pinned decode)
+    assert len(out) == len(spurts) == 635, (len(out), len(spurts))
+    speakers = set()
+    for i, s in enumerate(out):
+        a, b, _ = spurts[i]
+        assert a - 1e-6 <= s.start <= s.end, (i, s.start, s.end)
+        assert s.end <= b + 30.0, (i, s.end, b)
+        if i + 1 < len(out):
+            assert s.end <= out[i + 1].start + 1e-9, (i, s.end, out[i + 1].start)   # overlap clip
+        assert s.text and not _MARKER.search(s.text), (i, s.text)
+        assert s.words, i
+        for w in s.words:
+            assert s.start - 1e-9 <= w.start <= w.end <= s.end + 1e-9, (i, w, s.start, s.end)
+            assert w.text and not _MARKER.search(w.text), (i, w.text)
+        assert s.speaker_id is not None
+        speakers.add(s.speaker_id)
+    ids = sorted(x for x in speakers if x != "?")
+    assert ids and ids == [str(k) for k in range(1, len(ids) + 1)], speakers
+    print(dict(test="c4_shard", segments=len(out), speakers=sorted(speakers), words=sum(len(s.words) for s in out)))

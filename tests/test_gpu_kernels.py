@@ -102,6 +102,35 @@ def test_step_projection_rows_bit_identical(lib, N, K, epi):
         np.testing.assert_array_equal(got, one[:M], err_msg="M=%d" % M)
 
 
+ROWS = 0x200   # include/wdr.h WDR_DBG_PROJ_ROWS
+
+
+@pytest.mark.parametrize("N,K,epi", [(1280, 5120, 2), (1280, 1280, 2), (3840, 1280, 0), (5120, 1280, 1),
+                                     (51866, 1280, 3)])
+def test_rows_projection_bit_identical_any_m(lib, N, K, epi):
+    """The decoder-rows kernel (csrc/rows.h: every decoder projection of steps, prompt prefills
+    and DTW re-forwards): a row's result must not depend on how many rows share the launch --
+    M = 1 .. 300 rows, one to several row tiles, the narrow (16-column) and wide (32-column)
+    tilings, the 16-wave K = 5120 form -- bit for bit, and match the fp64 product."""
+    rng = np.random.default_rng(N + K + epi + 1)
+    MX = 300
+    a = rng.standard_normal((MX, K)).astype(np.float16).astype(np.float32)
+    w = (rng.standard_normal((N, K)) * 0.03).astype(np.float16).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32) * 0.1
+    base = rng.standard_normal((MX, N)).astype(np.float32)
+    full = _proj(lib, a, w, bias, epi | ROWS, base if epi == 2 else None)
+    ref = a[:20].astype(np.float64) @ w.T.astype(np.float64) + bias
+    want = {0: ref, 1: _gelu(ref), 2: base[:20] + ref, 3: ref}[epi]
+    tol = dict(rtol=0, atol=2e-4) if epi in (2, 3) else dict(rtol=2e-3, atol=2e-3)
+    np.testing.assert_allclose(full[:20], want, **tol)
+    for M in (1, 2, 7, 16, 17, 33, 64, 130):
+        got = _proj(lib, a[:M], w, bias, epi | ROWS, base[:M] if epi == 2 else None)
+        np.testing.assert_array_equal(got, full[:M], err_msg="M=%d" % M)
+    # a row in the middle of a launch equals the same row alone
+    one = _proj(lib, a[257:258], w, bias, epi | ROWS, base[257:258] if epi == 2 else None)
+    np.testing.assert_array_equal(one, full[257:258])
+
+
 def test_projection_logits_shape(lib):
     """decoder logits: N not a multiple of the tile (51866 x d), M = 1 (GEMV path)."""
     rng = np.random.default_rng(7)
@@ -183,6 +212,35 @@ def test_decode_cross_attention(lib):
     np.testing.assert_allclose(grouped, gref, rtol=0, atol=1e-2)
     single = _xattn(lib, q, kv, H, gslot)   # same rows, every row its own group
     np.testing.assert_array_equal(grouped, single)
+
+
+def test_decode_cross_attention_mma_tiles(lib):
+    """The decoder-rows cross-attention of prompt prefills / DTW re-forwards (groups above 8
+    rows): MFMA row tiles of <= 128 rows (k_xattn_mma) beside VALU groups, merged by one
+    combine.  Every row matches the fp64 attention; a row's result does not depend on its
+    group's size or tile (a 40-row group equals the same rows as a 12 + 28 split, and a 200-row
+    group spans two tiles)."""
+    rng = np.random.default_rng(17)
+    H, S = 4, 3
+    sizes = [40, 3, 200, 1, 12]
+    R = sum(sizes)
+    q = (rng.standard_normal((R, H * 64)) * 1.5).astype(np.float16).astype(np.float32)
+    kv = rng.standard_normal((S, 1500, 2 * H * 64)).astype(np.float16).astype(np.float32)
+    grp, slot = np.zeros(R, np.int32), np.zeros(R, np.int64)
+    r0 = 0
+    for i, n in enumerate(sizes):
+        grp[r0] = n
+        slot[r0:r0 + n] = i % S
+        r0 += n
+    got = _xattn(lib, q, kv, H, slot, grp)
+    pick = list(range(0, 40, 7)) + [40, 42] + list(range(43, 243, 37)) + [243, 244, 255]
+    ref = np.concatenate([_attn_ref(q[r:r + 1], kv[slot[r], :, :H * 64], kv[slot[r], :, H * 64:], H, 0)
+                          for r in pick])
+    np.testing.assert_allclose(got[pick], ref, rtol=0, atol=1e-2)
+    assert np.abs(got[pick] - ref).mean() < 1.5e-3
+    split = grp.copy()
+    split[0], split[12] = 12, 28
+    np.testing.assert_array_equal(_xattn(lib, q, kv, H, slot, split), got)
     np.testing.assert_array_equal(_xattn(lib, q, kv, H, gslot, grp, iters=3), grouped)
     # shared K/V (one segment's beams on a State's own step), R <= 8
     shared = _xattn(lib, q[:5], kv[:1], H)

@@ -15,11 +15,16 @@ import glob
 import os
 from collections import defaultdict
 
+import re
+
+# kernel classes (bench.py's live roofline classes plus the diarization stack): the encoder
+# GEMMs are k_gemm / k_gemm2..5 / k_gemm8 -- NOT the f32 VALU k_gemm32 of CAM++ / segmentation
 CLASSES = {
-    "gemv": ("k_gemv", "k_dgemv", "k_mgemv"),   # k_mgemv also matches k_mgemv_s
-    "gemm": ("k_gemm<", "k_gemm(", "wdr::k_gemm"),
-    "flash": ("k_flash_attn",),
-    "xattn": ("k_xattn_partial",),   # the launches bench.py times (the combine is not)
+    "gemm": re.compile(r"\bk_gemm\d?[<(]"),
+    "rows": re.compile(r"\bk_skinny<"),                       # decoder row projections (rows.h)
+    "flash": re.compile(r"\bk_flash_attn\("),                # encoder self-attention
+    "xattn": re.compile(r"\bk_xattn_(partial|mma)\b"),       # decoder cross-attention partials
+    "diar": re.compile(r"\bk_(gemm32|lstm_scan|im2col_2d_b|im2col_1d_b|fbank|colstats_b|cam_|inorm|maxpool3|logsoftmax7)"),
 }
 
 
@@ -36,8 +41,8 @@ def col(row, *names):
 
 
 def classify(name):
-    for c, keys in CLASSES.items():
-        if any(k in name for k in keys):
+    for c, rx in CLASSES.items():
+        if rx.search(name):
             return c
     return None
 
@@ -99,7 +104,9 @@ def main():
     for k, (c, ns) in sorted(cls.items()):
         print("%-8s launches %8d  total %10.2f ms  avg %8.3f us  share %5.1f%%" % (k, c, ns / 1e6, ns / c / 1e3,
                                                                                   100 * ns / tot))
-    out = {"classes": {k: {"launches": c, "avg_us": ns / c / 1e3} for k, (c, ns) in cls.items()}}
+    out = {"total_kernel_ms": tot / 1e6,
+           "classes": {k: {"launches": c, "avg_us": ns / c / 1e3, "total_ms": ns / 1e6, "share": ns / tot}
+                       for k, (c, ns) in cls.items()}}
     for label, dd, counter, scale in (("FETCH_SIZE x2 (gfx950 correction)", a.fetch, "FETCH_SIZE", 2.0),
                                       ("WRITE_SIZE", a.write, "WRITE_SIZE", 1.0)):
         if not dd:

@@ -104,7 +104,8 @@ struct ProjArgs {
   int tile_gm = 0;
   // decoder rows of any count (steps, prompt prefills, DTW re-forwards) on the row kernel
   // (k_skinny's arithmetic: 8 waves split K, fixed k order, fixed wave order in the reduce), so
-  // a row's result never depends on how many rows share the launch; LN needs M <= 32
+  // a row's result never depends on how many rows share the launch (the LN prologue normalises
+  // each workgroup's own row tiles)
   int rows_mma = 0;
   // optional row map: A / ln_x row m is row_map[m] (logit rows gathered from the residual stream)
   const int* row_map = nullptr;

@@ -234,6 +234,7 @@ struct wdr_context {
   int early_fixup = -1;
   struct ChainStats {
     long long chains = 1, launches = 0, rows = 0, fixups = 0, replays = 0, early = 0;
+    long long prefill_rows = 0, dtw_rows = 0, prefills = 0, dtws = 0, mixed = 0, vgroups = 0, tiles = 0;
     double spec_s = 0, fixup_s = 0, step_s = 0;
   } cs;                                           // the last run_pipeline's multi-chain figures
   std::unique_ptr<CamModel> cam;   // EmbeddingExtractor, created on the first diarized run
@@ -718,18 +719,24 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
   std::atomic<bool> stop{false};
   std::vector<std::exception_ptr> errs(C);
   c->cs.chains = C;
-  auto batch_stats = [&](long long* l, long long* r, double* t) {
-    *l = 0, *r = 0, *t = 0;
+  auto batch_stats = [&]() {
+    Context::BatchStats o;
     for (int g = 0; g < std::min(G, C); ++g) {
-      StepBatcher& sb = (g == 0 ? *c->ctx : *c->peers[g - 1]).step_batcher();
-      *l += sb.launches;
-      *r += sb.rows;
-      *t = std::max(*t, sb.step_s);
+      const Context::BatchStats b = (g == 0 ? *c->ctx : *c->peers[g - 1]).batcher_stats();
+      o.launches += b.launches;
+      o.rows += b.rows;
+      o.prefill_rows += b.prefill_rows;
+      o.dtw_rows += b.dtw_rows;
+      o.prefills += b.prefills;
+      o.dtws += b.dtws;
+      o.mixed += b.mixed;
+      o.vgroups += b.vgroups;
+      o.tiles += b.tiles;
+      o.step_s = std::max(o.step_s, b.step_s);
     }
+    return o;
   };
-  long long l0, r0;
-  double s0;
-  batch_stats(&l0, &r0, &s0);
+  const Context::BatchStats b0 = batch_stats();
   const double t_spec = now_s();
   // dec_in[k]: the prompt chain k's first segment was last decoded from
   std::vector<Prompt> dec_in(C, e0);
@@ -936,12 +943,17 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
   }
   c->cs.fixup_s = now_s() - t_fix;
   {
-    long long l1, r1;
-    double s1;
-    batch_stats(&l1, &r1, &s1);
-    c->cs.launches = l1 - l0;
-    c->cs.rows = r1 - r0;
-    c->cs.step_s = s1 - s0;
+    const Context::BatchStats b1 = batch_stats();
+    c->cs.launches = b1.launches - b0.launches;
+    c->cs.rows = b1.rows - b0.rows;
+    c->cs.prefill_rows = b1.prefill_rows - b0.prefill_rows;
+    c->cs.dtw_rows = b1.dtw_rows - b0.dtw_rows;
+    c->cs.prefills = b1.prefills - b0.prefills;
+    c->cs.dtws = b1.dtws - b0.dtws;
+    c->cs.mixed = b1.mixed - b0.mixed;
+    c->cs.vgroups = b1.vgroups - b0.vgroups;
+    c->cs.tiles = b1.tiles - b0.tiles;
+    c->cs.step_s = b1.step_s - b0.step_s;
   }
   // stage accounting: chains' times summed into the context's state
   for (int k = 1; k < C; ++k) {
@@ -1788,6 +1800,13 @@ int wdr_context_stage_times(wdr_context* c, wdr_stage_times* o) {
     o->fixup_s = c->cs.fixup_s;
     o->batch_step_s = c->cs.step_s;
     o->early_fixup_segments = c->cs.early;
+    o->batch_prefill_rows = c->cs.prefill_rows;
+    o->batch_dtw_rows = c->cs.dtw_rows;
+    o->batch_prefills = c->cs.prefills;
+    o->batch_dtws = c->cs.dtws;
+    o->batch_mixed = c->cs.mixed;
+    o->batch_xattn_groups = c->cs.vgroups;
+    o->batch_xattn_tiles = c->cs.tiles;
     return 0;
   })
 }
@@ -1889,6 +1908,32 @@ int wdr_dbg_step(wdr_context* c, const int32_t* tokens, size_t n, float* logits_
   })
 }
 
+int wdr_dbg_logits(wdr_context* c, const float* logits, int32_t R, const int32_t* ctl, const float* temperature,
+                   float max_initial_ts, int32_t suppress_blank, int32_t* ids_out, float* f_out) {
+  WDR_GUARD({
+    WDR_CHECK(R >= 1 && R <= 8, "dbg_logits: 1..8 rows");
+    std::vector<LogitsCtl> lc(R);
+    for (int r = 0; r < R; ++r) {
+      const int32_t* q = ctl + 7 * r;
+      lc[r] = LogitsCtl{q[0], q[1], q[2], q[3], q[4], q[5], q[6], temperature[r]};
+    }
+    std::vector<TokenData> out(R);
+    std::vector<float> nosp(R);
+    c->st->dbg_logits(logits, R, lc.data(), max_initial_ts, suppress_blank != 0, out.data(), nosp.data());
+    for (int r = 0; r < R; ++r) {
+      ids_out[2 * r] = out[r].id;
+      ids_out[2 * r + 1] = out[r].tid;
+      float* f = f_out + 5 * r;
+      f[0] = out[r].p;
+      f[1] = out[r].plog;
+      f[2] = out[r].pt;
+      f[3] = out[r].ptsum;
+      f[4] = nosp[r];
+    }
+    return 0;
+  })
+}
+
 int wdr_dbg_batch_step(wdr_context* c, const int32_t* tokens, size_t n, int32_t rows, int32_t iters,
                        double* ms_per_step) {
   WDR_GUARD({
@@ -1980,14 +2025,17 @@ int wdr_dbg_proj(const uint16_t* a16, const uint16_t* w16, const float* bias, in
     WDR_HIP(hipMemcpy(da.p, a16, da.bytes, hipMemcpyHostToDevice));
     WDR_HIP(hipMemcpy(dw.p, w16, dw.bytes, hipMemcpyHostToDevice));
     if (bias) WDR_HIP(hipMemcpy(db.p, bias, db.bytes, hipMemcpyHostToDevice));
-    // epi | WDR_DBG_PROJ_STEP: the decode-step schedule (ProjArgs::step_rows, 9..16-row shapes)
+    // epi | WDR_DBG_PROJ_STEP: the decode-step schedule (ProjArgs::step_rows, 9..16-row shapes);
+    // epi | WDR_DBG_PROJ_ROWS: the decoder-rows kernel (ProjArgs::rows_mma, any M)
     const bool step = (epi & 0x100) != 0;
+    const bool rows = (epi & 0x200) != 0;
     epi &= 0xff;
     const bool f16out = epi == EPI_F16 || epi == EPI_F16_GELU;
     std::vector<f16> h16;
     if (!f16out) WDR_HIP(hipMemcpy(dout.p, out, dout.bytes, hipMemcpyHostToDevice));
     ProjArgs a{da.as<f16>(), K, dw.as<f16>(), K, bias ? db.as<float>() : nullptr, dout.p, N, nullptr, 0, M, N, K, epi};
     a.step_rows = step ? 1 : 0;
+    a.rows_mma = rows ? 1 : 0;
     launch_proj(a, nullptr);
     WDR_HIP(hipDeviceSynchronize());
     if (f16out) {
@@ -2034,7 +2082,7 @@ int wdr_dbg_attn(const uint16_t* q, const uint16_t* k, const uint16_t* v, int32_
 int wdr_dbg_xattn(const uint16_t* q, const uint16_t* kv, const int32_t* row_slot, const int32_t* grp, int32_t R,
                   int32_t S, int32_t H, int32_t iters, float* out) {
   WDR_GUARD({
-    WDR_CHECK(R >= 1 && R <= 128 && S >= 1 && H >= 1 && H <= 32 && iters >= 1, "dbg xattn: bad shape");
+    WDR_CHECK(R >= 1 && R <= 1024 && S >= 1 && H >= 1 && H <= 32 && iters >= 1, "dbg xattn: bad shape");
     const int d = H * 64, T = 1500;
     DevMem dq((size_t)R * d * 2), dkv((size_t)S * T * 2 * d * 2), dout((size_t)R * d * 2);
     DevMem po((size_t)24 * R * H * 64 * 4), pml((size_t)24 * R * H * 8);
@@ -2052,6 +2100,41 @@ int wdr_dbg_xattn(const uint16_t* q, const uint16_t* kv, const int32_t* row_slot
       WDR_HIP(hipMemcpy(drk.p, rk.data(), R * sizeof(void*), hipMemcpyHostToDevice));
       xa.row_k = drk.as<const f16*>();
       xa.v_off = d;   // this probe's K/V: [S][1500][2d], K then V per key
+      bool big = false;
+      for (int r = 0; grp && r < R; ++r) big = big || grp[r] > XATTN_GRP_MAX;
+      if (grp && big) {
+        // the decoder-rows form (rows_forward): groups of <= XATTN_GRP_MAX rows on the VALU kernel,
+        // larger ones as MFMA row tiles of <= 128 rows, one combine for every row
+        std::vector<int> g(R, 0), lead;
+        std::vector<int4> tiles;
+        for (int r = 0; r < R; ++r) {
+          if (grp[r] == 0) continue;
+          WDR_CHECK(r + grp[r] <= R, "dbg xattn: bad group");
+          if (grp[r] <= XATTN_GRP_MAX) {
+            g[r] = grp[r];
+            lead.push_back(r);
+          } else {
+            for (int t = 0; t < grp[r]; t += 128) tiles.push_back(make_int4(r + t, std::min(128, grp[r] - t), 1 << 30, 0));
+          }
+        }
+        WDR_HIP(hipMemcpy(dg.p, g.data(), R * 4, hipMemcpyHostToDevice));
+        if (!lead.empty()) WDR_HIP(hipMemcpy(dl.p, lead.data(), lead.size() * 4, hipMemcpyHostToDevice));
+        DevMem dt(std::max<size_t>(16, tiles.size() * 16));
+        if (!tiles.empty()) WDR_HIP(hipMemcpy(dt.p, tiles.data(), tiles.size() * 16, hipMemcpyHostToDevice));
+        xa.grp = dg.as<int>();
+        xa.lead = dl.as<int>();
+        xa.n_vgrp = (int)lead.size();
+        xa.vgrp_max = 1;
+        for (int r : lead) xa.vgrp_max = std::max(xa.vgrp_max, g[r]);
+        xa.tiles = dt.as<int4>();
+        xa.n_tiles = (int)tiles.size();
+        for (int i = 0; i < iters; ++i) launch_xattn_rows(xa, nullptr);
+        WDR_HIP(hipDeviceSynchronize());
+        std::vector<f16> h((size_t)R * d);
+        WDR_HIP(hipMemcpy(h.data(), dout.p, h.size() * 2, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < h.size(); ++i) out[i] = (float)h[i];
+        return 0;
+      }
       if (grp) {
         int ng = 0;
         for (int r = 0; r < R; ++r) {

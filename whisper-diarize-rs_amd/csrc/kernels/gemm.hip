@@ -2140,7 +2140,7 @@ static void launch_rows_epi(const ProjArgs& a, hipStream_t s) {
   const int mt = cdiv(a.M, 16);
   const bool ln = a.ln_x != nullptr;
   const bool wide = a.N >= 4096;
-  const int prof = a.M <= 16 ? PROF_GEMV : PROF_SKINNY;
+  const int prof = PROF_GEMV;   // the "rows" class of bench.py's live roofline (any row count)
   if (!wide) {
     // one 16-row tile per workgroup: the row tiles of a column tile re-read its weights from L2.
     // K > 2048 (fc2): 16 waves, each wave's 10 k-steps as ONE batch of loads (8 waves took three
@@ -2179,7 +2179,8 @@ static void launch_rows_epi(const ProjArgs& a, hipStream_t s) {
 
 static void launch_rows(const ProjArgs& a, hipStream_t s) {
   WDR_CHECK(a.K % 32 == 0 && a.lda % 8 == 0 && a.ldb % 8 == 0, "row projection: K % 32, lda / ldb % 8");
-  WDR_CHECK(!a.ln_x || (a.K <= 1280 && a.K % 4 == 0 && a.M <= 32), "row projection LN prologue: K <= 1280, M <= 32");
+  // LN prologue: every workgroup normalises only its own <= 32 rows (any M)
+  WDR_CHECK(!a.ln_x || (a.K <= 1280 && a.K % 4 == 0), "row projection LN prologue: K <= 1280");
   WDR_CHECK(a.epi != EPI_QKV_CACHE || (a.kc && a.vc && a.row_seq && a.row_pos && a.d > 0), "qkv-cache epilogue args");
   switch (a.epi) {
     case EPI_F16: launch_rows_epi<EPI_F16>(a, s); break;

@@ -6,6 +6,7 @@
 #include "prof.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace wdr {
@@ -160,9 +161,11 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s) {
   const float scale = 1.0f / 8.0f;
   WDR_CHECK(R >= 1 && io.tok && io.xkv, "rows forward: no rows / tables");
   launch_embed(md.tok_emb, md.dec_pos, io.tok, io.pos, R, d, io.xd, s);
-  // the projection's input rows LayerNorm(x): inside the row kernel up to 32 rows, else one
-  // k_layernorm launch (the same arithmetic) into io.hd
-  const bool fuse_ln = R <= 32;
+  // the projection's input rows LayerNorm(x): inside the row kernel (each workgroup normalises
+  // its own row tiles; WDR_ROWS_LN_SPLIT=1: one k_layernorm launch into io.hd above 32 rows --
+  // the same arithmetic either way)
+  static const bool ln_split = getenv("WDR_ROWS_LN_SPLIT") && atoi(getenv("WDR_ROWS_LN_SPLIT")) != 0;
+  const bool fuse_ln = R <= 32 || !ln_split;
   auto P = [&](const f16* A, int lda, const f16* W, const float* b, void* out, int ldo, int N, int K, int epi,
                const float* lng = nullptr, const float* lnb = nullptr) {
     ProjArgs a{A, lda, W, K, b, out, ldo, nullptr, 0, R, N, K, epi};
@@ -233,7 +236,7 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s) {
     // final LayerNorm + logits of the logit rows only, gathered by lrow (compact output)
     ProjArgs a{nullptr, d, md.tok_emb, d, nullptr, io.logits, io.ldlogits, nullptr, 0, io.n_logit, hp.n_vocab, d, EPI_F32};
     a.rows_mma = 1;
-    if (io.n_logit <= 32) {
+    if (io.n_logit <= 32 || !ln_split) {
       a.ln_x = io.xd;
       a.ldln = d;
       a.ln_g = md.ln_g;

@@ -10,7 +10,8 @@
 //   * self-attention: one workgroup per (row, head) over that row's cache prefix;
 //   * cross-attention: groups of <= XATTN_GRP_MAX rows on the VALU split kernel (a row scored with
 //     the one-row arithmetic), larger groups on the MFMA tile kernel, both merged by one combine;
-//   * LayerNorm fused into the projection up to 32 rows, else k_layernorm (same arithmetic).
+//   * LayerNorm fused into the projection (each workgroup normalises its own row tiles; the
+//     k_layernorm alternative has the same arithmetic).
 // So batching decode steps with prompt prefills and DTW re-forwards of other chains changes no
 // result: decode chains stay bit-identical to one sequential chain.
 #pragma once

@@ -98,8 +98,18 @@ class Context {
   int max_chains = 1;
   DevMem kv_k, kv_v;
   long long kv_seq_stride = 0, kv_layer_stride = 0;   // elements per (layer, sequence) / per layer
-  std::unique_ptr<class StepBatcher> batcher;     // multi-chain greedy steps (created on demand)
-  StepBatcher& step_batcher();
+  // multi-chain batched steps (created on demand): WDR_BATCHERS groups of chains, each its own
+  // batcher and stream, so the latency-bound step chains of two groups overlap on the GPU;
+  // `chain` is the State's chain index on this context
+  std::vector<std::unique_ptr<class StepBatcher>> batchers;
+  int n_batchers = 1;
+  StepBatcher& step_batcher(int chain = 0);
+  struct BatchStats {
+    long long launches = 0, rows = 0, prefill_rows = 0, dtw_rows = 0, prefills = 0, dtws = 0, mixed = 0;
+    long long vgroups = 0, tiles = 0;   // cross-attention groups (VALU) / row tiles (MFMA) launched
+    double step_s = 0;                  // the slowest batcher's launch wall
+  };
+  BatchStats batcher_stats();
   // fp8 (e4m3) encoder GEMMs (BASELINE configs[4]; wdr_context_set_encoder_fp8, WDR_FP8_ENCODER):
   // the encoder's projection and cross-K/V weights quantised per output channel, made once on
   // first use; activations are quantised per row in the encoder
@@ -199,7 +209,8 @@ class StepBatcher {
   void leave();
   void step(Req& r);           // blocks until the batch holding r has run
   void run(std::vector<Req*>& batch) { launch(batch); }   // one batch, caller's thread (test seam)
-  long long launches = 0, rows = 0, prefill_rows = 0, dtw_rows = 0, mixed = 0;
+  long long launches = 0, rows = 0, prefill_rows = 0, dtw_rows = 0, prefills = 0, dtws = 0, mixed = 0;
+  long long vgroups = 0, tiles = 0;
   double step_s = 0;           // wall of the launches (submit -> results on the host)
   struct Impl;
 
@@ -256,6 +267,10 @@ class State {
   void decode_logits(const int* toks, int n, float* logits_out);   // prefill from an empty cache
   void dbg_step(const int* toks, int n, float* logits_out);
   void dtw_capture(const int* toks, int n, float* cap_out);        // [n_aheads][n][1500]
+  // the logit rules + greedy pick (k_logits_process) on host-given logits [R][n_vocab], with
+  // full()'s rule constants for (max_initial_ts, suppress_blank)
+  void dbg_logits(const float* logits, int R, const LogitsCtl* ctl, float max_initial_ts, bool suppress_blank,
+                  TokenData* out, float* nosp);
 
   struct Impl;
 
@@ -279,6 +294,9 @@ class State {
   void kv_reorder(const std::vector<std::pair<int, int>>& moves, int n_rows);
   void run_logits(int R, const LogitsCtl* ctl, TokenData* out, float* nosp);
   void heuristic_timestamps(int i_segment, const FullParams& p);
+  void dtw_attach(StepBatcher::Req& q);
+  void dtw_after_step();
+  void flush_dtw();
   void dtw_timestamps(int i_segment, int n_segments, int seek, int n_frames, const std::string& language);
 };
 

@@ -346,6 +346,8 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
     // KV pool for the decode chains of every State of this context (multi-chain pipeline)
     const char* e = getenv("WDR_DECODE_CHAINS");
     max_chains = std::max(1, std::min(32, e ? atoi(e) : 16));
+    const char* nb = getenv("WDR_BATCHERS");
+    n_batchers = std::max(1, std::min(8, nb ? atoi(nb) : 1));
     fp8_encoder = getenv("WDR_FP8_ENCODER") && atoi(getenv("WDR_FP8_ENCODER")) != 0;
     const size_t per = (size_t)hp.n_text_layer * 21 * hp.n_text_ctx * hp.n_text_state;   // NSLOT = 21
     kv_k = DevMem(per * max_chains * 2);
@@ -356,7 +358,7 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
 }
 
 Context::~Context() {
-  batcher.reset();
+  batchers.clear();
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -438,6 +440,17 @@ struct State::Impl {
     hipEvent_t done = nullptr;
   };
   std::vector<DtwJob> jobs;        // enqueued by the current full() call
+  // multi-chain run: the last window's DTW re-forward waits to ride in the chain's next batcher
+  // request (the next segment's prompt prefill), one request instead of two per segment
+  struct PendingDtw {
+    bool on = false;
+    std::vector<int> toks;
+    const f16* xkv = nullptr;
+    int slot = -1;                 // slot whose release waits for the re-forward (-1: none)
+    int sot_len = 0, seek = 0, n_audio = 0;
+    int* blk = nullptr;
+    hipEvent_t done = nullptr;
+  } pend;
   std::vector<int*> blk_pool;
   std::vector<hipEvent_t> ev_pool;
   // host pinned
@@ -802,6 +815,7 @@ void State::plan(const int16_t* const* pcm, const int* n, int count, bool detect
 
 void State::unplan() {
   Impl& m = *m_;
+  flush_dtw();
   WDR_HIP(hipStreamSynchronize(m.es));
   m.plan.pcm.clear();
   m.plan.n.clear();
@@ -1133,7 +1147,7 @@ double State::dbg_batch_step(const int* toks, int n, int R, int iters) {
   WDR_CHECK(n >= 2 && n <= 448 && R >= 1 && R <= 16 && iters >= 1, "dbg_batch_step: bad shape");
   decoder_prefill(toks, n - 1, 0, false, false);
   WDR_HIP(hipStreamSynchronize(s_));
-  StepBatcher& b = ctx_.step_batcher();
+  StepBatcher& b = ctx_.step_batcher(chain);
   std::vector<StepBatcher::Req> rq(R);
   std::vector<StepBatcher::Req*> batch(R);
   for (int r = 0; r < R; ++r) {
@@ -1166,6 +1180,17 @@ void State::decode_logits(const int* toks, int n, float* logits_out) {
   decoder_prefill(toks, n, 0, true, false);
   WDR_HIP(wdr_memcpy_async(logits_out, m_->mb.logits.p, (size_t)m_->V * 4, hipMemcpyDeviceToHost, s_));
   WDR_HIP(hipStreamSynchronize(s_));
+}
+
+void State::dbg_logits(const float* logits, int R, const LogitsCtl* ctl, float max_initial_ts, bool suppress_blank,
+                       TokenData* out, float* nosp) {
+  Impl& m = *m_;
+  WDR_CHECK(R >= 1 && R <= NSEQ, "dbg_logits: 1..8 rows");
+  const float precision = 30.0f / ctx_.model.hp.n_audio_ctx;
+  m.vids.max_initial_tid = max_initial_ts > 0.0f ? (int)std::round(max_initial_ts / precision) : -1;
+  m.vids.suppress_blank = suppress_blank ? 1 : 0;
+  WDR_HIP(wdr_memcpy_async(m.mb.logits.p, logits, (size_t)R * m.V * 4, hipMemcpyHostToDevice, s_));
+  run_logits(R, ctl, out, nosp);
 }
 
 void State::dtw_capture(const int* toks, int n, float* cap_out) {
@@ -1334,29 +1359,21 @@ void State::dtw_timestamps(int i_segment, int n_segments, int seek, int n_frames
   m.jobs.push_back(job);
   Impl::DtwSet& D = m.dset;
   if (batched) {
-    // multi-chain run: the re-forward's rows ride in the batched step (capture into this
-    // state's DTW buffer, which the previous job's DTW kernels must have finished reading); the
-    // DTW kernels then follow on the DTW stream
-    WDR_HIP(hipEventSynchronize(m.ev_dtw));
+    // multi-chain run: the re-forward's rows ride in the chain's next batched request (its next
+    // prompt prefill, or a request of their own: flush_dtw); the DTW kernels follow on the DTW
+    // stream (dtw_after_step)
+    WDR_CHECK(!m.pend.on, "DTW re-forward already pending");
     WDR_HIP(hipStreamSynchronize(s_));   // the window's cross-K/V (on-demand encodes) in place
-    StepBatcher& b = ctx_.step_batcher();
-    StepBatcher::Req q;
-    q.n = 0;
-    q.dn = N;
-    q.dtok = toks.data();
-    q.dseq = chain * NSLOT + DTW_SEQ;
-    q.dxkv = m.xkv();
-    q.dcap = D.cap.as<float>();
-    q.dl_end = capture_l_end(ctx_);
-    q.vids = m.vids;
-    b.enter();
-    try {
-      b.step(q);
-    } catch (...) {
-      b.leave();
-      throw;
-    }
-    b.leave();
+    m.pend.on = true;
+    m.pend.toks = toks;
+    m.pend.xkv = m.xkv();
+    m.pend.slot = -1;
+    m.pend.sot_len = sot_len;
+    m.pend.seek = seek;
+    m.pend.n_audio = n_frames / 2;
+    m.pend.blk = job.blk;
+    m.pend.done = job.done;
+    return;
   } else {
     // the window's cross-K/V (encoded ahead, or on demand on the decode stream) must be in place
     WDR_HIP(hipEventRecord(m.ev_sync, s_));
@@ -1371,6 +1388,58 @@ void State::dtw_timestamps(int i_segment, int n_segments, int seek, int n_frames
   WDR_HIP(hipEventRecord(m.ev_dtw, m.sd));
 }
 
+// the pending DTW re-forward's rows into a batcher request (capture into this state's DTW
+// buffer, which the previous job's DTW kernels must have finished reading)
+void State::dtw_attach(StepBatcher::Req& q) {
+  Impl& m = *m_;
+  if (!m.pend.on) return;
+  WDR_HIP(hipEventSynchronize(m.ev_dtw));
+  q.dn = (int)m.pend.toks.size();
+  q.dtok = m.pend.toks.data();
+  q.dseq = chain * NSLOT + DTW_SEQ;
+  q.dxkv = m.pend.xkv;
+  q.dcap = m.dset.cap.as<float>();
+  q.dl_end = capture_l_end(ctx_);
+}
+
+// after the batched request that carried the pending re-forward: the DTW kernels on the DTW
+// stream, the times back to the job's pinned block, and the slot (if its release waited)
+void State::dtw_after_step() {
+  Impl& m = *m_;
+  if (!m.pend.on) return;
+  Impl::DtwSet& D = m.dset;
+  const int N = (int)m.pend.toks.size();
+  launch_dtw(D.cap.as<float>(), (int)ctx_.aheads.size(), N, 1500, m.pend.n_audio, m.pend.sot_len, m.pend.seek,
+             D.nrm.as<float>(), D.xdtw.as<float>(), D.times.as<int>(), D.times.as<int>() + RMAX + 4, m.sd);
+  WDR_HIP(wdr_memcpy_async(m.pend.blk + 3 * RMAX, D.times.p, (RMAX + 8) * 4, hipMemcpyDeviceToHost, m.sd));
+  WDR_HIP(hipEventRecord(m.pend.done, m.sd));
+  WDR_HIP(hipEventRecord(m.ev_dtw, m.sd));
+  if (m.pend.slot >= 0) WDR_HIP(hipEventRecord(m.slots[m.pend.slot].freed, m.sd));
+  m.pend.on = false;
+  m.pend.slot = -1;
+}
+
+// the pending re-forward as a batcher request of its own (before anything that overwrites its
+// slot, and before its result is read)
+void State::flush_dtw() {
+  Impl& m = *m_;
+  if (!m.pend.on) return;
+  StepBatcher& b = ctx_.step_batcher(chain);
+  StepBatcher::Req q;
+  q.n = 0;
+  q.vids = m.vids;
+  dtw_attach(q);
+  b.enter();
+  try {
+    b.step(q);
+  } catch (...) {
+    b.leave();
+    throw;
+  }
+  b.leave();
+  dtw_after_step();
+}
+
 std::vector<DtwTicket> State::take_dtw_jobs() {
   Impl& m = *m_;
   std::vector<DtwTicket> out;
@@ -1382,6 +1451,7 @@ std::vector<DtwTicket> State::take_dtw_jobs() {
 void State::resolve_dtw(DtwTicket& t, std::vector<ResultSeg>& segs) {
   Impl& m = *m_;
   const Vocab& v = ctx_.vocab;
+  if (m.pend.on && m.pend.done == (hipEvent_t)t.event) flush_dtw();
   WDR_HIP(hipEventSynchronize((hipEvent_t)t.event));
   const int* times = t.blk + 3 * RMAX;
   const int nt = times[RMAX + 4];
@@ -1501,7 +1571,7 @@ Seq State::decode_beam(const std::vector<int>& prompt, const FullParams& params,
       }
       if (batched) {
         if (!seat.b) {
-          seat.b = &ctx_.step_batcher();
+          seat.b = &ctx_.step_batcher(chain);
           seat.b->enter();
         }
         StepBatcher::Req q;
@@ -1848,6 +1918,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
   auto encode = [&](int seek) {
     if (encoded_seek != seek) {
       const double t = now_s();
+      flush_dtw();   // a pending re-forward reads the slot this encode overwrites
       WDR_HIP(hipStreamWaitEvent(s_, m.ev_dtw, 0));   // a DTW job may still read this slot
       encode_window(seek);
       WDR_HIP(hipStreamSynchronize(s_));
@@ -1922,6 +1993,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
       // logits give the first token), so the chain never leaves the batch
       const bool pre_batched = batched && single;
       if (!pre_batched) {
+        flush_dtw();
         WDR_HIP(hipEventRecord(m.ev_p0, s_));
         decoder_prefill(prompt.data(), (int)prompt.size(), 0, true, false);
         WDR_HIP(hipEventRecord(m.ev_p1, s_));
@@ -1963,7 +2035,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
         float ns = 0.f;
         if (i == 0 && pre_batched) {
           if (!lockstep.b) {
-            lockstep.b = &ctx_.step_batcher();
+            lockstep.b = &ctx_.step_batcher(chain);
             lockstep.b->enter();
           }
           StepBatcher::Req rq;
@@ -1974,7 +2046,9 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
           rq.pxkv = m.xkv();
           rq.pctl = c;
           rq.vids = m.vids;
+          dtw_attach(rq);   // the previous window's re-forward rides along
           lockstep.b->step(rq);
+          dtw_after_step();
           tok = rq.pout;
           nosp = rq.pnosp;
           times.prefills++;
@@ -1987,7 +2061,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
           const int prev_id = sq.tokens.back().id;
           if (batched) {
             if (!lockstep.b) {
-              lockstep.b = &ctx_.step_batcher();
+              lockstep.b = &ctx_.step_batcher(chain);
               lockstep.b->enter();
             }
             StepBatcher::Req rq = row_req(prev_id, chain * NSLOT + seq0, pos, m.xkv(), c, m.vids);
@@ -2082,6 +2156,14 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
       seek_delta = std::min(seek_end - seek, 3000);
     seek += seek_delta;
   }
+  if (m.pend.on && planned && async_dtw) {
+    // the last window's re-forward rides in the next segment's first request: this slot is
+    // released once it has run (dtw_after_step), not here
+    m.pend.slot = m.cur;
+    release.on = false;
+  } else {
+    flush_dtw();
+  }
   if (!async_dtw) {
     std::vector<DtwTicket> tk = take_dtw_jobs();
     for (auto& t : tk) resolve_dtw(t, result_all);
@@ -2156,11 +2238,31 @@ StepBatcher::~StepBatcher() {
   (void)hipHostFree(m_->h_beam);
 }
 
-StepBatcher& Context::step_batcher() {
+StepBatcher& Context::step_batcher(int chain) {
   static std::mutex mu;
   std::lock_guard<std::mutex> g(mu);
-  if (!batcher) batcher = std::make_unique<StepBatcher>(*this);
-  return *batcher;
+  if (batchers.empty()) batchers.resize(std::max(1, n_batchers));
+  auto& b = batchers[(size_t)std::max(0, chain) % batchers.size()];
+  if (!b) b = std::make_unique<StepBatcher>(*this);
+  return *b;
+}
+
+Context::BatchStats Context::batcher_stats() {
+  BatchStats o;
+  for (int i = 0; i < std::max(1, n_batchers); ++i) {
+    StepBatcher& sb = step_batcher(i);
+    o.launches += sb.launches;
+    o.rows += sb.rows;
+    o.prefill_rows += sb.prefill_rows;
+    o.dtw_rows += sb.dtw_rows;
+    o.prefills += sb.prefills;
+    o.dtws += sb.dtws;
+    o.mixed += sb.mixed;
+    o.vgroups += sb.vgroups;
+    o.tiles += sb.tiles;
+    o.step_s = std::max(o.step_s, sb.step_s);
+  }
+  return o;
 }
 
 void StepBatcher::enter() {
@@ -2245,6 +2347,7 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
       g.l_end = q->dl_end;
       tb.add(g);
       n_dtw += q->dn;
+      dtws++;
     }
     if (q->n > 0) {
       RowGroupDesc g;
@@ -2268,6 +2371,7 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
       lpre[i] = tb.add(g);
       m.h_ctl[lpre[i]] = q->pctl;
       n_pre += q->pn;
+      prefills++;
     }
   }
   const int R = tb.R, NL = tb.n_logit;
@@ -2359,6 +2463,8 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
   }
   launches++;
   rows += R;
+  vgroups += tb.n_vgrp;
+  tiles += tb.n_tiles;
   prefill_rows += n_pre;
   dtw_rows += n_dtw;
   if (!decode_only) mixed++;

@@ -720,6 +720,25 @@ class WhisperContext:
                                        out.ctypes.data_as(C.POINTER(C.c_float))))
         return out
 
+    def logit_rules(self, logits, ctls, temps=None, max_initial_ts: float = 1.0, suppress_blank: bool = True):
+        """whisper.cpp's logit rules + greedy pick on the GPU (wdr_dbg_logits): logits [R][n_vocab],
+        ctls = R dicts of n_tokens / last_ts / pen_ts / has_ts / seek_delta / force_kind / force_tok.
+        Returns R dicts: id, tid, p, plog, pt, ptsum, nosp."""
+        lg = np.ascontiguousarray(logits, np.float32)
+        R = lg.shape[0]
+        keys = ("n_tokens", "last_ts", "pen_ts", "has_ts", "seek_delta", "force_kind", "force_tok")
+        ctl = np.ascontiguousarray([[int(c.get(k, 0)) for k in keys] for c in ctls], np.int32)
+        tt = np.ascontiguousarray(temps if temps is not None else [0.0] * R, np.float32)
+        ids = np.zeros((R, 2), np.int32)
+        f = np.zeros((R, 5), np.float32)
+        L.check(self._lib.wdr_dbg_logits(self.h, lg.ctypes.data_as(C.POINTER(C.c_float)), R,
+                                         ctl.ctypes.data_as(C.POINTER(C.c_int32)),
+                                         tt.ctypes.data_as(C.POINTER(C.c_float)), float(max_initial_ts),
+                                         1 if suppress_blank else 0, ids.ctypes.data_as(C.POINTER(C.c_int32)),
+                                         f.ctypes.data_as(C.POINTER(C.c_float))))
+        return [dict(id=int(ids[r, 0]), tid=int(ids[r, 1]), p=float(f[r, 0]), plog=float(f[r, 1]), pt=float(f[r, 2]),
+                     ptsum=float(f[r, 3]), nosp=float(f[r, 4])) for r in range(R)]
+
     def batch_step_ms(self, tokens, rows: int, iters: int = 50) -> float:
         """Host ms per multi-chain batched step of `rows` rows on the last encoded window
         (wdr_dbg_batch_step probe seam)."""

@@ -86,7 +86,9 @@ class StageTimes(C.Structure):
                 ("windows", i64), ("decode_steps", i64), ("prefills", i64), ("lang", f64), ("prompt_gpu", f64),
                 ("embed", f64), ("chains", i64), ("batch_launches", i64), ("batch_rows", i64),
                 ("fixup_segments", i64), ("replay_segments", i64), ("spec_s", f64), ("fixup_s", f64),
-                ("batch_step_s", f64), ("early_fixup_segments", i64)]
+                ("batch_step_s", f64), ("early_fixup_segments", i64), ("batch_prefill_rows", i64),
+                ("batch_dtw_rows", i64), ("batch_prefills", i64), ("batch_dtws", i64), ("batch_mixed", i64),
+                ("batch_xattn_groups", i64), ("batch_xattn_tiles", i64)]
 
 
 class Token(C.Structure):
@@ -163,6 +165,7 @@ _SIGS = {
     "wdr_dbg_decode": (C.c_int, [vp, P(i32), sz, P(f32)]),
     "wdr_dbg_cross_kv": (C.c_int, [vp, P(f32)]),
     "wdr_dbg_step": (C.c_int, [vp, P(i32), sz, P(f32)]),
+    "wdr_dbg_logits": (C.c_int, [vp, P(f32), i32, P(i32), P(f32), f32, i32, P(i32), P(f32)]),
     "wdr_dbg_capture": (C.c_int, [vp, P(i32), sz, P(f32)]),
     "wdr_dbg_dtw": (C.c_int, [P(f32), i32, i32, i32, i32, i32, P(f32), P(i32), P(i32)]),
     "wdr_dbg_discrete": (C.c_int, [P(f32), sz, C.c_uint32, i32, P(i32)]),
