@@ -192,15 +192,16 @@ def test_state_full_greedy_dtw_one_window(model, speech):
 
 def test_state_full_beam5_dtw_one_window(model, speech):
     """whisper_full with the reference's DEFAULT strategy -- beam search, 5 beams, patience -1
-    (src/transcribe.rs:22-33) -- on a ~8-s segment, lang auto, heuristic timestamps and DTW:
+    (src/transcribe.rs:22-33) -- on the ~20-s segment of the greedy test, lang auto, heuristic
+    timestamps and DTW:
     the beams' candidates (top-K per beam, ordered by cumulative log-prob, duplicates dropped,
     KV caches following their parents) and the final ranking, token by token against the
     oracle's WhisperState.decode_beam.  At large-v3 this runs the beam-group cross-attention
     and the rows kernel at the full width."""
     name, ctx, hp, W, m = model
     pcm, spurts = speech
-    a = spurts[1][0]
-    x = pcm_i16_to_f32(pcm[int(a * 16000):int((a + 8.0) * 16000)])
+    a = spurts[0][0]
+    x = pcm_i16_to_f32(pcm[int(a * 16000):int((a + 20.0) * 16000)])
     opts = wdr.TranscribeOptions(lang="auto")          # advanced None: beam search, 5 beams
     got, lang_id = ctx.state_full(x, opts)
     st = WhisperState(m, Vocab(hp.n_vocab), name)

@@ -11,8 +11,12 @@ oracle can follow, by properties where it cannot (VERDICT r2 "next round" item 1
     + pyannote diarization + speaker assignment (the bench workload) -- the oracle cannot follow
     an hour of large-v3 in a test, so its output is held to the properties the reference's glue
     guarantees: one segment list in time order after the overlap clip (src/transcribe.rs:447-459),
-    word times inside their segment, speaker ids "1".."k" or "?" (src/transcribe.rs:478-497), no
-    control token or embedded marker left in any text (src/transcribe.rs:206-240).
+    segment bounds = its first word's start and last word's end (:439-440, the clip moving both),
+    every word inside its 30-s window, speaker ids "1".."k" or "?" (src/transcribe.rs:478-497),
+    no control token or embedded marker left in any text (src/transcribe.rs:206-240).  A word may
+    end before it starts: its start is the heuristic t0 while its end is a DTW-anchor midpoint
+    (:291-306) -- the reference's own output shows such words (tests/golden/reference_segments.json);
+    they are counted, not rejected.
 
 Synthetic weights on both sides (seeded, bit-identical), decode length pinned.
 Tolerances as tests/test_gpu_baseline_models.py: segment text equal; words within 20 ms
@@ -53,7 +57,7 @@ def _vad_pipeline_vs_oracle(tmp_path, model, seconds, seed, greedy):
     mask, vsegs = oracle_vad(pcm)
     gmask, gsegs = wdr.Vad().get_segments(pcm)
     assert [(round(a, 6), round(b, 6)) for a, b in gmask] == [(round(a, 6), round(b, 6)) for a, b in mask]
-    assert [(s.start, s.end) for s in gsegs] == [(s.start, s.end) for s in vsegs] and len(vsegs) >= 2
+    assert [(s.start, s.end) for s in gsegs] == [(s.start, s.end) for s in vsegs] and len(vsegs) >= 1
     hp = hparams_for(model)
     st = WhisperState(Whisper(hp, synth_weights(hp, std=0.02, emb_std=EMB_STD)), Vocab(hp.n_vocab), model)
     o = dict(lang="auto", synthetic=dict(force_len_rate=3.3, logprob_thold=-np.inf, entropy_thold=-1.0))
@@ -105,19 +109,22 @@ def test_c4_shard_one_hour_large_v3_diarize_properties():
     # one whisper segment per talk spurt (one window each, single_segment, pinned decode)
     assert len(out) == len(spurts) == 635, (len(out), len(spurts))
     speakers = set()
+    inverted = 0
     for i, s in enumerate(out):
         a, b, _ = spurts[i]
-        assert a - 1e-6 <= s.start <= s.end, (i, s.start, s.end)
-        assert s.end <= b + 30.0, (i, s.end, b)
         if i + 1 < len(out):
             assert s.end <= out[i + 1].start + 1e-9, (i, s.end, out[i + 1].start)   # overlap clip
+            assert s.start <= out[i + 1].start, i
         assert s.text and not _MARKER.search(s.text), (i, s.text)
         assert s.words, i
+        assert s.start == s.words[0].start and s.end == s.words[-1].end, (i, s.start, s.end)
         for w in s.words:
-            assert s.start - 1e-9 <= w.start <= w.end <= s.end + 1e-9, (i, w, s.start, s.end)
+            assert a - 1e-6 <= w.start <= a + 30.0 + 1e-6 and a - 1e-6 <= w.end <= a + 30.0 + 1e-6, (i, w, a)
             assert w.text and not _MARKER.search(w.text), (i, w.text)
+            inverted += w.end < w.start
         assert s.speaker_id is not None
         speakers.add(s.speaker_id)
     ids = sorted(x for x in speakers if x != "?")
     assert ids and ids == [str(k) for k in range(1, len(ids) + 1)], speakers
-    print(dict(test="c4_shard", segments=len(out), speakers=sorted(speakers), words=sum(len(s.words) for s in out)))
+    print(dict(test="c4_shard", segments=len(out), speakers=sorted(speakers), words=sum(len(s.words) for s in out),
+               inverted_words=inverted))

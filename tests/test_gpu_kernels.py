@@ -212,6 +212,12 @@ def test_decode_cross_attention(lib):
     np.testing.assert_allclose(grouped, gref, rtol=0, atol=1e-2)
     single = _xattn(lib, q, kv, H, gslot)   # same rows, every row its own group
     np.testing.assert_array_equal(grouped, single)
+    np.testing.assert_array_equal(_xattn(lib, q, kv, H, gslot, grp, iters=3), grouped)
+    # shared K/V (one segment's beams on a State's own step), R <= 8
+    shared = _xattn(lib, q[:5], kv[:1], H)
+    np.testing.assert_array_equal(shared, _xattn(lib, q[:5], kv[:1], H, np.zeros(5), [5, 0, 0, 0, 0]))
+    np.testing.assert_allclose(shared, _attn_ref(q[:5], kv[0, :, :H * 64], kv[0, :, H * 64:], H, 0), rtol=0,
+                               atol=1e-2)
 
 
 def test_decode_cross_attention_mma_tiles(lib):
@@ -241,12 +247,6 @@ def test_decode_cross_attention_mma_tiles(lib):
     split = grp.copy()
     split[0], split[12] = 12, 28
     np.testing.assert_array_equal(_xattn(lib, q, kv, H, slot, split), got)
-    np.testing.assert_array_equal(_xattn(lib, q, kv, H, gslot, grp, iters=3), grouped)
-    # shared K/V (one segment's beams on a State's own step), R <= 8
-    shared = _xattn(lib, q[:5], kv[:1], H)
-    np.testing.assert_array_equal(shared, _xattn(lib, q[:5], kv[:1], H, np.zeros(5), [5, 0, 0, 0, 0]))
-    np.testing.assert_allclose(shared, _attn_ref(q[:5], kv[0, :, :H * 64], kv[0, :, H * 64:], H, 0), rtol=0,
-                               atol=1e-2)
 
 
 @pytest.mark.parametrize("N,K,epi", [(1280, 5120, 2), (3840, 1280, 0)])
