@@ -161,10 +161,12 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s) {
   const float scale = 1.0f / 8.0f;
   WDR_CHECK(R >= 1 && io.tok && io.xkv, "rows forward: no rows / tables");
   launch_embed(md.tok_emb, md.dec_pos, io.tok, io.pos, R, d, io.xd, s);
-  // the projection's input rows LayerNorm(x): inside the row kernel (each workgroup normalises
-  // its own row tiles; WDR_ROWS_LN_SPLIT=1: one k_layernorm launch into io.hd above 32 rows --
-  // the same arithmetic either way)
-  static const bool ln_split = getenv("WDR_ROWS_LN_SPLIT") && atoi(getenv("WDR_ROWS_LN_SPLIT")) != 0;
+  // the projection's input rows LayerNorm(x): inside the row kernel up to 32 rows (every
+  // workgroup normalises its own row tiles), above that one k_layernorm launch into io.hd -- the
+  // same arithmetic either way.  Fused at every row count the redundant per-column-tile LN cost
+  // more than the launch it saves (1-h trace: decoder rows class 4.98 vs 4.83 s over two runs);
+  // WDR_ROWS_LN_SPLIT=0 fuses at every count (A/B)
+  static const bool ln_split = !(getenv("WDR_ROWS_LN_SPLIT") && atoi(getenv("WDR_ROWS_LN_SPLIT")) == 0);
   const bool fuse_ln = R <= 32 || !ln_split;
   auto P = [&](const f16* A, int lda, const f16* W, const float* b, void* out, int ldo, int N, int K, int epi,
                const float* lng = nullptr, const float* lnb = nullptr) {

@@ -345,7 +345,7 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
   {
     // KV pool for the decode chains of every State of this context (multi-chain pipeline)
     const char* e = getenv("WDR_DECODE_CHAINS");
-    max_chains = std::max(1, std::min(32, e ? atoi(e) : 16));
+    max_chains = std::max(1, std::min(64, e ? atoi(e) : 16));
     const char* nb = getenv("WDR_BATCHERS");
     n_batchers = std::max(1, std::min(8, nb ? atoi(nb) : 1));
     fp8_encoder = getenv("WDR_FP8_ENCODER") && atoi(getenv("WDR_FP8_ENCODER")) != 0;
@@ -2176,10 +2176,11 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
 // ------------------------------------------------------------------ multi-chain step batcher
 namespace wdr {
 
-// rows of one batched launch: decode rows, prompt prefills and DTW re-forwards of up to 32
-// chains (a prefill <= 228 rows, a DTW re-forward <= 229)
-static constexpr int RB = 16384;
-static constexpr int LB = 320;    // logit rows (32 chains x (8 beams + a prefill's last row))
+// rows of one batched launch: decode rows, prompt prefills and DTW re-forwards of every chain
+// of the context (a prefill <= 228 rows, a DTW re-forward <= 229; 16384 rows cover 32 chains'
+// typical mixes, above that 470 per chain), logit rows: 8 beams + a prefill's last row per chain
+static int rows_cap(const Context& c) { return std::max(16384, c.max_chains * 470); }
+static int logit_cap(const Context& c) { return std::max(320, c.max_chains * 10); }
 
 struct StepBatcher::Impl {
   std::mutex mu;
@@ -2191,6 +2192,7 @@ struct StepBatcher::Impl {
   std::exception_ptr err;         // failure of the last launch (rethrown to its requesters)
   hipStream_t s = nullptr;
   int d = 0, V = 0, H = 0;
+  int RB = 0, LB = 0;             // row / logit-row capacity of one launch
   RowsBufs bufs;
   std::unique_ptr<RowBatch> tb;
   DevMem work, tokout, ctl, beamc;
@@ -2214,6 +2216,9 @@ StepBatcher::StepBatcher(Context& ctx) : ctx_(ctx), m_(new Impl) {
   int lo = 0, hi = 0;
   WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
   WDR_HIP(hipStreamCreateWithPriority(&m.s, hipStreamNonBlocking, hi));
+  const int RB = rows_cap(ctx), LB = logit_cap(ctx);
+  m.RB = RB;
+  m.LB = LB;
   m.bufs.alloc(RB, LB, m.d, m.H, m.V);
   m.tb = std::make_unique<RowBatch>(RB, LB, RB);
   m.work = DevMem((size_t)LB * m.V * 4);
