@@ -52,7 +52,7 @@ std::vector<float> plus_one(std::vector<float> v) {
 
 // ================================================================== segmentation-3.0
 static constexpr int kWin = 160000, kFrames = 589, kFrameStart = 721, kFrameSize = 270;
-static constexpr int kSegBatch = 16;   // windows per forward
+static constexpr int kSegBatch = 128;  // windows per forward: the BiLSTM scans run one workgroup per (window, direction), so 128 windows fill the GPU (16 left 224 of 256 CUs idle for the whole scan)
 static constexpr float kClass0Offset = 0.86f;   // oracle/diarize.py SEG_CLASS0_OFFSET
 
 struct SegModel::W {

@@ -93,9 +93,102 @@ __global__ __launch_bounds__(256) void k_gemm32(Gemm32Args a) {
   }
 }
 
+// ---------------------------------------------------------------- f32 MFMA GEMM
+// The same contraction on the matrix cores: v_mfma_f32_32x32x2_f32 (exact f32 products, one
+// fma per k in k order -- the arithmetic of k_gemm32's per-thread fma chain), 4 waves of 32 x 32
+// output tiles arranged WM x WN (64 x 64, or 128 x 32 for narrow N), BK 16 k-major LDS tiles
+// with the next tile's loads in flight (registers) during the current tile's MFMAs.
+template <int WM, int WN>
+__global__ __launch_bounds__(256) void k_gemm32m(Gemm32Args a) {
+  constexpr int BM = 32 * WM, BN = 32 * WN, BK = 16;
+  constexpr int LA = BM * BK / 256, LB = BN * BK / 256;   // elements staged per thread
+  __shared__ float As[BK][BM + 4];
+  __shared__ float Bs[BK][BN + 4];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid / WN, wc = wid % WN;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  float ra[LA], rb[LB];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int r = 0; r < LA; ++r) {
+      const int e = tid + r * 256, row = e >> 4, kk = e & 15, gk = k0 + kk;
+      float va = 0.f;
+      if (m0 + row < a.M && gk < a.K) {
+        va = a.A[(long long)(m0 + row) * a.lda + gk];
+        if (a.pro_scale) va = fmaxf(va * a.pro_scale[gk] + a.pro_shift[gk], 0.f);
+      }
+      ra[r] = va;
+    }
+#pragma unroll
+    for (int r = 0; r < LB; ++r) {
+      const int e = tid + r * 256, row = e >> 4, kk = e & 15, gk = k0 + kk;
+      rb[r] = (n0 + row < a.N && gk < a.K) ? a.B[(long long)(n0 + row) * a.ldb + gk] : 0.f;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int r = 0; r < LA; ++r) {
+      const int e = tid + r * 256;
+      As[e & 15][e >> 4] = ra[r];
+    }
+#pragma unroll
+    for (int r = 0; r < LB; ++r) {
+      const int e = tid + r * 256;
+      Bs[e & 15][e >> 4] = rb[r];
+    }
+  };
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  load(0);
+  const int fi = lane & 31, fk = lane >> 5;
+  for (int k0 = 0; k0 < a.K; k0 += BK) {
+    store();
+    __syncthreads();
+    if (k0 + BK < a.K) load(k0 + BK);   // next tile's loads overlap this tile's MFMAs
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[kk + fk][wr * 32 + fi], Bs[kk + fk][wc * 32 + fi], acc, 0, 0, 0);
+    __syncthreads();
+  }
+  const int n = n0 + wc * 32 + fi;
+  if (n >= a.N) return;
+  const float bias = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * fk;
+    if (m >= a.M) continue;
+    float v = acc[r];
+    if (a.bias) v += bias;
+    if (a.scale) v = v * a.scale[n] + a.shift[n];
+    float* c = a.C + (long long)m * a.ldc + n;
+    if (a.accum) v += *c;
+    *c = act_apply(v, a.act);
+  }
+}
+
+// WDR_GEMM32=0: the VALU kernel (A/B; read per call: tests/test_gpu_diarize.py compares both)
+static bool gemm32_mfma() {
+  const char* e = getenv("WDR_GEMM32");
+  return !(e && atoi(e) == 0);
+}
+
 void launch_gemm32(const Gemm32Args& a, hipStream_t s) {
   if (a.M <= 0 || a.N <= 0) return;
-  WDR_KLAUNCH(k_gemm32, dim3(cdiv(a.N, G_BN), cdiv(a.M, G_BM)), dim3(256), 0, s, a);
+  if (gemm32_mfma()) {
+    // 128 x 32 tiles where they waste fewer columns than 64 x 64 (N = 7, 32, 80), else 64 x 64
+    const int w64 = cdiv(a.N, 64) * 64 - a.N, w32 = cdiv(a.N, 32) * 32 - a.N;
+    if (w32 < w64 || a.N <= 32) {
+      WDR_CHECK(cdiv(a.M, 128) <= 65535, "gemm32: too many row tiles");
+      WDR_KLAUNCH((k_gemm32m<4, 1>), dim3(cdiv(a.N, 32), cdiv(a.M, 128)), dim3(256), 0, s, a);
+    } else {
+      WDR_CHECK(cdiv(a.M, 64) <= 65535, "gemm32: too many row tiles");
+      WDR_KLAUNCH((k_gemm32m<2, 2>), dim3(cdiv(a.N, 64), cdiv(a.M, 64)), dim3(256), 0, s, a);
+    }
+  } else {
+    WDR_CHECK(cdiv(a.M, G_BM) <= 65535, "gemm32: too many row tiles");
+    WDR_KLAUNCH(k_gemm32, dim3(cdiv(a.N, G_BN), cdiv(a.M, G_BM)), dim3(256), 0, s, a);
+  }
   WDR_HIP(hipGetLastError());
 }
 

@@ -500,7 +500,16 @@ const Context::Fp8W& Context::fp8_xkv() {
 }
 
 static constexpr int kBatch = 4;     // encoder windows per encode-ahead launch (M = 6000 rows)
-static constexpr int kSlots = 16;    // in-flight segments in the cross-K/V ring
+static constexpr int kSlots = 16;    // in-flight segments in the cross-K/V ring (most)
+// WDR_SLOTS: ring slots per chain (a multiple of kBatch, 4..16; default 16)
+static int ring_slots() {
+  static const int v = [] {
+    const char* e = getenv("WDR_SLOTS");
+    const int n = e ? atoi(e) / kBatch * kBatch : kSlots;
+    return std::max(kBatch, std::min(kSlots, n));
+  }();
+  return v;
+}
 
 static void alloc_enc(State::Impl::EncBufs& e, int nb, int d, int kp1) {
   e.nb = nb;
@@ -537,7 +546,7 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
   const int d = m.d;
   alloc_enc(m.e1, 1, d, m.kp1);
   alloc_enc(m.eb, kBatch, d, m.kp1);
-  m.S = kSlots;
+  m.S = ring_slots();
   m.slots.resize(m.S + 1);
   for (auto& sl : m.slots) {
     sl.gmax = DevMem(16);
