@@ -60,6 +60,10 @@ def parse():
     ap.add_argument("--strategy", default="greedy", choices=["greedy", "beam"],
                     help="greedy (configs[2]) or the reference's default beam search, 5 beams")
     ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3) encoder GEMMs (configs[4])")
+    ap.add_argument("--multi", default="ranks", choices=["ranks", "inproc"],
+                    help="N > 1: one process per GPU over RCCL (wdr/distributed.py, default) or ONE process "
+                         "driving N GPUs through libwdr's gpu_device=None context (the C-ABI path a Rust host "
+                         "gets, src/engine.rs:14; under torch.distributed.run only rank 0 works)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-audio", type=float, default=60.0,
                     help="audio seconds of the workload the CPU baseline is extrapolated over (rank 0, N=1)")
@@ -241,8 +245,118 @@ def cpu_baseline(model, segs, audio_target):
     return out, sample, threads_max
 
 
+def main_inproc(args):
+    """--multi inproc: ONE process, N GPUs, libwdr's own multi-GPU path (gpu_device = None,
+    WDR_DEVICES = 0..N-1 unless set; decode chains spread over the GPUs, chain k on GPU k % N,
+    the exact prompt fix-up across them: csrc/engine.cpp).  One file of N x --seconds of audio
+    (seeds 0..N-1 concatenated: weak scaling, ~--seconds per GPU).  The pyannote windows are split
+    in N contiguous shards, one Diarizer per GPU in its own thread, and stitched in file order
+    (Diarizer.segments_from_classes); the segments handed downstream are the generator's
+    ground-truth spurts (synthetic pin, as the one-GPU line).  Under torch.distributed.run the
+    ranks > 0 only join the barriers (gloo: they never touch a GPU)."""
+    import threading
+    import numpy as np
+    import wdr
+    from wdr.synth import synth_speech
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    N = max(1, args.gpus)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group(backend="gloo")
+        if rank != 0:
+            dist.barrier()   # rank 0's run
+            dist.destroy_process_group()
+            return
+    os.environ.setdefault("WDR_DEVICES", ",".join(str(g) for g in range(N)))
+    devs = [int(x) for x in os.environ["WDR_DEVICES"].split(",")]
+    diarize = args.seg == "diarize"
+    syn = wdr.Synthetic(weight_std=0.02, emb_std=0.02, force_len_rate=3.3, disable_fallback=True)
+    t_load = time.perf_counter()
+    ctx = wdr.WhisperContext(args.model, gpu_device=None, enable_dtw=True, synthetic=syn)
+    if args.fp8:
+        ctx.set_encoder_fp8(True)
+    t_load = time.perf_counter() - t_load
+    parts = [synth_speech(args.seconds, seed=r, n_speakers=3 if diarize else 1) for r in range(N)]
+    pcm = np.concatenate([p for p, _ in parts])
+    spurts = [(a + r * args.seconds, b + r * args.seconds) for r, (_, sp) in enumerate(parts) for a, b, _ in sp]
+    del parts
+    segs = [wdr.SpeechSegment(a, b, pcm[int(round(a * 16000)):int(round(b * 16000))]) for a, b in spurts]
+    opts = wdr.TranscribeOptions(model=args.model, lang="auto", enable_vad=not diarize,
+                                 enable_diarize=True if diarize else None,
+                                 advanced=wdr.AdvancedTranscribe(
+                                     sampling_strategy="greedy" if args.strategy == "greedy" else None))
+    dopts = wdr.DiarizeOptions.from_options(opts) if diarize else None
+    dzs = [wdr.Diarizer(gpu_device=g) for g in devs] if diarize else []
+    vad = None if diarize else wdr.Vad(gpu_device=devs[0])
+    WIN, FR = 160000, 589
+    seg_t = [0.0]
+
+    def segment():
+        t = time.perf_counter()
+        if diarize:
+            W = pcm.size // WIN + 1
+            cuts = [round(W * i / len(dzs)) for i in range(len(dzs) + 1)]
+            out = [None] * len(dzs)
+
+            def run(i):
+                a, b = cuts[i], cuts[i + 1]
+                out[i] = dzs[i].frame_classes(pcm[a * WIN:min(pcm.size, b * WIN)])[:b - a] if b > a else \
+                    np.zeros((0, FR), np.int32)
+            th = [threading.Thread(target=run, args=(i,)) for i in range(len(dzs))]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            n = len(wdr.Diarizer.segments_from_classes(np.concatenate(out, 0), pcm))
+        else:
+            n = len(vad.get_segments(pcm, materialize=False)[1])
+        seg_t[0] += time.perf_counter() - t
+        return n
+
+    def step():
+        segment()
+        return ctx.run_pipeline(segs, opts, diarize_options=dopts)
+    for _ in range(args.warmup):
+        step()
+    seg_t[0] = 0.0
+    t0 = time.perf_counter()
+    n_out = 0
+    for _ in range(args.steps):
+        out, _ = step()
+        n_out += len(out)
+    dt = time.perf_counter() - t0
+    times = ctx.stage_times()
+    shard_s = pcm.size / 16000.0
+    line = {
+        "metric": "audio-sec/wall-sec (xRT), large-v3 + DTW + diarize, 1/2/4/8 MI355X",
+        "value": round(shard_s * args.steps / dt, 3), "unit": "audio-sec/wall-sec", "n_gpus": N, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 1), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f16 (f32 accumulate)", "data": "synthetic",
+        "config": {"strategy": "greedy" if args.strategy == "greedy" else "beam search, 5 beams (reference default)",
+                   "workload": "one file of %d x %.0f s synthetic audio (%d segments, 3 speakers), %s + DTW + %s, "
+                               "lang auto, ground-truth spurt segments downstream (synthetic pin)"
+                               % (N, args.seconds, len(segs), args.model, "diarize" if diarize else "Silero VAD"),
+                   "model": args.model, "global_batch": len(segs), "seq_len": 1500,
+                   "parallelism": "ONE process, libwdr gpu_device=None over devices %s (decode chains spread, "
+                                  "exact prompt fix-up across GPUs); pyannote windows sharded per GPU" % devs},
+        "roofline": None, "cpu_baseline": None,
+        "stages_s": {k: round(v, 3) for k, v in times.items() if isinstance(v, float)},
+        "counts": {k: v for k, v in times.items() if isinstance(v, int)},
+        "segmentation": {"s_per_step": round(seg_t[0] / args.steps, 4)},
+        "devices": ctx.devices, "load_s": round(t_load, 2), "segments_out": n_out // max(1, args.steps),
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.multi == "inproc":
+        return main_inproc(args)
     import numpy as np
     import torch
     import torch.distributed as dist

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define WDR_ABI_VERSION 3
+#define WDR_ABI_VERSION 4
 
 typedef struct wdr_engine wdr_engine;
 typedef struct wdr_context wdr_context;   /* ~ whisper_rs::WhisperContext (+ its state) */
@@ -164,6 +164,9 @@ typedef struct {
    * reads: one-row / beam groups (VALU kernel) and MFMA row tiles, each one slot per layer */
   int64_t batch_prefill_rows, batch_dtw_rows, batch_prefills, batch_dtws, batch_mixed;
   int64_t batch_xattn_groups, batch_xattn_tiles;
+  /* ABI 4: the DTW queue (multi-chain runs: every chain's DTW re-forwards batched off the decode
+   * chain) -- passes launched, the rows they carried, windows queued */
+  int64_t dtwq_passes, dtwq_rows, dtwq_jobs;
 } wdr_stage_times;
 
 const char* wdr_last_error(void);

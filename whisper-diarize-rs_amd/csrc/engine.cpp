@@ -235,6 +235,7 @@ struct wdr_context {
   struct ChainStats {
     long long chains = 1, launches = 0, rows = 0, fixups = 0, replays = 0, early = 0;
     long long prefill_rows = 0, dtw_rows = 0, prefills = 0, dtws = 0, mixed = 0, vgroups = 0, tiles = 0;
+    long long dq_passes = 0, dq_rows = 0, dq_jobs = 0;   // DTW queue
     double spec_s = 0, fixup_s = 0, step_s = 0;
   } cs;                                           // the last run_pipeline's multi-chain figures
   std::unique_ptr<CamModel> cam;   // EmbeddingExtractor, created on the first diarized run
@@ -521,7 +522,7 @@ static std::unique_ptr<wdr_context> make_context(const std::string& model_name, 
       pc.gpu_device = c->devices[g];
       c->peers.push_back(std::make_unique<Context>(model_name, hp, pc, gf.get()));
     }
-    c->chains = c->ctx->max_chains;   // WDR_DECODE_CHAINS (default 16), wdr_context_set_chains
+    c->chains = c->ctx->max_chains;   // WDR_DECODE_CHAINS (default 24), wdr_context_set_chains
   } catch (const std::exception& ex) {
     throw std::runtime_error(std::string("create whisper context crash: ") + ex.what());
   }
@@ -733,6 +734,9 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
       o.vgroups += b.vgroups;
       o.tiles += b.tiles;
       o.step_s = std::max(o.step_s, b.step_s);
+      o.dq_passes += b.dq_passes;
+      o.dq_rows += b.dq_rows;
+      o.dq_jobs += b.dq_jobs;
     }
     return o;
   };
@@ -799,7 +803,24 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
         }
       } guard{st};
       Prompt e = e0;
-      std::vector<DtwTicket> prev_tk;
+      // the block's DTW tickets, resolved after its last segment: the re-forwards run batched
+      // with the other chains' (DtwQueue) and nothing on the chain waits for them before that
+      std::vector<std::pair<size_t, std::vector<DtwTicket>>> tks;
+      struct Resolve {   // on an error too: return the tickets' blocks / events to the state
+        State& st;
+        std::vector<std::pair<size_t, std::vector<DtwTicket>>>& tks;
+        std::vector<SegOut>& out;
+        ~Resolve() {
+          for (auto& p : tks)
+            for (auto& t : p.second)
+              if (t.blk) {
+                try {
+                  st.resolve_dtw(t, out[p.first].res);
+                } catch (...) {
+                }
+              }
+        }
+      } resolve_guard{st, tks, out};
       bool drew = false;   // a segment of this block drew before: decoder 0's RNG is no longer initial
       for (size_t i = a; i < b && !stop; ++i) {
         if (st.full(with_prompt(params, e), nullptr, 0, (int)(i - a), true) != 0)
@@ -810,14 +831,12 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
         out[i].rng_clean = !drew;
         drew = drew || st.sampled;
         if (st.sampled) out[i].rng_after = st.rng_state();
-        std::vector<DtwTicket> tk = st.take_dtw_jobs();
-        if (i > a)
-          for (auto& t : prev_tk) st.resolve_dtw(t, out[i - 1].res);
-        prev_tk = std::move(tk);
+        tks.emplace_back(i, st.take_dtw_jobs());
         e = next_prompt(e, out[i].res);
         spec_out[i] = e;
       }
-      for (auto& t : prev_tk) st.resolve_dtw(t, out[b - 1].res);
+      for (auto& p : tks)
+        for (auto& t : p.second) st.resolve_dtw(t, out[p.first].res);
     } catch (...) {
       errs[k] = std::current_exception();
       stop = true;
@@ -954,6 +973,9 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
     c->cs.vgroups = b1.vgroups - b0.vgroups;
     c->cs.tiles = b1.tiles - b0.tiles;
     c->cs.step_s = b1.step_s - b0.step_s;
+    c->cs.dq_passes = b1.dq_passes - b0.dq_passes;
+    c->cs.dq_rows = b1.dq_rows - b0.dq_rows;
+    c->cs.dq_jobs = b1.dq_jobs - b0.dq_jobs;
   }
   // stage accounting: chains' times summed into the context's state
   for (int k = 1; k < C; ++k) {
@@ -1807,6 +1829,9 @@ int wdr_context_stage_times(wdr_context* c, wdr_stage_times* o) {
     o->batch_mixed = c->cs.mixed;
     o->batch_xattn_groups = c->cs.vgroups;
     o->batch_xattn_tiles = c->cs.tiles;
+    o->dtwq_passes = c->cs.dq_passes;
+    o->dtwq_rows = c->cs.dq_rows;
+    o->dtwq_jobs = c->cs.dq_jobs;
     return 0;
   })
 }

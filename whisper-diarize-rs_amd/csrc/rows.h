@@ -99,4 +99,12 @@ struct RowsBufs {
 // embed + every layer + (LayerNorm + logits of the logit rows); capture of DTW rows
 void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s);
 
+// the DTW re-forwards of several segments as one pass (the DTW queue, whisper_ctx.cpp): every
+// row is a capture row, no logits; the pass stops after the cross-attention of the last
+// alignment-head layer (l_end - 1: later layers cannot change a captured probability).
+// Projections run on the tiled MFMA GEMM family (ProjArgs::gemm_rows) with k_layernorm before
+// them -- per-row arithmetic independent of the row count, so a segment's DTW times do not
+// depend on which other segments share the pass.
+void dtw_rows_forward(const Context& ctx, const RowsIO& io, int R, int l_end, hipStream_t s);
+
 }  // namespace wdr

@@ -104,10 +104,16 @@ class Context {
   std::vector<std::unique_ptr<class StepBatcher>> batchers;
   int n_batchers = 1;
   StepBatcher& step_batcher(int chain = 0);
+  // multi-chain runs: the windows' DTW re-forwards of every chain, batched off the decode
+  // chain's critical path (DtwQueue, created on demand; WDR_DTW_QUEUE=0: they ride in the step
+  // batcher's requests instead)
+  std::unique_ptr<class DtwQueue> dtwq;
+  class DtwQueue& dtw_queue();
   struct BatchStats {
     long long launches = 0, rows = 0, prefill_rows = 0, dtw_rows = 0, prefills = 0, dtws = 0, mixed = 0;
     long long vgroups = 0, tiles = 0;   // cross-attention groups (VALU) / row tiles (MFMA) launched
     double step_s = 0;                  // the slowest batcher's launch wall
+    long long dq_passes = 0, dq_rows = 0, dq_jobs = 0;   // the DTW queue's
   };
   BatchStats batcher_stats();
   // fp8 (e4m3) encoder GEMMs (BASELINE configs[4]; wdr_context_set_encoder_fp8, WDR_FP8_ENCODER):
@@ -223,10 +229,54 @@ class StepBatcher {
 struct Seq;           // one decoder's sequence (whisper_ctx.cpp)
 
 // a window's DTW job in flight on the DTW stream (State::dtw_timestamps)
+// one window's DTW re-forward queued to the context's DtwQueue (multi-chain runs)
+struct DtwQJob {
+  std::vector<int> toks;
+  int seq = 0;                 // absolute KV-pool sequence (the chain's DTW sequence)
+  const f16* xkv = nullptr;    // the window's cross-K/V slot
+  int sot_len = 0, seek = 0, n_audio = 0;
+  int* blk = nullptr;          // pinned: the times land at blk + 3 * RMAX (State::resolve_dtw)
+  hipEvent_t done = nullptr;   // recorded after the times copy (the state's event)
+  hipEvent_t fwd = nullptr;    // recorded after the pass: the slot's cross-K/V has been read
+  bool issued = false;         // the queue has enqueued the pass and both events
+  double t_submit = 0;
+  size_t cap_off = 0;          // the queue's capture buffer offset (floats)
+  DtwQJob();
+  ~DtwQJob();
+};
+
 struct DtwTicket {
   int i0 = 0, n = 0;          // result range of the full() call that enqueued it
   int* blk = nullptr;         // pinned tokens + times
   void* event = nullptr;      // hipEvent_t
+  std::shared_ptr<DtwQJob> q; // queued re-forward (null: stream-ordered on the state)
+};
+
+// The DTW re-forwards of all chains of a context as few wide passes on a stream of their own
+// (dtw_rows_forward: projections on the tiled GEMM family, the pass stopping after the last
+// alignment-head layer), then each window's DTW kernels.  Submitting never blocks the chain; a
+// chain waits only where it needs a result: before a slot the pass reads is overwritten
+// (State::top_up / on-demand encodes) and when it resolves the times at the end of its block.
+// A pass starts when WDR_DTW_MIN_ROWS rows are queued (256), when the oldest job is
+// WDR_DTW_AGE_MS old (50) or when a chain waits; one job per chain per pass (each chain has one
+// DTW KV sequence).
+class DtwQueue {
+ public:
+  explicit DtwQueue(Context& ctx);
+  ~DtwQueue();
+  DtwQueue(const DtwQueue&) = delete;
+  DtwQueue& operator=(const DtwQueue&) = delete;
+  void submit(const std::shared_ptr<DtwQJob>& j);
+  void wait_issued(const std::shared_ptr<DtwQJob>& j);   // starts its pass at once if still queued
+  bool is_issued(const std::shared_ptr<DtwQJob>& j);
+  long long passes = 0, rows = 0, jobs = 0;
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> m_;
+  Context& ctx_;
+  void run();
+  void issue(std::vector<std::shared_ptr<DtwQJob>>& batch);
 };
 
 class State {
@@ -239,6 +289,8 @@ class State {
   // full() resolves them into result_all before returning.
   int full(const FullParams& p, const float* samples, int n, int job = -1, bool async_dtw = false);
   std::vector<DtwTicket> take_dtw_jobs();
+  void slot_dtw_fence(int slot, hipStream_t s);   // queued DTW pass reading the slot -> s waits
+  void dtw_queue_fence(hipStream_t s);            // queued passes writing the DTW sequence -> s waits
   void resolve_dtw(DtwTicket& t, std::vector<ResultSeg>& segs);
   // encode-ahead: the pipeline's whole segment list (int16 PCM), see whisper_ctx.cpp
   void plan(const int16_t* const* pcm, const int* n, int count, bool detect_lang = false);

@@ -15,6 +15,9 @@
 #include <random>
 #include <exception>
 #include <condition_variable>
+#include <deque>
+#include <set>
+#include <thread>
 #include <mutex>
 #include <sstream>
 
@@ -345,7 +348,7 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
   {
     // KV pool for the decode chains of every State of this context (multi-chain pipeline)
     const char* e = getenv("WDR_DECODE_CHAINS");
-    max_chains = std::max(1, std::min(64, e ? atoi(e) : 16));
+    max_chains = std::max(1, std::min(64, e ? atoi(e) : 24));
     const char* nb = getenv("WDR_BATCHERS");
     n_batchers = std::max(1, std::min(8, nb ? atoi(nb) : 1));
     fp8_encoder = getenv("WDR_FP8_ENCODER") && atoi(getenv("WDR_FP8_ENCODER")) != 0;
@@ -358,6 +361,7 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
 }
 
 Context::~Context() {
+  dtwq.reset();
   batchers.clear();
   if (stream) (void)hipStreamDestroy(stream);
 }
@@ -388,6 +392,7 @@ struct State::Impl {
     int16_t* h_pcm = nullptr;   // pinned staging for the H2D copy of the segment's PCM
     int pcm_cap = 0, x_cap = 0, mel_cap = 0, n_fft_frames = 0, n_samples = 0;
     hipEvent_t ready = nullptr, freed = nullptr;
+    std::shared_ptr<DtwQJob> dtw;   // the queued DTW re-forward that reads this slot (DtwQueue)
   };
   std::vector<Slot> slots;
   int S = 0;                  // ring slots (multiple of kBatch)
@@ -438,7 +443,9 @@ struct State::Impl {
     int i0 = 0, n = 0;             // result_all range of the full() call that produced it
     int* blk = nullptr;            // pinned: tokens [3*RMAX] then times [RMAX + 8]
     hipEvent_t done = nullptr;
+    std::shared_ptr<DtwQJob> q;    // queued to the context's DtwQueue (multi-chain run)
   };
+  std::vector<std::shared_ptr<DtwQJob>> qlive;   // queued re-forwards that may still write DTW_SEQ
   std::vector<DtwJob> jobs;        // enqueued by the current full() call
   // multi-chain run: the last window's DTW re-forward waits to ride in the chain's next batcher
   // request (the next segment's prompt prefill), one request instead of two per segment
@@ -614,6 +621,14 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
 
 State::~State() {
   if (m_) {
+    try {   // queued passes read this state's slots and write its pinned blocks
+      for (auto& q : m_->qlive) {
+        ctx_.dtw_queue().wait_issued(q);
+        (void)hipEventSynchronize(q->done);
+      }
+    } catch (...) {
+    }
+    m_->qlive.clear();
     for (auto& g : m_->graphs)
       if (g.second.exec) (void)hipGraphExecDestroy(g.second.exec);
     (void)hipHostFree(m_->h_tok);
@@ -843,6 +858,27 @@ static int enc_ahead(int S) {
   return std::max(kBatch, std::min(a > 0 ? a : S, S));
 }
 
+// stream `s` waits until the queued DTW pass reading slot `k` has read it (the pass is started
+// at once if it is still queued)
+void State::slot_dtw_fence(int k, hipStream_t s) {
+  Impl& m = *m_;
+  std::shared_ptr<DtwQJob>& q = m.slots[k].dtw;
+  if (!q) return;
+  ctx_.dtw_queue().wait_issued(q);
+  WDR_HIP(hipStreamWaitEvent(s, q->fwd, 0));
+  q.reset();
+}
+
+// stream `s` waits for every queued pass that may still write this chain's DTW KV sequence
+void State::dtw_queue_fence(hipStream_t s) {
+  Impl& m = *m_;
+  for (auto& q : m.qlive) {
+    ctx_.dtw_queue().wait_issued(q);
+    WDR_HIP(hipStreamWaitEvent(s, q->fwd, 0));
+  }
+  m.qlive.clear();
+}
+
 // enqueue every group of segments whose slots' previous occupants (j - S ...) have finished
 void State::top_up(int j) {
   Impl& m = *m_;
@@ -865,6 +901,7 @@ void State::top_up(int j) {
     for (int k = g0; k < g1; ++k) {
       Impl::Slot& sl = m.slots[k % m.S];
       if (k >= m.S) WDR_HIP(hipStreamWaitEvent(m.es, sl.freed, 0));
+      slot_dtw_fence(k % m.S, m.es);   // a queued DTW pass may still read the slot
       const int nk = m.plan.n[k];
       if (nk > sl.pcm_cap) {
         if (sl.h_pcm) WDR_HIP(hipHostFree(sl.h_pcm));
@@ -924,6 +961,16 @@ void State::top_up(int j) {
 
 // the first layer a capture-only pass (the DTW re-forward) can skip: nothing after the last
 // alignment-head layer's cross-attention changes a captured probability
+// WDR_DTW_QUEUE=0: multi-chain DTW re-forwards ride in the step batcher's requests (the round-3
+// schedule) instead of the DtwQueue
+static bool dtw_queue_on() {
+  static const bool on = [] {
+    const char* e = getenv("WDR_DTW_QUEUE");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 static int capture_l_end(const Context& ctx) {
   const int L = ctx.model.hp.n_text_layer;
   if (ctx.aheads_per_layer.size() != (size_t)L) return L;
@@ -1367,10 +1414,37 @@ void State::dtw_timestamps(int i_segment, int n_segments, int seek, int n_frames
   m.ev_pool.pop_back();
   m.jobs.push_back(job);
   Impl::DtwSet& D = m.dset;
+  if (batched && dtw_queue_on()) {
+    // multi-chain run: the re-forward goes to the context's DTW queue, batched with the other
+    // chains' off the decode chain's critical path; the slot keeps a handle (reused only after
+    // the pass has read it)
+    WDR_HIP(hipStreamSynchronize(s_));   // the window's cross-K/V (on-demand encodes) in place
+    auto q = std::make_shared<DtwQJob>();
+    q->toks = toks;
+    q->seq = chain * NSLOT + DTW_SEQ;
+    q->xkv = m.xkv();
+    q->sot_len = sot_len;
+    q->seek = seek;
+    q->n_audio = n_frames / 2;
+    q->blk = job.blk;
+    q->done = job.done;
+    m.jobs.back().q = q;
+    m.slots[m.cur].dtw = q;
+    // passes already run no longer write the DTW sequence
+    DtwQueue& dq = ctx_.dtw_queue();
+    m.qlive.erase(std::remove_if(m.qlive.begin(), m.qlive.end(),
+                                 [&](const std::shared_ptr<DtwQJob>& x) {
+                                   return dq.is_issued(x) && hipEventQuery(x->fwd) == hipSuccess;
+                                 }),
+                  m.qlive.end());
+    m.qlive.push_back(q);
+    ctx_.dtw_queue().submit(q);
+    return;
+  }
   if (batched) {
-    // multi-chain run: the re-forward's rows ride in the chain's next batched request (its next
-    // prompt prefill, or a request of their own: flush_dtw); the DTW kernels follow on the DTW
-    // stream (dtw_after_step)
+    // multi-chain run (WDR_DTW_QUEUE=0): the re-forward's rows ride in the chain's next batched
+    // request (its next prompt prefill, or a request of their own: flush_dtw); the DTW kernels
+    // follow on the DTW stream (dtw_after_step)
     WDR_CHECK(!m.pend.on, "DTW re-forward already pending");
     WDR_HIP(hipStreamSynchronize(s_));   // the window's cross-K/V (on-demand encodes) in place
     m.pend.on = true;
@@ -1384,6 +1458,8 @@ void State::dtw_timestamps(int i_segment, int n_segments, int seek, int n_frames
     m.pend.done = job.done;
     return;
   } else {
+    // queued re-forwards of an earlier batched run write the same DTW sequence: after them
+    dtw_queue_fence(m.sd);
     // the window's cross-K/V (encoded ahead, or on demand on the decode stream) must be in place
     WDR_HIP(hipEventRecord(m.ev_sync, s_));
     WDR_HIP(hipStreamWaitEvent(m.sd, m.ev_sync, 0));
@@ -1452,7 +1528,7 @@ void State::flush_dtw() {
 std::vector<DtwTicket> State::take_dtw_jobs() {
   Impl& m = *m_;
   std::vector<DtwTicket> out;
-  for (auto& j : m.jobs) out.push_back(DtwTicket{j.i0, j.n, j.blk, (void*)j.done});
+  for (auto& j : m.jobs) out.push_back(DtwTicket{j.i0, j.n, j.blk, (void*)j.done, j.q});
   m.jobs.clear();
   return out;
 }
@@ -1461,7 +1537,9 @@ void State::resolve_dtw(DtwTicket& t, std::vector<ResultSeg>& segs) {
   Impl& m = *m_;
   const Vocab& v = ctx_.vocab;
   if (m.pend.on && m.pend.done == (hipEvent_t)t.event) flush_dtw();
+  if (t.q) ctx_.dtw_queue().wait_issued(t.q);
   WDR_HIP(hipEventSynchronize((hipEvent_t)t.event));
+  t.q.reset();
   const int* times = t.blk + 3 * RMAX;
   const int nt = times[RMAX + 4];
   int k = 0;
@@ -1929,6 +2007,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
       const double t = now_s();
       flush_dtw();   // a pending re-forward reads the slot this encode overwrites
       WDR_HIP(hipStreamWaitEvent(s_, m.ev_dtw, 0));   // a DTW job may still read this slot
+      slot_dtw_fence(m.cur, s_);                       // ... or a queued pass
       encode_window(seek);
       WDR_HIP(hipStreamSynchronize(s_));
       times.encode += now_s() - t;
@@ -2213,6 +2292,7 @@ struct StepBatcher::Impl {
     VocabIds vids{};
   };
   std::map<long long, G> graphs;  // decode-only batches, by (K, group kind, groups, rows)
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;   // a launch's GPU span (WDR_BATCH_LOG)
 };
 
 StepBatcher::StepBatcher(Context& ctx) : ctx_(ctx), m_(new Impl) {
@@ -2237,6 +2317,8 @@ StepBatcher::StepBatcher(Context& ctx) : ctx_(ctx), m_(new Impl) {
   WDR_HIP(hipHostMalloc((void**)&m.h_beam, (size_t)LB * BEAM_KMAX * sizeof(BeamCand), hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_ctl, LB * sizeof(LogitsCtl), hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_tok, LB * sizeof(TokOut), hipHostMallocDefault));
+  WDR_HIP(hipEventCreate(&m.ev0));
+  WDR_HIP(hipEventCreate(&m.ev1));
 }
 
 StepBatcher::~StepBatcher() {
@@ -2250,6 +2332,8 @@ StepBatcher::~StepBatcher() {
   (void)hipHostFree(m_->h_ctl);
   (void)hipHostFree(m_->h_tok);
   (void)hipHostFree(m_->h_beam);
+  if (m_->ev0) (void)hipEventDestroy(m_->ev0);
+  if (m_->ev1) (void)hipEventDestroy(m_->ev1);
 }
 
 StepBatcher& Context::step_batcher(int chain) {
@@ -2275,6 +2359,11 @@ Context::BatchStats Context::batcher_stats() {
     o.vgroups += sb.vgroups;
     o.tiles += sb.tiles;
     o.step_s = std::max(o.step_s, sb.step_s);
+  }
+  if (dtwq) {
+    o.dq_passes = dtwq->passes;
+    o.dq_rows = dtwq->rows;
+    o.dq_jobs = dtwq->jobs;
   }
   return o;
 }
@@ -2407,6 +2496,8 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
   const double t_step = now_s();
   const bool sampled = prof_step();
   const bool decode_only = n_pre == 0 && n_dtw == 0;
+  static FILE* blog = getenv("WDR_BATCH_LOG") ? fopen(getenv("WDR_BATCH_LOG"), "w") : nullptr;
+  if (blog) WDR_HIP(hipEventRecord(m.ev0, m.s));
   if (sampled || getenv("WDR_NO_GRAPH") || !decode_only) {
     // sampled step for live kernel timing (prof.h), graphs disabled, or a mixed batch
     prof_in_step(sampled);
@@ -2450,6 +2541,7 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
       WDR_HIP(ge);
     }
   }
+  if (blog) WDR_HIP(hipEventRecord(m.ev1, m.s));
   WDR_HIP(hipStreamSynchronize(m.s));
   auto tok_of = [&](int i) {
     const TokOut& o = m.h_tok[i];
@@ -2484,12 +2576,197 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
   if (!decode_only) mixed++;
   const double t_end = now_s();
   step_s += t_end - t_step;
-  // WDR_BATCH_LOG=<file>: one line per launch (start s, rows, wall ms, prefill rows, DTW rows)
-  static FILE* blog = getenv("WDR_BATCH_LOG") ? fopen(getenv("WDR_BATCH_LOG"), "w") : nullptr;
+  // WDR_BATCH_LOG=<file>: one line per launch (start s, rows, wall ms, prefill rows, DTW rows,
+  // GPU ms: the launch's span on its stream, first command to last)
   if (blog) {
-    fprintf(blog, "%.6f %d %.3f %d %d\n", t_step, R, (t_end - t_step) * 1e3, n_pre, n_dtw);
+    float gms = 0.f;
+    (void)hipEventElapsedTime(&gms, m.ev0, m.ev1);
+    fprintf(blog, "%.6f %d %.3f %d %d %.3f\n", t_step, R, (t_end - t_step) * 1e3, n_pre, n_dtw, gms);
     fflush(blog);
   }
+}
+
+}  // namespace wdr
+
+// ------------------------------------------------------------------ DTW queue
+namespace wdr {
+
+DtwQJob::DtwQJob() { WDR_HIP(hipEventCreateWithFlags(&fwd, hipEventDisableTiming)); }
+DtwQJob::~DtwQJob() {
+  if (fwd) (void)hipEventDestroy(fwd);
+}
+
+struct DtwQueue::Impl {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::shared_ptr<DtwQJob>> pend;
+  int pend_rows = 0;
+  int urgent = 0;
+  bool stop = false;
+  std::exception_ptr err;
+  std::thread th;
+  hipStream_t s = nullptr;
+  int RB = 0, A = 1, l_end = 1, min_rows = 256;
+  double max_age = 0.05;
+  RowsBufs bufs;
+  std::unique_ptr<RowBatch> tb;
+  DevMem cap, nrm, xdtw, times;
+};
+
+DtwQueue& Context::dtw_queue() {
+  static std::mutex mu;
+  std::lock_guard<std::mutex> g(mu);
+  if (!dtwq) dtwq = std::make_unique<DtwQueue>(*this);
+  return *dtwq;
+}
+
+DtwQueue::DtwQueue(Context& ctx) : m_(new Impl), ctx_(ctx) {
+  WDR_HIP(hipSetDevice(ctx.cp.gpu_device));
+  Impl& m = *m_;
+  const HParams& hp = ctx.model.hp;
+  m.A = std::max<int>(1, (int)ctx.aheads.size());
+  m.l_end = capture_l_end(ctx);
+  m.RB = 1024;   // rows of one pass (a DTW re-forward is <= RMAX + 1 rows)
+  if (const char* e = getenv("WDR_DTW_MIN_ROWS")) m.min_rows = std::max(1, atoi(e));
+  if (const char* e = getenv("WDR_DTW_AGE_MS")) m.max_age = std::max(0.0, atof(e)) * 1e-3;
+  int lo = 0, hi = 0;
+  WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  WDR_HIP(hipStreamCreateWithPriority(&m.s, hipStreamNonBlocking, lo));
+  m.bufs.alloc(m.RB, 1, hp.n_text_state, hp.n_text_head, hp.n_vocab);
+  m.tb = std::make_unique<RowBatch>(m.RB, 1, m.RB);
+  m.cap = DevMem((size_t)m.A * m.RB * 1500 * 4);
+  m.nrm = DevMem((size_t)m.A * RMAX * 1500 * 4);
+  m.xdtw = DevMem((size_t)RMAX * 1500 * 4);
+  m.times = DevMem((RMAX + 8) * 4);
+  m.th = std::thread([this] { run(); });
+}
+
+DtwQueue::~DtwQueue() {
+  {
+    std::lock_guard<std::mutex> g(m_->mu);
+    m_->stop = true;
+  }
+  m_->cv.notify_all();
+  if (m_->th.joinable()) m_->th.join();
+  if (m_->s) {
+    (void)hipStreamSynchronize(m_->s);
+    (void)hipStreamDestroy(m_->s);
+  }
+}
+
+void DtwQueue::submit(const std::shared_ptr<DtwQJob>& j) {
+  WDR_CHECK((int)j->toks.size() >= 1 && (int)j->toks.size() <= RMAX + 1 && j->xkv && j->blk && j->done,
+            "DTW queue: bad job");
+  {
+    std::lock_guard<std::mutex> g(m_->mu);
+    j->t_submit = now_s();
+    m_->pend.push_back(j);
+    m_->pend_rows += (int)j->toks.size();
+    jobs++;
+  }
+  m_->cv.notify_all();
+}
+
+bool DtwQueue::is_issued(const std::shared_ptr<DtwQJob>& j) {
+  std::lock_guard<std::mutex> g(m_->mu);
+  return j->issued;
+}
+
+void DtwQueue::wait_issued(const std::shared_ptr<DtwQJob>& j) {
+  Impl& m = *m_;
+  std::unique_lock<std::mutex> lk(m.mu);
+  if (j->issued) {
+    if (m.err) std::rethrow_exception(m.err);
+    return;
+  }
+  m.urgent++;
+  m.cv.notify_all();
+  m.cv.wait(lk, [&] { return j->issued; });
+  m.urgent--;
+  if (m.err) std::rethrow_exception(m.err);
+}
+
+void DtwQueue::run() {
+  Impl& m = *m_;
+  try {
+    WDR_HIP(hipSetDevice(ctx_.cp.gpu_device));
+  } catch (...) {
+    std::lock_guard<std::mutex> g(m.mu);
+    m.err = std::current_exception();
+  }
+  std::unique_lock<std::mutex> lk(m.mu);
+  while (true) {
+    auto ready = [&] {
+      return !m.pend.empty() && (m.stop || m.urgent > 0 || m.pend_rows >= m.min_rows ||
+                                 now_s() - m.pend.front()->t_submit >= m.max_age);
+    };
+    m.cv.wait_for(lk, std::chrono::milliseconds(2), [&] { return ready() || (m.stop && m.pend.empty()); });
+    if (m.pend.empty()) {
+      if (m.stop) break;
+      continue;
+    }
+    if (!ready()) continue;
+    // oldest first, one job per DTW sequence (chain), within the pass's row capacity
+    std::vector<std::shared_ptr<DtwQJob>> batch;
+    std::set<int> seqs;
+    int rows = 0;
+    for (auto it = m.pend.begin(); it != m.pend.end();) {
+      const int n = (int)(*it)->toks.size();
+      if (seqs.count((*it)->seq) || rows + n > m.RB) {
+        ++it;
+        continue;
+      }
+      seqs.insert((*it)->seq);
+      rows += n;
+      batch.push_back(*it);
+      it = m.pend.erase(it);
+    }
+    m.pend_rows -= rows;
+    lk.unlock();
+    std::exception_ptr e;
+    if (!m.err) {
+      try {
+        issue(batch);
+      } catch (...) {
+        e = std::current_exception();
+      }
+    }
+    lk.lock();
+    if (e && !m.err) m.err = e;
+    for (auto& j : batch) j->issued = true;
+    m.cv.notify_all();
+  }
+}
+
+void DtwQueue::issue(std::vector<std::shared_ptr<DtwQJob>>& batch) {
+  Impl& m = *m_;
+  RowBatch& tb = *m.tb;
+  tb.clear();
+  size_t off = 0;
+  for (auto& j : batch) {
+    RowGroupDesc g;
+    g.n = (int)j->toks.size();
+    g.tok = j->toks.data();
+    g.seq0 = j->seq;
+    g.xkv = j->xkv;
+    g.cap = m.cap.as<float>() + off;
+    g.l_end = m.l_end;
+    tb.add(g);
+    j->cap_off = off;
+    off += (size_t)m.A * g.n * 1500;
+  }
+  RowsIO io = m.bufs.io(ctx_, ctx_.model.hp.n_vocab);
+  tb.upload(io, m.s, true, true);
+  dtw_rows_forward(ctx_, io, tb.R, m.l_end, m.s);
+  for (auto& j : batch) WDR_HIP(hipEventRecord(j->fwd, m.s));
+  for (auto& j : batch) {
+    launch_dtw(m.cap.as<float>() + j->cap_off, m.A, (int)j->toks.size(), 1500, j->n_audio, j->sot_len, j->seek,
+               m.nrm.as<float>(), m.xdtw.as<float>(), m.times.as<int>(), m.times.as<int>() + RMAX + 4, m.s);
+    WDR_HIP(wdr_memcpy_async(j->blk + 3 * RMAX, m.times.p, (RMAX + 8) * 4, hipMemcpyDeviceToHost, m.s));
+    WDR_HIP(hipEventRecord(j->done, m.s));
+  }
+  passes++;
+  rows += tb.R;
 }
 
 }  // namespace wdr

@@ -88,7 +88,8 @@ class StageTimes(C.Structure):
                 ("fixup_segments", i64), ("replay_segments", i64), ("spec_s", f64), ("fixup_s", f64),
                 ("batch_step_s", f64), ("early_fixup_segments", i64), ("batch_prefill_rows", i64),
                 ("batch_dtw_rows", i64), ("batch_prefills", i64), ("batch_dtws", i64), ("batch_mixed", i64),
-                ("batch_xattn_groups", i64), ("batch_xattn_tiles", i64)]
+                ("batch_xattn_groups", i64), ("batch_xattn_tiles", i64), ("dtwq_passes", i64), ("dtwq_rows", i64),
+                ("dtwq_jobs", i64)]
 
 
 class Token(C.Structure):
