@@ -159,10 +159,6 @@ struct ProjArgs {
   // lno_cnt: one arrival counter per row tile, zero between launches (the last arriver resets it)
   f16* lno_y = nullptr; int ldlno = 0; const float* lno_g = nullptr; const float* lno_b = nullptr;
   int* lno_cnt = nullptr;
-  // rows of any count on the tiled MFMA GEMM family (k_gemm2 for N <= 4096, else k_gemm: the
-  // same per-row arithmetic, rows masked): the batched DTW re-forwards, whose row count depends
-  // on timing while each row's result must not (csrc/rows.h dtw_rows_forward)
-  int gemm_rows = 0;
 };
 
 // Live kernel clock (csrc/prof.cpp): a launch the profiler samples carries ts -> {earliest wave

@@ -295,8 +295,9 @@ constexpr int XA_KC = 64, XA_NS = 24;
 // G: the largest group a launch holds -- 1 for the greedy batched step (every row its own
 // group), which keeps the kernel at <= 64 VGPRs so a workgroup still fits on a CU beside an
 // encoder GEMM tile (k_gemm4: 2 x 224 of the SIMD's 512)
-// one (row, head) of the combine: lane d merges dimension d over the NS chunk partials (also the
-// body of k_xattn_combine, so the fused and separate combines are the same arithmetic)
+// one (row, head) of the combine inside the partial launch (FC): lane d merges dimension d over
+// the NS chunk partials in k_xattn_combine's arithmetic (the same reductions, the sum over c in
+// order), its loads in groups of 8 to bound the fused kernel's registers
 template <int NS>
 __device__ __forceinline__ void xattn_combine_row(const XAttnArgs& a, int r, int h, int d) {
   float2 ml = make_float2(-INFINITY, 0.f);
@@ -304,8 +305,6 @@ __device__ __forceinline__ void xattn_combine_row(const XAttnArgs& a, int r, int
   const float M = wave_max(ml.x);
   const float w = (d < NS && ml.x != -INFINITY) ? __expf(ml.x - M) : 0.f;
   const float L = wave_sum(ml.y * w);
-  // chunk partials in groups of 8 loads (bounded registers: the fused form runs inside the
-  // 47-VGPR partial kernel); the sum is over c = 0 .. NS-1 in order either way
   const float* pb = a.part_o + ((long long)r * a.n_head + h) * 64 + d;
   const long long cs = (long long)a.R * a.n_head * 64;
   float acc = 0.f;
@@ -438,7 +437,20 @@ __global__ __launch_bounds__(64) void k_xattn_combine(XAttnArgs a) {
     if ((r & 127) >= t.y) return;
     r = t.x + (r & 127);
   }
-  xattn_combine_row<NS>(a, r, blockIdx.y, threadIdx.x);
+  const int h = blockIdx.y, d = threadIdx.x;
+  float po[NS];
+#pragma unroll
+  for (int c = 0; c < NS; ++c) po[c] = a.part_o[(((long long)c * a.R + r) * a.n_head + h) * 64 + d];
+  float2 ml = make_float2(-INFINITY, 0.f);
+  if (d < NS) ml = a.part_ml[((long long)d * a.R + r) * a.n_head + h];
+  const float M = wave_max(ml.x);
+  const float w = (d < NS && ml.x != -INFINITY) ? __expf(ml.x - M) : 0.f;
+  const float L = wave_sum(ml.y * w);
+  float acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < NS; ++c) acc += po[c] * __shfl(w, c, 64);
+  a.o[(long long)r * a.ldo + h * 64 + d] = (f16)(acc / L);
+  if (a.ml_out && d == 0) a.ml_out[(long long)r * a.n_head + h] = make_float2(M, L);
 }
 
 // ---------------------------------------------------------------- cross-attention, MFMA row tiles

@@ -2248,37 +2248,8 @@ static void launch_rows(const ProjArgs& a, hipStream_t s) {
   WDR_HIP(hipGetLastError());
 }
 
-template <int EPI>
-static void launch_gemm_rows_epi(const ProjArgs& a, hipStream_t s) {
-  const int ob = (EPI == EPI_F32_RESID || EPI == EPI_F32 || EPI == EPI_F32_GELU_POS) ? 4 : 2;
-  const double bytes = (double)a.N * a.K * 2 + (double)a.M * a.K * 2 + (double)a.M * a.N * ob;
-  const double flops = 2.0 * a.M * a.N * a.K;
-  if (a.K % G2_BK == 0 && a.N <= 4096)
-    wdr_launch(PROF_GEMM, bytes, flops, k_gemm2<EPI>, dim3((a.N / GB_N) * cdiv(a.M, GB_M)), dim3(256), 0, s, a);
-  else
-    wdr_launch(PROF_GEMM, bytes, flops, k_gemm<EPI>, dim3(a.N / GB_N, cdiv(a.M, GB_M)), dim3(256), 0, s, a);
-}
-
-// ProjArgs::gemm_rows: any M on k_gemm2 / k_gemm (tile-independent per-row arithmetic)
-static void launch_gemm_rows(const ProjArgs& a, hipStream_t s) {
-  WDR_CHECK(a.N % GB_N == 0 && a.K % GB_K == 0 && a.lda % 8 == 0 && a.ldb % 8 == 0 && !a.ln_x && !a.row_map,
-            "GEMM rows: N % 128, K % 32, no LN prologue / row map");
-  switch (a.epi) {
-    case EPI_F16: launch_gemm_rows_epi<EPI_F16>(a, s); break;
-    case EPI_F16_GELU: launch_gemm_rows_epi<EPI_F16_GELU>(a, s); break;
-    case EPI_F32_RESID: launch_gemm_rows_epi<EPI_F32_RESID>(a, s); break;
-    case EPI_QKV_CACHE: launch_gemm_rows_epi<EPI_QKV_CACHE>(a, s); break;
-    default: throw std::runtime_error("GEMM rows: bad epilogue");
-  }
-  WDR_HIP(hipGetLastError());
-}
-
 void launch_proj(const ProjArgs& a, hipStream_t s) {
   WDR_CHECK(a.M > 0 && a.K > 0 && a.N > 0, "projection: empty shape");
-  if (a.gemm_rows) {
-    launch_gemm_rows(a, s);
-    return;
-  }
   if (a.rows_mma) {
     launch_rows(a, s);
     return;

@@ -163,7 +163,7 @@ RowsIO RowsBufs::io(const Context& ctx, int V) const {
   return o;
 }
 
-void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s) {
+void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, int l_stop) {
   const Model& md = ctx.model;
   const HParams& hp = md.hp;
   const int d = hp.n_text_state, L = hp.n_text_layer, H = hp.n_text_head;
@@ -269,6 +269,7 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s) {
       launch_aheads_capture_rows(ca, (int)ctx.aheads_per_layer[l].size(), s);
     }
     if (ctx.aheads_per_layer.size() == (size_t)L) cap_slot0 += (int)ctx.aheads_per_layer[l].size();
+    if (l + 1 >= l_stop) return;   // a DTW pass: nothing after this layer's capture matters
     launch_proj(LNO(P(io.attd, d, e.w_xo, e.b_xo, io.xd, d, d, d, EPI_F32_RESID), 1, l, e.ln3_g, e.ln3_b), s);
     launch_proj(P(nullptr, d, e.w_fc1, e.b_fc1, io.mlpd, 4 * d, 4 * d, d, EPI_F16_GELU, e.ln3_g, e.ln3_b), s);
     // fc2 leaves the next layer's ln1 -- after the last layer the final LN of the logit rows
@@ -299,68 +300,10 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s) {
 }
 
 void dtw_rows_forward(const Context& ctx, const RowsIO& io, int R, int l_end, hipStream_t s) {
-  const Model& md = ctx.model;
-  const HParams& hp = md.hp;
-  const int d = hp.n_text_state, L = hp.n_text_layer, H = hp.n_text_head;
-  const float scale = 1.0f / 8.0f;
-  WDR_CHECK(R >= 1 && io.tok && io.xkv && io.n_cap == R && ctx.aheads_per_layer.size() == (size_t)L,
+  WDR_CHECK(io.n_cap == R && ctx.aheads_per_layer.size() == (size_t)ctx.model.hp.n_text_layer,
             "DTW rows forward: every row a capture row, alignment heads known");
-  WDR_CHECK(l_end >= 1 && l_end <= L, "DTW rows forward: bad last layer");
-  auto G = [&](const f16* A, int lda, const f16* W, const float* b, void* out, int ldo, int N, int K, int epi) {
-    ProjArgs a{A, lda, W, K, b, out, ldo, nullptr, 0, R, N, K, epi};
-    a.gemm_rows = 1;
-    return a;
-  };
-  launch_embed(md.tok_emb, md.dec_pos, io.tok, io.pos, R, d, io.xd, s);
-  int cap_slot0 = 0;
-  for (int l = 0; l < l_end; ++l) {
-    const DecLayer& e = md.dec[l];
-    f16* kc = io.kc + (size_t)l * io.layer_stride;
-    f16* vc = io.vc + (size_t)l * io.layer_stride;
-    launch_layernorm(io.xd, d, e.ln1_g, e.ln1_b, io.hd, d, R, d, s);
-    ProjArgs q = G(io.hd, d, e.w_qkv, e.b_qkv, io.qkvd, 3 * d, 3 * d, d, EPI_QKV_CACHE);
-    q.kc = kc;
-    q.vc = vc;
-    q.seq_stride = io.seq_stride;
-    q.row_seq = io.seq;
-    q.row_pos = io.pos;
-    q.d = d;
-    launch_proj(q, s);
-    DecSelfArgs sa{io.qkvd, 3 * d, kc, vc, io.seq_stride, d, io.seq, io.pos, io.attd, d, scale};
-    launch_dec_self_attn(sa, R, H, s);
-    launch_proj(G(io.attd, d, e.w_o, e.b_o, io.xd, d, d, d, EPI_F32_RESID), s);
-    launch_layernorm(io.xd, d, e.ln2_g, e.ln2_b, io.hd, d, R, d, s);
-    launch_proj(G(io.hd, d, e.w_xq, e.b_xq, io.qx, d, d, d, EPI_F16), s);
-    const bool cap_layer = !ctx.aheads_per_layer[l].empty();
-    XAttnArgs xa{io.qx, d, nullptr, nullptr, 64, XKV_T, R, H, scale, io.part_o, io.part_ml, io.attd, d};
-    xa.row_k = io.xkv;
-    xa.layer_off = xkv_k_off(l, H);
-    xa.v_off = xkv_v_off(l, H) - xkv_k_off(l, H);
-    xa.hs = XKV_HS;
-    xa.grp = io.grp;
-    xa.lead = io.lead;
-    xa.n_grp = io.n_vgrp;
-    xa.n_vgrp = io.n_vgrp;
-    xa.vgrp_max = io.vgrp_max;
-    xa.lend = io.lend;
-    xa.layer = l;
-    xa.tiles = io.tiles;
-    xa.n_tiles = io.n_tiles;
-    xa.ml_out = cap_layer ? io.ml : nullptr;
-    launch_xattn_rows(xa, s);
-    if (cap_layer) {
-      CaptureRowsArgs ca{io.qx, d, io.xkv, xkv_k_off(l, H), XKV_HS, io.ml,
-                         ctx.aheads_dev.as<int>() + ctx.aheads_dev_off[l], io.crow, io.cdst, io.cstride,
-                         io.n_cap, cap_slot0, XKV_T, H, scale};
-      launch_aheads_capture_rows(ca, (int)ctx.aheads_per_layer[l].size(), s);
-    }
-    cap_slot0 += (int)ctx.aheads_per_layer[l].size();
-    if (l + 1 == l_end) break;   // nothing after the last alignment-head layer's capture matters
-    launch_proj(G(io.attd, d, e.w_xo, e.b_xo, io.xd, d, d, d, EPI_F32_RESID), s);
-    launch_layernorm(io.xd, d, e.ln3_g, e.ln3_b, io.hd, d, R, d, s);
-    launch_proj(G(io.hd, d, e.w_fc1, e.b_fc1, io.mlpd, 4 * d, 4 * d, d, EPI_F16_GELU), s);
-    launch_proj(G(io.mlpd, 4 * d, e.w_fc2, e.b_fc2, io.xd, d, d, 4 * d, EPI_F32_RESID), s);
-  }
+  WDR_CHECK(l_end >= 1 && l_end <= ctx.model.hp.n_text_layer, "DTW rows forward: bad last layer");
+  rows_forward(ctx, io, R, s, l_end);
 }
 
 }  // namespace wdr

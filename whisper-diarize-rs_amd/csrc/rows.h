@@ -96,15 +96,15 @@ struct RowsBufs {
   RowsIO io(const Context& ctx, int V) const;   // tables unset
 };
 
-// embed + every layer + (LayerNorm + logits of the logit rows); capture of DTW rows
-void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s);
+// embed + every layer + (LayerNorm + logits of the logit rows); capture of DTW rows.  l_stop:
+// return after the cross-attention (+ capture) of layer l_stop - 1 (no logits then)
+void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, int l_stop = 1 << 30);
 
-// the DTW re-forwards of several segments as one pass (the DTW queue, whisper_ctx.cpp): every
-// row is a capture row, no logits; the pass stops after the cross-attention of the last
-// alignment-head layer (l_end - 1: later layers cannot change a captured probability).
-// Projections run on the tiled MFMA GEMM family (ProjArgs::gemm_rows) with k_layernorm before
-// them -- per-row arithmetic independent of the row count, so a segment's DTW times do not
-// depend on which other segments share the pass.
+// the DTW re-forwards of several segments as one pass (the DTW queue, whisper_ctx.cpp, and a
+// single chain's own re-forward): every row a capture row, no logits, the pass stopping after
+// the cross-attention of the last alignment-head layer (l_end - 1: later layers cannot change a
+// captured probability).  The rows arithmetic above -- independent of the row count -- so a
+// segment's DTW times do not depend on which other segments share the pass.
 void dtw_rows_forward(const Context& ctx, const RowsIO& io, int R, int l_end, hipStream_t s);
 
 }  // namespace wdr

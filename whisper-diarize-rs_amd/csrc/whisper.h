@@ -331,7 +331,10 @@ class State {
   hipStream_t s_;
   std::unique_ptr<Impl> m_;
   // pieces of full()
-  void top_up(int job);
+  void top_up(int job);              // encodes through segment job + lookahead issued (waits)
+  bool top_up_batch(int job);        // issue the next encode-ahead batch if allowed; false: none
+  void enc_loop();                   // the encode-ahead host thread (WDR_ENC_THREAD)
+  void enc_quiesce();                // no batch in flight on the encode-ahead thread
   Seq decode_sample(const std::vector<int>& prompt, const FullParams& params, float t_cur, int seek, int seek_end,
                     int Lf, int window, float* nosp);
   Seq decode_beam(const std::vector<int>& prompt, const FullParams& params, float t_cur, int seek, int seek_end, int Lf,

@@ -390,6 +390,11 @@ struct State::Impl {
   struct Slot {
     DevMem x, mel, gmax, pcm;
     int16_t* h_pcm = nullptr;   // pinned staging for the H2D copy of the segment's PCM
+    // the segment's signal energy (heuristic timestamps), computed on the encode-ahead stream
+    // and copied back before `ready`: the decode chain reads it without a GPU round trip
+    DevMem energy_d;
+    float* h_energy = nullptr;
+    int energy_cap = 0, energy_n = -1;
     int pcm_cap = 0, x_cap = 0, mel_cap = 0, n_fft_frames = 0, n_samples = 0;
     hipEvent_t ready = nullptr, freed = nullptr;
     std::shared_ptr<DtwQJob> dtw;   // the queued DTW re-forward that reads this slot (DtwQueue)
@@ -410,6 +415,27 @@ struct State::Impl {
   // logits of each slot's window 0 (pinned, written by the encode stream before `ready`)
   RowsBufs lb;                   // its rows forward (kBatch rows)
   std::unique_ptr<RowBatch> tlb;
+  // full encode-ahead batches (kBatch windows: encoder + cross-K/V + language detection) as one
+  // hipGraph per ring slot group (and fp8 mode): ~560 launches become one replay, which keeps
+  // the chain thread's host time between its batched steps short (top_up runs on it).  Each
+  // group has its own language-detection table (its slots' cross-K/V pointers are constant).
+  struct EncGraph {
+    hipGraphExec_t exec = nullptr;
+    std::unique_ptr<RowBatch> tl;
+  };
+  std::map<int, EncGraph> enc_graphs;
+  // WDR_CHAIN_LOG: DTW-queue waits / encoder launch host time (ns; the encode-ahead thread adds too)
+  std::atomic<long long> t_fence{0}, t_enc_launch{0};
+  // the encode-ahead host thread: issues the plan's batches (top_up_batch) up to the lookahead of
+  // the highest segment whose full() has started (enc_target), so the ~600 launches / copies of
+  // a batch leave the chain thread (which waits only when its segment's batch is not issued yet)
+  std::thread enc_th;
+  std::mutex enc_mu;
+  std::condition_variable enc_cv;
+  int enc_target = -1;
+  bool enc_stop = false, enc_busy = false;
+  std::exception_ptr enc_err;
+  std::atomic<long long> enc_windows{0};
   float* h_lang = nullptr;      // [(S + 1)][100]
   DevMem energy_d; int energy_cap = 0;
   const f16* xkv() const { return xkv_ring.as<f16>() + (size_t)cur * xkv_slot_elems; }
@@ -620,6 +646,14 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
 }
 
 State::~State() {
+  if (m_ && m_->enc_th.joinable()) {
+    {
+      std::lock_guard<std::mutex> g(m_->enc_mu);
+      m_->enc_stop = true;
+    }
+    m_->enc_cv.notify_all();
+    m_->enc_th.join();
+  }
   if (m_) {
     try {   // queued passes read this state's slots and write its pinned blocks
       for (auto& q : m_->qlive) {
@@ -630,6 +664,9 @@ State::~State() {
     }
     m_->qlive.clear();
     for (auto& g : m_->graphs)
+      if (g.second.exec) (void)hipGraphExecDestroy(g.second.exec);
+    if (m_->es) (void)hipStreamSynchronize(m_->es);
+    for (auto& g : m_->enc_graphs)
       if (g.second.exec) (void)hipGraphExecDestroy(g.second.exec);
     (void)hipHostFree(m_->h_tok);
     (void)hipHostFree(m_->h_ctl);
@@ -659,6 +696,7 @@ State::~State() {
     if (m_->ev_dtw) (void)hipEventDestroy(m_->ev_dtw);
     for (auto& sl : m_->slots) {
       if (sl.h_pcm) (void)hipHostFree(sl.h_pcm);
+      if (sl.h_energy) (void)hipHostFree(sl.h_energy);
       if (sl.ready) (void)hipEventDestroy(sl.ready);
       if (sl.freed) (void)hipEventDestroy(sl.freed);
     }
@@ -829,21 +867,29 @@ void State::read_encoder_out(float* out) {
 // on its slot's `ready` event, and slot j % S is reused once segment j - S has recorded `freed`.
 void State::plan(const int16_t* const* pcm, const int* n, int count, bool detect_lang) {
   Impl& m = *m_;
+  enc_quiesce();
   WDR_HIP(hipStreamSynchronize(m.es));
-  m.plan.detect_lang = detect_lang;
-  m.plan.pcm.assign(pcm, pcm + count);
-  m.plan.n.assign(n, n + count);
-  m.plan.next_enq = 0;
+  {
+    std::lock_guard<std::mutex> g(m.enc_mu);
+    m.plan.detect_lang = detect_lang;
+    m.plan.pcm.assign(pcm, pcm + count);
+    m.plan.n.assign(n, n + count);
+    m.plan.next_enq = 0;
+    m.enc_err = nullptr;
+  }
   top_up(0);
 }
 
 void State::unplan() {
   Impl& m = *m_;
+  enc_quiesce();
   flush_dtw();
   WDR_HIP(hipStreamSynchronize(m.es));
+  std::lock_guard<std::mutex> g(m.enc_mu);
   m.plan.pcm.clear();
   m.plan.n.clear();
   m.plan.next_enq = 0;
+  times.windows += m.enc_windows.exchange(0);
 }
 
 // Segments the encode-ahead stream may run ahead of the decoder (WDR_ENC_AHEAD, kBatch..S;
@@ -864,7 +910,9 @@ void State::slot_dtw_fence(int k, hipStream_t s) {
   Impl& m = *m_;
   std::shared_ptr<DtwQJob>& q = m.slots[k].dtw;
   if (!q) return;
+  const double t = now_s();
   ctx_.dtw_queue().wait_issued(q);
+  m.t_fence += (long long)((now_s() - t) * 1e9);
   WDR_HIP(hipStreamWaitEvent(s, q->fwd, 0));
   q.reset();
 }
@@ -879,24 +927,97 @@ void State::dtw_queue_fence(hipStream_t s) {
   m.qlive.clear();
 }
 
-// enqueue every group of segments whose slots' previous occupants (j - S ...) have finished
+static bool enc_thread_on() {
+  static const bool on = !(getenv("WDR_ENC_THREAD") && atoi(getenv("WDR_ENC_THREAD")) == 0);
+  return on;
+}
+
+// the encode-ahead host thread of this state
+void State::enc_loop() {
+  Impl& m = *m_;
+  std::unique_lock<std::mutex> lk(m.enc_mu);
+  try {
+    WDR_HIP(hipSetDevice(ctx_.cp.gpu_device));
+  } catch (...) {
+    m.enc_err = std::current_exception();
+  }
+  while (!m.enc_stop) {
+    if (m.enc_err || m.enc_target < 0) {
+      m.enc_cv.wait(lk);
+      continue;
+    }
+    const int j = m.enc_target;
+    m.enc_busy = true;
+    lk.unlock();
+    bool issued = false;
+    std::exception_ptr e;
+    try {
+      issued = top_up_batch(j);
+    } catch (...) {
+      e = std::current_exception();
+    }
+    lk.lock();
+    m.enc_busy = false;
+    if (e) m.enc_err = e;
+    m.enc_cv.notify_all();
+    if (!issued && !e && m.enc_target == j) m.enc_cv.wait(lk);   // nothing allowed until the target moves
+  }
+}
+
+// the encode-ahead thread idle (no batch being issued), its target cleared
+void State::enc_quiesce() {
+  Impl& m = *m_;
+  if (!m.enc_th.joinable()) return;
+  std::unique_lock<std::mutex> lk(m.enc_mu);
+  m.enc_target = -1;
+  m.enc_cv.notify_all();
+  m.enc_cv.wait(lk, [&] { return !m.enc_busy; });
+}
+
+// segment j's encode (and every batch the lookahead allows) issued; on the encode-ahead thread
+// when it runs (the chain waits only if j's own batch is not issued yet)
 void State::top_up(int j) {
+  Impl& m = *m_;
+  if (!enc_thread_on()) {
+    while (top_up_batch(j)) {
+    }
+    return;
+  }
+  if (!m.enc_th.joinable()) m.enc_th = std::thread([this] { enc_loop(); });
+  std::unique_lock<std::mutex> lk(m.enc_mu);
+  m.enc_target = std::max(m.enc_target, j);
+  m.enc_cv.notify_all();
+  m.enc_cv.wait(lk, [&] { return m.enc_err || (int)m.plan.next_enq > j || m.plan.pcm.empty(); });
+  if (m.enc_err) std::rethrow_exception(m.enc_err);
+}
+
+// issue the plan's next encode-ahead batch if the lookahead of segment j allows it: every group
+// of segments whose slots' previous occupants (j - S ...) have finished
+bool State::top_up_batch(int j) {
   Impl& m = *m_;
   const int N = (int)m.plan.pcm.size();
   // WDR_ENC_FIRST: windows in the first batch of a plan (A/B: 1 / 2 / 4 measured 491-493 /
   // 495 / 496 xRT on the 1-h bench, so a full batch stays the default); a batch never wraps
   // around the ring (its slots stay contiguous for the cross-K/V GEMM).  Encoder results do not
   // depend on the batch.
+  // With the encode-ahead thread, a plan's second batch is issued only once its first has been
+  // encoded: at the start of a run every chain waits for its first batch, and with all chains'
+  // look-ahead batches queued at once the first batches finished late (1-h bench, chain log:
+  // 0.58 -> 0.46 s per chain).  A first batch of 1 or 2 windows (WDR_ENC_FIRST) measured slower
+  // (570 / 580 vs 624 xRT: partial, ungraphed batches and a misaligned ring).
   static const int first = [] {
     const char* e = getenv("WDR_ENC_FIRST");
     const int v = e ? atoi(e) : kBatch;
     return std::max(1, std::min(kBatch, v));
   }();
-  while ((int)m.plan.next_enq < N) {
+  {
+    if ((int)m.plan.next_enq >= N) return false;
     const int g0 = (int)m.plan.next_enq;
     int g1 = std::min(N, g0 + (g0 == 0 ? first : kBatch));
     g1 = std::min(g1, (g0 / m.S + 1) * m.S);
-    if (g1 - 1 > j + enc_ahead(m.S) - 1) break;
+    if (g1 - 1 > j + enc_ahead(m.S) - 1) return false;
+    if (g0 == first && g0 > 0 && enc_thread_on() && std::this_thread::get_id() == m.enc_th.get_id())
+      WDR_HIP(hipEventSynchronize(m.slots[(g0 - 1) % m.S].ready));   // the first window encoded
     const int slot0 = g0 % m.S;
     for (int k = g0; k < g1; ++k) {
       Impl::Slot& sl = m.slots[k % m.S];
@@ -915,20 +1036,30 @@ void State::top_up(int j) {
         memcpy(sl.h_pcm, m.plan.pcm[k], (size_t)nk * 2);
         WDR_HIP(wdr_memcpy_async(sl.pcm.p, sl.h_pcm, (size_t)nk * 2, hipMemcpyHostToDevice, m.es));
         launch_i16_to_f32(sl.pcm.as<int16_t>(), nk, sl.x.as<float>(), m.es);
+        if (nk > sl.energy_cap) {
+          if (sl.h_energy) WDR_HIP(hipHostFree(sl.h_energy));
+          WDR_HIP(hipHostMalloc((void**)&sl.h_energy, (size_t)nk * 4, hipHostMallocDefault));
+          sl.energy_d = DevMem((size_t)nk * 4);
+          sl.energy_cap = nk;
+        }
+        launch_energy(sl.x.as<float>(), nk, sl.energy_d.as<float>(), m.es);
+        WDR_HIP(wdr_memcpy_async(sl.h_energy, sl.energy_d.p, (size_t)nk * 4, hipMemcpyDeviceToHost, m.es));
       }
+      sl.energy_n = nk;
       slot_mel(ctx_, m, sl, nk, m.es);
       Im2colMelArgs ia{sl.mel.as<float>(), m.n_mels, sl.n_fft_frames, sl.gmax.as<int>(), 0, m.kp1,
                        m.eb.im2col.as<f16>() + (size_t)(k - g0) * 3000 * m.kp1};
       launch_im2col_mel(ia, m.es);
     }
-    encoder_body(ctx_, m, m.eb, g1 - g0, m.xkv_ring.as<f16>() + (size_t)slot0 * m.xkv_slot_elems, m.es);
-    if (m.plan.detect_lang) {
-      // whisper.cpp's language detection (one SOT pass over window 0, argmax of the language
-      // logits) depends on nothing decoded, so it runs here, off the decode chain: the batch's
-      // windows as the rows of ONE decode step, each with its own cross-K/V slot and sequence
-      // (every window a one-row group: the arithmetic of decoder_prefill(SOT) on the decode stream)
+    // the batch's encoder + cross-K/V (+ language detection): whisper.cpp's language detection
+    // (one SOT pass over window 0, argmax of the language logits) depends on nothing decoded, so
+    // it runs here, off the decode chain: the batch's windows as the rows of ONE decode step,
+    // each with its own cross-K/V slot and sequence (every window a one-row group: the
+    // arithmetic of decoder_prefill(SOT) on the decode stream)
+    auto body = [&](RowBatch& tl, bool capturing) {
+      encoder_body(ctx_, m, m.eb, g1 - g0, m.xkv_ring.as<f16>() + (size_t)slot0 * m.xkv_slot_elems, m.es);
+      if (!m.plan.detect_lang) return;
       const int R = g1 - g0;
-      RowBatch& tl = *m.tlb;
       tl.clear();   // waits for the previous batch's table copy
       const int sot = ctx_.vocab.sot;
       for (int r = 0; r < R; ++r) {
@@ -941,17 +1072,63 @@ void State::top_up(int j) {
         tl.add(g);
       }
       RowsIO io = m.lb.io(ctx_, m.V);
-      tl.upload(io, m.es, true, true);
+      tl.upload(io, m.es, true, !capturing);
       rows_forward(ctx_, io, R, m.es);
       for (int r = 0; r < R; ++r)
         WDR_HIP(wdr_memcpy_async(m.h_lang + (size_t)((g0 + r) % m.S) * 100,
                                m.lb.logits.as<float>() + (size_t)r * m.V + sot + 1, 100 * 4,
                                hipMemcpyDeviceToHost, m.es));
+    };
+    const double t_el = now_s();
+    struct ElT {
+      double t0;
+      std::atomic<long long>& acc;
+      ~ElT() { acc += (long long)((now_s() - t0) * 1e9); }
+    } el_t{t_el, m.t_enc_launch};
+    static const bool enc_graph = !(getenv("WDR_ENC_GRAPH") && atoi(getenv("WDR_ENC_GRAPH")) == 0);
+    if (enc_graph && g1 - g0 == kBatch && !getenv("WDR_NO_GRAPH")) {
+      const bool f8 = ctx_.fp8_encoder.load();
+      const int key = slot0 * 4 + (f8 ? 2 : 0) + (m.plan.detect_lang ? 1 : 0);   // the batch's slots
+      Impl::EncGraph& eg = m.enc_graphs[key];
+      if (!eg.exec) {
+        if (f8) {   // lazily built weights: not inside the capture
+          (void)ctx_.fp8_layers();
+          (void)ctx_.fp8_xkv();
+        }
+        if (!eg.tl) eg.tl = std::make_unique<RowBatch>(kBatch, kBatch, 0);
+        hipGraph_t graph;
+        prof_capture(true);
+        WDR_HIP(hipStreamBeginCapture(m.es, hipStreamCaptureModeThreadLocal));
+        try {
+          body(*eg.tl, true);
+        } catch (...) {
+          hipGraph_t dead = nullptr;
+          (void)hipStreamEndCapture(m.es, &dead);
+          if (dead) (void)hipGraphDestroy(dead);
+          prof_capture(false);
+          throw;
+        }
+        prof_capture(false);
+        WDR_HIP(hipStreamEndCapture(m.es, &graph));
+        WDR_HIP(hipGraphInstantiate(&eg.exec, graph, nullptr, nullptr, 0));
+        WDR_HIP(hipGraphDestroy(graph));
+      }
+      std::mutex* mu = launch_lock();   // WDR_LAUNCH_LOCK (prof.h)
+      if (mu) mu->lock();
+      const hipError_t ge = hipGraphLaunch(eg.exec, m.es);
+      if (mu) mu->unlock();
+      WDR_HIP(ge);
+    } else {
+      body(*m.tlb, false);
     }
     for (int k = g0; k < g1; ++k) WDR_HIP(hipEventRecord(m.slots[k % m.S].ready, m.es));
-    m.plan.next_enq = g1;
-    times.windows += g1 - g0;
+    {
+      std::lock_guard<std::mutex> g(m.enc_mu);   // the chain reads next_enq under this lock
+      m.plan.next_enq = g1;
+    }
+    m.enc_windows += g1 - g0;
   }
+  return true;
 }
 
 // ------------------------------------------------------------------ decoder
@@ -1005,7 +1182,12 @@ void State::prefill_on(const int* toks, int n, int seq, bool want_logits, bool c
   tb.add(g);
   RowsIO io = B.io(ctx_, m.V);
   tb.upload(io, st, true, true);
-  rows_forward(ctx_, io, n, st);
+  if (capture && !want_logits && ctx_.aheads_per_layer.size() == (size_t)ctx_.model.hp.n_text_layer) {
+    // a DTW re-forward: the DtwQueue's pass (stops after the last alignment-head layer)
+    dtw_rows_forward(ctx_, io, n, capture_l_end(ctx_), st);
+  } else {
+    rows_forward(ctx_, io, n, st);
+  }
   if (st == s_) times.prefills++;
 }
 
@@ -1968,13 +2150,27 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
     }
   } release{m, s_, planned};
   int encoded_seek = -1;
+  // WDR_CHAIN_LOG=<file>: one line per full() call -- chain, job, wall at entry and exit (s), top_up ms,
+  // ready-wait ms, energy ms, decode ms (windows' decode loops), post ms (results, heuristic
+  // timestamps, DTW submit) -- where a chain spends the time between its batched steps
+  static FILE* clog = getenv("WDR_CHAIN_LOG") ? fopen(getenv("WDR_CHAIN_LOG"), "w") : nullptr;
+  static std::mutex clog_mu;
+  double c_top = 0, c_ready = 0, c_energy = 0, c_dec = 0, c_post = 0;
+  const double c_t0 = now_s();
+  m.t_fence = 0;
+  m.t_enc_launch = 0;
   if (planned) {
     top_up(job);
-    WDR_CHECK((int)m.plan.next_enq > job, "encode-ahead plan out of order");
+    c_top = now_s() - c_t0;
+    {
+      std::lock_guard<std::mutex> g(m.enc_mu);
+      WDR_CHECK((int)m.plan.next_enq > job, "encode-ahead plan out of order");
+    }
     m.cur = job % m.S;
     n = m.plan.n[job];
     WDR_HIP(hipEventSynchronize(m.slots[m.cur].ready));
     times.encode += now_s() - t_start;   // time the decoder waited on the encode-ahead stream
+    c_ready = now_s() - c_t0 - c_top;
     t_start = now_s();
     encoded_seek = 0;
   } else {
@@ -1983,7 +2179,10 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
   if (params.token_timestamps) {
     t_beg = t_last = tid_last = 0;
     energy.assign(n, 0.f);
-    if (n > 0) {
+    if (n > 0 && planned && m.slots[m.cur].energy_n == n) {
+      // computed on the encode-ahead stream before `ready` (top_up)
+      memcpy(energy.data(), m.slots[m.cur].h_energy, (size_t)n * 4);
+    } else if (n > 0) {
       if (n > m.energy_cap) {
         m.energy_d = DevMem((size_t)n * 4);
         m.energy_cap = n;
@@ -1994,6 +2193,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
   }
   WDR_HIP(hipStreamSynchronize(s_));
   times.mel += now_s() - t_start;
+  c_energy = now_s() - t_start;
   const int seek_start = 0;
   const int seek_end = 1 + (int)((n + 200 - 400) / 160);
   const int delta_min = 10;
@@ -2208,6 +2408,13 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
       if (success) break;
     }
     times.decode += now_s() - t_dec;
+    c_dec += now_s() - t_dec;
+    const double t_post = now_s();
+    struct PostT {
+      double t0;
+      double& acc;
+      ~PostT() { acc += now_s() - t0; }
+    } post_t{t_post, c_post};
     if (prompt_timed) {
       float ms = 0.f;
       if (hipEventElapsedTime(&ms, m.ev_p0, m.ev_p1) == hipSuccess) times.prompt_gpu += ms * 1e-3;
@@ -2243,6 +2450,13 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
     if (tokens_cur.size() > 1 && tokens_cur[tokens_cur.size() - 2].id < v.beg && tokens_cur.back().id > v.beg)
       seek_delta = std::min(seek_end - seek, 3000);
     seek += seek_delta;
+  }
+  if (clog) {
+    std::lock_guard<std::mutex> g(clog_mu);
+    fprintf(clog, "%d %d %.6f %.6f %.3f %.3f %.3f %.3f %.3f %.3f %.3f\n", chain, job, c_t0, now_s(), c_top * 1e3,
+            c_ready * 1e3, c_energy * 1e3, c_dec * 1e3, c_post * 1e3, m.t_fence.load() * 1e-6,
+            m.t_enc_launch.load() * 1e-6);
+    fflush(clog);
   }
   if (m.pend.on && planned && async_dtw) {
     // the last window's re-forward rides in the next segment's first request: this slot is
