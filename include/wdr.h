@@ -378,11 +378,6 @@ int wdr_dbg_proj(const uint16_t* a_f16, const uint16_t* w_f16, const float* bias
  * WDR_DBG_PROJ_ROWS the decoder-rows kernel (any M, per-row arithmetic independent of M) */
 #define WDR_DBG_PROJ_STEP 0x100
 #define WDR_DBG_PROJ_ROWS 0x200
-/* decoder-rows residual projection with the LN-out epilogue (rows_forward): x [M][N] f32 += a.w^T
- * + bias, and y = LayerNorm(x) (g, b) written by each 16-row tile's last workgroup (f16 -> f32);
- * y_ref = the same rows through k_layernorm (the separate LayerNorm launch it replaces) */
-int wdr_dbg_proj_ln(const uint16_t* a_f16, const uint16_t* w_f16, const float* bias, const float* g, const float* b,
-                    int32_t M, int32_t N, int32_t K, float* x /* [M][N] in / out */, float* y_out, float* y_ref);
 int wdr_dbg_attn(const uint16_t* q, const uint16_t* k, const uint16_t* v, int32_t Tq, int32_t Tk, int32_t n_head,
                  int32_t causal, float* out /* [Tq][n_head*64] */);
 // decode-step cross-attention over 1500 keys (beam groups / per-row slots; see engine.cpp)

@@ -128,28 +128,3 @@ def test_beam_chains_equal_single_chain(name, seconds, chains, monkeypatch):
     assert lang == lang1
     assert got == ref
     ctx.close()
-
-
-@pytest.mark.parametrize("name", ["tiny-test", "large-v3"])
-def test_layernorm_schedules_equal(name, monkeypatch):
-    """The decoder rows' LayerNorms written by the residual launches (LN-out: WDR_ROWS_LNO=1) and
-    the default schedule (in-kernel LN prologue up to 32 rows, a k_layernorm launch above), and the
-    cross-attention combine inside the partial launch (WDR_XATTN_FC=1) or as its own launch
-    (default), compute the same arithmetic: the multi-chain pipeline (steps, prompt prefills and
-    DTW re-forwards of > 32 rows in one launch) must give identical segments, words and DTW
-    times."""
-    syn = wdr.Synthetic(weight_std=0.02, emb_std=0.5, force_len_rate=3.3, disable_fallback=True)
-    ctx = wdr.WhisperContext(name, synthetic=syn, enable_dtw=True)
-    pcm, spurts = synth_speech(45.0, seed=7, n_speakers=1)
-    segs = _segs(pcm, spurts)
-    opts = wdr.TranscribeOptions(lang="auto", advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
-    ref, lang1 = _run(ctx, segs, opts, 4)
-    monkeypatch.setenv("WDR_ROWS_LNO", "1")
-    got, lang = _run(ctx, segs, opts, 4)
-    assert lang == lang1
-    assert got == ref
-    monkeypatch.setenv("WDR_XATTN_FC", "1")
-    got, lang = _run(ctx, segs, opts, 4)
-    assert lang == lang1
-    assert got == ref
-    ctx.close()

@@ -77,50 +77,6 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
-// One wave normalises one row (d <= 1280, d % 4 == 0): y = (x - mean) / sqrt(var + 1e-5) * g + b
-// as f16 -- ggml_norm's two passes in k_layernorm's exact arithmetic (lane l holds columns
-// 4 l + 256 j, j < 5), so every LayerNorm site of the decoder rows produces the same f16 bits.
-__device__ __forceinline__ void ln_row_wave(const float* xr, const float* g, const float* b, f16* yr, int d,
-                                            int lane) {
-  float v[5][4], gg[5][4], bb[5][4];
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    const int c = lane * 4 + j * 256;
-    const bool ok = c < d;
-    const int cc = ok ? c : 0;
-    const float4 q = *(const float4*)(xr + cc);
-    const float4 g4 = *(const float4*)(g + cc);
-    const float4 b4 = *(const float4*)(b + cc);
-    v[j][0] = ok ? q.x : 0.f; v[j][1] = ok ? q.y : 0.f; v[j][2] = ok ? q.z : 0.f; v[j][3] = ok ? q.w : 0.f;
-    gg[j][0] = g4.x; gg[j][1] = g4.y; gg[j][2] = g4.z; gg[j][3] = g4.w;
-    bb[j][0] = b4.x; bb[j][1] = b4.y; bb[j][2] = b4.z; bb[j][3] = b4.w;
-    s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
-  }
-  s = wave_sum(s);
-  const float mean = s / d;
-  float s2 = 0.f;
-#pragma unroll
-  for (int j = 0; j < 5; ++j)
-    if (lane * 4 + j * 256 < d)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float t = v[j][e] - mean;
-        s2 += t * t;
-      }
-  s2 = wave_sum(s2);
-  const float scale = 1.0f / sqrtf(s2 / d + 1e-5f);
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    const int c = lane * 4 + j * 256;
-    if (c >= d) continue;
-    f16x4 o;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = (f16)((v[j][e] - mean) * scale * gg[j][e] + bb[j][e]);
-    *(f16x4*)(yr + c) = o;
-  }
-}
-
 // Projection launchers (kernels/gemm.hip).
 struct ProjArgs {
   const f16* A; int lda;            // activations [M][K] f16
@@ -153,12 +109,6 @@ struct ProjArgs {
   int rows_mma = 0;
   // optional row map: A / ln_x row m is row_map[m] (logit rows gathered from the residual stream)
   const int* row_map = nullptr;
-  // LayerNorm of the updated residual rows (EPI_F32_RESID on the row kernel, rows_forward): the
-  // last workgroup to finish a 16-row tile normalises the tile's rows of `out` with (lno_g,
-  // lno_b) into lno_y [M][ldlno] f16 -- the next projection's input, without a LayerNorm launch.
-  // lno_cnt: one arrival counter per row tile, zero between launches (the last arriver resets it)
-  f16* lno_y = nullptr; int ldlno = 0; const float* lno_g = nullptr; const float* lno_b = nullptr;
-  int* lno_cnt = nullptr;
 };
 
 // Live kernel clock (csrc/prof.cpp): a launch the profiler samples carries ts -> {earliest wave

@@ -527,6 +527,7 @@ void CamModel::embed_batch(const int16_t* const* pcm, const size_t* n, int B, fl
   // row tables: offT[Bv+1] lenT[Bv] offT2[Bv+1] lenT2[Bv] ctxoff[Bv+1]
   const int tab_n = 5 * Bv + 3;
   if (w.tab_cap < Bv) {
+    std::lock_guard<std::recursive_mutex> g(hip_alloc_mutex());   // not during another thread's capture
     if (w.h_tab) (void)hipHostFree(w.h_tab);
     WDR_HIP(hipHostMalloc((void**)&w.h_tab, (size_t)tab_n * 4, hipHostMallocDefault));
     w.tab = DevMem((size_t)tab_n * 4);

@@ -2074,45 +2074,6 @@ int wdr_dbg_proj(const uint16_t* a16, const uint16_t* w16, const float* bias, in
   })
 }
 
-int wdr_dbg_proj_ln(const uint16_t* a16, const uint16_t* w16, const float* bias, const float* g, const float* b,
-                    int32_t M, int32_t N, int32_t K, float* x, float* y_out, float* y_ref) {
-  WDR_GUARD({
-    WDR_CHECK(M >= 1 && N >= 4 && K >= 32 && g && b && x && y_out && y_ref, "dbg_proj_ln: bad arguments");
-    DevMem da((size_t)M * K * 2), dw((size_t)N * K * 2), db(bias ? (size_t)N * 4 : 0), dx((size_t)M * N * 4);
-    DevMem dg((size_t)N * 4), dbb((size_t)N * 4), dy((size_t)M * N * 2), dyr((size_t)M * N * 2);
-    DevMem cnt((size_t)cdiv(M, 16) * 4);
-    WDR_HIP(hipMemcpy(da.p, a16, da.bytes, hipMemcpyHostToDevice));
-    WDR_HIP(hipMemcpy(dw.p, w16, dw.bytes, hipMemcpyHostToDevice));
-    if (bias) WDR_HIP(hipMemcpy(db.p, bias, db.bytes, hipMemcpyHostToDevice));
-    WDR_HIP(hipMemcpy(dx.p, x, dx.bytes, hipMemcpyHostToDevice));
-    WDR_HIP(hipMemcpy(dg.p, g, dg.bytes, hipMemcpyHostToDevice));
-    WDR_HIP(hipMemcpy(dbb.p, b, dbb.bytes, hipMemcpyHostToDevice));
-    WDR_HIP(hipMemset(cnt.p, 0, cnt.bytes));
-    ProjArgs a{da.as<f16>(), K, dw.as<f16>(), K, bias ? db.as<float>() : nullptr, dx.p, N, nullptr, 0, M, N, K,
-               EPI_F32_RESID};
-    a.rows_mma = 1;
-    a.lno_y = dy.as<f16>();
-    a.ldlno = N;
-    a.lno_g = dg.as<float>();
-    a.lno_b = dbb.as<float>();
-    a.lno_cnt = cnt.as<int>();
-    launch_proj(a, nullptr);
-    launch_layernorm(dx.as<float>(), N, dg.as<float>(), dbb.as<float>(), dyr.as<f16>(), N, M, N, nullptr);
-    WDR_HIP(hipDeviceSynchronize());
-    WDR_HIP(hipMemcpy(x, dx.p, dx.bytes, hipMemcpyDeviceToHost));
-    std::vector<f16> h((size_t)M * N);
-    WDR_HIP(hipMemcpy(h.data(), dy.p, h.size() * 2, hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < h.size(); ++i) y_out[i] = (float)h[i];
-    WDR_HIP(hipMemcpy(h.data(), dyr.p, h.size() * 2, hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < h.size(); ++i) y_ref[i] = (float)h[i];
-    // the arrival counters must be back at zero (the last workgroup of every tile resets its own)
-    std::vector<int> hc(cdiv(M, 16));
-    WDR_HIP(hipMemcpy(hc.data(), cnt.p, cnt.bytes, hipMemcpyDeviceToHost));
-    for (int c : hc) WDR_CHECK(c == 0, "dbg_proj_ln: an LN-out counter was not reset");
-    return 0;
-  })
-}
-
 int wdr_dbg_attn(const uint16_t* q, const uint16_t* k, const uint16_t* v, int32_t Tq, int32_t Tk, int32_t H,
                  int32_t causal, float* out) {
   WDR_GUARD({

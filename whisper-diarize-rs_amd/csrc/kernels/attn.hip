@@ -295,33 +295,7 @@ constexpr int XA_KC = 64, XA_NS = 24;
 // G: the largest group a launch holds -- 1 for the greedy batched step (every row its own
 // group), which keeps the kernel at <= 64 VGPRs so a workgroup still fits on a CU beside an
 // encoder GEMM tile (k_gemm4: 2 x 224 of the SIMD's 512)
-// one (row, head) of the combine inside the partial launch (FC): lane d merges dimension d over
-// the NS chunk partials in k_xattn_combine's arithmetic (the same reductions, the sum over c in
-// order), its loads in groups of 8 to bound the fused kernel's registers
-template <int NS>
-__device__ __forceinline__ void xattn_combine_row(const XAttnArgs& a, int r, int h, int d) {
-  float2 ml = make_float2(-INFINITY, 0.f);
-  if (d < NS) ml = a.part_ml[((long long)d * a.R + r) * a.n_head + h];
-  const float M = wave_max(ml.x);
-  const float w = (d < NS && ml.x != -INFINITY) ? __expf(ml.x - M) : 0.f;
-  const float L = wave_sum(ml.y * w);
-  const float* pb = a.part_o + ((long long)r * a.n_head + h) * 64 + d;
-  const long long cs = (long long)a.R * a.n_head * 64;
-  float acc = 0.f;
-#pragma unroll 1
-  for (int c0 = 0; c0 < NS; c0 += 8) {
-    float po[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) po[c] = c0 + c < NS ? pb[(c0 + c) * cs] : 0.f;
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-      if (c0 + c < NS) acc += po[c] * __shfl(w, c0 + c, 64);
-  }
-  a.o[(long long)r * a.ldo + h * 64 + d] = (f16)(acc / L);
-  if (a.ml_out && d == 0) a.ml_out[(long long)r * a.n_head + h] = make_float2(M, L);
-}
-
-template <bool ROWS, int G, bool FC = false>
+template <bool ROWS, int G>
 __global__ __launch_bounds__(256) void k_xattn_partial(XAttnArgs a) {
   ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
   __shared__ __attribute__((aligned(16))) f16 Vs[XA_KC * 64];
@@ -391,53 +365,15 @@ __global__ __launch_bounds__(256) void k_xattn_partial(XAttnArgs a) {
   for (int e = tid; e < nr * 64; e += 256) {
     const int j = e >> 6, dd = e & 63;
     const long long cr = (long long)c * a.R + r0 + j;
-    const float po = pv[j][0][dd] + pv[j][1][dd] + pv[j][2][dd] + pv[j][3][dd];
-    const float2 pml = make_float2(mx[j], red[1][j][0] + red[1][j][1] + red[1][j][2] + red[1][j][3]);
-    if constexpr (FC) {   // write-through (sc1): read by the group's last arriver in this launch
-      __hip_atomic_store(a.part_o + (cr * a.n_head + h) * 64 + dd, po, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (dd == 0) {
-        float* ml = (float*)(a.part_ml + cr * a.n_head + h);
-        __hip_atomic_store(ml, pml.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(ml + 1, pml.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    } else {
-      a.part_o[(cr * a.n_head + h) * 64 + dd] = po;
-      if (dd == 0) a.part_ml[cr * a.n_head + h] = pml;
-    }
-  }
-  if constexpr (FC) {
-    // in-launch combine (cdna_hip_programming.md: sc1 slabs, relaxed ticket, one acquire): the
-    // last of the XA_NS chunk workgroups of this (group, head) merges the group's rows
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
-    __syncthreads();
-    int* flag = (int*)&red[0][0][0];
-    int* ticket = a.cnt + (long long)blockIdx.z * a.n_head + h;
-    if (tid == 0)
-      *flag = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
-    __syncthreads();
-    if (!*flag) return;
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-#pragma unroll 1
-    for (int j = wid; j < nr; j += 4) xattn_combine_row<XA_NS>(a, r0 + j, h, lane);
-    if (tid == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a.part_o[(cr * a.n_head + h) * 64 + dd] = pv[j][0][dd] + pv[j][1][dd] + pv[j][2][dd] + pv[j][3][dd];
+    if (dd == 0)
+      a.part_ml[cr * a.n_head + h] = make_float2(mx[j], red[1][j][0] + red[1][j][1] + red[1][j][2] + red[1][j][3]);
   }
 }
 
-// ROWS_OF_TILES: only the rows of the MFMA tiles (blockIdx.x = tile * 128 + i), the VALU groups
-// having been combined inside their partial launch
-template <int NS, bool ROWS_OF_TILES = false>
+template <int NS>
 __global__ __launch_bounds__(64) void k_xattn_combine(XAttnArgs a) {
-  int r = blockIdx.x;
-  if constexpr (ROWS_OF_TILES) {
-    const int4 t = a.tiles[r >> 7];
-    if ((r & 127) >= t.y) return;
-    r = t.x + (r & 127);
-  }
-  const int h = blockIdx.y, d = threadIdx.x;
+  const int r = blockIdx.x, h = blockIdx.y, d = threadIdx.x;
   float po[NS];
 #pragma unroll
   for (int c = 0; c < NS; ++c) po[c] = a.part_o[(((long long)c * a.R + r) * a.n_head + h) * 64 + d];
@@ -556,25 +492,19 @@ void launch_xattn_rows(const XAttnArgs& a, hipStream_t s) {
   WDR_CHECK(a.row_k && a.R >= 1 && (a.n_vgrp == 0 || (a.grp && a.lead)) && (a.n_tiles == 0 || a.tiles),
             "cross-attention rows: bad tables");
   const double kv = (double)a.Tk * a.n_head * 64 * 2 * 2;
-  const bool fc = a.cnt != nullptr;
   if (a.n_vgrp > 0) {
     const double flops = (double)a.R * a.Tk * a.n_head * 64 * 4;
-    const dim3 g(XA_NS, a.n_head, a.n_vgrp);
-    if (a.vgrp_max <= 1) {
-      if (fc) wdr_launch(PROF_XATTN, a.n_vgrp * kv, flops, k_xattn_partial<true, 1, true>, g, dim3(256), 0, s, a);
-      else wdr_launch(PROF_XATTN, a.n_vgrp * kv, flops, k_xattn_partial<true, 1>, g, dim3(256), 0, s, a);
-    } else {
-      if (fc) wdr_launch(PROF_XATTN, a.n_vgrp * kv, flops, k_xattn_partial<true, XATTN_GRP_MAX, true>, g, dim3(256),
-                         0, s, a);
-      else wdr_launch(PROF_XATTN, a.n_vgrp * kv, flops, k_xattn_partial<true, XATTN_GRP_MAX>, g, dim3(256), 0, s, a);
-    }
+    if (a.vgrp_max <= 1)
+      wdr_launch(PROF_XATTN, a.n_vgrp * kv, flops, k_xattn_partial<true, 1>, dim3(XA_NS, a.n_head, a.n_vgrp),
+                 dim3(256), 0, s, a);
+    else
+      wdr_launch(PROF_XATTN, a.n_vgrp * kv, flops, k_xattn_partial<true, XATTN_GRP_MAX>,
+                 dim3(XA_NS, a.n_head, a.n_vgrp), dim3(256), 0, s, a);
   }
   if (a.n_tiles > 0)
     wdr_launch(PROF_XATTN, a.n_tiles * kv, (double)a.n_tiles * 128 * a.Tk * a.n_head * 64 * 4, k_xattn_mma,
                dim3(XA_NS, a.n_head, a.n_tiles), dim3(256), 0, s, a);
-  if (!fc) WDR_KLAUNCH(k_xattn_combine<XA_NS>, dim3(a.R, a.n_head), dim3(64), 0, s, a);
-  else if (a.n_tiles > 0)
-    WDR_KLAUNCH((k_xattn_combine<XA_NS, true>), dim3(a.n_tiles * 128, a.n_head), dim3(64), 0, s, a);
+  WDR_KLAUNCH(k_xattn_combine<XA_NS>, dim3(a.R, a.n_head), dim3(64), 0, s, a);
   WDR_HIP(hipGetLastError());
 }
 

@@ -323,31 +323,6 @@ void launch_embed(const f16* E, const float* P, const int* tok, const int* pos, 
   WDR_HIP(hipGetLastError());
 }
 
-// token + position embedding of 4 rows per workgroup (one wave per row), with the first layer's
-// LayerNorm of the row written to y: the f32 values are the ones k_embed stores, normalised in
-// registers with ln_row_wave's arithmetic (k_layernorm's), so y equals LN(x) bit for bit
-__global__ __launch_bounds__(256) void k_embed_ln(const f16* E, const float* P, const int* tok, const int* pos, int R,
-                                                  int d, float* x, const float* g, const float* b, f16* y, int ldy) {
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (r >= R) return;
-  const int t = tok[r], p = pos[r];
-  float* xr = x + (long long)r * d;
-  for (int c = lane * 4; c < d; c += 256) {
-    const f16x4 e = *(const f16x4*)(E + (long long)t * d + c);
-    const float4 q = *(const float4*)(P + (long long)p * d + c);
-    *(float4*)(xr + c) = make_float4((float)e[0] + q.x, (float)e[1] + q.y, (float)e[2] + q.z, (float)e[3] + q.w);
-  }
-  // the wave re-reads its own stores (same wave, program order: no fence needed)
-  ln_row_wave(xr, g, b, y + (long long)r * ldy, d, lane);
-}
-
-void launch_embed_ln(const f16* E, const float* P, const int* tok, const int* pos, int R, int d, float* x,
-                     const float* g, const float* b, f16* y, int ldy, hipStream_t s) {
-  WDR_CHECK(d % 4 == 0 && d <= 1280 && ldy % 4 == 0, "embed + LayerNorm: unsupported width");
-  WDR_KLAUNCH(k_embed_ln, dim3(cdiv(R, 4)), dim3(256), 0, s, E, P, tok, pos, R, d, x, g, b, y, ldy);
-  WDR_HIP(hipGetLastError());
-}
-
 __global__ void k_kv_scatter(const f16* qkv, int ldqkv, int d, const int* row_seq, const int* row_pos, f16* kc,
                              f16* vc, long long seq_stride) {
   const int r = blockIdx.x;

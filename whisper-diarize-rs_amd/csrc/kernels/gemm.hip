@@ -1647,12 +1647,7 @@ __global__ __launch_bounds__(256) void k_gemv(ProjArgs a) {
 // first (k_layernorm's arithmetic, so the f16 operands are bit-identical to the unfused path;
 // row stride K + 8 halfs keeps the 16-row fragment reads conflict-free) -- which removes the
 // separate LayerNorm launch and its f16 round trip from the prefill / DTW passes.
-// LNO (EPI_F32_RESID, MT = NT = 1, rows_forward): the updated residual values are stored
-// write-through (sc1) and the workgroup takes a ticket on its row tile's counter; the last of the
-// gridDim.x column tiles to arrive acquires (agent scope) and normalises the tile's rows into
-// lno_y with ln_row_wave -- the LayerNorm launch that would follow, in the same arithmetic
-// (cdna_hip_programming.md, in-launch split-K reduction: sc1 slabs + relaxed ticket + acquire).
-template <int EPI, int MT, int NT, int W = 4, bool LN = false, int UU = 0, bool LNO = false>
+template <int EPI, int MT, int NT, int W = 4, bool LN = false, int UU = 0>
 __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
   __shared__ float red[W][MT][NT][4][64];
   extern __shared__ __attribute__((aligned(16))) f16 xln[];   // LN: [16*MT][K + 8]
@@ -1767,42 +1762,6 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[wid][i][j][r][lane] = acc[i][j][r];
   __syncthreads();
-  if constexpr (LNO) {
-    static_assert(EPI == EPI_F32_RESID && MT == 1 && NT == 1, "LN-out epilogue: residual rows, one tile");
-    if (threadIdx.x < 256) {
-      const int l = threadIdx.x & 63, r = threadIdx.x >> 6;
-      float v = 0.f;
-#pragma unroll
-      for (int w = 0; w < W; ++w) v += red[w][0][0][r][l];
-      const int row = m0 + (l >> 4) * 4 + r, col = n0 + (l & 15);
-      if (row < a.M && col < a.N) {
-        if (a.bias) v += a.bias[col];
-        float* o = (float*)a.out + (size_t)row * a.ldo + col;
-        __hip_atomic_store(o, *o + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
-    __syncthreads();
-    int* flag = (int*)&red[0][0][0][0][0];
-    if (threadIdx.x == 0)
-      *flag = __hip_atomic_fetch_add(a.lno_cnt + blockIdx.y, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-              (int)gridDim.x - 1;
-    __syncthreads();
-    if (!*flag) return;
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    for (int i = wid; i < 16; i += W) {
-      const int row = m0 + i;
-      if (row < a.M)
-        ln_row_wave((const float*)a.out + (size_t)row * a.ldo, a.lno_g, a.lno_b, a.lno_y + (size_t)row * a.ldlno,
-                    a.N, lane);
-    }
-    if (threadIdx.x == 0) __hip_atomic_store(a.lno_cnt + blockIdx.y, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
   for (int e = threadIdx.x; e < MT * NT * 4 * 64; e += W * 64) {
     const int l = e & 63, r = (e >> 6) & 3, j = (e >> 8) % NT, i = (e >> 8) / NT;
     float v = 0.f;
@@ -2186,20 +2145,6 @@ static void launch_rows_epi(const ProjArgs& a, hipStream_t s) {
     // one 16-row tile per workgroup: the row tiles of a column tile re-read its weights from L2.
     // K > 2048 (fc2): 16 waves, each wave's 10 k-steps as ONE batch of loads (8 waves took three
     // dependent batches: fc2 at 1 row 9.8 us against 5.4 us on the GEMV)
-    if constexpr (EPI == EPI_F32_RESID) {
-      if (a.lno_y) {
-        // residual rows + the next LayerNorm by each row tile's last workgroup (k_skinny LNO)
-        WDR_CHECK(!ln && a.lno_cnt && a.lno_g && a.lno_b && a.N <= 1280 && a.N % 4 == 0 && a.ldo % 4 == 0 &&
-                      a.ldlno % 4 == 0,
-                  "row projection LN-out: residual rows of width <= 1280");
-        dim3 grid(cdiv(a.N, 16), mt);
-        if (a.K > 2048 && rows_w16k())
-          wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 16, false, 12, true>, grid, dim3(1024), 0, s, a);
-        else
-          wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 8, false, 0, true>, grid, dim3(512), 0, s, a);
-        return;
-      }
-    }
     if (a.K > 2048) {
       WDR_CHECK(!ln, "row projection: LN prologue needs K <= 1280");
       dim3 grid(cdiv(a.N, 16), mt), blk(1024);

@@ -35,8 +35,6 @@ void launch_synth_fill(void* dst, long long rows, int src_cols, int dst_cols, ui
 void launch_layernorm(const float* x, int ldx, const float* g, const float* b, f16* y, int ldy, int rows, int d,
                       hipStream_t s);
 void launch_embed(const f16* E, const float* P, const int* tok, const int* pos, int R, int d, float* x, hipStream_t s);
-void launch_embed_ln(const f16* E, const float* P, const int* tok, const int* pos, int R, int d, float* x,
-                     const float* g, const float* b, f16* y, int ldy, hipStream_t s);
 void launch_kv_scatter(const f16* qkv, int ldqkv, int d, const int* row_seq, const int* row_pos, int R, f16* kc, f16* vc,
                        long long seq_stride, hipStream_t s);
 
@@ -142,11 +140,6 @@ struct XAttnArgs {
   int n_vgrp = 0;                     // VALU groups (lead list length); 0 with tiles: none
   int vgrp_max = 1;                   // largest VALU group (1: the 47-VGPR one-row kernel)
   float2* ml_out = nullptr;           // combine: (max, sum) per (row, head) for the DTW capture
-  // rows_forward: the VALU groups' combine inside the partial launch -- the last of a (group,
-  // head)'s XA_NS chunk workgroups to arrive merges the group's rows (k_xattn_combine's
-  // arithmetic).  One ticket per (leader index, head), zero between launches.  Null: a separate
-  // combine launch.
-  int* cnt = nullptr;
 };
 constexpr int XATTN_GRP_MAX = 8;   // rows sharing one K/V without row_k
 inline unsigned long long* prof_attach(XAttnArgs& a) { return a.ts = prof_slot(); }

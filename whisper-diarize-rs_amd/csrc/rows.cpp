@@ -18,6 +18,7 @@ size_t up16(size_t x) { return (x + 15) & ~size_t(15); }
 }  // namespace
 
 RowBatch::RowBatch(int cr, int cl, int cc) : cap_rows(cr), cap_logits(cl), cap_caps(cc) {
+  std::lock_guard<std::recursive_mutex> g(hip_alloc_mutex());
   // worst-case packed size: 5 ints per row, lead / lrow / crow / cstride, tiles, pointers
   bytes_ = up16((size_t)cr * 4) * 5 + up16((size_t)cr * 4) + up16((size_t)cl * 4) + 2 * up16((size_t)cc * 4) +
            up16((size_t)(cr / 8 + 2 + cr / kTileRows + 2) * 16) + up16((size_t)cr * 8) + up16((size_t)cc * 8) + 256;
@@ -27,6 +28,7 @@ RowBatch::RowBatch(int cr, int cl, int cc) : cap_rows(cr), cap_logits(cl), cap_c
 }
 
 RowBatch::~RowBatch() {
+  std::lock_guard<std::recursive_mutex> g(hip_alloc_mutex());
   if (pending_) (void)hipEventSynchronize(ev_);
   if (ev_) (void)hipEventDestroy(ev_);
   if (h_) (void)hipHostFree(h_);
@@ -120,6 +122,7 @@ void RowBatch::upload(RowsIO& io, hipStream_t s, bool copy, bool track) {
 }
 
 void RowsBufs::alloc(int r, int lr, int d, int H, int V) {
+  std::lock_guard<std::recursive_mutex> g(hip_alloc_mutex());
   rows = r;
   logit_rows = lr;
   xd = DevMem((size_t)r * d * 4);
@@ -132,13 +135,6 @@ void RowsBufs::alloc(int r, int lr, int d, int H, int V) {
   part_ml = DevMem((size_t)24 * r * H * sizeof(float2));
   ml = DevMem((size_t)r * H * sizeof(float2));
   logits = DevMem((size_t)std::max(1, lr) * V * 4);
-  // LN-out tickets (k_skinny LNO): zero once here, reset by each tile's last workgroup
-  const size_t nc = (size_t)3 * kRowsMaxLayers * cdiv(r, 16);
-  lncnt = DevMem(nc * 4);
-  WDR_HIP(hipMemset(lncnt.p, 0, nc * 4));
-  // cross-attention combine tickets, one per (VALU group leader, head): reset by the last arriver
-  xcnt = DevMem((size_t)r * H * 4);
-  WDR_HIP(hipMemset(xcnt.p, 0, (size_t)r * H * 4));
 }
 
 RowsIO RowsBufs::io(const Context& ctx, int V) const {
@@ -154,8 +150,6 @@ RowsIO RowsBufs::io(const Context& ctx, int V) const {
   o.ml = ml.as<float2>();
   o.logits = logits.as<float>();
   o.ldlogits = V;
-  o.lncnt = lncnt.as<int>();
-  o.xcnt = xcnt.as<int>();
   o.kc = ctx.kv_k.as<f16>();
   o.vc = ctx.kv_v.as<f16>();
   o.layer_stride = ctx.kv_layer_stride;
@@ -169,36 +163,21 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, in
   const int d = hp.n_text_state, L = hp.n_text_layer, H = hp.n_text_head;
   const float scale = 1.0f / 8.0f;
   WDR_CHECK(R >= 1 && io.tok && io.xkv, "rows forward: no rows / tables");
-  // the projections' input rows LayerNorm(x) (ln1 / ln2 / ln3 / the final LN), f16 in io.hd:
-  //  * inside the row kernel up to 32 rows (every workgroup normalises its own row tiles), above
-  //    that one k_layernorm launch (default);
-  //  * WDR_ROWS_LNO=1: LN-out -- written by the launch that updates x (k_embed_ln, and each
-  //    residual projection's last workgroup per 16-row tile: k_skinny LNO), no LayerNorm launch.
-  //    Measured slower inside the pipeline (1-h bench 529 vs 557 xRT, profiles/r03/ab_lno_xfc.txt):
-  //    the in-launch hand-off (sc1 stores, ticket, acquire) costs more than the launch it saves.
-  // Every form is k_layernorm's arithmetic, so the f16 inputs (and every result) are identical.
-  // (read per call: tests/test_gpu_chains.py compares the schedules in one process)
-  const char* lno_env = getenv("WDR_ROWS_LNO");
-  const bool lno = lno_env && atoi(lno_env) != 0;
+  // the projection's input rows LayerNorm(x): inside the row kernel up to 32 rows (every
+  // workgroup normalises its own row tiles), above that one k_layernorm launch into io.hd -- the
+  // same arithmetic either way.  Fused at every row count the redundant per-column-tile LN cost
+  // more than the launch it saves (1-h trace: decoder rows class 4.98 vs 4.83 s over two runs);
+  // WDR_ROWS_LN_SPLIT=0 fuses at every count (A/B).  (Writing LN(x) from the residual launch's
+  // last workgroup per row tile -- an in-launch hand-off -- measured slower still: 529 vs 557 xRT,
+  // profiles/r03/ab_lno_xfc.txt.)
   static const bool ln_split = !(getenv("WDR_ROWS_LN_SPLIT") && atoi(getenv("WDR_ROWS_LN_SPLIT")) == 0);
-  WDR_CHECK(!lno || L <= kRowsMaxLayers, "rows forward: more decoder layers than LN-out counters");
-  // WDR_XATTN_FC=1: the VALU groups' cross-attention combine inside the partial launch
-  // (k_xattn_partial FC: the last of a (group, head)'s chunk workgroups merges its rows); default
-  // a separate k_xattn_combine launch -- the fused form measured slower in the pipeline (529 ->
-  // 492 xRT: an acquire per (group, head) episode).  Same arithmetic; read per call.
-  const char* xfc_env = getenv("WDR_XATTN_FC");
-  const bool xfc = xfc_env && atoi(xfc_env) != 0;
   const bool fuse_ln = R <= 32 || !ln_split;
-  const int ntile = cdiv(R, 16);
   auto P = [&](const f16* A, int lda, const f16* W, const float* b, void* out, int ldo, int N, int K, int epi,
                const float* lng = nullptr, const float* lnb = nullptr) {
     ProjArgs a{A, lda, W, K, b, out, ldo, nullptr, 0, R, N, K, epi};
     a.rows_mma = 1;
     if (lng) {
-      if (lno) {
-        a.A = io.hd;   // LN(x) already there (LN-out of the launch that updated x)
-        a.lda = d;
-      } else if (fuse_ln) {
+      if (fuse_ln) {
         a.ln_x = io.xd;
         a.ldln = d;
         a.ln_g = lng;
@@ -211,19 +190,7 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, in
     }
     return a;
   };
-  // a residual projection that also leaves LN(x) (g, b) in io.hd: counters [site][layer][tile]
-  auto LNO = [&](ProjArgs a, int site, int l, const float* g, const float* b) {
-    if (!lno) return a;
-    a.lno_y = io.hd;
-    a.ldlno = d;
-    a.lno_g = g;
-    a.lno_b = b;
-    a.lno_cnt = io.lncnt + ((size_t)site * kRowsMaxLayers + l) * ntile;
-    return a;
-  };
-  if (lno) launch_embed_ln(md.tok_emb, md.dec_pos, io.tok, io.pos, R, d, io.xd, md.dec[0].ln1_g, md.dec[0].ln1_b,
-                           io.hd, d, s);
-  else launch_embed(md.tok_emb, md.dec_pos, io.tok, io.pos, R, d, io.xd, s);
+  launch_embed(md.tok_emb, md.dec_pos, io.tok, io.pos, R, d, io.xd, s);
   const bool any_cap = io.n_cap > 0 && ctx.aheads_per_layer.size() == (size_t)L;
   int cap_slot0 = 0;
   for (int l = 0; l < L; ++l) {
@@ -242,7 +209,7 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, in
     // predecessors' keys: causal by position)
     DecSelfArgs sa{io.qkvd, 3 * d, kc, vc, io.seq_stride, d, io.seq, io.pos, io.attd, d, scale};
     launch_dec_self_attn(sa, R, H, s);
-    launch_proj(LNO(P(io.attd, d, e.w_o, e.b_o, io.xd, d, d, d, EPI_F32_RESID), 0, l, e.ln2_g, e.ln2_b), s);
+    launch_proj(P(io.attd, d, e.w_o, e.b_o, io.xd, d, d, d, EPI_F32_RESID), s);
     launch_proj(P(nullptr, d, e.w_xq, e.b_xq, io.qx, d, d, d, EPI_F16, e.ln2_g, e.ln2_b), s);
     XAttnArgs xa{io.qx, d, nullptr, nullptr, 64, XKV_T, R, H, scale, io.part_o, io.part_ml, io.attd, d};
     xa.row_k = io.xkv;
@@ -260,7 +227,6 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, in
     xa.n_tiles = io.n_tiles;
     const bool cap_layer = any_cap && !ctx.aheads_per_layer[l].empty();
     xa.ml_out = cap_layer ? io.ml : nullptr;
-    if (xfc) xa.cnt = io.xcnt;
     launch_xattn_rows(xa, s);
     if (cap_layer) {
       CaptureRowsArgs ca{io.qx, d, io.xkv, xkv_k_off(l, H), XKV_HS, io.ml,
@@ -270,22 +236,15 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, in
     }
     if (ctx.aheads_per_layer.size() == (size_t)L) cap_slot0 += (int)ctx.aheads_per_layer[l].size();
     if (l + 1 >= l_stop) return;   // a DTW pass: nothing after this layer's capture matters
-    launch_proj(LNO(P(io.attd, d, e.w_xo, e.b_xo, io.xd, d, d, d, EPI_F32_RESID), 1, l, e.ln3_g, e.ln3_b), s);
+    launch_proj(P(io.attd, d, e.w_xo, e.b_xo, io.xd, d, d, d, EPI_F32_RESID), s);
     launch_proj(P(nullptr, d, e.w_fc1, e.b_fc1, io.mlpd, 4 * d, 4 * d, d, EPI_F16_GELU, e.ln3_g, e.ln3_b), s);
-    // fc2 leaves the next layer's ln1 -- after the last layer the final LN of the logit rows
-    const bool last = l + 1 == L;
-    launch_proj(LNO(P(io.mlpd, 4 * d, e.w_fc2, e.b_fc2, io.xd, d, d, 4 * d, EPI_F32_RESID), 2, l,
-                    last ? md.ln_g : md.dec[l + 1].ln1_g, last ? md.ln_b : md.dec[l + 1].ln1_b),
-                s);
+    launch_proj(P(io.mlpd, 4 * d, e.w_fc2, e.b_fc2, io.xd, d, d, 4 * d, EPI_F32_RESID), s);
   }
   if (io.n_logit > 0) {
     // final LayerNorm + logits of the logit rows only, gathered by lrow (compact output)
     ProjArgs a{nullptr, d, md.tok_emb, d, nullptr, io.logits, io.ldlogits, nullptr, 0, io.n_logit, hp.n_vocab, d, EPI_F32};
     a.rows_mma = 1;
-    if (lno) {
-      a.A = io.hd;   // every row's final LN from the last fc2; the logit rows gathered by lrow
-      a.row_map = io.lrow;
-    } else if (io.n_logit <= 32 || !ln_split) {
+    if (io.n_logit <= 32 || !ln_split) {
       a.ln_x = io.xd;
       a.ldln = d;
       a.ln_g = md.ln_g;

@@ -74,8 +74,6 @@ struct RowsIO {
   float* xd; f16* hd; f16* qkvd; f16* attd; f16* qx; f16* mlpd;
   float* part_o; float2* part_ml; float2* ml;
   float* logits; int ldlogits;                       // [n_logit][ldlogits]
-  int* lncnt;                                        // LN-out arrival counters [3][kMaxLayers][row tiles]
-  int* xcnt;                                         // fused cross-attention combine tickets [rows][H]
   f16* kc; f16* vc; long long layer_stride, seq_stride;   // KV pool (layer 0) and its strides
   // tables (device; RowBatch::upload)
   const int* tok = nullptr; const int* pos = nullptr; const int* seq = nullptr;
@@ -88,9 +86,8 @@ struct RowsIO {
 };
 
 // working-set buffers of a rows forward for up to `rows` rows and `logit_rows` logit rows
-constexpr int kRowsMaxLayers = 32;   // decoder layers the LN-out counters cover (whisper: <= 32)
 struct RowsBufs {
-  DevMem xd, hd, qkvd, attd, qx, mlpd, part_o, part_ml, ml, logits, lncnt, xcnt;
+  DevMem xd, hd, qkvd, attd, qx, mlpd, part_o, part_ml, ml, logits;
   int rows = 0, logit_rows = 0;
   void alloc(int rows, int logit_rows, int d, int H, int V);
   RowsIO io(const Context& ctx, int V) const;   // tables unset

@@ -30,6 +30,9 @@ bool hparams_for(const std::string& name, HParams* hp);
 
 std::vector<std::pair<int, int>> alignment_heads_for(const std::string& model_name);
 
+// serialises device / pinned allocation and free with hipGraph captures (whisper_ctx.cpp)
+std::recursive_mutex& hip_alloc_mutex();
+
 struct DevMem {
   void* p = nullptr;
   size_t bytes = 0;

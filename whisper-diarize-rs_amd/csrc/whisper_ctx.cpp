@@ -95,15 +95,34 @@ std::vector<std::pair<int, int>> alignment_heads_for(const std::string& n) {
 }
 
 // ------------------------------------------------------------------ device memory
+// Allocation / free and hipGraph capture are serialised by one process-wide mutex: several host
+// threads capture graphs (step batchers, encode-ahead threads) while others run, and a
+// synchronising call (hipFree, a legacy-stream memset, pinned host allocation) issued by one
+// thread while another captures invalidates that capture on ROCm 7.2 ("operation would make the
+// legacy stream depend on a capturing blocking stream"), whatever the capture mode.
+std::recursive_mutex& hip_alloc_mutex() {
+  static std::recursive_mutex mu;
+  return mu;
+}
+
 DevMem::DevMem(size_t n) : bytes(n) {
-  if (n) WDR_HIP(hipMalloc(&p, n));
+  if (n) {
+    std::lock_guard<std::recursive_mutex> g(hip_alloc_mutex());
+    WDR_HIP(hipMalloc(&p, n));
+  }
 }
 DevMem::~DevMem() {
-  if (p) (void)hipFree(p);
+  if (p) {
+    std::lock_guard<std::recursive_mutex> g(hip_alloc_mutex());
+    (void)hipFree(p);
+  }
 }
 DevMem& DevMem::operator=(DevMem&& o) noexcept {
   if (this != &o) {
-    if (p) (void)hipFree(p);
+    if (p) {
+      std::lock_guard<std::recursive_mutex> g(hip_alloc_mutex());
+      (void)hipFree(p);
+    }
     p = o.p;
     bytes = o.bytes;
     o.p = nullptr;
@@ -424,6 +443,7 @@ struct State::Impl {
     std::unique_ptr<RowBatch> tl;
   };
   std::map<int, EncGraph> enc_graphs;
+  hipStream_t es_cap = nullptr;   // the stream those graphs are captured on (never launched on)
   // WDR_CHAIN_LOG: DTW-queue waits / encoder launch host time (ns; the encode-ahead thread adds too)
   std::atomic<long long> t_fence{0}, t_enc_launch{0};
   // the encode-ahead host thread: issues the plan's batches (top_up_batch) up to the lookahead of
@@ -668,6 +688,7 @@ State::~State() {
     if (m_->es) (void)hipStreamSynchronize(m_->es);
     for (auto& g : m_->enc_graphs)
       if (g.second.exec) (void)hipGraphExecDestroy(g.second.exec);
+    if (m_->es_cap) (void)hipStreamDestroy(m_->es_cap);
     (void)hipHostFree(m_->h_tok);
     (void)hipHostFree(m_->h_ctl);
     (void)hipHostFree(m_->h_times);
@@ -725,6 +746,32 @@ static void slot_reserve_x(State::Impl::Slot& sl, int n) {
   if (n > sl.x_cap) {
     sl.x = DevMem((size_t)std::max(n, 1) * 4);
     sl.x_cap = n;
+  }
+}
+
+// a slot's buffers for segments of up to n samples (PCM staging, samples, energy, log-mel)
+static void slot_reserve_all(State::Impl::Slot& sl, int n, int n_mels) {
+  if (n <= 0) return;
+  std::lock_guard<std::recursive_mutex> g(hip_alloc_mutex());
+  if (n > sl.pcm_cap) {
+    if (sl.h_pcm) WDR_HIP(hipHostFree(sl.h_pcm));
+    sl.h_pcm = nullptr;
+    WDR_HIP(hipHostMalloc((void**)&sl.h_pcm, (size_t)n * 2, hipHostMallocDefault));
+    sl.pcm = DevMem((size_t)n * 2);
+    sl.pcm_cap = n;
+  }
+  slot_reserve_x(sl, n);
+  if (n > sl.energy_cap) {
+    if (sl.h_energy) WDR_HIP(hipHostFree(sl.h_energy));
+    sl.h_energy = nullptr;
+    WDR_HIP(hipHostMalloc((void**)&sl.h_energy, (size_t)n * 4, hipHostMallocDefault));
+    sl.energy_d = DevMem((size_t)n * 4);
+    sl.energy_cap = n;
+  }
+  const int frames = std::min((n + 200) / 160 + 1, (n + 480000) / 160);   // slot_mel's n_fft_frames
+  if (frames > sl.mel_cap) {
+    sl.mel = DevMem((size_t)frames * n_mels * 4);
+    sl.mel_cap = frames;
   }
 }
 
@@ -869,6 +916,11 @@ void State::plan(const int16_t* const* pcm, const int* n, int count, bool detect
   Impl& m = *m_;
   enc_quiesce();
   WDR_HIP(hipStreamSynchronize(m.es));
+  // every ring slot sized for the plan's longest segment here, on the chain thread: no device
+  // or pinned allocation happens on the encode-ahead thread while other threads capture graphs
+  int nmax = 0;
+  for (int i = 0; i < count; ++i) nmax = std::max(nmax, n[i]);
+  for (int k = 0; k < m.S; ++k) slot_reserve_all(m.slots[k], nmax, m.n_mels);
   {
     std::lock_guard<std::mutex> g(m.enc_mu);
     m.plan.detect_lang = detect_lang;
@@ -1024,6 +1076,7 @@ bool State::top_up_batch(int j) {
       if (k >= m.S) WDR_HIP(hipStreamWaitEvent(m.es, sl.freed, 0));
       slot_dtw_fence(k % m.S, m.es);   // a queued DTW pass may still read the slot
       const int nk = m.plan.n[k];
+      slot_reserve_all(sl, nk, m.n_mels);   // normally sized by plan() already
       if (nk > sl.pcm_cap) {
         if (sl.h_pcm) WDR_HIP(hipHostFree(sl.h_pcm));
         WDR_HIP(hipHostMalloc((void**)&sl.h_pcm, (size_t)std::max(nk, 1) * 2, hipHostMallocDefault));
@@ -1056,8 +1109,8 @@ bool State::top_up_batch(int j) {
     // it runs here, off the decode chain: the batch's windows as the rows of ONE decode step,
     // each with its own cross-K/V slot and sequence (every window a one-row group: the
     // arithmetic of decoder_prefill(SOT) on the decode stream)
-    auto body = [&](RowBatch& tl, bool capturing) {
-      encoder_body(ctx_, m, m.eb, g1 - g0, m.xkv_ring.as<f16>() + (size_t)slot0 * m.xkv_slot_elems, m.es);
+    auto body = [&](RowBatch& tl, bool capturing, hipStream_t es) {
+      encoder_body(ctx_, m, m.eb, g1 - g0, m.xkv_ring.as<f16>() + (size_t)slot0 * m.xkv_slot_elems, es);
       if (!m.plan.detect_lang) return;
       const int R = g1 - g0;
       tl.clear();   // waits for the previous batch's table copy
@@ -1072,12 +1125,12 @@ bool State::top_up_batch(int j) {
         tl.add(g);
       }
       RowsIO io = m.lb.io(ctx_, m.V);
-      tl.upload(io, m.es, true, !capturing);
-      rows_forward(ctx_, io, R, m.es);
+      tl.upload(io, es, true, !capturing);
+      rows_forward(ctx_, io, R, es);
       for (int r = 0; r < R; ++r)
         WDR_HIP(wdr_memcpy_async(m.h_lang + (size_t)((g0 + r) % m.S) * 100,
                                m.lb.logits.as<float>() + (size_t)r * m.V + sot + 1, 100 * 4,
-                               hipMemcpyDeviceToHost, m.es));
+                               hipMemcpyDeviceToHost, es));
     };
     const double t_el = now_s();
     struct ElT {
@@ -1086,7 +1139,11 @@ bool State::top_up_batch(int j) {
       ~ElT() { acc += (long long)((now_s() - t0) * 1e9); }
     } el_t{t_el, m.t_enc_launch};
     static const bool enc_graph = !(getenv("WDR_ENC_GRAPH") && atoi(getenv("WDR_ENC_GRAPH")) == 0);
-    if (enc_graph && g1 - g0 == kBatch && !getenv("WDR_NO_GRAPH")) {
+    // the live profiler (bench.py's roofline) samples eager launches only: while it is on, 1 in
+    // kStepEvery batches runs eagerly with its launches sampled 1 in kEvery (prof.h), the rate
+    // decode steps are sampled at -- a uniform sample of the encoder GEMMs
+    const bool sampled = prof_step();
+    if (enc_graph && g1 - g0 == kBatch && !getenv("WDR_NO_GRAPH") && !sampled) {
       const bool f8 = ctx_.fp8_encoder.load();
       const int key = slot0 * 4 + (f8 ? 2 : 0) + (m.plan.detect_lang ? 1 : 0);   // the batch's slots
       Impl::EncGraph& eg = m.enc_graphs[key];
@@ -1096,20 +1153,24 @@ bool State::top_up_batch(int j) {
           (void)ctx_.fp8_xkv();
         }
         if (!eg.tl) eg.tl = std::make_unique<RowBatch>(kBatch, kBatch, 0);
+        std::lock_guard<std::recursive_mutex> cap_lock(hip_alloc_mutex());   // no allocation meanwhile
+        // captured on a stream of its own: the chain thread waits on events recorded on m.es,
+        // which HIP refuses while m.es itself is capturing
+        if (!m.es_cap) WDR_HIP(hipStreamCreateWithFlags(&m.es_cap, hipStreamNonBlocking));
         hipGraph_t graph;
         prof_capture(true);
-        WDR_HIP(hipStreamBeginCapture(m.es, hipStreamCaptureModeThreadLocal));
+        WDR_HIP(hipStreamBeginCapture(m.es_cap, hipStreamCaptureModeRelaxed));
         try {
-          body(*eg.tl, true);
+          body(*eg.tl, true, m.es_cap);
         } catch (...) {
           hipGraph_t dead = nullptr;
-          (void)hipStreamEndCapture(m.es, &dead);
+          (void)hipStreamEndCapture(m.es_cap, &dead);
           if (dead) (void)hipGraphDestroy(dead);
           prof_capture(false);
           throw;
         }
         prof_capture(false);
-        WDR_HIP(hipStreamEndCapture(m.es, &graph));
+        WDR_HIP(hipStreamEndCapture(m.es_cap, &graph));
         WDR_HIP(hipGraphInstantiate(&eg.exec, graph, nullptr, nullptr, 0));
         WDR_HIP(hipGraphDestroy(graph));
       }
@@ -1119,7 +1180,14 @@ bool State::top_up_batch(int j) {
       if (mu) mu->unlock();
       WDR_HIP(ge);
     } else {
-      body(*m.tlb, false);
+      prof_in_step(sampled);
+      try {
+        body(*m.tlb, false, m.es);
+      } catch (...) {
+        prof_in_step(false);
+        throw;
+      }
+      prof_in_step(false);
     }
     for (int k = g0; k < g1; ++k) WDR_HIP(hipEventRecord(m.slots[k % m.S].ready, m.es));
     {
@@ -1257,9 +1325,10 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
     g.exec = nullptr;
   }
   if (!g.exec) {
+    std::lock_guard<std::recursive_mutex> cap_lock(hip_alloc_mutex());   // no allocation meanwhile
     hipGraph_t graph;
     prof_capture(true);
-    WDR_HIP(hipStreamBeginCapture(s_, hipStreamCaptureModeThreadLocal));
+    WDR_HIP(hipStreamBeginCapture(s_, hipStreamCaptureModeRelaxed));
     tb.upload(io, s_, true, false);
     WDR_HIP(wdr_memcpy_async(m.ctl.p, m.h_ctl, R * sizeof(LogitsCtl), hipMemcpyHostToDevice, s_));
     rows_forward(ctx_, io, R, s_);
@@ -2733,9 +2802,10 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
       g.exec = nullptr;
     }
     if (!g.exec) {
+      std::lock_guard<std::recursive_mutex> cap_lock(hip_alloc_mutex());   // no allocation meanwhile
       hipGraph_t graph;
       prof_capture(true);
-      WDR_HIP(hipStreamBeginCapture(m.s, hipStreamCaptureModeThreadLocal));
+      WDR_HIP(hipStreamBeginCapture(m.s, hipStreamCaptureModeRelaxed));
       tb.upload(io, m.s, true, false);
       rows_forward(ctx_, io, R, m.s);
       tail();
