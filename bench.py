@@ -89,8 +89,19 @@ def pmc_traffic(cls):
 # conv1, conv2, 32 x (qkv, o, fc1, fc2), the cross-K/V projection -- and the self-attention),
 # and a decoder pass's bytes: the decoder weights (streamed once per rows launch, shared by its
 # rows) and one slot's cross-K/V (read once per cross-attention group or MFMA row tile).
+# rows_weight_bytes: the weight bytes a row-kernel launch streams, by its template arguments
+# <EPI, MT, NT, W, LN, U> (EPI 5 qkv 3d x d, 2 o / xo d x d or fc2 d x 4d (16 waves), 0 xq, 1 fc1
+# 4d x d, 3 logits V x d), large-v3 d = 1280
+_D, _V = 1280, 51866
+_RW = {"5": 3 * _D * _D * 2, "0": _D * _D * 2, "1": 4 * _D * _D * 2, "3": _V * _D * 2}
 WORK = {"large-v3": {"enc_flops": 2.589e12, "enc_gemm_flops": 2.221e12, "enc_attn_flops": 0.369e12,
-                     "dec_weight_bytes": 1.601e9, "xkv_row_bytes": 0.246e9},
+                     "dec_weight_bytes": 1.601e9, "xkv_row_bytes": 0.246e9,
+                     "rows_weight_bytes": {**{"%s,%d,%d,%d,%s,%d" % (e, mt, nt, wv, ln, u): _RW[e]
+                                              for e in _RW for mt in (1, 2, 3, 4) for nt in (1, 2)
+                                              for wv in (8, 16) for ln in ("false", "true") for u in (0, 3, 12)},
+                                           **{"2,1,1,8,%s,%d" % (ln, u): _D * _D * 2 for ln in ("false", "true")
+                                              for u in (0, 3)},
+                                           "2,1,1,16,false,12": 4 * _D * _D * 2}},
         "base.en": {"enc_flops": 96.8e9, "enc_gemm_flops": 87.6e9, "enc_attn_flops": 9.2e9,
                     "dec_weight_bytes": 97.1e6, "xkv_row_bytes": 18.4e6}}
 
@@ -141,12 +152,30 @@ def trace_roofline(model, fp8=False):
     c = line["counts"]
     out = {"source": os.path.relpath(d, ROOT), "traced_runs": runs}
     pk = MFMA_FP8_PEAK_TFS if fp8 else MFMA_F16_PEAK_TFS
+    # the decoder rows class: every row-kernel launch of the trace (batched steps, prompt
+    # prefills, DTW passes, language detection) streams its projection's weights once --
+    # N*K*2 bytes by the kernel's epilogue / tiling (csrc/kernels/gemm.hip launch_rows_epi)
+    rows_bytes = rows_ms = 0.0
+    wb = w.get("rows_weight_bytes")
+    stats = os.path.join(d, "run_kernel_stats.csv")
+    if wb and os.path.exists(stats):
+        import csv
+        for r in csv.DictReader(open(stats)):
+            nm = r.get("Name", r.get("KernelName", ""))
+            if nm.startswith("k_skinny<") or "k_skinny" in nm:
+                key = nm[nm.index("<") + 1:nm.index(">")].replace(" ", "")
+                b = wb.get(key)
+                if b:
+                    rows_bytes += float(r.get("Calls", 0)) * b
+                    rows_ms += float(r.get("TotalDurationNs", 0)) * 1e-6
     for k, work, unit in (("gemm", runs * c["windows"] * w["enc_gemm_flops"], "TFLOP/s"),
                           ("flash", runs * c["windows"] * w["enc_attn_flops"], "TFLOP/s"),
-                          ("rows", runs * c.get("batch_launches", 0) * w["dec_weight_bytes"], "GB/s"),
+                          ("rows", rows_bytes, "GB/s"),
                           ("xattn", runs * (c.get("batch_xattn_groups", 0) + c.get("batch_xattn_tiles", 0))
                            * w["xkv_row_bytes"], "GB/s")):
             k_ms = cls["classes"].get(k, {}).get("total_ms")
+            if k == "rows":
+                k_ms = rows_ms   # the projection launches the bytes count (the live sampler's set)
             if not k_ms or not work:
                 continue
             if unit == "TFLOP/s":

@@ -1649,6 +1649,7 @@ __global__ __launch_bounds__(256) void k_gemv(ProjArgs a) {
 // separate LayerNorm launch and its f16 round trip from the prefill / DTW passes.
 template <int EPI, int MT, int NT, int W = 4, bool LN = false, int UU = 0>
 __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
   __shared__ float red[W][MT][NT][4][64];
   extern __shared__ __attribute__((aligned(16))) f16 xln[];   // LN: [16*MT][K + 8]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
