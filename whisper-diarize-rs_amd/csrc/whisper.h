@@ -32,6 +32,8 @@ std::vector<std::pair<int, int>> alignment_heads_for(const std::string& model_na
 
 // serialises device / pinned allocation and free with hipGraph captures (whisper_ctx.cpp)
 std::recursive_mutex& hip_alloc_mutex();
+// a stream on a dedicated hardware queue (env knob `knob`, default `def`; else priority `prio`)
+hipStream_t dedicated_stream(const char* knob, bool def, int prio);
 
 struct DevMem {
   void* p = nullptr;

@@ -105,6 +105,77 @@ std::recursive_mutex& hip_alloc_mutex() {
   return mu;
 }
 
+// A stream on a hardware queue of its own.  HIP multiplexes the process's streams onto at most
+// GPU_MAX_HW_QUEUES (4) hardware queues per priority level, in order: a kernel of the step batcher
+// then waits behind whatever another stream sharing its queue has in front of it (an encoder GEMM
+// launch, a barrier packet waiting on a slot event).  A stream created with a CU mask gets a
+// dedicated queue; the mask here is every CU of the device.  kind: a WDR_<kind>_HWQ env knob
+// (0 = the shared priority pool, A/B runs), default `def`.
+hipStream_t dedicated_stream(const char* knob, bool def, int prio) {
+  const char* e = getenv(knob);
+  const bool on = e ? atoi(e) != 0 : def;
+  hipStream_t s = nullptr;
+  if (!on) {
+    WDR_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio));
+    return s;
+  }
+  int dev = 0, ncu = 0;
+  WDR_HIP(hipGetDevice(&dev));
+  WDR_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+  for (int c = 0; c < ncu; ++c) mask[c / 32] |= 1u << (c % 32);
+  WDR_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+  return s;
+}
+
+// The encode-ahead streams of all states: WDR_ENC_POOL (default 2) CU-masked streams per device,
+// a dedicated hardware queue each, shared round-robin by the states, which leave WDR_ENC_MASK
+// (default 32) CUs -- 4 per XCD -- to the decode chain.  1-h bench, A/B on one box
+// (profiles/r03/ab_enc_queues.txt): 608-619 xRT with one low-priority stream per state (24 streams
+// on HIP's 4 shared low-priority queues) against 642-646 with 2 or 3 masked queues; 4 or 8
+// masked queues 576, one 547 (the encoder starves), 24 (one per state) 398.  Both knobs -1: one
+// low-priority stream per state.  Returns null then.
+static hipStream_t enc_masked_stream(bool* shared) {
+  static const int n_res = getenv("WDR_ENC_MASK") ? atoi(getenv("WDR_ENC_MASK")) : 32;
+  static const int pool = getenv("WDR_ENC_POOL") ? atoi(getenv("WDR_ENC_POOL")) : 2;
+  *shared = false;
+  if (n_res < 0 && pool < 0) return nullptr;
+  int dev = 0, ncu = 0;
+  WDR_HIP(hipGetDevice(&dev));
+  WDR_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  if (ncu != 256 && !getenv("WDR_ENC_MASK") && !getenv("WDR_ENC_POOL")) return nullptr;   // tuned on MI355X
+  WDR_CHECK(n_res < ncu, "WDR_ENC_MASK: must leave the encoder at least one CU");
+  // WDR_ENC_MASK_PAT=1: the reserved CUs spread over the 8 XCDs whether mask bit c is CU c % 32
+  // of XCD c / 32 or CU c / 8 of XCD c % 8 (bits 32x + 8j + x, j < n/8): a decode launch's
+  // workgroups go round-robin over the XCDs, so every XCD needs free CUs.  0: the top n bits.
+  static const int pat = getenv("WDR_ENC_MASK_PAT") ? atoi(getenv("WDR_ENC_MASK_PAT")) : 1;
+  auto make = [&] {
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    std::vector<char> res(ncu, 0);
+    if (pat == 1 && ncu == 256) {
+      WDR_CHECK(n_res % 8 == 0 && n_res <= 32, "WDR_ENC_MASK_PAT=1: 0, 8, 16, 24 or 32 CUs");
+      for (int x = 0; x < 8; ++x)
+        for (int j = 0; j < std::max(0, n_res) / 8; ++j) res[32 * x + 8 * j + x] = 1;
+    } else {
+      for (int c = ncu - std::max(0, n_res); c < ncu; ++c) res[c] = 1;
+    }
+    for (int c = 0; c < ncu; ++c)
+      if (!res[c]) mask[c / 32] |= 1u << (c % 32);
+    hipStream_t st = nullptr;
+    WDR_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+    return st;
+  };
+  if (pool <= 0) return make();
+  static std::mutex mu;
+  static std::map<int, std::pair<std::vector<hipStream_t>, int>> pools;   // device -> streams, next
+  std::lock_guard<std::mutex> g(mu);
+  auto& P = pools[dev];
+  if (P.first.empty())
+    for (int i = 0; i < pool; ++i) P.first.push_back(make());
+  *shared = true;
+  return P.first[P.second++ % pool];
+}
+
 DevMem::DevMem(size_t n) : bytes(n) {
   if (n) {
     std::lock_guard<std::recursive_mutex> g(hip_alloc_mutex());
@@ -423,6 +494,7 @@ struct State::Impl {
   DevMem xkv_ring;
   size_t xkv_slot_elems = 0;
   int cur = 0;                // slot the decoder reads (cross-K/V, samples)
+  bool es_shared = false;     // es from the WDR_ENC_MASK pool (not destroyed with the state)
   hipStream_t es = nullptr;   // encode-ahead stream (lower priority than the decode stream)
   struct Plan {
     std::vector<const int16_t*> pcm;
@@ -616,7 +688,8 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
     WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
     static const int ep = getenv("WDR_ENC_PRIO") ? atoi(getenv("WDR_ENC_PRIO")) : 0;
     const int prio = ep == 2 ? hi : ep == 1 ? (lo + hi) / 2 : lo;
-    WDR_HIP(hipStreamCreateWithPriority(&m.es, hipStreamNonBlocking, prio));
+    m.es = enc_masked_stream(&m.es_shared);
+    if (!m.es) WDR_HIP(hipStreamCreateWithPriority(&m.es, hipStreamNonBlocking, prio));
   }
   // this state's rows forwards: prompt prefills / DTW re-forwards up to RMAX rows, steps of up
   // to NSEQ logit rows; the DTW set captures; language detection kBatch rows
@@ -696,7 +769,7 @@ State::~State() {
     (void)hipHostFree(m_->h_pairs);
     if (m_->es) {
       (void)hipStreamSynchronize(m_->es);
-      (void)hipStreamDestroy(m_->es);
+      if (!m_->es_shared) (void)hipStreamDestroy(m_->es);
     }
     if (m_->sd) {
       (void)hipStreamSynchronize(m_->sd);
@@ -912,10 +985,16 @@ void State::read_encoder_out(float* out) {
 // every segment does not depend on any decode result, so it is encoded ahead on the low-
 // priority stream in batches of kBatch windows into the cross-K/V ring; segment j waits only
 // on its slot's `ready` event, and slot j % S is reused once segment j - S has recorded `freed`.
+// this state's encode-ahead work done: every batch ends by recording its slots' `ready` events
+// (the stream itself may be shared with other states' encodes)
+static void es_sync(State::Impl& m) {
+  for (auto& sl : m.slots) WDR_HIP(hipEventSynchronize(sl.ready));
+}
+
 void State::plan(const int16_t* const* pcm, const int* n, int count, bool detect_lang) {
   Impl& m = *m_;
   enc_quiesce();
-  WDR_HIP(hipStreamSynchronize(m.es));
+  es_sync(m);
   // every ring slot sized for the plan's longest segment here, on the chain thread: no device
   // or pinned allocation happens on the encode-ahead thread while other threads capture graphs
   int nmax = 0;
@@ -936,7 +1015,7 @@ void State::unplan() {
   Impl& m = *m_;
   enc_quiesce();
   flush_dtw();
-  WDR_HIP(hipStreamSynchronize(m.es));
+  es_sync(m);
   std::lock_guard<std::mutex> g(m.enc_mu);
   m.plan.pcm.clear();
   m.plan.n.clear();
@@ -2587,7 +2666,7 @@ StepBatcher::StepBatcher(Context& ctx) : ctx_(ctx), m_(new Impl) {
   m.H = hp.n_text_head;
   int lo = 0, hi = 0;
   WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-  WDR_HIP(hipStreamCreateWithPriority(&m.s, hipStreamNonBlocking, hi));
+  m.s = dedicated_stream("WDR_BATCH_HWQ", false, hi);
   const int RB = rows_cap(ctx), LB = logit_cap(ctx);
   m.RB = RB;
   m.LB = LB;
@@ -2915,7 +2994,7 @@ DtwQueue::DtwQueue(Context& ctx) : m_(new Impl), ctx_(ctx) {
   if (const char* e = getenv("WDR_DTW_AGE_MS")) m.max_age = std::max(0.0, atof(e)) * 1e-3;
   int lo = 0, hi = 0;
   WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-  WDR_HIP(hipStreamCreateWithPriority(&m.s, hipStreamNonBlocking, lo));
+  m.s = dedicated_stream("WDR_DTWQ_HWQ", false, lo);
   m.bufs.alloc(m.RB, 1, hp.n_text_state, hp.n_text_head, hp.n_vocab);
   m.tb = std::make_unique<RowBatch>(m.RB, 1, m.RB);
   m.cap = DevMem((size_t)m.A * m.RB * 1500 * 4);
