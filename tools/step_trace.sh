@@ -7,7 +7,7 @@
 set -e -o pipefail
 TAG=${1:-steps}
 SECS=${2:-900}
-export TMPDIR=/tmp WDR_LAUNCH_LOCK=1
+export TMPDIR=/tmp WDR_LAUNCH_LOCK=${LOCK:-1}
 O=gpurun_out/trace_$TAG
 rm -rf $O && mkdir -p $O
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/trace -o run -- \

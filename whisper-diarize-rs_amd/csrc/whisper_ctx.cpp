@@ -135,19 +135,16 @@ hipStream_t dedicated_stream(const char* knob, bool def, int prio) {
 // on HIP's 4 shared low-priority queues) against 642-646 with 2 or 3 masked queues; 4 or 8
 // masked queues 576, one 547 (the encoder starves), 24 (one per state) 398.  Both knobs -1: one
 // low-priority stream per state.  Returns null then.
-static hipStream_t enc_masked_stream(bool* shared) {
-  static const int n_res = getenv("WDR_ENC_MASK") ? atoi(getenv("WDR_ENC_MASK")) : 32;
-  static const int pool = getenv("WDR_ENC_POOL") ? atoi(getenv("WDR_ENC_POOL")) : 2;
-  *shared = false;
-  if (n_res < 0 && pool < 0) return nullptr;
+// A stream of a pool of `pool` CU-masked streams (dedicated hardware queues) per (tag, device),
+// handed out round-robin, that leave n_res CUs free (WDR_ENC_MASK_PAT=1: spread over the 8 XCDs
+// whether mask bit c is CU c % 32 of XCD c / 32 or CU c / 8 of XCD c % 8 -- bits 32x + 8j + x,
+// j < n/8 -- since a decode launch's workgroups go round-robin over the XCDs, every XCD needs free
+// CUs; 0: the top n bits).  pool <= 0: a stream of its own.
+static hipStream_t masked_pool_stream(const char* tag, int n_res, int pool, bool* shared) {
   int dev = 0, ncu = 0;
   WDR_HIP(hipGetDevice(&dev));
   WDR_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-  if (ncu != 256 && !getenv("WDR_ENC_MASK") && !getenv("WDR_ENC_POOL")) return nullptr;   // tuned on MI355X
-  WDR_CHECK(n_res < ncu, "WDR_ENC_MASK: must leave the encoder at least one CU");
-  // WDR_ENC_MASK_PAT=1: the reserved CUs spread over the 8 XCDs whether mask bit c is CU c % 32
-  // of XCD c / 32 or CU c / 8 of XCD c % 8 (bits 32x + 8j + x, j < n/8): a decode launch's
-  // workgroups go round-robin over the XCDs, so every XCD needs free CUs.  0: the top n bits.
+  WDR_CHECK(n_res < ncu, "masked stream: must leave at least one CU");
   static const int pat = getenv("WDR_ENC_MASK_PAT") ? atoi(getenv("WDR_ENC_MASK_PAT")) : 1;
   auto make = [&] {
     std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
@@ -165,15 +162,46 @@ static hipStream_t enc_masked_stream(bool* shared) {
     WDR_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
     return st;
   };
+  *shared = false;
   if (pool <= 0) return make();
   static std::mutex mu;
-  static std::map<int, std::pair<std::vector<hipStream_t>, int>> pools;   // device -> streams, next
+  static std::map<std::pair<std::string, int>, std::pair<std::vector<hipStream_t>, int>> pools;
   std::lock_guard<std::mutex> g(mu);
-  auto& P = pools[dev];
+  auto& P = pools[{tag, dev}];
   if (P.first.empty())
     for (int i = 0; i < pool; ++i) P.first.push_back(make());
   *shared = true;
   return P.first[P.second++ % pool];
+}
+
+// The encode-ahead streams of all states: WDR_ENC_POOL (default 2) CU-masked streams per device,
+// a dedicated hardware queue each, shared round-robin by the states, which leave WDR_ENC_MASK
+// (default 32) CUs -- 4 per XCD -- to the decode chain.  1-h bench, A/B on one box
+// (profiles/r03/ab_enc_queues.txt): 608-619 xRT with one low-priority stream per state (24 streams
+// on HIP's 4 shared low-priority queues) against 642-646 with 2 or 3 masked queues; 4 or 8
+// masked queues 576, one 547 (the encoder starves), 24 (one per state) 398.  Both knobs -1: one
+// low-priority stream per state.  Returns null then.
+static hipStream_t enc_masked_stream(bool* shared) {
+  static const int n_res = getenv("WDR_ENC_MASK") ? atoi(getenv("WDR_ENC_MASK")) : 32;
+  static const int pool = getenv("WDR_ENC_POOL") ? atoi(getenv("WDR_ENC_POOL")) : 2;
+  *shared = false;
+  if (n_res < 0 && pool < 0) return nullptr;
+  int dev = 0, ncu = 0;
+  WDR_HIP(hipGetDevice(&dev));
+  WDR_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  if (ncu != 256 && !getenv("WDR_ENC_MASK") && !getenv("WDR_ENC_POOL")) return nullptr;   // tuned on MI355X
+  return masked_pool_stream("enc", n_res, pool, shared);
+}
+
+// WDR_OWN_POOL=P (A/B): the states' own streams from P masked streams (WDR_OWN_MASK CUs left
+// free, default 0) instead of one highest-priority stream each, so no chain's own work (on-demand
+// encodes, fix-up passes) shares the step batcher's hardware queue.  Null when unset.
+static hipStream_t own_masked_stream(bool* shared) {
+  static const int pool = getenv("WDR_OWN_POOL") ? atoi(getenv("WDR_OWN_POOL")) : -1;
+  static const int n_res = getenv("WDR_OWN_MASK") ? atoi(getenv("WDR_OWN_MASK")) : 0;
+  *shared = false;
+  if (pool < 0) return nullptr;
+  return masked_pool_stream("own", n_res, pool, shared);
 }
 
 DevMem::DevMem(size_t n) : bytes(n) {
@@ -494,6 +522,7 @@ struct State::Impl {
   DevMem xkv_ring;
   size_t xkv_slot_elems = 0;
   int cur = 0;                // slot the decoder reads (cross-K/V, samples)
+  bool own_shared = false;    // own from the WDR_OWN_POOL pool
   bool es_shared = false;     // es from the WDR_ENC_MASK pool (not destroyed with the state)
   hipStream_t es = nullptr;   // encode-ahead stream (lower priority than the decode stream)
   struct Plan {
@@ -659,7 +688,12 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
     // every state has its own highest-priority decode stream (chains run concurrently)
     int lo = 0, hi = 0;
     WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    WDR_HIP(hipStreamCreateWithPriority(&m.own, hipStreamNonBlocking, hi));
+    // WDR_OWN_PRIO=1|2 (A/B): the state's own stream at the normal / lowest priority
+    static const int op = getenv("WDR_OWN_PRIO") ? atoi(getenv("WDR_OWN_PRIO")) : 0;
+    m.own = own_masked_stream(&m.own_shared);
+    if (m.own) {
+    } else if (op == 1) WDR_HIP(hipStreamCreateWithFlags(&m.own, hipStreamNonBlocking));
+    else WDR_HIP(hipStreamCreateWithPriority(&m.own, hipStreamNonBlocking, op == 2 ? lo : hi));
     s_ = m.own;
   }
   m.d = hp.n_text_state;
@@ -777,7 +811,7 @@ State::~State() {
     }
     if (m_->own) {
       (void)hipStreamSynchronize(m_->own);
-      (void)hipStreamDestroy(m_->own);
+      if (!m_->own_shared) (void)hipStreamDestroy(m_->own);
     }
     for (auto& j : m_->jobs) {
       if (j.blk) m_->blk_pool.push_back(j.blk);
@@ -2905,6 +2939,7 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
     }
   }
   if (blog) WDR_HIP(hipEventRecord(m.ev1, m.s));
+  const double t_enq = now_s();   // host side of the launch done (eager: every kernel enqueued)
   WDR_HIP(hipStreamSynchronize(m.s));
   auto tok_of = [&](int i) {
     const TokOut& o = m.h_tok[i];
@@ -2940,11 +2975,12 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
   const double t_end = now_s();
   step_s += t_end - t_step;
   // WDR_BATCH_LOG=<file>: one line per launch (start s, rows, wall ms, prefill rows, DTW rows,
-  // GPU ms: the launch's span on its stream, first command to last)
+  // GPU ms: the launch's span on its stream, first command to last, host enqueue ms)
   if (blog) {
     float gms = 0.f;
     (void)hipEventElapsedTime(&gms, m.ev0, m.ev1);
-    fprintf(blog, "%.6f %d %.3f %d %d %.3f\n", t_step, R, (t_end - t_step) * 1e3, n_pre, n_dtw, gms);
+    fprintf(blog, "%.6f %d %.3f %d %d %.3f %.3f\n", t_step, R, (t_end - t_step) * 1e3, n_pre, n_dtw, gms,
+            (t_enq - t_step) * 1e3);
     fflush(blog);
   }
 }
