@@ -193,6 +193,19 @@ static hipStream_t enc_masked_stream(bool* shared) {
   return masked_pool_stream("enc", n_res, pool, shared);
 }
 
+// One mutex per pooled stream: a state's encode batch is issued onto a shared stream as one
+// unit, so batches run one after another instead of interleaving kernel by kernel (at the start
+// of a run every state issues its first batch at once: interleaved, all 12 batches of a stream
+// finished together, ~0.6 s in; one after another, the first chains start decoding ~50 ms in).
+static std::mutex& stream_issue_mutex(hipStream_t st) {
+  static std::mutex mu;
+  static std::map<hipStream_t, std::unique_ptr<std::mutex>> m;
+  std::lock_guard<std::mutex> g(mu);
+  auto& p = m[st];
+  if (!p) p = std::make_unique<std::mutex>();
+  return *p;
+}
+
 // WDR_OWN_POOL=P (A/B): the states' own streams from P masked streams (WDR_OWN_MASK CUs left
 // free, default 0) instead of one highest-priority stream each, so no chain's own work (on-demand
 // encodes, fix-up passes) shares the step batcher's hardware queue.  Null when unset.
@@ -1184,6 +1197,10 @@ bool State::top_up_batch(int j) {
     if (g0 == first && g0 > 0 && enc_thread_on() && std::this_thread::get_id() == m.enc_th.get_id())
       WDR_HIP(hipEventSynchronize(m.slots[(g0 - 1) % m.S].ready));   // the first window encoded
     const int slot0 = g0 % m.S;
+    // a shared (pooled) encode stream: the whole batch issued as one unit (WDR_ENC_ATOMIC=0: A/B)
+    static const bool atomic_issue = !(getenv("WDR_ENC_ATOMIC") && atoi(getenv("WDR_ENC_ATOMIC")) == 0);
+    std::unique_lock<std::mutex> issue_lk;
+    if (m.es_shared && atomic_issue) issue_lk = std::unique_lock<std::mutex>(stream_issue_mutex(m.es));
     for (int k = g0; k < g1; ++k) {
       Impl::Slot& sl = m.slots[k % m.S];
       if (k >= m.S) WDR_HIP(hipStreamWaitEvent(m.es, sl.freed, 0));
