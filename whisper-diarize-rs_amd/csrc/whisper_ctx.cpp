@@ -5,7 +5,6 @@
 #include "rows.h"
 #include "ggml_file.h"
 #include "prof.h"
-#include "blaslt.h"
 
 #include <algorithm>
 #include <chrono>
@@ -478,10 +477,6 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
   }
   WDR_HIP(hipStreamSynchronize(s));
   {
-    const int Ms[2] = {1500, 4 * 1500};   // on-demand windows, encode-ahead batches (kBatch)
-    blaslt_prewarm(hp.n_audio_state, Ms, 2, s);   // WDR_ENC_BLASLT=1 only
-  }
-  {
     // KV pool for the decode chains of every State of this context (multi-chain pipeline)
     const char* e = getenv("WDR_DECODE_CHAINS");
     max_chains = std::max(1, std::min(64, e ? atoi(e) : 24));
@@ -953,7 +948,6 @@ static void encoder_body(Context& ctx, State::Impl& m, State::Impl::EncBufs& e, 
     if (!W8) {
       ProjArgs p{A, lda, W, K, bias, out, ldo, nullptr, 0, M, N, K, epi};
       if (epi == EPI_XKV) p.seq_stride = (long long)m.xkv_slot_elems;   // window b -> slot b
-      if (epi != EPI_XKV && enc_blaslt_on() && blaslt_proj(p, s)) return;   // A/B (csrc/blaslt.cpp)
       launch_proj(p, s);
       return;
     }
