@@ -64,6 +64,9 @@ def parse():
                     help="N > 1: one process per GPU over RCCL (wdr/distributed.py, default) or ONE process "
                          "driving N GPUs through libwdr's gpu_device=None context (the C-ABI path a Rust host "
                          "gets, src/engine.rs:14; under torch.distributed.run only rank 0 works)")
+    ap.add_argument("--beam-seconds", type=float, default=900.0,
+                    help="N=1 greedy runs: also time the reference's default decode (beam search, 5 beams, "
+                         "src/transcribe.rs:22-33) over the first this-many seconds of the shard (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-audio", type=float, default=60.0,
                     help="audio seconds of the workload the CPU baseline is extrapolated over (rank 0, N=1)")
@@ -96,6 +99,9 @@ _D, _V = 1280, 51866
 _RW = {"5": 3 * _D * _D * 2, "0": _D * _D * 2, "1": 4 * _D * _D * 2, "3": _V * _D * 2}
 WORK = {"large-v3": {"enc_flops": 2.589e12, "enc_gemm_flops": 2.221e12, "enc_attn_flops": 0.369e12,
                      "dec_weight_bytes": 1.601e9, "xkv_row_bytes": 0.246e9,
+                     # the 32 layers' projection weights without the logits (14 d^2 x 2 B each); a
+                     # DTW pass stops after the last alignment-head layer: 26 of 32
+                     "dec_layer_bytes": 14 * _D * _D * 2 * 32, "dtw_layer_frac": 26 / 32,
                      "rows_weight_bytes": {**{"%s,%d,%d,%d,%s,%d" % (e, mt, nt, wv, ln, u): _RW[e]
                                               for e in _RW for mt in (1, 2, 3, 4) for nt in (1, 2)
                                               for wv in (8, 16) for ln in ("false", "true") for u in (0, 3, 12)},
@@ -103,16 +109,21 @@ WORK = {"large-v3": {"enc_flops": 2.589e12, "enc_gemm_flops": 2.221e12, "enc_att
                                               for u in (0, 3)},
                                            "2,1,1,16,false,12": 4 * _D * _D * 2}},
         "base.en": {"enc_flops": 96.8e9, "enc_gemm_flops": 87.6e9, "enc_attn_flops": 9.2e9,
-                    "dec_weight_bytes": 97.1e6, "xkv_row_bytes": 18.4e6}}
+                    "dec_weight_bytes": 97.1e6, "xkv_row_bytes": 18.4e6, "dec_layer_bytes": 14 * 512 * 512 * 2 * 6,
+                    "dtw_layer_frac": 6 / 6}}
 
 
 def pipeline_roofline(model, times, t_wall):
     """Whole-pipeline roofline of one step (BASELINE.md §3 'roofline.achieved = T_roof / T_wall'
-    with the schedule actually used): encoder windows at the dense f16 MFMA peak; the decoder
-    passes at the HBM peak -- every rows launch streams the decoder weights once for all its
-    rows (decode steps, prompt prefills, DTW re-forwards: csrc/rows.h), every cross-attention
-    group / MFMA row tile reads its slot's cross-K/V once.  Passes outside the batcher (one
-    chain: each step, prefill and DTW pass its own launch) count one launch and one slot each."""
+    with the schedule actually used): encoder windows at the dense f16 MFMA peak; every decoder
+    pass at the HBM peak -- each rows launch streams the decoder weights once for all its rows
+    (decode steps and prompt prefills in the step batcher, csrc/rows.h), each cross-attention
+    group / MFMA row tile reads its slot's cross-K/V once; the DTW queue's passes stream the
+    layers up to the last alignment-head layer (large-v3: 26 of 32, no logits) and read each
+    job's slot over those layers; the language-detection passes (one per encode-ahead batch, its
+    windows as one-row groups) stream every layer and read each row's slot.  Passes outside the
+    batcher (one chain: each step, prefill and DTW pass its own launch) count one launch and one
+    slot each."""
     w = WORK.get(model)
     if w is None:
         return None
@@ -124,12 +135,20 @@ def pipeline_roofline(model, times, t_wall):
     else:
         launches = times["decode_steps"] + times["prefills"] + windows
         slot_reads = launches
+    dtw_frac = w.get("dtw_layer_frac", 1.0)
+    dtw_passes, dtw_jobs = times.get("dtwq_passes", 0), times.get("dtwq_jobs", 0)
+    lang_passes, lang_rows = times.get("lang_passes", 0), times.get("lang_rows", 0)
     t_enc = windows * w["enc_flops"] / (MFMA_F16_PEAK_TFS * 1e12)
-    t_dec = (launches * w["dec_weight_bytes"] + slot_reads * w["xkv_row_bytes"]) / (HBM_PEAK_GBS * 1e9)
-    t_roof = t_enc + t_dec
+    bw = HBM_PEAK_GBS * 1e9
+    t_dec = (launches * w["dec_weight_bytes"] + slot_reads * w["xkv_row_bytes"]) / bw
+    t_dtw = dtw_frac * (dtw_passes * w["dec_layer_bytes"] + dtw_jobs * w["xkv_row_bytes"]) / bw
+    t_lang = (lang_passes * w["dec_weight_bytes"] + lang_rows * w["xkv_row_bytes"]) / bw
+    t_roof = t_enc + t_dec + t_dtw + t_lang
     return {"t_roof_s": round(t_roof, 4), "t_wall_s": round(t_wall, 4), "frac": round(t_roof / t_wall, 4),
-            "terms_s": {"encoder_mfma": round(t_enc, 4), "decoder_rows_hbm": round(t_dec, 4)},
-            "rows_launches": launches, "slot_reads": slot_reads}
+            "terms_s": {"encoder_mfma": round(t_enc, 4), "decoder_rows_hbm": round(t_dec, 4),
+                        "dtw_queue_hbm": round(t_dtw, 4), "lang_detect_hbm": round(t_lang, 4)},
+            "rows_launches": launches, "slot_reads": slot_reads, "dtw_passes": dtw_passes, "dtw_jobs": dtw_jobs,
+            "lang_passes": lang_passes, "lang_rows": lang_rows}
 
 
 def trace_roofline(model, fp8=False):
@@ -274,6 +293,38 @@ def cpu_baseline(model, segs, audio_target):
     return out, sample, threads_max
 
 
+def beam5_record(ctx, dia, vad, pcm, segs, opts, dopts, diarize, args):
+    """The reference's DEFAULT decode -- beam search, 5 beams, patience -1 (src/transcribe.rs:22-33)
+    -- on the first --beam-seconds of the same shard, same context: segmentation of that audio +
+    run_transcription_pipeline over its segments, one untimed run (beam graphs) then two timed."""
+    import wdr
+    n = int(args.beam_seconds * 16000)
+    sub = [s for s in segs if s.end * 16000 <= n]
+    if not sub:
+        return None
+    bopts = wdr.TranscribeOptions(model=args.model, lang="auto", enable_vad=not diarize,
+                                  enable_diarize=True if diarize else None, advanced=None)
+
+    def run():
+        if diarize:
+            dia.get_segments(pcm[:n])
+        else:
+            vad.get_segments(pcm[:n], materialize=False)
+        return ctx.run_pipeline(sub, bopts, diarize_options=dopts)
+    run()
+    steps = 2
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    dt = time.perf_counter() - t0
+    audio = n / 16000.0
+    return {"metric": "audio-sec/wall-sec (xRT)", "value": round(audio * steps / dt, 3), "unit": "audio-sec/wall-sec",
+            "strategy": "beam search, 5 beams, patience -1 (reference default, src/transcribe.rs:22-33)",
+            "audio_s": audio, "segments": len(sub), "steps": steps, "warmup": 1,
+            "ms_per_step": round(dt * 1e3 / steps, 1),
+            "note": "same context, weights and pins as the main line; the first %.0f s of its shard" % audio}
+
+
 def main_inproc(args):
     """--multi inproc: ONE process, N GPUs, libwdr's own multi-GPU path (gpu_device = None,
     WDR_DEVICES = 0..N-1 unless set; decode chains spread over the GPUs, chain k on GPU k % N,
@@ -364,7 +415,8 @@ def main_inproc(args):
         "scaling": "weak", "vs_baseline": None, "dtype": "f16 (f32 accumulate)", "data": "synthetic",
         "config": {"strategy": "greedy" if args.strategy == "greedy" else "beam search, 5 beams (reference default)",
                    "workload": "one file of %d x %.0f s synthetic audio (%d segments, 3 speakers), %s + DTW + %s, "
-                               "lang auto, ground-truth spurt segments downstream (synthetic pin)"
+                               "lang auto, ground-truth spurt segments downstream, decode length pinned and the "
+                               "temperature fallback off (disable_fallback: synthetic pin)"
                                % (N, args.seconds, len(segs), args.model, "diarize" if diarize else "Silero VAD"),
                    "model": args.model, "global_batch": len(segs), "seq_len": 1500,
                    "parallelism": "ONE process, libwdr gpu_device=None over devices %s (decode chains spread, "
@@ -566,6 +618,10 @@ def main():
 
     pipe = pipeline_roofline(args.model, times, dt / args.steps)
 
+    beam = None
+    if rank == 0 and world == 1 and args.strategy == "greedy" and args.beam_seconds > 0:
+        beam = beam5_record(ctx, dia, vad, pcm, segs, opts, dopts, diarize, args)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ctx.close()
@@ -590,16 +646,19 @@ def main():
                        "workload": ("configs[3] per-GPU shard with configs[2]'s greedy decode: %s + DTW + diarize "
                                     "(pyannote segmentation-3.0 run + timed, CAM++ embeddings + speaker assignment), "
                                     "%.0f s synthetic audio per rank (%d segments, %.0f s speech, 3 speakers), lang auto, "
-                                    "ground-truth spurt segments downstream (synthetic pin)" if diarize else
+                                    "ground-truth spurt segments downstream, decode length pinned to round(3.3 tok/s x "
+                                    "window) + 3 and the temperature fallback off (disable_fallback: synthetic pin)"
+                                    if diarize else
                                     "configs[2]: %s + DTW, Silero VAD run + timed, %.0f s synthetic audio per rank "
                                     "(%d segments, %.0f s speech), lang auto, ground-truth spurt segments "
-                                    "downstream (synthetic pin)") % (args.model, shard_s, segs_n // world, audio_s),
+                                    "downstream, decode length pinned to round(3.3 tok/s x window) + 3 and the "
+                                    "temperature fallback off (disable_fallback: synthetic pin)") % (args.model, shard_s, segs_n // world, audio_s),
                        "model": args.model, "global_batch": segs_n if world > 1 else segs_n * world, "seq_len": 1500,
                        "parallelism": ("one file of %d x %.0f s over %d GPUs: pyannote windows + speech-segment blocks "
                                        "sharded, parallel prompt fix-up rounds, results gathered (wdr/distributed.py)"
                                        % (world, shard_s, world)) if world > 1 else "1 GPU"},
             "roofline": roof, "roofline_classes": classes, "roofline_trace": trace, "pipeline_roofline": pipe,
-            "cpu_baseline": cpu,
+            "beam5": beam, "cpu_baseline": cpu,
             "stages_s": {k: round(v, 3) for k, v in times.items() if isinstance(v, float)},
             "counts": {k: v for k, v in times.items() if isinstance(v, int)},
             "segmentation": ({"stage": "pyannote", "s_per_step": round(vad_t[0] / args.steps, 4), "segments": vad_t[1],
@@ -612,6 +671,9 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    # every libwdr handle (context threads, streams, device memory) released while the HIP
+    # runtime is up -- not left to interpreter teardown (wdr_shutdown, include/wdr.h)
+    lib.wdr_shutdown()
 
 
 if __name__ == "__main__":

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define WDR_ABI_VERSION 4
+#define WDR_ABI_VERSION 5
 
 typedef struct wdr_engine wdr_engine;
 typedef struct wdr_context wdr_context;   /* ~ whisper_rs::WhisperContext (+ its state) */
@@ -167,11 +167,19 @@ typedef struct {
   /* ABI 4: the DTW queue (multi-chain runs: every chain's DTW re-forwards batched off the decode
    * chain) -- passes launched, the rows they carried, windows queued */
   int64_t dtwq_passes, dtwq_rows, dtwq_jobs;
+  /* ABI 5: language-detection decoder passes (lang "auto": one per encode-ahead batch, its
+   * windows as one-row groups; or one SOT prefill per on-demand segment) and their rows */
+  int64_t lang_passes, lang_rows;
 } wdr_stage_times;
 
 const char* wdr_last_error(void);
 int wdr_abi_version(void);
 int wdr_device_count(void);
+/* ABI 5: releases every handle the caller has not freed (engines, contexts with their worker
+ * threads, VADs, diarizers, speaker managers) and the process-wide stream pools / profiler
+ * buffers, while the HIP runtime is still up.  Registered with atexit() when the first handle is
+ * created; a host may call it earlier.  Freeing a handle it released is a no-op. */
+void wdr_shutdown(void);
 
 /* ---- Engine (whole-call drop-in) ---- */
 int wdr_engine_new(const wdr_engine_config* cfg, wdr_engine** out);
@@ -374,9 +382,9 @@ int wdr_dbg_proj_fp8(const uint16_t* a_f16, const uint16_t* w_f16, const float* 
                      float* w_scale_out);
 int wdr_dbg_proj(const uint16_t* a_f16, const uint16_t* w_f16, const float* bias, int32_t M, int32_t N, int32_t K,
                  int32_t epi, float* out /* [M][N] f32 (f16 epilogues are widened) */);
-/* epi | WDR_DBG_PROJ_STEP selects the decode-step GEMV schedule (M <= 16 rows); epi |
- * WDR_DBG_PROJ_ROWS the decoder-rows kernel (any M, per-row arithmetic independent of M) */
-#define WDR_DBG_PROJ_STEP 0x100
+/* epi | WDR_DBG_PROJ_ROWS: the decoder-rows kernel (any M, per-row arithmetic independent of M);
+ * projections of <= 64 rows run on it anyway (0x100, the removed decode-step GEMV schedule of
+ * ABI <= 4, is rejected) */
 #define WDR_DBG_PROJ_ROWS 0x200
 int wdr_dbg_attn(const uint16_t* q, const uint16_t* k, const uint16_t* v, int32_t Tq, int32_t Tk, int32_t n_head,
                  int32_t causal, float* out /* [Tq][n_head*64] */);

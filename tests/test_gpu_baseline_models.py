@@ -21,7 +21,8 @@ Tolerances (f16 operands, f32 accumulation on both sides, different summation or
   * token ids equal except at a greedy pick whose oracle logprob gap is below MARGIN (an f16
     near-tie: the test stops comparing that segment there and records the flip); heuristic
     t0/t1 within 2 cs; DTW anchors within 2 cs, at most 1 in 20 within 4 cs (near-equal path
-    costs of the random-weight alignment matrix); pipeline words within 20 ms (the north star).
+    costs of the random-weight alignment matrix, analysed in test_c1_flat_alignment_near_ties);
+    C1's words within 20 ms (the north star) on alignment-conditioned weights.
 """
 import json
 import os
@@ -238,17 +239,29 @@ def test_c1_whole_file_transcribe_audio(tmp_path):
     """configs[0] (C1): base.en, 30-s mono 16 kHz WAV, enable_vad=false, enable_diarize=false,
     default options (beam search 5, lang auto, fallback thresholds active) through
     Engine::transcribe_audio's whole-file branch (src/engine.rs:141-147) and the subtitle
-    formatting on the output path (src/engine.rs:179-199).  Synthetic weights in explicit
-    synthetic mode; decode length pinned.  Checked in three links:
-      1. token level (state.full): ids equal, heuristic t0/t1 and DTW anchors within 2 cs;
-      2. the pipeline's words (src/transcribe.rs:242-320 glue) within 20 ms of the oracle's
-         (>= 90 %; the rest within 40 ms where a DTW anchor sits two frames off a near-tie);
-      3. transcribe_audio's output == the oracle formatting applied to the GPU pipeline's own
-         words, exactly (formatting's tiny-word growth and mid-point clamps can stretch a
-         sub-20-ms word difference, so end-to-end times are bounded through 2 and 3)."""
+    formatting on the output path (src/engine.rs:179-199), against the oracle's output committed
+    as a fixture (tests/golden/c1_base_en_30s.json, alignment-conditioned weights N(0, 0.05)):
+    every cue's text equal, every word and cue bound within +-20 ms (north_star)."""
+    from tests.test_gpu_configs import fixture_vs_transcribe_audio
+    n, dw = fixture_vs_transcribe_audio(tmp_path, "c1_base_en_30s.json")
+    _report(test="c1", cues=n, word_max_dt=dw)
+
+
+def test_c1_flat_alignment_near_ties(tmp_path):
+    """C1 on the round-1 weights N(0, 0.02), whose alignment heads attend almost uniformly over
+    the 1500 frames (alignment-matrix spread 0.048 against 0.40 at 0.05): token ids, text,
+    heuristic times and formatting must still agree exactly; a DTW anchor may move only at a
+    near-tie -- where the GPU's path, priced under the ORACLE's own alignment matrix, is within
+    the perturbation the capture's f16-rounding-level error puts on the two paths
+    (tests/dtw_neartie.py; the round-3 record: 3 tokens, path margin 7.6e-6 on a path cost of
+    101, perturbation 2.5, profiles/r04/dtw_diag.jsonl).  The links:
+      1. token level (state.full): ids equal, heuristic t0/t1 within 2 cs, DTW anchors compared
+         window by window with the near-tie analysis on the same tokens;
+      2. transcribe_audio's output == the oracle formatting applied to the GPU pipeline's own
+         words, exactly."""
     from oracle import formatting as F
-    from oracle.pipeline import SpeechSegment as OSeg
-    from oracle.pipeline import run_transcription_pipeline, write_wav
+    from oracle.pipeline import write_wav
+    from tests.dtw_neartie import analyse, gpu_capture, record_dtw_calls
     pcm, _ = synth_speech(30.0, seed=31)
     path = str(tmp_path / "c1.wav")
     write_wav(path, pcm)
@@ -256,44 +269,46 @@ def test_c1_whole_file_transcribe_audio(tmp_path):
     eng = wdr.Engine(wdr.EngineConfig(cache_dir=str(tmp_path / "cache")), synthetic=syn)
     opts = wdr.TranscribeOptions(model="base.en", enable_vad=False)        # src/types.rs:46-61 defaults otherwise
     got = eng.transcribe_audio(path, opts)
+    eng.close()
     hp = hparams_for("base.en")
     m = Whisper(hp, synth_weights(hp, std=0.02, emb_std=EMB_STD))
-    # 1. token level
     ctx = wdr.WhisperContext("base.en", synthetic=syn)
     x = pcm_i16_to_f32(pcm)
     toks_got, _ = ctx.state_full(x, opts)
     st = WhisperState(m, Vocab(hp.n_vocab), "base.en")
+    calls = record_dtw_calls(st, m)
     st.full(x, FullParams(language="auto", force_len_rate=3.3))
-    n = _compare_results(toks_got, st.result_all, "base.en", "c1-tokens")
-    # 2. pipeline words
+    ref = st.result_all
+    assert len(toks_got) == len(ref)
+    moved = ties = 0
+    for g, r in zip(toks_got, ref):
+        assert [t["id"] for t in g["tokens"]] == [t.id for t in r.tokens] and g["text"] == r.text
+        for tg, tr in zip(g["tokens"], r.tokens):
+            assert abs(tg["t0"] - tr.t0) <= 2 and abs(tg["t1"] - tr.t1) <= 2, (tg, tr)
+    for c in calls:
+        a = analyse(c["qk_o"], gpu_capture(ctx, x, c, len(st.aheads)), c["n_frames"], c["sot_len"], c["seek"])
+        if a["moved"]:
+            moved += len(a["moved"])
+            assert a["path_margin"] <= a["perturbation"], ("anchor moved off a near-tie", a["moved"],
+                                                           a["path_margin"], a["perturbation"])
+            ties += 1
+        _report(test="c1_flat_dtw", seek=c["seek"], moved=a["moved"], path_margin=a["path_margin"],
+                perturbation=a["perturbation"], path_cost=a["path_cost"], x_spread=a["x_spread"])
+    # the pipeline's own anchors against the oracle's: a moved one must be one the seam showed
+    d = [abs(tg["t_dtw"] - tr.t_dtw) for g, r in zip(toks_got, ref) for tg, tr in zip(g["tokens"], r.tokens)]
+    assert sum(v > 0 for v in d) <= moved, (d, moved)
+    # 2. formatting of the GPU's own words == transcribe_audio's output
     seg = [wdr.SpeechSegment(0.0, len(pcm) / 16000.0, pcm)]
     raw_got, lang_got = ctx.run_pipeline(seg, opts)
     ctx.close()
-    st = WhisperState(m, Vocab(hp.n_vocab), "base.en")
-    raw, lang = run_transcription_pipeline(st, [OSeg(0.0, len(pcm) / 16000.0, pcm)],
-                                           dict(lang="auto", synthetic=dict(force_len_rate=3.3)))
-    assert lang_got == lang and [s.text for s in raw_got] == [s.text for s in raw]
-    dts = []
-    for g, r in zip(raw_got, raw):
-        assert len(g.words) == len(r.words)
-        for a, b in zip(g.words, r.words):
-            assert a.text == b.text
-            dts += [abs(a.start - b.start), abs(a.end - b.end)]
-    dw = max(dts)
-    within = sum(d <= 0.02 + 1e-9 for d in dts) / len(dts)
-    # 3. formatting of the GPU's own words == transcribe_audio's output
     want = F.process_segments([F.Seg(s.start, s.end, s.text, None if s.words is None else
                                      [F.Word(w.text, w.start, w.end, w.probability) for w in s.words], None)
                                for s in raw_got], F.config_for_language(lang_got or "auto"))
-    _report(test="c1", tokens_compared=n, segments=len(got), word_max_dt=dw, words_within_20ms=within,
-            fallbacks=st.stats["fallbacks"])
-    # word bounds are midpoints of neighbouring DTW anchors: one anchor two DTW frames off (a
-    # near-tie of the random-weight alignment matrix, see _compare_results) moves a bound 20-40 ms
-    assert dw <= 0.04 + 1e-9 and within >= 0.9, (dw, within)
     assert len(got) == len(want) >= 1
     for g, w in zip(got, want):
         assert (g.text, g.start, g.end) == (w.text, w.start, w.end)
         assert [(a.text, a.start, a.end) for a in g.words] == [(b.text, b.start, b.end) for b in w.words]
+    _report(test="c1_flat", windows=len(calls), anchors_moved=moved, windows_at_near_tie=ties)
 
 
 @pytest.mark.parametrize("strategy", ["beam_search", "greedy"])

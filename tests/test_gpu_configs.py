@@ -1,12 +1,15 @@
 """BASELINE.json configs exercised end to end through the C ABI, against the CPU oracle where the
-oracle can follow, by properties where it cannot (VERDICT r2 "next round" item 1(b), 1(c)).
+oracle can follow, by properties where it cannot.
 
-  * configs[1] (C2): base.en, Silero VAD segmentation, DTW on, the reference's default decode
-    (beam 5, lang auto), 60 s of synthetic speech through Engine::transcribe_audio
-    (src/engine.rs:123-139, 169-199) against the oracle: oracle VAD + merge (src/vad.rs:6-84)
-    -> oracle run_transcription_pipeline (src/transcribe.rs:323-535) -> oracle formatting with
-    the VAD mask (src/engine.rs:192-199);
-  * configs[2] (C3): large-v3, VAD, DTW, greedy, 30 s, the same chain;
+  * configs[1] (C2) at its full size: base.en, Silero VAD segmentation, DTW on, the reference's
+    default decode (beam 5, lang auto), 600 s of synthetic speech through Engine::transcribe_audio
+    (src/engine.rs:123-139, 169-199);
+  * configs[2] (C3): large-v3, VAD, DTW, greedy, 120 s, the same chain;
+  both against the oracle's output committed as fixtures (tests/golden/make_pipeline_fixtures.py
+  ran the oracle -- VAD + merge (src/vad.rs:6-84), run_transcription_pipeline
+  (src/transcribe.rs:323-535), formatting with the VAD mask (src/engine.rs:192-199) -- in the
+  build container; the GPU box only compares): VAD mask and segments equal, every cue's text
+  equal, every word and cue bound within north_star's +-20 ms;
   * configs[3]'s per-GPU shard at full size: 1 h of 3-speaker synthetic audio, large-v3 + DTW
     + pyannote diarization + speaker assignment (the bench workload) -- the oracle cannot follow
     an hour of large-v3 in a test, so its output is held to the properties the reference's glue
@@ -19,76 +22,68 @@ oracle can follow, by properties where it cannot (VERDICT r2 "next round" item 1
     they are counted, not rejected.
 
 Synthetic weights on both sides (seeded, bit-identical), decode length pinned.
-Tolerances as tests/test_gpu_baseline_models.py: segment text equal; words within 20 ms
-(>= 90 %, the rest within 40 ms: a DTW anchor two frames off a near-tie of the random-weight
-alignment matrix moves a midpoint bound by 20-40 ms).
+The fixtures' weights are N(0, 0.05) ("alignment-conditioned", make_pipeline_fixtures.py): at
+0.02 the alignment heads' cross-attention is near-uniform and the DTW path has competitors
+within f32 rounding of its cost (tests/test_gpu_baseline_models.py test_c1_flat_alignment_near_ties).
 """
+import json
+import os
 import re
 
-import numpy as np
 import pytest
 
 import wdr
-from oracle import formatting as F
-from oracle.model import Whisper
-from oracle.pipeline import SpeechSegment as OSeg
-from oracle.pipeline import run_transcription_pipeline, write_wav
-from oracle.vad import get_segments as oracle_vad
-from oracle.vocab import Vocab
-from oracle.weights import hparams_for, synth_weights
-from oracle.whisper_full import WhisperState
+from oracle.pipeline import write_wav
 from wdr.synth import synth_speech
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(1200)]
 
-EMB_STD = 0.5
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+TOL = 0.02 + 1e-9   # north_star: word start / end within +-20 ms of the CPU reference
 
 
-def _vad_pipeline_vs_oracle(tmp_path, model, seconds, seed, greedy):
-    pcm, _ = synth_speech(seconds, seed=seed)
+def fixture_vs_transcribe_audio(tmp_path, name):
+    """Engine::transcribe_audio on the fixture's synthetic audio and weights against the oracle's
+    committed output: (cues, max word / cue bound difference in s)."""
+    fx = json.load(open(os.path.join(GOLDEN, name)))
+    c = fx["config"]
+    pcm, _ = synth_speech(c["seconds"], seed=c["seed"])
     path = str(tmp_path / "a.wav")
     write_wav(path, pcm)
-    syn = wdr.Synthetic(weight_std=0.02, emb_std=EMB_STD, force_len_rate=3.3, disable_fallback=True)
+    syn = wdr.Synthetic(weight_std=c["weight_std"], emb_std=c["emb_std"], force_len_rate=c["force_len_rate"],
+                        disable_fallback=not c["fallback"])
     eng = wdr.Engine(wdr.EngineConfig(cache_dir=str(tmp_path / "cache")), synthetic=syn)
-    adv = wdr.AdvancedTranscribe(sampling_strategy="greedy") if greedy else None
-    opts = wdr.TranscribeOptions(model=model, enable_vad=True, advanced=adv)   # lang auto, DTW on
+    adv = wdr.AdvancedTranscribe(sampling_strategy="greedy") if c["greedy"] else None
+    opts = wdr.TranscribeOptions(model=c["model"], enable_vad=c["vad"], advanced=adv)   # lang auto, DTW on
     got = eng.transcribe_audio(path, opts)
-    # oracle: VAD + merge on the same (synthetic Silero) weights, then the pipeline + formatting
-    mask, vsegs = oracle_vad(pcm)
-    gmask, gsegs = wdr.Vad().get_segments(pcm)
-    assert [(round(a, 6), round(b, 6)) for a, b in gmask] == [(round(a, 6), round(b, 6)) for a, b in mask]
-    assert [(s.start, s.end) for s in gsegs] == [(s.start, s.end) for s in vsegs] and len(vsegs) >= 1
-    hp = hparams_for(model)
-    st = WhisperState(Whisper(hp, synth_weights(hp, std=0.02, emb_std=EMB_STD)), Vocab(hp.n_vocab), model)
-    o = dict(lang="auto", synthetic=dict(force_len_rate=3.3, logprob_thold=-np.inf, entropy_thold=-1.0))
-    if greedy:
-        o["advanced"] = dict(sampling_strategy="greedy")
-    raw, lang = run_transcription_pipeline(st, [OSeg(s.start, s.end, s.samples) for s in vsegs], o)
-    want = F.process_segments([F.Seg(s.start, s.end, s.text, None if s.words is None else
-                                     [F.Word(w.text, w.start, w.end, w.probability) for w in s.words], None)
-                               for s in raw], F.config_for_language(lang or "auto"), mask)
+    eng.close()
+    if c["vad"]:
+        gmask, gsegs = wdr.Vad().get_segments(pcm)
+        assert [(round(a, 6), round(b, 6)) for a, b in gmask] == [(round(a, 6), round(b, 6)) for a, b in fx["vad_mask"]]
+        assert [[s.start, s.end] for s in gsegs] == fx["vad_segments"]
+    want = fx["formatted"]
     assert len(got) == len(want) >= 1, (len(got), len(want))
     dts = []
     for g, w in zip(got, want):
-        assert g.text == w.text, (g.text, w.text)
-        assert len(g.words or []) == len(w.words or [])
-        for a, b in zip(g.words or [], w.words or []):
-            assert a.text == b.text
-            dts += [abs(a.start - b.start), abs(a.end - b.end)]
-        dts += [abs(g.start - w.start), abs(g.end - w.end)]
-    within = sum(d <= 0.02 + 1e-9 for d in dts) / max(1, len(dts))
-    assert max(dts) <= 0.04 + 1e-9 and within >= 0.9, (max(dts), within)
-    return len(vsegs), len(got), max(dts), within
+        assert g.text == w["text"], (g.text, w["text"])
+        gw, ww = g.words or [], w["words"] or []
+        assert [a.text for a in gw] == [b[0] for b in ww]
+        for a, b in zip(gw, ww):
+            dts += [abs(a.start - b[1]), abs(a.end - b[2])]
+        dts += [abs(g.start - w["start"]), abs(g.end - w["end"])]
+    dw = max(dts)
+    assert dw <= TOL, (dw, sorted(dts)[-5:])
+    return len(got), dw
 
 
-def test_c2_base_en_vad_beam5_dtw(tmp_path):
-    n_vad, n_out, dw, within = _vad_pipeline_vs_oracle(tmp_path, "base.en", 60.0, 51, greedy=False)
-    print(dict(test="c2", vad_segments=n_vad, segments=n_out, word_max_dt=dw, within_20ms=within))
+def test_c2_base_en_vad_beam5_dtw_600s(tmp_path):
+    n, dw = fixture_vs_transcribe_audio(tmp_path, "c2_base_en_600s.json")
+    print(dict(test="c2", seconds=600, cues=n, word_max_dt=dw))
 
 
-def test_c3_large_v3_vad_greedy_dtw(tmp_path):
-    n_vad, n_out, dw, within = _vad_pipeline_vs_oracle(tmp_path, "large-v3", 30.0, 52, greedy=True)
-    print(dict(test="c3", vad_segments=n_vad, segments=n_out, word_max_dt=dw, within_20ms=within))
+def test_c3_large_v3_vad_greedy_dtw_120s(tmp_path):
+    n, dw = fixture_vs_transcribe_audio(tmp_path, "c3_large_v3_120s.json")
+    print(dict(test="c3", seconds=120, cues=n, word_max_dt=dw))
 
 
 _MARKER = re.compile(r"\[_|<\||\|>|_\]")

@@ -76,32 +76,6 @@ def test_encoder_gemm_tiles(lib, N, monkeypatch):
     np.testing.assert_array_equal(_proj(lib, a, w, bias, 2, base), resid)
 
 
-STEP = 0x100   # include/wdr.h WDR_DBG_PROJ_STEP
-
-
-@pytest.mark.parametrize("N,K,epi", [(1280, 5120, 2), (1280, 4096, 2), (1280, 1280, 2), (3840, 1280, 0),
-                                     (5120, 1280, 1)])
-def test_step_projection_rows_bit_identical(lib, N, K, epi):
-    """Decode-step GEMV schedule (ProjArgs::step_rows): every row of an M-row step (M = 1..16:
-    k_dgemv, k_mgemv_s 4/8/16-row images, the K > 3072 two-pass 8-row image) must equal the
-    1-row step's result for that row bit for bit -- batched chains depend on it -- and match
-    the fp64 product within f16-operand accumulation error."""
-    rng = np.random.default_rng(N + K + epi)
-    a = rng.standard_normal((16, K)).astype(np.float16).astype(np.float32)
-    w = (rng.standard_normal((N, K)) * 0.03).astype(np.float16).astype(np.float32)
-    bias = rng.standard_normal(N).astype(np.float32) * 0.1
-    base = rng.standard_normal((16, N)).astype(np.float32)
-    ref = a.astype(np.float64) @ w.T.astype(np.float64) + bias
-    one = np.concatenate([_proj(lib, a[i:i + 1], w, bias, epi | STEP, base[i:i + 1] if epi == 2 else None)
-                          for i in range(16)])
-    want = {0: ref, 1: _gelu(ref), 2: base + ref}[epi]
-    tol = dict(rtol=0, atol=2e-4) if epi == 2 else dict(rtol=2e-3, atol=2e-3)
-    np.testing.assert_allclose(one, want, **tol)
-    for M in (2, 3, 5, 8, 9, 12, 16):
-        got = _proj(lib, a[:M], w, bias, epi | STEP, base[:M] if epi == 2 else None)
-        np.testing.assert_array_equal(got, one[:M], err_msg="M=%d" % M)
-
-
 ROWS = 0x200   # include/wdr.h WDR_DBG_PROJ_ROWS
 
 
@@ -132,7 +106,7 @@ def test_rows_projection_bit_identical_any_m(lib, N, K, epi):
 
 
 def test_projection_logits_shape(lib):
-    """decoder logits: N not a multiple of the tile (51866 x d), M = 1 (GEMV path)."""
+    """decoder logits: N not a multiple of the tile (51866 x d), M = 1 (the row kernel)."""
     rng = np.random.default_rng(7)
     K, N = 128, 51866
     a = rng.standard_normal((1, K)).astype(np.float16).astype(np.float32)
@@ -247,23 +221,6 @@ def test_decode_cross_attention_mma_tiles(lib):
     split = grp.copy()
     split[0], split[12] = 12, 28
     np.testing.assert_array_equal(_xattn(lib, q, kv, H, slot, split), got)
-
-
-@pytest.mark.parametrize("N,K,epi", [(1280, 5120, 2), (3840, 1280, 0)])
-def test_step_projection_wide_batches(lib, N, K, epi):
-    """Batched steps of more than 16 rows (beams of many segments) run as one multi-pass launch
-    (k_mgemv_sp: 16 or 8 rows per pass, the weights streamed once): every row equals its one-row
-    result bit for bit."""
-    rng = np.random.default_rng(N + K)
-    a = rng.standard_normal((80, K)).astype(np.float16).astype(np.float32)
-    w = (rng.standard_normal((N, K)) * 0.03).astype(np.float16).astype(np.float32)
-    bias = rng.standard_normal(N).astype(np.float32) * 0.1
-    base = rng.standard_normal((80, N)).astype(np.float32)
-    one = np.concatenate([_proj(lib, a[i:i + 1], w, bias, epi | STEP, base[i:i + 1] if epi == 2 else None)
-                          for i in range(0, 80, 7)])
-    for M in (17, 40, 80):
-        got = _proj(lib, a[:M], w, bias, epi | STEP, base[:M] if epi == 2 else None)
-        np.testing.assert_array_equal(got[0:M:7], one[:len(range(0, M, 7))], err_msg="M=%d" % M)
 
 
 def test_signal_energy_is_bit_exact(lib):

@@ -55,3 +55,51 @@ def test_two_models_equal_one(name, seconds, strategy, chains, monkeypatch):
     assert lang == lang1
     assert got == ref
     two.close()
+
+
+def _progress(**kw):
+    """A line under gpurun_out/ between the phases of a long test (the GPU box treats minutes of
+    silence as a hang)."""
+    import json
+    import os
+    p = os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", "multidevice_progress.jsonl")
+    try:
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        with open(p, "a") as f:
+            f.write(json.dumps(kw) + "\n")
+    except OSError:
+        pass
+
+
+@pytest.mark.timeout(1500)
+def test_configs3_split_eight_logical_devices(monkeypatch):
+    """BASELINE configs[3]'s split at full size on one GPU: a 4-h, 3-speaker large-v3 + DTW +
+    diarization run (speaker embeddings + assignment) through run_pipeline with
+    WDR_DEVICES=0,0,0,0,0,0,0,0 -- eight models, eight step batchers and DTW queues, 3 decode
+    chains each: 24 speculative blocks over 8 "GPUs" and the exact prompt fix-up rounds across
+    them (src/engine.rs:14, src/transcribe.rs:110-112) -- must equal one model with 24 chains bit
+    for bit (which the chain tests pin to one chain).  Greedy decode (the bench's), so the 4 h
+    fit the test's time."""
+    syn = wdr.Synthetic(weight_std=0.02, emb_std=0.02, force_len_rate=3.3, disable_fallback=True)
+    pcm, spurts = synth_speech(14400.0, seed=1, n_speakers=3)
+    segs = _segs(pcm, spurts)
+    _progress(phase="audio", segments=len(segs))
+    opts = wdr.TranscribeOptions(model="large-v3", lang="auto", enable_vad=False, enable_diarize=True,
+                                 advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    dopts = wdr.DiarizeOptions.from_options(opts)
+    one = wdr.WhisperContext("large-v3", gpu_device=0, enable_dtw=True, synthetic=syn)
+    one.set_chains(24)
+    ref, lang1 = one.run_pipeline(segs, opts, diarize_options=dopts)
+    one.close()
+    _progress(phase="one device", segments=len(ref))
+    monkeypatch.setenv("WDR_DEVICES", ",".join(["0"] * 8))
+    eight = wdr.WhisperContext("large-v3", enable_dtw=True, synthetic=syn)
+    assert eight.devices == [0] * 8
+    eight.set_chains(3)
+    got, lang = eight.run_pipeline(segs, opts, diarize_options=dopts)
+    st = eight.stage_times()
+    eight.close()
+    _progress(phase="eight devices", segments=len(got), fixups=st.get("fixup_segments"), chains=st.get("chains"))
+    assert st["chains"] == 24
+    assert lang == lang1 and len(got) == len(ref) >= 2000
+    assert [dataclasses.asdict(s) for s in got] == [dataclasses.asdict(s) for s in ref]

@@ -281,3 +281,33 @@ def test_engine_whole_file_path(tmp_path, translate):
         [(s.text, round(s.start, 6), round(s.end, 6)) for s in want]
     assert [[(w.text, round(w.start, 6), round(w.end, 6)) for w in s.words] for s in got] == \
         [[(w.text, round(w.start, 6), round(w.end, 6)) for w in s.words] for s in want]
+
+
+@pytest.mark.parametrize("chains", [1, 4])
+def test_cancellation_through_c_abi(chains):
+    """Callbacks::is_cancelled (src/engine.rs:35-40) wired to whisper.cpp's abort callback
+    (src/transcribe.rs:348-350): once it returns true the run stops with "failed to transcribe"
+    -- polled before each segment (one chain) or by the calling thread while the decode chains
+    run (multi-chain: chains stop at their next segment).  The context is reusable afterwards:
+    the next uncancelled run equals a fresh one (no stale DTW job, batcher seat or slot left)."""
+    name = "tiny-test"
+    ctx = wdr.WhisperContext(name, synthetic=SYN)
+    ctx.set_chains(chains)
+    pcm, spurts = synth_speech(40.0, seed=0)
+    segs = [wdr.SpeechSegment(a, b, pcm[int(a * 16000):int(b * 16000)]) for a, b, _ in spurts]
+    assert len(segs) >= 6
+    opts = wdr.TranscribeOptions(lang="auto", advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    ref, _ = ctx.run_pipeline(segs, opts)
+    seen = []
+    if chains == 1:
+        cb = wdr.Callbacks(new_segment_callback=lambda s: seen.append(s.text), is_cancelled=lambda: len(seen) >= 2)
+    else:
+        cb = wdr.Callbacks(new_segment_callback=lambda s: seen.append(s.text), is_cancelled=lambda: True)
+    with pytest.raises(wdr.WdrError, match="failed to transcribe"):
+        ctx.run_pipeline(segs, opts, cb)
+    assert len(seen) < len(ref)
+    if chains == 1:
+        assert seen == [s.text for s in ref[:len(seen)]] and len(seen) >= 2
+    again, _ = ctx.run_pipeline(segs, opts)
+    assert [(s.text, s.start, s.end) for s in again] == [(s.text, s.start, s.end) for s in ref]
+    ctx.close()

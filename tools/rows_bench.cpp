@@ -1,9 +1,9 @@
-// Decoder-row projection microbenchmark (large-v3 decoder shapes): the decode step's GEMV
-// schedule (launch_proj with step_rows, LayerNorm by k_ln_rows above 2 rows, as
-// decode_step_layers issues it) against the row kernel (ProjArgs::rows_mma: k_skinny's
-// arithmetic for any row count, LayerNorm fused up to 32 rows), per launch, replayed from a
-// hipGraph of 32 launches over 32 distinct weight copies (> the 256 MiB Infinity Cache).
-// Build: make -C whisper-diarize-rs_amd rows_bench ; run on the GPU box.
+// Decoder-row projection microbenchmark (large-v3 decoder shapes): the row kernel
+// (ProjArgs::rows_mma: k_skinny's arithmetic for any row count, LayerNorm fused up to 32 rows),
+// per launch, replayed from a hipGraph of 32 launches over 32 distinct weight copies (> the
+// 256 MiB Infinity Cache).
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/rows_bench.cpp -Lwhisper-diarize-rs_amd -lwdr \
+//          -Wl,-rpath,'$ORIGIN/../whisper-diarize-rs_amd' -o tools/rows_bench
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -80,8 +80,7 @@ int main(int argc, char** argv) {
   CK(hipMemset(b, 0, 4 * d * 4));
   CK(hipMemset(bias, 0, 51866 * 4));
   CK(hipMemset(xa, 0, (size_t)MX * 4 * d * 2));
-  printf("%-14s %4s %10s %10s %8s   (us per launch incl. LN launch; TB/s of the weights)\n", "shape", "M", "gemv", "rows",
-         "rows/gemv");
+  printf("%-14s %4s %10s   (us per launch incl. LN launch; TB/s of the weights)\n", "shape", "M", "rows");
   for (const Shape& sh : shapes) {
     const size_t wel = (size_t)sh.N * sh.K;
     const int nl = sh.N > 10000 ? 4 : L;   // the logits weights once per step
@@ -92,25 +91,6 @@ int main(int argc, char** argv) {
     }
     const double mb = wel * 2 / 1e6;
     for (int M : Ms) {
-      // the decode step's schedule (decode_step_layers: LN by k_ln_rows above 2 rows)
-      float tg = -1.f;
-      {
-        tg = time_graph([&] {
-          for (int l = 0; l < nl; ++l) {
-            ProjArgs a{xa, sh.K, W[l], sh.K, bias, out, sh.N, nullptr, 0, M, sh.N, sh.K, sh.epi};
-            a.step_rows = 1;
-            if (sh.ln) {
-              a.ln_x = xf; a.ldln = sh.K; a.ln_g = g; a.ln_b = b;
-              if (M > 2) {
-                launch_ln_rows(a, hd, d, s);
-                a.ln_x = nullptr;
-                a.A = hd;
-              }
-            }
-            launch_proj(a, s);
-          }
-        }, s, 10);
-      }
       const float tr = time_graph([&] {
         for (int l = 0; l < nl; ++l) {
           ProjArgs a{xa, sh.K, W[l], sh.K, bias, out, sh.N, nullptr, 0, M, sh.N, sh.K, sh.epi};
@@ -126,9 +106,8 @@ int main(int argc, char** argv) {
           launch_proj(a, s);
         }
       }, s, 10);
-      const double ug = tg * 1e3 / nl, ur = tr * 1e3 / nl;
-      printf("%-14s %4d %7.2f us %7.2f us %8.2f   %5.2f / %5.2f TB/s\n", sh.name, M, ug, ur, tg > 0 ? ur / ug : 0.0,
-             tg > 0 ? mb / ug / 1e3 : 0.0, mb / ur / 1e3);
+      const double ur = tr * 1e3 / nl;
+      printf("%-14s %4d %7.2f us   %5.2f TB/s\n", sh.name, M, ur, mb / ur / 1e3);
       fflush(stdout);
     }
     for (int l = 0; l < nl; ++l) CK(hipFree(W[l]));

@@ -92,9 +92,6 @@ struct ProjArgs {
   // EPI_QKV_CACHE
   f16* kc = nullptr; f16* vc = nullptr; long long seq_stride = 0; const int* row_seq = nullptr;
   const int* row_pos = nullptr; int d = 0;
-  // decode-step rows (up to 16, the multi-chain batched step): stay on the GEMV kernels, whose
-  // per-row arithmetic does not depend on the row count
-  int step_rows = 0;
   unsigned long long* ts = nullptr;   // live kernel clock of a sampled launch (ProfClock)
   // fp8 (OCP e4m3) operands (launch_proj_fp8): A8 [M][lda] and B8 [N][ldb] bytes, dequantised
   // in the epilogue by a_scale[row] * b_scale[col] (per-row / per-output-channel scales)
@@ -136,6 +133,8 @@ template <typename A>
 inline unsigned long long* prof_attach(A&) { return nullptr; }
 inline unsigned long long* prof_attach(ProjArgs& a) { return a.ts = prof_slot(); }
 void launch_proj(const ProjArgs& a, hipStream_t s);   // picks GEMV (M<=8) or MFMA GEMM
+// WDR_ROWS_LEAN A/B mode of the row projections (gemm.hip): 0 off, 1 lean for K <= 2048, 2 also fc2
+int rows_lean();
 // fp8 encoder GEMM (BASELINE configs[4]): ProjArgs::A8 / B8 / a_scale / b_scale, M > 64,
 // N % 128 == 0, K % 128 == 0; epilogues as launch_proj
 void launch_proj_fp8(const ProjArgs& a, hipStream_t s);
@@ -143,6 +142,5 @@ void launch_proj_fp8(const ProjArgs& a, hipStream_t s);
 void launch_quant_rows(const f16* x, int ldx, int M, int K, uint8_t* y, int ldy, float* scale, hipStream_t s);
 // the LayerNorm prologue of a decode-step projection as its own launch (k_dgemv's arithmetic):
 // rows ln_x -> y [M][ldy] f16
-void launch_ln_rows(const ProjArgs& a, f16* y, int ldy, hipStream_t s);
 
 }  // namespace wdr

@@ -24,6 +24,7 @@
 #include <condition_variable>
 #include <exception>
 #include <mutex>
+#include <set>
 #include <thread>
 #include <vector>
 
@@ -34,6 +35,7 @@
 #include "whisper.h"
 #include "ggml_file.h"
 #include "model_files.h"
+#include "prof.h"
 
 using namespace wdr;
 
@@ -984,6 +986,7 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
     m.mel += t.mel; m.encode += t.encode; m.decode += t.decode; m.dtw += t.dtw;
     m.windows += t.windows; m.decode_steps += t.decode_steps; m.prefills += t.prefills;
     m.lang += t.lang; m.prompt_gpu += t.prompt_gpu;
+    m.lang_passes += t.lang_passes; m.lang_rows += t.lang_rows;
   }
   return out;
 }
@@ -1271,7 +1274,61 @@ static int diar_segments_out(const std::vector<DiarSegment>& ds, const int16_t* 
   }
 }
 
+// ------------------------------------------------------------------ live handles and teardown
+// Every handle libwdr hands out is registered until it is freed, so that wdr_shutdown (and the
+// process-exit hook below) can release what the host left alive -- contexts with their worker
+// threads (DTW queue, encode-ahead, step batchers), streams, device memory -- while the HIP
+// runtime is still up.  A free of a handle that is no longer registered (freed already, or
+// released by wdr_shutdown) does nothing.
+namespace {
+struct Live {
+  std::mutex mu;
+  std::set<void*> eng, ctx, vad, dia, spk;
+};
+Live& live() {
+  static Live* l = new Live();   // never destroyed: the exit hook and late frees may run after statics
+  return *l;
+}
+void wdr_exit_hook() { wdr_shutdown(); }
+template <typename T>
+T* track(std::set<void*> Live::*set, T* p) {
+  static std::once_flag once;
+  // registered after the HIP runtime has initialised (its first handle needs it): exit runs this
+  // hook before the runtime's own teardown (handlers run in reverse order of registration)
+  std::call_once(once, [] { std::atexit(wdr_exit_hook); });
+  std::lock_guard<std::mutex> g(live().mu);
+  (live().*set).insert(p);
+  return p;
+}
+template <typename T>
+bool untrack(std::set<void*> Live::*set, T* p) {
+  if (!p) return false;
+  std::lock_guard<std::mutex> g(live().mu);
+  return (live().*set).erase(p) > 0;
+}
+}  // namespace
+
 extern "C" {
+
+void wdr_shutdown(void) {
+  std::set<void*> eng, ctx, vad, dia, spk;
+  {
+    std::lock_guard<std::mutex> g(live().mu);
+    eng.swap(live().eng);
+    ctx.swap(live().ctx);
+    vad.swap(live().vad);
+    dia.swap(live().dia);
+    spk.swap(live().spk);
+  }
+  // engines own their cached contexts; contexts join their threads and free their device memory
+  for (void* p : eng) delete (wdr_engine*)p;
+  for (void* p : ctx) delete (wdr_context*)p;
+  for (void* p : vad) delete (wdr_vad*)p;
+  for (void* p : dia) delete (wdr_diarizer*)p;
+  for (void* p : spk) delete (wdr_speakers*)p;
+  destroy_stream_pools();
+  prof_shutdown();
+}
 
 const char* wdr_last_error(void) { return g_err.c_str(); }
 int wdr_abi_version(void) { return WDR_ABI_VERSION; }
@@ -1297,12 +1354,14 @@ int wdr_engine_new(const wdr_engine_config* cfg, wdr_engine** out) {
       e->cfg.use_gpu = 1;
       e->cache_dir = "./cache";
     }
-    *out = e;
+    *out = track(&Live::eng, e);
     return 0;
   })
 }
 
-void wdr_engine_free(wdr_engine* e) { delete e; }
+void wdr_engine_free(wdr_engine* e) {
+  if (untrack(&Live::eng, e)) delete e;
+}
 
 int wdr_engine_set_synthetic(wdr_engine* e, const wdr_synthetic* syn) {
   WDR_GUARD({
@@ -1405,12 +1464,14 @@ int wdr_vad_create(const char* model_path, int8_t has_gpu_device, int32_t gpu_de
     if (model_path && !file_exists(model_path)) return fail(std::string("VAD model file doesn't exist: ") + model_path);
     auto v = std::make_unique<wdr_vad>();
     v->m = std::make_unique<VadModel>(has_gpu_device ? gpu_device : 0, model_path ? model_path : "");
-    *out = v.release();
+    *out = track(&Live::vad, v.release());
     return 0;
   })
 }
 
-void wdr_vad_free(wdr_vad* v) { delete v; }
+void wdr_vad_free(wdr_vad* v) {
+  if (untrack(&Live::vad, v)) delete v;
+}
 
 int wdr_vad_probs(wdr_vad* v, const int16_t* samples, size_t n, float* probs_out, double* us_per_step) {
   WDR_GUARD({
@@ -1472,12 +1533,14 @@ int wdr_diarizer_create(const char* segment_model_path, const char* embedding_mo
     // load eagerly: a bad file fails here, as ORT session creation does in the reference
     if (!d->seg_path.empty()) d->S();
     if (!d->emb_path.empty()) d->E();
-    *out = d.release();
+    *out = track(&Live::dia, d.release());
     return 0;
   })
 }
 
-void wdr_diarizer_free(wdr_diarizer* d) { delete d; }
+void wdr_diarizer_free(wdr_diarizer* d) {
+  if (untrack(&Live::dia, d)) delete d;
+}
 
 int wdr_diarize_frame_classes(wdr_diarizer* d, const int16_t* samples, size_t n, int32_t* cls_out, float* logprobs_out) {
   WDR_GUARD({
@@ -1542,12 +1605,14 @@ int wdr_speakers_new(int8_t has_max_speakers, uint64_t max_speakers, wdr_speaker
   WDR_GUARD({
     auto m = std::make_unique<wdr_speakers>();
     m->m = std::make_unique<SpeakerManager>((has_max_speakers && max_speakers != 0) ? max_speakers : UINT64_MAX);
-    *out = m.release();
+    *out = track(&Live::spk, m.release());
     return 0;
   })
 }
 
-void wdr_speakers_free(wdr_speakers* m) { delete m; }
+void wdr_speakers_free(wdr_speakers* m) {
+  if (untrack(&Live::spk, m)) delete m;
+}
 
 int wdr_speakers_assign(wdr_speakers* m, const float* emb, int32_t dim, float threshold, char* id_out, size_t cap) {
   WDR_GUARD({
@@ -1685,14 +1750,16 @@ int wdr_context_create(const char* model_path, const char* model_name, int8_t ha
   WDR_GUARD({
     if (model_path && *model_path && !file_exists(model_path)) return fail("whisper file doesn't exist");
     if ((!model_path || !*model_path) && !syn) return fail("whisper file doesn't exist");
-    *out = make_context(model_name ? model_name : "base", has_gpu_device == 1, gpu_device, use_gpu, enable_dtw,
-                        syn_of(syn), model_path ? std::string(model_path) : std::string())
-               .release();
+    *out = track(&Live::ctx, make_context(model_name ? model_name : "base", has_gpu_device == 1, gpu_device, use_gpu,
+                                          enable_dtw, syn_of(syn), model_path ? std::string(model_path) : std::string())
+                                 .release());
     return 0;
   })
 }
 
-void wdr_context_free(wdr_context* c) { delete c; }
+void wdr_context_free(wdr_context* c) {
+  if (untrack(&Live::ctx, c)) delete c;
+}
 
 int wdr_ggml_info(const char* path, int32_t* hparams, int64_t* n_tensors, int64_t* n_vocab_tokens) {
   WDR_GUARD({
@@ -1832,6 +1899,8 @@ int wdr_context_stage_times(wdr_context* c, wdr_stage_times* o) {
     o->dtwq_passes = c->cs.dq_passes;
     o->dtwq_rows = c->cs.dq_rows;
     o->dtwq_jobs = c->cs.dq_jobs;
+    o->lang_passes = t.lang_passes;
+    o->lang_rows = t.lang_rows;
     return 0;
   })
 }
@@ -2050,16 +2119,15 @@ int wdr_dbg_proj(const uint16_t* a16, const uint16_t* w16, const float* bias, in
     WDR_HIP(hipMemcpy(da.p, a16, da.bytes, hipMemcpyHostToDevice));
     WDR_HIP(hipMemcpy(dw.p, w16, dw.bytes, hipMemcpyHostToDevice));
     if (bias) WDR_HIP(hipMemcpy(db.p, bias, db.bytes, hipMemcpyHostToDevice));
-    // epi | WDR_DBG_PROJ_STEP: the decode-step schedule (ProjArgs::step_rows, 9..16-row shapes);
-    // epi | WDR_DBG_PROJ_ROWS: the decoder-rows kernel (ProjArgs::rows_mma, any M)
-    const bool step = (epi & 0x100) != 0;
+    // epi | WDR_DBG_PROJ_ROWS: the decoder-rows kernel (ProjArgs::rows_mma, any M); <= 64 rows
+    // run on it anyway
+    if (epi & 0x100) return fail("WDR_DBG_PROJ_STEP: the decode-step GEMV schedule was removed (the row kernel serves every row count)");
     const bool rows = (epi & 0x200) != 0;
     epi &= 0xff;
     const bool f16out = epi == EPI_F16 || epi == EPI_F16_GELU;
     std::vector<f16> h16;
     if (!f16out) WDR_HIP(hipMemcpy(dout.p, out, dout.bytes, hipMemcpyHostToDevice));
     ProjArgs a{da.as<f16>(), K, dw.as<f16>(), K, bias ? db.as<float>() : nullptr, dout.p, N, nullptr, 0, M, N, K, epi};
-    a.step_rows = step ? 1 : 0;
     a.rows_mma = rows ? 1 : 0;
     launch_proj(a, nullptr);
     WDR_HIP(hipDeviceSynchronize());

@@ -254,9 +254,10 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* x, int ldx, cons
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
   const float* xr = x + (long long)(row_map ? row_map[row] : row) * ldx;
-  // d <= 1280: each lane keeps its <= 20 values in registers; fully unrolled (compile-time
-  // indices keep them out of scratch) and gamma / beta are loaded together with x
-  float v[5][4], gg[5][4], bb[5][4];
+  // d <= 1280: each lane keeps its <= 20 values in registers (fully unrolled: compile-time
+  // indices keep them out of scratch); gamma / beta are read only in the output loop, so the
+  // kernel stays under 64 VGPRs and fits beside an encoder GEMM tile on a CU
+  float v[5][4];
   float s = 0.f;
 #pragma unroll
   for (int j = 0; j < 5; ++j) {
@@ -264,11 +265,7 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* x, int ldx, cons
     const bool ok = c < d;
     const int cc = ok ? c : 0;
     const float4 q = *(const float4*)(xr + cc);
-    const float4 g4 = *(const float4*)(g + cc);
-    const float4 b4 = *(const float4*)(b + cc);
     v[j][0] = ok ? q.x : 0.f; v[j][1] = ok ? q.y : 0.f; v[j][2] = ok ? q.z : 0.f; v[j][3] = ok ? q.w : 0.f;
-    gg[j][0] = g4.x; gg[j][1] = g4.y; gg[j][2] = g4.z; gg[j][3] = g4.w;
-    bb[j][0] = b4.x; bb[j][1] = b4.y; bb[j][2] = b4.z; bb[j][3] = b4.w;
     s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
   }
   s = wave_sum(s);
@@ -289,9 +286,12 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* x, int ldx, cons
   for (int j = 0; j < 5; ++j) {
     const int c = lane * 4 + j * 256;
     if (c >= d) continue;
+    const float4 g4 = *(const float4*)(g + c);
+    const float4 b4 = *(const float4*)(b + c);
+    const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, bb[4] = {b4.x, b4.y, b4.z, b4.w};
     f16x4 o;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = (f16)((v[j][e] - mean) * scale * gg[j][e] + bb[j][e]);
+    for (int e = 0; e < 4; ++e) o[e] = (f16)((v[j][e] - mean) * scale * gg[e] + bb[e]);
     *(f16x4*)(yr + c) = o;
   }
 }

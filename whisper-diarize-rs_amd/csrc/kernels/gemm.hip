@@ -1,15 +1,16 @@
 // Projection kernels: the dense contractions of the Whisper encoder / decoder
 // (SURVEY.md §8(a) a5-a7, a9, a12).
 //
-//  * k_gemm  — MFMA GEMM for M > 8 rows (encoder windows, cross-K/V, prompt prefill,
-//              DTW re-forward):  C[M][N] = A[M][K] . B[N][K]^T  (+ fused epilogue).
+//  * k_gemm  — MFMA GEMM for M > 64 rows (encoder windows, cross-K/V; the general fallback
+//              of the tiled family k_gemm2..5):  C[M][N] = A[M][K] . B[N][K]^T  (+ fused epilogue).
 //              f16 operands (what ggml's mul_mat feeds: f16 weights, activations cast to
 //              f16), f32 accumulation, v_mfma_f32_32x32x16_f16.  128x128x32 block tile,
 //              4 waves of 64x64, register-staged double-buffered LDS, row padding for
 //              conflict-free ds_read_b128.  Roofline: MFMA (2.5 PF/s dense f16).
-//  * k_gemv  — M <= 8 rows (decoder step, one row per decoder): each wave streams one
-//              weight row with 16-B loads, v_dot2_f32_f16, wave-shuffle reduction.
-//              Roofline: HBM (bytes = N*K*2 per launch).
+//  * k_skinny — the decoder row kernel (any row count; decode steps, prompt prefills, DTW
+//              re-forwards, language detection) and every other projection of <= 64 rows:
+//              16-row MFMA tiles, K split over the waves in a fixed order, so a row's result
+//              does not depend on the launch's other rows.  Roofline: HBM (N*K*2 per launch).
 #include "../common.h"
 #include "../prof.h"
 
@@ -903,741 +904,6 @@ void launch_quant_rows(const f16* x, int ldx, int M, int K, uint8_t* y, int ldy,
   WDR_HIP(hipGetLastError());
 }
 
-// ---------------------------------------------------------------- GEMV (M <= 8)
-// Grid-stride over output rows (one weight row per wave per iteration), 16-B weight loads,
-// v_dot2_f32_f16.  With the fused LayerNorm prologue (LN, K <= 1536) every wave normalises
-// its input rows itself, straight into the registers that hold exactly the K-slices its lane
-// multiplies (lane l owns k in [512 i + 8 l, +8)): one round of loads, no LDS, no barrier.
-template <int NCH>
-__device__ __forceinline__ void ln_row_regs(const ProjArgs& a, int r, int lane, f16x8 (&xo)[NCH]) {
-  const float* xr = a.ln_x + (size_t)r * a.ldln;
-  float v[NCH][8];
-  float s = 0.f;
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int k = c * 512 + lane * 8;
-    if (k < a.K) {
-      const float4 p0 = *(const float4*)(xr + k), p1 = *(const float4*)(xr + k + 4);
-      v[c][0] = p0.x; v[c][1] = p0.y; v[c][2] = p0.z; v[c][3] = p0.w;
-      v[c][4] = p1.x; v[c][5] = p1.y; v[c][6] = p1.z; v[c][7] = p1.w;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[c][e] = 0.f;
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s += v[c][e];
-  }
-  s = wave_sum(s);
-  const float mean = s / a.K;
-  float s2 = 0.f;
-#pragma unroll
-  for (int c = 0; c < NCH; ++c)
-    if (c * 512 + lane * 8 < a.K)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float t = v[c][e] - mean;
-        s2 += t * t;
-      }
-  s2 = wave_sum(s2);
-  const float scale = 1.0f / sqrtf(s2 / a.K + 1e-5f);
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int k = c * 512 + lane * 8;
-    if (k < a.K) {
-      const float4 g0 = *(const float4*)(a.ln_g + k), g1 = *(const float4*)(a.ln_g + k + 4);
-      const float4 b0 = *(const float4*)(a.ln_b + k), b1 = *(const float4*)(a.ln_b + k + 4);
-      const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-      for (int e = 0; e < 8; ++e) xo[c][e] = (f16)((v[c][e] - mean) * scale * gg[e] + bb[e]);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) xo[c][e] = (f16)0.f;
-    }
-  }
-}
-
-__device__ __forceinline__ float dot8(f16x8 w, f16x8 x, float s) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    f16x2 wp = {w[2 * q], w[2 * q + 1]};
-    f16x2 xp = {x[2 * q], x[2 * q + 1]};
-    s = __builtin_amdgcn_fdot2(wp, xp, s, false);
-  }
-  return s;
-}
-
-template <int EPI, int MR>
-__device__ __forceinline__ void gemv_store(const ProjArgs& a, float (&acc)[MR], int lane, int n) {
-#pragma unroll
-  for (int r = 0; r < MR; ++r) acc[r] = wave_sum(acc[r]);
-  if (lane < MR && lane < a.M) {
-    float v = 0.f;
-#pragma unroll
-    for (int r = 0; r < MR; ++r)
-      if (r == lane) v = acc[r];
-    epi_store<EPI>(a, lane, n, v);
-  }
-}
-
-// Decode GEMV for M <= 2 (the hot path of every greedy step): each wave owns R consecutive
-// weight rows and issues ALL of their loads before anything else, then (optionally) the
-// LayerNorm of the activation rows -- computed once per wave and amortised over its R rows,
-// its latency hidden under the weight stream -- then the dot products and the fused epilogue.
-// grid = ceil(N / 4R), one pass, no grid-stride loop.
-template <int EPI, int MR, int R, int NCH, bool LN>
-__global__ __launch_bounds__(256) void k_dgemv(ProjArgs a) {
-  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int n0 = (blockIdx.x * 4 + wid) * R;
-  const int K = a.K, M = a.M;
-  // Every load below is unconditional (clamped address, masked value): no exec-mask branch
-  // per load, so the whole batch issues back to back.
-  int kc[NCH];
-  bool kin[NCH];
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int k = c * 512 + lane * 8;
-    kin[c] = k < K;
-    kc[c] = kin[c] ? k : K - 8;
-  }
-  // 1. activations (+ LayerNorm parameters) first: they are L2 hits, and the in-order return of
-  //    vector loads means the LayerNorm can then run while the weight stream is in flight
-  float xf[LN ? MR : 1][LN ? NCH : 1][8];
-  float gv[LN ? NCH : 1][8], bv[LN ? NCH : 1][8];
-  f16x8 xr[MR][NCH];
-#pragma unroll
-  for (int m = 0; m < MR; ++m) {
-    const int mm = m < M ? m : M - 1;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      if constexpr (LN) {
-        const float* xs = a.ln_x + (size_t)mm * a.ldln + kc[c];
-        const float4 p0 = *(const float4*)xs, p1 = *(const float4*)(xs + 4);
-        xf[m][c][0] = p0.x; xf[m][c][1] = p0.y; xf[m][c][2] = p0.z; xf[m][c][3] = p0.w;
-        xf[m][c][4] = p1.x; xf[m][c][5] = p1.y; xf[m][c][6] = p1.z; xf[m][c][7] = p1.w;
-        if (!kin[c])
-#pragma unroll
-          for (int e = 0; e < 8; ++e) xf[m][c][e] = 0.f;
-      } else {
-        const f16x8 t = *(const f16x8*)(a.A + (size_t)mm * a.lda + kc[c]);
-        xr[m][c] = kin[c] ? t : (f16x8){};
-      }
-    }
-  }
-  if constexpr (LN) {
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const float4 g0 = *(const float4*)(a.ln_g + kc[c]), g1 = *(const float4*)(a.ln_g + kc[c] + 4);
-      const float4 b0 = *(const float4*)(a.ln_b + kc[c]), b1 = *(const float4*)(a.ln_b + kc[c] + 4);
-      gv[c][0] = g0.x; gv[c][1] = g0.y; gv[c][2] = g0.z; gv[c][3] = g0.w;
-      gv[c][4] = g1.x; gv[c][5] = g1.y; gv[c][6] = g1.z; gv[c][7] = g1.w;
-      bv[c][0] = b0.x; bv[c][1] = b0.y; bv[c][2] = b0.z; bv[c][3] = b0.w;
-      bv[c][4] = b1.x; bv[c][5] = b1.y; bv[c][6] = b1.z; bv[c][7] = b1.w;
-    }
-  }
-  // 2. the weight stream: every load of the wave's R rows in flight at once
-  f16x8 wv[R][NCH];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int n = n0 + r < a.N ? n0 + r : a.N - 1;
-    const f16* w = a.B + (size_t)n * a.ldb;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const f16x8 t = *(const f16x8*)(w + kc[c]);
-      wv[r][c] = kin[c] ? t : (f16x8){};
-    }
-  }
-  const int mrow = lane < M ? lane : 0;   // lane m stores output row m
-  float pbias[R], pold[R];
-  long long cdst = 0;
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int n = n0 + r < a.N ? n0 + r : a.N - 1;
-    pbias[r] = a.bias ? a.bias[n] : 0.f;
-    pold[r] = 0.f;
-    if constexpr (EPI == EPI_F32_RESID) pold[r] = ((const float*)a.out)[(size_t)mrow * a.ldo + n];
-  }
-  if constexpr (EPI == EPI_QKV_CACHE) cdst = a.row_seq[mrow] * a.seq_stride + (long long)a.row_pos[mrow] * a.d;
-  // 3. LayerNorm (ggml_norm, eps 1e-5) once per wave, amortised over its R rows
-  if constexpr (LN) {
-#pragma unroll
-    for (int m = 0; m < MR; ++m) {
-      float sm = 0.f;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sm += xf[m][c][e];
-      sm = wave_sum(sm);
-      const float mean = sm / a.K;
-      float s2 = 0.f;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float t = xf[m][c][e] - mean;
-          s2 += kin[c] ? t * t : 0.f;
-        }
-      s2 = wave_sum(s2);
-      const float scale = 1.0f / sqrtf(s2 / a.K + 1e-5f);
-#pragma unroll
-      for (int c = 0; c < NCH; ++c)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) xr[m][c][e] = (f16)((xf[m][c][e] - mean) * scale * gv[c][e] + bv[c][e]);
-    }
-  }
-  // 4. dot products, wave reductions, fused epilogue
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int n = n0 + r;
-    float acc[MR];
-#pragma unroll
-    for (int m = 0; m < MR; ++m) {
-      acc[m] = 0.f;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) acc[m] = dot8(wv[r][c], xr[m][c], acc[m]);
-      acc[m] = wave_sum(acc[m]);
-    }
-    if (n >= a.N || lane >= MR || lane >= a.M) continue;
-    float v = acc[0];
-#pragma unroll
-    for (int m = 1; m < MR; ++m)
-      if (lane == m) v = acc[m];
-    v += pbias[r];
-    const size_t o = (size_t)lane * a.ldo + n;
-    if constexpr (EPI == EPI_F16) {
-      ((f16*)a.out)[o] = (f16)v;
-    } else if constexpr (EPI == EPI_F16_GELU) {
-      ((f16*)a.out)[o] = (f16)gelu_tanh(v);
-    } else if constexpr (EPI == EPI_F32_RESID) {
-      ((float*)a.out)[o] = pold[r] + v;
-    } else if constexpr (EPI == EPI_F32) {
-      ((float*)a.out)[o] = v;
-    } else if constexpr (EPI == EPI_QKV_CACHE) {
-      if (n < a.d) ((f16*)a.out)[o] = (f16)v;
-      else if (n < 2 * a.d) a.kc[cdst + n - a.d] = (f16)v;
-      else a.vc[cdst + n - 2 * a.d] = (f16)v;
-    } else {
-      epi_store<EPI>(a, lane, n, v - pbias[r]);
-    }
-  }
-}
-
-// Decode GEMV for 2 < M <= 8 rows (the multi-chain batched step, whisper_ctx.cpp StepBatcher):
-// k_dgemv's weight stream (each wave owns R weight rows, every load issued up front) with the
-// activation rows shared through LDS instead of registers.  With the LayerNorm prologue, wave w
-// normalises rows w, w+4 (the same arithmetic as k_dgemv, so every row's result is bit-identical
-// to the 1-row step's: multi-chain decoding equals one chain exactly) into LDS; without it the
-// rows are read per 512-wide chunk from L2.  Per (weight row, activation row) the dot product
-// runs over the chunks in the same order as k_dgemv, then the same wave reduction.
-template <int EPI, int MR, int R, int NCH, bool LN>
-__global__ __launch_bounds__(256) void k_mgemv(ProjArgs a) {
-  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
-  constexpr int KP = NCH * 512;
-  constexpr int LR = LN ? (MR + 3) / 4 : 1;   // LayerNorm rows per wave
-  extern __shared__ __attribute__((aligned(16))) f16 xsh[];   // LN: [MR][KP] normalised rows
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int n0 = (blockIdx.x * 4 + wid) * R;
-  const int K = a.K, M = a.M;
-  int kc[NCH];
-  bool kin[NCH];
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int k = c * 512 + lane * 8;
-    kin[c] = k < K;
-    kc[c] = kin[c] ? k : K - 8;
-  }
-  // 1. this wave's LayerNorm rows (+ gamma / beta) first, then the weight stream
-  float xf[LR][LN ? NCH : 1][8];
-  float gv[LN ? NCH : 1][8], bv[LN ? NCH : 1][8];
-  if constexpr (LN) {
-#pragma unroll
-    for (int j = 0; j < LR; ++j) {
-      const int m = wid + 4 * j;
-      const int mm = m < M ? m : M - 1;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const float* xs = a.ln_x + (size_t)mm * a.ldln + kc[c];
-        const float4 p0 = *(const float4*)xs, p1 = *(const float4*)(xs + 4);
-        xf[j][c][0] = p0.x; xf[j][c][1] = p0.y; xf[j][c][2] = p0.z; xf[j][c][3] = p0.w;
-        xf[j][c][4] = p1.x; xf[j][c][5] = p1.y; xf[j][c][6] = p1.z; xf[j][c][7] = p1.w;
-        if (!kin[c])
-#pragma unroll
-          for (int e = 0; e < 8; ++e) xf[j][c][e] = 0.f;
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const float4 g0 = *(const float4*)(a.ln_g + kc[c]), g1 = *(const float4*)(a.ln_g + kc[c] + 4);
-      const float4 b0 = *(const float4*)(a.ln_b + kc[c]), b1 = *(const float4*)(a.ln_b + kc[c] + 4);
-      gv[c][0] = g0.x; gv[c][1] = g0.y; gv[c][2] = g0.z; gv[c][3] = g0.w;
-      gv[c][4] = g1.x; gv[c][5] = g1.y; gv[c][6] = g1.z; gv[c][7] = g1.w;
-      bv[c][0] = b0.x; bv[c][1] = b0.y; bv[c][2] = b0.z; bv[c][3] = b0.w;
-      bv[c][4] = b1.x; bv[c][5] = b1.y; bv[c][6] = b1.z; bv[c][7] = b1.w;
-    }
-  }
-  f16x8 wv[R][NCH];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int n = n0 + r < a.N ? n0 + r : a.N - 1;
-    const f16* w = a.B + (size_t)n * a.ldb;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const f16x8 t = *(const f16x8*)(w + kc[c]);
-      wv[r][c] = kin[c] ? t : (f16x8){};
-    }
-  }
-  const int mrow = lane < M ? lane : 0;   // lane m stores output row m
-  float pbias[R], pold[R];
-  long long cdst = 0;
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int n = n0 + r < a.N ? n0 + r : a.N - 1;
-    pbias[r] = a.bias ? a.bias[n] : 0.f;
-    pold[r] = 0.f;
-    if constexpr (EPI == EPI_F32_RESID) pold[r] = ((const float*)a.out)[(size_t)mrow * a.ldo + n];
-  }
-  if constexpr (EPI == EPI_QKV_CACHE) cdst = a.row_seq[mrow] * a.seq_stride + (long long)a.row_pos[mrow] * a.d;
-  // 2. LayerNorm (ggml_norm, eps 1e-5; k_dgemv's arithmetic) into LDS
-  if constexpr (LN) {
-#pragma unroll
-    for (int j = 0; j < LR; ++j) {
-      const int m = wid + 4 * j;
-      float sm = 0.f;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sm += xf[j][c][e];
-      sm = wave_sum(sm);
-      const float mean = sm / a.K;
-      float s2 = 0.f;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float t = xf[j][c][e] - mean;
-          s2 += kin[c] ? t * t : 0.f;
-        }
-      s2 = wave_sum(s2);
-      const float scale = 1.0f / sqrtf(s2 / a.K + 1e-5f);
-      if (m < MR) {
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-          f16x8 o;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = (f16)((xf[j][c][e] - mean) * scale * gv[c][e] + bv[c][e]);
-          *(f16x8*)(xsh + m * KP + c * 512 + lane * 8) = o;
-        }
-      }
-    }
-    __syncthreads();
-  }
-  // 3. dot products chunk by chunk (activation rows from LDS / L2), reductions, epilogue
-  float acc[R][MR];
-#pragma unroll
-  for (int r = 0; r < R; ++r)
-#pragma unroll
-    for (int m = 0; m < MR; ++m) acc[r][m] = 0.f;
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    f16x8 xv[MR];
-#pragma unroll
-    for (int m = 0; m < MR; ++m) {
-      if constexpr (LN) {
-        xv[m] = *(const f16x8*)(xsh + m * KP + c * 512 + lane * 8);
-      } else {
-        const int mm = m < M ? m : M - 1;
-        const f16x8 t = *(const f16x8*)(a.A + (size_t)mm * a.lda + kc[c]);
-        xv[m] = kin[c] ? t : (f16x8){};
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-      for (int m = 0; m < MR; ++m) acc[r][m] = dot8(wv[r][c], xv[m], acc[r][m]);
-  }
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int n = n0 + r;
-#pragma unroll
-    for (int m = 0; m < MR; ++m) acc[r][m] = wave_sum(acc[r][m]);
-    if (n >= a.N || lane >= MR || lane >= a.M) continue;
-    float v = acc[r][0];
-#pragma unroll
-    for (int m = 1; m < MR; ++m)
-      if (lane == m) v = acc[r][m];
-    v += pbias[r];
-    const size_t o = (size_t)lane * a.ldo + n;
-    if constexpr (EPI == EPI_F16) {
-      ((f16*)a.out)[o] = (f16)v;
-    } else if constexpr (EPI == EPI_F16_GELU) {
-      ((f16*)a.out)[o] = (f16)gelu_tanh(v);
-    } else if constexpr (EPI == EPI_F32_RESID) {
-      ((float*)a.out)[o] = pold[r] + v;
-    } else if constexpr (EPI == EPI_F32) {
-      ((float*)a.out)[o] = v;
-    } else if constexpr (EPI == EPI_QKV_CACHE) {
-      if (n < a.d) ((f16*)a.out)[o] = (f16)v;
-      else if (n < 2 * a.d) a.kc[cdst + n - a.d] = (f16)v;
-      else a.vc[cdst + n - 2 * a.d] = (f16)v;
-    } else {
-      epi_store<EPI>(a, lane, n, v - pbias[r]);
-    }
-  }
-}
-
-
-// LayerNorm of decode-step rows into f16 with k_dgemv's in-register arithmetic (same per-lane
-// chunk order, sums and masks), so a GEMV over these rows gives exactly what the fused-LN GEMV
-// gives.  One wave per row.  Used for 9..16-row steps, where recomputing the LayerNorm of every
-// row in every GEMV workgroup (k_mgemv's LN prologue) costs more L2 traffic than the weights.
-template <int NCH>
-__global__ __launch_bounds__(64) void k_ln_rows(ProjArgs a, f16* y, int ldy) {
-  const int lane = threadIdx.x, row = blockIdx.x;
-  const int K = a.K;
-  int kc[NCH];
-  bool kin[NCH];
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int k = c * 512 + lane * 8;
-    kin[c] = k < K;
-    kc[c] = kin[c] ? k : K - 8;
-  }
-  float xf[NCH][8], gv[NCH][8], bv[NCH][8];
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const float* xs = a.ln_x + (size_t)row * a.ldln + kc[c];
-    const float4 p0 = *(const float4*)xs, p1 = *(const float4*)(xs + 4);
-    xf[c][0] = p0.x; xf[c][1] = p0.y; xf[c][2] = p0.z; xf[c][3] = p0.w;
-    xf[c][4] = p1.x; xf[c][5] = p1.y; xf[c][6] = p1.z; xf[c][7] = p1.w;
-    if (!kin[c])
-#pragma unroll
-      for (int e = 0; e < 8; ++e) xf[c][e] = 0.f;
-    const float4 g0 = *(const float4*)(a.ln_g + kc[c]), g1 = *(const float4*)(a.ln_g + kc[c] + 4);
-    const float4 b0 = *(const float4*)(a.ln_b + kc[c]), b1 = *(const float4*)(a.ln_b + kc[c] + 4);
-    gv[c][0] = g0.x; gv[c][1] = g0.y; gv[c][2] = g0.z; gv[c][3] = g0.w;
-    gv[c][4] = g1.x; gv[c][5] = g1.y; gv[c][6] = g1.z; gv[c][7] = g1.w;
-    bv[c][0] = b0.x; bv[c][1] = b0.y; bv[c][2] = b0.z; bv[c][3] = b0.w;
-    bv[c][4] = b1.x; bv[c][5] = b1.y; bv[c][6] = b1.z; bv[c][7] = b1.w;
-  }
-  float sm = 0.f;
-#pragma unroll
-  for (int c = 0; c < NCH; ++c)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) sm += xf[c][e];
-  sm = wave_sum(sm);
-  const float mean = sm / a.K;
-  float s2 = 0.f;
-#pragma unroll
-  for (int c = 0; c < NCH; ++c)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float t = xf[c][e] - mean;
-      s2 += kin[c] ? t * t : 0.f;
-    }
-  s2 = wave_sum(s2);
-  const float scale = 1.0f / sqrtf(s2 / a.K + 1e-5f);
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    if (!kin[c]) continue;
-    f16x8 o;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = (f16)((xf[c][e] - mean) * scale * gv[c][e] + bv[c][e]);
-    *(f16x8*)(y + (size_t)row * ldy + kc[c]) = o;
-  }
-}
-
-void launch_ln_rows(const ProjArgs& a, f16* y, int ldy, hipStream_t s) {
-  WDR_CHECK(a.ln_x && a.K % 8 == 0 && a.K <= 1536, "step LayerNorm rows: K must be <= 1536");
-  const int nch = cdiv(a.K, 512);
-  if (nch == 1) WDR_KLAUNCH(k_ln_rows<1>, dim3(a.M), dim3(64), 0, s, a, y, ldy);
-  else if (nch == 2) WDR_KLAUNCH(k_ln_rows<2>, dim3(a.M), dim3(64), 0, s, a, y, ldy);
-  else WDR_KLAUNCH(k_ln_rows<3>, dim3(a.M), dim3(64), 0, s, a, y, ldy);
-  WDR_HIP(hipGetLastError());
-}
-
-// Decode GEMV for 3..16 step rows without a LayerNorm prologue (o / xo / fc2, and every
-// projection of a 9..16-row step after k_ln_rows): the workgroup stages its M activation rows
-// into LDS once (issued before the weight stream, so the L2 reads overlap the HBM latency)
-// instead of every wave re-reading all rows from L2, and the R x MR dot products of a wave
-// are reduced with one reduce-scatter butterfly (V - 1 + log2(64 / V) shuffles instead of
-// 6 V).  Per (weight row, activation row) the chunk order, dot8 order and the butterfly tree
-// are those of k_dgemv / k_mgemv (each butterfly step adds the partner lane's partial of the
-// same value), so every row's result is bit-identical to the 1-row step's.
-template <int V, int O, int CNT>
-__device__ __forceinline__ void reduce_scatter_step(float (&v)[V], int lane) {
-  if constexpr (CNT > 1) {
-    constexpr int H = CNT / 2;
-    const bool up = (lane & O) != 0;
-#pragma unroll
-    for (int i = 0; i < H; ++i) {
-      const float keep = up ? v[i + H] : v[i];
-      const float send = up ? v[i] : v[i + H];
-      v[i] = keep + __shfl_xor(send, O, 64);
-    }
-  } else {
-    v[0] += __shfl_xor(v[0], O, 64);
-  }
-  if constexpr (O > 1) reduce_scatter_step<V, O / 2, (CNT > 1 ? CNT / 2 : 1)>(v, lane);
-}
-template <int V>
-__device__ __forceinline__ float reduce_scatter(float (&v)[V], int lane) {
-  static_assert(V >= 1 && V <= 64 && (V & (V - 1)) == 0, "V: power of two <= 64");
-  reduce_scatter_step<V, 32, V>(v, lane);
-  return v[0];   // the value index lane >> (6 - log2 V)
-}
-
-// NP > 1: the M <= MR * NP rows go through the LDS image MR at a time (pass p covers rows
-// p*MR .. p*MR + MR - 1) with the wave's weight rows held in registers across the passes, so a
-// K = 5120 projection (fc2) of a 9..16-row step streams its weights once from one launch
-// within an 8-row LDS image; the next pass's rows are loaded while the current one is
-// multiplied.  Per row, the arithmetic is that of the NP = 1 kernel.
-template <int EPI, int MR, int R, int NCH, int NP = 1>
-__global__ __launch_bounds__(256) void k_mgemv_s(ProjArgs a) {
-  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
-  constexpr int KP = NCH * 512, V = R * MR;
-  constexpr int SH = V >= 64 ? 0 : V >= 32 ? 1 : V >= 16 ? 2 : V >= 8 ? 3 : V >= 4 ? 4 : V >= 2 ? 5 : 6;
-  constexpr int NV = MR * KP / 8, PER = (NV + 255) / 256;
-  extern __shared__ __attribute__((aligned(16))) f16 xsh[];   // [MR][KP] activation rows
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int n0 = (blockIdx.x * 4 + wid) * R;
-  const int K = a.K, M = a.M;
-  // 1. activation rows -> registers (zero past K, rows >= M not staged: their results are dropped)
-  f16x8 t[PER];
-  auto fetch = [&](int p) {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int v = i * 256 + threadIdx.x;
-      const int m = v / (KP / 8) + p * MR, k = (v % (KP / 8)) * 8;
-      t[i] = (v < NV && m < M && k < K) ? *(const f16x8*)(a.A + (size_t)m * a.lda + k) : (f16x8){};
-    }
-  };
-  auto put = [&]() {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int v = i * 256 + threadIdx.x;
-      if (v < NV) *(f16x8*)(xsh + (size_t)v * 8) = t[i];
-    }
-  };
-  fetch(0);
-  // 2. the weight stream, every load of the wave's R rows in flight at once
-  int kc[NCH];
-  bool kin[NCH];
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int k = c * 512 + lane * 8;
-    kin[c] = k < K;
-    kc[c] = kin[c] ? k : K - 8;
-  }
-  f16x8 wv[R][NCH];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int n = n0 + r < a.N ? n0 + r : a.N - 1;
-    const f16* w = a.B + (size_t)n * a.ldb;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const f16x8 tw = *(const f16x8*)(w + kc[c]);
-      wv[r][c] = kin[c] ? tw : (f16x8){};
-    }
-  }
-  put();
-  // epilogue operands of the (weight row, activation row) this lane stores, per pass
-  const int j = lane >> SH, jr = j / MR, jm = j % MR;
-  const bool lead = (lane & ((1 << SH) - 1)) == 0 && n0 + jr < a.N;
-  const int nst = n0 + jr < a.N ? n0 + jr : a.N - 1;
-  const float pbias = a.bias ? a.bias[nst] : 0.f;
-  float pold[NP];
-  long long cdst[NP];
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int mr = jm + p * MR, mst = mr < M ? mr : 0;
-    pold[p] = 0.f;
-    cdst[p] = 0;
-    if constexpr (EPI == EPI_F32_RESID) pold[p] = ((const float*)a.out)[(size_t)mst * a.ldo + nst];
-    if constexpr (EPI == EPI_QKV_CACHE) cdst[p] = a.row_seq[mst] * a.seq_stride + (long long)a.row_pos[mst] * a.d;
-  }
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    if (p > 0) {
-      __syncthreads();   // every wave is done with the previous pass's rows
-      put();
-    }
-    if (p + 1 < NP) fetch(p + 1);   // in flight while this pass is multiplied
-    __syncthreads();
-    // 3. dot products chunk by chunk (k_mgemv's order), one reduce-scatter, fused epilogue
-    float acc[V];
-#pragma unroll
-    for (int i = 0; i < V; ++i) acc[i] = 0.f;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-#pragma unroll
-      for (int m = 0; m < MR; ++m) {
-        const f16x8 xv = *(const f16x8*)(xsh + m * KP + c * 512 + lane * 8);
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r * MR + m] = dot8(wv[r][c], xv, acc[r * MR + m]);
-      }
-    }
-    float v = reduce_scatter<V>(acc, lane);
-    const int mr = jm + p * MR;
-    if (!lead || mr >= M) continue;
-    v += pbias;
-    const size_t o = (size_t)mr * a.ldo + nst;
-    if constexpr (EPI == EPI_F16) {
-      ((f16*)a.out)[o] = (f16)v;
-    } else if constexpr (EPI == EPI_F16_GELU) {
-      ((f16*)a.out)[o] = (f16)gelu_tanh(v);
-    } else if constexpr (EPI == EPI_F32_RESID) {
-      ((float*)a.out)[o] = pold[p] + v;
-    } else if constexpr (EPI == EPI_F32) {
-      ((float*)a.out)[o] = v;
-    } else if constexpr (EPI == EPI_QKV_CACHE) {
-      if (nst < a.d) ((f16*)a.out)[o] = (f16)v;
-      else if (nst < 2 * a.d) a.kc[cdst[p] + nst - a.d] = (f16)v;
-      else a.vc[cdst[p] + nst - 2 * a.d] = (f16)v;
-    } else {
-      epi_store<EPI>(a, mr, nst, v - pbias);
-    }
-  }
-}
-
-// General GEMV (optional LN prologue through LDS for 2 < M <= 8).
-// A decode step of more than 16 rows (the beams of several segments, StepBatcher): k_mgemv_s's
-// arithmetic with the pass count a runtime value -- ceil(M / MR) passes of MR rows through the
-// LDS image, the wave's weight rows held in registers across them -- so the weights stream once
-// for every row of the step (16-row launches streamed them once per 16 rows).  MR is the row
-// count of the <= 16-row kernel for the same K (16, or 8 for K > 3072), so each row's result is
-// bit-identical to the one it gets in a smaller step.
-template <int EPI, int MR, int R, int NCH>
-__global__ __launch_bounds__(256) void k_mgemv_sp(ProjArgs a) {
-  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
-  constexpr int KP = NCH * 512, V = R * MR;
-  constexpr int SH = V >= 64 ? 0 : V >= 32 ? 1 : V >= 16 ? 2 : V >= 8 ? 3 : V >= 4 ? 4 : V >= 2 ? 5 : 6;
-  constexpr int NV = MR * KP / 8, PER = (NV + 255) / 256;
-  extern __shared__ __attribute__((aligned(16))) f16 xsh[];   // [MR][KP] activation rows
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int n0 = (blockIdx.x * 4 + wid) * R;
-  const int K = a.K, M = a.M, np = (M + MR - 1) / MR;
-  f16x8 t[PER];
-  auto fetch = [&](int p) {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int v = i * 256 + threadIdx.x;
-      const int m = v / (KP / 8) + p * MR, k = (v % (KP / 8)) * 8;
-      t[i] = (v < NV && m < M && k < K) ? *(const f16x8*)(a.A + (size_t)m * a.lda + k) : (f16x8){};
-    }
-  };
-  auto put = [&]() {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int v = i * 256 + threadIdx.x;
-      if (v < NV) *(f16x8*)(xsh + (size_t)v * 8) = t[i];
-    }
-  };
-  fetch(0);
-  int kc[NCH];
-  bool kin[NCH];
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int k = c * 512 + lane * 8;
-    kin[c] = k < K;
-    kc[c] = kin[c] ? k : K - 8;
-  }
-  f16x8 wv[R][NCH];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int n = n0 + r < a.N ? n0 + r : a.N - 1;
-    const f16* w = a.B + (size_t)n * a.ldb;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const f16x8 tw = *(const f16x8*)(w + kc[c]);
-      wv[r][c] = kin[c] ? tw : (f16x8){};
-    }
-  }
-  put();
-  const int j = lane >> SH, jr = j / MR, jm = j % MR;
-  const bool lead = (lane & ((1 << SH) - 1)) == 0 && n0 + jr < a.N;
-  const int nst = n0 + jr < a.N ? n0 + jr : a.N - 1;
-  const float pbias = a.bias ? a.bias[nst] : 0.f;
-  for (int p = 0; p < np; ++p) {
-    if (p > 0) {
-      __syncthreads();   // every wave is done with the previous pass's rows
-      put();
-    }
-    if (p + 1 < np) fetch(p + 1);   // in flight while this pass is multiplied
-    __syncthreads();
-    float acc[V];
-#pragma unroll
-    for (int i = 0; i < V; ++i) acc[i] = 0.f;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-#pragma unroll
-      for (int m = 0; m < MR; ++m) {
-        const f16x8 xv = *(const f16x8*)(xsh + m * KP + c * 512 + lane * 8);
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r * MR + m] = dot8(wv[r][c], xv, acc[r * MR + m]);
-      }
-    }
-    float v = reduce_scatter<V>(acc, lane);
-    const int mr = jm + p * MR;
-    if (!lead || mr >= M) continue;
-    v += pbias;
-    const size_t o = (size_t)mr * a.ldo + nst;
-    if constexpr (EPI == EPI_F16) {
-      ((f16*)a.out)[o] = (f16)v;
-    } else if constexpr (EPI == EPI_F16_GELU) {
-      ((f16*)a.out)[o] = (f16)gelu_tanh(v);
-    } else if constexpr (EPI == EPI_F32_RESID) {
-      ((float*)a.out)[o] += v;
-    } else if constexpr (EPI == EPI_F32) {
-      ((float*)a.out)[o] = v;
-    } else if constexpr (EPI == EPI_QKV_CACHE) {
-      const long long cdst = a.row_seq[mr] * a.seq_stride + (long long)a.row_pos[mr] * a.d;
-      if (nst < a.d) ((f16*)a.out)[o] = (f16)v;
-      else if (nst < 2 * a.d) a.kc[cdst + nst - a.d] = (f16)v;
-      else a.vc[cdst + nst - 2 * a.d] = (f16)v;
-    } else {
-      epi_store<EPI>(a, mr, nst, v - pbias);
-    }
-  }
-}
-
-template <int EPI, int MR, bool LN>
-__global__ __launch_bounds__(256) void k_gemv(ProjArgs a) {
-  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
-  extern __shared__ __attribute__((aligned(16))) f16 xs[];   // [MR][K] when LN
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if constexpr (LN) {
-    for (int r = wid; r < a.M; r += 4) {
-      f16x8 t[3];
-      ln_row_regs<3>(a, r, lane, t);
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const int k = c * 512 + lane * 8;
-        if (k < a.K) *(f16x8*)(xs + r * a.K + k) = t[c];
-      }
-    }
-    __syncthreads();
-  }
-  for (int n = blockIdx.x * 4 + wid; n < a.N; n += gridDim.x * 4) {
-    const f16* w = a.B + (size_t)n * a.ldb;
-    float acc[MR];
-#pragma unroll
-    for (int r = 0; r < MR; ++r) acc[r] = 0.f;
-#pragma unroll 4
-    for (int k = lane * 8; k < a.K; k += 512) {
-      const f16x8 wv = *(const f16x8*)(w + k);
-#pragma unroll
-      for (int r = 0; r < MR; ++r) {
-        if (r < a.M) {
-          const f16x8 xv = LN ? *(const f16x8*)(xs + r * a.K + k) : *(const f16x8*)(a.A + (size_t)r * a.lda + k);
-          acc[r] = dot8(wv, xv, acc[r]);
-        }
-      }
-    }
-    gemv_store<EPI, MR>(a, acc, lane, n);
-  }
-}
-
 // ---------------------------------------------------------------- skinny MFMA GEMM (8 < M <= 64)
 // Prompt prefill / DTW re-forward rows.  A workgroup owns 16*NT output columns for ALL rows;
 // its 4 waves split K (interleaved 32-wide steps), stream the weight fragments straight from
@@ -1671,7 +937,7 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
       int row = m0 + rr;
       if (a.row_map) row = a.row_map[row];
       const float* xr = a.ln_x + (long long)row * a.ldln;
-      float v[5][4], gg[5][4], bb[5][4];
+      float v[5][4];
       float sm = 0.f;
 #pragma unroll
       for (int j = 0; j < 5; ++j) {
@@ -1679,11 +945,7 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
         const bool ok = c < d;
         const int cc = ok ? c : 0;
         const float4 q = *(const float4*)(xr + cc);
-        const float4 g4 = *(const float4*)(a.ln_g + cc);
-        const float4 b4 = *(const float4*)(a.ln_b + cc);
         v[j][0] = ok ? q.x : 0.f; v[j][1] = ok ? q.y : 0.f; v[j][2] = ok ? q.z : 0.f; v[j][3] = ok ? q.w : 0.f;
-        gg[j][0] = g4.x; gg[j][1] = g4.y; gg[j][2] = g4.z; gg[j][3] = g4.w;
-        bb[j][0] = b4.x; bb[j][1] = b4.y; bb[j][2] = b4.z; bb[j][3] = b4.w;
         sm += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
       }
       sm = wave_sum(sm);
@@ -1703,9 +965,12 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
       for (int j = 0; j < 5; ++j) {
         const int c = lane * 4 + j * 256;
         if (c >= d) continue;
+        const float4 g4 = *(const float4*)(a.ln_g + c);
+        const float4 b4 = *(const float4*)(a.ln_b + c);
+        const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, bb[4] = {b4.x, b4.y, b4.z, b4.w};
         f16x4 o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (f16)((v[j][e] - mean) * scale * gg[j][e] + bb[j][e]);
+        for (int e = 0; e < 4; ++e) o[e] = (f16)((v[j][e] - mean) * scale * gg[e] + bb[e]);
         *(f16x4*)(xln + rr * lds_ld + c) = o;
       }
     }
@@ -1774,66 +1039,35 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
 }
 
 
-// WDR_SKINNY_MSPLIT=0: narrow skinny GEMMs keep all row tiles in one workgroup (A/B runs)
-// WDR_MGEMV_STAGED=0: 3..16-row GEMVs without LN on k_mgemv (rows re-read from L2 per wave)
-static bool mgemv_staged() {
-  static const bool on = [] {
-    const char* e = getenv("WDR_MGEMV_STAGED");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-// WDR_MGEMV_R=1|2|4: weight rows per wave of k_mgemv_s (default 2 for N >= 1024, else 1)
-static int mgemv_rows() {
-  static const int r = [] {
-    const char* e = getenv("WDR_MGEMV_R");
-    const int v = e ? atoi(e) : 0;
-    return (v == 1 || v == 2 || v == 4) ? v : 0;
-  }();
-  return r;
-}
-// WDR_MGEMV_NP2=0: K > 3072 projections of 9..16-row steps as two 8-row launches (the
-// previous schedule) instead of one two-pass launch
-static bool mgemv_np2() {
-  static const bool on = [] {
-    const char* e = getenv("WDR_MGEMV_NP2");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-static bool skinny_msplit_off() {
-  const char* e = getenv("WDR_SKINNY_MSPLIT");
-  return e && atoi(e) == 0;
-}
 
-// WDR_GEMM1=1: every M > 64 projection on k_gemm (A/B runs of tools/gemm_bench); read per call
+// A/B knobs of the encoder GEMM dispatch, read once per process (tools/gemm_bench A/B runs set
+// them per run): WDR_GEMM1=1 every M > 64 projection on k_gemm; WDR_GEMM3=0 the big shapes off
+// k_gemm3; WDR_GEMM4=0|1 the ping-pong 256 x 256 GEMM off / forced on for every shape it takes
+// (unset: the measured dispatch rule); WDR_GEMM4_GM row tiles per group of the k_gemm4 / k_gemm5
+// tile order (default 4); WDR_GEMM5=0 the narrow projections on k_gemm4's tiles
+static int env_int(const char* name, int def) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : def;
+}
 static bool gemm1_forced() {
-  const char* e = getenv("WDR_GEMM1");
-  return e && atoi(e) != 0;
+  static const bool v = env_int("WDR_GEMM1", 0) != 0;
+  return v;
 }
-// WDR_GEMM3=0: keep the big encoder GEMMs on k_gemm2 / k_gemm (A/B runs); read per call
 static bool gemm3_enabled() {
-  const char* e = getenv("WDR_GEMM3");
-  return !(e && atoi(e) == 0) && !gemm1_forced();
+  static const bool v = env_int("WDR_GEMM3", 1) != 0 && !gemm1_forced();
+  return v;
 }
-
-// WDR_GEMM4=0|1: the ping-pong 256 x 256 GEMM (k_gemm4) off / forced on for every M > 64 shape
-// it takes (A/B runs of tools/gemm_bench); unset: the measured dispatch rule; read per call
 static int gemm4_mode() {
-  const char* e = getenv("WDR_GEMM4");
-  return e ? atoi(e) : -1;
+  static const int v = env_int("WDR_GEMM4", -1);
+  return v;
 }
-
-// WDR_GEMM4_GM: row tiles per group of the k_gemm4 / k_gemm5 tile order (default 4: qkv and
-// cross-K/V 1 % faster than row-major in tools/gemm_bench); read per call (A/B runs)
 static int gemm_tile_gm() {
-  const char* e = getenv("WDR_GEMM4_GM");
-  return e ? atoi(e) : 4;
+  static const int v = env_int("WDR_GEMM4_GM", 4);
+  return v;
 }
-// WDR_GEMM5=0: the narrow encoder projections on k_gemm4's 256 x 256 tiles (A/B); read per call
 static bool gemm5_on() {
-  const char* e = getenv("WDR_GEMM5");
-  return !(e && atoi(e) == 0);
+  static const bool v = env_int("WDR_GEMM5", 1) != 0;
+  return v;
 }
 
 template <int EPI>
@@ -1841,166 +1075,8 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
   const int ob = (EPI == EPI_F32_RESID || EPI == EPI_F32 || EPI == EPI_F32_GELU_POS) ? 4 : 2;
   const double bytes = (double)a.N * a.K * 2 + (double)a.M * a.K * 2 + (double)a.M * a.N * ob;
   const double flops = 2.0 * a.M * a.N * a.K;
-  if (a.step_rows && a.M > 8 && !a.ln_x && a.K > 3072 && mgemv_staged() && mgemv_np2() && a.K <= 5120 &&
-      a.K % 512 == 0) {
-    // 9..16 step rows through a K > 3072 projection (fc2): one launch, two 8-row passes through
-    // the LDS image, the weights streamed once
-    const int nch = a.K / 512;
-    const uint32_t lds = (uint32_t)8 * nch * 512 * 2;
-    dim3 g2(cdiv(a.N, 4)), blk(256);
-    switch (nch) {
-      case 8: wdr_launch(PROF_GEMV, bytes, flops, k_mgemv_s<EPI, 8, 1, 8, 2>, g2, blk, lds, s, a); break;
-      case 10: wdr_launch(PROF_GEMV, bytes, flops, k_mgemv_s<EPI, 8, 1, 10, 2>, g2, blk, lds, s, a); break;
-      default: WDR_CHECK(false, "step GEMV: two-pass staging needs K = 4096 or 5120");
-    }
-    return;
-  }
-  if (a.step_rows && a.M > 8 && !a.ln_x && a.K > 3072) {
-    // 9..16 step rows through a K > 3072 projection (fc2): two 8-row launches -- the 16-row
-    // shape would spill its activation registers; per-row results are unchanged
-    ProjArgs lo = a, hi = a;
-    lo.M = 8;
-    hi.M = a.M - 8;
-    hi.A = a.A + (size_t)8 * a.lda;
-    const int ob = (EPI == EPI_F32_RESID || EPI == EPI_F32 || EPI == EPI_F32_GELU_POS) ? 4 : 2;
-    hi.out = (char*)a.out + (size_t)8 * a.ldo * ob;
-    if (a.row_seq) hi.row_seq = a.row_seq + 8;
-    if (a.row_pos) hi.row_pos = a.row_pos + 8;
-    launch_epi<EPI>(lo, s);
-    launch_epi<EPI>(hi, s);
-    return;
-  }
-  if (a.M <= 8 || (a.step_rows && a.M <= 16)) {
-    const int nwg = std::min(cdiv(a.N, 4), 1024);
-    dim3 grid(nwg), blk(256);
-    const bool ln = a.ln_x != nullptr;
-    const int nch = cdiv(a.K, 512);
-    if (a.M <= 2 && ((ln && a.K <= 1536) || (!ln && a.K <= 5120 && (a.K % 512 == 0 || a.K <= 1536)))) {
-      // two rows per wave once there are enough rows to keep every CU busy
-      const int R = a.N >= 1024 ? 2 : 1;
-      dim3 g2(cdiv(a.N, 4 * R));
-#define WDR_DG(MR, RR, NCH)                                                                               \
-  if (ln) wdr_launch(PROF_GEMV, bytes, flops, k_dgemv<EPI, MR, RR, NCH, true>, g2, blk, 0, s, a);        \
-  else wdr_launch(PROF_GEMV, bytes, flops, k_dgemv<EPI, MR, RR, NCH, false>, g2, blk, 0, s, a);
-#define WDR_DG_N(MR, RR)                                                                                  \
-  switch (nch) {                                                                                          \
-    case 1: WDR_DG(MR, RR, 1) break;                                                                      \
-    case 2: WDR_DG(MR, RR, 2) break;                                                                      \
-    case 3: WDR_DG(MR, RR, 3) break;                                                                      \
-    case 4: if (!ln) { wdr_launch(PROF_GEMV, bytes, flops, k_dgemv<EPI, MR, RR, 4, false>, g2, blk, 0, s, a); } break; \
-    case 6: if (!ln) { wdr_launch(PROF_GEMV, bytes, flops, k_dgemv<EPI, MR, RR, 6, false>, g2, blk, 0, s, a); } break; \
-    case 8: if (!ln) { wdr_launch(PROF_GEMV, bytes, flops, k_dgemv<EPI, MR, RR, 8, false>, g2, blk, 0, s, a); } break; \
-    default: if (!ln) { wdr_launch(PROF_GEMV, bytes, flops, k_dgemv<EPI, MR, RR, 10, false>, g2, blk, 0, s, a); } break; \
-  }
-      if (a.M == 1) {
-        if (R == 2) { WDR_DG_N(1, 2) } else { WDR_DG_N(1, 1) }
-      } else {
-        if (R == 2) { WDR_DG_N(2, 2) } else { WDR_DG_N(2, 1) }
-      }
-#undef WDR_DG_N
-#undef WDR_DG
-    } else if (!ln && mgemv_staged() && a.K <= 5120 && (a.K % 512 == 0 || a.K <= 1536) &&
-               (a.M <= 8 || a.K <= 1536)) {
-      // 3..16 rows without LN: activation rows staged in LDS once per workgroup, one
-      // reduce-scatter per wave (k_mgemv_s)
-      const int rq = mgemv_rows();
-      // tools/gemv_bench GB_ROWS: one weight row per wave except the wide projections
-      // (qkv / fc1) of 9..16-row steps, where two halve the activation staging per weight byte
-      const int R = rq ? rq : (a.M > 8 && a.N >= 2048 ? 2 : 1);
-      dim3 g2(cdiv(a.N, 4 * R));
-      const int MRr = a.M <= 4 ? 4 : a.M <= 8 ? 8 : 16;
-      const uint32_t lds = (uint32_t)MRr * nch * 512 * 2;
-#define WDR_MS(MR, RR, NCH) wdr_launch(PROF_GEMV, bytes, flops, k_mgemv_s<EPI, MR, RR, NCH>, g2, blk, lds, s, a);
-#define WDR_MS_N(MR, RR)                         \
-  switch (nch) {                                 \
-    case 1: WDR_MS(MR, RR, 1) break;             \
-    case 2: WDR_MS(MR, RR, 2) break;             \
-    case 3: WDR_MS(MR, RR, 3) break;             \
-    case 4: WDR_MS(MR, RR, 4) break;             \
-    case 6: WDR_MS(MR, RR, 6) break;             \
-    case 8: WDR_MS(MR, RR, 8) break;             \
-    default: WDR_MS(MR, RR, 10) break;           \
-  }
-#define WDR_MS_R(MR)                                                        \
-  if (R == 1) { WDR_MS_N(MR, 1) } else if (R == 2) { WDR_MS_N(MR, 2) } else { WDR_MS_N(MR, 4) }
-      if (MRr == 4) { WDR_MS_R(4) }
-      else if (MRr == 8) { WDR_MS_R(8) }
-      else {
-        switch (nch) {
-          case 1: if (R == 1) { WDR_MS(16, 1, 1) } else if (R == 2) { WDR_MS(16, 2, 1) } else { WDR_MS(16, 4, 1) } break;
-          case 2: if (R == 1) { WDR_MS(16, 1, 2) } else if (R == 2) { WDR_MS(16, 2, 2) } else { WDR_MS(16, 4, 2) } break;
-          default: if (R == 1) { WDR_MS(16, 1, 3) } else if (R == 2) { WDR_MS(16, 2, 3) } else { WDR_MS(16, 4, 3) } break;
-        }
-      }
-#undef WDR_MS_R
-#undef WDR_MS_N
-#undef WDR_MS
-    } else if ((ln && a.K <= 1536) || (!ln && a.K <= 5120 && (a.K % 512 == 0 || a.K <= 1536))) {
-      // 3..8 rows (multi-chain batched steps): weight stream as k_dgemv, rows through LDS / L2
-      const int R = a.N >= 1024 ? 2 : 1;
-      dim3 g2(cdiv(a.N, 4 * R));
-      const bool m4 = a.M <= 4;
-      const uint32_t lds = ln ? (uint32_t)(m4 ? 4 : a.M <= 8 ? 8 : 16) * nch * 512 * 2 : 0;
-#define WDR_MG(MR, RR, NCH)                                                                                  \
-  if (ln) wdr_launch(PROF_GEMV, bytes, flops, k_mgemv<EPI, MR, RR, NCH, true>, g2, blk, lds, s, a);         \
-  else wdr_launch(PROF_GEMV, bytes, flops, k_mgemv<EPI, MR, RR, NCH, false>, g2, blk, 0, s, a);
-#define WDR_MG_N(MR, RR)                                                                                     \
-  switch (nch) {                                                                                             \
-    case 1: WDR_MG(MR, RR, 1) break;                                                                         \
-    case 2: WDR_MG(MR, RR, 2) break;                                                                         \
-    case 3: WDR_MG(MR, RR, 3) break;                                                                         \
-    case 4: if (!ln) { wdr_launch(PROF_GEMV, bytes, flops, k_mgemv<EPI, MR, RR, 4, false>, g2, blk, 0, s, a); } break; \
-    case 6: if (!ln) { wdr_launch(PROF_GEMV, bytes, flops, k_mgemv<EPI, MR, RR, 6, false>, g2, blk, 0, s, a); } break; \
-    case 8: if (!ln) { wdr_launch(PROF_GEMV, bytes, flops, k_mgemv<EPI, MR, RR, 8, false>, g2, blk, 0, s, a); } break; \
-    default: if (!ln) { wdr_launch(PROF_GEMV, bytes, flops, k_mgemv<EPI, MR, RR, 10, false>, g2, blk, 0, s, a); } break; \
-  }
-      if (m4) {
-        if (R == 2) { WDR_MG_N(4, 2) } else { WDR_MG_N(4, 1) }
-      } else if (a.M <= 8) {
-        if (R == 2) { WDR_MG_N(8, 2) } else { WDR_MG_N(8, 1) }
-      } else {
-        if (R == 2) { WDR_MG_N(16, 2) } else { WDR_MG_N(16, 1) }
-      }
-#undef WDR_MG_N
-#undef WDR_MG
-    } else {
-      WDR_CHECK(a.M <= 8, "gemv: more than 8 rows need the k_mgemv shapes");
-      const uint32_t lds = ln ? (uint32_t)a.M * a.K * 2 : 0;
-#define WDR_GEMV(MR)                                                                          \
-  if (ln) wdr_launch(PROF_GEMV, bytes, flops, k_gemv<EPI, MR, true>, grid, blk, lds, s, a);  \
-  else wdr_launch(PROF_GEMV, bytes, flops, k_gemv<EPI, MR, false>, grid, blk, 0, s, a);
-      if (a.M <= 1) { WDR_GEMV(1) }
-      else if (a.M <= 2) { WDR_GEMV(2) }
-      else if (a.M <= 4) { WDR_GEMV(4) }
-      else { WDR_GEMV(8) }
-#undef WDR_GEMV
-    }
-  } else if (a.M <= 64 && a.N <= 2048 && !skinny_msplit_off()) {
-    // narrow N (o / xq / xo / fc2: 80 column tiles): one 16-row tile per workgroup, the row
-    // tiles of a column tile on one XCD (gridDim.x % 8 == 0 there) so its weights hit that L2
-    const int mt = cdiv(a.M, 16);
-    dim3 grid(cdiv(a.N, 16), mt), blk(512);
-    if (a.ln_x) wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, 1, 1, 8, true>, grid, blk,
-                           (uint32_t)16 * (a.K + 8) * 2, s, a);
-    else wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, 1, 1, 8>, grid, blk, 0, s, a);
-  } else if (a.M <= 64) {
-    // 8 waves per workgroup split K (tools/skinny_bench: 5-12 % faster than 4 at M 24-64)
-    const bool wide = a.N >= 4096;
-    const int mt = cdiv(a.M, 16);
-    dim3 grid(cdiv(a.N, wide ? 32 : 16)), blk(512);
-    const uint32_t lds = a.ln_x ? (uint32_t)16 * mt * (a.K + 8) * 2 : 0;
-#define WDR_SK(MTV)                                                                                             \
-  if (a.ln_x) {                                                                                                 \
-    if (wide) wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, MTV, 2, 8, true>, grid, blk, lds, s, a);      \
-    else wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, MTV, 1, 8, true>, grid, blk, lds, s, a);           \
-  } else if (wide) wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, MTV, 2, 8>, grid, blk, 0, s, a);         \
-  else wdr_launch(PROF_SKINNY, bytes, flops, k_skinny<EPI, MTV, 1, 8>, grid, blk, 0, s, a);
-    if (mt == 1) { WDR_SK(1) }
-    else if (mt == 2) { WDR_SK(2) }
-    else if (mt == 3) { WDR_SK(3) }
-    else { WDR_SK(4) }
-#undef WDR_SK
-  } else if (a.N % 128 == 0 && a.N < 2048 && a.K % G3_BK == 0 && a.M >= 4096 && !gemm1_forced() && gemm5_on() &&
+  WDR_CHECK(a.M > 64, "encoder GEMM: more than 64 rows (fewer go to the row kernel)");
+  if (a.N % 128 == 0 && a.N < 2048 && a.K % G3_BK == 0 && a.M >= 4096 && !gemm1_forced() && gemm5_on() &&
              gemm4_mode() != 0 && (a.N / G3_N) * cdiv(a.M, G3_M) < 192) {
     // the narrow encoder projections (o, fc2) where 256 x 256 tiles would leave CUs idle: 256 x
     // 128 tiles fill 240 of 256 CUs at M = 6000 (tools/gemm_bench: o 53 vs 62 us on k_gemm2, fc2
@@ -2060,63 +1136,6 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
   }
 }
 
-// > 16 step rows through k_mgemv_sp: one launch, ceil(M / MR) passes, the weights streamed once.
-// MR / R / NCH as the <= 16-row dispatch of launch_epi picks them for the same N, K (16 rows per
-// pass up to K = 1536 -- 8 above K = 3072 with the two-pass fc2's shapes), so the per-row
-// arithmetic is unchanged.  False: the shape has no multi-pass form (the caller chunks it).
-template <int EPI>
-static bool launch_mgemv_passes_epi(const ProjArgs& a, hipStream_t s) {
-  const int ob = (EPI == EPI_F32_RESID || EPI == EPI_F32 || EPI == EPI_F32_GELU_POS) ? 4 : 2;
-  const double bytes = (double)a.N * a.K * 2 + (double)a.M * a.K * 2 + (double)a.M * a.N * ob;
-  const double flops = 2.0 * a.M * a.N * a.K;
-  dim3 blk(256);
-  if (a.K <= 1536) {
-    // the 9..16-row k_mgemv_s shape: MR 16, R = 2 for N >= 2048 (unless WDR_MGEMV_R)
-    const int rq = mgemv_rows();
-    const int R = rq ? rq : (a.N >= 2048 ? 2 : 1);
-    const int nch = cdiv(a.K, 512);
-    const uint32_t lds = (uint32_t)16 * nch * 512 * 2;
-    dim3 g(cdiv(a.N, 4 * R));
-#define WDR_SP(RR, NCHV) wdr_launch(PROF_GEMV, bytes, flops, k_mgemv_sp<EPI, 16, RR, NCHV>, g, blk, lds, s, a)
-    if (R == 1) {
-      if (nch == 1) WDR_SP(1, 1); else if (nch == 2) WDR_SP(1, 2); else WDR_SP(1, 3);
-    } else if (R == 2) {
-      if (nch == 1) WDR_SP(2, 1); else if (nch == 2) WDR_SP(2, 2); else WDR_SP(2, 3);
-    } else {
-      return false;
-    }
-#undef WDR_SP
-    return true;
-  }
-  if (a.K > 3072 && a.K <= 5120 && a.K % 512 == 0 && mgemv_np2()) {
-    // the two-pass fc2 shape (MR 8, R 1): 8 rows per pass
-    const int nch = a.K / 512;
-    const uint32_t lds = (uint32_t)8 * nch * 512 * 2;
-    dim3 g(cdiv(a.N, 4));
-    if (nch == 8) wdr_launch(PROF_GEMV, bytes, flops, k_mgemv_sp<EPI, 8, 1, 8>, g, blk, lds, s, a);
-    else if (nch == 10) wdr_launch(PROF_GEMV, bytes, flops, k_mgemv_sp<EPI, 8, 1, 10>, g, blk, lds, s, a);
-    else return false;
-    return true;
-  }
-  return false;
-}
-
-static bool launch_mgemv_passes(const ProjArgs& a, hipStream_t s) {
-  static const bool on = [] {
-    const char* e = getenv("WDR_MGEMV_PASSES");
-    return !(e && atoi(e) == 0);
-  }();
-  if (!on) return false;
-  switch (a.epi) {
-    case EPI_F16: return launch_mgemv_passes_epi<EPI_F16>(a, s);
-    case EPI_F16_GELU: return launch_mgemv_passes_epi<EPI_F16_GELU>(a, s);
-    case EPI_F32_RESID: return launch_mgemv_passes_epi<EPI_F32_RESID>(a, s);
-    case EPI_F32: return launch_mgemv_passes_epi<EPI_F32>(a, s);
-    case EPI_QKV_CACHE: return launch_mgemv_passes_epi<EPI_QKV_CACHE>(a, s);
-    default: return false;
-  }
-}
-
 // Decoder rows of any count on the row kernel (k_skinny, 8 waves splitting K): the k order of a
 // wave (k = 32 wid + 256 t, t = 0, 1, ...) and the wave order of the reduce do not depend on the
 // tile shape (MT, NT, U) or the row split, so every row's result is the same whatever the launch
@@ -2133,6 +1152,13 @@ static bool rows_w16n() {
   return e && atoi(e) != 0;
 }
 
+// WDR_ROWS_LEAN=1 (A/B): the row projections without a LayerNorm prologue on 4-wave workgroups
+// under 64 VGPRs (room beside an encoder GEMM tile on every CU); 2: fc2 too
+int rows_lean() {
+  static const int v = getenv("WDR_ROWS_LEAN") ? atoi(getenv("WDR_ROWS_LEAN")) : 0;
+  return v;
+}
+
 template <int EPI>
 static void launch_rows_epi(const ProjArgs& a, hipStream_t s) {
   const int ob = (EPI == EPI_F32_RESID || EPI == EPI_F32 || EPI == EPI_F32_GELU_POS) ? 4 : 2;
@@ -2142,6 +1168,12 @@ static void launch_rows_epi(const ProjArgs& a, hipStream_t s) {
   const bool ln = a.ln_x != nullptr;
   const bool wide = a.N >= 4096;
   const int prof = PROF_GEMV;   // the "rows" class of bench.py's live roofline (any row count)
+  if (rows_lean() && !ln && (a.K <= 2048 || rows_lean() >= 2)) {
+    if (wide) wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 2, 4, false, 3>, dim3(cdiv(a.N, 32), mt), dim3(256), 0, s, a);
+    else if (a.K > 2048) wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 4, false, 5>, dim3(cdiv(a.N, 16), mt), dim3(256), 0, s, a);
+    else wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 4, false, 5>, dim3(cdiv(a.N, 16), mt), dim3(256), 0, s, a);
+    return;
+  }
   if (!wide) {
     // one 16-row tile per workgroup: the row tiles of a column tile re-read its weights from L2.
     // K > 2048 (fc2): 16 waves, each wave's 10 k-steps as ONE batch of loads (8 waves took three
@@ -2196,40 +1228,15 @@ static void launch_rows(const ProjArgs& a, hipStream_t s) {
 
 void launch_proj(const ProjArgs& a, hipStream_t s) {
   WDR_CHECK(a.M > 0 && a.K > 0 && a.N > 0, "projection: empty shape");
-  if (a.rows_mma) {
+  // decoder rows (any count, rows_mma) and every other projection of <= 64 rows run on the row
+  // kernel; the encoder's M > 64 GEMMs on the MFMA tile family
+  if (a.rows_mma || a.M <= 64) {
     launch_rows(a, s);
     return;
   }
-  if (a.step_rows && a.M > 16 && !a.ln_x && mgemv_staged() && launch_mgemv_passes(a, s)) return;
-  if (a.step_rows && a.M > 16) {
-    // a batched step of more than 16 rows (beams of several segments): 16-row GEMV launches,
-    // so every row's arithmetic stays that of a <= 16-row step whatever the batch holds
-    // (batch composition depends on timing; results must not)
-    const int ob = (a.epi == EPI_F32_RESID || a.epi == EPI_F32 || a.epi == EPI_F32_GELU_POS) ? 4 : 2;
-    for (int r0 = 0; r0 < a.M; r0 += 16) {
-      ProjArgs c = a;
-      c.M = std::min(16, a.M - r0);
-      if (a.A) c.A = a.A + (size_t)r0 * a.lda;
-      if (a.ln_x) c.ln_x = a.ln_x + (size_t)r0 * a.ldln;
-      c.out = (char*)a.out + (size_t)r0 * a.ldo * ob;
-      if (a.row_seq) c.row_seq = a.row_seq + r0;
-      if (a.row_pos) c.row_pos = a.row_pos + r0;
-      launch_proj(c, s);
-    }
-    return;
-  }
   WDR_CHECK(a.K % 8 == 0 && a.lda % 8 == 0 && a.ldb % 8 == 0, "projection: K/lda/ldb must be multiples of 8");
-  if (a.M > 64) {
-    WDR_CHECK(a.N % GB_N == 0, "gemm: N must be a multiple of 128");
-    WDR_CHECK(a.K % GB_K == 0, "gemm: K must be a multiple of 32");
-  } else if (a.step_rows && a.M <= 16) {
-    WDR_CHECK(!a.ln_x || a.K <= 1536, "gemv LN prologue: K must be <= 1536");
-  } else if (a.M > 8) {
-    WDR_CHECK(a.K % 32 == 0, "skinny gemm: K must be a multiple of 32");
-    WDR_CHECK(!a.ln_x || (a.K <= 1280 && a.K % 4 == 0 && a.M <= 32), "skinny LN prologue: K <= 1280, M <= 32");
-  } else if (a.ln_x) {
-    WDR_CHECK(a.K <= 1536 && a.K % 8 == 0, "gemv LN prologue: K must be <= 1536");
-  }
+  WDR_CHECK(a.N % GB_N == 0, "gemm: N must be a multiple of 128");
+  WDR_CHECK(a.K % GB_K == 0, "gemm: K must be a multiple of 32");
   WDR_CHECK(a.epi != EPI_QKV_CACHE || (a.kc && a.vc && a.row_seq && a.row_pos && a.d > 0), "qkv-cache epilogue args");
   switch (a.epi) {
     case EPI_F16: launch_epi<EPI_F16>(a, s); break;

@@ -206,6 +206,29 @@ hipEvent_t prof_event() {
   return e;
 }
 
+void prof_shutdown() {
+  std::lock_guard<std::mutex> l(g_mu);
+  g_mask = 0;
+  for (auto& r : g_pending) {
+    (void)hipEventSynchronize(r.b);
+    g_pool.push_back(r.a);
+    g_pool.push_back(r.b);
+  }
+  g_pending.clear();
+  g_clk_pending.clear();
+  for (hipEvent_t e : g_pool) (void)hipEventDestroy(e);
+  g_pool.clear();
+  if (g_ring) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipSetDevice(g_ring_dev);
+    (void)hipFree(g_ring);
+    (void)hipSetDevice(dev);
+    g_ring = nullptr;
+  }
+  (void)hipGetLastError();
+}
+
 void prof_push(int cls, hipEvent_t a, hipEvent_t b, unsigned long long* ts, double bytes, double flops) {
   std::lock_guard<std::mutex> l(g_mu);
   g_pending.push_back({a, b, cls});

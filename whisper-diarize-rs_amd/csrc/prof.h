@@ -24,6 +24,8 @@ bool prof_step();
 void prof_capture(bool on);
 void prof_in_step(bool on);   // around the eager launches of a step prof_step() picked
 hipEvent_t prof_event();
+// frees the kernel-clock ring and the pooled events (wdr_shutdown)
+void prof_shutdown();
 // WDR_LAUNCH_LOCK=1: kernel launches and graph replays from all host threads go through one
 // process-wide mutex (profiling runs: rocprofv3's kernel-trace interception of a launch faults
 // inside the tool when several threads launch at once -- tools/prof_crash_ab.sh)

@@ -171,7 +171,7 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, in
   // last workgroup per row tile -- an in-launch hand-off -- measured slower still: 529 vs 557 xRT,
   // profiles/r03/ab_lno_xfc.txt.)
   static const bool ln_split = !(getenv("WDR_ROWS_LN_SPLIT") && atoi(getenv("WDR_ROWS_LN_SPLIT")) == 0);
-  const bool fuse_ln = R <= 32 || !ln_split;
+  const bool fuse_ln = (R <= 32 || !ln_split) && !rows_lean();
   auto P = [&](const f16* A, int lda, const f16* W, const float* b, void* out, int ldo, int N, int K, int epi,
                const float* lng = nullptr, const float* lnb = nullptr) {
     ProjArgs a{A, lda, W, K, b, out, ldo, nullptr, 0, R, N, K, epi};
@@ -244,7 +244,7 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, in
     // final LayerNorm + logits of the logit rows only, gathered by lrow (compact output)
     ProjArgs a{nullptr, d, md.tok_emb, d, nullptr, io.logits, io.ldlogits, nullptr, 0, io.n_logit, hp.n_vocab, d, EPI_F32};
     a.rows_mma = 1;
-    if (io.n_logit <= 32 || !ln_split) {
+    if ((io.n_logit <= 32 || !ln_split) && !rows_lean()) {
       a.ln_x = io.xd;
       a.ldln = d;
       a.ln_g = md.ln_g;

@@ -34,6 +34,8 @@ std::vector<std::pair<int, int>> alignment_heads_for(const std::string& model_na
 std::recursive_mutex& hip_alloc_mutex();
 // a stream on a dedicated hardware queue (env knob `knob`, default `def`; else priority `prio`)
 hipStream_t dedicated_stream(const char* knob, bool def, int prio);
+// destroys the process-wide pools of CU-masked streams (wdr_shutdown; no context may be alive)
+void destroy_stream_pools();
 
 struct DevMem {
   void* p = nullptr;
@@ -174,6 +176,7 @@ struct StageTimes {   // host wall-clock per phase (seconds), accumulated
   double mel = 0, encode = 0, decode = 0, dtw = 0, glue = 0;
   long long windows = 0, decode_steps = 0, prefills = 0;
   double lang = 0, prompt_gpu = 0;   // language-detect wall time; GPU time of the prompt prefills
+  long long lang_passes = 0, lang_rows = 0;   // language-detection decoder passes and their rows
 };
 
 // Multi-chain decoding: several States ("chains", each decoding its own contiguous block of
@@ -246,6 +249,7 @@ struct DtwQJob {
   bool issued = false;         // the queue has enqueued the pass and both events
   double t_submit = 0;
   size_t cap_off = 0;          // the queue's capture buffer offset (floats)
+  std::exception_ptr err;      // failure of the pass that carried this job (rethrown to its waiters)
   DtwQJob();
   ~DtwQJob();
 };

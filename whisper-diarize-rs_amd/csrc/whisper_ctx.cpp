@@ -140,6 +140,29 @@ hipStream_t dedicated_stream(const char* knob, bool def, int prio) {
 // whether mask bit c is CU c % 32 of XCD c / 32 or CU c / 8 of XCD c % 8 -- bits 32x + 8j + x,
 // j < n/8 -- since a decode launch's workgroups go round-robin over the XCDs, every XCD needs free
 // CUs; 0: the top n bits).  pool <= 0: a stream of its own.
+using StreamPools = std::map<std::pair<std::string, int>, std::pair<std::vector<hipStream_t>, int>>;
+static std::mutex& stream_pools_mu() {
+  static std::mutex mu;
+  return mu;
+}
+static StreamPools& stream_pools() {
+  static StreamPools* p = new StreamPools();   // outlives static destruction (exit hook)
+  return *p;
+}
+
+void destroy_stream_pools() {
+  std::lock_guard<std::mutex> g(stream_pools_mu());
+  for (auto& kv : stream_pools()) {
+    (void)hipSetDevice(kv.first.second);
+    for (hipStream_t st : kv.second.first) {
+      (void)hipStreamSynchronize(st);
+      (void)hipStreamDestroy(st);
+    }
+  }
+  stream_pools().clear();
+  (void)hipGetLastError();
+}
+
 static hipStream_t masked_pool_stream(const char* tag, int n_res, int pool, bool* shared) {
   int dev = 0, ncu = 0;
   WDR_HIP(hipGetDevice(&dev));
@@ -164,10 +187,8 @@ static hipStream_t masked_pool_stream(const char* tag, int n_res, int pool, bool
   };
   *shared = false;
   if (pool <= 0) return make();
-  static std::mutex mu;
-  static std::map<std::pair<std::string, int>, std::pair<std::vector<hipStream_t>, int>> pools;
-  std::lock_guard<std::mutex> g(mu);
-  auto& P = pools[{tag, dev}];
+  std::lock_guard<std::mutex> g(stream_pools_mu());
+  auto& P = stream_pools()[{tag, dev}];
   if (P.first.empty())
     for (int i = 0; i < pool; ++i) P.first.push_back(make());
   *shared = true;
@@ -570,6 +591,7 @@ struct State::Impl {
   bool enc_stop = false, enc_busy = false;
   std::exception_ptr enc_err;
   std::atomic<long long> enc_windows{0};
+  std::atomic<long long> lang_passes{0}, lang_rows{0};   // encode-ahead language-detection passes
   float* h_lang = nullptr;      // [(S + 1)][100]
   DevMem energy_d; int energy_cap = 0;
   const f16* xkv() const { return xkv_ring.as<f16>() + (size_t)cur * xkv_slot_elems; }
@@ -1068,6 +1090,8 @@ void State::unplan() {
   m.plan.n.clear();
   m.plan.next_enq = 0;
   times.windows += m.enc_windows.exchange(0);
+  times.lang_passes += m.lang_passes.exchange(0);
+  times.lang_rows += m.lang_rows.exchange(0);
 }
 
 // Segments the encode-ahead stream may run ahead of the decoder (WDR_ENC_AHEAD, kBatch..S;
@@ -1325,6 +1349,10 @@ bool State::top_up_batch(int j) {
       m.plan.next_enq = g1;
     }
     m.enc_windows += g1 - g0;
+    if (m.plan.detect_lang) {
+      m.lang_passes++;
+      m.lang_rows += g1 - g0;
+    }
   }
   return true;
 }
@@ -1776,29 +1804,37 @@ void State::dtw_timestamps(int i_segment, int n_segments, int seek, int n_frames
       if (t.id < v.eot) toks.push_back(t.id);
   toks.push_back(v.eot);
   const int N = (int)toks.size();
+  // validated before anything is registered: a job that is never issued would block every later
+  // wait on it (positions past n_text_ctx have no embedding, the DTW buffers hold RMAX rows)
+  WDR_CHECK(N >= 1 && N <= RMAX, "DTW re-forward: token count out of range");
   Impl::DtwJob job;
   job.i0 = i_segment;
   job.n = n_segments;
-  if (m.blk_pool.empty()) {
-    int* blk = nullptr;
-    WDR_HIP(hipHostMalloc((void**)&blk, (3 * RMAX + RMAX + 8) * 4, hipHostMallocDefault));
-    m.blk_pool.push_back(blk);
+  if (m.blk_pool.empty() || m.ev_pool.empty()) {
+    // other chain threads may be capturing graphs: a pinned allocation outside the process-wide
+    // allocation mutex would invalidate their capture (whisper_ctx.cpp top, ROCm 7.2)
+    std::lock_guard<std::recursive_mutex> g(hip_alloc_mutex());
+    if (m.blk_pool.empty()) {
+      int* blk = nullptr;
+      WDR_HIP(hipHostMalloc((void**)&blk, (3 * RMAX + RMAX + 8) * 4, hipHostMallocDefault));
+      m.blk_pool.push_back(blk);
+    }
+    if (m.ev_pool.empty()) {
+      hipEvent_t e;
+      WDR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      m.ev_pool.push_back(e);
+    }
   }
   job.blk = m.blk_pool.back();
   m.blk_pool.pop_back();
-  if (m.ev_pool.empty()) {
-    hipEvent_t e;
-    WDR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    m.ev_pool.push_back(e);
-  }
   job.done = m.ev_pool.back();
   m.ev_pool.pop_back();
-  m.jobs.push_back(job);
   Impl::DtwSet& D = m.dset;
   if (batched && dtw_queue_on()) {
     // multi-chain run: the re-forward goes to the context's DTW queue, batched with the other
     // chains' off the decode chain's critical path; the slot keeps a handle (reused only after
-    // the pass has read it)
+    // the pass has read it).  Registered only once the queue has accepted it: a job that is
+    // never issued must not be waited on.
     WDR_HIP(hipStreamSynchronize(s_));   // the window's cross-K/V (on-demand encodes) in place
     auto q = std::make_shared<DtwQJob>();
     q->toks = toks;
@@ -1809,19 +1845,21 @@ void State::dtw_timestamps(int i_segment, int n_segments, int seek, int n_frames
     q->n_audio = n_frames / 2;
     q->blk = job.blk;
     q->done = job.done;
-    m.jobs.back().q = q;
+    DtwQueue& dq = ctx_.dtw_queue();
+    dq.submit(q);
+    job.q = q;
+    m.jobs.push_back(job);
     m.slots[m.cur].dtw = q;
     // passes already run no longer write the DTW sequence
-    DtwQueue& dq = ctx_.dtw_queue();
     m.qlive.erase(std::remove_if(m.qlive.begin(), m.qlive.end(),
                                  [&](const std::shared_ptr<DtwQJob>& x) {
                                    return dq.is_issued(x) && hipEventQuery(x->fwd) == hipSuccess;
                                  }),
                   m.qlive.end());
     m.qlive.push_back(q);
-    ctx_.dtw_queue().submit(q);
     return;
   }
+  m.jobs.push_back(job);
   if (batched) {
     // multi-chain run (WDR_DTW_QUEUE=0): the re-forward's rows ride in the chain's next batched
     // request (its next prompt prefill, or a request of their own: flush_dtw); the DTW kernels
@@ -2425,6 +2463,8 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
     } else {
       const int sot = v.sot;
       decoder_prefill(&sot, 1, 0, true, false);
+      times.lang_passes++;
+      times.lang_rows++;
       WDR_HIP(wdr_memcpy_async(ll.data(), m.mb.logits.as<float>() + v.sot + 1, 100 * 4, hipMemcpyDeviceToHost, s_));
       WDR_HIP(hipStreamSynchronize(s_));
     }
@@ -2657,14 +2697,10 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
             m.t_enc_launch.load() * 1e-6);
     fflush(clog);
   }
-  if (m.pend.on && planned && async_dtw) {
-    // the last window's re-forward rides in the next segment's first request: this slot is
-    // released once it has run (dtw_after_step), not here
-    m.pend.slot = m.cur;
-    release.on = false;
-  } else {
-    flush_dtw();
-  }
+  // the last window's pending re-forward (WDR_DTW_QUEUE=0) runs before the slot is released:
+  // deferring the release into the next segment's first request let an encode-ahead batch wait
+  // on the slot's previous `freed` record and overwrite the cross-K/V the re-forward still reads
+  flush_dtw();
   if (!async_dtw) {
     std::vector<DtwTicket> tk = take_dtw_jobs();
     for (auto& t : tk) resolve_dtw(t, result_all);
@@ -3071,7 +3107,7 @@ DtwQueue::~DtwQueue() {
 }
 
 void DtwQueue::submit(const std::shared_ptr<DtwQJob>& j) {
-  WDR_CHECK((int)j->toks.size() >= 1 && (int)j->toks.size() <= RMAX + 1 && j->xkv && j->blk && j->done,
+  WDR_CHECK((int)j->toks.size() >= 1 && (int)j->toks.size() <= RMAX && j->xkv && j->blk && j->done,
             "DTW queue: bad job");
   {
     std::lock_guard<std::mutex> g(m_->mu);
@@ -3091,14 +3127,14 @@ bool DtwQueue::is_issued(const std::shared_ptr<DtwQJob>& j) {
 void DtwQueue::wait_issued(const std::shared_ptr<DtwQJob>& j) {
   Impl& m = *m_;
   std::unique_lock<std::mutex> lk(m.mu);
-  if (j->issued) {
-    if (m.err) std::rethrow_exception(m.err);
-    return;
+  if (!j->issued) {
+    m.urgent++;
+    m.cv.notify_all();
+    m.cv.wait(lk, [&] { return j->issued; });
+    m.urgent--;
   }
-  m.urgent++;
-  m.cv.notify_all();
-  m.cv.wait(lk, [&] { return j->issued; });
-  m.urgent--;
+  // only the failure of the pass that carried this job (or of the worker's start) reaches it
+  if (j->err) std::rethrow_exception(j->err);
   if (m.err) std::rethrow_exception(m.err);
 }
 
@@ -3139,8 +3175,8 @@ void DtwQueue::run() {
     }
     m.pend_rows -= rows;
     lk.unlock();
-    std::exception_ptr e;
-    if (!m.err) {
+    std::exception_ptr e = m.err;
+    if (!e) {
       try {
         issue(batch);
       } catch (...) {
@@ -3148,8 +3184,10 @@ void DtwQueue::run() {
       }
     }
     lk.lock();
-    if (e && !m.err) m.err = e;
-    for (auto& j : batch) j->issued = true;
+    for (auto& j : batch) {
+      j->err = e;   // scoped to this pass: later passes (and later runs) start clean
+      j->issued = true;
+    }
     m.cv.notify_all();
   }
 }

@@ -3,6 +3,7 @@
 (there is no CPU fallback: the CPU restatement under oracle/ is test-only)."""
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import os
 import re
@@ -89,7 +90,7 @@ class StageTimes(C.Structure):
                 ("batch_step_s", f64), ("early_fixup_segments", i64), ("batch_prefill_rows", i64),
                 ("batch_dtw_rows", i64), ("batch_prefills", i64), ("batch_dtws", i64), ("batch_mixed", i64),
                 ("batch_xattn_groups", i64), ("batch_xattn_tiles", i64), ("dtwq_passes", i64), ("dtwq_rows", i64),
-                ("dtwq_jobs", i64)]
+                ("dtwq_jobs", i64), ("lang_passes", i64), ("lang_rows", i64)]
 
 
 class Token(C.Structure):
@@ -106,6 +107,7 @@ _SIGS = {
     "wdr_last_error": (cstr, []),
     "wdr_abi_version": (C.c_int, []),
     "wdr_device_count": (C.c_int, []),
+    "wdr_shutdown": (None, []),
     "wdr_engine_new": (C.c_int, [P(EngineConfig), P(vp)]),
     "wdr_engine_free": (None, [vp]),
     "wdr_engine_set_synthetic": (C.c_int, [vp, P(Synthetic)]),
@@ -203,6 +205,9 @@ def load():
         fn.restype = res
         fn.argtypes = args
     _lib = lib
+    # release every handle still alive (contexts' worker threads, streams, device memory) before
+    # the interpreter and the HIP runtime tear down; later frees of those handles are no-ops
+    atexit.register(lib.wdr_shutdown)
     return lib
 
 
