@@ -92,22 +92,28 @@ def pmc_traffic(cls):
 # conv1, conv2, 32 x (qkv, o, fc1, fc2), the cross-K/V projection -- and the self-attention),
 # and a decoder pass's bytes: the decoder weights (streamed once per rows launch, shared by its
 # rows) and one slot's cross-K/V (read once per cross-attention group or MFMA row tile).
-# rows_weight_bytes: the weight bytes a row-kernel launch streams, by its template arguments
-# <EPI, MT, NT, W, LN, U> (EPI 5 qkv 3d x d, 2 o / xo d x d or fc2 d x 4d (16 waves), 0 xq, 1 fc1
-# 4d x d, 3 logits V x d), large-v3 d = 1280
+# rows_weight_bytes: the weight bytes a row-kernel launch streams, by k_rowproj's template
+# arguments <EPI, MT, NT, U, KS> (csrc/kernels/gemm.hip): KS 5 = o / xo (d x d, split into 5 K
+# slices), KS 8 = fc2 (d x 4d, 8 slices); KS 1 by epilogue: 5 qkv (3d x d), 0 xq (d x d), 1 fc1
+# (4d x d), 3 logits (V x d); large-v3 d = 1280
 _D, _V = 1280, 51866
-_RW = {"5": 3 * _D * _D * 2, "0": _D * _D * 2, "1": 4 * _D * _D * 2, "3": _V * _D * 2}
+
+
+def rows_weight_bytes(targs):
+    epi, _mt, _nt, _u, ks = (int(x) for x in targs.split(","))
+    if ks == 5:
+        return _D * _D * 2
+    if ks == 8:
+        return 4 * _D * _D * 2
+    return {5: 3 * _D * _D * 2, 0: _D * _D * 2, 1: 4 * _D * _D * 2, 3: _V * _D * 2}.get(epi)
+
+
 WORK = {"large-v3": {"enc_flops": 2.589e12, "enc_gemm_flops": 2.221e12, "enc_attn_flops": 0.369e12,
                      "dec_weight_bytes": 1.601e9, "xkv_row_bytes": 0.246e9,
                      # the 32 layers' projection weights without the logits (14 d^2 x 2 B each); a
                      # DTW pass stops after the last alignment-head layer: 26 of 32
                      "dec_layer_bytes": 14 * _D * _D * 2 * 32, "dtw_layer_frac": 26 / 32,
-                     "rows_weight_bytes": {**{"%s,%d,%d,%d,%s,%d" % (e, mt, nt, wv, ln, u): _RW[e]
-                                              for e in _RW for mt in (1, 2, 3, 4) for nt in (1, 2)
-                                              for wv in (8, 16) for ln in ("false", "true") for u in (0, 3, 12)},
-                                           **{"2,1,1,8,%s,%d" % (ln, u): _D * _D * 2 for ln in ("false", "true")
-                                              for u in (0, 3)},
-                                           "2,1,1,16,false,12": 4 * _D * _D * 2}},
+                     "rows_weight_bytes": rows_weight_bytes},
         "base.en": {"enc_flops": 96.8e9, "enc_gemm_flops": 87.6e9, "enc_attn_flops": 9.2e9,
                     "dec_weight_bytes": 97.1e6, "xkv_row_bytes": 18.4e6, "dec_layer_bytes": 14 * 512 * 512 * 2 * 6,
                     "dtw_layer_frac": 6 / 6}}
@@ -181,9 +187,9 @@ def trace_roofline(model, fp8=False):
         import csv
         for r in csv.DictReader(open(stats)):
             nm = r.get("Name", r.get("KernelName", ""))
-            if nm.startswith("k_skinny<") or "k_skinny" in nm:
-                key = nm[nm.index("<") + 1:nm.index(">")].replace(" ", "")
-                b = wb.get(key)
+            if "k_rowproj<" in nm:
+                key = nm[nm.index("k_rowproj<") + 10:].split(">")[0].replace(" ", "")
+                b = wb(key)
                 if b:
                     rows_bytes += float(r.get("Calls", 0)) * b
                     rows_ms += float(r.get("TotalDurationNs", 0)) * 1e-6

@@ -1,5 +1,5 @@
 // Decoder-row projection microbenchmark (large-v3 decoder shapes): the row kernel
-// (ProjArgs::rows_mma: k_skinny's arithmetic for any row count, LayerNorm fused up to 32 rows),
+// (ProjArgs::rows_mma: k_rowproj for any row count, the LayerNorm step as its own launch),
 // per launch, replayed from a hipGraph of 32 launches over 32 distinct weight copies (> the
 // 256 MiB Infinity Cache).
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/rows_bench.cpp -Lwhisper-diarize-rs_amd -lwdr \
@@ -95,13 +95,11 @@ int main(int argc, char** argv) {
         for (int l = 0; l < nl; ++l) {
           ProjArgs a{xa, sh.K, W[l], sh.K, bias, out, sh.N, nullptr, 0, M, sh.N, sh.K, sh.epi};
           a.rows_mma = 1;
-          if (sh.ln) {
-            if (M <= 32) {
-              a.ln_x = xf; a.ldln = sh.K; a.ln_g = g; a.ln_b = b;
-            } else {
-              launch_layernorm(xf, d, g, b, hd, d, M, d, s);
-              a.A = hd;
-            }
+          if (sh.ln) {   // the LayerNorm step of rows_forward (k_resid_ln, no residual)
+            ResidLnArgs r;
+            r.R = M; r.x = xf; r.d = d; r.g = g; r.b = b; r.h = hd;
+            launch_resid_ln(r, s);
+            a.A = hd;
           }
           launch_proj(a, s);
         }

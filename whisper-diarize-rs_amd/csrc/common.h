@@ -100,12 +100,16 @@ struct ProjArgs {
   // k_gemm4 tile order: groups of tile_gm row tiles walked column by column (0: row-major)
   int tile_gm = 0;
   // decoder rows of any count (steps, prompt prefills, DTW re-forwards) on the row kernel
-  // (k_skinny's arithmetic: 8 waves split K, fixed k order, fixed wave order in the reduce), so
-  // a row's result never depends on how many rows share the launch (the LN prologue normalises
-  // each workgroup's own row tiles)
+  // (k_rowproj: 4 waves split K, fixed k order, fixed wave order in the reduce), so a row's
+  // result never depends on how many rows share the launch
   int rows_mma = 0;
   // optional row map: A / ln_x row m is row_map[m] (logit rows gathered from the residual stream)
   const int* row_map = nullptr;
+  // decoder rows, split-K over workgroups (k_rowproj): ksplit > 1 writes each K slice's f32
+  // partial to slab[s][M][N] (bias and epilogue left to k_resid_ln, which sums the slices in
+  // order); 1: the epilogue in the projection
+  int ksplit = 1;
+  float* slab = nullptr;
 };
 
 // Live kernel clock (csrc/prof.cpp): a launch the profiler samples carries ts -> {earliest wave
@@ -133,8 +137,6 @@ template <typename A>
 inline unsigned long long* prof_attach(A&) { return nullptr; }
 inline unsigned long long* prof_attach(ProjArgs& a) { return a.ts = prof_slot(); }
 void launch_proj(const ProjArgs& a, hipStream_t s);   // picks GEMV (M<=8) or MFMA GEMM
-// WDR_ROWS_LEAN A/B mode of the row projections (gemm.hip): 0 off, 1 lean for K <= 2048, 2 also fc2
-int rows_lean();
 // fp8 encoder GEMM (BASELINE configs[4]): ProjArgs::A8 / B8 / a_scale / b_scale, M > 64,
 // N % 128 == 0, K % 128 == 0; epilogues as launch_proj
 void launch_proj_fp8(const ProjArgs& a, hipStream_t s);

@@ -214,7 +214,7 @@ void launch_flash_attn(const FlashArgs& a, int n_batch, hipStream_t s) {
 // ---------------------------------------------------------------- decoder self-attention
 // one 256-thread workgroup per (decoder row, head) over that row's cache (<= 448 keys):
 // keys spread over all 4 waves for the scores, 4 key quarters in parallel for P.V.
-__global__ __launch_bounds__(256) void k_dec_self_attn(DecSelfArgs a) {
+__global__ __launch_bounds__(256, 8) void k_dec_self_attn(DecSelfArgs a) {   // <= 64 VGPRs: fits beside an encoder tile
   __shared__ float qs[64];
   __shared__ float sc[448];
   __shared__ float red[2][4];
@@ -226,20 +226,30 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecSelfArgs a) {
   __syncthreads();
   const f16* K = a.kc + seq * a.seq_stride + h * 64;
   const f16* V = a.vc + seq * a.seq_stride + h * 64;
+  // scores: four lanes per key, each a 16-dim partial dot in dim order, added in a fixed
+  // shuffle tree (64 keys per pass; the lane's 16 query values stay in registers)
   float mx = -INFINITY;
-  for (int k = tid; k < nk; k += 256) {
-    const f16* kr = K + (long long)k * a.d;
-    f16x8 kv[8];
+  const int kq = tid >> 2, qd = tid & 3;
+  float qv[16];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) kv[c] = *(const f16x8*)(kr + 8 * c);
-    float s = 0.f;
+  for (int e = 0; e < 16; ++e) qv[e] = qs[qd * 16 + e];
+#pragma unroll 1
+  for (int k0 = 0; k0 < nk; k0 += 64) {
+    const int k = k0 + kq;
+    const f16* kr = K + (long long)(k < nk ? k : nk - 1) * a.d + qd * 16;
+    const f16x8 k0v = *(const f16x8*)kr, k1v = *(const f16x8*)(kr + 8);
+    float t = 0.f;
 #pragma unroll
-    for (int c = 0; c < 8; ++c)
+    for (int e = 0; e < 8; ++e) t += qv[e] * (float)k0v[e];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s += qs[8 * c + e] * (float)kv[c][e];
-    s *= a.scale;
-    sc[k] = s;
-    mx = fmaxf(mx, s);
+    for (int e = 0; e < 8; ++e) t += qv[8 + e] * (float)k1v[e];
+    t += __shfl_xor(t, 1, 64);
+    t += __shfl_xor(t, 2, 64);
+    if (k < nk) {
+      t *= a.scale;
+      if (qd == 0) sc[k] = t;
+      mx = fmaxf(mx, t);
+    }
   }
   mx = wave_max(mx);
   if (lane == 0) red[0][wid] = mx;
@@ -259,12 +269,13 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecSelfArgs a) {
   // loads in flight per lane instead of one dependent load per key
   float acc = 0.f;
   int k = wid;
+#pragma unroll 1
   for (; k + 28 < nk; k += 32) {
-    float vv[8];
+    f16 vv[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) vv[j] = (float)V[(long long)(k + 4 * j) * a.d + lane];
+    for (int j = 0; j < 8; ++j) vv[j] = V[(long long)(k + 4 * j) * a.d + lane];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc += (float)(f16)(sc[k + 4 * j] * inv) * vv[j];
+    for (int j = 0; j < 8; ++j) acc += (float)(f16)(sc[k + 4 * j] * inv) * (float)vv[j];
   }
   for (; k < nk; k += 4) {
     const float p = (float)(f16)(sc[k] * inv);
@@ -296,7 +307,7 @@ constexpr int XA_KC = 64, XA_NS = 24;
 // group), which keeps the kernel at <= 64 VGPRs so a workgroup still fits on a CU beside an
 // encoder GEMM tile (k_gemm4: 2 x 224 of the SIMD's 512)
 template <bool ROWS, int G>
-__global__ __launch_bounds__(256) void k_xattn_partial(XAttnArgs a) {
+__global__ __launch_bounds__(256, 8) void k_xattn_partial(XAttnArgs a) {   // <= 64 VGPRs
   ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
   __shared__ __attribute__((aligned(16))) f16 Vs[XA_KC * 64];
   __shared__ float red[2][G][4];
