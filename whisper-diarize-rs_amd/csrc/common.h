@@ -86,9 +86,6 @@ struct ProjArgs {
   const float* pos; int pos_rows;   // EPI_F32_GELU_POS only
   int M, N, K;
   int epi;
-  // fused LayerNorm prologue (decoder GEMV): A is ignored, rows come from the f32 residual
-  // stream ln_x [M][ldln] normalised with (ln_g, ln_b) -- ggml_norm eps 1e-5.
-  const float* ln_x = nullptr; int ldln = 0; const float* ln_g = nullptr; const float* ln_b = nullptr;
   // EPI_QKV_CACHE
   f16* kc = nullptr; f16* vc = nullptr; long long seq_stride = 0; const int* row_seq = nullptr;
   const int* row_pos = nullptr; int d = 0;
@@ -103,7 +100,7 @@ struct ProjArgs {
   // (k_rowproj: 4 waves split K, fixed k order, fixed wave order in the reduce), so a row's
   // result never depends on how many rows share the launch
   int rows_mma = 0;
-  // optional row map: A / ln_x row m is row_map[m] (logit rows gathered from the residual stream)
+  // optional row map: A row m is row_map[m] (logit rows gathered from the residual stream)
   const int* row_map = nullptr;
   // decoder rows, split-K over workgroups (k_rowproj): ksplit > 1 writes each K slice's f32
   // partial to slab[s][M][N] (bias and epilogue left to k_resid_ln, which sums the slices in
@@ -136,13 +133,12 @@ unsigned long long* prof_slot();   // next clock slot of the sampled-launch ring
 template <typename A>
 inline unsigned long long* prof_attach(A&) { return nullptr; }
 inline unsigned long long* prof_attach(ProjArgs& a) { return a.ts = prof_slot(); }
-void launch_proj(const ProjArgs& a, hipStream_t s);   // picks GEMV (M<=8) or MFMA GEMM
+// M <= 64 (or rows_mma) on the row kernel k_rowproj, larger M on the MFMA GEMM tiles
+void launch_proj(const ProjArgs& a, hipStream_t s);
 // fp8 encoder GEMM (BASELINE configs[4]): ProjArgs::A8 / B8 / a_scale / b_scale, M > 64,
 // N % 128 == 0, K % 128 == 0; epilogues as launch_proj
 void launch_proj_fp8(const ProjArgs& a, hipStream_t s);
 // per-row fp8 quantisation: y[r][0..K) = e4m3(x[r][k] / scale[r]), scale[r] = max_k |x[r][k]| / 448
 void launch_quant_rows(const f16* x, int ldx, int M, int K, uint8_t* y, int ldy, float* scale, hipStream_t s);
-// the LayerNorm prologue of a decode-step projection as its own launch (k_dgemv's arithmetic):
-// rows ln_x -> y [M][ldy] f16
 
 }  // namespace wdr

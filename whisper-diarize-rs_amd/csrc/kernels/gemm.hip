@@ -1129,7 +1129,6 @@ static void launch_rows(const ProjArgs& a, hipStream_t s) {
   WDR_CHECK(a.K % (32 * S) == 0 && a.lda % 8 == 0 && a.ldb % 8 == 0, "row projection: K % (32 ksplit), lda / ldb % 8");
   WDR_CHECK(S == 1 || a.slab, "row projection: a split needs a slab");
   WDR_CHECK(S > 1 || a.out, "row projection: no output");
-  WDR_CHECK(!a.ln_x, "row projection: LayerNorm runs in k_resid_ln, not in the projection");
   WDR_CHECK(a.epi != EPI_QKV_CACHE || (a.kc && a.vc && a.row_seq && a.row_pos && a.d > 0), "qkv-cache epilogue args");
   switch (a.epi) {
     case EPI_F16: launch_rows_epi<EPI_F16>(a, s); break;

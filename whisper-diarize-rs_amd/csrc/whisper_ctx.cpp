@@ -111,6 +111,12 @@ std::recursive_mutex& hip_alloc_mutex() {
 // launch, a barrier packet waiting on a slot event).  A stream created with a CU mask gets a
 // dedicated queue; the mask here is every CU of the device.  kind: a WDR_<kind>_HWQ env knob
 // (0 = the shared priority pool, A/B runs), default `def`.
+// WDR_NO_GRAPH: eager decode steps and encode batches (no hipGraph replay); read once
+static bool no_graph() {
+  static const bool v = getenv("WDR_NO_GRAPH") != nullptr;
+  return v;
+}
+
 hipStream_t dedicated_stream(const char* knob, bool def, int prio) {
   const char* e = getenv(knob);
   const bool on = e ? atoi(e) != 0 : def;
@@ -1297,7 +1303,7 @@ bool State::top_up_batch(int j) {
     // kStepEvery batches runs eagerly with its launches sampled 1 in kEvery (prof.h), the rate
     // decode steps are sampled at -- a uniform sample of the encoder GEMMs
     const bool sampled = prof_step();
-    if (enc_graph && g1 - g0 == kBatch && !getenv("WDR_NO_GRAPH") && !sampled) {
+    if (enc_graph && g1 - g0 == kBatch && !no_graph() && !sampled) {
       const bool f8 = ctx_.fp8_encoder.load();
       const int key = slot0 * 4 + (f8 ? 2 : 0) + (m.plan.detect_lang ? 1 : 0);   // the batch's slots
       Impl::EncGraph& eg = m.enc_graphs[key];
@@ -1448,7 +1454,7 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
   Impl& m = *m_;
   WDR_CHECK(R >= 1 && R <= NSEQ, "decoder step: row count out of range");
   const bool sampled = prof_step();
-  if (sampled || getenv("WDR_NO_GRAPH")) {
+  if (sampled || no_graph()) {
     // live per-kernel HIP-event timing cannot read events recorded inside a graph on this
     // ROCm: a sampled step runs the same kernels eagerly (prof.h)
     prof_in_step(sampled);
@@ -2947,7 +2953,7 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
   const bool decode_only = n_pre == 0 && n_dtw == 0;
   static FILE* blog = getenv("WDR_BATCH_LOG") ? fopen(getenv("WDR_BATCH_LOG"), "w") : nullptr;
   if (blog) WDR_HIP(hipEventRecord(m.ev0, m.s));
-  if (sampled || getenv("WDR_NO_GRAPH") || !decode_only) {
+  if (sampled || no_graph() || !decode_only) {
     // sampled step for live kernel timing (prof.h), graphs disabled, or a mixed batch
     prof_in_step(sampled);
     try {

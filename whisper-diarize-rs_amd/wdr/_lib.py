@@ -9,7 +9,8 @@ import os
 import re
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libwdr.so")
+# WDR_AB_LIB: another build of libwdr for same-box A/B runs (tools/ab_env.sh); unset = in-tree
+LIB_PATH = os.environ.get("WDR_AB_LIB") or os.path.join(PKG_DIR, "libwdr.so")
 HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "wdr.h")
 
 i8, i32, i64, u64 = C.c_int8, C.c_int32, C.c_int64, C.c_uint64
