@@ -389,6 +389,9 @@ int wdr_dbg_proj(const uint16_t* a_f16, const uint16_t* w_f16, const float* bias
 /* epi (EPI_F32_RESID) | WDR_DBG_PROJ_SPLIT: a residual projection as the decoder rows run it --
  * the K slices into slabs, then their sum + bias added to out (N <= 1280) */
 #define WDR_DBG_PROJ_SPLIT 0x400
+/* epi | WDR_DBG_PROJ_GEMM1: M > 64 on the register-staged reference tile (k_gemm) whatever the
+ * dispatch rule picks -- the tiled GEMM family is bit-identical to it */
+#define WDR_DBG_PROJ_GEMM1 0x800
 int wdr_dbg_attn(const uint16_t* q, const uint16_t* k, const uint16_t* v, int32_t Tq, int32_t Tk, int32_t n_head,
                  int32_t causal, float* out /* [Tq][n_head*64] */);
 // decode-step cross-attention over 1500 keys (beam groups / per-row slots; see engine.cpp)

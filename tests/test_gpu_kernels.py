@@ -53,12 +53,15 @@ def test_projection_matches_fp32_reference(lib, M):
     np.testing.assert_allclose(_proj(lib, a, w, bias, 2, base), base + ref, rtol=0, atol=2e-4)
 
 
+GEMM1 = 0x800   # include/wdr.h WDR_DBG_PROJ_GEMM1
+
+
 @pytest.mark.parametrize("N", [1280, 2560])
-def test_encoder_gemm_tiles(lib, N, monkeypatch):
+def test_encoder_gemm_tiles(lib, N):
     """The encoder-batch GEMMs (M >= 4096): k_gemm5 (256 x 128 ping-pong, N = 1280) and k_gemm4
     (256 x 256 ping-pong, N = 2560), a ragged last row tile (M = 4200): against the fp64 product
     within the f32 / f16 output rounding, and bit for bit equal to the register-staged k_gemm
-    (WDR_GEMM1=1), whose per-row arithmetic every other GEMM path shares."""
+    (WDR_DBG_PROJ_GEMM1), whose per-row arithmetic every other GEMM path shares -- every epilogue."""
     rng = np.random.default_rng(N)
     M, K = 4200, 256
     a = rng.standard_normal((M, K)).astype(np.float16).astype(np.float32)
@@ -71,9 +74,27 @@ def test_encoder_gemm_tiles(lib, N, monkeypatch):
     base = rng.standard_normal((M, N)).astype(np.float32)
     resid = _proj(lib, a, w, bias, 2, base)
     np.testing.assert_allclose(resid, base + ref, rtol=0, atol=2e-4)
-    monkeypatch.setenv("WDR_GEMM1", "1")
-    np.testing.assert_array_equal(_proj(lib, a, w, bias, 3), got)
-    np.testing.assert_array_equal(_proj(lib, a, w, bias, 2, base), resid)
+    np.testing.assert_array_equal(_proj(lib, a, w, bias, 3 | GEMM1), got)
+    np.testing.assert_array_equal(_proj(lib, a, w, bias, 2 | GEMM1, base), resid)
+    np.testing.assert_array_equal(_proj(lib, a, w, bias, 0 | GEMM1), _proj(lib, a, w, bias, 0))
+    np.testing.assert_array_equal(_proj(lib, a, w, bias, 1 | GEMM1), _proj(lib, a, w, bias, 1))
+
+
+@pytest.mark.parametrize("M", [300, 1500])
+def test_gemm2_tiles_bit_identical(lib, M):
+    """k_gemm2 (the 128 x 128 LDS-DMA tile of single-window encodes, M < 4096) with its
+    transposed-accumulator vector epilogue: every epilogue bit for bit equal to the reference
+    tile k_gemm (WDR_DBG_PROJ_GEMM1), a ragged last row tile included."""
+    rng = np.random.default_rng(M + 7)
+    K, N = 512, 1280
+    a = rng.standard_normal((M, K)).astype(np.float16).astype(np.float32)
+    w = (rng.standard_normal((N, K)) * 0.05).astype(np.float16).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32) * 0.1
+    base = rng.standard_normal((M, N)).astype(np.float32)
+    for epi in (0, 1, 3):
+        np.testing.assert_array_equal(_proj(lib, a, w, bias, epi), _proj(lib, a, w, bias, epi | GEMM1))
+    np.testing.assert_array_equal(_proj(lib, a, w, bias, 2, base), _proj(lib, a, w, bias, 2 | GEMM1, base))
+    np.testing.assert_array_equal(_proj(lib, a, w, None, 3), _proj(lib, a, w, None, 3 | GEMM1))
 
 
 ROWS = 0x200   # include/wdr.h WDR_DBG_PROJ_ROWS

@@ -71,6 +71,7 @@ int main(int argc, char** argv) {
       setenv("WDR_GEMM4_GM", variant == 5 ? "8" : "4", 1);
       if (variant == 0) setenv("WDR_GEMM1", "1", 1);
       if (variant == 1) setenv("WDR_GEMM3", "0", 1);
+      gemm_knobs_reload();   // launch_proj reads the knobs once per process
       // EPI_F32 into a zeroed buffer for the cross-check (the timed runs use the real epilogue)
       const size_t on = (size_t)M * sh.N;
       if (sh.N <= 5120) {

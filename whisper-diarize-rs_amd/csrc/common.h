@@ -59,9 +59,17 @@ __host__ __device__ inline long long xkv_v_off(int l, int H) { return (long long
 __host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 __device__ __forceinline__ float gelu_tanh(float x) {
-  // ggml_gelu (tanh form): 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3)))
-  const float c = 0.7978845608028654f;
-  return 0.5f * x * (1.0f + tanhf(c * (x + 0.044715f * x * x * x)));
+  // ggml_gelu (tanh form): 0.5 x (1 + tanh(u)), u = sqrt(2/pi) (x + 0.044715 x^3), evaluated as
+  // x * sigmoid(2u) = x / (1 + exp(-2u)) -- the same function without the cancellation of
+  // 1 + tanh at large negative u, in 7 instructions (v_exp_f32 + v_rcp_f32) where tanhf takes ~30:
+  // the GELU epilogue of the encoder fc1 GEMM is MFMA-shadow work (within 5e-7 absolute of the
+  // tanhf form over |x| <= 12, far under the f16 rounding of the output)
+  // Contraction off and the one fma explicit: every kernel's epilogue (scalar or 4-wide) then
+  // evaluates the same instruction sequence, so the GEMM family stays bit-identical under GELU.
+#pragma clang fp contract(off)
+  const float c2 = 2.0f * 0.7978845608028654f;
+  const float u2 = c2 * __builtin_fmaf(0.044715f * x, x * x, x);
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u2 * -1.4426950408889634f));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -96,6 +104,9 @@ struct ProjArgs {
   const float* a_scale = nullptr; const float* b_scale = nullptr;
   // k_gemm4 tile order: groups of tile_gm row tiles walked column by column (0: row-major)
   int tile_gm = 0;
+  // M > 64: the register-staged reference tile k_gemm whatever the dispatch rule picks
+  // (wdr_dbg_proj WDR_DBG_PROJ_GEMM1: the bit-identity tests of the tiled GEMM family)
+  int gemm_ref = 0;
   // decoder rows of any count (steps, prompt prefills, DTW re-forwards) on the row kernel
   // (k_rowproj: 4 waves split K, fixed k order, fixed wave order in the reduce), so a row's
   // result never depends on how many rows share the launch
@@ -135,6 +146,9 @@ inline unsigned long long* prof_attach(A&) { return nullptr; }
 inline unsigned long long* prof_attach(ProjArgs& a) { return a.ts = prof_slot(); }
 // M <= 64 (or rows_mma) on the row kernel k_rowproj, larger M on the MFMA GEMM tiles
 void launch_proj(const ProjArgs& a, hipStream_t s);
+// re-read the encoder GEMM dispatch knobs (WDR_GEMM*), which launch_proj reads once per process:
+// tools/gemm_bench's per-variant A/B only
+void gemm_knobs_reload();
 // fp8 encoder GEMM (BASELINE configs[4]): ProjArgs::A8 / B8 / a_scale / b_scale, M > 64,
 // N % 128 == 0, K % 128 == 0; epilogues as launch_proj
 void launch_proj_fp8(const ProjArgs& a, hipStream_t s);

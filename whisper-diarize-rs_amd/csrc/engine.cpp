@@ -2125,12 +2125,14 @@ int wdr_dbg_proj(const uint16_t* a16, const uint16_t* w16, const float* bias, in
     if (epi & 0x100) return fail("WDR_DBG_PROJ_STEP: the decode-step GEMV schedule was removed (the row kernel serves every row count)");
     const bool rows = (epi & 0x200) != 0;
     const bool split = (epi & 0x400) != 0;
+    const bool gemm_ref = (epi & 0x800) != 0;
     epi &= 0xff;
     const bool f16out = epi == EPI_F16 || epi == EPI_F16_GELU;
     std::vector<f16> h16;
     if (!f16out) WDR_HIP(hipMemcpy(dout.p, out, dout.bytes, hipMemcpyHostToDevice));
     ProjArgs a{da.as<f16>(), K, dw.as<f16>(), K, bias ? db.as<float>() : nullptr, dout.p, N, nullptr, 0, M, N, K, epi};
     a.rows_mma = rows ? 1 : 0;
+    a.gemm_ref = gemm_ref ? 1 : 0;
     if (split) {
       // WDR_DBG_PROJ_SPLIT: a residual projection as rows_forward runs it -- K slices into
       // slabs (k_rowproj), then k_resid_ln adds their sum and the bias to out

@@ -55,6 +55,49 @@ __device__ __forceinline__ void epi_store(const ProjArgs& a, int row, int col, f
   }
 }
 
+// Four consecutive columns col..col+3 of one row (col % 4 == 0; N, ldo, d, pos and bias rows
+// multiples of 4 elements): the epilogue of the transposed-accumulator tiles (k_gemm4 / k_gemm5),
+// one 8-B (f16) or 16-B (f32) access per lane where epi_store makes four scalar ones; per element
+// the same arithmetic as epi_store, so the same bits.
+template <int EPI>
+__device__ __forceinline__ void epi_store4(const ProjArgs& a, int row, int col, f32x4 v, bool has_bias, f32x4 bias) {
+  if (row >= a.M) return;
+  if (has_bias) v += bias;
+  if constexpr (EPI == EPI_F16 || EPI == EPI_F16_GELU) {
+    f16x4 h;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) h[r] = (f16)(EPI == EPI_F16_GELU ? gelu_tanh(v[r]) : v[r]);
+    *(f16x4*)((f16*)a.out + (size_t)row * a.ldo + col) = h;
+  } else if constexpr (EPI == EPI_F32_RESID) {
+    f32x4* o = (f32x4*)((float*)a.out + (size_t)row * a.ldo + col);
+    *o = *o + v;
+  } else if constexpr (EPI == EPI_F32) {
+    *(f32x4*)((float*)a.out + (size_t)row * a.ldo + col) = v;
+  } else if constexpr (EPI == EPI_F32_GELU_POS) {
+    const f32x4 p = *(const f32x4*)(a.pos + (size_t)(row % a.pos_rows) * a.N + col);
+    f32x4 g;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) g[r] = gelu_tanh(v[r]) + p[r];
+    *(f32x4*)((float*)a.out + (size_t)row * a.ldo + col) = g;
+  } else {
+    f16x4 h;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) h[r] = (f16)v[r];
+    if constexpr (EPI == EPI_XKV) {
+      const int w = row / XKV_T, t = row - w * XKV_T;
+      *(f16x4*)((f16*)a.out + w * a.seq_stride + (long long)(col >> 6) * XKV_HS + t * 64 + (col & 63)) = h;
+    } else {  // EPI_QKV_CACHE: d % 4 == 0, so the four columns lie in one of Q / K / V
+      if (col < a.d) {
+        *(f16x4*)((f16*)a.out + (size_t)row * a.ldo + col) = h;
+      } else {
+        const long long dst = a.row_seq[row] * a.seq_stride + (long long)a.row_pos[row] * a.d;
+        if (col < 2 * a.d) *(f16x4*)(a.kc + dst + col - a.d) = h;
+        else *(f16x4*)(a.vc + dst + col - 2 * a.d) = h;
+      }
+    }
+  }
+}
+
 template <int EPI>
 __global__ __launch_bounds__(256, 2) void k_gemm(ProjArgs a) {
   ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
@@ -233,23 +276,28 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(ProjArgs a) {
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
+  // transposed accumulators (B fragment first): element 4g..4g+3 of a 32 x 32 tile is row fr,
+  // columns 8g + 4h .. +3 -- four consecutive columns, one vector access (epi_store4)
   const int h = lane >> 5;
+  const bool hb = a.bias != nullptr;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int g = 0; g < 4; ++g) {
+      const int col = bn * GB_N + wc * 64 + j * 32 + 8 * g + 4 * h;
+      const f32x4 bz = hb ? *(const f32x4*)(a.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = bm * GB_M + wr * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int col = bn * GB_N + wc * 64 + j * 32 + fr;
-        epi_store<EPI>(a, row, col, acc[i][j][r]);
+      for (int i = 0; i < 2; ++i) {
+        const f32x4 v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+        epi_store4<EPI>(a, bm * GB_M + wr * 64 + i * 32 + fr, col, v, hb, bz);
       }
+    }
 }
 
 
@@ -469,7 +517,7 @@ __device__ __forceinline__ void gemm4_tile(const ProjArgs& a, f16* lds4, int ori
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[qa * 4 + i][qb * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_f16(af[ks][i], bf[ks][j], acc[qa * 4 + i][qb * 2 + j], 0, 0, 0);
+              __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[ks][j], af[ks][i], acc[qa * 4 + i][qb * 2 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
   // end of a load section: fragments in registers, then the barrier into the MFMA section
@@ -522,16 +570,18 @@ __device__ __forceinline__ void gemm4_tile(const ProjArgs& a, f16* lds4, int ori
   }
   if (grp == 0) __builtin_amdgcn_s_barrier();   // matches the stagger barrier of waves 4-7
 
+  // transposed accumulators (B fragment first): lane (fr, fq) holds row fr, columns fq*4..+3 of
+  // every 16 x 16 tile -- four consecutive columns, one vector access
+  const bool hb = a.bias != nullptr;
+  f32x4 bz[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    bz[j] = hb ? *(const f32x4*)(a.bias + bn * G3_N + wn * 64 + j * 16 + fq * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = bm * G3_M + grp * 128 + i * 16 + fq * 4 + r;
-        const int col = bn * G3_N + wn * 64 + j * 16 + fr;
-        epi_store<EPI>(a, row, col, acc[i][j][r]);
-      }
+      epi_store4<EPI>(a, bm * G3_M + grp * 128 + i * 16 + fr, bn * G3_N + wn * 64 + j * 16 + fq * 4, acc[i][j], hb, bz[j]);
 }
 
 // Persistent form: gridDim.x workgroups (a multiple of 8, <= the tile count) walk the tiles
@@ -650,7 +700,7 @@ __device__ __forceinline__ void gemm5_tile(const ProjArgs& a, f16* lds5, int ori
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[qa * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[ks][i], bf[ks][j], acc[qa * 4 + i][j], 0, 0, 0);
+          acc[qa * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[ks][j], af[ks][i], acc[qa * 4 + i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
   auto sync_in = [&]() {
@@ -699,16 +749,17 @@ __device__ __forceinline__ void gemm5_tile(const ProjArgs& a, f16* lds5, int ori
   }
   if (grp == 0) __builtin_amdgcn_s_barrier();   // matches the stagger barrier of waves 4-7
 
+  // transposed accumulators, as k_gemm4
+  const bool hb = a.bias != nullptr;
+  f32x4 bz[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    bz[j] = hb ? *(const f32x4*)(a.bias + bn * 128 + wn * 32 + j * 16 + fq * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = bm * G3_M + grp * 128 + i * 16 + fq * 4 + r;
-        const int col = bn * 128 + wn * 32 + j * 16 + fr;
-        epi_store<EPI>(a, row, col, acc[i][j][r]);
-      }
+      epi_store4<EPI>(a, bm * G3_M + grp * 128 + i * 16 + fr, bn * 128 + wn * 32 + j * 16 + fq * 4, acc[i][j], hb, bz[j]);
 }
 
 template <int EPI>
@@ -992,35 +1043,35 @@ __global__ __launch_bounds__(256) void k_rowproj(ProjArgs a) {
   }
 }
 
-// A/B knobs of the encoder GEMM dispatch, read once per process (tools/gemm_bench A/B runs set
-// them per run): WDR_GEMM1=1 every M > 64 projection on k_gemm; WDR_GEMM3=0 the big shapes off
-// k_gemm3; WDR_GEMM4=0|1 the ping-pong 256 x 256 GEMM off / forced on for every shape it takes
-// (unset: the measured dispatch rule); WDR_GEMM4_GM row tiles per group of the k_gemm4 / k_gemm5
-// tile order (default 4); WDR_GEMM5=0 the narrow projections on k_gemm4's tiles
+// A/B knobs of the encoder GEMM dispatch, read once per process (gemm_knobs_reload: tools/gemm_bench
+// A/B runs set them per variant): WDR_GEMM1=1 every M > 64 projection on k_gemm; WDR_GEMM3=0 the
+// big shapes off k_gemm3; WDR_GEMM4=0|1 the ping-pong 256 x 256 GEMM off / forced on for every
+// shape it takes (unset: the measured dispatch rule); WDR_GEMM4_GM row tiles per group of the
+// k_gemm4 / k_gemm5 tile order (default 4); WDR_GEMM5=0 the narrow projections on k_gemm4's
+// tiles; WDR_GEMM_CUS persistent k_gemm4 workgroups (multiple of 8; default one per tile)
+struct GemmKnobs {
+  bool gemm1, gemm3, gemm5;
+  int gemm4, tile_gm, cus;
+};
 static int env_int(const char* name, int def) {
   const char* e = getenv(name);
   return e ? atoi(e) : def;
 }
-static bool gemm1_forced() {
-  static const bool v = env_int("WDR_GEMM1", 0) != 0;
-  return v;
+static GemmKnobs read_knobs() {
+  GemmKnobs k;
+  k.gemm1 = env_int("WDR_GEMM1", 0) != 0;
+  k.gemm3 = env_int("WDR_GEMM3", 1) != 0 && !k.gemm1;
+  k.gemm4 = env_int("WDR_GEMM4", -1);
+  k.tile_gm = env_int("WDR_GEMM4_GM", 4);
+  k.gemm5 = env_int("WDR_GEMM5", 1) != 0;
+  k.cus = env_int("WDR_GEMM_CUS", 0) / 8 * 8;
+  return k;
 }
-static bool gemm3_enabled() {
-  static const bool v = env_int("WDR_GEMM3", 1) != 0 && !gemm1_forced();
-  return v;
+static GemmKnobs& knobs() {
+  static GemmKnobs k = read_knobs();
+  return k;
 }
-static int gemm4_mode() {
-  static const int v = env_int("WDR_GEMM4", -1);
-  return v;
-}
-static int gemm_tile_gm() {
-  static const int v = env_int("WDR_GEMM4_GM", 4);
-  return v;
-}
-static bool gemm5_on() {
-  static const bool v = env_int("WDR_GEMM5", 1) != 0;
-  return v;
-}
+void gemm_knobs_reload() { knobs() = read_knobs(); }
 
 template <int EPI>
 static void launch_epi(const ProjArgs& a, hipStream_t s) {
@@ -1028,8 +1079,11 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
   const double bytes = (double)a.N * a.K * 2 + (double)a.M * a.K * 2 + (double)a.M * a.N * ob;
   const double flops = 2.0 * a.M * a.N * a.K;
   WDR_CHECK(a.M > 64, "encoder GEMM: more than 64 rows (fewer go to the row kernel)");
-  if (a.N % 128 == 0 && a.N < 2048 && a.K % G3_BK == 0 && a.M >= 4096 && !gemm1_forced() && gemm5_on() &&
-             gemm4_mode() != 0 && (a.N / G3_N) * cdiv(a.M, G3_M) < 192) {
+  const GemmKnobs& kn = knobs();
+  const bool ref = kn.gemm1 || a.gemm_ref;
+  const bool vec4 = a.ldo % 4 == 0 && (a.epi != EPI_QKV_CACHE || a.d % 4 == 0);   // epi_store4
+  if (a.N % 128 == 0 && a.N < 2048 && a.K % G3_BK == 0 && a.M >= 4096 && !ref && vec4 && kn.gemm5 &&
+             kn.gemm4 != 0 && (a.N / G3_N) * cdiv(a.M, G3_M) < 192) {
     // the narrow encoder projections (o, fc2) where 256 x 256 tiles would leave CUs idle: 256 x
     // 128 tiles fill 240 of 256 CUs at M = 6000 (tools/gemm_bench: o 53 vs 62 us on k_gemm2, fc2
     // 107 vs 126 us; at M = 12000 k_gemm4's 235 tiles are faster: fc2 194 vs 216 us)
@@ -1039,12 +1093,11 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
     }();
     (void)attr5;
     ProjArgs g = a;
-    g.tile_gm = gemm_tile_gm();
+    g.tile_gm = kn.tile_gm;
     dim3 grid((a.N / 128) * cdiv(a.M, G3_M));
     wdr_launch(PROF_GEMM, bytes, flops, k_gemm5<EPI>, grid, dim3(512), G5_LDS, s, g);
-  } else if (a.N % G3_N == 0 && a.K % G3_BK == 0 && !gemm1_forced() &&
-             (gemm4_mode() == 1 ||
-              (gemm4_mode() != 0 && (a.M >= 4096 || a.N >= 16384)))) {
+  } else if (a.N % G3_N == 0 && a.K % G3_BK == 0 && !ref && vec4 &&
+             (kn.gemm4 == 1 || (kn.gemm4 != 0 && (a.M >= 4096 || a.N >= 16384)))) {
     // ping-pong 256 x 256 tiles (tools/gemm_bench, large-v3, alone on the GPU): M = 6000 qkv 600
     // vs 557 (k_gemm2), fc1 616 vs 574 (k_gemm3), cross-K/V 818 vs 742 TFLOP/s; M = 12000 every
     // shape (o 394 vs 382, fc2 811 vs 743); M = 1500 cross-K/V 773 vs 616.  The N = 1280 shapes
@@ -1055,17 +1108,12 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
       return true;
     }();
     (void)attr4;
-    // WDR_GEMM_CUS: persistent workgroups (multiple of 8; default one per tile)
     const int ntiles = (a.N / G3_N) * cdiv(a.M, G3_M);
-    static const int cus = [] {
-      const char* e = getenv("WDR_GEMM_CUS");
-      return e ? atoi(e) / 8 * 8 : 0;
-    }();
-    dim3 grid(cus > 0 && cus < ntiles ? cus : ntiles);
+    dim3 grid(kn.cus > 0 && kn.cus < ntiles ? kn.cus : ntiles);
     ProjArgs g = a;
-    g.tile_gm = gemm_tile_gm();
+    g.tile_gm = kn.tile_gm;
     wdr_launch(PROF_GEMM, bytes, flops, k_gemm4<EPI>, grid, dim3(512), G4_LDS, s, g);
-  } else if ((a.N >= 5120 || a.M >= 9000) && a.M > 2048 && a.N % G3_N == 0 && a.K % G3_BK == 0 && gemm3_enabled()) {
+  } else if ((a.N >= 5120 || a.M >= 9000) && a.M > 2048 && a.N % G3_N == 0 && a.K % G3_BK == 0 && kn.gemm3 && !ref) {
     // 256 x 256 tiles where they measured faster (tools/gemm_bench, large-v3 shapes): M = 6000
     // fc1 574 vs 509 TFLOP/s, cross-K/V 743 vs 641; at M = 12000 every encoder shape (qkv 667 vs
     // 520, o 387 vs 335, fc1 550 vs 527, fc2 746 vs 620).  Below that the 120..360 tiles of the
@@ -1077,7 +1125,7 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
     (void)attr;
     dim3 grid((a.N / G3_N) * cdiv(a.M, G3_M));
     wdr_launch(PROF_GEMM, bytes, flops, k_gemm3<EPI>, grid, dim3(512), G3_LDS, s, a);
-  } else if (a.K % G2_BK == 0 && a.N <= 4096 && !gemm1_forced()) {
+  } else if (a.K % G2_BK == 0 && a.N <= 4096 && !ref && vec4) {
     // LDS-DMA GEMM where it measured faster (tools/gemm_bench, M = 6000: qkv -5 %, o -11 %,
     // fc2 -23 %; fc1 and the 82k-column cross-K/V GEMM stay on k_gemm, +8 % / +7 % there)
     dim3 grid((a.N / GB_N) * cdiv(a.M, GB_M));
