@@ -69,7 +69,11 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 #pragma clang fp contract(off)
   const float c2 = 2.0f * 0.7978845608028654f;
   const float u2 = c2 * __builtin_fmaf(0.044715f * x, x * x, x);
-  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u2 * -1.4426950408889634f));
+  float g = x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u2 * -1.4426950408889634f));
+  // materialised in f32: the caller's f16 conversion must not fuse with the multiply into a
+  // single-rounding v_fma_mix (the compiler does so in some epilogues and not in others)
+  asm("" : "+v"(g));
+  return g;
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

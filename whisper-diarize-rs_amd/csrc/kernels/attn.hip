@@ -63,28 +63,30 @@ __global__ __launch_bounds__(256) void k_flash_attn(FlashArgs a) {
   // K / V tiles are register-staged one tile ahead: the loads of tile k0 + 64 are issued right
   // after tile k0 is published to LDS and land while tile k0 is multiplied; they are written to
   // LDS after the next barrier
+  // thread t stages keys 2(t/8) and 2(t/8) + 1, dims 8(t%8)..+7: per dim it holds two
+  // consecutive keys, so the transposed V image takes 8 packed 4-B writes instead of 16 scalar
   f16x8 kreg[2], vreg[2];
+  const int sr = 2 * (tid >> 3), scol = (tid & 7) * 8;
   auto load_tile = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int c = tid + 256 * i;
-      const int r = c >> 3, col = (c & 7) * 8;
-      int key = kt + r;
+      int key = kt + sr + i;
       key = key < kmax ? key : kmax - 1;
-      kreg[i] = *(const f16x8*)(K + (long long)key * a.ldk + col);
-      vreg[i] = *(const f16x8*)(V + (long long)key * a.ldv + col);
+      kreg[i] = *(const f16x8*)(K + (long long)key * a.ldk + scol);
+      vreg[i] = *(const f16x8*)(V + (long long)key * a.ldv + scol);
     }
   };
+  // scores in log2 units: p = 2^(s * scale * log2(e) - m), one fma + v_exp_f32 per score
+  const float sl2 = a.scale * 1.4426950408889634f;
   if (kbeg < kmax) load_tile(kbeg);
   for (int k0 = kbeg; k0 < kmax; k0 += FA_KB) {
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 256 * i;
-      const int r = c >> 3, col = (c & 7) * 8;
-      *(f16x8*)(Ks + r * FA_KS + col) = kreg[i];
+    for (int i = 0; i < 2; ++i) *(f16x8*)(Ks + (sr + i) * FA_KS + scol) = kreg[i];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) Vt[(col + e) * FA_VS + r] = vreg[i][e];
+    for (int e = 0; e < 8; ++e) {
+      typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+      *(f16x2_t*)(Vt + (scol + e) * FA_VS + sr) = (f16x2_t){vreg[0][e], vreg[1][e]};
     }
     __syncthreads();
     if (k0 + FA_KB < kmax) load_tile(k0 + FA_KB);
@@ -99,26 +101,35 @@ __global__ __launch_bounds__(256) void k_flash_attn(FlashArgs a) {
         st[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, qf[s], st[t], 0, 0, 0);
       }
     }
+    // raw-score max (the scale is positive: max(s) * sl2 is the max of the scaled scores);
+    // masking only on the last key tile or under the causal mask (wave-uniform branch)
     float mx = -INFINITY;
+    if (!a.causal && k0 + FA_KB <= kmax) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        const bool ok = key < kmax && (!a.causal || key <= qrow);
-        const float sv = ok ? st[t][r] * a.scale : -INFINITY;
-        st[t][r] = sv;
-        mx = fmaxf(mx, sv);
-      }
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[t][r]);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = k0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const bool ok = key < kmax && (!a.causal || key <= qrow);
+          st[t][r] = ok ? st[t][r] : -INFINITY;
+          mx = fmaxf(mx, st[t][r]);
+        }
+    }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mnew = fmaxf(m, mx);
-    const float alpha = (mnew == -INFINITY) ? 1.f : __expf(m - mnew);
+    const float mnew = fmaxf(m, mx == -INFINITY ? -INFINITY : mx * sl2);
+    const float alpha = (mnew == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m - mnew);
+    const float mu = (mnew == -INFINITY) ? 0.f : mnew;   // masked scores: 2^-inf = 0
     float rs = 0.f;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = (st[t][r] == -INFINITY) ? 0.f : __expf(st[t][r] - mnew);
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(st[t][r], sl2, -mu));
         st[t][r] = p;
         rs += p;
       }
@@ -158,7 +169,7 @@ __global__ __launch_bounds__(256) void k_flash_attn(FlashArgs a) {
         *(float4*)(po + 8 * g + 4 * hh) = make_float4(o0[4 * g], o0[4 * g + 1], o0[4 * g + 2], o0[4 * g + 3]);
         *(float4*)(po + 32 + 8 * g + 4 * hh) = make_float4(o1[4 * g], o1[4 * g + 1], o1[4 * g + 2], o1[4 * g + 3]);
       }
-      if (hh == 0) a.part_ml[((long long)b * a.n_head + h) * a.Tq + qrow] = make_float2(m, l);
+      if (hh == 0) a.part_ml[((long long)b * a.n_head + h) * a.Tq + qrow] = make_float2(m * 0.6931471805599453f, l);
     }
     return;
   }
@@ -176,7 +187,7 @@ __global__ __launch_bounds__(256) void k_flash_attn(FlashArgs a) {
       *(f16x4*)(O + 8 * g + 4 * hh) = w0;
       *(f16x4*)(O + 32 + 8 * g + 4 * hh) = w1;
     }
-    if (a.ml && hh == 0) a.ml[((long long)b * a.n_head + h) * a.Tq + qrow] = make_float2(m, l);
+    if (a.ml && hh == 0) a.ml[((long long)b * a.n_head + h) * a.Tq + qrow] = make_float2(m * 0.6931471805599453f, l);
   }
 }
 
