@@ -92,19 +92,18 @@ def pmc_traffic(cls):
 # conv1, conv2, 32 x (qkv, o, fc1, fc2), the cross-K/V projection -- and the self-attention),
 # and a decoder pass's bytes: the decoder weights (streamed once per rows launch, shared by its
 # rows) and one slot's cross-K/V (read once per cross-attention group or MFMA row tile).
-# rows_weight_bytes: the weight bytes a row-kernel launch streams, by k_rowproj's template
-# arguments <EPI, MT, NT, U, KS> (csrc/kernels/gemm.hip): KS 5 = o / xo (d x d, split into 5 K
-# slices), KS 8 = fc2 (d x 4d, 8 slices); KS 1 by epilogue: 5 qkv (3d x d), 0 xq (d x d), 1 fc1
-# (4d x d), 3 logits (V x d); large-v3 d = 1280
+# rows_weight_bytes: the weight bytes a row-kernel launch streams, by k_skinny's template
+# arguments <EPI, MT, NT, W, LN, U> (csrc/kernels/gemm.hip): EPI 5 qkv (3d x d), 2 o / xo (d x d)
+# or fc2 (d x 4d: the 16-wave form), 0 xq (d x d), 1 fc1 (4d x d), 3 logits (V x d); large-v3
+# d = 1280
 _D, _V = 1280, 51866
 
 
 def rows_weight_bytes(targs):
-    epi, _mt, _nt, _u, ks = (int(x) for x in targs.split(","))
-    if ks == 5:
-        return _D * _D * 2
-    if ks == 8:
-        return 4 * _D * _D * 2
+    f = [x.strip() for x in targs.split(",")]
+    epi, waves = int(f[0]), int(f[3]) if len(f) > 3 else 4
+    if epi == 2:
+        return (4 if waves == 16 else 1) * _D * _D * 2
     return {5: 3 * _D * _D * 2, 0: _D * _D * 2, 1: 4 * _D * _D * 2, 3: _V * _D * 2}.get(epi)
 
 
@@ -187,8 +186,8 @@ def trace_roofline(model, fp8=False):
         import csv
         for r in csv.DictReader(open(stats)):
             nm = r.get("Name", r.get("KernelName", ""))
-            if "k_rowproj<" in nm:
-                key = nm[nm.index("k_rowproj<") + 10:].split(">")[0].replace(" ", "")
+            if "k_skinny<" in nm:
+                key = nm[nm.index("k_skinny<") + 9:].split(">")[0].replace(" ", "")
                 b = wb(key)
                 if b:
                     rows_bytes += float(r.get("Calls", 0)) * b

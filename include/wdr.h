@@ -384,11 +384,8 @@ int wdr_dbg_proj(const uint16_t* a_f16, const uint16_t* w_f16, const float* bias
                  int32_t epi, float* out /* [M][N] f32 (f16 epilogues are widened) */);
 /* epi | WDR_DBG_PROJ_ROWS: the decoder-rows kernel (any M, per-row arithmetic independent of M);
  * projections of <= 64 rows run on it anyway (0x100, the removed decode-step GEMV schedule of
- * ABI <= 4, is rejected) */
+ * ABI <= 4, and 0x400, a split-K residual form tried in round 4, are rejected) */
 #define WDR_DBG_PROJ_ROWS 0x200
-/* epi (EPI_F32_RESID) | WDR_DBG_PROJ_SPLIT: a residual projection as the decoder rows run it --
- * the K slices into slabs, then their sum + bias added to out (N <= 1280) */
-#define WDR_DBG_PROJ_SPLIT 0x400
 /* epi | WDR_DBG_PROJ_GEMM1: M > 64 on the register-staged reference tile (k_gemm) whatever the
  * dispatch rule picks -- the tiled GEMM family is bit-identical to it */
 #define WDR_DBG_PROJ_GEMM1 0x800

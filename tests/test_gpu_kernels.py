@@ -105,8 +105,8 @@ ROWS = 0x200   # include/wdr.h WDR_DBG_PROJ_ROWS
 def test_rows_projection_bit_identical_any_m(lib, N, K, epi):
     """The decoder-rows kernel (csrc/rows.h: every decoder projection of steps, prompt prefills
     and DTW re-forwards): a row's result must not depend on how many rows share the launch --
-    M = 1 .. 300 rows, one or two row tiles per workgroup, the narrow (16-column) and wide
-    (32-column) tilings -- bit for bit, and match the fp64 product."""
+    M = 1 .. 300 rows, one to several row tiles, the narrow (16-column) and wide (32-column)
+    tilings, the 16-wave K = 5120 form -- bit for bit, and match the fp64 product."""
     rng = np.random.default_rng(N + K + epi + 1)
     MX = 300
     a = rng.standard_normal((MX, K)).astype(np.float16).astype(np.float32)
@@ -124,31 +124,6 @@ def test_rows_projection_bit_identical_any_m(lib, N, K, epi):
     # a row in the middle of a launch equals the same row alone
     one = _proj(lib, a[257:258], w, bias, epi | ROWS, base[257:258] if epi == 2 else None)
     np.testing.assert_array_equal(one, full[257:258])
-
-
-SPLIT = 0x400   # include/wdr.h WDR_DBG_PROJ_SPLIT
-
-
-@pytest.mark.parametrize("K", [1280, 5120])
-def test_rows_split_projection_bit_identical_any_m(lib, K):
-    """The decoder's residual projections (o, xo: 5 K slices; fc2: 8) as rows_forward runs them:
-    k_rowproj writes each K slice's partial to a slab, k_resid_ln adds the slices in order plus
-    the bias to the residual -- bit-identical for a row whatever M, and the fp64 product within
-    f32 accumulation error."""
-    N, MX = 1280, 300
-    rng = np.random.default_rng(K + 7)
-    a = rng.standard_normal((MX, K)).astype(np.float16).astype(np.float32)
-    w = (rng.standard_normal((N, K)) * 0.03).astype(np.float16).astype(np.float32)
-    bias = rng.standard_normal(N).astype(np.float32) * 0.1
-    base = rng.standard_normal((MX, N)).astype(np.float32)
-    full = _proj(lib, a, w, bias, 2 | ROWS | SPLIT, base)
-    ref = base[:20] + (a[:20].astype(np.float64) @ w.T.astype(np.float64) + bias)
-    np.testing.assert_allclose(full[:20], ref, rtol=0, atol=2e-4)
-    for M in (1, 2, 7, 16, 17, 33, 64, 130):
-        got = _proj(lib, a[:M], w, bias, 2 | ROWS | SPLIT, base[:M])
-        np.testing.assert_array_equal(got, full[:M], err_msg="M=%d" % M)
-    # the split and the one-launch forms agree within accumulation error
-    np.testing.assert_allclose(_proj(lib, a[:20], w, bias, 2 | ROWS, base[:20]), full[:20], rtol=0, atol=2e-4)
 
 
 def test_projection_logits_shape(lib):

@@ -1,7 +1,7 @@
 // Co-scheduling probe: how much a decode-step-like chain of dependent kernels slows down beside
-// the encoder's GEMMs, and why.  The chain (hipGraph, replayed): 32 layers x {qkv, o (5 K
-// slices) + residual/LN, xq, fc1 GELU, fc2 (8 K slices) + residual/LN} as rows_forward issues
-// them at R rows (large-v3 shapes, 32 distinct weight copies), or 160 tiny dependent k_layernorm
+// the encoder's GEMMs, and why.  The chain (hipGraph, replayed): 32 layers x {qkv, o, xq, fc1
+// GELU, fc2} as rows_forward issues them at R rows (large-v3 shapes, 32 distinct weight copies,
+// LayerNorm fused into qkv / xq / fc1), or 160 tiny dependent k_layernorm
 // launches ("tiny": boundary + latency only).  The load: a queue of encoder projections (M = 6000: qkv, o, fc1, fc2) on a
 // stream of its own, either CU-masked as the pipeline's encode-ahead streams (32 CUs, 4 per
 // XCD, left free) or on all CUs.
@@ -86,31 +86,29 @@ int main(int argc, char** argv) {
     CK(hipMemset(w.fc1, 0, (size_t)4 * d * d * 2));
     CK(hipMemset(w.fc2, 0, (size_t)4 * d * d * 2));
   }
-  float* slab;
-  CK(hipMalloc(&slab, (size_t)8 * R * d * 4));
-  auto P = [&](const f16* A, int lda, const f16* Wt, void* out, int ldo, int N, int K, int epi, int split) {
-    ProjArgs a{A, lda, Wt, K, split > 1 ? nullptr : bias, out, ldo, nullptr, 0, R, N, K, epi};
+  auto P = [&](const f16* A, int lda, const f16* Wt, void* out, int ldo, int N, int K, int epi, bool ln) {
+    ProjArgs a{A, lda, Wt, K, bias, out, ldo, nullptr, 0, R, N, K, epi};
     a.rows_mma = 1;
-    a.ksplit = split;
-    a.slab = split > 1 ? slab : nullptr;
+    if (ln) {
+      if (R <= 32) {
+        a.ln_x = xf; a.ldln = d; a.ln_g = g; a.ln_b = b;
+      } else {
+        launch_layernorm(xf, d, g, b, att, d, R, d, s);
+        a.A = att;
+        a.lda = d;
+      }
+    }
     launch_proj(a, s);
   };
-  auto RL = [&](int split) {
-    ResidLnArgs r;
-    r.slab = slab; r.S = split; r.R = R; r.bias = bias; r.x = xf; r.d = d; r.g = g; r.b = b; r.h = att;
-    launch_resid_ln(r, s);
-  };
-  // the decoder layer's projections and residual + LayerNorm steps as rows_forward runs them
-  // (attention left out): 7 launches per layer
+  // the decoder layer's projections as rows_forward runs them (attention left out): 5 launches
+  // per layer, LayerNorm fused into qkv / xq / fc1 up to 32 rows
   auto chain = [&] {
     for (int l = 0; l < L; ++l) {
-      P(att, d, W[l].qkv, hq, 3 * d, 3 * d, d, EPI_F16, 1);
-      P(att, d, W[l].o, nullptr, d, d, d, EPI_F32, 5);
-      RL(5);
-      P(att, d, W[l].xq, hq, d, d, d, EPI_F16, 1);
-      P(att, d, W[l].fc1, mlp, 4 * d, 4 * d, d, EPI_F16_GELU, 1);
-      P(mlp, 4 * d, W[l].fc2, nullptr, d, d, 4 * d, EPI_F32, 8);
-      RL(8);
+      P(nullptr, d, W[l].qkv, hq, 3 * d, 3 * d, d, EPI_F16, true);
+      P(att, d, W[l].o, xf, d, d, d, EPI_F32_RESID, false);
+      P(nullptr, d, W[l].xq, hq, d, d, d, EPI_F16, true);
+      P(nullptr, d, W[l].fc1, mlp, 4 * d, 4 * d, d, EPI_F16_GELU, true);
+      P(mlp, 4 * d, W[l].fc2, xf, d, d, 4 * d, EPI_F32_RESID, false);
     }
   };
   auto tiny = [&] {
@@ -178,7 +176,7 @@ int main(int argc, char** argv) {
   printf("R=%d\n", R);
   printf("encoder layer (qkv+o+fc1+fc2, M=6000) alone: masked %.3f ms, all CUs %.3f ms\n", time_enc(se_mask),
          time_enc(se_all));
-  const char* names[2] = {"chain (224 rows launches)", "tiny (160 k_layernorm)"};
+  const char* names[2] = {"chain (160 rows launches)", "tiny (160 k_layernorm)"};
   hipGraphExec_t gs[2] = {g_chain, g_tiny};
   for (int k = 0; k < 2; ++k) {
     const float alone = time_graph(gs[k], 10);
@@ -189,7 +187,7 @@ int main(int argc, char** argv) {
     enc_burst(se_all, 150);
     const float all = time_graph(gs[k], 10);
     CK(hipDeviceSynchronize());
-    const int nl = k == 0 ? 7 * L : 160;
+    const int nl = k == 0 ? 5 * L : 160;
     printf("%-30s alone %.3f ms (%.2f us/launch)  beside masked encoder %.3f ms (x%.2f)  beside unmasked %.3f ms "
            "(x%.2f)\n", names[k], alone, alone * 1e3 / nl, masked, masked / alone, all, all / alone);
     fflush(stdout);

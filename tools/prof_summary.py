@@ -21,7 +21,7 @@ import re
 # GEMMs are k_gemm / k_gemm2..5 / k_gemm8 -- NOT the f32 VALU k_gemm32 of CAM++ / segmentation
 CLASSES = {
     "gemm": re.compile(r"\bk_gemm\d?[<(]"),
-    "rows": re.compile(r"\bk_rowproj<"),                      # decoder row projections (rows.h)
+    "rows": re.compile(r"\bk_skinny<"),                       # decoder row projections (rows.h)
     "flash": re.compile(r"\bk_flash_attn\("),                # encoder self-attention
     "xattn": re.compile(r"\bk_xattn_(partial|mma)\b"),       # decoder cross-attention partials
     "diar": re.compile(r"\bk_(gemm32|lstm_scan|im2col_2d_b|im2col_1d_b|fbank|colstats_b|cam_|inorm|maxpool3|logsoftmax7)"),

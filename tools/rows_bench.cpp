@@ -1,9 +1,8 @@
 // Decoder-row projection microbenchmark (large-v3 decoder shapes): the row kernel
-// (ProjArgs::rows_mma: k_rowproj for any row count) as rows_forward launches it -- qkv / xq /
-// fc1 after a LayerNorm launch, o / fc2 as K slices into slabs + k_resid_ln -- per launch,
-// replayed from a hipGraph of 32 launches over RB_COPIES distinct weight copies (default 32:
-// > the 256 MiB Infinity Cache, HBM-bound; RB_COPIES=1: the weights served from cache, the
-// latency floor of the launch chain).
+// (ProjArgs::rows_mma: k_skinny's arithmetic for any row count, LayerNorm fused up to 32 rows),
+// per launch, replayed from a hipGraph of 32 launches over RB_COPIES distinct weight copies
+// (default 32: > the 256 MiB Infinity Cache, HBM-bound; RB_COPIES=1: the weights served from
+// cache, the latency floor of the launch chain).
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/rows_bench.cpp -Lwhisper-diarize-rs_amd -lwdr \
 //          -Wl,-rpath,'$ORIGIN/../whisper-diarize-rs_amd' -o tools/rows_bench
 #include <hip/hip_runtime.h>
@@ -84,8 +83,6 @@ int main(int argc, char** argv) {
   CK(hipMemset(b, 0, 4 * d * 4));
   CK(hipMemset(bias, 0, 51866 * 4));
   CK(hipMemset(xa, 0, (size_t)MX * 4 * d * 2));
-  float* slab;
-  CK(hipMalloc(&slab, (size_t)8 * MX * d * 4));
   printf("%-14s %4s %10s   (us per launch incl. LN launch; TB/s of the weights)\n", "shape", "M", "rows");
   for (const Shape& sh : shapes) {
     const size_t wel = (size_t)sh.N * sh.K;
@@ -96,31 +93,19 @@ int main(int argc, char** argv) {
       CK(hipMalloc(&W[l], wel * 2));
       CK(hipMemset(W[l], 0, wel * 2));
     }
-    // rows_ksplit (csrc/rows.cpp): the residual projections' K slices
-    const int split = sh.epi == EPI_F32_RESID ? (sh.K <= 2048 ? sh.K / 256 : sh.K / 640) : 1;
     const double mb = wel * 2 / 1e6;
     for (int M : Ms) {
       const float tr = time_graph([&] {
         for (int l = 0; l < nl; ++l) {
           ProjArgs a{xa, sh.K, W[l % nw], sh.K, bias, out, sh.N, nullptr, 0, M, sh.N, sh.K, sh.epi};
           a.rows_mma = 1;
-          if (split > 1) {   // K slices into slabs, then slices + bias + residual (+ LayerNorm)
-            a.epi = EPI_F32;
-            a.bias = nullptr;
-            a.out = nullptr;
-            a.ksplit = split;
-            a.slab = slab;
-            launch_proj(a, s);
-            ResidLnArgs r;
-            r.slab = slab; r.S = split; r.R = M; r.bias = bias; r.x = xf; r.d = d; r.g = g; r.b = b; r.h = hd;
-            launch_resid_ln(r, s);
-            continue;
-          }
-          if (sh.ln) {   // the LayerNorm step of rows_forward (k_resid_ln, no residual)
-            ResidLnArgs r;
-            r.R = M; r.x = xf; r.d = d; r.g = g; r.b = b; r.h = hd;
-            launch_resid_ln(r, s);
-            a.A = hd;
+          if (sh.ln) {
+            if (M <= 32) {
+              a.ln_x = xf; a.ldln = sh.K; a.ln_g = g; a.ln_b = b;
+            } else {
+              launch_layernorm(xf, d, g, b, hd, d, M, d, s);
+              a.A = hd;
+            }
           }
           launch_proj(a, s);
         }

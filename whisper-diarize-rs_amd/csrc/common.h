@@ -98,6 +98,9 @@ struct ProjArgs {
   const float* pos; int pos_rows;   // EPI_F32_GELU_POS only
   int M, N, K;
   int epi;
+  // fused LayerNorm prologue (decoder rows, k_skinny): A is ignored, rows come from the f32
+  // residual stream ln_x [M][ldln] normalised with (ln_g, ln_b) -- ggml_norm eps 1e-5.
+  const float* ln_x = nullptr; int ldln = 0; const float* ln_g = nullptr; const float* ln_b = nullptr;
   // EPI_QKV_CACHE
   f16* kc = nullptr; f16* vc = nullptr; long long seq_stride = 0; const int* row_seq = nullptr;
   const int* row_pos = nullptr; int d = 0;
@@ -112,16 +115,12 @@ struct ProjArgs {
   // (wdr_dbg_proj WDR_DBG_PROJ_GEMM1: the bit-identity tests of the tiled GEMM family)
   int gemm_ref = 0;
   // decoder rows of any count (steps, prompt prefills, DTW re-forwards) on the row kernel
-  // (k_rowproj: 4 waves split K, fixed k order, fixed wave order in the reduce), so a row's
-  // result never depends on how many rows share the launch
+  // (k_skinny's arithmetic: 8 or 16 waves split K, fixed k order, fixed wave order in the
+  // reduce), so a row's result never depends on how many rows share the launch (the LN
+  // prologue normalises each workgroup's own row tiles)
   int rows_mma = 0;
-  // optional row map: A row m is row_map[m] (logit rows gathered from the residual stream)
+  // optional row map: A / ln_x row m is row_map[m] (logit rows gathered from the residual stream)
   const int* row_map = nullptr;
-  // decoder rows, split-K over workgroups (k_rowproj): ksplit > 1 writes each K slice's f32
-  // partial to slab[s][M][N] (bias and epilogue left to k_resid_ln, which sums the slices in
-  // order); 1: the epilogue in the projection
-  int ksplit = 1;
-  float* slab = nullptr;
 };
 
 // Live kernel clock (csrc/prof.cpp): a launch the profiler samples carries ts -> {earliest wave
@@ -148,7 +147,7 @@ unsigned long long* prof_slot();   // next clock slot of the sampled-launch ring
 template <typename A>
 inline unsigned long long* prof_attach(A&) { return nullptr; }
 inline unsigned long long* prof_attach(ProjArgs& a) { return a.ts = prof_slot(); }
-// M <= 64 (or rows_mma) on the row kernel k_rowproj, larger M on the MFMA GEMM tiles
+// M <= 64 (or rows_mma) on the row kernel k_skinny, larger M on the MFMA GEMM tiles
 void launch_proj(const ProjArgs& a, hipStream_t s);
 // re-read the encoder GEMM dispatch knobs (WDR_GEMM*), which launch_proj reads once per process:
 // tools/gemm_bench's per-variant A/B only

@@ -36,7 +36,6 @@
 #include "ggml_file.h"
 #include "model_files.h"
 #include "prof.h"
-#include "rows.h"
 
 using namespace wdr;
 
@@ -2124,7 +2123,7 @@ int wdr_dbg_proj(const uint16_t* a16, const uint16_t* w16, const float* bias, in
     // run on it anyway
     if (epi & 0x100) return fail("WDR_DBG_PROJ_STEP: the decode-step GEMV schedule was removed (the row kernel serves every row count)");
     const bool rows = (epi & 0x200) != 0;
-    const bool split = (epi & 0x400) != 0;
+    if (epi & 0x400) return fail("WDR_DBG_PROJ_SPLIT: the split-K residual projections were removed (k_skinny runs them whole)");
     const bool gemm_ref = (epi & 0x800) != 0;
     epi &= 0xff;
     const bool f16out = epi == EPI_F16 || epi == EPI_F16_GELU;
@@ -2133,29 +2132,6 @@ int wdr_dbg_proj(const uint16_t* a16, const uint16_t* w16, const float* bias, in
     ProjArgs a{da.as<f16>(), K, dw.as<f16>(), K, bias ? db.as<float>() : nullptr, dout.p, N, nullptr, 0, M, N, K, epi};
     a.rows_mma = rows ? 1 : 0;
     a.gemm_ref = gemm_ref ? 1 : 0;
-    if (split) {
-      // WDR_DBG_PROJ_SPLIT: a residual projection as rows_forward runs it -- K slices into
-      // slabs (k_rowproj), then k_resid_ln adds their sum and the bias to out
-      if (epi != EPI_F32_RESID || N > 1280 || N % 4 != 0) return fail("WDR_DBG_PROJ_SPLIT: residual epilogue, N <= 1280");
-      const int S = rows_ksplit(K);
-      DevMem slab((size_t)S * M * N * 4);
-      a.rows_mma = 1;
-      a.bias = nullptr;
-      a.ksplit = S;
-      a.slab = slab.as<float>();
-      launch_proj(a, nullptr);
-      ResidLnArgs r;
-      r.slab = slab.as<float>();
-      r.S = S;
-      r.R = M;
-      r.bias = bias ? db.as<float>() : nullptr;
-      r.x = dout.as<float>();
-      r.d = N;
-      launch_resid_ln(r, nullptr);
-      WDR_HIP(hipDeviceSynchronize());
-      WDR_HIP(hipMemcpy(out, dout.p, dout.bytes, hipMemcpyDeviceToHost));
-      return 0;
-    }
     launch_proj(a, nullptr);
     WDR_HIP(hipDeviceSynchronize());
     if (f16out) {

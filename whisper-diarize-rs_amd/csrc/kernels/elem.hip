@@ -303,75 +303,11 @@ void launch_layernorm(const float* x, int ldx, const float* g, const float* b, f
   WDR_HIP(hipGetLastError());
 }
 
-
-// The decoder rows' residual + LayerNorm step between two projections (rows.cpp): one wave per
-// row, x[r] += (slab[0][r] + ... + slab[S-1][r]) + bias -- the K slices of a split projection
-// (k_rowproj) summed in slice order, so a row's sum does not depend on the launch -- then, with
-// g, h[r] = f16(LayerNorm(x[r]) * g + b) for the next projection (k_layernorm's arithmetic).
-// S = 0: LayerNorm of x only.  d <= 1280, under 64 VGPRs.
-__global__ __launch_bounds__(256) void k_resid_ln(ResidLnArgs a) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (row >= a.R) return;
-  const int d = a.d;
-  float* xr = a.x + (long long)row * d;
-  float v[5][4];
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    const int c = lane * 4 + j * 256;
-    const bool ok = c < d;
-    const int cc = ok ? c : 0;
-    float4 q = *(const float4*)(xr + cc);
-    if (a.S > 0) {
-      float4 acc = *(const float4*)(a.slab + (long long)row * d + cc);
-      for (int k = 1; k < a.S; ++k) {
-        const float4 p = *(const float4*)(a.slab + ((long long)k * a.R + row) * d + cc);
-        acc.x += p.x; acc.y += p.y; acc.z += p.z; acc.w += p.w;
-      }
-      if (a.bias) {
-        const float4 bb = *(const float4*)(a.bias + cc);
-        acc.x += bb.x; acc.y += bb.y; acc.z += bb.z; acc.w += bb.w;
-      }
-      q.x += acc.x; q.y += acc.y; q.z += acc.z; q.w += acc.w;
-      if (ok) *(float4*)(xr + c) = q;
-    }
-    v[j][0] = ok ? q.x : 0.f; v[j][1] = ok ? q.y : 0.f; v[j][2] = ok ? q.z : 0.f; v[j][3] = ok ? q.w : 0.f;
-    s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
-  }
-  if (!a.g) return;
-  s = wave_sum(s);
-  const float mean = s / d;
-  float s2 = 0.f;
-#pragma unroll
-  for (int j = 0; j < 5; ++j)
-    if (lane * 4 + j * 256 < d)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float t = v[j][e] - mean;
-        s2 += t * t;
-      }
-  s2 = wave_sum(s2);
-  const float scale = 1.0f / sqrtf(s2 / d + 1e-5f);
-  f16* hr = a.h + (long long)row * d;
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    const int c = lane * 4 + j * 256;
-    if (c >= d) continue;
-    const float4 g4 = *(const float4*)(a.g + c);
-    const float4 b4 = *(const float4*)(a.b + c);
-    const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, bb[4] = {b4.x, b4.y, b4.z, b4.w};
-    f16x4 o;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = (f16)((v[j][e] - mean) * scale * gg[e] + bb[e]);
-    *(f16x4*)(hr + c) = o;
-  }
-}
-
-void launch_resid_ln(const ResidLnArgs& a, hipStream_t s) {
-  WDR_CHECK(a.d % 4 == 0 && a.d <= 1280 && a.R >= 1 && (a.S == 0 || a.slab) && (!a.g || (a.b && a.h)),
-            "residual + LayerNorm: unsupported shape");
-  WDR_KLAUNCH(k_resid_ln, dim3(cdiv(a.R, 4)), dim3(256), 0, s, a);
+// the rows row_map[0 .. rows) of x (the logit rows of a rows_forward batch), compacted into y
+void launch_layernorm_rows(const float* x, int ldx, const float* g, const float* b, f16* y, int ldy, int rows, int d,
+                           const int* row_map, hipStream_t s) {
+  WDR_CHECK(d % 4 == 0 && d <= 1280 && ldx % 4 == 0 && ldy % 4 == 0, "layernorm: unsupported width");
+  WDR_KLAUNCH(k_layernorm, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, g, b, y, ldy, rows, d, row_map);
   WDR_HIP(hipGetLastError());
 }
 

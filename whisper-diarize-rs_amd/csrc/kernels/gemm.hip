@@ -7,11 +7,11 @@
 //              f16), f32 accumulation, v_mfma_f32_32x32x16_f16.  128x128x32 block tile,
 //              4 waves of 64x64, register-staged double-buffered LDS, row padding for
 //              conflict-free ds_read_b128.  Roofline: MFMA (2.5 PF/s dense f16).
-//  * k_rowproj — the decoder row kernel (any row count; decode steps, prompt prefills, DTW
+//  * k_skinny — the decoder row kernel (any row count; decode steps, prompt prefills, DTW
 //              re-forwards, language detection) and every other projection of <= 64 rows:
-//              16-row MFMA tiles, K split over 4 waves (and over workgroups into slabs) in a
-//              fixed order, so a row's result does not depend on the launch's other rows.
-//              Roofline: HBM (N*K*2 per launch).
+//              16-row MFMA tiles, K split over 8 or 16 waves in a fixed order (optionally a
+//              fused LayerNorm prologue), so a row's result does not depend on the launch's
+//              other rows.  Roofline: HBM (N*K*2 per launch).
 #include "../common.h"
 #include "../prof.h"
 
@@ -956,73 +956,122 @@ void launch_quant_rows(const f16* x, int ldx, int M, int K, uint8_t* y, int ldy,
   WDR_HIP(hipGetLastError());
 }
 
-// ---------------------------------------------------------------- decoder row projection (lean)
-// k_rowproj: every decoder pass's projections (decode steps of all chains, prompt prefills, DTW
-// re-forwards, language detection; csrc/rows.h).  A workgroup is 4 waves (one per SIMD) on a
-// 16*MT-row x 16*NT-column output tile and one K slice (ksplit > 1: slice blockIdx.x % ksplit of
-// K / ksplit; its f32 partial goes to a slab that k_resid_ln sums in slice order); wave w takes
-// the slice's 32-wide k-steps w, w + 4, ... in order, U of them per batch of loads (weights with
-// the non-temporal policy: every byte is read once), v_mfma_f32_16x16x32_f16, and the four
-// waves' sums are added in wave order.  None of that depends on M or on which rows share the
-// launch, so a row's result is the same in any batch.  Under 64 VGPRs and 8 KB of LDS: a
-// workgroup fits on a CU beside an encoder GEMM tile (k_gemm4: 2 x 224 of a SIMD's 512 VGPRs,
-// 128 of its 160 KB of LDS), so the decode chain is not confined to CUs the encoder leaves idle.
-template <int EPI, int MT, int NT, int U, int KS>
-__global__ __launch_bounds__(256) void k_rowproj(ProjArgs a) {
+// ---------------------------------------------------------------- skinny MFMA GEMM (8 < M <= 64)
+// Prompt prefill / DTW re-forward rows.  A workgroup owns 16*NT output columns for ALL rows;
+// its 4 waves split K (interleaved 32-wide steps), stream the weight fragments straight from
+// HBM into v_mfma_f32_16x16x32_f16 (B operand = 16 contiguous bytes of one weight row per
+// lane) and reduce through LDS.  N/16 workgroups instead of N/128 keep every CU streaming.
+// LN: the A rows are LayerNorm(ln_x rows) -- each workgroup normalises its 16*MT rows into LDS
+// first (k_layernorm's arithmetic, so the f16 operands are bit-identical to the unfused path;
+// row stride K + 8 halfs keeps the 16-row fragment reads conflict-free) -- which removes the
+// separate LayerNorm launch and its f16 round trip from the prefill / DTW passes.
+template <int EPI, int MT, int NT, int W = 4, bool LN = false, int UU = 0>
+__global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
   ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
-  __shared__ float red[4][MT][NT][4][64];
+  __shared__ float red[W][MT][NT][4][64];
+  extern __shared__ __attribute__((aligned(16))) f16 xln[];   // LN: [16*MT][K + 8]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  // KS K slices, each into its slab (large-v3's 5 and 8 are template values: the kernel name
-  // tells the launch's shape); KS 0: a.ksplit slices, from the arguments
-  constexpr bool SLAB = KS != 1;
-  const int S = KS > 1 ? KS : (KS == 0 ? a.ksplit : 1);
-  const int ct = blockIdx.x / S, ks = blockIdx.x - ct * S;
-  const int n0 = ct * 16 * NT, m0 = blockIdx.y * 16 * MT;
+  const int n0 = blockIdx.x * 16 * NT;
+  const int m0 = blockIdx.y * 16 * MT;   // row tiles split over gridDim.y workgroups (narrow N)
   const int fr = lane & 15, fk = 8 * (lane >> 4);
-  const int steps = a.K / (32 * S);   // k-steps of the slice
-  const int kb = ks * steps * 32;
   f32x4 acc[MT][NT];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int lds_ld = a.K + 8;
+  if constexpr (LN) {
+    const int d = a.K;
+    // rows past M are never stored (an MFMA output row depends on its own A row only): only
+    // the live rows are normalised, the rest of the tile stays whatever LDS holds
+    const int live = min(16 * MT, a.M - m0);
+    for (int rr = wid; rr < live; rr += W) {
+      int row = m0 + rr;
+      if (a.row_map) row = a.row_map[row];
+      const float* xr = a.ln_x + (long long)row * a.ldln;
+      float v[5][4];
+      float sm = 0.f;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const int c = lane * 4 + j * 256;
+        const bool ok = c < d;
+        const int cc = ok ? c : 0;
+        const float4 q = *(const float4*)(xr + cc);
+        v[j][0] = ok ? q.x : 0.f; v[j][1] = ok ? q.y : 0.f; v[j][2] = ok ? q.z : 0.f; v[j][3] = ok ? q.w : 0.f;
+        sm += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+      }
+      sm = wave_sum(sm);
+      const float mean = sm / d;
+      float s2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+        if (lane * 4 + j * 256 < d)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float t = v[j][e] - mean;
+            s2 += t * t;
+          }
+      s2 = wave_sum(s2);
+      const float scale = 1.0f / sqrtf(s2 / d + 1e-5f);
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const int c = lane * 4 + j * 256;
+        if (c >= d) continue;
+        const float4 g4 = *(const float4*)(a.ln_g + c);
+        const float4 b4 = *(const float4*)(a.ln_b + c);
+        const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, bb[4] = {b4.x, b4.y, b4.z, b4.w};
+        f16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (f16)((v[j][e] - mean) * scale * gg[e] + bb[e]);
+        *(f16x4*)(xln + rr * lds_ld + c) = o;
+      }
+    }
+    __syncthreads();
+  }
   const f16* arow[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
     int m = m0 + i * 16 + fr;
     m = m < a.M ? m : a.M - 1;
-    if (a.row_map) m = a.row_map[m];
-    arow[i] = a.A + (size_t)m * a.lda + kb + fk;
+    if (!LN && a.row_map) m = a.row_map[m];
+    arow[i] = LN ? xln + (i * 16 + fr) * lds_ld + fk : a.A + (size_t)m * a.lda + fk;
   }
   const f16* brow[NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     int n = n0 + j * 16 + fr;
     n = n < a.N ? n : a.N - 1;
-    brow[j] = a.B + (size_t)n * a.ldb + kb + fk;
+    brow[j] = a.B + (size_t)n * a.ldb + fk;
   }
-  for (int t0 = wid; t0 < steps; t0 += 4 * U) {
+  // U k-steps per batch: all of a batch's fragment loads are issued before its MFMAs, so each
+  // wave keeps U*(NT+MT) 16-B loads in flight instead of one dependent round trip per step
+  // (UU: a fixed batch, e.g. all of a wave's k-steps in one batch; the k order is the same)
+  constexpr int U = UU > 0 ? UU : (MT + NT) <= 3 ? 8 : 4;
+  for (int k0 = wid * 32; k0 < a.K; k0 += 32 * W * U) {
     f16x8 bf[U][NT], af[U][MT];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int t = t0 + 4 * u;
-      const int k = (t < steps ? t : 0) * 32;
+      const int k = k0 + u * 32 * W;
+      const bool ok = k < a.K;
+      const int kk = ok ? k : 0;
 #pragma unroll
-      for (int j = 0; j < NT; ++j) bf[u][j] = __builtin_nontemporal_load((const f16x8*)(brow[j] + k));
+      for (int j = 0; j < NT; ++j) {
+        const f16x8 t = *(const f16x8*)(brow[j] + kk);
+        bf[u][j] = ok ? t : (f16x8){};
+      }
 #pragma unroll
-      for (int i = 0; i < MT; ++i) af[u][i] = *(const f16x8*)(arow[i] + k);
+      for (int i = 0; i < MT; ++i) {
+        const f16x8 t = *(const f16x8*)(arow[i] + kk);
+        af[u][i] = ok ? t : (f16x8){};
+      }
     }
-    // every load of the batch is issued before the first MFMA waits on one
-    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (t0 + 4 * u >= steps) break;
+    for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[u][i], bf[u][j], acc[i][j], 0, 0, 0);
-    }
   }
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -1031,17 +1080,17 @@ __global__ __launch_bounds__(256) void k_rowproj(ProjArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[wid][i][j][r][lane] = acc[i][j][r];
   __syncthreads();
-  for (int e = threadIdx.x; e < MT * NT * 256; e += 256) {
+  for (int e = threadIdx.x; e < MT * NT * 4 * 64; e += W * 64) {
     const int l = e & 63, r = (e >> 6) & 3, j = (e >> 8) % NT, i = (e >> 8) / NT;
-    const float v = ((red[0][i][j][r][l] + red[1][i][j][r][l]) + red[2][i][j][r][l]) + red[3][i][j][r][l];
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < W; ++w) v += red[w][i][j][r][l];
     const int row = m0 + i * 16 + (l >> 4) * 4 + r, col = n0 + j * 16 + (l & 15);
-    if constexpr (SLAB) {
-      if (row < a.M && col < a.N) a.slab[((size_t)ks * a.M + row) * a.N + col] = v;
-    } else {
-      epi_store<EPI>(a, row, col, v);
-    }
+    epi_store<EPI>(a, row, col, v);
   }
 }
+
+
 
 // A/B knobs of the encoder GEMM dispatch, read once per process (gemm_knobs_reload: tools/gemm_bench
 // A/B runs set them per variant): WDR_GEMM1=1 every M > 64 projection on k_gemm; WDR_GEMM3=0 the
@@ -1136,47 +1185,57 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
   }
 }
 
-// Decoder rows of any count on k_rowproj: the tile shape (MT, NT) and the load batch U follow
-// the row count and N, the k order and the wave order of the reduce do not, so every row's
-// result is the same whatever the launch holds -- a prompt prefill of n rows equals n one-row
-// steps, bit for bit.  ksplit > 1 (with a slab): the K slices' partials for k_resid_ln.
-template <int EPI, int MT, int NT, int U>
-static void launch_rowproj(const ProjArgs& a, hipStream_t s, double bytes, double flops) {
-  const int S = a.ksplit > 1 ? a.ksplit : 1;
-  dim3 grid(cdiv(a.N, 16 * NT) * S, cdiv(a.M, 16 * MT)), blk(256);
-  switch (S) {
-    case 1: wdr_launch(PROF_GEMV, bytes, flops, k_rowproj<EPI, MT, NT, U, 1>, grid, blk, 0, s, a); break;
-    case 5: wdr_launch(PROF_GEMV, bytes, flops, k_rowproj<EPI_F32, MT, NT, U, 5>, grid, blk, 0, s, a); break;
-    case 8: wdr_launch(PROF_GEMV, bytes, flops, k_rowproj<EPI_F32, MT, NT, U, 8>, grid, blk, 0, s, a); break;
-    default: wdr_launch(PROF_GEMV, bytes, flops, k_rowproj<EPI_F32, MT, NT, U, 0>, grid, blk, 0, s, a); break;
-  }
-}
-
+// Decoder rows of any count on the row kernel (k_skinny, 8 or 16 waves splitting K): the k
+// order of a wave (k = 32 wid + 32 W t, t = 0, 1, ...) and the wave order of the reduce depend
+// only on the projection's shape (N, K), never on the tile shape (MT) or the row count, so every
+// row's result is the same whatever the launch holds -- a prompt prefill of n rows equals n
+// one-row steps, bit for bit.  (Round 4 tried a 4-wave, <= 64-VGPR variant with split-K slabs
+// for the residual projections, to share CUs with the encoder GEMM tiles: slower alone --
+// tools/rows_bench, o 15.0 vs 5.1 us, fc2 21.1 vs 13.7 us at 16 rows -- and 5 % slower in the
+// 1-h pipeline, profiles/r04/ab_epi4.txt.)
 template <int EPI>
 static void launch_rows_epi(const ProjArgs& a, hipStream_t s) {
-  const int ob = (EPI == EPI_F32_RESID || EPI == EPI_F32 || EPI == EPI_F32_GELU_POS) ? 4 : 2;
   // algorithmic bytes of the rows class (bench.py's live roofline and its trace counterpart,
   // bench.py rows_weight_bytes): the weights, streamed once per launch -- the activation rows and
   // outputs (<= 4 % of it at the batches' 10-60 rows) are L2 traffic
-  (void)ob;
   const double bytes = (double)a.N * a.K * 2;
   const double flops = 2.0 * a.M * a.N * a.K;
-  const bool wide = a.N >= 16384;   // the logits: 32 columns per workgroup
-  // U: the largest batch that keeps the workgroup under 64 VGPRs (AGPR accumulators included)
-  if (a.M <= 16) {
-    if (wide) launch_rowproj<EPI, 1, 2, 2>(a, s, bytes, flops);
-    else launch_rowproj<EPI, 1, 1, 5>(a, s, bytes, flops);
-  } else {
-    if (wide) launch_rowproj<EPI, 2, 2, 1>(a, s, bytes, flops);
-    else launch_rowproj<EPI, 2, 1, 2>(a, s, bytes, flops);
+  const int mt = cdiv(a.M, 16);
+  const bool ln = a.ln_x != nullptr;
+  const bool wide = a.N >= 4096;
+  const int prof = PROF_GEMV;   // the "rows" class of bench.py's live roofline (any row count)
+  if (!wide) {
+    // one 16-row tile per workgroup: the row tiles of a column tile re-read its weights from L2.
+    // K > 2048 (fc2): 16 waves, each wave's 10 k-steps as ONE batch of loads (8 waves took three
+    // dependent batches: fc2 at 1 row 9.8 us against 5.4 us)
+    if (a.K > 2048) {
+      WDR_CHECK(!ln, "row projection: LN prologue needs K <= 1280");
+      wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 16, false, 12>, dim3(cdiv(a.N, 16), mt), dim3(1024), 0, s, a);
+      return;
+    }
+    dim3 grid(cdiv(a.N, 16), mt), blk(512);
+    if (ln) wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 8, true>, grid, blk, (uint32_t)16 * (a.K + 8) * 2, s, a);
+    else wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 8>, grid, blk, 0, s, a);
+    return;
   }
+  // wide N (fc1, logits): 32 columns per workgroup, up to 4 row tiles per workgroup
+  const int mtw = std::min(mt, ln ? 2 : 4);
+  dim3 grid(cdiv(a.N, 32), cdiv(mt, mtw)), blk(512);
+  const uint32_t lds = ln ? (uint32_t)16 * mtw * (a.K + 8) * 2 : 0;
+#define WDR_RW(MTV)                                                                                        \
+  if (ln) wdr_launch(prof, bytes, flops, k_skinny<EPI, MTV, 2, 8, true>, grid, blk, lds, s, a);            \
+  else wdr_launch(prof, bytes, flops, k_skinny<EPI, MTV, 2, 8>, grid, blk, 0, s, a);
+  if (mtw == 1) { WDR_RW(1) }
+  else if (mtw == 2) { WDR_RW(2) }
+  else if (mtw == 3) { WDR_RW(3) }
+  else { WDR_RW(4) }
+#undef WDR_RW
 }
 
 static void launch_rows(const ProjArgs& a, hipStream_t s) {
-  const int S = a.ksplit > 1 ? a.ksplit : 1;
-  WDR_CHECK(a.K % (32 * S) == 0 && a.lda % 8 == 0 && a.ldb % 8 == 0, "row projection: K % (32 ksplit), lda / ldb % 8");
-  WDR_CHECK(S == 1 || a.slab, "row projection: a split needs a slab");
-  WDR_CHECK(S > 1 || a.out, "row projection: no output");
+  WDR_CHECK(a.K % 32 == 0 && a.lda % 8 == 0 && a.ldb % 8 == 0, "row projection: K % 32, lda / ldb % 8");
+  // LN prologue: every workgroup normalises only its own <= 32 rows (any M)
+  WDR_CHECK(!a.ln_x || (a.K <= 1280 && a.K % 4 == 0), "row projection LN prologue: K <= 1280");
   WDR_CHECK(a.epi != EPI_QKV_CACHE || (a.kc && a.vc && a.row_seq && a.row_pos && a.d > 0), "qkv-cache epilogue args");
   switch (a.epi) {
     case EPI_F16: launch_rows_epi<EPI_F16>(a, s); break;

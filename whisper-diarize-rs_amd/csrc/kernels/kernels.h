@@ -32,14 +32,6 @@ void launch_energy(const float* x, int n, float* e, hipStream_t s);
 void launch_i16_to_f32(const int16_t* in, int n, float* out, hipStream_t s);
 void launch_synth_fill(void* dst, long long rows, int src_cols, int dst_cols, uint64_t seed, float scale, bool f16out,
                        int mode, float cval, hipStream_t s);
-// decoder rows: x[r] += sum of the S split-K slices slab[s][r] (in order) + bias, then (g set)
-// h[r] = f16(LayerNorm(x[r]) * g + b); S = 0: the LayerNorm only (elem.hip)
-struct ResidLnArgs {
-  const float* slab = nullptr; int S = 0; int R = 0; const float* bias = nullptr;
-  float* x = nullptr; int d = 0;
-  const float* g = nullptr; const float* b = nullptr; f16* h = nullptr;
-};
-void launch_resid_ln(const ResidLnArgs& a, hipStream_t s);
 void launch_layernorm(const float* x, int ldx, const float* g, const float* b, f16* y, int ldy, int rows, int d,
                       hipStream_t s);
 void launch_embed(const f16* E, const float* P, const int* tok, const int* pos, int R, int d, float* x, hipStream_t s);
@@ -178,7 +170,8 @@ struct CaptureRowsArgs {
   float scale;
 };
 void launch_aheads_capture_rows(const CaptureRowsArgs& a, int n_sel, hipStream_t s);
-
+void launch_layernorm_rows(const float* x, int ldx, const float* g, const float* b, f16* y, int ldy, int rows, int d,
+                           const int* row_map, hipStream_t s);
 
 // Silero VAD (kernels/vad.hip); layouts [out][in*k] f16, biases f32
 struct VadWeights {

@@ -14,19 +14,6 @@ namespace wdr {
 namespace {
 constexpr int kTileRows = 128;   // rows of one MFMA cross-attention tile (4 waves x 32)
 constexpr int kNoEnd = 1 << 30;
-}  // namespace
-
-// the K slices of a residual projection (k_rowproj into slabs, summed by k_resid_ln): slices of
-// 8 k-steps (2 per wave) up to K = 2048 -- large-v3's o / xo (K = d = 1280) in 5 -- and of 20
-// (5 per wave) above -- its fc2 (K = 4d = 5120) in 8: 400 / 640 workgroups on the 80 column
-// tiles of N = 1280 instead of 80
-int rows_ksplit(int K) {
-  if (K % 256 != 0) return 1;
-  if (K <= 2048) return K / 256;
-  return K % 640 == 0 ? K / 640 : K / 256;
-}
-
-namespace {
 size_t up16(size_t x) { return (x + 15) & ~size_t(15); }
 }  // namespace
 
@@ -145,7 +132,6 @@ void RowsBufs::alloc(int r, int lr, int d, int H, int V) {
   qx = DevMem((size_t)r * d * 2);
   mlpd = DevMem((size_t)r * 4 * d * 2);
   part_o = DevMem((size_t)24 * r * H * 64 * 4);   // 24 key chunks (1500 / 64, rounded up)
-  slab = DevMem((size_t)std::max(rows_ksplit(d), rows_ksplit(4 * d)) * r * d * 4);   // residual K slices
   part_ml = DevMem((size_t)24 * r * H * sizeof(float2));
   ml = DevMem((size_t)r * H * sizeof(float2));
   logits = DevMem((size_t)std::max(1, lr) * V * 4);
@@ -160,7 +146,6 @@ RowsIO RowsBufs::io(const Context& ctx, int V) const {
   o.qx = qx.as<f16>();
   o.mlpd = mlpd.as<f16>();
   o.part_o = part_o.as<float>();
-  o.slab = slab.as<float>();
   o.part_ml = part_ml.as<float2>();
   o.ml = ml.as<float2>();
   o.logits = logits.as<float>();
@@ -177,55 +162,41 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, in
   const HParams& hp = md.hp;
   const int d = hp.n_text_state, L = hp.n_text_layer, H = hp.n_text_head;
   const float scale = 1.0f / 8.0f;
-  WDR_CHECK(R >= 1 && io.tok && io.xkv && io.slab, "rows forward: no rows / tables");
-  WDR_CHECK(d <= 1280 && d % 4 == 0, "rows forward: d");
-  // a projection of the rows: A [R][lda] f16; split > 1: the K slices' partials into io.slab
-  // (bias and residual in the following k_resid_ln)
+  WDR_CHECK(R >= 1 && io.tok && io.xkv, "rows forward: no rows / tables");
+  // the projection's input rows LayerNorm(x): inside the row kernel up to 32 rows (every
+  // workgroup normalises its own row tiles), above that one k_layernorm launch into io.hd -- the
+  // same arithmetic either way.  Fused at every row count the redundant per-column-tile LN cost
+  // more than the launch it saves (1-h trace: decoder rows class 4.98 vs 4.83 s over two runs).
+  // (Writing LN(x) from the residual launch's last workgroup per row tile -- an in-launch
+  // hand-off -- measured slower still: 529 vs 557 xRT, profiles/r03/ab_lno_xfc.txt; a separate
+  // residual + LayerNorm launch after split-K residual projections: profiles/r04/ab_epi4.txt.)
+  const bool fuse_ln = R <= 32;
   auto P = [&](const f16* A, int lda, const f16* W, const float* b, void* out, int ldo, int N, int K, int epi,
-               int split = 1) {
-    ProjArgs a{A, lda, W, K, split > 1 ? nullptr : b, out, ldo, nullptr, 0, R, N, K, epi};
+               const float* lng = nullptr, const float* lnb = nullptr) {
+    ProjArgs a{A, lda, W, K, b, out, ldo, nullptr, 0, R, N, K, epi};
     a.rows_mma = 1;
-    a.ksplit = split;
-    a.slab = split > 1 ? io.slab : nullptr;
+    if (lng) {
+      if (fuse_ln) {
+        a.ln_x = io.xd;
+        a.ldln = d;
+        a.ln_g = lng;
+        a.ln_b = lnb;
+      } else {
+        launch_layernorm(io.xd, d, lng, lnb, io.hd, d, R, d, s);
+        a.A = io.hd;
+        a.lda = d;
+      }
+    }
     return a;
   };
-  // x[r] += slices + bias, then h = LayerNorm(x) with (g, b) (g null: no LayerNorm)
-  auto RL = [&](int split, const float* bias, const float* g, const float* b) {
-    ResidLnArgs r;
-    r.slab = io.slab;
-    r.S = split;
-    r.R = R;
-    r.bias = bias;
-    r.x = io.xd;
-    r.d = d;
-    r.g = g;
-    r.b = b;
-    r.h = io.hd;
-    launch_resid_ln(r, s);
-  };
-  // a residual projection (o, xo, fc2) and the LayerNorm after it: split into K slices (slabs,
-  // summed with the bias by k_resid_ln), or -- a K too small to split -- one launch adding to x
-  // with the bias in its epilogue, then the LayerNorm alone
-  auto RP = [&](const f16* A, int lda, const f16* W, const float* bias, int K, int split, const float* g,
-                const float* b) {
-    if (split > 1) {
-      launch_proj(P(A, lda, W, bias, nullptr, d, d, K, EPI_F32, split), s);
-      RL(split, bias, g, b);
-    } else {
-      launch_proj(P(A, lda, W, bias, io.xd, d, d, K, EPI_F32_RESID), s);
-      RL(0, nullptr, g, b);
-    }
-  };
-  const int sd = rows_ksplit(d), sf = rows_ksplit(4 * d);
   launch_embed(md.tok_emb, md.dec_pos, io.tok, io.pos, R, d, io.xd, s);
-  RL(0, nullptr, md.dec[0].ln1_g, md.dec[0].ln1_b);
   const bool any_cap = io.n_cap > 0 && ctx.aheads_per_layer.size() == (size_t)L;
   int cap_slot0 = 0;
   for (int l = 0; l < L; ++l) {
     const DecLayer& e = md.dec[l];
     f16* kc = io.kc + (size_t)l * io.layer_stride;
     f16* vc = io.vc + (size_t)l * io.layer_stride;
-    ProjArgs q = P(io.hd, d, e.w_qkv, e.b_qkv, io.qkvd, 3 * d, 3 * d, d, EPI_QKV_CACHE);
+    ProjArgs q = P(nullptr, d, e.w_qkv, e.b_qkv, io.qkvd, 3 * d, 3 * d, d, EPI_QKV_CACHE, e.ln1_g, e.ln1_b);
     q.kc = kc;
     q.vc = vc;
     q.seq_stride = io.seq_stride;
@@ -237,8 +208,8 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, in
     // predecessors' keys: causal by position)
     DecSelfArgs sa{io.qkvd, 3 * d, kc, vc, io.seq_stride, d, io.seq, io.pos, io.attd, d, scale};
     launch_dec_self_attn(sa, R, H, s);
-    RP(io.attd, d, e.w_o, e.b_o, d, sd, e.ln2_g, e.ln2_b);
-    launch_proj(P(io.hd, d, e.w_xq, e.b_xq, io.qx, d, d, d, EPI_F16), s);
+    launch_proj(P(io.attd, d, e.w_o, e.b_o, io.xd, d, d, d, EPI_F32_RESID), s);
+    launch_proj(P(nullptr, d, e.w_xq, e.b_xq, io.qx, d, d, d, EPI_F16, e.ln2_g, e.ln2_b), s);
     XAttnArgs xa{io.qx, d, nullptr, nullptr, 64, XKV_T, R, H, scale, io.part_o, io.part_ml, io.attd, d};
     xa.row_k = io.xkv;
     xa.layer_off = xkv_k_off(l, H);
@@ -264,18 +235,24 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, in
     }
     if (ctx.aheads_per_layer.size() == (size_t)L) cap_slot0 += (int)ctx.aheads_per_layer[l].size();
     if (l + 1 >= l_stop) return;   // a DTW pass: nothing after this layer's capture matters
-    RP(io.attd, d, e.w_xo, e.b_xo, d, sd, e.ln3_g, e.ln3_b);
-    launch_proj(P(io.hd, d, e.w_fc1, e.b_fc1, io.mlpd, 4 * d, 4 * d, d, EPI_F16_GELU), s);
-    // then the next layer's LayerNorm 1, or after the last layer the decoder's final LayerNorm
-    // (the logits rows' input)
-    if (l + 1 < L) RP(io.mlpd, 4 * d, e.w_fc2, e.b_fc2, 4 * d, sf, md.dec[l + 1].ln1_g, md.dec[l + 1].ln1_b);
-    else RP(io.mlpd, 4 * d, e.w_fc2, e.b_fc2, 4 * d, sf, io.n_logit > 0 ? md.ln_g : nullptr, md.ln_b);
+    launch_proj(P(io.attd, d, e.w_xo, e.b_xo, io.xd, d, d, d, EPI_F32_RESID), s);
+    launch_proj(P(nullptr, d, e.w_fc1, e.b_fc1, io.mlpd, 4 * d, 4 * d, d, EPI_F16_GELU, e.ln3_g, e.ln3_b), s);
+    launch_proj(P(io.mlpd, 4 * d, e.w_fc2, e.b_fc2, io.xd, d, d, 4 * d, EPI_F32_RESID), s);
   }
   if (io.n_logit > 0) {
-    // logits of the logit rows only, gathered by lrow from the final LayerNorm (compact output)
-    ProjArgs a{io.hd, d, md.tok_emb, d, nullptr, io.logits, io.ldlogits, nullptr, 0, io.n_logit, hp.n_vocab, d, EPI_F32};
+    // final LayerNorm + logits of the logit rows only, gathered by lrow (compact output)
+    ProjArgs a{nullptr, d, md.tok_emb, d, nullptr, io.logits, io.ldlogits, nullptr, 0, io.n_logit, hp.n_vocab, d, EPI_F32};
     a.rows_mma = 1;
-    a.row_map = io.lrow;
+    if (io.n_logit <= 32) {
+      a.ln_x = io.xd;
+      a.ldln = d;
+      a.ln_g = md.ln_g;
+      a.ln_b = md.ln_b;
+      a.row_map = io.lrow;
+    } else {
+      launch_layernorm_rows(io.xd, d, md.ln_g, md.ln_b, io.hd, d, io.n_logit, d, io.lrow, s);
+      a.A = io.hd;
+    }
     launch_proj(a, s);
   }
 }

@@ -6,12 +6,12 @@
 //
 // Arithmetic contract: a row's result depends only on its own inputs and its group's kind, never
 // on the other rows of the launch --
-//   * projections: the row kernel (launch_proj with rows_mma, k_rowproj's fixed k order; the
-//     residual projections split over K into slabs that k_resid_ln sums in slice order);
+//   * projections: the row kernel (launch_proj with rows_mma, k_skinny's fixed k order);
 //   * self-attention: one workgroup per (row, head) over that row's cache prefix;
 //   * cross-attention: groups of <= XATTN_GRP_MAX rows on the VALU split kernel (a row scored with
 //     the one-row arithmetic), larger groups on the MFMA tile kernel, both merged by one combine;
-//   * residual + LayerNorm of each row in k_resid_ln (one wave per row).
+//   * LayerNorm fused into the projection (each workgroup normalises its own row tiles; the
+//     k_layernorm alternative has the same arithmetic).
 // So batching decode steps with prompt prefills and DTW re-forwards of other chains changes no
 // result: decode chains stay bit-identical to one sequential chain.
 #pragma once
@@ -73,7 +73,6 @@ class RowBatch {
 struct RowsIO {
   float* xd; f16* hd; f16* qkvd; f16* attd; f16* qx; f16* mlpd;
   float* part_o; float2* part_ml; float2* ml;
-  float* slab;                                       // [kSplitFc2][rows][d] split-K partials
   float* logits; int ldlogits;                       // [n_logit][ldlogits]
   f16* kc; f16* vc; long long layer_stride, seq_stride;   // KV pool (layer 0) and its strides
   // tables (device; RowBatch::upload)
@@ -88,14 +87,11 @@ struct RowsIO {
 
 // working-set buffers of a rows forward for up to `rows` rows and `logit_rows` logit rows
 struct RowsBufs {
-  DevMem xd, hd, qkvd, attd, qx, mlpd, part_o, part_ml, ml, logits, slab;
+  DevMem xd, hd, qkvd, attd, qx, mlpd, part_o, part_ml, ml, logits;
   int rows = 0, logit_rows = 0;
   void alloc(int rows, int logit_rows, int d, int H, int V);
   RowsIO io(const Context& ctx, int V) const;   // tables unset
 };
-
-// the K slices of a residual row projection of depth K (k_rowproj into slabs, k_resid_ln)
-int rows_ksplit(int K);
 
 // embed + every layer + (LayerNorm + logits of the logit rows); capture of DTW rows.  l_stop:
 // return after the cross-attention (+ capture) of layer l_stop - 1 (no logits then)
