@@ -572,10 +572,12 @@ def main():
 
     # per class: algorithmic flops (MFMA classes) or bytes (HBM classes) per launch / the average
     # duration of its sampled launches, timed by the kernels' own clock (first wave start -> last
-    # wave end: rocprofv3's dispatch span; csrc/common.h ProfClock); the same launches' HIP
-    # start/stop events are reported beside it (under the pipeline's multi-stream concurrency
-    # they also absorb the launch's wait for the GPU).  `roofline` is the class with the largest
-    # share of kernel time (every class is sampled at the same rate, csrc/prof.cpp)
+    # wave end: rocprofv3's dispatch span; csrc/common.h ProfClock), each sample weighted by
+    # 1 / its sampling probability (csrc/prof.h: every launch of 1 in 32 decode-only steps, which
+    # replay a second capture of their graph carrying clock slots; 1 in 64 eager launches, the
+    # encode batches' and the prefill / DTW batches'), so `launches_est` estimates the class's
+    # launch count; the eager samples' HIP start/stop events are reported beside it (under the
+    # pipeline's multi-stream concurrency they also absorb the launch's wait for the GPU).
     classes = {}
     for c, (ms, nl, by, fl) in live.items():
         if ms <= 0:
@@ -590,29 +592,26 @@ def main():
             ach = by / (ms * 1e-3) / 1e9
             r = {"kernel": c, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                  "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_launch": by / nl}
-        r.update({"traffic": None, "sampled_launches": nl, "avg_launch_us": round(ms * 1e3 / nl, 3),
-                  "sampled_ms": round(ms, 3), "timing": "kernel clock (wall_clock64, first wave -> last wave)"})
+        r.update({"traffic": None, "launches_est": nl, "avg_launch_us": round(ms * 1e3 / nl, 3),
+                  "kernel_ms_est": round(ms, 3), "timing": "kernel clock (wall_clock64, first wave -> last wave)"})
         if c in live_ev:
             r["hip_event_avg_launch_us"] = round(live_ev[c][0] * 1e3 / live_ev[c][1], 3)
         tr, src = pmc_traffic(c)
         if tr is not None:
             r["traffic"] = round(tr)
             r["traffic_source"] = src
-        # csrc/prof.h: decode steps replay hipGraphs; 1 in 32 steps runs eagerly and 1 in 2 of
-        # its launches carries HIP start/stop events on the launching stream; launches outside
-        # steps are timed 1 in 64
-        r["sampling"] = "1 in %d launches (decode steps: 1 in %d eager, 1 in %d of those)" % (
-            PROF_EVERY * PROF_STEP_EVERY, PROF_STEP_EVERY, PROF_EVERY)
+        r["sampling"] = ("every launch of 1 in %d decode-only steps (profiled graph replay), 1 in %d "
+                         "eager launches; weighted by 1 / sampling probability") % (
+            PROF_STEP_EVERY, PROF_EVERY * PROF_STEP_EVERY)
         classes[c] = r
     # `roofline` = the class with the largest share of kernel time in the committed rocprofv3
     # trace of this benched configuration (profiles/rNN/prof_graph/classes.json; r03: encoder
     # GEMMs 30.7 %, decoder rows 27.3 %, cross-attention 11.2 %, encoder flash 8.7 %), the
-    # encoder GEMM class without one.  The live sampler's own shares are not used for the pick:
-    # its sampled decode steps run eagerly (csrc/prof.h).
+    # encoder GEMM class without one.
     trace = trace_roofline(args.model, args.fp8)
     shares = {k: v.get("share", 0.0) for k, v in (trace or {}).items() if isinstance(v, dict) and k in classes}
     pick = max(shares, key=shares.get) if shares else "gemm"
-    roof = classes.get(pick) or (max(classes.values(), key=lambda r: r["sampled_ms"]) if classes else None)
+    roof = classes.get(pick) or (max(classes.values(), key=lambda r: r["kernel_ms_est"]) if classes else None)
     if roof is not None:
         roof = dict(roof, dominant_by="rocprofv3 kernel-time share of the benched configuration (%s)"
                     % ((trace or {}).get("source", "no committed trace")))

@@ -7,7 +7,7 @@ mkdir -p gpurun_out/ab
 i=0
 for v in "$@"; do
   i=$((i + 1))
-  env $v timeout -k 10 240 python3 bench.py --no-cpu-baseline --prof none > gpurun_out/ab/run$i.json 2> gpurun_out/ab/run$i.err
+  env $v timeout -k 10 240 python3 bench.py --no-cpu-baseline --prof none --beam-seconds 0 > gpurun_out/ab/run$i.json 2> gpurun_out/ab/run$i.err
   python3 - "$v" gpurun_out/ab/run$i.json <<'PY'
 import json, sys
 d = json.load(open(sys.argv[2]))

@@ -20,7 +20,7 @@ HB=$!
 trap "kill $HB 2>/dev/null" EXIT
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 900 rocprofv3 --pmc $c --output-format csv -d $O/$c -o run -- \
-    python3 bench.py --seconds $SECS --warmup 0 --steps 1 --prof none --no-cpu-baseline > $O/bench_$c.json 2> $O/$c.err
+    python3 bench.py --seconds $SECS --warmup 0 --steps 1 --prof none --no-cpu-baseline --beam-seconds 0 > $O/bench_$c.json 2> $O/$c.err
 done
 python3 tools/prof_summary.py $O/FETCH_SIZE --fetch $O/FETCH_SIZE --write $O/WRITE_SIZE --json $O/pmc.json > $O/pmc_summary.txt
 find $O -name "*counter_collection.csv" -delete

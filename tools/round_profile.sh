@@ -19,7 +19,7 @@ mkdir -p gpurun_out
 O=gpurun_out/prof_$TAG
 rm -rf $O && mkdir -p $O
 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- \
-  python3 bench.py --seconds $SECS --warmup 1 --steps 1 --no-cpu-baseline --prof none > $O/bench_trace.json 2> $O/trace.err
+  python3 bench.py --seconds $SECS --warmup 1 --steps 1 --no-cpu-baseline --prof none --beam-seconds 0 > $O/bench_trace.json 2> $O/trace.err
 python3 tools/kstat_groups.py $(find $O/trace -name "*kernel_stats.csv" | head -1) > $O/stages.txt
 python3 tools/busy.py $(find $O/trace -name "*kernel_trace.csv" | head -1) 0.1 >> $O/stages.txt
 python3 tools/prof_summary.py $O/trace --json $O/classes.json --drop-trace > $O/summary.txt

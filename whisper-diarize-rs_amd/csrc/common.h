@@ -147,6 +147,10 @@ unsigned long long* prof_slot();   // next clock slot of the sampled-launch ring
 template <typename A>
 inline unsigned long long* prof_attach(A&) { return nullptr; }
 inline unsigned long long* prof_attach(ProjArgs& a) { return a.ts = prof_slot(); }
+// argument structs with a clock slot take one (profiled graph captures, prof.h); others cannot
+template <typename A>
+inline bool prof_set_ts(A&, unsigned long long*) { return false; }
+inline bool prof_set_ts(ProjArgs& a, unsigned long long* t) { a.ts = t; return true; }
 // M <= 64 (or rows_mma) on the row kernel k_skinny, larger M on the MFMA GEMM tiles
 void launch_proj(const ProjArgs& a, hipStream_t s);
 // re-read the encoder GEMM dispatch knobs (WDR_GEMM*), which launch_proj reads once per process:

@@ -21,9 +21,10 @@ struct Rec {
   int cls;
 };
 struct ClkRec {
-  long long slot;   // kernel-clock slot in the ring
+  long long slot;   // kernel-clock slot in the ring (or in a profiled graph's arena)
   int cls;
   double bytes, flops;
+  double w;         // 1 / the launch's sampling probability
 };
 std::vector<ClkRec> g_clk_pending;
 constexpr int kClasses = 8;
@@ -37,7 +38,8 @@ std::vector<hipEvent_t> g_pool;
 struct Acc {
   double ms = 0, bytes = 0, flops = 0;
   long long n = 0;
-  double clk_ms = 0, clk_bytes = 0, clk_flops = 0;   // launches whose kernel clock span was read
+  // launches whose kernel clock span was read, each weighted by 1 / its sampling probability
+  double clk_ms = 0, clk_bytes = 0, clk_flops = 0, clk_w = 0;
   long long clk_n = 0;
 } g_acc[kClasses];
 
@@ -76,6 +78,25 @@ void ring_reset_locked() {
   g_next = 0;
 }
 
+// the clock spans of recs (slots of `words`): earliest wave start -> latest wave end, weighted
+void fold_clocks(const std::vector<ClkRec>& recs, const unsigned long long* words, size_t n_words) {
+  for (const auto& r : recs) {
+    if ((size_t)((r.slot + 1) * kSlotWords) > n_words) continue;
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (int j = 0; j < PROF_CLK_LANES; ++j) {
+      t0 = std::min(t0, words[r.slot * kSlotWords + j]);
+      t1 = std::max(t1, words[r.slot * kSlotWords + PROF_CLK_LANES + j]);
+    }
+    if (t0 == ~0ull || t1 < t0) continue;
+    Acc& A = g_acc[r.cls];
+    A.clk_ms += r.w * (double)(t1 - t0) * g_tick_ms;
+    A.clk_w += r.w;
+    A.clk_n++;
+    A.clk_bytes += r.w * r.bytes;
+    A.clk_flops += r.w * r.flops;
+  }
+}
+
 // events: waited for and folded in (batches during the run); kernel clocks (read_ring): read
 // back once, after a device synchronisation, at read time
 void drain_locked(bool read_ring = true) {
@@ -102,20 +123,7 @@ void drain_locked(bool read_ring = true) {
     g_broken = true;
     return;
   }
-  for (auto& r : g_clk_pending) {
-    if ((size_t)((r.slot + 1) * kSlotWords) > ring.size()) continue;
-    unsigned long long t0 = ~0ull, t1 = 0;
-    for (int j = 0; j < PROF_CLK_LANES; ++j) {
-      t0 = std::min(t0, ring[r.slot * kSlotWords + j]);
-      t1 = std::max(t1, ring[r.slot * kSlotWords + PROF_CLK_LANES + j]);
-    }
-    if (t0 == ~0ull || t1 < t0) continue;
-    Acc& A = g_acc[r.cls];
-    A.clk_ms += (double)(t1 - t0) * g_tick_ms;
-    A.clk_n++;
-    A.clk_bytes += r.bytes;
-    A.clk_flops += r.flops;
-  }
+  fold_clocks(g_clk_pending, ring.data(), ring.size());
   g_clk_pending.clear();
 }
 }  // namespace
@@ -232,11 +240,72 @@ void prof_shutdown() {
 void prof_push(int cls, hipEvent_t a, hipEvent_t b, unsigned long long* ts, double bytes, double flops) {
   std::lock_guard<std::mutex> l(g_mu);
   g_pending.push_back({a, b, cls});
-  if (ts && g_ring) g_clk_pending.push_back({(long long)((ts - g_ring) / kSlotWords), cls, bytes, flops});
+  if (ts && g_ring)
+    g_clk_pending.push_back({(long long)((ts - g_ring) / kSlotWords), cls, bytes, flops, (double)(kEvery * kStepEvery)});
   g_acc[cls].bytes += bytes;
   g_acc[cls].flops += flops;
   g_acc[cls].n++;
   if (g_pending.size() > 4096) drain_locked(false);
+}
+
+// ---------------------------------------------------------------- profiled graph replays
+struct ProfGraph {
+  static constexpr int kSlots = 1024;   // clocked launches per graph (a large-v3 step: ~260)
+  unsigned long long* arena = nullptr;  // [kSlots][kSlotWords], the ring's slot layout
+  unsigned long long* init = nullptr;   // the same size: start words ~0, end words 0
+  int dev = -1;
+  std::vector<ClkRec> recs;             // slot = position
+  std::vector<unsigned long long> host;
+};
+thread_local ProfGraph* t_graph = nullptr;
+
+ProfGraph* prof_graph_new() {
+  auto* g = new ProfGraph;
+  const size_t n = (size_t)ProfGraph::kSlots * kSlotWords;
+  std::vector<unsigned long long> init(n);
+  for (int i = 0; i < ProfGraph::kSlots; ++i)
+    for (int j = 0; j < PROF_CLK_LANES; ++j) {
+      init[(size_t)i * kSlotWords + j] = ~0ull;
+      init[(size_t)i * kSlotWords + PROF_CLK_LANES + j] = 0ull;
+    }
+  WDR_HIP(hipGetDevice(&g->dev));
+  WDR_HIP(hipMalloc(&g->arena, n * 8));
+  WDR_HIP(hipMalloc(&g->init, n * 8));
+  WDR_HIP(hipMemcpy(g->init, init.data(), n * 8, hipMemcpyHostToDevice));
+  return g;
+}
+void prof_graph_capture(ProfGraph* g) { t_graph = g; }
+bool prof_graph_on(int cls) {
+  return t_graph && (g_mask.load(std::memory_order_relaxed) & (1 << cls)) && (int)t_graph->recs.size() < ProfGraph::kSlots;
+}
+unsigned long long* prof_graph_slot(int cls, double bytes, double flops) {
+  ProfGraph* g = t_graph;
+  if (!g || (int)g->recs.size() >= ProfGraph::kSlots) return nullptr;
+  const long long i = (long long)g->recs.size();
+  g->recs.push_back({i, cls, bytes, flops, (double)kStepEvery});
+  return g->arena + (size_t)i * kSlotWords;
+}
+void prof_graph_reset(ProfGraph* g, hipStream_t s) {
+  if (g && !g->recs.empty())
+    WDR_HIP(wdr_memcpy_async(g->arena, g->init, g->recs.size() * kSlotWords * 8, hipMemcpyDeviceToDevice, s));
+}
+void prof_graph_collect(ProfGraph* g) {
+  if (!g || g->recs.empty()) return;
+  g->host.resize(g->recs.size() * kSlotWords);
+  WDR_HIP(hipMemcpy(g->host.data(), g->arena, g->host.size() * 8, hipMemcpyDeviceToHost));
+  std::lock_guard<std::mutex> l(g_mu);
+  if (g_tick_ms <= 0.0) return;   // the ring (and the clock rate) were never set up
+  fold_clocks(g->recs, g->host.data(), g->host.size());
+}
+void prof_graph_free(ProfGraph* g) {
+  if (!g) return;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipSetDevice(g->dev);
+  (void)hipFree(g->arena);
+  (void)hipFree(g->init);
+  (void)hipSetDevice(dev);
+  delete g;
 }
 
 }  // namespace wdr
@@ -272,8 +341,10 @@ int wdr_prof_read_clock(int32_t cls, double* total_ms, int64_t* launches, double
   wdr::drain_locked();
   if (wdr::g_broken) return -2;
   if (cls <= 0 || cls >= wdr::kClasses) return -1;
+  // weighted sums: total_ms / launches = the class's mean launch span, algo_bytes / launches its
+  // mean bytes per launch (launches = the weight total, an estimate of the class's launch count)
   *total_ms = wdr::g_acc[cls].clk_ms;
-  *launches = wdr::g_acc[cls].clk_n;
+  *launches = (int64_t)(wdr::g_acc[cls].clk_w + 0.5);
   *algo_bytes = wdr::g_acc[cls].clk_bytes;
   *algo_flops = wdr::g_acc[cls].clk_flops;
   return 0;

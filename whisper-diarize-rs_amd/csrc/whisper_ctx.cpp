@@ -2745,6 +2745,17 @@ struct StepBatcher::Impl {
   struct G {
     hipGraphExec_t exec = nullptr;
     VocabIds vids{};
+    // the same step captured with clock slots on its launches (prof.h, profiled graph replays):
+    // replayed instead of exec by the sampled steps while the live profiler is on
+    hipGraphExec_t pexec = nullptr;
+    ProfGraph* pg = nullptr;
+    void drop() {
+      if (exec) (void)hipGraphExecDestroy(exec);
+      if (pexec) (void)hipGraphExecDestroy(pexec);
+      prof_graph_free(pg);
+      exec = pexec = nullptr;
+      pg = nullptr;
+    }
   };
   std::map<long long, G> graphs;  // decode-only batches, by (K, group kind, groups, rows)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;   // a launch's GPU span (WDR_BATCH_LOG)
@@ -2778,8 +2789,8 @@ StepBatcher::StepBatcher(Context& ctx) : ctx_(ctx), m_(new Impl) {
 
 StepBatcher::~StepBatcher() {
   if (!m_) return;
-  for (auto& g : m_->graphs)
-    if (g.second.exec) (void)hipGraphExecDestroy(g.second.exec);
+  if (m_->s) (void)hipStreamSynchronize(m_->s);
+  for (auto& g : m_->graphs) g.second.drop();
   if (m_->s) {
     (void)hipStreamSynchronize(m_->s);
     (void)hipStreamDestroy(m_->s);
@@ -2953,8 +2964,10 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
   const bool decode_only = n_pre == 0 && n_dtw == 0;
   static FILE* blog = getenv("WDR_BATCH_LOG") ? fopen(getenv("WDR_BATCH_LOG"), "w") : nullptr;
   if (blog) WDR_HIP(hipEventRecord(m.ev0, m.s));
-  if (sampled || no_graph() || !decode_only) {
-    // sampled step for live kernel timing (prof.h), graphs disabled, or a mixed batch
+  bool prof_replay = false;   // a sampled decode-only step: its profiled graph replays
+  Impl::G* pgr = nullptr;
+  if (no_graph() || !decode_only) {
+    // graphs disabled, or a mixed batch (its launches sampled like every eager launch, prof.h)
     prof_in_step(sampled);
     try {
       tb.upload(io, m.s, true, false);
@@ -2969,30 +2982,42 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
     // the cross-attention grid has one workgroup row per group: the group count is in the key
     const bool grouped = tb.vgrp_max > 1;
     Impl::G& g = m.graphs[((long long)K << 40) + (grouped ? 1ll << 39 : 0ll) + ((long long)tb.n_vgrp << 16) + R];
-    if (g.exec && memcmp(&g.vids, &vids, sizeof(VocabIds)) != 0) {
-      (void)hipGraphExecDestroy(g.exec);
-      g.exec = nullptr;
-    }
-    if (!g.exec) {
+    if ((g.exec || g.pexec) && memcmp(&g.vids, &vids, sizeof(VocabIds)) != 0) g.drop();
+    prof_replay = sampled;
+    hipGraphExec_t& ex = prof_replay ? g.pexec : g.exec;
+    if (!ex) {
       std::lock_guard<std::recursive_mutex> cap_lock(hip_alloc_mutex());   // no allocation meanwhile
+      if (prof_replay && !g.pg) g.pg = prof_graph_new();
       hipGraph_t graph;
       prof_capture(true);
-      WDR_HIP(hipStreamBeginCapture(m.s, hipStreamCaptureModeRelaxed));
-      tb.upload(io, m.s, true, false);
-      rows_forward(ctx_, io, R, m.s);
-      tail();
+      if (prof_replay) prof_graph_capture(g.pg);
+      try {
+        WDR_HIP(hipStreamBeginCapture(m.s, hipStreamCaptureModeRelaxed));
+        tb.upload(io, m.s, true, false);
+        rows_forward(ctx_, io, R, m.s);
+        tail();
+      } catch (...) {
+        prof_graph_capture(nullptr);
+        prof_capture(false);
+        throw;
+      }
+      prof_graph_capture(nullptr);
       prof_capture(false);
       WDR_HIP(hipStreamEndCapture(m.s, &graph));
-      WDR_HIP(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
+      WDR_HIP(hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0));
       WDR_HIP(hipGraphDestroy(graph));
       g.vids = vids;
     } else {
       tb.upload(io, m.s, false, false);   // the captured copy node reads the staging
     }
+    if (prof_replay) {
+      pgr = &g;
+      prof_graph_reset(g.pg, m.s);
+    }
     {
       std::mutex* mu = launch_lock();   // WDR_LAUNCH_LOCK (prof.h)
       if (mu) mu->lock();
-      const hipError_t ge = hipGraphLaunch(g.exec, m.s);
+      const hipError_t ge = hipGraphLaunch(ex, m.s);
       if (mu) mu->unlock();
       WDR_HIP(ge);
     }
@@ -3000,6 +3025,7 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
   if (blog) WDR_HIP(hipEventRecord(m.ev1, m.s));
   const double t_enq = now_s();   // host side of the launch done (eager: every kernel enqueued)
   WDR_HIP(hipStreamSynchronize(m.s));
+  if (prof_replay && pgr) prof_graph_collect(pgr->pg);
   auto tok_of = [&](int i) {
     const TokOut& o = m.h_tok[i];
     TokenData t{};
