@@ -93,6 +93,10 @@ def test_configs3_split_eight_logical_devices(monkeypatch):
     one.close()
     _progress(phase="one device", segments=len(ref))
     monkeypatch.setenv("WDR_DEVICES", ",".join(["0"] * 8))
+    # the per-model pools (KV sequences, cross-K/V slot rings of the chains' states) are sized at
+    # creation for WDR_DECODE_CHAINS chains: 3 per model here, or eight 24-chain pools would not
+    # fit one GPU's 288 GB
+    monkeypatch.setenv("WDR_DECODE_CHAINS", "3")
     eight = wdr.WhisperContext("large-v3", enable_dtw=True, synthetic=syn)
     assert eight.devices == [0] * 8
     eight.set_chains(3)

@@ -25,7 +25,7 @@ namespace wdr {
 
 constexpr int FA_KB = 64, FA_KS = 72, FA_VS = 68;
 
-__global__ __launch_bounds__(256) void k_flash_attn(FlashArgs a) {
+__global__ __launch_bounds__(256, 3) void k_flash_attn(FlashArgs a) {
   ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
   __shared__ __attribute__((aligned(16))) f16 Ks[FA_KB * FA_KS];
   __shared__ __attribute__((aligned(16))) f16 Vt[64 * FA_VS];
@@ -135,9 +135,14 @@ __global__ __launch_bounds__(256) void k_flash_attn(FlashArgs a) {
       }
     rs += __shfl_xor(rs, 32, 64);
     l = l * alpha + rs;
+    // rescale only when some row's max moved (alpha == 1 exactly otherwise: the skip is exact);
+    // past the first key tiles of a 1500-key row that is rare, and it saves 32 multiplies a tile
+    const bool moved = __any(mnew != m);
     m = mnew;
+    if (moved) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+    }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
