@@ -5,12 +5,11 @@ import csv
 import sys
 
 GROUPS = [
-    ("step-gemv", ("k_dgemv", "k_mgemv", "k_gemv<")),
     ("step-attn", ("k_dec_self_attn", "k_xattn_partial", "k_xattn_combine", "k_embed")),
     ("logits", ("k_logits",)),
-    ("enc-gemm", ("k_gemm<",)),
+    ("enc-gemm", ("k_gemm<", "k_gemm2<", "k_gemm3<", "k_gemm4<", "k_gemm5<", "k_gemm8<")),
     ("flash", ("k_flash",)),
-    ("skinny", ("k_skinny",)),
+    ("rows", ("k_skinny",)),
     ("layernorm", ("k_layernorm",)),
     ("dtw", ("k_dtw", "k_aheads")),
     ("mel", ("k_mel", "k_im2col", "k_energy", "k_i16")),
