@@ -573,11 +573,10 @@ def main():
     # per class: algorithmic flops (MFMA classes) or bytes (HBM classes) per launch / the average
     # duration of its sampled launches, timed by the kernels' own clock (first wave start -> last
     # wave end: rocprofv3's dispatch span; csrc/common.h ProfClock), each sample weighted by
-    # 1 / its sampling probability (csrc/prof.h: every launch of 1 in 32 decode-only steps, which
-    # replay a second capture of their graph carrying clock slots; 1 in 64 eager launches, the
-    # encode batches' and the prefill / DTW batches'), so `launches_est` estimates the class's
-    # launch count; the eager samples' HIP start/stop events are reported beside it (under the
-    # pipeline's multi-stream concurrency they also absorb the launch's wait for the GPU).
+    # 1 / its sampling probability (every class is sampled 1 in 64, csrc/prof.cpp), so
+    # `launches_est` estimates the class's launch count; the same launches' HIP start/stop
+    # events are reported beside it (under the pipeline's multi-stream concurrency they also
+    # absorb the launch's wait for the GPU).
     classes = {}
     for c, (ms, nl, by, fl) in live.items():
         if ms <= 0:
@@ -600,9 +599,11 @@ def main():
         if tr is not None:
             r["traffic"] = round(tr)
             r["traffic_source"] = src
-        r["sampling"] = ("every launch of 1 in %d decode-only steps (profiled graph replay), 1 in %d "
-                         "eager launches; weighted by 1 / sampling probability") % (
-            PROF_STEP_EVERY, PROF_EVERY * PROF_STEP_EVERY)
+        # csrc/prof.h: decode steps replay hipGraphs; 1 in 32 steps runs eagerly and 1 in 2 of
+        # its launches is clocked; launches outside steps (encode batches, prefill / DTW batches)
+        # are clocked 1 in 64
+        r["sampling"] = "1 in %d launches (decode steps: 1 in %d eager, 1 in %d of those)" % (
+            PROF_EVERY * PROF_STEP_EVERY, PROF_STEP_EVERY, PROF_EVERY)
         classes[c] = r
     # `roofline` = the class with the largest share of kernel time in the committed rocprofv3
     # trace of this benched configuration (profiles/rNN/prof_graph/classes.json; r03: encoder

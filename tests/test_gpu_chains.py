@@ -68,6 +68,32 @@ def test_sixteen_chains_equal_single_chain(name, seconds, monkeypatch):
     ctx.close()
 
 
+@pytest.mark.parametrize("name,seconds", [("tiny-test", 90.0), ("large-v3", 60.0)])
+def test_partial_batches_equal_single_chain(name, seconds, monkeypatch):
+    """The step batcher launches once every chain has submitted or WDR_BATCH_WAIT_US after the
+    GPU became free: a chain busy on the host joins the next batch.  At 0 us (launch whatever is
+    pending the moment the GPU is free: the most fragmented batches) and at -1 (always wait for
+    every chain) 8 chains must give the one-chain result exactly -- a row's result does not
+    depend on the batch it rides in (csrc/rows.h)."""
+    syn = wdr.Synthetic(weight_std=0.02, emb_std=0.5, force_len_rate=3.3, disable_fallback=True)
+    pcm, spurts = synth_speech(seconds, seed=17, n_speakers=2)
+    segs = _segs(pcm, spurts)
+    assert len(segs) >= 8
+    opts = wdr.TranscribeOptions(lang="auto", advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    launches = {}
+    ref = None
+    for wait in ("-1", "0"):
+        monkeypatch.setenv("WDR_BATCH_WAIT_US", wait)   # read when the context's batchers are made
+        ctx = wdr.WhisperContext(name, synthetic=syn)
+        if ref is None:
+            ref, lang1 = _run(ctx, segs, opts, 1)
+        got, lang = _run(ctx, segs, opts, 8)
+        launches[wait] = ctx.stage_times()["batch_launches"]
+        ctx.close()
+        assert lang == lang1 and got == ref, wait
+    assert launches["0"] >= launches["-1"], launches
+
+
 @pytest.mark.parametrize("fallback", [False, True])
 def test_forced_early_fixup_is_exact(fallback):
     """The early prompt fix-up (a chain redoes its first segments from its predecessor's final

@@ -126,18 +126,19 @@ struct ProjArgs {
 // Live kernel clock (csrc/prof.cpp): a launch the profiler samples carries ts -> {earliest wave
 // start, latest wave end} in wall_clock64() ticks (the constant-rate clock), i.e. the span
 // rocprofv3's dispatch timestamps measure, free of the queueing that HIP start/stop events of a
-// launch absorb under multi-stream concurrency.  The first wave of every workgroup stamps the
-// start, lane 0 of every wave the end, with vector atomics spread over PROF_CLK_LANES words;
+// launch absorb under multi-stream concurrency.  Thread 0 of every workgroup stamps the start
+// when its wave starts and the end when its wave retires -- two vector atomics per workgroup,
+// spread over PROF_CLK_LANES words (one stamp per wave, on 32 words, serialised at L2 on the
+// 11 520-workgroup cross-attention launches and inflated their spans ~3x against the trace);
 // unsampled launches (ts null) skip it.
-constexpr int PROF_CLK_LANES = 32;   // stamp addresses per sampled launch (csrc/prof.cpp ring)
+constexpr int PROF_CLK_LANES = 128;   // stamp addresses per sampled launch (csrc/prof.cpp ring)
 struct ProfClock {
   unsigned long long* ts;
   __device__ __forceinline__ explicit ProfClock(unsigned long long* t) : ts(t) {
-    // a workgroup's waves start together: its first wave stamps the start
     if (ts && threadIdx.x == 0) atomicMin(ts + lane_of_block(), (unsigned long long)wall_clock64());
   }
   __device__ __forceinline__ ~ProfClock() {
-    if (ts && (threadIdx.x & 63) == 0) atomicMax(ts + PROF_CLK_LANES + lane_of_block(), (unsigned long long)wall_clock64());
+    if (ts && threadIdx.x == 0) atomicMax(ts + PROF_CLK_LANES + lane_of_block(), (unsigned long long)wall_clock64());
   }
   __device__ __forceinline__ static int lane_of_block() {
     return (int)((blockIdx.x + blockIdx.y * 7u + blockIdx.z * 13u) % PROF_CLK_LANES);
@@ -147,10 +148,6 @@ unsigned long long* prof_slot();   // next clock slot of the sampled-launch ring
 template <typename A>
 inline unsigned long long* prof_attach(A&) { return nullptr; }
 inline unsigned long long* prof_attach(ProjArgs& a) { return a.ts = prof_slot(); }
-// argument structs with a clock slot take one (profiled graph captures, prof.h); others cannot
-template <typename A>
-inline bool prof_set_ts(A&, unsigned long long*) { return false; }
-inline bool prof_set_ts(ProjArgs& a, unsigned long long* t) { a.ts = t; return true; }
 // M <= 64 (or rows_mma) on the row kernel k_skinny, larger M on the MFMA GEMM tiles
 void launch_proj(const ProjArgs& a, hipStream_t s);
 // re-read the encoder GEMM dispatch knobs (WDR_GEMM*), which launch_proj reads once per process:

@@ -95,7 +95,6 @@ struct FlashArgs {
   unsigned long long* ts = nullptr;   // live kernel clock (common.h ProfClock)
 };
 inline unsigned long long* prof_attach(FlashArgs& a) { return a.ts = prof_slot(); }
-inline bool prof_set_ts(FlashArgs& a, unsigned long long* t) { a.ts = t; return true; }
 void launch_flash_attn(const FlashArgs& a, int n_batch, hipStream_t s);
 struct DecSelfArgs {
   const f16* q; int ldq;
@@ -144,7 +143,6 @@ struct XAttnArgs {
 };
 constexpr int XATTN_GRP_MAX = 8;   // rows sharing one K/V without row_k
 inline unsigned long long* prof_attach(XAttnArgs& a) { return a.ts = prof_slot(); }
-inline bool prof_set_ts(XAttnArgs& a, unsigned long long* t) { a.ts = t; return true; }
 void launch_xattn(const XAttnArgs& a, hipStream_t s);
 struct CaptureArgs {
   const f16* q; int ldq;

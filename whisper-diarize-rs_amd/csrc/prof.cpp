@@ -21,7 +21,7 @@ struct Rec {
   int cls;
 };
 struct ClkRec {
-  long long slot;   // kernel-clock slot in the ring (or in a profiled graph's arena)
+  long long slot;   // kernel-clock slot in the ring
   int cls;
   double bytes, flops;
   double w;         // 1 / the launch's sampling probability
@@ -246,66 +246,6 @@ void prof_push(int cls, hipEvent_t a, hipEvent_t b, unsigned long long* ts, doub
   g_acc[cls].flops += flops;
   g_acc[cls].n++;
   if (g_pending.size() > 4096) drain_locked(false);
-}
-
-// ---------------------------------------------------------------- profiled graph replays
-struct ProfGraph {
-  static constexpr int kSlots = 1024;   // clocked launches per graph (a large-v3 step: ~260)
-  unsigned long long* arena = nullptr;  // [kSlots][kSlotWords], the ring's slot layout
-  unsigned long long* init = nullptr;   // the same size: start words ~0, end words 0
-  int dev = -1;
-  std::vector<ClkRec> recs;             // slot = position
-  std::vector<unsigned long long> host;
-};
-thread_local ProfGraph* t_graph = nullptr;
-
-ProfGraph* prof_graph_new() {
-  auto* g = new ProfGraph;
-  const size_t n = (size_t)ProfGraph::kSlots * kSlotWords;
-  std::vector<unsigned long long> init(n);
-  for (int i = 0; i < ProfGraph::kSlots; ++i)
-    for (int j = 0; j < PROF_CLK_LANES; ++j) {
-      init[(size_t)i * kSlotWords + j] = ~0ull;
-      init[(size_t)i * kSlotWords + PROF_CLK_LANES + j] = 0ull;
-    }
-  WDR_HIP(hipGetDevice(&g->dev));
-  WDR_HIP(hipMalloc(&g->arena, n * 8));
-  WDR_HIP(hipMalloc(&g->init, n * 8));
-  WDR_HIP(hipMemcpy(g->init, init.data(), n * 8, hipMemcpyHostToDevice));
-  return g;
-}
-void prof_graph_capture(ProfGraph* g) { t_graph = g; }
-bool prof_graph_on(int cls) {
-  return t_graph && (g_mask.load(std::memory_order_relaxed) & (1 << cls)) && (int)t_graph->recs.size() < ProfGraph::kSlots;
-}
-unsigned long long* prof_graph_slot(int cls, double bytes, double flops) {
-  ProfGraph* g = t_graph;
-  if (!g || (int)g->recs.size() >= ProfGraph::kSlots) return nullptr;
-  const long long i = (long long)g->recs.size();
-  g->recs.push_back({i, cls, bytes, flops, (double)kStepEvery});
-  return g->arena + (size_t)i * kSlotWords;
-}
-void prof_graph_reset(ProfGraph* g, hipStream_t s) {
-  if (g && !g->recs.empty())
-    WDR_HIP(wdr_memcpy_async(g->arena, g->init, g->recs.size() * kSlotWords * 8, hipMemcpyDeviceToDevice, s));
-}
-void prof_graph_collect(ProfGraph* g) {
-  if (!g || g->recs.empty()) return;
-  g->host.resize(g->recs.size() * kSlotWords);
-  WDR_HIP(hipMemcpy(g->host.data(), g->arena, g->host.size() * 8, hipMemcpyDeviceToHost));
-  std::lock_guard<std::mutex> l(g_mu);
-  if (g_tick_ms <= 0.0) return;   // the ring (and the clock rate) were never set up
-  fold_clocks(g->recs, g->host.data(), g->host.size());
-}
-void prof_graph_free(ProfGraph* g) {
-  if (!g) return;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  (void)hipSetDevice(g->dev);
-  (void)hipFree(g->arena);
-  (void)hipFree(g->init);
-  (void)hipSetDevice(dev);
-  delete g;
 }
 
 }  // namespace wdr

@@ -33,20 +33,6 @@ std::mutex* launch_lock();
 
 void prof_push(int cls, hipEvent_t a, hipEvent_t b, unsigned long long* ts, double bytes, double flops);
 
-// Profiled graph replays (the step batcher's decode-only steps): a sampled step replays a second
-// capture of its graph whose launches of the enabled classes carry clock slots in an arena of
-// their own -- reset before the replay, read after the step's stream synchronisation -- so the
-// live figure times the graph-replayed launches the trace sees, not eager substitutes.  Every
-// launch of such a replay counts with weight kStepEvery (1 in kStepEvery steps is sampled), an
-// eager sample with kEvery * kStepEvery (prof.cpp): the class average stays a uniform estimate.
-struct ProfGraph;
-ProfGraph* prof_graph_new();
-void prof_graph_capture(ProfGraph* g);   // this thread's launches attach to g until nullptr
-bool prof_graph_on(int cls);             // inside such a capture, the class enabled
-unsigned long long* prof_graph_slot(int cls, double bytes, double flops);
-void prof_graph_reset(ProfGraph* g, hipStream_t s);   // before a replay, on its stream
-void prof_graph_collect(ProfGraph* g);                // after the replay completed
-void prof_graph_free(ProfGraph* g);
 
 // async copies / fills under WDR_LAUNCH_LOCK too: HIP runs them as blit kernels, whose
 // dispatches the profiler intercepts like any launch
@@ -87,9 +73,6 @@ inline void wdr_launch(int cls, double bytes, double flops, F kernel, dim3 grid,
     unsigned long long* ts = prof_attach(a0);
     hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, a, b, 0, a0, args...);
     prof_push(cls, a, b, ts, bytes, flops);
-  } else if (prof_graph_on(cls) && prof_set_ts(a0, nullptr)) {
-    prof_set_ts(a0, prof_graph_slot(cls, bytes, flops));   // a profiled graph's capture
-    hipLaunchKernelGGL(kernel, grid, block, shmem, s, a0, args...);
   } else {
     hipLaunchKernelGGL(kernel, grid, block, shmem, s, a0, args...);
   }

@@ -7,6 +7,8 @@
 //            device work buffers, KV caches, streams, and the host-side decode loop
 //            `full()` = whisper_full_with_state as the reference drives it.
 #pragma once
+
+#include <exception>
 #include <atomic>
 #include <memory>
 #include <mutex>
@@ -218,6 +220,9 @@ class StepBatcher {
     const f16* dxkv = nullptr;
     float* dcap = nullptr;
     int dl_end = 1 << 30;
+    // set by the launch that carried this request (under the batcher's lock)
+    bool done = false;
+    std::exception_ptr err;
   };
   void enter();
   void leave();

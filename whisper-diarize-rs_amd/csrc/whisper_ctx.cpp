@@ -2730,9 +2730,16 @@ struct StepBatcher::Impl {
   std::condition_variable cv;
   int active = 0;                 // chains inside the batcher
   std::vector<Req*> pend;         // requests of the batch being collected
-  long long round = 0;            // completed launches
-  bool running = false;           // a batch is on the GPU (new requests wait for the next)
-  std::exception_ptr err;         // failure of the last launch (rethrown to its requesters)
+  bool running = false;           // a batch is on the GPU (new requests collect for the next)
+  // a batch launches when every chain inside has submitted, or WDR_BATCH_WAIT_US after the GPU
+  // became free with at least one request waiting: a chain busy on the host (a segment's end,
+  // its DTW submission, the next prompt) joins the following batch instead of holding the other
+  // chains' rows back -- exact, since a row's result does not depend on its batch (rows.h)
+  double t_free = 0;              // when the last batch's results were handed out
+  double t_first = 0;             // when the oldest pending request arrived
+  // WDR_BATCH_WAIT_US (read when the batcher is made): how long a batch may wait for stragglers
+  // once the GPU is free (default 300 us; negative: wait for every chain, the round-3 rule)
+  double wait_s = 300e-6;
   hipStream_t s = nullptr;
   int d = 0, V = 0, H = 0;
   int RB = 0, LB = 0;             // row / logit-row capacity of one launch
@@ -2745,16 +2752,9 @@ struct StepBatcher::Impl {
   struct G {
     hipGraphExec_t exec = nullptr;
     VocabIds vids{};
-    // the same step captured with clock slots on its launches (prof.h, profiled graph replays):
-    // replayed instead of exec by the sampled steps while the live profiler is on
-    hipGraphExec_t pexec = nullptr;
-    ProfGraph* pg = nullptr;
     void drop() {
       if (exec) (void)hipGraphExecDestroy(exec);
-      if (pexec) (void)hipGraphExecDestroy(pexec);
-      prof_graph_free(pg);
-      exec = pexec = nullptr;
-      pg = nullptr;
+      exec = nullptr;
     }
   };
   std::map<long long, G> graphs;  // decode-only batches, by (K, group kind, groups, rows)
@@ -2771,6 +2771,7 @@ StepBatcher::StepBatcher(Context& ctx) : ctx_(ctx), m_(new Impl) {
   int lo = 0, hi = 0;
   WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
   m.s = dedicated_stream("WDR_BATCH_HWQ", false, hi);
+  if (const char* e = getenv("WDR_BATCH_WAIT_US")) m.wait_s = atof(e) * 1e-6;
   const int RB = rows_cap(ctx), LB = logit_cap(ctx);
   m.RB = RB;
   m.LB = LB;
@@ -2840,55 +2841,52 @@ void StepBatcher::enter() {
 }
 
 void StepBatcher::leave() {
-  Impl& m = *m_;
-  std::unique_lock<std::mutex> lk(m.mu);
-  m.active--;
-  if (!m.running && !m.pend.empty() && (int)m.pend.size() >= m.active) {
-    std::vector<Req*> batch;
-    batch.swap(m.pend);
-    m.running = true;
-    lk.unlock();
-    std::exception_ptr e;
-    try {
-      launch(batch);
-    } catch (...) {
-      e = std::current_exception();
-    }
-    lk.lock();
-    m.err = e;
-    m.running = false;
-    m.round++;
-    m.cv.notify_all();
-  }
+  std::lock_guard<std::mutex> g(m_->mu);
+  m_->active--;
+  m_->cv.notify_all();   // a waiter may now hold the last missing request
 }
 
 void StepBatcher::step(Req& r) {
   Impl& m = *m_;
   std::unique_lock<std::mutex> lk(m.mu);
-  m.cv.wait(lk, [&] { return !m.running; });
+  r.done = false;
+  r.err = nullptr;
+  if (m.pend.empty()) m.t_first = now_s();
   m.pend.push_back(&r);
-  const long long my = m.round;
-  if ((int)m.pend.size() >= m.active) {
-    std::vector<Req*> batch;
-    batch.swap(m.pend);
-    m.running = true;
-    lk.unlock();
-    std::exception_ptr e;
-    try {
-      launch(batch);
-    } catch (...) {
-      e = std::current_exception();
+  const double wait = m.wait_s;
+  while (!r.done) {
+    if (!m.running && !m.pend.empty()) {
+      const bool all = (int)m.pend.size() >= m.active;
+      const double t_go = std::max(m.t_free, m.t_first) + wait;
+      if (all || (wait >= 0 && now_s() >= t_go)) {
+        std::vector<Req*> batch;
+        batch.swap(m.pend);
+        m.running = true;
+        lk.unlock();
+        std::exception_ptr e;
+        try {
+          launch(batch);
+        } catch (...) {
+          e = std::current_exception();
+        }
+        lk.lock();
+        for (Req* q : batch) {
+          q->err = e;
+          q->done = true;
+        }
+        m.running = false;
+        m.t_free = now_s();
+        m.cv.notify_all();
+        continue;
+      }
+      if (wait >= 0) {
+        m.cv.wait_for(lk, std::chrono::duration<double>(std::max(t_go - now_s(), 1e-6)));
+        continue;
+      }
     }
-    lk.lock();
-    m.err = e;
-    m.running = false;
-    m.round++;
-    m.cv.notify_all();
-    if (e) std::rethrow_exception(e);
-    return;
+    m.cv.wait(lk);
   }
-  m.cv.wait(lk, [&] { return m.round != my; });
-  if (m.err) std::rethrow_exception(m.err);
+  if (r.err) std::rethrow_exception(r.err);
 }
 
 // one batch: every request's DTW rows, decode rows and prefill rows as ONE rows forward (rows.h),
@@ -2964,10 +2962,9 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
   const bool decode_only = n_pre == 0 && n_dtw == 0;
   static FILE* blog = getenv("WDR_BATCH_LOG") ? fopen(getenv("WDR_BATCH_LOG"), "w") : nullptr;
   if (blog) WDR_HIP(hipEventRecord(m.ev0, m.s));
-  bool prof_replay = false;   // a sampled decode-only step: its profiled graph replays
-  Impl::G* pgr = nullptr;
-  if (no_graph() || !decode_only) {
-    // graphs disabled, or a mixed batch (its launches sampled like every eager launch, prof.h)
+  if (sampled || no_graph() || !decode_only) {
+    // sampled step for live kernel timing (prof.h: its launches run eagerly, 1 in 2 of them
+    // clocked), graphs disabled, or a mixed batch
     prof_in_step(sampled);
     try {
       tb.upload(io, m.s, true, false);
@@ -2982,42 +2979,27 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
     // the cross-attention grid has one workgroup row per group: the group count is in the key
     const bool grouped = tb.vgrp_max > 1;
     Impl::G& g = m.graphs[((long long)K << 40) + (grouped ? 1ll << 39 : 0ll) + ((long long)tb.n_vgrp << 16) + R];
-    if ((g.exec || g.pexec) && memcmp(&g.vids, &vids, sizeof(VocabIds)) != 0) g.drop();
-    prof_replay = sampled;
-    hipGraphExec_t& ex = prof_replay ? g.pexec : g.exec;
-    if (!ex) {
+    if (g.exec && memcmp(&g.vids, &vids, sizeof(VocabIds)) != 0) g.drop();
+    if (!g.exec) {
       std::lock_guard<std::recursive_mutex> cap_lock(hip_alloc_mutex());   // no allocation meanwhile
-      if (prof_replay && !g.pg) g.pg = prof_graph_new();
       hipGraph_t graph;
       prof_capture(true);
-      if (prof_replay) prof_graph_capture(g.pg);
-      try {
-        WDR_HIP(hipStreamBeginCapture(m.s, hipStreamCaptureModeRelaxed));
-        tb.upload(io, m.s, true, false);
-        rows_forward(ctx_, io, R, m.s);
-        tail();
-      } catch (...) {
-        prof_graph_capture(nullptr);
-        prof_capture(false);
-        throw;
-      }
-      prof_graph_capture(nullptr);
+      WDR_HIP(hipStreamBeginCapture(m.s, hipStreamCaptureModeRelaxed));
+      tb.upload(io, m.s, true, false);
+      rows_forward(ctx_, io, R, m.s);
+      tail();
       prof_capture(false);
       WDR_HIP(hipStreamEndCapture(m.s, &graph));
-      WDR_HIP(hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0));
+      WDR_HIP(hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0));
       WDR_HIP(hipGraphDestroy(graph));
       g.vids = vids;
     } else {
       tb.upload(io, m.s, false, false);   // the captured copy node reads the staging
     }
-    if (prof_replay) {
-      pgr = &g;
-      prof_graph_reset(g.pg, m.s);
-    }
     {
       std::mutex* mu = launch_lock();   // WDR_LAUNCH_LOCK (prof.h)
       if (mu) mu->lock();
-      const hipError_t ge = hipGraphLaunch(ex, m.s);
+      const hipError_t ge = hipGraphLaunch(g.exec, m.s);
       if (mu) mu->unlock();
       WDR_HIP(ge);
     }
@@ -3025,7 +3007,6 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
   if (blog) WDR_HIP(hipEventRecord(m.ev1, m.s));
   const double t_enq = now_s();   // host side of the launch done (eager: every kernel enqueued)
   WDR_HIP(hipStreamSynchronize(m.s));
-  if (prof_replay && pgr) prof_graph_collect(pgr->pg);
   auto tok_of = [&](int i) {
     const TokOut& o = m.h_tok[i];
     TokenData t{};
