@@ -398,6 +398,78 @@ __global__ __launch_bounds__(256, 8) void k_xattn_partial(XAttnArgs a) {   // <=
   }
 }
 
+// The greedy batched step's rows (every row its own group, row_k mode) two heads per workgroup:
+// half the workgroups of k_xattn_partial<true, 1>, twice the loads in flight per thread; each
+// head's arithmetic is that kernel's, instruction for instruction -- the same bits
+__global__ __launch_bounds__(256, 8) void k_xattn_partial2(XAttnArgs a) {   // <= 64 VGPRs
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
+  __shared__ __attribute__((aligned(16))) f16 Vs[2][XA_KC * 64];
+  __shared__ float red[2][2][4];
+  __shared__ float ps[2][XA_KC];
+  __shared__ float pv[2][4][64];
+  const int c = blockIdx.x, h0 = blockIdx.y * 2, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r0 = a.lead ? a.lead[blockIdx.z] : blockIdx.z;
+  if (a.grp && a.grp[r0] == 0) return;   // a row of a group led by an earlier row
+  if (a.lend && a.layer >= a.lend[r0]) return;   // a DTW re-forward past its last head layer
+  const f16* kb = a.row_k[r0] + a.layer_off;
+  const f16* vb = kb + a.v_off;
+  const int key0 = c * XA_KC;
+  const int kk = tid >> 2, qd = tid & 3;
+  const int key = key0 + kk;
+  const bool kok = key < a.Tk;
+  const long long row = (long long)(kok ? key : a.Tk - 1) * a.ldkv + h0 * a.hs + qd * 16;
+  const f16x8 ka0 = *(const f16x8*)(kb + row), ka1 = *(const f16x8*)(kb + row + 8);
+  const f16x8 kc0 = *(const f16x8*)(kb + row + a.hs), kc1 = *(const f16x8*)(kb + row + a.hs + 8);
+  {
+    const f16x8 v0 = *(const f16x8*)(vb + row), v1 = *(const f16x8*)(vb + row + 8);
+    const f16x8 v2 = *(const f16x8*)(vb + row + a.hs), v3 = *(const f16x8*)(vb + row + a.hs + 8);
+    *(f16x8*)(Vs[0] + kk * 64 + qd * 16) = v0;
+    *(f16x8*)(Vs[0] + kk * 64 + qd * 16 + 8) = v1;
+    *(f16x8*)(Vs[1] + kk * 64 + qd * 16) = v2;
+    *(f16x8*)(Vs[1] + kk * 64 + qd * 16 + 8) = v3;
+  }
+  auto score = [&](int hp, const f16x8& k0, const f16x8& k1) {
+    const f16* qr = a.q + (long long)r0 * a.ldq + (h0 + hp) * 64 + qd * 16;
+    const f16x8 q0 = *(const f16x8*)qr, q1 = *(const f16x8*)(qr + 8);
+    float t = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t += (float)q0[e] * (float)k0[e] + (float)q1[e] * (float)k1[e];
+    t += __shfl_xor(t, 1, 64);
+    t += __shfl_xor(t, 2, 64);
+    const float sc = kok ? t * a.scale : -INFINITY;
+    const float wm = wave_max(sc);
+    if (lane == 0) red[hp][0][wid] = wm;
+    return sc;
+  };
+  const float sc0 = score(0, ka0, ka1), sc1 = score(1, kc0, kc1);
+  __syncthreads();
+  float mx[2];
+  const float scs[2] = {sc0, sc1};
+#pragma unroll
+  for (int hp = 0; hp < 2; ++hp) {
+    mx[hp] = fmaxf(fmaxf(red[hp][0][0], red[hp][0][1]), fmaxf(red[hp][0][2], red[hp][0][3]));
+    const float p = scs[hp] == -INFINITY ? 0.f : __expf(scs[hp] - mx[hp]);
+    const float ws = wave_sum(qd == 0 ? p : 0.f);
+    if (qd == 0) ps[hp][kk] = p;
+    if (lane == 0) red[hp][1][wid] = ws;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int hp = 0; hp < 2; ++hp) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc += (float)(f16)ps[hp][wid * 16 + i] * (float)Vs[hp][(wid * 16 + i) * 64 + lane];
+    pv[hp][wid][lane] = acc;
+  }
+  __syncthreads();
+  if (tid < 128) {
+    const int hp = tid >> 6, dd = tid & 63, h = h0 + hp;
+    const long long cr = (long long)c * a.R + r0;
+    a.part_o[(cr * a.n_head + h) * 64 + dd] = pv[hp][0][dd] + pv[hp][1][dd] + pv[hp][2][dd] + pv[hp][3][dd];
+    if (dd == 0) a.part_ml[cr * a.n_head + h] = make_float2(mx[hp], red[hp][1][0] + red[hp][1][1] + red[hp][1][2] + red[hp][1][3]);
+  }
+}
+
 template <int NS>
 __global__ __launch_bounds__(64) void k_xattn_combine(XAttnArgs a) {
   const int r = blockIdx.x, h = blockIdx.y, d = threadIdx.x;
@@ -521,7 +593,10 @@ void launch_xattn_rows(const XAttnArgs& a, hipStream_t s) {
   const double kv = (double)a.Tk * a.n_head * 64 * 2 * 2;
   if (a.n_vgrp > 0) {
     const double flops = (double)a.R * a.Tk * a.n_head * 64 * 4;
-    if (a.vgrp_max <= 1)
+    if (a.vgrp_max <= 1 && a.n_head % 2 == 0)
+      wdr_launch(PROF_XATTN, a.n_vgrp * kv, flops, k_xattn_partial2, dim3(XA_NS, a.n_head / 2, a.n_vgrp), dim3(256),
+                 0, s, a);
+    else if (a.vgrp_max <= 1)
       wdr_launch(PROF_XATTN, a.n_vgrp * kv, flops, k_xattn_partial<true, 1>, dim3(XA_NS, a.n_head, a.n_vgrp),
                  dim3(256), 0, s, a);
     else
@@ -542,7 +617,9 @@ void launch_xattn(const XAttnArgs& a, hipStream_t s) {
   const int ng = a.row_k ? (a.grp ? a.n_grp : a.R) : 1;
   const double bytes = (double)ng * a.Tk * a.n_head * 64 * 2 * 2, flops = (double)a.R * a.Tk * a.n_head * 64 * 4;
   WDR_CHECK(!a.lead || (a.grp && a.n_grp >= 1 && a.n_grp <= a.R), "cross-attention decode: leaders need groups");
-  if (a.row_k && !a.grp)
+  if (a.row_k && !a.grp && a.n_head % 2 == 0)
+    wdr_launch(PROF_XATTN, bytes, flops, k_xattn_partial2, dim3(XA_NS, a.n_head / 2, a.R), dim3(256), 0, s, a);
+  else if (a.row_k && !a.grp)
     wdr_launch(PROF_XATTN, bytes, flops, k_xattn_partial<true, 1>, dim3(XA_NS, a.n_head, a.R), dim3(256), 0, s, a);
   else if (a.row_k)
     wdr_launch(PROF_XATTN, bytes, flops, k_xattn_partial<true, XATTN_GRP_MAX>,

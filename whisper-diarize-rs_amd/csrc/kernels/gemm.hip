@@ -1097,7 +1097,8 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
 // big shapes off k_gemm3; WDR_GEMM4=0|1 the ping-pong 256 x 256 GEMM off / forced on for every
 // shape it takes (unset: the measured dispatch rule); WDR_GEMM4_GM row tiles per group of the
 // k_gemm4 / k_gemm5 tile order (default 4); WDR_GEMM5=0 the narrow projections on k_gemm4's
-// tiles; WDR_GEMM_CUS persistent k_gemm4 workgroups (multiple of 8; default one per tile)
+// tiles; WDR_GEMM_CUS persistent k_gemm4 / k_gemm5 workgroups (multiple of 8; default one per
+// tile)
 struct GemmKnobs {
   bool gemm1, gemm3, gemm5;
   int gemm4, tile_gm, cus;
@@ -1143,7 +1144,8 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
     (void)attr5;
     ProjArgs g = a;
     g.tile_gm = kn.tile_gm;
-    dim3 grid((a.N / 128) * cdiv(a.M, G3_M));
+    const int ntiles5 = (a.N / 128) * cdiv(a.M, G3_M);
+    dim3 grid(kn.cus > 0 && kn.cus < ntiles5 ? kn.cus : ntiles5);
     wdr_launch(PROF_GEMM, bytes, flops, k_gemm5<EPI>, grid, dim3(512), G5_LDS, s, g);
   } else if (a.N % G3_N == 0 && a.K % G3_BK == 0 && !ref && vec4 &&
              (kn.gemm4 == 1 || (kn.gemm4 != 0 && (a.M >= 4096 || a.N >= 16384)))) {
