@@ -694,13 +694,7 @@ const Context::Fp8W& Context::fp8_xkv() {
   return fp8_xkv_;
 }
 
-// encoder windows per encode-ahead launch: 4 (M = 6000 rows) or, WDR_ENC_BATCH=8, 8 (M = 12000:
-// the tiled GEMMs quantise better on the encoder's 224 CUs); read once, at load
-static int read_enc_batch() {
-  const char* e = getenv("WDR_ENC_BATCH");
-  return e && atoi(e) == 8 ? 8 : 4;
-}
-static const int kBatch = read_enc_batch();
+static constexpr int kBatch = 4;     // encoder windows per encode-ahead launch (M = 6000 rows)
 static constexpr int kSlots = 16;    // in-flight segments in the cross-K/V ring (most)
 // WDR_SLOTS: ring slots per chain (a multiple of kBatch, 4..16; default 16)
 static int ring_slots() {
