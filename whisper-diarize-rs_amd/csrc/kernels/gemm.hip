@@ -1096,8 +1096,8 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
 // A/B runs set them per variant): WDR_GEMM1=1 every M > 64 projection on k_gemm; WDR_GEMM3=0 the
 // big shapes off k_gemm3; WDR_GEMM4=0|1 the ping-pong 256 x 256 GEMM off / forced on for every
 // shape it takes (unset: the measured dispatch rule); WDR_GEMM4_GM row tiles per group of the
-// k_gemm4 / k_gemm5 tile order (default 4); WDR_GEMM5=0 the narrow projections on k_gemm4's
-// tiles; WDR_GEMM_CUS persistent k_gemm4 / k_gemm5 workgroups (multiple of 8; default one per
+// k_gemm4 / k_gemm5 tile order (default 4); WDR_GEMM5=1 the narrow projections on k_gemm5's
+// 256 x 128 tiles; WDR_GEMM_CUS persistent k_gemm4 / k_gemm5 workgroups (multiple of 8; default one per
 // tile)
 struct GemmKnobs {
   bool gemm1, gemm3, gemm5;
@@ -1113,7 +1113,10 @@ static GemmKnobs read_knobs() {
   k.gemm3 = env_int("WDR_GEMM3", 1) != 0 && !k.gemm1;
   k.gemm4 = env_int("WDR_GEMM4", -1);
   k.tile_gm = env_int("WDR_GEMM4_GM", 4);
-  k.gemm5 = env_int("WDR_GEMM5", 1) != 0;
+  // k_gemm5 off by default since round 4: on the encode-ahead streams' 224 CUs its 240 tiles of
+  // o / fc2 take two rounds where k_gemm4's 120 take one and leave ~100 CUs to the decode chain
+  // (1-h bench 737-739 vs 725-731 xRT, profiles/r04/ab_gemm5.txt)
+  k.gemm5 = env_int("WDR_GEMM5", 0) != 0;
   k.cus = env_int("WDR_GEMM_CUS", 0) / 8 * 8;
   return k;
 }
