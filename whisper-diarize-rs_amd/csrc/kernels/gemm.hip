@@ -1198,6 +1198,13 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
 // for the residual projections, to share CUs with the encoder GEMM tiles: slower alone --
 // tools/rows_bench, o 15.0 vs 5.1 us, fc2 21.1 vs 13.7 us at 16 rows -- and 5 % slower in the
 // 1-h pipeline, profiles/r04/ab_epi4.txt.)
+// WDR_ROWS_PAIR=0: narrow projections of more than 32 rows one row tile per workgroup (A/B; read
+// once)
+static bool rows_pair_tiles() {
+  static const bool v = env_int("WDR_ROWS_PAIR", 1) != 0;
+  return v;
+}
+
 template <int EPI>
 static void launch_rows_epi(const ProjArgs& a, hipStream_t s) {
   // algorithmic bytes of the rows class (bench.py's live roofline and its trace counterpart,
@@ -1216,6 +1223,12 @@ static void launch_rows_epi(const ProjArgs& a, hipStream_t s) {
     if (a.K > 2048) {
       WDR_CHECK(!ln, "row projection: LN prologue needs K <= 1280");
       wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 16, false, 12>, dim3(cdiv(a.N, 16), mt), dim3(1024), 0, s, a);
+      return;
+    }
+    if (!ln && mt > 2 && rows_pair_tiles()) {
+      // above 32 rows (the batched steps that carry a prompt prefill, ~56 rows): two row tiles
+      // per workgroup, so a column tile's weights are read half as often
+      wdr_launch(prof, bytes, flops, k_skinny<EPI, 2, 1, 8>, dim3(cdiv(a.N, 16), cdiv(mt, 2)), dim3(512), 0, s, a);
       return;
     }
     dim3 grid(cdiv(a.N, 16), mt), blk(512);

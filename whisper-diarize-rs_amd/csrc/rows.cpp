@@ -170,10 +170,9 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, in
   // (Writing LN(x) from the residual launch's last workgroup per row tile -- an in-launch
   // hand-off -- measured slower still: 529 vs 557 xRT, profiles/r03/ab_lno_xfc.txt; a separate
   // residual + LayerNorm launch after split-K residual projections: profiles/r04/ab_epi4.txt.)
-  // up to 64 rows since round 4 (WDR_ROWS_LN_FUSE, read once; 32 before): the batched steps
-  // that carry a prompt prefill hold ~56 rows, and three separate LayerNorm launches per layer
-  // cost them more than each workgroup normalising its own 16-row tile
-  static const int ln_fuse_max = getenv("WDR_ROWS_LN_FUSE") ? atoi(getenv("WDR_ROWS_LN_FUSE")) : 64;
+  // WDR_ROWS_LN_FUSE (read once) moves the threshold: 64 measured even with 32 on the 1-h bench
+  // (737-739 vs 740-741 xRT, profiles/r04/ab_lnfuse.txt)
+  static const int ln_fuse_max = getenv("WDR_ROWS_LN_FUSE") ? atoi(getenv("WDR_ROWS_LN_FUSE")) : 32;
   const bool fuse_ln = R <= ln_fuse_max;
   auto P = [&](const f16* A, int lda, const f16* W, const float* b, void* out, int ldo, int N, int K, int epi,
                const float* lng = nullptr, const float* lnb = nullptr) {
