@@ -113,6 +113,12 @@ class Context {
   std::vector<std::unique_ptr<class StepBatcher>> batchers;
   int n_batchers = 1;
   StepBatcher& step_batcher(int chain = 0);
+  // the chains' prompt prefills on a batcher (and stream) of their own (WDR_PREFILL_SPLIT, default
+  // on): the decode steps of the other chains keep replaying their graphs while a prefill runs
+  // beside them, instead of turning into ~56-row eager steps (created on demand)
+  std::unique_ptr<class StepBatcher> prefill_b;
+  bool prefill_split = true;
+  StepBatcher& prefill_batcher();
   // multi-chain runs: the windows' DTW re-forwards of every chain, batched off the decode
   // chain's critical path (DtwQueue, created on demand; WDR_DTW_QUEUE=0: they ride in the step
   // batcher's requests instead)

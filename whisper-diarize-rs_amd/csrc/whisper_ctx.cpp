@@ -509,6 +509,7 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
     max_chains = std::max(1, std::min(64, e ? atoi(e) : 24));
     const char* nb = getenv("WDR_BATCHERS");
     n_batchers = std::max(1, std::min(8, nb ? atoi(nb) : 1));
+    prefill_split = !(getenv("WDR_PREFILL_SPLIT") && atoi(getenv("WDR_PREFILL_SPLIT")) == 0);
     fp8_encoder = getenv("WDR_FP8_ENCODER") && atoi(getenv("WDR_FP8_ENCODER")) != 0;
     const size_t per = (size_t)hp.n_text_layer * 21 * hp.n_text_ctx * hp.n_text_state;   // NSLOT = 21
     kv_k = DevMem(per * max_chains * 2);
@@ -521,6 +522,7 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
 Context::~Context() {
   dtwq.reset();
   batchers.clear();
+  prefill_b.reset();
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -2567,10 +2569,22 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
         TokenData tok;
         float ns = 0.f;
         if (i == 0 && pre_batched) {
-          if (!lockstep.b) {
+          // the prompt prefill: on the prefill batcher beside the other chains' decode steps, or
+          // (WDR_PREFILL_SPLIT=0) riding in their batched step
+          StepBatcher* pb = nullptr;
+          if (ctx_.prefill_split) {
+            pb = &ctx_.prefill_batcher();
+            pb->enter();
+          } else if (!lockstep.b) {
             lockstep.b = &ctx_.step_batcher(chain);
             lockstep.b->enter();
           }
+          struct Leave {
+            StepBatcher* b;
+            ~Leave() {
+              if (b) b->leave();
+            }
+          } leave_pb{pb};
           StepBatcher::Req rq;
           rq.n = 0;
           rq.pn = (int)prompt.size();
@@ -2580,7 +2594,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
           rq.pctl = c;
           rq.vids = m.vids;
           dtw_attach(rq);   // the previous window's re-forward rides along
-          lockstep.b->step(rq);
+          (pb ? pb : lockstep.b)->step(rq);
           dtw_after_step();
           tok = rq.pout;
           nosp = rq.pnosp;
@@ -2812,10 +2826,17 @@ StepBatcher& Context::step_batcher(int chain) {
   return *b;
 }
 
+StepBatcher& Context::prefill_batcher() {
+  static std::mutex mu;
+  std::lock_guard<std::mutex> g(mu);
+  if (!prefill_b) prefill_b = std::make_unique<StepBatcher>(*this);
+  return *prefill_b;
+}
+
 Context::BatchStats Context::batcher_stats() {
   BatchStats o;
-  for (int i = 0; i < std::max(1, n_batchers); ++i) {
-    StepBatcher& sb = step_batcher(i);
+  for (int i = 0; i < std::max(1, n_batchers) + (prefill_b ? 1 : 0); ++i) {
+    StepBatcher& sb = i < std::max(1, n_batchers) ? step_batcher(i) : *prefill_b;
     o.launches += sb.launches;
     o.rows += sb.rows;
     o.prefill_rows += sb.prefill_rows;
