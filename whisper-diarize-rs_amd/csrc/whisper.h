@@ -113,11 +113,12 @@ class Context {
   std::vector<std::unique_ptr<class StepBatcher>> batchers;
   int n_batchers = 1;
   StepBatcher& step_batcher(int chain = 0);
-  // the chains' prompt prefills on a batcher (and stream) of their own (WDR_PREFILL_SPLIT, default
-  // on): the decode steps of the other chains keep replaying their graphs while a prefill runs
-  // beside them, instead of turning into ~56-row eager steps (created on demand)
+  // WDR_PREFILL_SPLIT=1 (A/B): the chains' prompt prefills on a batcher (and stream) of their own
+  // beside the other chains' decode steps instead of riding in them -- measured slower (711-715
+  // vs 729-733 xRT: a 47-row prefill pass beside the decode steps took 13.6 ms, the chain waiting
+  // for it; profiles/r04/ab_psplit.txt), so off by default (created on demand)
   std::unique_ptr<class StepBatcher> prefill_b;
-  bool prefill_split = true;
+  bool prefill_split = false;
   StepBatcher& prefill_batcher();
   // multi-chain runs: the windows' DTW re-forwards of every chain, batched off the decode
   // chain's critical path (DtwQueue, created on demand; WDR_DTW_QUEUE=0: they ride in the step

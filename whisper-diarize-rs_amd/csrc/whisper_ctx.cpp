@@ -509,7 +509,7 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
     max_chains = std::max(1, std::min(64, e ? atoi(e) : 24));
     const char* nb = getenv("WDR_BATCHERS");
     n_batchers = std::max(1, std::min(8, nb ? atoi(nb) : 1));
-    prefill_split = !(getenv("WDR_PREFILL_SPLIT") && atoi(getenv("WDR_PREFILL_SPLIT")) == 0);
+    prefill_split = getenv("WDR_PREFILL_SPLIT") && atoi(getenv("WDR_PREFILL_SPLIT")) != 0;
     fp8_encoder = getenv("WDR_FP8_ENCODER") && atoi(getenv("WDR_FP8_ENCODER")) != 0;
     const size_t per = (size_t)hp.n_text_layer * 21 * hp.n_text_ctx * hp.n_text_state;   // NSLOT = 21
     kv_k = DevMem(per * max_chains * 2);
@@ -2569,8 +2569,8 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
         TokenData tok;
         float ns = 0.f;
         if (i == 0 && pre_batched) {
-          // the prompt prefill: on the prefill batcher beside the other chains' decode steps, or
-          // (WDR_PREFILL_SPLIT=0) riding in their batched step
+          // the prompt prefill rides in the other chains' batched step (WDR_PREFILL_SPLIT=1: on a
+          // prefill batcher of its own, A/B)
           StepBatcher* pb = nullptr;
           if (ctx_.prefill_split) {
             pb = &ctx_.prefill_batcher();
