@@ -315,6 +315,9 @@ int wdr_context_set_encoder_fp8(wdr_context* c, int8_t on);
  * 2 always (chain k waits for chain k-1, then redoes its first segments from the known prompt);
  * -1 restores the WDR_EARLY_FIXUP environment default */
 int wdr_dbg_set_early_fixup(wdr_context* c, int32_t mode);
+/* test seam: the diarization contractions on the f32 MFMA kernel (1, default) or the VALU f32
+ * kernel (0) for every later launch in the process */
+int wdr_dbg_set_gemm32(int32_t mfma);
 int wdr_context_stage_times(wdr_context* c, wdr_stage_times* out);
 int wdr_context_hparams(wdr_context* c, int32_t* out /* [10] */);
 

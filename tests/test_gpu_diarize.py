@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 import wdr
+from wdr import _lib as L
 from oracle import diarize as D
 from oracle.pipeline import write_wav
 from wdr.synth import synth_speech
@@ -129,18 +130,22 @@ def test_engine_transcribe_audio_with_diarize(tmp_path, dz):
         [(s.text, s.speaker_id, round(s.start, 6)) for s in want]
 
 
-def test_mfma_f32_gemm_equals_valu(dz, audio, monkeypatch):
+def test_mfma_f32_gemm_equals_valu(dz, audio):
     """The segmentation / CAM++ contractions on v_mfma_f32_32x32x2_f32 (k_gemm32m, default) and on
-    the VALU f32 kernel (WDR_GEMM32=0): both are one f32 fma per k in k order, so log-probabilities
+    the VALU f32 kernel (wdr_dbg_set_gemm32(0)): both are one f32 fma per k in k order, so log-probabilities
     and embeddings must agree to f32 rounding of the epilogues (1e-5), and the frame classes
     exactly wherever the class margin exceeds 1e-4."""
     pcm, spurts = audio
     cls, lp = dz.frame_classes(pcm, logprobs=True)
     x = pcm[int(spurts[0][0] * 16000):int(spurts[0][1] * 16000)]
     e = dz.embedding(x)
-    monkeypatch.setenv("WDR_GEMM32", "0")
-    cls0, lp0 = dz.frame_classes(pcm, logprobs=True)
-    e0 = dz.embedding(x)
+    lib = L.load()
+    L.check(lib.wdr_dbg_set_gemm32(0))
+    try:
+        cls0, lp0 = dz.frame_classes(pcm, logprobs=True)
+        e0 = dz.embedding(x)
+    finally:
+        L.check(lib.wdr_dbg_set_gemm32(1))
     np.testing.assert_allclose(lp, lp0, rtol=0, atol=1e-5)
     srt = np.sort(lp0, -1)
     clear = (srt[..., -1] - srt[..., -2]) > 1e-4

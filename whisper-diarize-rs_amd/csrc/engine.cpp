@@ -1851,6 +1851,13 @@ int wdr_dbg_set_early_fixup(wdr_context* c, int32_t mode) {
   })
 }
 
+int wdr_dbg_set_gemm32(int32_t mfma) {
+  WDR_GUARD({
+    set_gemm32_mfma(mfma != 0);
+    return 0;
+  })
+}
+
 int wdr_context_set_encoder_fp8(wdr_context* c, int8_t on) {
   WDR_GUARD({
     c->ctx->fp8_encoder = on != 0;

@@ -20,6 +20,8 @@
 //  k_colstats      per-utterance mean subtraction (CMN); stats pooling (mean, unbiased std).
 //  k_cam_context   CAM context rows: global mean + 100-frame segment means.
 //  k_cam_gate      out = y * m[segment] into the dense block's column range.
+#include <atomic>
+
 #include "../common.h"
 #include "kernels.h"
 #include "../prof.h"
@@ -167,11 +169,14 @@ __global__ __launch_bounds__(256) void k_gemm32m(Gemm32Args a) {
   }
 }
 
-// WDR_GEMM32=0: the VALU kernel (A/B; read per call: tests/test_gpu_diarize.py compares both)
-static bool gemm32_mfma() {
+// the f32 MFMA kernel (default) or the VALU one: WDR_GEMM32=0 at load, or wdr_dbg_set_gemm32
+// (tests/test_gpu_diarize.py compares both within one process)
+static std::atomic<int> g_gemm32_mfma{[] {
   const char* e = getenv("WDR_GEMM32");
-  return !(e && atoi(e) == 0);
-}
+  return e && atoi(e) == 0 ? 0 : 1;
+}()};
+void set_gemm32_mfma(bool on) { g_gemm32_mfma.store(on ? 1 : 0); }
+static bool gemm32_mfma() { return g_gemm32_mfma.load(std::memory_order_relaxed) != 0; }
 
 void launch_gemm32(const Gemm32Args& a, hipStream_t s) {
   if (a.M <= 0 || a.N <= 0) return;

@@ -203,6 +203,7 @@ struct Gemm32Args {
   int accum = 0;                     // C = act(v + C_old)
 };
 void launch_gemm32(const Gemm32Args& a, hipStream_t s);
+void set_gemm32_mfma(bool on);   // the f32 MFMA kernel (default) or the VALU one
 void launch_im2col_1d(const float* X, int ldx, int T, int C, int k, int stride, int dil, int pad, int To, float* col,
                       hipStream_t s);
 void launch_im2col_2d(const float* X, int T, int F, int C, int kf, int kt, int sf, int Fo, float* col, hipStream_t s);

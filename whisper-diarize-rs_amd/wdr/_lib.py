@@ -151,6 +151,7 @@ _SIGS = {
     "wdr_context_devices": (C.c_int, [vp, P(i32), P(i32), i32]),
     "wdr_context_set_encoder_fp8": (C.c_int, [vp, C.c_int8]),
     "wdr_dbg_set_early_fixup": (C.c_int, [vp, i32]),
+    "wdr_dbg_set_gemm32": (C.c_int, [i32]),
     "wdr_ggml_info": (C.c_int, [cstr, P(i32), P(i64), P(i64)]),
     "wdr_dbg_batch_step": (C.c_int, [vp, P(i32), sz, i32, i32, P(f64)]),
     "wdr_context_stage_times": (C.c_int, [vp, P(StageTimes)]),
