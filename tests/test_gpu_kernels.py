@@ -56,11 +56,11 @@ def test_projection_matches_fp32_reference(lib, M):
 GEMM1 = 0x800   # include/wdr.h WDR_DBG_PROJ_GEMM1
 
 
-@pytest.mark.parametrize("N", [1280, 2560])
+@pytest.mark.parametrize("N", [1280, 2560, 5120])
 def test_encoder_gemm_tiles(lib, N):
-    """The encoder-batch GEMM (M >= 4096): k_gemm4 (256 x 256 ping-pong; N = 1280 and 2560 -- the
-    narrow shapes' 256 x 128 k_gemm5 is an A/B option, WDR_GEMM5=1, checked by tools/gemm_bench),
-    a ragged last row tile (M = 4200): against the fp64 product
+    """The encoder-batch GEMMs (M >= 4096): k_gemm4 (256 x 256 ping-pong; N = 1280, 2560) and
+    k_gemm5 (256 x 128 ping-pong; the wide N = 4d of fc1), a ragged last row tile (M = 4200):
+    against the fp64 product
     within the f32 / f16 output rounding, and bit for bit equal to the register-staged k_gemm
     (WDR_DBG_PROJ_GEMM1), whose per-row arithmetic every other GEMM path shares -- every epilogue."""
     rng = np.random.default_rng(N)

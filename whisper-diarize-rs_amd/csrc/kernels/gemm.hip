@@ -1100,7 +1100,7 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
 // 256 x 128 tiles; WDR_GEMM_CUS persistent k_gemm4 / k_gemm5 workgroups (multiple of 8; default one per
 // tile)
 struct GemmKnobs {
-  bool gemm1, gemm3, gemm5;
+  bool gemm1, gemm3, gemm5, gemm5w;
   int gemm4, tile_gm, cus;
 };
 static int env_int(const char* name, int def) {
@@ -1117,6 +1117,7 @@ static GemmKnobs read_knobs() {
   // o / fc2 take two rounds where k_gemm4's 120 take one and leave ~100 CUs to the decode chain
   // (1-h bench 737-739 vs 725-731 xRT, profiles/r04/ab_gemm5.txt)
   k.gemm5 = env_int("WDR_GEMM5", 0) != 0;
+  k.gemm5w = env_int("WDR_GEMM5_WIDE", 1) != 0;
   k.cus = env_int("WDR_GEMM_CUS", 0) / 8 * 8;
   return k;
 }
@@ -1135,8 +1136,12 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
   const GemmKnobs& kn = knobs();
   const bool ref = kn.gemm1 || a.gemm_ref;
   const bool vec4 = a.ldo % 4 == 0 && (a.epi != EPI_QKV_CACHE || a.d % 4 == 0);   // epi_store4
-  if (a.N % 128 == 0 && a.N < 2048 && a.K % G3_BK == 0 && a.M >= 4096 && !ref && vec4 && kn.gemm5 &&
-             kn.gemm4 != 0 && (a.N / G3_N) * cdiv(a.M, G3_M) < 192) {
+  // fc1 (N = 4d) on k_gemm5's 256 x 128 tiles (WDR_GEMM5_WIDE, default on): on the encode-ahead
+  // streams' 224 CUs k_gemm4's 480 tiles take 3 rounds where k_gemm5's 960 half-size tiles take
+  // 5 (2.5 of the big ones); alone both run at the same per-tile rate (875 TFLOP/s)
+  const bool wide5 = kn.gemm5w && a.N >= 4096 && a.N < 16384 && a.M >= 4096;
+  if (a.N % 128 == 0 && a.K % G3_BK == 0 && a.M >= 4096 && !ref && vec4 && kn.gemm4 != 0 &&
+      (wide5 || (a.N < 2048 && kn.gemm5 && (a.N / G3_N) * cdiv(a.M, G3_M) < 192))) {
     // the narrow encoder projections (o, fc2) where 256 x 256 tiles would leave CUs idle: 256 x
     // 128 tiles fill 240 of 256 CUs at M = 6000 (tools/gemm_bench: o 53 vs 62 us on k_gemm2, fc2
     // 107 vs 126 us; at M = 12000 k_gemm4's 235 tiles are faster: fc2 194 vs 216 us)

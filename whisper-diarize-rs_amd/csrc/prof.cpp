@@ -31,7 +31,6 @@ constexpr int kClasses = 8;
 std::mutex g_mu;
 std::atomic<int> g_mask{0};   // enabled classes, bit (1 << cls)
 bool g_broken = false;
-std::atomic<unsigned> g_tick{0};
 constexpr unsigned kEvery = 2;    // launches timed inside a sampled (eager) decode step
 std::vector<Rec> g_pending;
 std::vector<hipEvent_t> g_pool;
@@ -170,7 +169,7 @@ struct FatalInit {
 } g_fatal_init;
 }  // namespace
 
-std::atomic<unsigned> g_step{0}, g_tick_out{0};
+
 constexpr unsigned kStepEvery = 32;   // decode steps run eagerly for sampling: 1 in 32 (was 1 in
                                       // 8: the eager steps cost the 1-h bench ~2 %)
 thread_local bool t_capture = false;
@@ -178,16 +177,25 @@ thread_local bool t_step = false;   // inside a sampled (eager) decode step
 
 // every launch of the class is timed with probability 1 / (kEvery * kStepEvery): 1 in kEvery
 // inside the sampled steps, 1 in kEvery * kStepEvery elsewhere (prefill, language detection),
-// so the average is over a uniform sample of the class's launches
+// so the average is over a uniform sample of the class's launches.  The picks are pseudo-random
+// (a per-thread xorshift), not every k-th launch: a fixed stride aliases with the fixed launch
+// sequence of an encode batch (131 GEMM / flash launches) and sampled, round 4, the 1.26-TFLOP
+// cross-K/V GEMM at another rate than the rest -- 16 % low on flops per launch vs the trace.
+static bool pick(unsigned every) {
+  thread_local uint64_t x = 0x9e3779b97f4a7c15ull ^ (uint64_t)(uintptr_t)&x;
+  x ^= x << 13;
+  x ^= x >> 7;
+  x ^= x << 17;
+  return (x >> 33) % every == 0;
+}
 bool prof_on(int cls) {
   if (!(g_mask.load(std::memory_order_relaxed) & (1 << cls)) || t_capture) return false;
   if (!on_ring_device()) return false;
-  if (t_step) return (g_tick++ % kEvery) == 0;
-  return (g_tick_out++ % (kEvery * kStepEvery)) == 0;
+  return pick(t_step ? kEvery : kEvery * kStepEvery);
 }
 bool prof_step() {
   if (!g_mask.load(std::memory_order_relaxed)) return false;
-  return (g_step++ % kStepEvery) == 0;
+  return pick(kStepEvery);
 }
 void prof_capture(bool on) { t_capture = on; }
 void prof_in_step(bool on) { t_step = on; }
@@ -258,9 +266,6 @@ int wdr_prof_set_mask(int32_t mask) {
   wdr::g_clk_pending.clear();
   if (wdr::g_mask) wdr::ring_reset_locked();
   wdr::g_broken = false;
-  wdr::g_tick = 0;
-  wdr::g_step = 0;
-  wdr::g_tick_out = 0;
   for (auto& a : wdr::g_acc) a = wdr::Acc{};
   return 0;
 }
