@@ -1240,6 +1240,9 @@ bool State::top_up_batch(int j) {
       const int nk = m.plan.n[k];
       slot_reserve_all(sl, nk, m.n_mels);   // normally sized by plan() already
       if (nk > sl.pcm_cap) {
+        // (a fallback: plan() sizes the slots) pinned host memory under the allocation mutex, as
+        // every allocation while other threads may be capturing graphs
+        std::lock_guard<std::recursive_mutex> g(hip_alloc_mutex());
         if (sl.h_pcm) WDR_HIP(hipHostFree(sl.h_pcm));
         WDR_HIP(hipHostMalloc((void**)&sl.h_pcm, (size_t)std::max(nk, 1) * 2, hipHostMallocDefault));
         sl.pcm = DevMem((size_t)std::max(nk, 1) * 2);
@@ -1252,6 +1255,7 @@ bool State::top_up_batch(int j) {
         WDR_HIP(wdr_memcpy_async(sl.pcm.p, sl.h_pcm, (size_t)nk * 2, hipMemcpyHostToDevice, m.es));
         launch_i16_to_f32(sl.pcm.as<int16_t>(), nk, sl.x.as<float>(), m.es);
         if (nk > sl.energy_cap) {
+          std::lock_guard<std::recursive_mutex> g(hip_alloc_mutex());
           if (sl.h_energy) WDR_HIP(hipHostFree(sl.h_energy));
           WDR_HIP(hipHostMalloc((void**)&sl.h_energy, (size_t)nk * 4, hipHostMallocDefault));
           sl.energy_d = DevMem((size_t)nk * 4);
