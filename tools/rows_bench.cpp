@@ -111,7 +111,7 @@ int main(int argc, char** argv) {
         }
       }, s, 10);
       const double ur = tr * 1e3 / nl;
-      printf("%-14s %4d %7.2f us   %5.2f TB/s\n", sh.name, M, ur, mb / ur / 1e3);
+      printf("%-14s %4d %7.2f us   %5.2f TB/s\n", sh.name, M, ur, mb / ur);
       fflush(stdout);
     }
     for (int l = 0; l < nw; ++l) CK(hipFree(W[l]));
