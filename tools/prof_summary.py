@@ -22,7 +22,7 @@ import re
 CLASSES = {
     "gemm": re.compile(r"\bk_gemm\d?[<(]"),
     "rows": re.compile(r"\bk_skinny<"),                       # decoder row projections (rows.h)
-    "flash": re.compile(r"\bk_flash_attn\("),                # encoder self-attention
+    "flash": re.compile(r"\bk_flash_attn(<\d+>)?\("),         # encoder self-attention
     "xattn": re.compile(r"\bk_xattn_(partial2?|mma)\b"),    # decoder cross-attention partials
     "diar": re.compile(r"\bk_(gemm32|lstm_scan|im2col_2d_b|im2col_1d_b|fbank|colstats_b|cam_|inorm|maxpool3|logsoftmax7)"),
 }

@@ -25,7 +25,10 @@ namespace wdr {
 
 constexpr int FA_KB = 64, FA_KS = 72, FA_VS = 68;
 
-__global__ __launch_bounds__(256, 3) void k_flash_attn(FlashArgs a) {
+// OCC = waves per SIMD the register budget is held to: 3 (<= 168 VGPRs) or 4 (<= 128), the
+// arithmetic identical (WDR_FLASH_OCC, flash_occ below)
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void k_flash_attn(FlashArgs a) {
   ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
   __shared__ __attribute__((aligned(16))) f16 Ks[FA_KB * FA_KS];
   __shared__ __attribute__((aligned(16))) f16 Vt[64 * FA_VS];
@@ -210,12 +213,18 @@ __global__ __launch_bounds__(64) void k_flash_combine(FlashArgs a) {
   if (a.ml && d == 0) a.ml[(long long)h * a.Tq + q] = make_float2(M, L);
 }
 
+static int flash_occ() {
+  static const int v = getenv("WDR_FLASH_OCC") && atoi(getenv("WDR_FLASH_OCC")) == 4 ? 4 : 3;
+  return v;
+}
+
 void launch_flash_attn(const FlashArgs& a, int n_batch, hipStream_t s) {
   WDR_CHECK(a.Tq > 0 && a.Tk > 0, "attention: empty");
+  auto* kfn = flash_occ() == 4 ? k_flash_attn<4> : k_flash_attn<3>;
   if (a.nsplit > 1) {
     WDR_CHECK(n_batch == 1 && !a.causal && a.nsplit <= 64 && a.part_o && a.part_ml, "flash split: bad args");
     wdr_launch(PROF_FLASH, (double)a.n_head * 64 * 2 * (2.0 * a.Tq + 2.0 * a.Tk), (double)a.n_head * a.Tq * a.Tk * 64 * 4,
-               k_flash_attn, dim3(cdiv(a.Tq, 128), a.n_head, a.nsplit), dim3(256), 0, s, a);
+               kfn, dim3(cdiv(a.Tq, 128), a.n_head, a.nsplit), dim3(256), 0, s, a);
     WDR_KLAUNCH(k_flash_combine, dim3(a.Tq, a.n_head), dim3(64), 0, s, a);
     WDR_HIP(hipGetLastError());
     return;
@@ -223,7 +232,7 @@ void launch_flash_attn(const FlashArgs& a, int n_batch, hipStream_t s) {
   dim3 grid(cdiv(a.Tq, 128), a.n_head, n_batch);
   const double pairs = a.causal ? 0.5 * (double)a.Tq * a.Tk : (double)a.Tq * a.Tk;
   wdr_launch(PROF_FLASH, (double)n_batch * a.n_head * 64 * 2 * (2.0 * a.Tq + 2.0 * a.Tk),
-             (double)n_batch * a.n_head * pairs * 64 * 4, k_flash_attn, grid, dim3(256), 0, s, a);
+             (double)n_batch * a.n_head * pairs * 64 * 4, kfn, grid, dim3(256), 0, s, a);
   WDR_HIP(hipGetLastError());
 }
 
