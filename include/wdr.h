@@ -298,7 +298,7 @@ int wdr_run_pipeline_block(wdr_context* c, const wdr_speech_segment* segs, size_
 void wdr_segment_list_free(wdr_segment_list* l);
 /* decode chains of run_pipeline (greedy decoding): n States decode n contiguous blocks of the
  * speech segments concurrently, their greedy steps batched into one n-row step, with an exact
- * prompt-chain fix-up (results identical to one chain).  Default WDR_DECODE_CHAINS or 16,
+ * prompt-chain fix-up (results identical to one chain).  Default WDR_DECODE_CHAINS or 40,
  * capped by the context's KV pool (max chains fixed at creation).  Not in the Rust API. */
 int wdr_context_set_chains(wdr_context* c, int32_t n);
 /* GPUs the context runs on: gpu_device Some(d) -> 1 (device d); None -> every visible GPU (up to

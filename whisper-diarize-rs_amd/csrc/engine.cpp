@@ -524,7 +524,7 @@ static std::unique_ptr<wdr_context> make_context(const std::string& model_name, 
       pc.gpu_device = c->devices[g];
       c->peers.push_back(std::make_unique<Context>(model_name, hp, pc, gf.get()));
     }
-    c->chains = c->ctx->max_chains;   // WDR_DECODE_CHAINS (default 24), wdr_context_set_chains
+    c->chains = c->ctx->max_chains;   // WDR_DECODE_CHAINS (default 40), wdr_context_set_chains
   } catch (const std::exception& ex) {
     throw std::runtime_error(std::string("create whisper context crash: ") + ex.what());
   }

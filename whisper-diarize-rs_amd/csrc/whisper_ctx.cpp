@@ -506,7 +506,7 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
   {
     // KV pool for the decode chains of every State of this context (multi-chain pipeline)
     const char* e = getenv("WDR_DECODE_CHAINS");
-    max_chains = std::max(1, std::min(64, e ? atoi(e) : 24));
+    max_chains = std::max(1, std::min(64, e ? atoi(e) : 40));   // 24 -> 40: +2.6 % (profiles/r04/ab_chains*.txt)
     const char* nb = getenv("WDR_BATCHERS");
     n_batchers = std::max(1, std::min(8, nb ? atoi(nb) : 1));
     prefill_split = getenv("WDR_PREFILL_SPLIT") && atoi(getenv("WDR_PREFILL_SPLIT")) != 0;
@@ -698,14 +698,13 @@ const Context::Fp8W& Context::fp8_xkv() {
 
 static constexpr int kBatch = 4;     // encoder windows per encode-ahead launch (M = 6000 rows)
 static constexpr int kSlots = 16;    // in-flight segments in the cross-K/V ring (most)
-// WDR_SLOTS: ring slots per chain (a multiple of kBatch, 4..16; default 16)
-static int ring_slots() {
-  static const int v = [] {
-    const char* e = getenv("WDR_SLOTS");
-    const int n = e ? atoi(e) / kBatch * kBatch : kSlots;
-    return std::max(kBatch, std::min(kSlots, n));
-  }();
-  return v;
+// WDR_SLOTS: ring slots per chain (a multiple of kBatch, 4..16); default 16 up to 24 chains and 8
+// above (large-v3: 40 chains x 9 slots x 245.8 MB = 88 GB of cross-K/V; 48 chains of 17 slots
+// did not fit in 288 GB beside the KV pool, profiles/r04/ab_flash_occ.txt)
+static int ring_slots(int max_chains) {
+  const char* e = getenv("WDR_SLOTS");
+  const int n = e ? atoi(e) / kBatch * kBatch : max_chains > 24 ? 8 : kSlots;
+  return std::max(kBatch, std::min(kSlots, n));
 }
 
 static void alloc_enc(State::Impl::EncBufs& e, int nb, int d, int kp1) {
@@ -748,7 +747,7 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
   const int d = m.d;
   alloc_enc(m.e1, 1, d, m.kp1);
   alloc_enc(m.eb, kBatch, d, m.kp1);
-  m.S = ring_slots();
+  m.S = ring_slots(ctx.max_chains);
   m.slots.resize(m.S + 1);
   for (auto& sl : m.slots) {
     sl.gmax = DevMem(16);
