@@ -172,8 +172,11 @@ struct FatalInit {
 
 constexpr unsigned kStepEvery = 32;   // decode steps run eagerly for sampling: 1 in 32 (was 1 in
                                       // 8: the eager steps cost the 1-h bench ~2 %)
+constexpr unsigned kEncEvery = 8;     // full encode batches run eagerly for sampling: 1 in 8 (a
+                                      // run has ~170 of them: 1 in 32 left 2-8 sampled batches and
+                                      // a class average at the mercy of which)
 thread_local bool t_capture = false;
-thread_local bool t_step = false;   // inside a sampled (eager) decode step
+thread_local unsigned t_rate = 0;   // inside a sampled (eager) step / batch: its launches' rate
 
 // every launch of the class is timed with probability 1 / (kEvery * kStepEvery): 1 in kEvery
 // inside the sampled steps, 1 in kEvery * kStepEvery elsewhere (prefill, language detection),
@@ -191,14 +194,19 @@ static bool pick(unsigned every) {
 bool prof_on(int cls) {
   if (!(g_mask.load(std::memory_order_relaxed) & (1 << cls)) || t_capture) return false;
   if (!on_ring_device()) return false;
-  return pick(t_step ? kEvery : kEvery * kStepEvery);
+  return pick(t_rate ? t_rate : kEvery * kStepEvery);
 }
 bool prof_step() {
   if (!g_mask.load(std::memory_order_relaxed)) return false;
   return pick(kStepEvery);
 }
+bool prof_enc_batch() {
+  if (!g_mask.load(std::memory_order_relaxed)) return false;
+  return pick(kEncEvery);
+}
 void prof_capture(bool on) { t_capture = on; }
-void prof_in_step(bool on) { t_step = on; }
+void prof_in_step(bool on) { t_rate = on ? kEvery : 0; }
+void prof_in_enc(bool on) { t_rate = on ? kEvery * kStepEvery / kEncEvery : 0; }
 int prof_class() { return g_mask.load(); }
 
 std::mutex* launch_lock() {

@@ -16,13 +16,18 @@ enum ProfClass : int { PROF_NONE = 0, PROF_GEMM = 1, PROF_GEMV = 2, PROF_FLASH =
 
 bool prof_on(int cls);
 int prof_class();
-// decode steps replay hipGraphs; while a class is enabled, 1 in kStepEvery steps runs its
-// kernels eagerly instead (events recorded inside a graph cannot be read on this ROCm), and
-// those launches are sampled 1 in kEvery.  prof_capture(true) around a stream capture keeps
-// event launches out of the graph.
+// decode steps and full encode batches replay hipGraphs; while a class is enabled, 1 in
+// kStepEvery steps (prof_step) or 1 in kEncEvery encode batches (prof_enc_batch) runs its kernels
+// eagerly instead (events recorded inside a graph cannot be read on this ROCm), and those launches
+// are sampled at the rate that makes every launch's probability 1 / (kEvery * kStepEvery).  Only
+// work that would otherwise replay a graph draws: work that always runs eagerly (mixed batches,
+// partial encode batches) is sampled at the base rate, or it would be over-represented.
+// prof_capture(true) around a stream capture keeps event launches out of the graph.
 bool prof_step();
+bool prof_enc_batch();
 void prof_capture(bool on);
-void prof_in_step(bool on);   // around the eager launches of a step prof_step() picked
+void prof_in_step(bool on);    // around the eager launches of a step prof_step() picked
+void prof_in_enc(bool on);     // around the eager launches of a batch prof_enc_batch() picked
 hipEvent_t prof_event();
 // frees the kernel-clock ring and the pooled events (wdr_shutdown)
 void prof_shutdown();

@@ -1305,10 +1305,12 @@ bool State::top_up_batch(int j) {
     } el_t{t_el, m.t_enc_launch};
     static const bool enc_graph = !(getenv("WDR_ENC_GRAPH") && atoi(getenv("WDR_ENC_GRAPH")) == 0);
     // the live profiler (bench.py's roofline) samples eager launches only: while it is on, 1 in
-    // kStepEvery batches runs eagerly with its launches sampled 1 in kEvery (prof.h), the rate
-    // decode steps are sampled at -- a uniform sample of the encoder GEMMs
-    const bool sampled = prof_step();
-    if (enc_graph && g1 - g0 == kBatch && !no_graph() && !sampled) {
+    // kEncEvery graphable batches runs eagerly with its launches sampled at the matching rate
+    // (prof.h); partial batches, always eager, are sampled at the base rate -- a uniform sample
+    // of the encoder GEMMs
+    const bool graphable = enc_graph && g1 - g0 == kBatch && !no_graph();
+    const bool sampled = graphable && prof_enc_batch();
+    if (graphable && !sampled) {
       const bool f8 = ctx_.fp8_encoder.load();
       const int key = slot0 * 4 + (f8 ? 2 : 0) + (m.plan.detect_lang ? 1 : 0);   // the batch's slots
       Impl::EncGraph& eg = m.enc_graphs[key];
@@ -1345,14 +1347,14 @@ bool State::top_up_batch(int j) {
       if (mu) mu->unlock();
       WDR_HIP(ge);
     } else {
-      prof_in_step(sampled);
+      prof_in_enc(sampled);
       try {
         body(*m.tlb, false, m.es);
       } catch (...) {
-        prof_in_step(false);
+        prof_in_enc(false);
         throw;
       }
-      prof_in_step(false);
+      prof_in_enc(false);
     }
     for (int k = g0; k < g1; ++k) WDR_HIP(hipEventRecord(m.slots[k % m.S].ready, m.es));
     {
@@ -1458,7 +1460,7 @@ void State::step_and_sample(const int* toks, const int* seqs, const int* pos, co
                             TokenData* out, int K, BeamCand* cands) {
   Impl& m = *m_;
   WDR_CHECK(R >= 1 && R <= NSEQ, "decoder step: row count out of range");
-  const bool sampled = prof_step();
+  const bool sampled = !no_graph() && prof_step();
   if (sampled || no_graph()) {
     // live per-kernel HIP-event timing cannot read events recorded inside a graph on this
     // ROCm: a sampled step runs the same kernels eagerly (prof.h)
@@ -2982,8 +2984,10 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
     }
   };
   const double t_step = now_s();
-  const bool sampled = prof_step();
   const bool decode_only = n_pre == 0 && n_dtw == 0;
+  // only a batch that would replay a graph draws an eager sampled run (prof.h): mixed batches
+  // always run eagerly and are sampled at the base rate
+  const bool sampled = decode_only && !no_graph() && prof_step();
   static FILE* blog = getenv("WDR_BATCH_LOG") ? fopen(getenv("WDR_BATCH_LOG"), "w") : nullptr;
   if (blog) WDR_HIP(hipEventRecord(m.ev0, m.s));
   if (sampled || no_graph() || !decode_only) {
