@@ -2757,8 +2757,9 @@ struct StepBatcher::Impl {
   double t_free = 0;              // when the last batch's results were handed out
   double t_first = 0;             // when the oldest pending request arrived
   // WDR_BATCH_WAIT_US (read when the batcher is made): how long a batch may wait for stragglers
-  // once the GPU is free (default 300 us; negative: wait for every chain, the round-3 rule)
-  double wait_s = 300e-6;
+  // once the GPU is free (default 1000 us: at 40 chains 300 / 600 / 1000 us gave 744 / 755 / 758
+  // xRT, profiles/r04/ab_wait40.txt; negative: wait for every chain, the round-3 rule)
+  double wait_s = 1000e-6;
   hipStream_t s = nullptr;
   int d = 0, V = 0, H = 0;
   int RB = 0, LB = 0;             // row / logit-row capacity of one launch
