@@ -43,7 +43,7 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_F16_PEAK_TFS = 2500.0  # dense f16/bf16 MFMA
 MFMA_FP8_PEAK_TFS = 5000.0  # dense block-scaled fp8 MFMA (MI355X_MICROARCH.md, matrix cores)
 PROF_EVERY, PROF_STEP_EVERY = 2, 32   # csrc/prof.cpp kEvery (launches in a sampled step), kStepEvery
-PROF_ENC_EVERY = 8   # csrc/prof.cpp kEncEvery (encode batches run eagerly for sampling)
+PROF_ENC_EVERY = 32   # csrc/prof.cpp kEncEvery (encode batches run eagerly for sampling)
 
 
 def parse():
@@ -601,7 +601,7 @@ def main():
             r["traffic"] = round(tr)
             r["traffic_source"] = src
         # csrc/prof.h: decode-only steps and full encode batches replay hipGraphs; 1 in 32 such
-        # steps (1 in 8 such batches) runs eagerly with 1 in 2 (1 in 8) of its launches clocked;
+        # steps (1 in 32 such batches) runs eagerly with 1 in 2 of its launches clocked;
         # always-eager launches (mixed / prefill / DTW batches, partial encode batches) are
         # clocked 1 in 64 -- every launch with probability 1 / 64
         r["sampling"] = ("1 in %d launches (graph-replayed work: decode steps 1 in %d eager, 1 in %d of "

@@ -172,9 +172,10 @@ struct FatalInit {
 
 constexpr unsigned kStepEvery = 32;   // decode steps run eagerly for sampling: 1 in 32 (was 1 in
                                       // 8: the eager steps cost the 1-h bench ~2 %)
-constexpr unsigned kEncEvery = 8;     // full encode batches run eagerly for sampling: 1 in 8 (a
-                                      // run has ~170 of them: 1 in 32 left 2-8 sampled batches and
-                                      // a class average at the mercy of which)
+constexpr unsigned kEncEvery = 32;    // full encode batches run eagerly for sampling: 1 in 32 (1 in
+                                      // 8 cost the profiled 1-h run 2-5 %: an eager batch holds its
+                                      // chain's thread ~1 ms, fragmenting the batched steps --
+                                      // profiles/r04/ab_prof_cost.txt)
 thread_local bool t_capture = false;
 thread_local unsigned t_rate = 0;   // inside a sampled (eager) step / batch: its launches' rate
 
