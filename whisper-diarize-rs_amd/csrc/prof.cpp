@@ -176,6 +176,16 @@ constexpr unsigned kEncEvery = 32;    // full encode batches run eagerly for sam
                                       // 8 cost the profiled 1-h run 2-5 %: an eager batch holds its
                                       // chain's thread ~1 ms, fragmenting the batched steps --
                                       // profiles/r04/ab_prof_cost.txt)
+// WDR_PROF_STEP_EVERY (A/B of the profiler's cost): decode steps run eagerly 1 in 16 / 32 / 64,
+// their launches clocked at the rate that keeps every launch's probability 1 / (kEvery * kStepEvery)
+static unsigned step_every() {
+  static const unsigned v = [] {
+    const char* e = getenv("WDR_PROF_STEP_EVERY");
+    const unsigned n = e ? (unsigned)atoi(e) : kStepEvery;
+    return n == 16 || n == 64 ? n : kStepEvery;
+  }();
+  return v;
+}
 thread_local bool t_capture = false;
 thread_local unsigned t_rate = 0;   // inside a sampled (eager) step / batch: its launches' rate
 
@@ -199,14 +209,14 @@ bool prof_on(int cls) {
 }
 bool prof_step() {
   if (!g_mask.load(std::memory_order_relaxed)) return false;
-  return pick(kStepEvery);
+  return pick(step_every());
 }
 bool prof_enc_batch() {
   if (!g_mask.load(std::memory_order_relaxed)) return false;
   return pick(kEncEvery);
 }
 void prof_capture(bool on) { t_capture = on; }
-void prof_in_step(bool on) { t_rate = on ? kEvery : 0; }
+void prof_in_step(bool on) { t_rate = on ? kEvery * kStepEvery / step_every() : 0; }
 void prof_in_enc(bool on) { t_rate = on ? kEvery * kStepEvery / kEncEvery : 0; }
 int prof_class() { return g_mask.load(); }
 
