@@ -42,7 +42,7 @@ sys.path.insert(0, os.path.join(ROOT, "whisper-diarize-rs_amd"))
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_F16_PEAK_TFS = 2500.0  # dense f16/bf16 MFMA
 MFMA_FP8_PEAK_TFS = 5000.0  # dense block-scaled fp8 MFMA (MI355X_MICROARCH.md, matrix cores)
-PROF_EVERY, PROF_STEP_EVERY = 2, 32   # csrc/prof.cpp kEvery (launches in a sampled step), kStepEvery
+PROF_EVERY, PROF_STEP_EVERY = 1, 64   # launches clocked in a sampled decode step, 1 in 64 steps sampled (csrc/prof.cpp step_every)
 PROF_ENC_EVERY = 32   # csrc/prof.cpp kEncEvery (encode batches run eagerly for sampling)
 
 
@@ -600,8 +600,8 @@ def main():
         if tr is not None:
             r["traffic"] = round(tr)
             r["traffic_source"] = src
-        # csrc/prof.h: decode-only steps and full encode batches replay hipGraphs; 1 in 32 such
-        # steps (1 in 32 such batches) runs eagerly with 1 in 2 of its launches clocked;
+        # csrc/prof.h: decode-only steps and full encode batches replay hipGraphs; 1 in 64 such
+        # steps (1 in 32 such batches) runs eagerly with every (1 in 2) of its launches clocked;
         # always-eager launches (mixed / prefill / DTW batches, partial encode batches) are
         # clocked 1 in 64 -- every launch with probability 1 / 64
         r["sampling"] = ("1 in %d launches (graph-replayed work: decode steps 1 in %d eager, 1 in %d of "

@@ -176,13 +176,15 @@ constexpr unsigned kEncEvery = 32;    // full encode batches run eagerly for sam
                                       // 8 cost the profiled 1-h run 2-5 %: an eager batch holds its
                                       // chain's thread ~1 ms, fragmenting the batched steps --
                                       // profiles/r04/ab_prof_cost.txt)
-// WDR_PROF_STEP_EVERY (A/B of the profiler's cost): decode steps run eagerly 1 in 16 / 32 / 64,
-// their launches clocked at the rate that keeps every launch's probability 1 / (kEvery * kStepEvery)
+// WDR_PROF_STEP_EVERY (A/B of the profiler's cost): decode steps run eagerly 1 in 16 / 32 / 64
+// (default 64, every launch of such a step clocked: 1 in 32 with 1 in 2 clocked cost the profiled
+// 1-h run ~3 % against ~1.6 %, profiles/r04/ab_prof_cost.txt), their launches clocked at the rate
+// that keeps every launch's probability 1 / (kEvery * kStepEvery)
 static unsigned step_every() {
   static const unsigned v = [] {
     const char* e = getenv("WDR_PROF_STEP_EVERY");
-    const unsigned n = e ? (unsigned)atoi(e) : kStepEvery;
-    return n == 16 || n == 64 ? n : kStepEvery;
+    const unsigned n = e ? (unsigned)atoi(e) : 64;
+    return n == 16 || n == 32 ? n : 64;
   }();
   return v;
 }
