@@ -178,7 +178,10 @@ int wdr_device_count(void);
 /* ABI 5: releases every handle the caller has not freed (engines, contexts with their worker
  * threads, VADs, diarizers, speaker managers) and the process-wide stream pools / profiler
  * buffers, while the HIP runtime is still up.  Registered with atexit() when the first handle is
- * created; a host may call it earlier.  Freeing a handle it released is a no-op. */
+ * created; a host may call it earlier.  Freeing a handle it released is a no-op.  A handle that
+ * an entry point is still using on another thread (a call in flight) is not released; every entry
+ * point rejects a released handle with an error, and a released handle's address is never
+ * reused by a later one. */
 void wdr_shutdown(void);
 
 /* ---- Engine (whole-call drop-in) ---- */

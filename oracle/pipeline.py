@@ -214,10 +214,14 @@ def setup_params(options: dict) -> FullParams:
     return p
 
 
-def run_transcription_pipeline(state: WhisperState, speech_segments, options: dict, raw: bool = False):
-    """src/transcribe.rs:323-535 without diarization.  Returns (segments, detected_lang).
+def run_transcription_pipeline(state: WhisperState, speech_segments, options: dict, raw: bool = False,
+                               speaker_of=None):
+    """src/transcribe.rs:323-535.  Returns (segments, detected_lang).
     raw: no overlap clip against the next segment; returns (results grouped per speech
-    segment, detected_lang) -- the form wdr_run_pipeline_raw / the multi-GPU merge use."""
+    segment, detected_lang) -- the form wdr_run_pipeline_raw / the multi-GPU merge use.
+    speaker_of(i): diarization (src/transcribe.rs:461-497) -- called once per whisper segment of
+    speech segment i, in order (the reference recomputes the embedding of the speech segment's
+    samples for every whisper segment and assigns it through the EmbeddingManager)."""
     vocab = state.v
     params = setup_params(options)
     user_offset = options.get("offset") or 0.0
@@ -260,7 +264,8 @@ def run_transcription_pipeline(state: WhisperState, speech_segments, options: di
                     if last.words[-1].end > last.end:
                         last.words[-1].end = last.end
             previous_text = text if text.strip() else None
-            segments.append(Segment(seg_start, seg_end, text, words or None, None))
+            spk = speaker_of(i) if speaker_of is not None else None
+            segments.append(Segment(seg_start, seg_end, text, words or None, spk))
             groups[-1].append(segments[-1])
     if raw:
         return groups, detected_lang

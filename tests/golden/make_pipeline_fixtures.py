@@ -18,8 +18,11 @@ so anchors flip on f32 rounding alone; trained alignment heads are peaked, as at
   c2_base_en_600s.json   configs[1]: base.en, 600 s (its full size), Silero VAD, DTW, beam 5,
                          lang auto, fallback off (synthetic decode-length pin)
   c3_large_v3_120s.json  configs[2]: large-v3, 120 s, VAD, DTW, greedy, lang auto, fallback off
+  c3_large_v3_900s.json  configs[2] at a real size: 900 s, 35 VAD segments,
+                         ~50 windows, same options
+  c4_large_v3_diarize_300s.json  configs[3] diarized on the bench's weights (DIAR below)
 
-Usage:  python tests/golden/make_pipeline_fixtures.py [c1|c2|c3 ...]
+Usage:  python tests/golden/make_pipeline_fixtures.py [c1|c2|c3|c3l|c4d ...]
 """
 from __future__ import annotations
 
@@ -46,12 +49,77 @@ CONFIGS = {
                fallback=False),
     "c3": dict(file="c3_large_v3_120s.json", model="large-v3", seconds=120.0, seed=52, vad=True, greedy=True,
                fallback=False),
+    "c3l": dict(file="c3_large_v3_900s.json", model="large-v3", seconds=900.0, seed=52, vad=True, greedy=True,
+                fallback=False),
 }
+
+# configs[3] (C4) diarized, on the BENCH's own weights (N(0, 0.02), embeddings N(0, 0.02): the
+# weights bench.py measures) and the bench's segmentation pin (SURVEY §8(d):
+# in synthetic mode the segment list passed downstream is the generator's ground-truth spurt
+# table; the pyannote kernels are compared with the oracle in tests/test_gpu_diarize.py):
+# large-v3, 300 s, 3 speakers, seed 1, greedy, lang auto, DTW, speaker assignment with
+# max_speakers 3.  The synthetic CAM++ puts every embedding within cosine 0.9997-1.0 of every
+# other (random weights, ReLU stats pooling), so the default threshold 0.5 makes everyone
+# speaker "1"; 0.9999 separates the three synthetic voices (F0 110 / 140 / 190 Hz) on 48 of 54
+# spurts, and the fixture records each assignment's decision margin.
+DIAR = dict(file="c4_large_v3_diarize_300s.json", model="large-v3", seconds=300.0, seed=1, n_speakers=3,
+            weight_std=0.02, emb_std=0.02, max_speakers=3, threshold=0.9999)
 
 
 def _seg(s):
     return dict(start=s.start, end=s.end, text=s.text,
                 words=None if s.words is None else [[w.text, w.start, w.end] for w in s.words])
+
+
+def make_diarized():
+    from oracle import diarize as D
+    from oracle.model import Whisper
+    from oracle.pipeline import SpeechSegment as OSeg
+    from oracle.pipeline import run_transcription_pipeline
+    from oracle.vocab import Vocab
+    from oracle.weights import hparams_for, synth_weights
+    from oracle.whisper_full import WhisperState
+    from wdr.synth import synth_speech
+
+    c = DIAR
+    t0 = time.time()
+    pcm, spurts = synth_speech(c["seconds"], seed=c["seed"], n_speakers=c["n_speakers"])
+    segs = [OSeg(a, b, pcm[int(round(a * 16000)):int(round(b * 16000))]) for a, b, _ in spurts]
+    W = D.cam_weights()
+    embs = [D.compute_embedding(s.samples, W) for s in segs]
+    mgr = D.EmbeddingManager(c["max_speakers"])
+    margins = []
+
+    def speaker_of(i):
+        e = embs[i]
+        if e is not None and mgr.speakers:
+            sims = sorted((float(D.EmbeddingManager.cosine(e, v)) for v in mgr.speakers.values()), reverse=True)
+            full = len(mgr.speakers) == mgr.max_speakers
+            # distance of the decision from flipping: best vs runner-up, and (search) best vs threshold
+            m = sims[0] - sims[1] if len(sims) > 1 else np.inf
+            if not full:
+                m = min(m, abs(sims[0] - c["threshold"]))
+            margins.append(m)
+        else:
+            margins.append(None)
+        return mgr.assign(e, c["threshold"])
+
+    hp = hparams_for(c["model"])
+    st = WhisperState(Whisper(hp, synth_weights(hp, std=c["weight_std"], emb_std=c["emb_std"])),
+                      Vocab(hp.n_vocab), c["model"])
+    o = dict(lang="auto", advanced=dict(sampling_strategy="greedy"),
+             synthetic=dict(force_len_rate=FORCE_LEN, logprob_thold=-np.inf, entropy_thold=-1.0))
+    raw, lang = run_transcription_pipeline(st, segs, o, speaker_of=speaker_of)
+    out = dict(config=dict(c, force_len_rate=FORCE_LEN, lang="auto", greedy=True, fallback=False,
+                           segmentation="ground-truth spurts"),
+               spurts=[[a, b, k] for a, b, k in spurts], lang=lang,
+               raw=[dict(_seg(s), speaker_id=s.speaker_id) for s in raw],
+               speaker_margins=[None if m is None or not np.isfinite(m) else m for m in margins],
+               oracle_seconds=round(time.time() - t0, 1))
+    with open(os.path.join(HERE, c["file"]), "w") as f:
+        json.dump(out, f, indent=0)
+    print("c4d", c["file"], "segments", len(raw), "speakers", "".join(s.speaker_id for s in raw),
+          "s", out["oracle_seconds"], flush=True)
 
 
 def make(key):
@@ -97,5 +165,5 @@ def make(key):
 
 
 if __name__ == "__main__":
-    for k in (sys.argv[1:] or list(CONFIGS)):
-        make(k)
+    for k in (sys.argv[1:] or list(CONFIGS) + ["c4d"]):
+        make_diarized() if k == "c4d" else make(k)

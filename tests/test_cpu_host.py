@@ -177,3 +177,34 @@ def test_ggml_info_rejects_bad_files(tmp_path, kind, msg):
         p = str(tmp_path / "absent.bin")
     with pytest.raises(wdr.WdrError, match=msg):
         wdr.ggml_info(p)
+
+
+def test_shutdown_releases_handles_and_stale_calls_fail():
+    """wdr_shutdown: a released handle is rejected by every entry point, freeing it is
+    a no-op, and a handle created afterwards is a fresh one.  Run in a child process: shutdown
+    releases every handle of the process."""
+    import subprocess
+    import sys
+    code = r'''
+import ctypes as C
+from wdr import _lib as L
+lib = L.load()
+h = C.c_void_p()
+assert lib.wdr_speakers_new(0, 0, C.byref(h)) == 0
+emb = (C.c_float * 4)(1, 0, 0, 0)
+buf = C.create_string_buffer(16)
+assert lib.wdr_speakers_assign(h, emb, 4, 0.5, buf, 16) == 0 and buf.value == b"1"
+lib.wdr_shutdown()
+assert lib.wdr_speakers_assign(h, emb, 4, 0.5, buf, 16) != 0
+assert b"released" in lib.wdr_last_error()
+lib.wdr_speakers_free(h)          # no-op on a released handle
+h2 = C.c_void_p()
+assert lib.wdr_speakers_new(0, 0, C.byref(h2)) == 0 and h2.value != h.value
+assert lib.wdr_speakers_assign(h2, emb, 4, 0.5, buf, 16) == 0 and buf.value == b"1"
+lib.wdr_speakers_free(h2)
+print("ok")
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([os.path.join(root, "whisper-diarize-rs_amd"), root]))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, (r.stdout, r.stderr)

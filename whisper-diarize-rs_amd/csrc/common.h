@@ -127,7 +127,11 @@ struct ProjArgs {
 // start, latest wave end} in wall_clock64() ticks (the constant-rate clock), i.e. the span
 // rocprofv3's dispatch timestamps measure, free of the queueing that HIP start/stop events of a
 // launch absorb under multi-stream concurrency.  Thread 0 of every workgroup stamps the start
-// when its wave starts and the end when its wave retires -- two vector atomics per workgroup,
+// when its wave (the first dispatched) starts, and lane 0 of the workgroup's LAST wave stamps the
+// end when that wave retires -- the wave that finishes last in the multi-wave kernels (k_gemm4 /
+// k_gemm5 run waves 4-7 one barrier behind waves 0-3; the k_skinny / flash / cross-attention
+// waves end together after their final barrier), so the span is the workgroup's, not wave 0's
+//  -- two vector atomics per workgroup,
 // spread over PROF_CLK_LANES words (one stamp per wave, on 32 words, serialised at L2 on the
 // 11 520-workgroup cross-attention launches and inflated their spans ~3x against the trace);
 // unsampled launches (ts null) skip it.
@@ -138,7 +142,7 @@ struct ProfClock {
     if (ts && threadIdx.x == 0) atomicMin(ts + lane_of_block(), (unsigned long long)wall_clock64());
   }
   __device__ __forceinline__ ~ProfClock() {
-    if (ts && threadIdx.x == 0) atomicMax(ts + PROF_CLK_LANES + lane_of_block(), (unsigned long long)wall_clock64());
+    if (ts && threadIdx.x == ((blockDim.x - 1) & ~63u)) atomicMax(ts + PROF_CLK_LANES + lane_of_block(), (unsigned long long)wall_clock64());
   }
   __device__ __forceinline__ static int lane_of_block() {
     return (int)((blockIdx.x + blockIdx.y * 7u + blockIdx.z * 13u) % PROF_CLK_LANES);

@@ -1280,15 +1280,41 @@ static int diar_segments_out(const std::vector<DiarSegment>& ds, const int16_t* 
 // threads (DTW queue, encode-ahead, step batchers), streams, device memory -- while the HIP
 // runtime is still up.  A free of a handle that is no longer registered (freed already, or
 // released by wdr_shutdown) does nothing.
+// Calls in flight: every entry point that takes a handle holds it (InUse) for the call's
+// duration; wdr_shutdown releases only handles no call holds -- a host thread still inside
+// wdr_run_pipeline when exit() runs the hook keeps its context -- and releases a handle by
+// destroying its contents in place without returning the allocation, so a later handle can never
+// reuse the address of a released one and a stale free of it stays a no-op.
 namespace {
 struct Live {
   std::mutex mu;
   std::set<void*> eng, ctx, vad, dia, spk;
+  std::map<const void*, int> busy;   // handle -> entry-point calls in flight
 };
 Live& live() {
   static Live* l = new Live();   // never destroyed: the exit hook and late frees may run after statics
   return *l;
 }
+// an entry point's hold on a handle; a handle that is not (or no longer) registered is an error
+struct InUse {
+  const void* p = nullptr;
+  InUse(std::set<void*> Live::*set, const void* h) {
+    if (!h) throw std::runtime_error("null handle");
+    std::lock_guard<std::mutex> g(live().mu);
+    if (!(live().*set).count(const_cast<void*>(h))) throw std::runtime_error("handle was freed or released by wdr_shutdown");
+    ++live().busy[h];
+    p = h;
+  }
+  ~InUse() {
+    if (!p) return;
+    std::lock_guard<std::mutex> g(live().mu);
+    auto it = live().busy.find(p);
+    if (it != live().busy.end() && --it->second == 0) live().busy.erase(it);
+  }
+  InUse(const InUse&) = delete;
+  InUse& operator=(const InUse&) = delete;
+};
+#define WDR_USE(SET, H) InUse wdr_in_use_(&Live::SET, (H))
 void wdr_exit_hook() { wdr_shutdown(); }
 template <typename T>
 T* track(std::set<void*> Live::*set, T* p) {
@@ -1312,20 +1338,36 @@ extern "C" {
 
 void wdr_shutdown(void) {
   std::set<void*> eng, ctx, vad, dia, spk;
+  bool any_busy = false;
   {
     std::lock_guard<std::mutex> g(live().mu);
-    eng.swap(live().eng);
-    ctx.swap(live().ctx);
-    vad.swap(live().vad);
-    dia.swap(live().dia);
-    spk.swap(live().spk);
+    Live& L = live();
+    // take the handles no call holds; a held one stays registered (its owner frees it later)
+    auto take = [&](std::set<void*>& from, std::set<void*>& to) {
+      for (auto it = from.begin(); it != from.end();) {
+        if (L.busy.count(*it)) {
+          any_busy = true;
+          ++it;
+        } else {
+          to.insert(*it);
+          it = from.erase(it);
+        }
+      }
+    };
+    take(L.eng, eng);
+    take(L.ctx, ctx);
+    take(L.vad, vad);
+    take(L.dia, dia);
+    take(L.spk, spk);
   }
-  // engines own their cached contexts; contexts join their threads and free their device memory
-  for (void* p : eng) delete (wdr_engine*)p;
-  for (void* p : ctx) delete (wdr_context*)p;
-  for (void* p : vad) delete (wdr_vad*)p;
-  for (void* p : dia) delete (wdr_diarizer*)p;
-  for (void* p : spk) delete (wdr_speakers*)p;
+  // engines own their cached contexts; contexts join their threads and free their device memory.
+  // Destroyed in place, the allocation kept: no later handle reuses a released address.
+  for (void* p : eng) ((wdr_engine*)p)->~wdr_engine();
+  for (void* p : ctx) ((wdr_context*)p)->~wdr_context();
+  for (void* p : vad) ((wdr_vad*)p)->~wdr_vad();
+  for (void* p : dia) ((wdr_diarizer*)p)->~wdr_diarizer();
+  for (void* p : spk) ((wdr_speakers*)p)->~wdr_speakers();
+  if (any_busy) return;   // the stream pools / profiler serve the calls still running
   destroy_stream_pools();
   prof_shutdown();
 }
@@ -1365,6 +1407,7 @@ void wdr_engine_free(wdr_engine* e) {
 
 int wdr_engine_set_synthetic(wdr_engine* e, const wdr_synthetic* syn) {
   WDR_GUARD({
+    WDR_USE(eng, e);
     e->syn = syn_of(syn);
     e->syn_set = true;
     e->contexts.clear();
@@ -1375,6 +1418,7 @@ int wdr_engine_set_synthetic(wdr_engine* e, const wdr_synthetic* syn) {
 int wdr_transcribe_audio(wdr_engine* e, const char* audio_path, const wdr_transcribe_options* o,
                          const wdr_formatting_overrides* fmt, const wdr_callbacks* cb, wdr_segment_list** out) {
   WDR_GUARD({
+    WDR_USE(eng, e);
     if (!audio_path || !file_exists(audio_path)) return fail("audio file doesn't exist");
     const std::string model = (o && o->model) ? o->model : "base";
     // ModelManager::ensure_whisper_model (src/engine.rs:78-81): the cached ggml file, offline.
@@ -1475,6 +1519,7 @@ void wdr_vad_free(wdr_vad* v) {
 
 int wdr_vad_probs(wdr_vad* v, const int16_t* samples, size_t n, float* probs_out, double* us_per_step) {
   WDR_GUARD({
+    WDR_USE(vad, v);
     const std::vector<float> p = v->m->probs(samples, n);
     if (!p.empty()) memcpy(probs_out, p.data(), p.size() * 4);
     if (us_per_step) *us_per_step = v->m->last_scan_us_per_step;
@@ -1484,6 +1529,7 @@ int wdr_vad_probs(wdr_vad* v, const int16_t* samples, size_t n, float* probs_out
 
 int wdr_vad_stats(wdr_vad* v, double* us_per_chunk) {
   WDR_GUARD({
+    WDR_USE(vad, v);
     *us_per_chunk = v->m->last_scan_us_per_step;
     return 0;
   })
@@ -1505,6 +1551,7 @@ int wdr_vad_segments_from_probs(const float* probs, size_t n_probs, float* cs_ou
 int wdr_vad_get_segments(wdr_vad* v, const int16_t* samples, size_t n, double** mask_out, size_t* n_mask,
                          wdr_speech_segment** segs_out, size_t* n_segs) {
   WDR_GUARD({
+    WDR_USE(vad, v);
     std::vector<std::pair<double, double>> mask;
     std::vector<wdr_speech_segment> segs;
     vad_get_segments(*v->m, samples, n, &mask, &segs);
@@ -1544,6 +1591,7 @@ void wdr_diarizer_free(wdr_diarizer* d) {
 
 int wdr_diarize_frame_classes(wdr_diarizer* d, const int16_t* samples, size_t n, int32_t* cls_out, float* logprobs_out) {
   WDR_GUARD({
+    WDR_USE(dia, d);
     std::vector<float> lp;
     const std::vector<int> cls = d->S().frame_classes(samples, n, logprobs_out ? &lp : nullptr);
     for (size_t i = 0; i < cls.size(); ++i) cls_out[i] = cls[i];
@@ -1568,6 +1616,7 @@ int wdr_diarize_segments_from_classes(const int32_t* cls, size_t n_windows, cons
 
 int wdr_diarize_fbank(wdr_diarizer* d, const int16_t* samples, size_t n, float* feats_out, size_t* n_frames) {
   WDR_GUARD({
+    WDR_USE(dia, d);
     const std::vector<float> f = d->E().feats(samples, n);
     if (!f.empty()) memcpy(feats_out, f.data(), f.size() * 4);
     *n_frames = f.size() / 80;
@@ -1577,6 +1626,7 @@ int wdr_diarize_fbank(wdr_diarizer* d, const int16_t* samples, size_t n, float* 
 
 int wdr_diarize_embedding(wdr_diarizer* d, const int16_t* samples, size_t n, float* emb_out, int8_t* ok) {
   WDR_GUARD({
+    WDR_USE(dia, d);
     *ok = d->E().embed(samples, n, emb_out) ? 1 : 0;
     return 0;
   })
@@ -1585,6 +1635,7 @@ int wdr_diarize_embedding(wdr_diarizer* d, const int16_t* samples, size_t n, flo
 int wdr_diarize_embedding_batch(wdr_diarizer* d, const int16_t* const* samples, const size_t* n, int32_t B,
                                 float* emb_out, int8_t* ok) {
   WDR_GUARD({
+    WDR_USE(dia, d);
     if (B < 0) return fail("embedding batch: negative count");
     std::vector<char> k(B);
     if (B) d->E().embed_batch(samples, n, B, emb_out, k.data());
@@ -1595,6 +1646,7 @@ int wdr_diarize_embedding_batch(wdr_diarizer* d, const int16_t* const* samples, 
 
 int wdr_diarize_stats(wdr_diarizer* d, double* seg_ms, double* emb_ms) {
   WDR_GUARD({
+    WDR_USE(dia, d);
     *seg_ms = d->seg ? d->seg->last_ms : 0.0;
     *emb_ms = d->cam ? d->cam->last_ms : 0.0;
     return 0;
@@ -1616,6 +1668,7 @@ void wdr_speakers_free(wdr_speakers* m) {
 
 int wdr_speakers_assign(wdr_speakers* m, const float* emb, int32_t dim, float threshold, char* id_out, size_t cap) {
   WDR_GUARD({
+    WDR_USE(spk, m);
     const std::string id = m->m->assign(emb, dim, threshold);
     WDR_CHECK(cap > id.size(), "speaker id buffer too small");
     memcpy(id_out, id.c_str(), id.size() + 1);
@@ -1776,6 +1829,7 @@ int wdr_run_pipeline(wdr_context* c, const wdr_speech_segment* segs, size_t n_se
                      const wdr_diarize_options* dopts, const wdr_synthetic* syn, const wdr_callbacks* cb,
                      wdr_segment_list** out) {
   WDR_GUARD({
+    WDR_USE(ctx, c);
     std::vector<wdr_speech_segment> v(segs, segs + n_segs);
     std::string lang;
     bool has_lang = false;
@@ -1792,6 +1846,7 @@ int wdr_run_pipeline(wdr_context* c, const wdr_speech_segment* segs, size_t n_se
 int wdr_run_pipeline_raw(wdr_context* c, const wdr_speech_segment* segs, size_t n_segs,
                          const wdr_transcribe_options* o, const wdr_synthetic* syn, wdr_segment_list** out) {
   WDR_GUARD({
+    WDR_USE(ctx, c);
     std::vector<wdr_speech_segment> v(segs, segs + n_segs);
     std::string lang;
     bool has_lang = false;
@@ -1810,6 +1865,7 @@ int wdr_run_pipeline_block(wdr_context* c, const wdr_speech_segment* segs, size_
                            const wdr_transcribe_options* o, const wdr_synthetic* syn, const char* rng_in,
                            int8_t* sampled_out, char** rng_out, wdr_segment_list** out) {
   WDR_GUARD({
+    WDR_USE(ctx, c);
     std::vector<wdr_speech_segment> v(segs, segs + n_segs);
     std::string lang;
     bool has_lang = false;
@@ -1845,6 +1901,7 @@ void wdr_segment_list_free(wdr_segment_list* l) {
 
 int wdr_dbg_set_early_fixup(wdr_context* c, int32_t mode) {
   WDR_GUARD({
+    WDR_USE(ctx, c);
     if (mode < -1 || mode > 2) return fail("early fix-up mode: -1 (env default), 0, 1 or 2");
     c->early_fixup = mode;
     return 0;
@@ -1860,6 +1917,7 @@ int wdr_dbg_set_gemm32(int32_t mfma) {
 
 int wdr_context_set_encoder_fp8(wdr_context* c, int8_t on) {
   WDR_GUARD({
+    WDR_USE(ctx, c);
     c->ctx->fp8_encoder = on != 0;
     for (auto& p : c->peers) p->fp8_encoder = on != 0;
     return 0;
@@ -1868,6 +1926,7 @@ int wdr_context_set_encoder_fp8(wdr_context* c, int8_t on) {
 
 int wdr_context_devices(const wdr_context* c, int32_t* n, int32_t* device_ids, int32_t cap) {
   WDR_GUARD({
+    WDR_USE(ctx, c);
     *n = (int32_t)c->devices.size();
     for (int32_t i = 0; device_ids && i < cap && i < *n; ++i) device_ids[i] = c->devices[i];
     return 0;
@@ -1876,6 +1935,7 @@ int wdr_context_devices(const wdr_context* c, int32_t* n, int32_t* device_ids, i
 
 int wdr_context_set_chains(wdr_context* c, int32_t n) {
   WDR_GUARD({
+    WDR_USE(ctx, c);
     if (n < 1) return fail("decode chains: need >= 1");
     c->chains = std::min<int>(n, c->ctx->max_chains);
     return 0;
@@ -1884,6 +1944,7 @@ int wdr_context_set_chains(wdr_context* c, int32_t n) {
 
 int wdr_context_stage_times(wdr_context* c, wdr_stage_times* o) {
   WDR_GUARD({
+    WDR_USE(ctx, c);
     const StageTimes& t = c->st->times;
     *o = wdr_stage_times{t.mel,          t.encode,   t.decode,  t.dtw,        0.0,  t.glue, t.windows,
                          t.decode_steps, t.prefills, t.lang,    t.prompt_gpu, c->embed_s};
@@ -1914,6 +1975,7 @@ int wdr_context_stage_times(wdr_context* c, wdr_stage_times* o) {
 
 int wdr_context_hparams(wdr_context* c, int32_t* o) {
   WDR_GUARD({
+    WDR_USE(ctx, c);
     const HParams& h = c->ctx->model.hp;
     const int32_t v[10] = {h.n_vocab, h.n_audio_ctx, h.n_audio_state, h.n_audio_head, h.n_audio_layer,
                            h.n_text_ctx, h.n_text_state, h.n_text_head, h.n_text_layer, h.n_mels};
@@ -1926,6 +1988,7 @@ int wdr_state_full(wdr_context* c, const float* samples, size_t n, const wdr_tra
                    const wdr_synthetic* syn, const char* initial_prompt, wdr_result_seg** segs, size_t* n_segs,
                    int32_t* lang_id) {
   WDR_GUARD({
+    WDR_USE(ctx, c);
     FullParams p = setup_params(o, syn_of(syn));
     if (initial_prompt) {
       p.initial_prompt = initial_prompt;
@@ -1964,6 +2027,7 @@ void wdr_result_free(wdr_result_seg* segs, size_t n) {
 
 int wdr_dbg_log_mel(wdr_context* c, const float* x, size_t n, int32_t seek, float* out) {
   WDR_GUARD({
+    WDR_USE(ctx, c);
     c->st->compute_mel(x, (int)n);
     c->st->read_mel_window(seek, out);
     return 0;
@@ -1982,6 +2046,7 @@ int wdr_dbg_energy(const float* x, size_t n, float* out) {
 
 int wdr_dbg_encode(wdr_context* c, const float* mel_window, float* enc_out) {
   WDR_GUARD({
+    WDR_USE(ctx, c);
     c->st->encode_from_mel_window(mel_window);
     c->st->read_encoder_out(enc_out);
     return 0;
@@ -1990,6 +2055,7 @@ int wdr_dbg_encode(wdr_context* c, const float* mel_window, float* enc_out) {
 
 int wdr_dbg_cross_kv(wdr_context* c, float* out) {
   WDR_GUARD({
+    WDR_USE(ctx, c);
     c->st->read_cross_kv(out);
     return 0;
   })
@@ -1997,6 +2063,7 @@ int wdr_dbg_cross_kv(wdr_context* c, float* out) {
 
 int wdr_dbg_decode(wdr_context* c, const int32_t* tokens, size_t n, float* logits_out) {
   WDR_GUARD({
+    WDR_USE(ctx, c);
     c->st->decode_logits(tokens, (int)n, logits_out);
     return 0;
   })
@@ -2004,6 +2071,7 @@ int wdr_dbg_decode(wdr_context* c, const int32_t* tokens, size_t n, float* logit
 
 int wdr_dbg_step(wdr_context* c, const int32_t* tokens, size_t n, float* logits_out) {
   WDR_GUARD({
+    WDR_USE(ctx, c);
     c->st->dbg_step(tokens, (int)n, logits_out);
     return 0;
   })
@@ -2012,6 +2080,7 @@ int wdr_dbg_step(wdr_context* c, const int32_t* tokens, size_t n, float* logits_
 int wdr_dbg_logits(wdr_context* c, const float* logits, int32_t R, const int32_t* ctl, const float* temperature,
                    float max_initial_ts, int32_t suppress_blank, int32_t* ids_out, float* f_out) {
   WDR_GUARD({
+    WDR_USE(ctx, c);
     WDR_CHECK(R >= 1 && R <= 8, "dbg_logits: 1..8 rows");
     std::vector<LogitsCtl> lc(R);
     for (int r = 0; r < R; ++r) {
@@ -2038,6 +2107,7 @@ int wdr_dbg_logits(wdr_context* c, const float* logits, int32_t R, const int32_t
 int wdr_dbg_batch_step(wdr_context* c, const int32_t* tokens, size_t n, int32_t rows, int32_t iters,
                        double* ms_per_step) {
   WDR_GUARD({
+    WDR_USE(ctx, c);
     *ms_per_step = c->st->dbg_batch_step(tokens, (int)n, rows, iters);
     return 0;
   })
@@ -2045,6 +2115,7 @@ int wdr_dbg_batch_step(wdr_context* c, const int32_t* tokens, size_t n, int32_t 
 
 int wdr_dbg_capture(wdr_context* c, const int32_t* tokens, size_t n, float* cap_out) {
   WDR_GUARD({
+    WDR_USE(ctx, c);
     if (c->ctx->aheads.empty()) return fail("context created without DTW");
     c->st->dtw_capture(tokens, (int)n, cap_out);
     return 0;

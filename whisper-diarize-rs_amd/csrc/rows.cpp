@@ -88,6 +88,12 @@ int RowBatch::add(const RowGroupDesc& g) {
 
 void RowBatch::upload(RowsIO& io, hipStream_t s, bool copy, bool track) {
   WDR_CHECK(R >= 1, "row batch: no rows");
+  // every row's KV-pool sequence inside the pool the tables address (layer stride / sequence
+  // stride sequences): a row past it would read / write another chain's cache or past the pool
+  if (io.seq_stride > 0 && io.layer_stride > 0) {
+    const long long nseq = io.layer_stride / io.seq_stride;
+    for (int i = 0; i < R; ++i) WDR_CHECK(seq_[i] >= 0 && seq_[i] < nseq, "row batch: KV sequence outside the pool");
+  }
   size_t off = 0;
   auto put = [&](const void* src, size_t n) -> const void* {
     const size_t o = off;

@@ -697,6 +697,11 @@ const Context::Fp8W& Context::fp8_xkv() {
 }
 
 static constexpr int kBatch = 4;     // encoder windows per encode-ahead launch (M = 6000 rows)
+// the batch's language-detection pass gives every window its own KV sequence LANG_SEQ + r of the
+// chain's NSLOT: a larger batch would write into the next chain's sequences (round 4's 8-window
+// A/B faulted exactly so), so the pool layout bounds the batch at compile time
+static_assert(LANG_SEQ + kBatch <= NSLOT, "encode-ahead batch: language-detection sequences past the chain's NSLOT");
+static_assert(DTW_SEQ < LANG_SEQ && NSEQ * 2 <= DTW_SEQ, "KV sequences: decoders + reorder scratch, DTW, language");
 static constexpr int kSlots = 16;    // in-flight segments in the cross-K/V ring (most)
 // WDR_SLOTS: ring slots per chain (a multiple of kBatch, 4..16); default 16 up to 24 chains and 8
 // above (large-v3: 40 chains x 9 slots x 245.8 MB = 88 GB of cross-K/V; 48 chains of 17 slots
