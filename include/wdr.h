@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define WDR_ABI_VERSION 5
+#define WDR_ABI_VERSION 6
 
 typedef struct wdr_engine wdr_engine;
 typedef struct wdr_context wdr_context;   /* ~ whisper_rs::WhisperContext (+ its state) */
@@ -356,6 +356,9 @@ void wdr_result_free(wdr_result_seg* segs, size_t n);
 /* ---- kernel-level test seams (host buffers in / out) ---- */
 int wdr_dbg_log_mel(wdr_context* c, const float* x, size_t n, int32_t seek, float* window_out /* [n_mels][3000] */);
 int wdr_dbg_energy(const float* x, size_t n, float* out);
+/* one v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3) on raw per-lane operands: a / b [64 lanes][32 B],
+ * scale registers sa / sb [64] (op_sel 0), out [64 lanes][4] accumulators */
+int wdr_dbg_mfma_scale(const uint8_t* a, const uint8_t* b, const int32_t* sa, const int32_t* sb, float* out);
 int wdr_dbg_encode(wdr_context* c, const float* mel_window /* [n_mels][3000] */, float* enc_out /* [1500][d] */);
 /* cross K/V of the last wdr_dbg_encode window: [1500][n_text_layer][2 (K, V)][d] (f16 -> f32) */
 int wdr_dbg_cross_kv(wdr_context* c, float* out);
@@ -380,12 +383,13 @@ int wdr_dbg_dtw(const float* cap, int32_t n_heads, int32_t n_tok, int32_t n_audi
                 float* x_out /* [n_tok-sot_len-1][n_audio] */, int32_t* times_out, int32_t* n_times);
 int wdr_dbg_discrete(const float* w, size_t n, uint32_t seed, int32_t n_draws, int32_t* out);
 int wdr_dbg_dtw_dp(const float* x, int32_t rows, int32_t cols, int32_t seek, int32_t* times_out, int32_t* n_times);
-/* fp8 (e4m3) encoder projection (BASELINE configs[4]): per-row quantisation of a [M][K] and
- * w [N][K] on the GPU, the block-scaled fp8 MFMA GEMM, epilogue as wdr_dbg_proj; the quantised
- * bytes / scales are returned (nullable) for the reference product */
+/* fp8 (MX e4m3) encoder projection (BASELINE configs[4]): a [M][K] and w [N][K] quantised on the
+ * GPU to e4m3 with one E8M0 scale per 32 k, the block-scaled fp8 MFMA GEMM, epilogue as
+ * wdr_dbg_proj (7 = GELU written back as e4m3 + scales, returned dequantised); M > 64, N % 256,
+ * K % 128.  The quantised bytes and the scale bytes ([rows][K/32], E8M0) are returned (nullable) */
 int wdr_dbg_proj_fp8(const uint16_t* a_f16, const uint16_t* w_f16, const float* bias, int32_t M, int32_t N, int32_t K,
-                     int32_t epi, float* out, uint8_t* a8_out, float* a_scale_out, uint8_t* w8_out,
-                     float* w_scale_out);
+                     int32_t epi, float* out, uint8_t* a8_out, uint8_t* a_scale_out, uint8_t* w8_out,
+                     uint8_t* w_scale_out);
 int wdr_dbg_proj(const uint16_t* a_f16, const uint16_t* w_f16, const float* bias, int32_t M, int32_t N, int32_t K,
                  int32_t epi, float* out /* [M][N] f32 (f16 epilogues are widened) */);
 /* epi | WDR_DBG_PROJ_ROWS: the decoder-rows kernel (any M, per-row arithmetic independent of M);

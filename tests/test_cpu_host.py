@@ -16,7 +16,7 @@ def test_library_exports_every_header_symbol(lib):
     assert len(syms) >= 25
     missing = [s for s in syms if not hasattr(lib, s)]
     assert not missing, missing
-    assert lib.wdr_abi_version() == 5
+    assert lib.wdr_abi_version() == 6
 
 
 def _wav(path, samples, ch=1, rate=16000, bits=16, fmt=1):

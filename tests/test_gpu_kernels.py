@@ -320,42 +320,76 @@ def _e4m3_grid():
     return np.unique(g[np.isfinite(g)])
 
 
+def _mx_exp(amax):
+    """E8M0 exponent of an F8 block (k_gemm8's f8_block_exp): the smallest e with amax / 2^e <=
+    448, amax = m 2^x (m in [0.5, 1)): x - 9 if m <= 0.875 else x - 8, clamped to [-126, 126]."""
+    m, x = np.frexp(amax.astype(np.float32))
+    e = np.where(m <= 0.875, x - 9, x - 8)
+    return np.where(amax > 0, np.clip(e, -126, 126), -126)
+
+
+def _mx_check(x, q8, sc):
+    """x [R][K] f64 values, q8 [R][K] e4m3 bytes, sc [R][K/32] E8M0 bytes: each block's scale is
+    _mx_exp of its max |x|, and each byte the nearest e4m3 value of x / 2^e (ties either way)."""
+    R, K = x.shape
+    xb = x.reshape(R, K // 32, 32)
+    e = _mx_exp(np.abs(xb).max(-1))
+    np.testing.assert_array_equal(sc.astype(np.int64) - 127, e)
+    y = (xb / np.exp2(e)[..., None]).reshape(R, K)
+    assert np.abs(y).max() <= 448
+    grid = _e4m3_grid()
+    q = _e4m3_decode(q8)
+    idx = np.clip(np.searchsorted(grid, y), 1, len(grid) - 1)
+    nearest = np.minimum(np.abs(grid[idx] - y), np.abs(grid[idx - 1] - y))
+    excess = np.abs(q - y) - nearest
+    bad = excess > 1e-5 * np.maximum(np.abs(y), 1.0)
+    assert not bad.any(), (int(bad.sum()), float(excess.max()), y[bad][:5], q[bad][:5])
+
+
+def _mx_dequant(q8, sc):
+    R, K = q8.shape
+    return (_e4m3_decode(q8).reshape(R, K // 32, 32) * np.exp2(sc.astype(np.float64) - 127)[..., None]).reshape(R, K)
+
+
 @pytest.mark.parametrize("M,N,K,epi", [(300, 256, 256, 3), (1500, 1280, 1280, 2), (777, 3840, 1280, 0),
-                                       (600, 1280, 5120, 2), (256, 5120, 1280, 1)])
+                                       (600, 1280, 5120, 2), (256, 5120, 1280, 1), (333, 512, 1280, 7)])
 def test_fp8_projection(lib, M, N, K, epi):
-    """fp8 encoder GEMM (BASELINE configs[4]): the per-row e4m3 quantisation is round-to-nearest
-    onto the e4m3 grid at scale max|row| / 448, and the GEMM output equals the fp64 product of
-    the dequantised operands (scales applied in the epilogue) within f32 accumulation error,
-    for both tile widths (N = 1280: 128-column tiles) and every epilogue."""
+    """fp8 encoder GEMM (BASELINE configs[4], k_gemm8, MX): every row of both operands is e4m3
+    with one E8M0 scale per 32 k -- the smallest power of two that maps the block's max |x| to
+    <= 448, the values rounded to nearest -- and the GEMM output equals the fp64 product of the
+    dequantised operands (the scales applied inside the block-scaled MFMA) within f32
+    accumulation error, for every epilogue, row counts off the 256-row tile (rows past M read as
+    zeros through the buffer descriptor) and the GELU -> e4m3 epilogue that feeds fc2 (7: its
+    output blocks are checked like the inputs)."""
     rng = np.random.default_rng(M + N + K)
     a = (rng.standard_normal((M, K)) * rng.uniform(0.1, 3.0, (M, 1))).astype(np.float16)
+    a[:, :32] *= np.float16(0.01)   # blocks of very different magnitude in one row
     w = (rng.standard_normal((N, K)) * 0.05).astype(np.float16)
     bias = (rng.standard_normal(N) * 0.1).astype(np.float32)
     base = rng.standard_normal((M, N)).astype(np.float32)
     out = base.copy() if epi == 2 else np.zeros((M, N), np.float32)
     a8, w8 = np.zeros((M, K), np.uint8), np.zeros((N, K), np.uint8)
-    asc, wsc = np.zeros(M, np.float32), np.zeros(N, np.float32)
+    asc, wsc = np.zeros((M, K // 32), np.uint8), np.zeros((N, K // 32), np.uint8)
     U8 = C.POINTER(C.c_uint8)
     _lib.check(lib.wdr_dbg_proj_fp8(a.view(np.uint16).ctypes.data_as(U16), w.view(np.uint16).ctypes.data_as(U16),
                                     bias.ctypes.data_as(F32), M, N, K, epi, out.ctypes.data_as(F32),
-                                    a8.ctypes.data_as(U8), asc.ctypes.data_as(F32), w8.ctypes.data_as(U8),
-                                    wsc.ctypes.data_as(F32)))
-    # quantisation: scale and nearest grid point (ties may go either way: within half a step)
-    np.testing.assert_allclose(asc, np.abs(a.astype(np.float32)).max(1) / 448, rtol=1e-6)
-    grid = _e4m3_grid()
-    x = a.astype(np.float64) / asc[:, None].astype(np.float64)
-    q = _e4m3_decode(a8)
-    idx = np.clip(np.searchsorted(grid, x), 1, len(grid) - 1)
-    nearest = np.minimum(np.abs(grid[idx] - x), np.abs(grid[idx - 1] - x))
-    # x is computed here in f64 (the kernel multiplies by 448 / amax in f32): near-ties may round
-    # to the other neighbour
-    excess = np.abs(q - x) - nearest
-    bad = excess > 1e-5 * np.maximum(np.abs(x), 1.0)
-    assert not bad.any(), (int(bad.sum()), float(excess.max()), x[bad][:5], q[bad][:5])
-    # GEMM on the dequantised operands
-    A = _e4m3_decode(a8) * asc[:, None]
-    W = _e4m3_decode(w8) * wsc[:, None]
+                                    a8.ctypes.data_as(U8), asc.ctypes.data_as(U8), w8.ctypes.data_as(U8),
+                                    wsc.ctypes.data_as(U8)))
+    _mx_check(a.astype(np.float64), a8, asc)
+    _mx_check(w.astype(np.float64), w8, wsc)
+    A, W = _mx_dequant(a8, asc), _mx_dequant(w8, wsc)
     ref = A @ W.T + bias
+    if epi == 7:
+        g = _gelu(ref)
+        gb = g.reshape(M, N // 32, 32)
+        # the kernel rounded its f32 GELU to e4m3 at its block's scale: half an ulp, 2^-4
+        # relative in the normal range, 2^(e-10) absolute in the subnormal one (x2: the kernel's
+        # block max may round to the neighbouring exponent)
+        e = _mx_exp(np.abs(gb).max(-1))[..., None]
+        err = np.abs(out.reshape(M, N // 32, 32) - gb)
+        bound = 2 * np.maximum(np.abs(gb) * 2.0 ** -4, np.exp2(e - 10.0)) + 1e-5 * np.abs(gb).max()
+        assert (err <= bound).all(), float((err / bound).max())
+        return
     want = {0: ref, 1: _gelu(ref), 2: base + ref, 3: ref}[epi]
     tol = dict(rtol=2e-3, atol=2e-3) if epi in (0, 1) else dict(rtol=0, atol=1e-4 * np.abs(A).max() * np.abs(W).max() * K ** 0.5 + 1e-4)
     np.testing.assert_allclose(out, want, **tol)
@@ -363,3 +397,57 @@ def test_fp8_projection(lib, M, N, K, epi):
     f16ref = a.astype(np.float64) @ w.T.astype(np.float64) + bias
     rel = np.linalg.norm(ref - f16ref) / np.linalg.norm(f16ref)
     assert rel < 0.06, rel
+
+
+def test_mfma_scale_lane_map(lib):
+    """The lane maps k_gemm8 relies on for v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3), measured:
+    lane l (g = l >> 4) holds k = 16g .. 16g+15 of row (A) / column (B) l & 15 in its bytes 0-15
+    and k = 64+16g .. +15 in bytes 16-31, and its scale register (op_sel 0: byte 0) scales the
+    k-block g (k = 32g .. 32g+31) of that row / column: out[m][n] = sum_k 2^(sa[16 (k/32)+m]-127)
+    2^(sb[16 (k/32)+n]-127) A[m][k] B[k][n].  (A first hypothesis, bytes 0-31 = k 32g .. 32g+31,
+    failed the "data" case: 80 where it predicts 64.)  Exact small integers, asymmetric patterns."""
+    U8 = C.POINTER(C.c_uint8)
+    I32 = C.POINTER(C.c_int32)
+    one = 0x38                                   # e4m3 1.0
+    rng = np.random.default_rng(7)
+    vals = np.array([0x30, 0x38, 0x40, 0x44, 0xb8, 0x00], np.uint8)   # 0.5, 1, 2, 3, -1, 0
+    cases = []
+    for name in ("blocks", "rows", "data", "random"):
+        a = np.full((64, 32), one, np.uint8)
+        b = np.full((64, 32), one, np.uint8)
+        sa = np.full(64, 127, np.int32)
+        sb = np.full(64, 127, np.int32)
+        if name == "blocks":
+            sa = 127 + (np.arange(64) >> 4)
+        elif name == "rows":
+            sa = 127 + (np.arange(64) & 3)
+            sb = 127 - (np.arange(64) & 1)
+        elif name == "data":
+            a[(np.arange(64) >> 4) != 1] = 0
+            sa = 127 + (np.arange(64) >> 4)
+        else:
+            a = vals[rng.integers(0, len(vals), (64, 32))]
+            b = vals[rng.integers(0, len(vals), (64, 32))]
+            sa = (127 + rng.integers(-3, 4, 64)).astype(np.int32)
+            sb = (127 + rng.integers(-3, 4, 64)).astype(np.int32)
+        out = np.zeros((64, 4), np.float32)
+        _lib.check(lib.wdr_dbg_mfma_scale(a.ctypes.data_as(U8), b.ctypes.data_as(U8), sa.astype(np.int32).ctypes.data_as(I32),
+                                          sb.astype(np.int32).ctypes.data_as(I32), out.ctypes.data_as(F32)))
+        A = _e4m3_decode(a)                      # [lane][byte]
+        Bv = _e4m3_decode(b)
+        want = np.zeros((16, 16))
+        for m in range(16):
+            for n in range(16):
+                for g in range(4):
+                    for j in range(32):
+                        k = 16 * g + j if j < 16 else 64 + 16 * g + (j - 16)
+                        blk = k // 32
+                        want[m, n] += (2.0 ** (sa[16 * blk + m] - 127) * 2.0 ** (sb[16 * blk + n] - 127) *
+                                       float(A[16 * g + m, j] * Bv[16 * g + n, j]))
+        got = np.zeros((16, 16))
+        for l in range(64):
+            for r in range(4):
+                got[(l >> 4) * 4 + r, l & 15] = out[l, r]
+        cases.append((name, got, want))
+    for name, got, want in cases:
+        assert np.array_equal(got, want), (name, got[:4, :4], want[:4, :4])

@@ -107,3 +107,42 @@ def test_configs3_split_eight_logical_devices(monkeypatch):
     assert st["chains"] == 24
     assert lang == lang1 and len(got) == len(ref) >= 2000
     assert [dataclasses.asdict(s) for s in got] == [dataclasses.asdict(s) for s in ref]
+
+
+@pytest.mark.timeout(1500)
+def test_configs4_eight_logical_devices_fp8(monkeypatch):
+    """BASELINE configs[4] at full size on one GPU: 8 h of 4-speaker audio (seed 2,
+    4 speakers), large-v3, lang auto, DTW, diarization (speaker embeddings + assignment), the fp8
+    MX encoder GEMMs (k_gemm8), through WDR_DEVICES=0 x 8 -- eight models, 3 decode chains each,
+    the exact prompt fix-up across them -- against one fp8 model with 24 chains: bit-identical
+    output, and every segment holds the properties the reference's glue guarantees
+    (tests/pipeline_props.py).  Greedy decode, as the bench."""
+    from tests.pipeline_props import check_pipeline_properties
+    syn = wdr.Synthetic(weight_std=0.02, emb_std=0.02, force_len_rate=3.3, disable_fallback=True)
+    pcm, spurts = synth_speech(28800.0, seed=2, n_speakers=4)
+    segs = _segs(pcm, spurts)
+    _progress(phase="c4 audio", segments=len(segs))
+    opts = wdr.TranscribeOptions(model="large-v3", lang="auto", enable_vad=False, enable_diarize=True,
+                                 advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    dopts = wdr.DiarizeOptions.from_options(opts)
+    one = wdr.WhisperContext("large-v3", gpu_device=0, enable_dtw=True, synthetic=syn)
+    one.set_encoder_fp8(True)
+    one.set_chains(24)
+    ref, lang1 = one.run_pipeline(segs, opts, diarize_options=dopts)
+    one.close()
+    _progress(phase="c4 one device", segments=len(ref))
+    speakers, words, inverted = check_pipeline_properties(ref, spurts)
+    monkeypatch.setenv("WDR_DEVICES", ",".join(["0"] * 8))
+    monkeypatch.setenv("WDR_DECODE_CHAINS", "3")
+    eight = wdr.WhisperContext("large-v3", enable_dtw=True, synthetic=syn)
+    assert eight.devices == [0] * 8
+    eight.set_encoder_fp8(True)
+    eight.set_chains(3)
+    got, lang = eight.run_pipeline(segs, opts, diarize_options=dopts)
+    st = eight.stage_times()
+    eight.close()
+    _progress(phase="c4 eight devices", segments=len(got), fixups=st.get("fixup_segments"), chains=st.get("chains"),
+              speakers=speakers, words=words, inverted_words=inverted)
+    assert st["chains"] == 24
+    assert lang == lang1 and len(got) == len(ref) >= 4000
+    assert [dataclasses.asdict(s) for s in got] == [dataclasses.asdict(s) for s in ref]

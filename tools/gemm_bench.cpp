@@ -112,6 +112,62 @@ int main(int argc, char** argv) {
     }
   }
   {
+    // fp8 MX encoder GEMMs (BASELINE configs[4], k_gemm8): operands quantised once (launch_quant_f8),
+    // the production epilogues (fc1: GELU written as the e4m3 fc2 operand); relative error of the
+    // f32 product against the f16 kernel's
+    const int mp = (M + 255) / 256 * 256;
+    uint8_t *A8, *W8, *O8;
+    uint32_t *As, *Ws, *Os;
+    CK(hipMalloc(&A8, (size_t)mp * 5120));
+    CK(hipMalloc(&W8, (size_t)5120 * 5120));
+    CK(hipMalloc(&O8, (size_t)mp * 5120));
+    CK(hipMalloc(&As, (size_t)40 * mp * 4));
+    CK(hipMalloc(&Ws, (size_t)40 * 5120 * 4));
+    CK(hipMalloc(&Os, (size_t)40 * mp * 4));
+    for (int si = 0; si < 4; ++si) {
+      const Shape& sh = shapes[si];
+      launch_quant_f8(A, sh.K, M, sh.K, A8, sh.K, As, mp, s);
+      launch_quant_f8(W, sh.K, sh.N, sh.K, W8, sh.K, Ws, sh.N, s);
+      const size_t on = (size_t)M * sh.N;
+      // cross-check in f32 against the f16 GEMM (k_gemm reference path)
+      ProjArgs c8{nullptr, sh.K, nullptr, sh.K, bias, out, sh.N, nullptr, 0, M, sh.N, sh.K, EPI_F32};
+      c8.A8 = A8; c8.a_sc = As; c8.ld_asc = mp; c8.B8 = W8; c8.b_sc = Ws; c8.ld_bsc = sh.N;
+      CK(hipMemsetAsync(out, 0, on * 4, s));
+      launch_proj_fp8(c8, s);
+      r.resize(on);
+      CK(hipMemcpyAsync(r.data(), out, on * 4, hipMemcpyDeviceToHost, s));
+      setenv("WDR_GEMM1", "1", 1);
+      gemm_knobs_reload();
+      ProjArgs c{A, sh.K, W, sh.K, bias, out, sh.N, nullptr, 0, M, sh.N, sh.K, EPI_F32};
+      launch_proj(c, s);
+      ref.resize(on);
+      CK(hipMemcpyAsync(ref.data(), out, on * 4, hipMemcpyDeviceToHost, s));
+      CK(hipStreamSynchronize(s));
+      unsetenv("WDR_GEMM1");
+      gemm_knobs_reload();
+      double num = 0, den = 0;
+      for (size_t i = 0; i < on; ++i) {
+        num += ((double)r[i] - ref[i]) * ((double)r[i] - ref[i]);
+        den += (double)ref[i] * ref[i];
+      }
+      const int epi = sh.epi == EPI_F16_GELU ? EPI_F8_GELU : sh.epi;
+      ProjArgs p{nullptr, sh.K, nullptr, sh.K, bias, epi == EPI_F8_GELU ? (void*)O8 : (void*)out, sh.N, nullptr, 0,
+                 M, sh.N, sh.K, epi};
+      p.A8 = A8; p.a_sc = As; p.ld_asc = mp; p.B8 = W8; p.b_sc = Ws; p.ld_bsc = sh.N; p.o_sc = Os; p.ld_osc = mp;
+      for (int i = 0; i < 3; ++i) launch_proj_fp8(p, s);
+      const int reps = 20;
+      CK(hipEventRecord(a, s));
+      for (int i = 0; i < reps; ++i) launch_proj_fp8(p, s);
+      CK(hipEventRecord(b, s));
+      CK(hipEventSynchronize(b));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, a, b));
+      const double us = ms * 1e3 / reps, tf = 2.0 * M * sh.N * sh.K / (us * 1e-6) / 1e12;
+      printf("%-20s fp8mx M=%d N=%5d K=%4d  %9.1f us  %7.1f TFLOP/s  (rel. err vs f16 %.4f)\n", sh.name, M, sh.N, sh.K,
+             us, tf, std::sqrt(num / std::max(den, 1e-30)));
+    }
+  }
+  {
     // encoder self-attention of the same batch: nb = M / 1500 windows x 20 heads x 1500^2
     const int nb = M / 1500, d = 1280;
     f16* att;

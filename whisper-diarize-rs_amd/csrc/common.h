@@ -42,8 +42,10 @@ enum Epi : int {
   EPI_F32 = 3,          // out32 = acc + bias
   EPI_F32_GELU_POS = 4, // out32 = gelu_tanh(acc + bias) + pos[row % pos_rows]  (conv2 + positional)
   EPI_QKV_CACHE = 5,    // cols [0,d) -> out16 (Q); [d,2d) / [2d,3d) -> K / V self-attention cache rows
-  EPI_XKV = 6           // cross K/V of all layers (N = L*2d) into head-major slots (XKV_* below):
+  EPI_XKV = 6,          // cross K/V of all layers (N = L*2d) into head-major slots (XKV_* below):
                         // row = window*1500 + key -> slot out + window*seq_stride
+  EPI_F8_GELU = 7       // fp8 GEMM only: out8 = e4m3(gelu_tanh(acc + bias)) with MX scales o_sc
+                        // (the encoder fc1 -> fc2 operand, Fp8Operand layout)
 };
 
 // Cross-K/V slot layout (one per encoded 30-s window): head-major [L][2][H][1500][64] f16, so
@@ -105,10 +107,13 @@ struct ProjArgs {
   f16* kc = nullptr; f16* vc = nullptr; long long seq_stride = 0; const int* row_seq = nullptr;
   const int* row_pos = nullptr; int d = 0;
   unsigned long long* ts = nullptr;   // live kernel clock of a sampled launch (ProfClock)
-  // fp8 (OCP e4m3) operands (launch_proj_fp8): A8 [M][lda] and B8 [N][ldb] bytes, dequantised
-  // in the epilogue by a_scale[row] * b_scale[col] (per-row / per-output-channel scales)
+  // fp8 (OCP e4m3) MX operands (launch_proj_fp8): A8 [M][lda] and B8 [N][ldb] bytes, each row
+  // with one E8M0 scale per 32 k, as u32 words [K/128][ld_*sc] (byte b of word (t, r): k = 128 t
+  // + 32 b .. +32 of row r; ld_asc >= M rounded up to 256) applied inside the MFMA; EPI_F8_GELU
+  // writes out [M][ldo] bytes and the scales o_sc [N/128][ld_osc]
   const uint8_t* A8 = nullptr; const uint8_t* B8 = nullptr;
-  const float* a_scale = nullptr; const float* b_scale = nullptr;
+  const uint32_t* a_sc = nullptr; const uint32_t* b_sc = nullptr; int ld_asc = 0, ld_bsc = 0;
+  uint32_t* o_sc = nullptr; int ld_osc = 0;
   // k_gemm4 tile order: groups of tile_gm row tiles walked column by column (0: row-major)
   int tile_gm = 0;
   // M > 64: the register-staged reference tile k_gemm whatever the dispatch rule picks
@@ -157,10 +162,17 @@ void launch_proj(const ProjArgs& a, hipStream_t s);
 // re-read the encoder GEMM dispatch knobs (WDR_GEMM*), which launch_proj reads once per process:
 // tools/gemm_bench's per-variant A/B only
 void gemm_knobs_reload();
-// fp8 encoder GEMM (BASELINE configs[4]): ProjArgs::A8 / B8 / a_scale / b_scale, M > 64,
-// N % 128 == 0, K % 128 == 0; epilogues as launch_proj
+// fp8 MX encoder GEMM (BASELINE configs[4], k_gemm8): ProjArgs::A8 / B8 / a_sc / b_sc, M > 64,
+// N % 256 == 0, K % 128 == 0; epilogues as launch_proj plus EPI_F8_GELU
 void launch_proj_fp8(const ProjArgs& a, hipStream_t s);
-// per-row fp8 quantisation: y[r][0..K) = e4m3(x[r][k] / scale[r]), scale[r] = max_k |x[r][k]| / 448
-void launch_quant_rows(const f16* x, int ldx, int M, int K, uint8_t* y, int ldy, float* scale, hipStream_t s);
+// f16 rows -> e4m3 + one E8M0 scale per 32 k (the smallest power of two that maps the block's
+// max |x| to <= 448), scale words [K/128][ld_sc]
+void launch_quant_f8(const f16* x, int ldx, int rows, int K, uint8_t* y, int ldy, uint32_t* sc, int ld_sc,
+                     hipStream_t s);
+// one scaled MFMA on raw per-lane operands (a / b [64][32] bytes, sa / sb [64], out [64][4])
+void launch_probe_mfma_scale(const void* a, const void* b, const int* sa, const int* sb, float* out, hipStream_t s);
+// LayerNorm (k_layernorm's arithmetic) written as e4m3 + MX scales
+void launch_layernorm_f8(const float* x, int ldx, const float* g, const float* b, uint8_t* y, int ldy, uint32_t* sc,
+                         int ld_sc, int rows, int d, hipStream_t s);
 
 }  // namespace wdr

@@ -2034,6 +2034,20 @@ int wdr_dbg_log_mel(wdr_context* c, const float* x, size_t n, int32_t seek, floa
   })
 }
 
+int wdr_dbg_mfma_scale(const uint8_t* a, const uint8_t* b, const int32_t* sa, const int32_t* sb, float* out) {
+  WDR_GUARD({
+    DevMem d(64 * 32 * 2 + 64 * 4 * 2 + 64 * 16);
+    char* p = (char*)d.p;
+    WDR_HIP(hipMemcpy(p, a, 2048, hipMemcpyHostToDevice));
+    WDR_HIP(hipMemcpy(p + 2048, b, 2048, hipMemcpyHostToDevice));
+    WDR_HIP(hipMemcpy(p + 4096, sa, 256, hipMemcpyHostToDevice));
+    WDR_HIP(hipMemcpy(p + 4352, sb, 256, hipMemcpyHostToDevice));
+    launch_probe_mfma_scale(p, p + 2048, (const int*)(p + 4096), (const int*)(p + 4352), (float*)(p + 4608), nullptr);
+    WDR_HIP(hipMemcpy(out, p + 4608, 1024, hipMemcpyDeviceToHost));
+    return 0;
+  })
+}
+
 int wdr_dbg_energy(const float* x, size_t n, float* out) {
   WDR_GUARD({
     DevMem dx(std::max<size_t>(1, n) * 4), de(std::max<size_t>(1, n) * 4);
@@ -2153,29 +2167,58 @@ int wdr_dbg_dtw_dp(const float* x, int32_t rows, int32_t cols, int32_t seek, int
   })
 }
 
-// fp8 encoder projection: a, w quantised per row on the GPU (launch_quant_rows), the fp8 GEMM
-// with the epilogue `epi` (out f32 in / out, as wdr_dbg_proj); the quantised bytes and scales
-// come back for the reference product
+// fp8 encoder projection (MX): a, w quantised on the GPU (launch_quant_f8: e4m3 + one E8M0 scale
+// per 32 k), the fp8 GEMM k_gemm8 with the epilogue `epi` (out f32 in / out, as wdr_dbg_proj;
+// EPI_F8_GELU: out = the dequantised e4m3 GELU output); the quantised bytes and the scale bytes
+// ([rows][K/32]) come back for the reference product
 int wdr_dbg_proj_fp8(const uint16_t* a16, const uint16_t* w16, const float* bias, int32_t M, int32_t N, int32_t K,
-                     int32_t epi, float* out, uint8_t* a8_out, float* a_scale_out, uint8_t* w8_out, float* w_scale_out) {
+                     int32_t epi, float* out, uint8_t* a8_out, uint8_t* a_sc_out, uint8_t* w8_out, uint8_t* w_sc_out) {
   WDR_GUARD({
+    WDR_CHECK(M > 64 && N % 256 == 0 && K % 128 == 0, "dbg fp8 projection: M > 64, N % 256, K % 128");
+    const int mp = (M + 255) / 256 * 256;
     DevMem da((size_t)M * K * 2), dw((size_t)N * K * 2), db(bias ? (size_t)N * 4 : 0), dout((size_t)M * N * 4);
-    DevMem a8((size_t)M * K), w8((size_t)N * K), as((size_t)M * 4), ws((size_t)N * 4);
+    DevMem a8((size_t)M * K), w8((size_t)N * K), as((size_t)K / 128 * mp * 4), ws((size_t)K / 128 * N * 4);
+    DevMem osc((size_t)N / 128 * mp * 4);
     WDR_HIP(hipMemcpy(da.p, a16, da.bytes, hipMemcpyHostToDevice));
     WDR_HIP(hipMemcpy(dw.p, w16, dw.bytes, hipMemcpyHostToDevice));
     if (bias) WDR_HIP(hipMemcpy(db.p, bias, db.bytes, hipMemcpyHostToDevice));
-    launch_quant_rows(da.as<f16>(), K, M, K, a8.as<uint8_t>(), K, as.as<float>(), nullptr);
-    launch_quant_rows(dw.as<f16>(), K, N, K, w8.as<uint8_t>(), K, ws.as<float>(), nullptr);
+    launch_quant_f8(da.as<f16>(), K, M, K, a8.as<uint8_t>(), K, as.as<uint32_t>(), mp, nullptr);
+    launch_quant_f8(dw.as<f16>(), K, N, K, w8.as<uint8_t>(), K, ws.as<uint32_t>(), N, nullptr);
     const bool f16out = epi == EPI_F16 || epi == EPI_F16_GELU;
-    if (!f16out) WDR_HIP(hipMemcpy(dout.p, out, dout.bytes, hipMemcpyHostToDevice));
+    if (!f16out && epi != EPI_F8_GELU) WDR_HIP(hipMemcpy(dout.p, out, dout.bytes, hipMemcpyHostToDevice));
     ProjArgs p{nullptr, K, nullptr, K, bias ? db.as<float>() : nullptr, dout.p, N, nullptr, 0, M, N, K, epi};
     p.A8 = a8.as<uint8_t>();
+    p.a_sc = as.as<uint32_t>();
+    p.ld_asc = mp;
     p.B8 = w8.as<uint8_t>();
-    p.a_scale = as.as<float>();
-    p.b_scale = ws.as<float>();
+    p.b_sc = ws.as<uint32_t>();
+    p.ld_bsc = N;
+    p.o_sc = osc.as<uint32_t>();
+    p.ld_osc = mp;
     launch_proj_fp8(p, nullptr);
     WDR_HIP(hipDeviceSynchronize());
-    if (f16out) {
+    // a scale image [K/128][ld] of u32 -> bytes [rows][K/32]
+    auto unscale = [](const DevMem& d, int rows, int ld, int K, uint8_t* dst) {
+      std::vector<uint32_t> h(d.bytes / 4);
+      WDR_HIP(hipMemcpy(h.data(), d.p, d.bytes, hipMemcpyDeviceToHost));
+      for (int r = 0; r < rows; ++r)
+        for (int b = 0; b < K / 32; ++b) dst[(size_t)r * (K / 32) + b] = (uint8_t)(h[(size_t)(b / 4) * ld + r] >> (8 * (b % 4)));
+    };
+    if (epi == EPI_F8_GELU) {
+      std::vector<uint8_t> q((size_t)M * N), sc((size_t)M * (N / 32));
+      WDR_HIP(hipMemcpy(q.data(), dout.p, q.size(), hipMemcpyDeviceToHost));
+      unscale(osc, M, mp, N, sc.data());
+      for (int r = 0; r < M; ++r)
+        for (int c = 0; c < N; ++c) {
+          const uint8_t v = q[(size_t)r * N + c];
+          // OCP e4m3fn: s eeee mmm, bias 7, no infinities, 0x7f / 0xff NaN
+          const int e = (v >> 3) & 15, mt = v & 7;
+          float x = e ? std::ldexp(1.0f + mt / 8.0f, e - 7) : std::ldexp(mt / 8.0f, -6);
+          if ((v & 0x7f) == 0x7f) x = NAN;
+          x = (v & 0x80) ? -x : x;
+          out[(size_t)r * N + c] = std::ldexp(x, (int)sc[(size_t)r * (N / 32) + c / 32] - 127);
+        }
+    } else if (f16out) {
       std::vector<f16> h((size_t)M * N);
       WDR_HIP(hipMemcpy(h.data(), dout.p, h.size() * 2, hipMemcpyDeviceToHost));
       for (size_t i = 0; i < h.size(); ++i) out[i] = (float)h[i];
@@ -2183,9 +2226,9 @@ int wdr_dbg_proj_fp8(const uint16_t* a16, const uint16_t* w16, const float* bias
       WDR_HIP(hipMemcpy(out, dout.p, dout.bytes, hipMemcpyDeviceToHost));
     }
     if (a8_out) WDR_HIP(hipMemcpy(a8_out, a8.p, a8.bytes, hipMemcpyDeviceToHost));
-    if (a_scale_out) WDR_HIP(hipMemcpy(a_scale_out, as.p, as.bytes, hipMemcpyDeviceToHost));
+    if (a_sc_out) unscale(as, M, mp, K, a_sc_out);
     if (w8_out) WDR_HIP(hipMemcpy(w8_out, w8.p, w8.bytes, hipMemcpyDeviceToHost));
-    if (w_scale_out) WDR_HIP(hipMemcpy(w_scale_out, ws.p, ws.bytes, hipMemcpyDeviceToHost));
+    if (w_sc_out) unscale(ws, N, N, K, w_sc_out);
     return 0;
   })
 }

@@ -440,28 +440,40 @@ __device__ __forceinline__ void gemm4_tile(const ProjArgs& a, f16* lds4, int ori
   // staging: wave w writes pieces 2w, 2w+1 (8 image rows each) of every half-tile
   //   AH[h] image row q -> A row bm*256 + (q >> 6)*128 + 64h + (q & 63)
   //   BH[h] image row q -> B row bn*256 + (q >> 5)*64 + 32h + (q & 31)
-  const f16* ga[2][2];   // [half][piece]; rows past M read row M - 1
-  const f16* gb[2];      // [piece]; BH1 = BH0 + 32 rows
+  // as buffer-resource DMA (buffer_load_dwordx4 ... lds): the piece's row base and k0 a
+  // wave-uniform scalar offset, one loop-invariant 32-bit lane offset per piece jj (row lane/8,
+  // g2_swz chunk (lane & 7) ^ ((4 jj + lane/16) & 7) -- wid drops out of the swizzle).  No VGPR an
+  // LDS DMA reads is ever rewritten: hipcc treats those operands like store data and waits
+  // vmcnt(0) before redefining one, which with per-K-tile 64-bit addresses put a full drain of
+  // the two tiles in flight at the head of every K-tile (round 4's k_gemm4 carried it).  Rows
+  // past M read zeros (the descriptor's bounds) and are never stored.
+  // A: the descriptor starts at the tile's first row and ends at row M (rows past it read zeros:
+  // the buffer range check covers the VGPR offset, which carries the row), k0 in the scalar offset
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.A + (size_t)bm * G3_M * a.lda), (short)0, max(0, a.M - bm * G3_M) * a.lda * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, (short)0, a.N * a.ldb * 2, 0x00020000);
+  uint32_t offa[2][2], offb[2];   // offa[half][jj]: the row inside the tile and the chunk
 #pragma unroll
   for (int jj = 0; jj < 2; ++jj) {
-    const int qa = (2 * wid + jj) * 8 + (lane >> 3);
-    const int ca = g2_swz(qa, lane & 7);
+    const uint32_t ca = (lane & 7) ^ ((4 * jj + (lane >> 4)) & 7);
+    const int p = 2 * wid + jj;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      int gm = bm * G3_M + (qa >> 6) * 128 + 64 * h + (qa & 63);
-      gm = gm < a.M ? gm : a.M - 1;
-      ga[h][jj] = a.A + (size_t)gm * a.lda + ca * 8;
-    }
-    const int gn = bn * G3_N + (qa >> 5) * 64 + (qa & 31);
-    gb[jj] = a.B + (size_t)gn * a.ldb + ca * 8;
+    for (int h = 0; h < 2; ++h)
+      offa[h][jj] = (uint32_t)((p >> 3) * 128 + 64 * h + (p & 7) * 8 + (lane >> 3)) * (uint32_t)a.lda * 2u + ca * 16u;
+    offb[jj] = (uint32_t)(lane >> 3) * (uint32_t)a.ldb * 2u + ca * 16u;
   }
-  const size_t b_half = (size_t)32 * a.ldb;
+  typedef __attribute__((address_space(3))) void* lds_ptr;
   auto stage = [&](int buf, int half, int k0) {   // half: 0 AH0, 1 AH1, 2 BH0, 3 BH1
     f16* dst = lds4 + (buf * 4 + half) * G4_HALF + (2 * wid) * 512;
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
-      const f16* src = half < 2 ? ga[half][jj] + k0 : gb[jj] + (half - 2) * b_half + k0;
-      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(dst + jj * 512), 16, 0, 0);
+      const int p = 2 * wid + jj;
+      if (half < 2) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr)(dst + jj * 512), 16, offa[half][jj], k0 * 2, 0, 0);
+      } else {
+        const int row = bn * G3_N + (p >> 2) * 64 + 32 * (half - 2) + (p & 3) * 8;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr)(dst + jj * 512), 16, offb[jj], (row * a.ldb + k0) * 2, 0, 0);
+      }
     }
   };
   const int nk = a.K / G3_BK;
@@ -629,26 +641,34 @@ __device__ __forceinline__ void gemm5_tile(const ProjArgs& a, f16* lds5, int ori
   const int grp = wid >> 2, wn = wid & 3;
   // staging: wave w writes pieces 2w, 2w+1 (8 image rows each) of every half
   //   AH[h] image row q -> A row bm*256 + (q >> 6)*128 + 64h + (q & 63);  BT row q -> B row bn*128 + q
-  const f16* ga[2][2];
-  const f16* gb[2];
+  // buffer-resource DMA with loop-invariant lane offsets, as k_gemm4
+  // A: the descriptor starts at the tile's first row and ends at row M (rows past it read zeros:
+  // the buffer range check covers the VGPR offset, which carries the row), k0 in the scalar offset
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.A + (size_t)bm * G3_M * a.lda), (short)0, max(0, a.M - bm * G3_M) * a.lda * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, (short)0, a.N * a.ldb * 2, 0x00020000);
+  uint32_t offa[2][2], offb[2];   // offa[half][jj]: the row inside the tile and the chunk
 #pragma unroll
   for (int jj = 0; jj < 2; ++jj) {
-    const int qa = (2 * wid + jj) * 8 + (lane >> 3);
-    const int ca = g2_swz(qa, lane & 7);
+    const uint32_t ca = (lane & 7) ^ ((4 * jj + (lane >> 4)) & 7);
+    const int p = 2 * wid + jj;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      int gm = bm * G3_M + (qa >> 6) * 128 + 64 * h + (qa & 63);
-      gm = gm < a.M ? gm : a.M - 1;
-      ga[h][jj] = a.A + (size_t)gm * a.lda + ca * 8;
-    }
-    gb[jj] = a.B + (size_t)(bn * 128 + qa) * a.ldb + ca * 8;
+    for (int h = 0; h < 2; ++h)
+      offa[h][jj] = (uint32_t)((p >> 3) * 128 + 64 * h + (p & 7) * 8 + (lane >> 3)) * (uint32_t)a.lda * 2u + ca * 16u;
+    offb[jj] = (uint32_t)(lane >> 3) * (uint32_t)a.ldb * 2u + ca * 16u;
   }
+  typedef __attribute__((address_space(3))) void* lds_ptr;
   auto stage = [&](int buf, int half, int k0) {   // half: 0 AH0, 1 AH1, 2 BT
     f16* dst = lds5 + (buf * 3 + half) * G4_HALF + (2 * wid) * 512;
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
-      const f16* src = half < 2 ? ga[half][jj] + k0 : gb[jj] + k0;
-      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(dst + jj * 512), 16, 0, 0);
+      const int p = 2 * wid + jj;
+      if (half < 2) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr)(dst + jj * 512), 16, offa[half][jj], k0 * 2, 0, 0);
+      } else {
+        const int row = bn * 128 + p * 8;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr)(dst + jj * 512), 16, offb[jj], (row * a.ldb + k0) * 2, 0, 0);
+      }
     }
   };
   const int nk = a.K / G3_BK;
@@ -774,185 +794,480 @@ __global__ __launch_bounds__(512, 1) void k_gemm5(ProjArgs a) {
 }
 
 
-// ---------------------------------------------------------------- fp8 (e4m3) MFMA GEMM
-// The encoder GEMMs of BASELINE configs[4]: k_gemm3's structure (8 waves of 128 x BN/4, operand
-// tiles staged by global_load_lds into two LDS buffers, g2_swz source swizzle, XCD-aware tile
-// order) on fp8 operands: a K-tile is 128 k = 128 B per row (the bytes of k_gemm3's f16 BK = 64
-// tile), one v_mfma_scale_f32_16x16x128_f8f6f4 per 16 x 16 output tile and K-tile -- the
-// block-scaled form runs twice the f16 MFMA rate (MI355X_MICROARCH.md, matrix cores); its
-// block scales are all 1 (E8M0 127) and the per-row / per-channel scales of the quantisation
-// are applied in the epilogue.  Lane l holds bytes 32 (l >> 4) .. +32 of row (l & 15) of both
-// operands: the same k for A and B, so the dot product is that of the rows whatever k order the
-// hardware sums them in.  BN = 128 for the N = d projections (o, fc2), so M = 6000 fills 240
-// tiles, BN = 256 otherwise.
+// ---------------------------------------------------------------- fp8 (e4m3) MX MFMA GEMM
+// The encoder GEMMs of BASELINE configs[4] on the block-scaled fp8 MFMA
+// (v_mfma_scale_f32_16x16x128_f8f6f4: twice the f16 MFMA rate, MI355X_MICROARCH.md "Matrix
+// cores") with MX scaling: every operand row carries one E8M0 (power-of-two) scale per 32
+// consecutive k (an F8 block), applied by the MFMA itself -- no dequantisation in the epilogue,
+// and the producers of the A operand quantise as they write it (the LayerNorm k_layernorm_f8,
+// the fc1 GEMM's GELU epilogue EPI_F8_GELU, k_quant_f8 behind the attention), so no separate
+// quantisation pass runs before a projection.
+// Operand layout (Fp8Operand): bytes [rows][ld] e4m3 (OCP e4m3fn) and scales as u32 words
+// [K / 128][ld_sc] (ld_sc = rows rounded up to 256): byte b of word (kt, r) is the E8M0 scale of
+// k = 128 kt + 32 b .. +32 of row r, so one K-tile's scales of a 256-row tile are one 1-KB run --
+// one LDS-DMA wave instruction.
+//
+// k_gemm8 is k_gemm4's ping-pong schedule byte for byte: a BK = 128 fp8 K-tile is the 128-B row
+// of k_gemm4's BK = 64 f16 tile, so the half-tile images, the g2_swz source swizzle, the four
+// quadrant phases, the stagger of waves 4-7 and the counted vmcnt(6) are unchanged; a quadrant is
+// 8 scaled MFMAs (4 row x 2 column tiles, K = 128: 32 cycles each -- the 256 cycles of k_gemm4's
+// 16 f16 MFMAs for twice the k).  A K-tile's two scale images are staged with its first half (BH0,
+// phase 1 of the tile before; waves 0 / 1, one DMA each) into a 4-KB double buffer behind the
+// tile images, retired by the same vmcnt(6), and read into registers in phase 1 of the tile.
+// Lane (fr, fq) of a 16 x 16 x 128 operand holds k = 16 fq .. +15 and 64 + 16 fq .. +15 of row fr
+// (bytes 0-15 / 16-31) and its scale register scales k-block fq (k = 32 fq .. +31), so the
+// fragment is the row's 16-B chunks fq and 4 + fq (test_mfma_scale_lane_map pins both maps).
 typedef int i32x8 __attribute__((ext_vector_type(8)));
-constexpr int G8_M = 256, G8_BK = 128;
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+constexpr int G8_BK = 128;                              // k per K-tile (bytes per row)
+constexpr uint32_t G8_SC = 2u * 2u * 1024u;             // scale images: [buf][A | B][256 words]
+constexpr uint32_t G8_LDS = G4_LDS + G8_SC;             // 132 KB
 
-template <int EPI, int BN>
-__global__ __launch_bounds__(512, 1) void k_gemm8(ProjArgs a) {
-  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];   // [buf][A 256 x 128 B, B BN x 128 B]
-  constexpr int NJ = BN / 64;          // 16-column tiles per wave
-  constexpr int BI = BN / 64;          // B DMA instructions (8 rows each) per wave
-  constexpr int BUF = (G8_M + BN) * G8_BK;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int nwg = gridDim.x, orig = blockIdx.x;
+// E8M0 exponent of an F8 block whose largest magnitude is amax: the smallest e with
+// amax / 2^e <= 448 (e4m3's largest finite value), exactly -- amax = m 2^x, m in [0.5, 1), and
+// 448 = 0.875 2^9 -- clamped to [-126, 126] so that 2^-e is a normal f32.
+__device__ __forceinline__ int f8_block_exp(float amax) {
+  if (!(amax > 0.f)) return -126;   // an all-zero block (a NaN propagates through the values)
+  int x;
+  const float m = frexpf(amax, &x);
+  const int e = m <= 0.875f ? x - 9 : x - 8;
+  return max(-126, min(126, e));
+}
+__device__ __forceinline__ float f8_pow2(int e) { return __int_as_float((127 + e) << 23); }   // 2^e
+// four values (already multiplied by 2^-e) to e4m3, round to nearest even, little-endian bytes
+__device__ __forceinline__ uint32_t f8_pack4(float a, float b, float c, float d) {
+  uint32_t w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+}
+
+// LDS reads the compiler does not see as LDS loads: hipcc (ROCm 7.2) cannot tell a ds_read of the
+// current K-tile's image from the LDS-DMA writes still in flight into the other images, and puts
+// an s_waitcnt vmcnt(0) at the head of every K-tile in front of the first compiler-visible
+// ds_read (k_gemm4 carries it too) -- which drains the two tiles in flight the counted vmcnt(6)
+// schedule is built for.  The phases order these reads themselves: every load section ends in
+// s_waitcnt lgkmcnt(0) + sched_barrier(0) (sync_in) before the MFMAs that use them.
+__device__ __forceinline__ i32x4 lds_read16(const void* p) {
+  i32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)p));
+  return v;
+}
+__device__ __forceinline__ uint32_t lds_read4(const void* p) {
+  uint32_t v;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)p));
+  return v;
+}
+
+template <int EPI>
+__device__ __forceinline__ void gemm8_tile(const ProjArgs& a, uint8_t* lds, int orig, int nwg) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
   const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
-  const int ntn = a.N / BN;
-  const int bm = id / ntn, bn = id % ntn;
-  const int wm = wid >> 2, wn = wid & 3;
-  const uint8_t* ga[4];
-  const uint8_t* gb[BI];
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) {
-    const int row = (wid * 4 + jj) * 8 + (lane >> 3);
-    const int c = g2_swz(row, lane & 7);
-    int gm = bm * G8_M + row;
-    gm = gm < a.M ? gm : a.M - 1;
-    ga[jj] = a.A8 + (size_t)gm * a.lda + c * 16;
+  const int ntn = a.N / G3_N;
+  int bm = id / ntn, bn = id % ntn;
+  if (a.tile_gm > 1) {
+    const int ntm = cdiv(a.M, G3_M), gsz = a.tile_gm * ntn, g = id / gsz, m0 = g * a.tile_gm;
+    const int gm = min(a.tile_gm, ntm - m0), l = id - g * gsz;
+    bm = m0 + l % gm;
+    bn = l / gm;
   }
+  const int grp = wid >> 2, wn = wid & 3;
+  // staging as k_gemm4 (bytes): AH[h] image row q -> A row bm*256 + (q >> 6)*128 + 64h + (q & 63),
+  // BH[h] image row q -> B row bn*256 + (q >> 5)*64 + 32h + (q & 31), q = (2 wid + jj)*8 + lane/8.
+  // Buffer-resource DMA (buffer_load_dwordx4 ... lds): the row base and k0 are a wave-uniform
+  // scalar offset, a lane adds one loop-invariant 32-bit offset per piece jj -- its row lane/8 and
+  // its g2_swz chunk ((lane & 7) ^ ((4 jj + lane/16) & 7): wid drops out).  A VGPR that an LDS
+  // DMA reads is then never rewritten: hipcc treats an LDS-DMA's VGPR operands like store data and
+  // puts an s_waitcnt vmcnt(0) in front of any redefinition, which with per-K-tile 64-bit
+  // addresses sat at the head of every K-tile and drained the two tiles in flight.  Rows past M
+  // read zeros (the descriptor's bounds), and are never stored.
+  // A: the descriptor starts at the tile's first row and ends at row M (rows past it read zeros:
+  // the buffer range check covers the VGPR offset, which carries the row), k0 in the scalar offset
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.A8 + (size_t)bm * G3_M * a.lda), (short)0, max(0, a.M - bm * G3_M) * a.lda, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)a.B8, (short)0, a.N * a.ldb, 0x00020000);
+  uint32_t offa[2][2], offb[2];   // offa[half][jj]: the row inside the tile and the chunk
 #pragma unroll
-  for (int jj = 0; jj < BI; ++jj) {
-    const int row = (wid * BI + jj) * 8 + (lane >> 3);
-    const int c = g2_swz(row, lane & 7);
-    gb[jj] = a.B8 + (size_t)(bn * BN + row) * a.ldb + c * 16;
+  for (int jj = 0; jj < 2; ++jj) {
+    const uint32_t ca = (lane & 7) ^ ((4 * jj + (lane >> 4)) & 7);
+    const int p = 2 * wid + jj;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      offa[h][jj] = (uint32_t)((p >> 3) * 128 + 64 * h + (p & 7) * 8 + (lane >> 3)) * (uint32_t)a.lda + ca * 16u;
+    offb[jj] = (uint32_t)(lane >> 3) * (uint32_t)a.ldb + ca * 16u;
   }
-  auto stage = [&](int buf, int k0) {
+  constexpr int HB = G4_HALF * 2;   // bytes per half-tile image
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  auto stage = [&](int buf, int half, int k0) {   // half: 0 AH0, 1 AH1, 2 BH0, 3 BH1; k0 in bytes
+    uint8_t* dst = lds + (buf * 4 + half) * HB + (2 * wid) * 1024;
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj)
-      __builtin_amdgcn_global_load_lds((const void*)(ga[jj] + k0), (void*)(lds8 + buf * BUF + (wid * 4 + jj) * 1024),
-                                       16, 0, 0);
-#pragma unroll
-    for (int jj = 0; jj < BI; ++jj)
-      __builtin_amdgcn_global_load_lds((const void*)(gb[jj] + k0),
-                                       (void*)(lds8 + buf * BUF + G8_M * G8_BK + (wid * BI + jj) * 1024), 16, 0, 0);
-  };
-  const int nk = a.K / G8_BK;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-
-  f32x4 acc[8][NJ];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int fr = lane & 15, fq = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * G8_BK);
-    const uint8_t* As = lds8 + cur * BUF;
-    const uint8_t* Bs = As + G8_M * G8_BK;
-    i32x8 bf[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int r = wn * (BN / 4) + j * 16 + fr;
-      const int4 lo = *(const int4*)(Bs + r * G8_BK + g2_swz(r, 2 * fq) * 16);
-      const int4 hi = *(const int4*)(Bs + r * G8_BK + g2_swz(r, 2 * fq + 1) * 16);
-      bf[j] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int r = wm * 128 + i * 16 + fr;
-      const int4 lo = *(const int4*)(As + r * G8_BK + g2_swz(r, 2 * fq) * 16);
-      const int4 hi = *(const int4*)(As + r * G8_BK + g2_swz(r, 2 * fq + 1) * 16);
-      const i32x8 af = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bf[j], acc[i][j], 0, 0, 0, 0x7f7f7f7f, 0,
-                                                                      0x7f7f7f7f);
-    }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = bm * G8_M + wm * 128 + i * 16 + fq * 4 + r;
-      const float xs = row < a.M ? a.a_scale[row] : 0.f;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int col = bn * BN + wn * (BN / 4) + j * 16 + fr;
-        epi_store<EPI>(a, row, col, acc[i][j][r] * xs * a.b_scale[col]);
+    for (int jj = 0; jj < 2; ++jj) {
+      const int p = 2 * wid + jj;
+      if (half < 2) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr)(dst + jj * 1024), 16, offa[half][jj], k0, 0, 0);
+      } else {
+        const int row = bn * G3_N + (p >> 2) * 64 + 32 * (half - 2) + (p & 3) * 8;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr)(dst + jj * 1024), 16, offb[jj], row * a.ldb + k0, 0, 0);
       }
     }
+  };
+  uint8_t* sc_lds = lds + G4_LDS;
+  const int nk = a.K / G8_BK;
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)a.a_sc, (short)0, nk * a.ld_asc * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)a.b_sc, (short)0, nk * a.ld_bsc * 4, 0x00020000);
+  const uint32_t offs = (uint32_t)lane * 16u;
+  auto stage_sc = [&](int buf, int kt) {   // wave 0: A scales of the tile's 256 rows, wave 1: B's
+    if (wid == 0)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_ptr)(sc_lds + buf * 2048), 16, offs, (kt * a.ld_asc + bm * G3_M) * 4, 0, 0);
+    else if (wid == 1)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_ptr)(sc_lds + buf * 2048 + 1024), 16, offs, (kt * a.ld_bsc + bn * G3_N) * 4, 0, 0);
+  };
+  stage_sc(0, 0);
+  stage(0, 0, 0);
+  stage(0, 2, 0);
+  stage(0, 3, 0);
+  stage(0, 1, 0);
+  if (nk > 1) {
+    stage(1, 0, G8_BK);
+    stage(1, 3, G8_BK);
+    stage(1, 1, G8_BK);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();   // waves 4-7 run one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  i32x8 af[4], bf[2];            // the current quadrant's fragments (one K = 128 step)
+  int sa[4], sb[2];              // the quadrant's scale bytes (in bits 0..7) per row / column tile
+  // lane (fr, fq) of a 16 x 16 x 128 operand holds k = 16 fq .. +15 in its bytes 0-15 and
+  // k = 64 + 16 fq .. +15 in bytes 16-31, and its scale register scales the k-block fq (32 k):
+  // measured, tests/test_gpu_kernels.py test_mfma_scale_lane_map -- so the fragment is the 16-B
+  // chunks fq and 4 + fq of the row, and the hardware k is the memory k
+  auto frag = [&](const uint8_t* img, int r) {
+    const i32x4 lo = lds_read16(img + r * 128 + g2_swz(r, fq) * 16);
+    const i32x4 hi = lds_read16(img + r * 128 + g2_swz(r, 4 + fq) * 16);
+    return (i32x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  auto read_a = [&](const uint8_t* img) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = frag(img, grp * 64 + i * 16 + fr);
+  };
+  auto read_b = [&](const uint8_t* img) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bf[j] = frag(img, wn * 32 + j * 16 + fr);
+  };
+  // the quadrant's scales: rows grp*128 + (4 qa + i)*16 + fr, columns wn*64 + (2 qb + j)*16 + fr
+  // (read per phase: 6 registers where a whole tile's 12 would spill beside the accumulators)
+  auto read_sc = [&](int buf, int qa, int qb) {
+    const uint32_t* s = (const uint32_t*)(sc_lds + buf * 2048);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sa[i] = (int)(lds_read4(s + grp * 128 + (qa * 4 + i) * 16 + fr) >> (8 * fq));
+#pragma unroll
+    for (int j = 0; j < 2; ++j) sb[j] = (int)(lds_read4(s + 256 + wn * 64 + (qb * 2 + j) * 16 + fr) >> (8 * fq));
+  };
+  auto mfma_q = [&](int qa, int qb) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[qa * 4 + i][qb * 2 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+            bf[j], af[i], acc[qa * 4 + i][qb * 2 + j], 0, 0, 0, sb[j], 0, sa[i]);
+    // pin the quadrant's MFMAs inside their phase: without a use here the (pure) scaled-MFMA
+    // calls sink past the phase barriers to the end of the K-tile, which keeps all four phases'
+    // fragments live at once and spills
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      asm volatile("" : "+v"(acc[qa * 4 + i][qb * 2]), "+v"(acc[qa * 4 + i][qb * 2 + 1]));
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto sync_in = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto sync_out = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const uint8_t* img = lds + cur * 4 * HB;
+    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+    // phase 1: Q00 -- read AH0 + BH0 (and the quadrant's scales); stage the scales and BH0 of
+    // tile kt+1
+    read_sc(cur, 0, 0);
+    read_b(img + 2 * HB);
+    read_a(img);
+    if (n1) {
+      stage_sc(cur ^ 1, kt + 1);
+      stage(cur ^ 1, 2, (kt + 1) * G8_BK);
+    }
+    sync_in();
+    mfma_q(0, 0);
+    sync_out();
+    // phase 2: Q01 -- read BH1; stage AH0 of tile kt+2
+    read_sc(cur, 0, 1);
+    read_b(img + 3 * HB);
+    if (n2) stage(cur, 0, (kt + 2) * G8_BK);
+    sync_in();
+    mfma_q(0, 1);
+    sync_out();
+    // phase 3: Q11 -- read AH1; stage BH1 of tile kt+2
+    read_sc(cur, 1, 1);
+    read_a(img + HB);
+    if (n2) stage(cur, 3, (kt + 2) * G8_BK);
+    sync_in();
+    mfma_q(1, 1);
+    sync_out();
+    // phase 4: Q10 -- read BH0; stage AH1 of tile kt+2; retire everything up to BH0 (and the
+    // scales) of tile kt+1
+    read_sc(cur, 1, 0);
+    read_b(img + 2 * HB);
+    if (n2) {
+      stage(cur, 1, (kt + 2) * G8_BK);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    sync_in();
+    mfma_q(1, 0);
+    sync_out();
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();   // matches the stagger barrier of waves 4-7
+
+  // transposed accumulators (B fragment first): lane (fr, fq) holds row fr, columns fq*4..+3 of
+  // every 16 x 16 tile
+  const bool hb = a.bias != nullptr;
+  f32x4 bz[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    bz[j] = hb ? *(const f32x4*)(a.bias + bn * G3_N + wn * 64 + j * 16 + fq * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (EPI == EPI_F8_GELU) {
+    // fc1 -> the fc2 operand: GELU, then e4m3 with one E8M0 scale per 32 columns (column tiles
+    // 2p, 2p+1 of the wave: 8 values per lane, the block's 4 lanes fq = 0..3 of row fr)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = bm * G3_M + grp * 128 + i * 16 + fr;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        f32x4 g[2];
+        float am = 0.f;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4 v = acc[i][2 * p + h] + bz[2 * p + h];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            g[h][r] = gelu_tanh(v[r]);
+            am = fmaxf(am, fabsf(g[h][r]));
+          }
+        }
+        am = fmaxf(am, __shfl_xor(am, 16, 64));
+        am = fmaxf(am, __shfl_xor(am, 32, 64));
+        const int e = f8_block_exp(am);
+        const float inv = f8_pow2(-e);
+        if (row < a.M) {
+          const int col = bn * G3_N + wn * 64 + 32 * p;
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            *(uint32_t*)((uint8_t*)a.out + (size_t)row * a.ldo + col + 16 * h + fq * 4) =
+                f8_pack4(g[h][0] * inv, g[h][1] * inv, g[h][2] * inv, g[h][3] * inv);
+          if (fq == 0) {
+            const int blk = col >> 5;
+            ((uint8_t*)a.o_sc)[((size_t)(blk >> 2) * a.ld_osc + row) * 4 + (blk & 3)] = (uint8_t)(e + 127);
+          }
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        epi_store4<EPI>(a, bm * G3_M + grp * 128 + i * 16 + fr, bn * G3_N + wn * 64 + j * 16 + fq * 4, acc[i][j], hb, bz[j]);
+  }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm8(ProjArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8[];   // [buf][AH0, AH1, BH0, BH1] + scales
+  const int ntiles = (a.N / G3_N) * cdiv(a.M, G3_M);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    gemm8_tile<EPI>(a, lds8, t, ntiles);
+    __builtin_amdgcn_s_barrier();   // every wave's last LDS reads done before the next prologue
+  }
 }
 
 template <int EPI>
 static void launch_epi8(const ProjArgs& a, hipStream_t s) {
-  const double bytes = (double)a.N * a.K + (double)a.M * a.K + (double)a.M * a.N * 2;
+  // algorithmic bytes: fp8 operands + their scales, the output at its epilogue's width
+  const double ob = EPI == EPI_F8_GELU ? 1.0 : (EPI == EPI_F32_RESID || EPI == EPI_F32) ? 4.0 : 2.0;
+  const double bytes = ((double)a.N + a.M) * a.K * (1.0 + 1.0 / 32) + (double)a.M * a.N * ob;
   const double flops = 2.0 * a.M * a.N * a.K;
-  const bool narrow = a.N % 256 != 0 || a.N <= 2048;
-  const uint32_t lds = 2u * (G8_M + (narrow ? 128u : 256u)) * G8_BK;
   static bool attr = [] {
-    WDR_HIP(hipFuncSetAttribute((const void*)k_gemm8<EPI, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                2 * (G8_M + 128) * G8_BK));
-    WDR_HIP(hipFuncSetAttribute((const void*)k_gemm8<EPI, 256>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                2 * (G8_M + 256) * G8_BK));
+    WDR_HIP(hipFuncSetAttribute((const void*)k_gemm8<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G8_LDS));
     return true;
   }();
   (void)attr;
-  if (narrow) {
-    dim3 grid((a.N / 128) * cdiv(a.M, G8_M));
-    wdr_launch(PROF_GEMM, bytes, flops, k_gemm8<EPI, 128>, grid, dim3(512), lds, s, a);
-  } else {
-    dim3 grid((a.N / 256) * cdiv(a.M, G8_M));
-    wdr_launch(PROF_GEMM, bytes, flops, k_gemm8<EPI, 256>, grid, dim3(512), lds, s, a);
-  }
+  static const int tile_gm = getenv("WDR_GEMM4_GM") ? atoi(getenv("WDR_GEMM4_GM")) : 4;   // as k_gemm4
+  ProjArgs g = a;
+  g.tile_gm = tile_gm;
+  const int ntiles = (a.N / G3_N) * cdiv(a.M, G3_M);
+  wdr_launch(PROF_GEMM, bytes, flops, k_gemm8<EPI>, dim3(ntiles), dim3(512), G8_LDS, s, g);
 }
 
 void launch_proj_fp8(const ProjArgs& a, hipStream_t s) {
-  WDR_CHECK(a.A8 && a.B8 && a.a_scale && a.b_scale, "fp8 projection: operands / scales missing");
-  WDR_CHECK(a.M > 64 && a.N % 128 == 0 && a.K % G8_BK == 0 && a.lda % 16 == 0 && a.ldb % 16 == 0,
-            "fp8 projection: M > 64, N % 128 == 0, K % 128 == 0 required");
+  WDR_CHECK(a.A8 && a.B8 && a.a_sc && a.b_sc, "fp8 projection: operands / scales missing");
+  WDR_CHECK(a.M > 64 && a.N % G3_N == 0 && a.K % G8_BK == 0 && a.lda % 16 == 0 && a.ldb % 16 == 0,
+            "fp8 projection: M > 64, N % 256 == 0, K % 128 == 0, lda / ldb % 16 required");
+  WDR_CHECK(a.ld_asc >= cdiv(a.M, G3_M) * G3_M && a.ld_bsc >= a.N && a.ld_asc % 4 == 0 && a.ld_bsc % 4 == 0,
+            "fp8 projection: scale images need the rows rounded up to 256");
+  WDR_CHECK(a.epi != EPI_F8_GELU || (a.o_sc && a.ld_osc >= cdiv(a.M, G3_M) * G3_M && a.ldo % 16 == 0),
+            "fp8 projection: GELU -> fp8 epilogue needs an output scale image");
   switch (a.epi) {
     case EPI_F16: launch_epi8<EPI_F16>(a, s); break;
     case EPI_F16_GELU: launch_epi8<EPI_F16_GELU>(a, s); break;
     case EPI_F32_RESID: launch_epi8<EPI_F32_RESID>(a, s); break;
     case EPI_F32: launch_epi8<EPI_F32>(a, s); break;
-    case EPI_XKV: launch_epi8<EPI_XKV>(a, s); break;
+    case EPI_F8_GELU: launch_epi8<EPI_F8_GELU>(a, s); break;
     default: throw std::runtime_error("fp8 projection: unsupported epilogue");
   }
   WDR_HIP(hipGetLastError());
 }
 
-// one workgroup per row: max |x| -> scale = amax / 448 (e4m3's largest finite value), then
-// the row scaled by 448 / amax, rounded to nearest-even e4m3 (v_cvt_pk_fp8_f32, OCP e4m3fn)
-__global__ __launch_bounds__(256) void k_quant_rows(const f16* x, int ldx, int K, uint8_t* y, int ldy, float* scale) {
-  __shared__ float red[4];
-  const int r = blockIdx.x, tid = threadIdx.x;
-  const f16* xr = x + (size_t)r * ldx;
-  float am = 0.f;
-  for (int c = tid * 8; c < K; c += 2048) {
-    const f16x8 v = *(const f16x8*)(xr + c);
+// f16 rows -> e4m3 + MX scales (Fp8Operand layout): one wave per row, 8 values per lane per
+// step; a 32-k block is 4 lanes (max by two xor shuffles), a scale word 16 lanes (gathered by
+// shuffles, stored by the group's first lane).  The weights (once, Context::fp8_build) and the
+// attention output ahead of the o projection.
+__global__ __launch_bounds__(256) void k_quant_f8(const f16* x, int ldx, int rows, int K, uint8_t* y, int ldy,
+                                                  uint32_t* sc, int ld_sc) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const f16* xr = x + (size_t)row * ldx;
+  for (int c0 = 0; c0 < K; c0 += 512) {
+    const int c = c0 + lane * 8;
+    const bool ok = c < K;
+    f16x8 v = ok ? *(const f16x8*)(xr + c) : f16x8{};
+    float am = 0.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf((float)v[e]));
-  }
-  am = wave_max(am);
-  if ((tid & 63) == 0) red[tid >> 6] = am;
-  __syncthreads();
-  am = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  const float inv = am > 0.f ? 448.f / am : 1.f;
-  if (tid == 0) scale[r] = am > 0.f ? am / 448.f : 1.f;
-  uint8_t* yr = y + (size_t)r * ldy;
-  for (int c = tid * 8; c < K; c += 2048) {
-    const f16x8 v = *(const f16x8*)(xr + c);
-    unsigned lo = 0, hi = 0;
-    lo = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[0] * inv, (float)v[1] * inv, lo, false);
-    lo = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[2] * inv, (float)v[3] * inv, lo, true);
-    hi = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[4] * inv, (float)v[5] * inv, hi, false);
-    hi = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[6] * inv, (float)v[7] * inv, hi, true);
-    *(uint2*)(yr + c) = make_uint2(lo, hi);
+    am = fmaxf(am, __shfl_xor(am, 1, 64));
+    am = fmaxf(am, __shfl_xor(am, 2, 64));
+    const int e = f8_block_exp(am);
+    const float inv = f8_pow2(-e);
+    const uint32_t lo = f8_pack4((float)v[0] * inv, (float)v[1] * inv, (float)v[2] * inv, (float)v[3] * inv);
+    const uint32_t hi = f8_pack4((float)v[4] * inv, (float)v[5] * inv, (float)v[6] * inv, (float)v[7] * inv);
+    if (ok) *(uint2*)(y + (size_t)row * ldy + c) = make_uint2(lo, hi);
+    // scale word of k 128 t .. +128 (lanes 16 u .. 16 u + 15): the bytes of lanes +0, 4, 8, 12
+    const int b = e + 127, base = lane & ~15;
+    const uint32_t w = (uint32_t)__shfl(b, base, 64) | (uint32_t)__shfl(b, base + 4, 64) << 8 |
+                       (uint32_t)__shfl(b, base + 8, 64) << 16 | (uint32_t)__shfl(b, base + 12, 64) << 24;
+    if ((lane & 15) == 0 && ok) sc[(size_t)(c >> 7) * ld_sc + row] = w;
   }
 }
 
-void launch_quant_rows(const f16* x, int ldx, int M, int K, uint8_t* y, int ldy, float* scale, hipStream_t s) {
-  WDR_CHECK(M >= 1 && K % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0, "fp8 quantisation: K, ld must be multiples of 8");
-  WDR_KLAUNCH(k_quant_rows, dim3(M), dim3(256), 0, s, x, ldx, K, y, ldy, scale);
+// one v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3) on raw per-lane operands: lane l's 32 A
+// bytes a[l], B bytes b[l], scale registers sa[l] / sb[l] (op_sel 0), its 4 accumulators out[l]
+// -- the probe that pins the lane -> (row, k-block) map of the data and the scales
+__global__ __launch_bounds__(64) void k_probe_mfma_scale(const i32x8* a, const i32x8* b, const int* sa, const int* sb,
+                                                          f32x4* out) {
+  const int l = threadIdx.x;
+  out[l] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[l], b[l], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0, sa[l], 0,
+                                                             sb[l]);
+}
+void launch_probe_mfma_scale(const void* a, const void* b, const int* sa, const int* sb, float* out, hipStream_t s) {
+  WDR_KLAUNCH(k_probe_mfma_scale, dim3(1), dim3(64), 0, s, (const i32x8*)a, (const i32x8*)b, sa, sb, (f32x4*)out);
+  WDR_HIP(hipGetLastError());
+}
+
+void launch_quant_f8(const f16* x, int ldx, int rows, int K, uint8_t* y, int ldy, uint32_t* sc, int ld_sc,
+                     hipStream_t s) {
+  WDR_CHECK(rows >= 1 && K % 128 == 0 && ldx % 8 == 0 && ldy % 16 == 0 && ld_sc >= rows,
+            "fp8 quantisation: K % 128, ldx % 8, ldy % 16, scale rows");
+  WDR_KLAUNCH(k_quant_f8, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, rows, K, y, ldy, sc, ld_sc);
+  WDR_HIP(hipGetLastError());
+}
+
+// LayerNorm (k_layernorm's arithmetic: ggml_norm, eps 1e-5, gamma / beta) quantised as it is
+// written: the encoder's LN1 / LN2 straight into the qkv / fc1 fp8 operands.  One wave per row,
+// 4 consecutive columns per lane and step (lanes 0-31 cover a 128-column scale word, a 32-column
+// block is 8 lanes).
+__global__ __launch_bounds__(256) void k_layernorm_f8(const float* x, int ldx, const float* g, const float* b,
+                                                      uint8_t* y, int ldy, uint32_t* sc, int ld_sc, int rows, int d) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* xr = x + (long long)row * ldx;
+  float v[5][4];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int c = lane * 4 + j * 256;
+    const bool ok = c < d;
+    const int cc = ok ? c : 0;
+    const float4 q = *(const float4*)(xr + cc);
+    v[j][0] = ok ? q.x : 0.f; v[j][1] = ok ? q.y : 0.f; v[j][2] = ok ? q.z : 0.f; v[j][3] = ok ? q.w : 0.f;
+    s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+  }
+  s = wave_sum(s);
+  const float mean = s / d;
+  float s2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < 5; ++j)
+    if (lane * 4 + j * 256 < d)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float t = v[j][e] - mean;
+        s2 += t * t;
+      }
+  s2 = wave_sum(s2);
+  const float scale = 1.0f / sqrtf(s2 / d + 1e-5f);
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int c = lane * 4 + j * 256;
+    if (j * 256 >= d) break;   // wave-uniform: the shuffles below need every lane
+    const bool ok = c < d;
+    const int cc = ok ? c : 0;
+    const float4 g4 = *(const float4*)(g + cc);
+    const float4 b4 = *(const float4*)(b + cc);
+    const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, bb[4] = {b4.x, b4.y, b4.z, b4.w};
+    float o[4], am = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o[e] = ok ? (v[j][e] - mean) * scale * gg[e] + bb[e] : 0.f;
+      am = fmaxf(am, fabsf(o[e]));
+    }
+    am = fmaxf(am, __shfl_xor(am, 1, 64));
+    am = fmaxf(am, __shfl_xor(am, 2, 64));
+    am = fmaxf(am, __shfl_xor(am, 4, 64));
+    const int e = f8_block_exp(am);
+    const float inv = f8_pow2(-e);
+    if (ok) *(uint32_t*)(y + (size_t)row * ldy + c) = f8_pack4(o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
+    const int bb8 = e + 127, base = lane & 32;
+    const uint32_t w = (uint32_t)__shfl(bb8, base, 64) | (uint32_t)__shfl(bb8, base + 8, 64) << 8 |
+                       (uint32_t)__shfl(bb8, base + 16, 64) << 16 | (uint32_t)__shfl(bb8, base + 24, 64) << 24;
+    if ((lane & 31) == 0 && ok) sc[(size_t)(c >> 7) * ld_sc + row] = w;
+  }
+}
+
+void launch_layernorm_f8(const float* x, int ldx, const float* g, const float* b, uint8_t* y, int ldy, uint32_t* sc,
+                         int ld_sc, int rows, int d, hipStream_t s) {
+  WDR_CHECK(d % 128 == 0 && d <= 1280 && ldx % 4 == 0 && ldy % 16 == 0 && ld_sc >= rows,
+            "fp8 layernorm: d % 128, d <= 1280");
+  WDR_KLAUNCH(k_layernorm_f8, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, ldx, g, b, y, ldy, sc, ld_sc, rows, d);
   WDR_HIP(hipGetLastError());
 }
 

@@ -132,23 +132,21 @@ class Context {
     long long dq_passes = 0, dq_rows = 0, dq_jobs = 0;   // the DTW queue's
   };
   BatchStats batcher_stats();
-  // fp8 (e4m3) encoder GEMMs (BASELINE configs[4]; wdr_context_set_encoder_fp8, WDR_FP8_ENCODER):
-  // the encoder's projection and cross-K/V weights quantised per output channel, made once on
-  // first use; activations are quantised per row in the encoder
+  // fp8 (MX e4m3) encoder GEMMs (BASELINE configs[4]; wdr_context_set_encoder_fp8,
+  // WDR_FP8_ENCODER): the encoder layers' projection weights as e4m3 with one E8M0 scale per 32 k,
+  // made once on first use; the activations are quantised by their producers in the encoder
   std::atomic<bool> fp8_encoder{false};
   struct Fp8W {
-    DevMem w, s;   // [N][K] e4m3, [N] f32 scales
+    DevMem w, s;   // [N][K] e4m3, scale words [K/128][N] (byte b of word (t, n): k 128t + 32b ..)
   };
   struct Fp8Layer {
     Fp8W qkv, o, fc1, fc2;
   };
   const std::vector<Fp8Layer>& fp8_layers();   // thread-safe lazy quantisation
-  const Fp8W& fp8_xkv();
 
  private:
   std::mutex fp8_mu_;
   std::vector<Fp8Layer> fp8_layers_;
-  Fp8W fp8_xkv_;
   void fp8_build();
 };
 

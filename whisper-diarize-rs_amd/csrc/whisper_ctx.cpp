@@ -541,7 +541,9 @@ struct State::Impl {
   struct EncBufs {
     int nb = 0;
     DevMem im2col, c1, ex, eh, eqkv, eatt, emlp;
-    DevMem q8, qs;   // fp8 encoder: the GEMM input quantised per row, its row scales
+    // fp8 encoder (MX e4m3): the d-wide GEMM operand (LN1 / attention output / LN2) and the 4d-wide
+    // fc2 operand (fc1's GELU epilogue), each with its scale image [K/128][rows rounded to 256]
+    DevMem q8a, qsa, q8m, qsm;
   };
   EncBufs eb, e1;
   // cross-K/V ring: one slot per in-flight speech segment, [slot][1500][L*2d] f16, plus a
@@ -667,11 +669,13 @@ void Context::fp8_build() {
   WDR_HIP(hipSetDevice(cp.gpu_device));
   const HParams& hp = model.hp;
   const int d = hp.n_audio_state;
+  // every weight row (output channel) as e4m3 with one E8M0 scale per 32 k, scale image
+  // [K/128][N] (launch_quant_f8); k_gemm8 applies both operands' block scales in the MFMA
   auto quant = [&](const f16* w, int N, int K) {
     Fp8W q;
     q.w = DevMem((size_t)N * K);
-    q.s = DevMem((size_t)N * 4);
-    launch_quant_rows(w, K, N, K, q.w.as<uint8_t>(), K, q.s.as<float>(), stream);
+    q.s = DevMem((size_t)K / 128 * N * 4);
+    launch_quant_f8(w, K, N, K, q.w.as<uint8_t>(), K, q.s.as<uint32_t>(), N, stream);
     return q;
   };
   std::vector<Fp8Layer> L(hp.n_audio_layer);
@@ -682,7 +686,6 @@ void Context::fp8_build() {
     L[l].fc1 = quant(e.w_fc1, 4 * d, d);
     L[l].fc2 = quant(e.w_fc2, d, 4 * d);
   }
-  fp8_xkv_ = quant(model.w_xkv, hp.n_text_layer * 2 * hp.n_text_state, d);
   WDR_HIP(hipStreamSynchronize(stream));
   fp8_layers_ = std::move(L);
 }
@@ -690,10 +693,6 @@ const std::vector<Context::Fp8Layer>& Context::fp8_layers() {
   std::lock_guard<std::mutex> g(fp8_mu_);
   if (fp8_layers_.empty()) fp8_build();
   return fp8_layers_;
-}
-const Context::Fp8W& Context::fp8_xkv() {
-  fp8_layers();
-  return fp8_xkv_;
 }
 
 static constexpr int kBatch = 4;     // encoder windows per encode-ahead launch (M = 6000 rows)
@@ -721,8 +720,12 @@ static void alloc_enc(State::Impl::EncBufs& e, int nb, int d, int kp1) {
   e.eqkv = DevMem((size_t)nb * 1500 * 3 * d * 2);
   e.eatt = DevMem((size_t)nb * 1500 * d * 2);
   e.emlp = DevMem((size_t)nb * 1500 * 4 * d * 2);
-  e.q8 = DevMem((size_t)nb * 1500 * 4 * d);
-  e.qs = DevMem((size_t)nb * 1500 * 4);
+  // fp8 MX operands (configs[4]): rows padded to the GEMM's 256-row tiles for the scale images
+  const size_t mp = (size_t)cdiv(nb * 1500, 256) * 256;
+  e.q8a = DevMem(mp * d);
+  e.qsa = DevMem((size_t)d / 128 * mp * 4);
+  e.q8m = DevMem(mp * 4 * d);
+  e.qsm = DevMem((size_t)4 * d / 128 * mp * 4);
 }
 
 State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
@@ -972,47 +975,70 @@ static void encoder_body(Context& ctx, State::Impl& m, State::Impl::EncBufs& e, 
        md.enc_pos, hp.n_audio_ctx);
   const float scale = 1.0f / 8.0f;   // d_head^-1/2
   const long long bs = 1500ll * 3 * d, obs = 1500ll * d;
-  // fp8 encoder (BASELINE configs[4]): every projection's input quantised per row into e.q8,
-  // the weights per output channel (Context::fp8_layers), the block-scaled fp8 MFMA GEMM with
-  // the same epilogues; LayerNorm, attention and the residual stream stay f16 / f32
+  // fp8 encoder (BASELINE configs[4]): the four projections of every layer on the MX fp8 GEMM
+  // (k_gemm8, twice the f16 MFMA rate); their A operands are written as e4m3 + E8M0 block scales
+  // by their producers -- LN1 / LN2 (k_layernorm_f8), fc1's GELU epilogue (EPI_F8_GELU) -- or
+  // quantised once behind the attention (k_quant_f8); the weights were quantised once
+  // (Context::fp8_layers).  The residual stream, attention, the final LayerNorm and the cross-K/V
+  // projection the decoder reads stay f16 / f32.
   const bool f8 = ctx.fp8_encoder.load() && d % 128 == 0;
-  const std::vector<Context::Fp8Layer>* F8 = f8 ? &ctx.fp8_layers() : nullptr;
-  auto gemm = [&](const f16* A, int lda, const f16* W, const Context::Fp8W* W8, const float* bias, void* out, int ldo,
-                  int N, int K, int epi) {
-    if (!W8) {
-      ProjArgs p{A, lda, W, K, bias, out, ldo, nullptr, 0, M, N, K, epi};
-      if (epi == EPI_XKV) p.seq_stride = (long long)m.xkv_slot_elems;   // window b -> slot b
-      launch_proj(p, s);
-      return;
+  if (f8) {
+    const std::vector<Context::Fp8Layer>& F8 = ctx.fp8_layers();
+    const int mp = cdiv(M, 256) * 256;
+    uint8_t* qa = e.q8a.as<uint8_t>();
+    uint8_t* qm = e.q8m.as<uint8_t>();
+    uint32_t* sa = e.qsa.as<uint32_t>();
+    uint32_t* sm = e.qsm.as<uint32_t>();
+    auto gemm8 = [&](const uint8_t* A, const uint32_t* asc, int K, const Context::Fp8W& W, const float* bias, void* out,
+                     int ldo, int N, int epi) {
+      ProjArgs p{nullptr, K, nullptr, K, bias, out, ldo, nullptr, 0, M, N, K, epi};
+      p.A8 = A;
+      p.a_sc = asc;
+      p.ld_asc = mp;
+      p.B8 = W.w.as<uint8_t>();
+      p.b_sc = W.s.as<uint32_t>();
+      p.ld_bsc = N;
+      if (epi == EPI_F8_GELU) {
+        p.o_sc = sm;
+        p.ld_osc = mp;
+      }
+      launch_proj_fp8(p, s);
+    };
+    for (int l = 0; l < hp.n_audio_layer; ++l) {
+      const EncLayer& w = md.enc[l];
+      const Context::Fp8Layer& w8 = F8[l];
+      launch_layernorm_f8(e.ex.as<float>(), d, w.ln1_g, w.ln1_b, qa, d, sa, mp, M, d, s);
+      gemm8(qa, sa, d, w8.qkv, w.b_qkv, e.eqkv.p, 3 * d, 3 * d, EPI_F16);
+      FlashArgs fa{e.eqkv.as<f16>(), 3 * d, bs, e.eqkv.as<f16>() + d, 3 * d, bs, e.eqkv.as<f16>() + 2 * d, 3 * d, bs,
+                   e.eatt.as<f16>(), d, obs, nullptr, 1500, 1500, hp.n_audio_head, 0, scale};
+      launch_flash_attn(fa, nb, s);
+      launch_quant_f8(e.eatt.as<f16>(), d, M, d, qa, d, sa, mp, s);
+      gemm8(qa, sa, d, w8.o, w.b_o, e.ex.p, d, d, EPI_F32_RESID);
+      launch_layernorm_f8(e.ex.as<float>(), d, w.ln2_g, w.ln2_b, qa, d, sa, mp, M, d, s);
+      gemm8(qa, sa, d, w8.fc1, w.b_fc1, qm, 4 * d, 4 * d, EPI_F8_GELU);
+      gemm8(qm, sm, 4 * d, w8.fc2, w.b_fc2, e.ex.p, d, d, EPI_F32_RESID);
     }
-    launch_quant_rows(A, lda, M, K, e.q8.as<uint8_t>(), K, e.qs.as<float>(), s);
-    ProjArgs p{nullptr, K, nullptr, K, bias, out, ldo, nullptr, 0, M, N, K, epi};
-    if (epi == EPI_XKV) p.seq_stride = (long long)m.xkv_slot_elems;
-    p.A8 = e.q8.as<uint8_t>();
-    p.B8 = W8->w.as<uint8_t>();
-    p.a_scale = e.qs.as<float>();
-    p.b_scale = W8->s.as<float>();
-    launch_proj_fp8(p, s);
-  };
-  for (int l = 0; l < hp.n_audio_layer; ++l) {
-    const EncLayer& w = md.enc[l];
-    const Context::Fp8Layer* w8 = F8 ? &(*F8)[l] : nullptr;
-    launch_layernorm(e.ex.as<float>(), d, w.ln1_g, w.ln1_b, e.eh.as<f16>(), d, M, d, s);
-    gemm(e.eh.as<f16>(), d, w.w_qkv, w8 ? &w8->qkv : nullptr, w.b_qkv, e.eqkv.p, 3 * d, 3 * d, d, EPI_F16);
-    FlashArgs fa{e.eqkv.as<f16>(), 3 * d, bs, e.eqkv.as<f16>() + d, 3 * d, bs, e.eqkv.as<f16>() + 2 * d, 3 * d, bs,
-                 e.eatt.as<f16>(), d, obs, nullptr, 1500, 1500, hp.n_audio_head, 0, scale};
-    launch_flash_attn(fa, nb, s);
-    gemm(e.eatt.as<f16>(), d, w.w_o, w8 ? &w8->o : nullptr, w.b_o, e.ex.p, d, d, d, EPI_F32_RESID);
-    launch_layernorm(e.ex.as<float>(), d, w.ln2_g, w.ln2_b, e.eh.as<f16>(), d, M, d, s);
-    gemm(e.eh.as<f16>(), d, w.w_fc1, w8 ? &w8->fc1 : nullptr, w.b_fc1, e.emlp.p, 4 * d, 4 * d, d, EPI_F16_GELU);
-    gemm(e.emlp.as<f16>(), 4 * d, w.w_fc2, w8 ? &w8->fc2 : nullptr, w.b_fc2, e.ex.p, d, d, 4 * d, EPI_F32_RESID);
+  } else {
+    for (int l = 0; l < hp.n_audio_layer; ++l) {
+      const EncLayer& w = md.enc[l];
+      launch_layernorm(e.ex.as<float>(), d, w.ln1_g, w.ln1_b, e.eh.as<f16>(), d, M, d, s);
+      proj(s, e.eh.as<f16>(), d, w.w_qkv, d, w.b_qkv, e.eqkv.p, 3 * d, M, 3 * d, d, EPI_F16);
+      FlashArgs fa{e.eqkv.as<f16>(), 3 * d, bs, e.eqkv.as<f16>() + d, 3 * d, bs, e.eqkv.as<f16>() + 2 * d, 3 * d, bs,
+                   e.eatt.as<f16>(), d, obs, nullptr, 1500, 1500, hp.n_audio_head, 0, scale};
+      launch_flash_attn(fa, nb, s);
+      proj(s, e.eatt.as<f16>(), d, w.w_o, d, w.b_o, e.ex.p, d, M, d, d, EPI_F32_RESID);
+      launch_layernorm(e.ex.as<float>(), d, w.ln2_g, w.ln2_b, e.eh.as<f16>(), d, M, d, s);
+      proj(s, e.eh.as<f16>(), d, w.w_fc1, d, w.b_fc1, e.emlp.p, 4 * d, M, 4 * d, d, EPI_F16_GELU);
+      proj(s, e.emlp.as<f16>(), 4 * d, w.w_fc2, 4 * d, w.b_fc2, e.ex.p, d, M, d, 4 * d, EPI_F32_RESID);
+    }
   }
   launch_layernorm(e.ex.as<float>(), d, md.ln_post_g, md.ln_post_b, e.eh.as<f16>(), d, M, d, s);
   // cross K/V for every decoder layer in one GEMM (N = L*2d), scattered by the epilogue into the
   // windows' head-major slots (common.h XKV_*; the batch's slots are contiguous)
   const int L = hp.n_text_layer;
-  gemm(e.eh.as<f16>(), d, md.w_xkv, f8 ? &ctx.fp8_xkv() : nullptr, md.b_xkv, xkv_out, L * 2 * d, L * 2 * d, d,
-       EPI_XKV);
+  ProjArgs px{e.eh.as<f16>(), d, md.w_xkv, d, md.b_xkv, xkv_out, L * 2 * d, nullptr, 0, M, L * 2 * d, d, EPI_XKV};
+  px.seq_stride = (long long)m.xkv_slot_elems;   // window b -> slot b
+  launch_proj(px, s);
 }
 
 // one window of the current slot's segment on the decode stream (on-demand path)
@@ -1322,7 +1348,6 @@ bool State::top_up_batch(int j) {
       if (!eg.exec) {
         if (f8) {   // lazily built weights: not inside the capture
           (void)ctx_.fp8_layers();
-          (void)ctx_.fp8_xkv();
         }
         if (!eg.tl) eg.tl = std::make_unique<RowBatch>(kBatch, kBatch, 0);
         std::lock_guard<std::recursive_mutex> cap_lock(hip_alloc_mutex());   // no allocation meanwhile

@@ -166,6 +166,7 @@ _SIGS = {
     "wdr_result_free": (None, [P(ResultSeg), sz]),
     "wdr_dbg_log_mel": (C.c_int, [vp, P(f32), sz, i32, P(f32)]),
     "wdr_dbg_energy": (C.c_int, [P(f32), sz, P(f32)]),
+    "wdr_dbg_mfma_scale": (C.c_int, [P(C.c_uint8), P(C.c_uint8), P(i32), P(i32), P(f32)]),
     "wdr_dbg_encode": (C.c_int, [vp, P(f32), P(f32)]),
     "wdr_dbg_decode": (C.c_int, [vp, P(i32), sz, P(f32)]),
     "wdr_dbg_cross_kv": (C.c_int, [vp, P(f32)]),
@@ -177,7 +178,7 @@ _SIGS = {
     "wdr_dbg_dtw_dp": (C.c_int, [P(f32), i32, i32, i32, P(i32), P(i32)]),
     "wdr_dbg_proj": (C.c_int, [P(C.c_uint16), P(C.c_uint16), P(f32), i32, i32, i32, i32, P(f32)]),
     "wdr_dbg_proj_fp8": (C.c_int, [P(C.c_uint16), P(C.c_uint16), P(f32), i32, i32, i32, i32, P(f32), P(C.c_uint8),
-                                   P(f32), P(C.c_uint8), P(f32)]),
+                                   P(C.c_uint8), P(C.c_uint8), P(C.c_uint8)]),
     "wdr_dbg_attn": (C.c_int, [P(C.c_uint16), P(C.c_uint16), P(C.c_uint16), i32, i32, i32, i32, P(f32)]),
     "wdr_dbg_xattn": (C.c_int, [P(C.c_uint16), P(C.c_uint16), P(i32), P(i32), i32, i32, i32, i32, P(f32)]),
 }
