@@ -1111,6 +1111,196 @@ __global__ __launch_bounds__(512, 1) void k_gemm8(ProjArgs a) {
   }
 }
 
+// k_gemm8n: the narrow fp8 projections (o, fc2: N = d = 1280) on k_gemm5's 256 x 128 tile and
+// two-phase schedule (8 waves of 128 x 32, B fragments kept across the two 64-row phases): 240
+// tiles at M = 6000 where k_gemm8's 256 x 256 tiles leave half the CUs idle.  Scale images: A
+// (256 rows) and B (128 rows, the first 512 B of the image) per K-tile, in a 3-deep ring: a
+// K-tile's scales are staged with its AH0 / BT (phase 2 of the tile two before), so the tile in
+// between still reads its own.
+constexpr uint32_t G8N_LDS = 2u * 3u * G4_HALF * 2u + 3u * 2048u;   // 96 KB + 6 KB
+
+template <int EPI>
+__device__ __forceinline__ void gemm8n_tile(const ProjArgs& a, uint8_t* lds, int orig, int nwg) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+  const int id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int ntn = a.N / 128;
+  int bm = id / ntn, bn = id % ntn;
+  if (a.tile_gm > 1) {
+    const int ntm = cdiv(a.M, G3_M), gsz = a.tile_gm * ntn, g = id / gsz, m0 = g * a.tile_gm;
+    const int gm = min(a.tile_gm, ntm - m0), l = id - g * gsz;
+    bm = m0 + l % gm;
+    bn = l / gm;
+  }
+  const int grp = wid >> 2, wn = wid & 3;
+  // staging (bytes) as k_gemm5: AH[h] image row q -> A row bm*256 + (q >> 6)*128 + 64h + (q & 63);
+  // BT row q -> B row bn*128 + q; buffer-resource DMA as k_gemm8 (rows past M read zeros)
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.A8 + (size_t)bm * G3_M * a.lda), (short)0, max(0, a.M - bm * G3_M) * a.lda, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)a.B8, (short)0, a.N * a.ldb, 0x00020000);
+  uint32_t offa[2][2], offb[2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const uint32_t ca = (lane & 7) ^ ((4 * jj + (lane >> 4)) & 7);
+    const int p = 2 * wid + jj;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      offa[h][jj] = (uint32_t)((p >> 3) * 128 + 64 * h + (p & 7) * 8 + (lane >> 3)) * (uint32_t)a.lda + ca * 16u;
+    offb[jj] = (uint32_t)(p * 8 + (lane >> 3)) * (uint32_t)a.ldb + ca * 16u;
+  }
+  constexpr int HB = G4_HALF * 2;
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  auto stage = [&](int buf, int half, int k0) {   // half: 0 AH0, 1 AH1, 2 BT; k0 in bytes
+    uint8_t* dst = lds + (buf * 3 + half) * HB + (2 * wid) * 1024;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      if (half < 2)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr)(dst + jj * 1024), 16, offa[half][jj], k0, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr)(dst + jj * 1024), 16, offb[jj], bn * 128 * a.ldb + k0, 0, 0);
+    }
+  };
+  uint8_t* sc_lds = lds + 2 * 3 * HB;
+  const int nk = a.K / G8_BK;
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)a.a_sc, (short)0, nk * a.ld_asc * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)a.b_sc, (short)0, nk * a.ld_bsc * 4, 0x00020000);
+  const uint32_t offs = (uint32_t)lane * 16u;
+  auto stage_sc = [&](int kt) {   // wave 0: A scales (256 rows), wave 1 lanes 0-31: B scales (128 rows)
+    uint8_t* dst = sc_lds + (kt % 3) * 2048;
+    if (wid == 0)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_ptr)dst, 16, offs, (kt * a.ld_asc + bm * G3_M) * 4, 0, 0);
+    else if (wid == 1 && lane < 32)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_ptr)(dst + 1024), 16, offs, (kt * a.ld_bsc + bn * 128) * 4, 0, 0);
+  };
+  stage_sc(0);
+  stage(0, 0, 0);
+  stage(0, 2, 0);
+  stage(0, 1, 0);
+  if (nk > 1) {
+    stage_sc(1);
+    stage(1, 0, G8_BK);
+    stage(1, 2, G8_BK);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();   // waves 4-7 run one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  f32x4 acc[8][2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  i32x8 af[4], bf[2];
+  int sa[4], sb[2];
+  auto frag = [&](const uint8_t* img, int r) {   // chunks fq and 4 + fq: k_gemm8's lane map
+    const i32x4 lo = lds_read16(img + r * 128 + g2_swz(r, fq) * 16);
+    const i32x4 hi = lds_read16(img + r * 128 + g2_swz(r, 4 + fq) * 16);
+    return (i32x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  auto read_a = [&](const uint8_t* img, const uint32_t* sc, int h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      af[i] = frag(img, grp * 64 + i * 16 + fr);
+      sa[i] = (int)(lds_read4(sc + grp * 128 + 64 * h + i * 16 + fr) >> (8 * fq));
+    }
+  };
+  auto read_b = [&](const uint8_t* img, const uint32_t* sc) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bf[j] = frag(img, wn * 32 + j * 16 + fr);
+      sb[j] = (int)(lds_read4(sc + 256 + wn * 32 + j * 16 + fr) >> (8 * fq));
+    }
+  };
+  auto mfma_h = [&](int h) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[h * 4 + i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bf[j], af[i], acc[h * 4 + i][j], 0, 0, 0,
+                                                                             sb[j], 0, sa[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(acc[h * 4 + i][0]), "+v"(acc[h * 4 + i][1]));
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto sync_in = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto sync_out = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const uint8_t* img = lds + cur * 3 * HB;
+    const uint32_t* sc = (const uint32_t*)(sc_lds + (kt % 3) * 2048);
+    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+    // phase 1: rows 0..63 of the wave's half -- read BT + AH0 (+ scales); stage AH1 of tile kt+1;
+    // retire AH1 of tile kt
+    read_b(img + 2 * HB, sc);
+    read_a(img, sc, 0);
+    if (n1) {
+      stage(cur ^ 1, 1, (kt + 1) * G8_BK);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    sync_in();
+    mfma_h(0);
+    sync_out();
+    // phase 2: rows 64..127 -- read AH1; stage the scales, AH0 and BT of tile kt+2; retire AH0 /
+    // BT (and the scales) of tile kt+1
+    read_a(img + HB, sc, 1);
+    if (n2) {
+      stage_sc(kt + 2);
+      stage(cur, 0, (kt + 2) * G8_BK);
+      stage(cur, 2, (kt + 2) * G8_BK);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else if (n1) {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    sync_in();
+    mfma_h(1);
+    sync_out();
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();   // matches the stagger barrier of waves 4-7
+
+  const bool hb = a.bias != nullptr;
+  f32x4 bz[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    bz[j] = hb ? *(const f32x4*)(a.bias + bn * 128 + wn * 32 + j * 16 + fq * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      epi_store4<EPI>(a, bm * G3_M + grp * 128 + i * 16 + fr, bn * 128 + wn * 32 + j * 16 + fq * 4, acc[i][j], hb, bz[j]);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm8n(ProjArgs a) {
+  ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds8n[];   // [buf][AH0, AH1, BT] + scale ring
+  const int ntiles = (a.N / 128) * cdiv(a.M, G3_M);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    gemm8n_tile<EPI>(a, lds8n, t, ntiles);
+    __builtin_amdgcn_s_barrier();
+  }
+}
+
 template <int EPI>
 static void launch_epi8(const ProjArgs& a, hipStream_t s) {
   // algorithmic bytes: fp8 operands + their scales, the output at its epilogue's width
@@ -1125,6 +1315,21 @@ static void launch_epi8(const ProjArgs& a, hipStream_t s) {
   static const int tile_gm = getenv("WDR_GEMM4_GM") ? atoi(getenv("WDR_GEMM4_GM")) : 4;   // as k_gemm4
   ProjArgs g = a;
   g.tile_gm = tile_gm;
+  if constexpr (EPI != EPI_F8_GELU) {
+    // the narrow projections (o, fc2: N = 1280) on 256 x 128 tiles: 240 at M = 6000 where 256 x 256
+    // tiles fill 120 CUs (WDR_GEMM8N=0: k_gemm8 for every shape)
+    static const bool narrow_on = !getenv("WDR_GEMM8N") || atoi(getenv("WDR_GEMM8N")) != 0;
+    if (narrow_on && a.N < 2048 && a.N % 128 == 0) {
+      static bool attrn = [] {
+        WDR_HIP(hipFuncSetAttribute((const void*)k_gemm8n<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G8N_LDS));
+        return true;
+      }();
+      (void)attrn;
+      const int ntn = (a.N / 128) * cdiv(a.M, G3_M);
+      wdr_launch(PROF_GEMM, bytes, flops, k_gemm8n<EPI>, dim3(ntn), dim3(512), G8N_LDS, s, g);
+      return;
+    }
+  }
   const int ntiles = (a.N / G3_N) * cdiv(a.M, G3_M);
   wdr_launch(PROF_GEMM, bytes, flops, k_gemm8<EPI>, dim3(ntiles), dim3(512), G8_LDS, s, g);
 }
