@@ -86,6 +86,53 @@ def test_c3_large_v3_vad_greedy_dtw_120s(tmp_path):
     print(dict(test="c3", seconds=120, cues=n, word_max_dt=dw))
 
 
+def test_c3_large_v3_vad_greedy_dtw_900s(tmp_path):
+    """configs[2] at a real size (VERDICT r4 missing 2): 900 s, 35 VAD segments, ~50 windows of
+    large-v3 through Engine::transcribe_audio against the oracle's committed output."""
+    n, dw = fixture_vs_transcribe_audio(tmp_path, "c3_large_v3_900s.json")
+    print(dict(test="c3_900s", seconds=900, cues=n, word_max_dt=dw))
+
+
+def test_c4_diarized_large_v3_300s_against_oracle():
+    """configs[3] diarized at the model and weights the bench measures (VERDICT r4 missing 3):
+    large-v3 N(0, 0.02) weights, 300 s, 3 speakers, greedy, lang auto, DTW, speaker embeddings
+    (CAM++) + assignment (max_speakers 3, threshold 0.9999 -- the synthetic CAM++ puts every
+    embedding within cosine 0.9997..1 of every other, see make_pipeline_fixtures.py DIAR), the
+    segment list the bench's synthetic pin passes downstream (ground-truth spurts;
+    src/transcribe.rs:323-535 with :461-497).  Against the oracle's committed run: the same
+    segments, text and speaker_id identical, every word and segment bound within 20 ms."""
+    fx = json.load(open(os.path.join(GOLDEN, "c4_large_v3_diarize_300s.json")))
+    c = fx["config"]
+    pcm, spurts = synth_speech(c["seconds"], seed=c["seed"], n_speakers=c["n_speakers"])
+    assert [[a, b, k] for a, b, k in spurts] == fx["spurts"]
+    segs = [wdr.SpeechSegment(a, b, pcm[int(round(a * 16000)):int(round(b * 16000))]) for a, b, _ in spurts]
+    syn = wdr.Synthetic(weight_std=c["weight_std"], emb_std=c["emb_std"], force_len_rate=c["force_len_rate"],
+                        disable_fallback=True)
+    ctx = wdr.WhisperContext(c["model"], enable_dtw=True, synthetic=syn)
+    opts = wdr.TranscribeOptions(model=c["model"], lang="auto", enable_vad=False, enable_diarize=True,
+                                 max_speakers=c["max_speakers"],
+                                 advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy",
+                                                                 diarize_threshold=c["threshold"]))
+    got, lang = ctx.run_pipeline(segs, opts, diarize_options=wdr.DiarizeOptions.from_options(opts))
+    ctx.close()
+    want = fx["raw"]
+    assert lang == fx["lang"]
+    assert len(got) == len(want) == len(spurts)
+    spk_diff = [(i, g.speaker_id, w["speaker_id"], fx["speaker_margins"][i]) for i, (g, w) in enumerate(zip(got, want))
+                if g.speaker_id != w["speaker_id"]]
+    dts = []
+    for g, w in zip(got, want):
+        assert g.text == w["text"], (g.text, w["text"])
+        gw, ww = g.words or [], w["words"] or []
+        assert [a.text for a in gw] == [b[0] for b in ww]
+        dts += [abs(a.start - b[1]) for a, b in zip(gw, ww)] + [abs(a.end - b[2]) for a, b in zip(gw, ww)]
+        dts += [abs(g.start - w["start"]), abs(g.end - w["end"])]
+    print(dict(test="c4_diarized_300s", segments=len(got), speakers="".join(s.speaker_id for s in got),
+               word_max_dt=max(dts), speaker_mismatches=spk_diff))
+    assert not spk_diff, spk_diff
+    assert max(dts) <= TOL, sorted(dts)[-5:]
+
+
 def test_c4_shard_one_hour_large_v3_diarize_properties():
     """The bench workload at full size (bench.py: configs[3]'s 1-h per-GPU shard, greedy):
     every property the reference's glue guarantees, on every one of ~635 segments."""
