@@ -40,6 +40,12 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "whisper-diarize-rs_amd"))
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
+# synthetic weights (no checkpoints offline): the "alignment-conditioned" N(0, 0.05) / embeddings
+# N(0, 0.5) of the parity fixtures (tests/golden/make_pipeline_fixtures.py), whose alignment heads
+# attend peaked like trained ones -- the benched weights are the ones the +-20 ms word parity is
+# shown on (round 4 benched N(0, 0.02), near-uniform alignment heads; the work per window is the
+# same: the decode length is pinned and the fallback off)
+BENCH_WSTD, BENCH_EMB_STD = 0.05, 0.5
 MFMA_F16_PEAK_TFS = 2500.0  # dense f16/bf16 MFMA
 MFMA_FP8_PEAK_TFS = 5000.0  # dense block-scaled fp8 MFMA (MI355X_MICROARCH.md, matrix cores)
 PROF_EVERY, PROF_STEP_EVERY = 1, 64   # launches clocked in a sampled decode step, 1 in 64 steps sampled (csrc/prof.cpp step_every)
@@ -233,7 +239,7 @@ def cpu_baseline(model, segs, audio_target):
     from oracle.weights import hparams_for, synth_weights
     from oracle.whisper_full import aheads_for_model_name
     hp = hparams_for(model)
-    m = Whisper(hp, synth_weights(hp, std=0.02, emb_std=0.02))
+    m = Whisper(hp, synth_weights(hp, std=BENCH_WSTD, emb_std=BENCH_EMB_STD))
     v = Vocab(hp.n_vocab)
     # the workload sample: segments in order until audio_target seconds
     sel, audio = [], 0.0
@@ -357,7 +363,7 @@ def main_inproc(args):
     os.environ.setdefault("WDR_DEVICES", ",".join(str(g) for g in range(N)))
     devs = [int(x) for x in os.environ["WDR_DEVICES"].split(",")]
     diarize = args.seg == "diarize"
-    syn = wdr.Synthetic(weight_std=0.02, emb_std=0.02, force_len_rate=3.3, disable_fallback=True)
+    syn = wdr.Synthetic(weight_std=BENCH_WSTD, emb_std=BENCH_EMB_STD, force_len_rate=3.3, disable_fallback=True)
     t_load = time.perf_counter()
     ctx = wdr.WhisperContext(args.model, gpu_device=None, enable_dtw=True, synthetic=syn)
     if args.fp8:
@@ -470,7 +476,7 @@ def main():
             torch.cuda.synchronize()
 
     diarize = args.seg == "diarize"
-    syn = wdr.Synthetic(weight_std=0.02, emb_std=0.02, force_len_rate=3.3, disable_fallback=True)
+    syn = wdr.Synthetic(weight_std=BENCH_WSTD, emb_std=BENCH_EMB_STD, force_len_rate=3.3, disable_fallback=True)
     t_load = time.perf_counter()
     ctx = wdr.WhisperContext(args.model, gpu_device=local, enable_dtw=True, synthetic=syn)
     if args.fp8:

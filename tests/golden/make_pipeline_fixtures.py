@@ -53,8 +53,10 @@ CONFIGS = {
                 fallback=False),
 }
 
-# configs[3] (C4) diarized, on the BENCH's own weights (N(0, 0.02), embeddings N(0, 0.02): the
-# weights bench.py measures) and the bench's segmentation pin (SURVEY §8(d):
+# configs[3] (C4) diarized, on the BENCH's own weights (bench.py measures the fixtures'
+# alignment-conditioned N(0, 0.05) / embeddings N(0, 0.5) since round 5, VERDICT r4 weak 1: at
+# N(0, 0.02) the alignment heads attend near-uniformly and this fixture's words moved up to 1.7 s
+# on DTW near-ties while text and speakers matched) and the bench's segmentation pin (SURVEY §8(d):
 # in synthetic mode the segment list passed downstream is the generator's ground-truth spurt
 # table; the pyannote kernels are compared with the oracle in tests/test_gpu_diarize.py):
 # large-v3, 300 s, 3 speakers, seed 1, greedy, lang auto, DTW, speaker assignment with
@@ -63,7 +65,7 @@ CONFIGS = {
 # speaker "1"; 0.9999 separates the three synthetic voices (F0 110 / 140 / 190 Hz) on 48 of 54
 # spurts, and the fixture records each assignment's decision margin.
 DIAR = dict(file="c4_large_v3_diarize_300s.json", model="large-v3", seconds=300.0, seed=1, n_speakers=3,
-            weight_std=0.02, emb_std=0.02, max_speakers=3, threshold=0.9999)
+            weight_std=WSTD, emb_std=EMB_STD, max_speakers=3, threshold=0.9999)
 
 
 def _seg(s):

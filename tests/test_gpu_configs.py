@@ -95,7 +95,8 @@ def test_c3_large_v3_vad_greedy_dtw_900s(tmp_path):
 
 def test_c4_diarized_large_v3_300s_against_oracle():
     """configs[3] diarized at the model and weights the bench measures (VERDICT r4 missing 3):
-    large-v3 N(0, 0.02) weights, 300 s, 3 speakers, greedy, lang auto, DTW, speaker embeddings
+    large-v3 on the bench's N(0, 0.05) / N(0, 0.5) weights, 300 s, 3 speakers, greedy, lang auto,
+    DTW, speaker embeddings
     (CAM++) + assignment (max_speakers 3, threshold 0.9999 -- the synthetic CAM++ puts every
     embedding within cosine 0.9997..1 of every other, see make_pipeline_fixtures.py DIAR), the
     segment list the bench's synthetic pin passes downstream (ground-truth spurts;
@@ -138,7 +139,7 @@ def test_c4_shard_one_hour_large_v3_diarize_properties():
     every property the reference's glue guarantees, on every one of ~635 segments."""
     pcm, spurts = synth_speech(3600.0, seed=0, n_speakers=3)
     segs = [wdr.SpeechSegment(a, b, pcm[int(round(a * 16000)):int(round(b * 16000))]) for a, b, _ in spurts]
-    syn = wdr.Synthetic(weight_std=0.02, emb_std=0.02, force_len_rate=3.3, disable_fallback=True)
+    syn = wdr.Synthetic(weight_std=0.05, emb_std=0.5, force_len_rate=3.3, disable_fallback=True)   # bench.py's
     ctx = wdr.WhisperContext("large-v3", enable_dtw=True, synthetic=syn)
     opts = wdr.TranscribeOptions(model="large-v3", lang="auto", enable_vad=False, enable_diarize=True,
                                  advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
