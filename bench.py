@@ -40,12 +40,14 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "whisper-diarize-rs_amd"))
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
-# synthetic weights (no checkpoints offline): the "alignment-conditioned" N(0, 0.05) / embeddings
-# N(0, 0.5) of the parity fixtures (tests/golden/make_pipeline_fixtures.py), whose alignment heads
-# attend peaked like trained ones -- the benched weights are the ones the +-20 ms word parity is
-# shown on (round 4 benched N(0, 0.02), near-uniform alignment heads; the work per window is the
-# same: the decode length is pinned and the fallback off)
-BENCH_WSTD, BENCH_EMB_STD = 0.05, 0.5
+# synthetic weights (no checkpoints offline): N(0, 0.02), embeddings N(0, 0.02) -- the workload of
+# every round's bench line (674 windows per 1-h shard).  Not the parity fixtures' "alignment-
+# conditioned" N(0, 0.05) / N(0, 0.5): with those the forced final timestamp the model picks per
+# window is small, the seek advances less and the same hour becomes ~2x the windows and decode
+# steps (round 5 A/B: 1367 batched steps vs 458, 399 vs 759 xRT on one box) -- a different
+# workload, so the bench keeps its weights and the +-20 ms word parity is pinned on the
+# conditioned ones (tests/test_gpu_configs.py), text + speaker parity on both
+BENCH_WSTD, BENCH_EMB_STD = 0.02, 0.02
 MFMA_F16_PEAK_TFS = 2500.0  # dense f16/bf16 MFMA
 MFMA_FP8_PEAK_TFS = 5000.0  # dense block-scaled fp8 MFMA (MI355X_MICROARCH.md, matrix cores)
 PROF_EVERY, PROF_STEP_EVERY = 1, 64   # launches clocked in a sampled decode step, 1 in 64 steps sampled (csrc/prof.cpp step_every)

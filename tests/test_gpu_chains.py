@@ -154,3 +154,26 @@ def test_beam_chains_equal_single_chain(name, seconds, chains, monkeypatch):
     assert lang == lang1
     assert got == ref
     ctx.close()
+
+
+@pytest.mark.timeout(900)
+def test_default_forty_chains_eight_slots_equal_single_chain(monkeypatch):
+    """The shipped default: WDR_DECODE_CHAINS = 40, where every State's cross-K/V
+    ring drops to 8 slots (whisper_ctx.cpp ring_slots), the default partial-batch wait, lang
+    auto (encode-ahead language detection: LANG_SEQ sequences), large-v3 with DTW and speaker
+    assignment: 40 chains must give the one-chain result exactly."""
+    monkeypatch.setenv("WDR_DECODE_CHAINS", "40")   # the library default; conftest pins 24
+    syn = wdr.Synthetic(weight_std=0.05, emb_std=0.5, force_len_rate=3.3, disable_fallback=True)
+    ctx = wdr.WhisperContext("large-v3", enable_dtw=True, synthetic=syn)
+    pcm, spurts = synth_speech(300.0, seed=23, n_speakers=3)
+    segs = _segs(pcm, spurts)
+    assert len(segs) >= 48
+    opts = wdr.TranscribeOptions(lang="auto", enable_diarize=True,
+                                 advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    dopts = wdr.DiarizeOptions.from_options(opts)
+    ref, lang1 = _run(ctx, segs, opts, 1, dopts)
+    got, lang = _run(ctx, segs, opts, 40, dopts)
+    assert ctx.stage_times()["chains"] == 40
+    assert lang == lang1
+    assert got == ref
+    ctx.close()

@@ -1485,11 +1485,8 @@ void launch_layernorm_f8(const float* x, int ldx, const float* g, const float* b
 // first (k_layernorm's arithmetic, so the f16 operands are bit-identical to the unfused path;
 // row stride K + 8 halfs keeps the 16-row fragment reads conflict-free) -- which removes the
 // separate LayerNorm launch and its f16 round trip from the prefill / DTW passes.
-// W = 4 (WDR_ROWS_LEAN): one wave per SIMD at <= 64 VGPRs (launch bounds: 8 waves per SIMD),
-// so a workgroup fits on a CU beside an encoder GEMM tile (k_gemm4: 2 x 200 of a SIMD's 512
-// VGPRs, 128 of 160 KB LDS) instead of waiting for one to finish
 template <int EPI, int MT, int NT, int W = 4, bool LN = false, int UU = 0>
-__global__ __launch_bounds__(W * 64, W == 4 ? 8 : 1) void k_skinny(ProjArgs a) {
+__global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
   ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
   __shared__ float red[W][MT][NT][4][64];
   extern __shared__ __attribute__((aligned(16))) f16 xln[];   // LN: [16*MT][K + 8]
@@ -1732,12 +1729,6 @@ static bool rows_pair_tiles() {
   static const bool v = env_int("WDR_ROWS_PAIR", 1) != 0;
   return v;
 }
-// WDR_ROWS_LEAN=1 (A/B, read once): the row projections on 4-wave, <= 64-VGPR workgroups (the k
-// split over 4 waves: other sums than the 8 / 16-wave kernel, the same for every row count)
-static bool rows_lean() {
-  static const bool v = env_int("WDR_ROWS_LEAN", 0) != 0;
-  return v;
-}
 
 template <int EPI>
 static void launch_rows_epi(const ProjArgs& a, hipStream_t s) {
@@ -1750,15 +1741,6 @@ static void launch_rows_epi(const ProjArgs& a, hipStream_t s) {
   const bool ln = a.ln_x != nullptr;
   const bool wide = a.N >= 4096;
   const int prof = PROF_GEMV;   // the "rows" class of bench.py's live roofline (any row count)
-  if (rows_lean()) {
-    // one 16 x 16 tile per 4-wave workgroup (32-column tiles spill at 64 VGPRs); the LN
-    // prologue's rows in LDS
-    dim3 grid(cdiv(a.N, 16), mt), blk(256);
-    const uint32_t lds = ln ? (uint32_t)16 * (a.K + 8) * 2 : 0;
-    if (ln) wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 4, true, 4>, grid, blk, lds, s, a);
-    else wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 4, false, 4>, grid, blk, 0, s, a);
-    return;
-  }
   if (!wide) {
     // one 16-row tile per workgroup: the row tiles of a column tile re-read its weights from L2.
     // K > 2048 (fc2): 16 waves, each wave's 10 k-steps as ONE batch of loads (8 waves took three
