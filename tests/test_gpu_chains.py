@@ -167,7 +167,7 @@ def test_default_forty_chains_eight_slots_equal_single_chain(monkeypatch):
     ctx = wdr.WhisperContext("large-v3", enable_dtw=True, synthetic=syn)
     pcm, spurts = synth_speech(300.0, seed=23, n_speakers=3)
     segs = _segs(pcm, spurts)
-    assert len(segs) >= 48
+    assert len(segs) > 40
     opts = wdr.TranscribeOptions(lang="auto", enable_diarize=True,
                                  advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
     dopts = wdr.DiarizeOptions.from_options(opts)
