@@ -122,8 +122,11 @@ def test_configs4_eight_logical_devices_fp8(monkeypatch):
     pcm, spurts = synth_speech(28800.0, seed=2, n_speakers=4)
     segs = _segs(pcm, spurts)
     _progress(phase="c4 audio", segments=len(segs))
+    # speaker assignment with 4 speakers and the threshold that separates the synthetic voices
+    # (make_pipeline_fixtures.py DIAR: at the default 0.5 every segment is speaker "1")
     opts = wdr.TranscribeOptions(model="large-v3", lang="auto", enable_vad=False, enable_diarize=True,
-                                 advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+                                 max_speakers=4,
+                                 advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy", diarize_threshold=0.9999))
     dopts = wdr.DiarizeOptions.from_options(opts)
     one = wdr.WhisperContext("large-v3", gpu_device=0, enable_dtw=True, synthetic=syn)
     one.set_encoder_fp8(True)

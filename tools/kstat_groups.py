@@ -7,7 +7,7 @@ import sys
 GROUPS = [
     ("step-attn", ("k_dec_self_attn", "k_xattn_partial", "k_xattn_combine", "k_embed")),
     ("logits", ("k_logits",)),
-    ("enc-gemm", ("k_gemm<", "k_gemm2<", "k_gemm3<", "k_gemm4<", "k_gemm5<", "k_gemm8<")),
+    ("enc-gemm", ("k_gemm<", "k_gemm2<", "k_gemm3<", "k_gemm4<", "k_gemm5<", "k_gemm8<", "k_gemm8n<")),
     ("flash", ("k_flash",)),
     ("rows", ("k_skinny",)),
     ("layernorm", ("k_layernorm",)),

@@ -18,9 +18,9 @@ from collections import defaultdict
 import re
 
 # kernel classes (bench.py's live roofline classes plus the diarization stack): the encoder
-# GEMMs are k_gemm / k_gemm2..5 / k_gemm8 -- NOT the f32 VALU k_gemm32 of CAM++ / segmentation
+# GEMMs are k_gemm / k_gemm2..5 / k_gemm8 / k_gemm8n -- NOT the f32 VALU k_gemm32 of CAM++ / segmentation
 CLASSES = {
-    "gemm": re.compile(r"\bk_gemm\d?[<(]"),
+    "gemm": re.compile(r"\bk_gemm\d?n?[<(]"),
     "rows": re.compile(r"\bk_skinny<"),                       # decoder row projections (rows.h)
     "flash": re.compile(r"\bk_flash_attn(<\d+>)?\("),         # encoder self-attention
     "xattn": re.compile(r"\bk_xattn_(partial2?|mma)\b"),    # decoder cross-attention partials
