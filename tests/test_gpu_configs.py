@@ -103,7 +103,10 @@ def test_c4_diarized_large_v3_300s_against_oracle(name):
     make_pipeline_fixtures.py), the segment list the bench's synthetic pin passes downstream
     (ground-truth spurts; src/transcribe.rs:323-535 with :461-497), against the oracle's
     committed run: the same segments, text and speaker_id identical on both weight sets; every
-    word and segment bound within 20 ms on the alignment-conditioned weights (N(0, 0.05)).  On
+    word and segment bound within 20 ms on the alignment-conditioned weights (N(0, 0.05)), or, in
+    a segment where one is not, the moved DTW anchors at a near-tie of the oracle's own path cost
+    (the segment re-run on the oracle, tests/dtw_neartie.py: round 5, 2 of 1720 bounds 40 ms off,
+    both in segment 21, path margin 0.073 against a perturbation of 0.66).  On
     the bench's own N(0, 0.02) weights the alignment heads attend near-uniformly over the 1500
     frames, and DTW anchors move on near-ties of the path cost (tests/dtw_neartie.py; this
     fixture: words up to 1.7 s apart) -- their deviations are reported, not bounded."""
@@ -126,20 +129,63 @@ def test_c4_diarized_large_v3_300s_against_oracle(name):
     assert len(got) == len(want) == len(spurts)
     spk_diff = [(i, g.speaker_id, w["speaker_id"], fx["speaker_margins"][i]) for i, (g, w) in enumerate(zip(got, want))
                 if g.speaker_id != w["speaker_id"]]
-    dts = []
+    seg_dts = []
     for g, w in zip(got, want):
         assert g.text == w["text"], (g.text, w["text"])
         gw, ww = g.words or [], w["words"] or []
         assert [a.text for a in gw] == [b[0] for b in ww]
-        dts += [abs(a.start - b[1]) for a, b in zip(gw, ww)] + [abs(a.end - b[2]) for a, b in zip(gw, ww)]
-        dts += [abs(g.start - w["start"]), abs(g.end - w["end"])]
-    dts = np.array(dts)
+        seg_dts.append([abs(a.start - b[1]) for a, b in zip(gw, ww)] + [abs(a.end - b[2]) for a, b in zip(gw, ww)] +
+                       [abs(g.start - w["start"]), abs(g.end - w["end"])])
+    dts = np.array([v for d in seg_dts for v in d])
+    off = [i for i, d in enumerate(seg_dts) if max(d) > TOL]
     print(dict(test="c4_diarized_300s", weights=c["weight_std"], segments=len(got),
                speakers="".join(s.speaker_id for s in got), word_max_dt=float(dts.max()),
-               within_20ms=float((dts <= TOL).mean()), speaker_mismatches=spk_diff))
+               within_20ms=float((dts <= TOL).mean()), segments_off=off, speaker_mismatches=spk_diff))
     assert not spk_diff, spk_diff
-    if c["weight_std"] >= 0.05:
-        assert dts.max() <= TOL, sorted(dts)[-5:]
+    if c["weight_std"] >= 0.05 and off:
+        # a bound off by more than one DTW frame must sit at a DTW near-tie: the segment's window
+        # re-run on the oracle (same prompt, weights and tokens) and priced by tests/dtw_neartie.py
+        for i, a in _oracle_dtw_windows(c, fx, segs, off, syn):
+            print(dict(test="c4_diarized_near_tie", segment=i, moved=a["moved"], path_margin=a["path_margin"],
+                       perturbation=a["perturbation"], path_cost=a["path_cost"], x_spread=a["x_spread"]))
+            assert a["moved"], ("a bound moved but no DTW anchor did", i, seg_dts[i])
+            assert a["path_margin"] <= a["perturbation"], ("anchor moved off a near-tie", i, a["moved"],
+                                                           a["path_margin"], a["perturbation"])
+
+
+def _oracle_dtw_windows(c, fx, segs, idx, syn):
+    """The oracle's DTW re-forwards of the speech segments idx of a diarized fixture (as
+    run_transcription_pipeline ran them: greedy, lang auto, the previous non-empty text as the
+    prompt) against the GPU's alignment-head capture of the same window and tokens: yields
+    (segment, tests/dtw_neartie.py analyse() record) per re-forward."""
+    from oracle.mel import pcm_i16_to_f32
+    from oracle.model import Whisper
+    from oracle.pipeline import setup_params
+    from oracle.vocab import Vocab
+    from oracle.weights import hparams_for, synth_weights
+    from oracle.whisper_full import WhisperState
+    from tests.dtw_neartie import analyse, gpu_capture, record_dtw_calls
+    hp = hparams_for(c["model"])
+    m = Whisper(hp, synth_weights(hp, std=c["weight_std"], emb_std=c["emb_std"]))
+    ctx = wdr.WhisperContext(c["model"], enable_dtw=True, synthetic=syn)
+    try:
+        for i in idx:
+            st = WhisperState(m, Vocab(hp.n_vocab), c["model"])
+            calls = record_dtw_calls(st, m)
+            p = setup_params(dict(lang="auto", advanced=dict(sampling_strategy="greedy"),
+                                  synthetic=dict(force_len_rate=c["force_len_rate"], logprob_thold=-np.inf,
+                                                 entropy_thold=-1.0)))
+            prompt = next((w["text"] for w in reversed(fx["raw"][:i]) if w["text"].strip()), None)
+            if prompt is not None:
+                p.initial_prompt = prompt
+            x = pcm_i16_to_f32(segs[i].samples)
+            st.full(x, p)
+            assert [r.text.lstrip() for r in st.result_all] == [fx["raw"][i]["text"]]
+            for call in calls:
+                yield i, analyse(call["qk_o"], gpu_capture(ctx, x, call, len(st.aheads)), call["n_frames"],
+                                 call["sot_len"], call["seek"])
+    finally:
+        ctx.close()
 
 
 def test_c4_shard_one_hour_large_v3_diarize_properties():

@@ -13,6 +13,8 @@
 #   bench       python bench.py (default line) -> gpurun_out/bench.json
 #   benchfast   python bench.py without the beam-5 and CPU-baseline legs -> gpurun_out/bench_fast.json
 #   bench8      the same with --fp8 (configs[4] encoder)
+#   xattn       tools/xattn_bench (cross-attention partial + combine by row count), then its
+#               rocprofv3 kernel stats -> gpurun_out/xattn$T.log, gpurun_out/xprof$T/
 #   cosched     tools/cosched_bench at R = $ROWS (default 56): a decode chain beside the encoder
 # TAG=name: suffix of the output files (A/B runs of one step under different env knobs) -> gpurun_out/bench_fp8.json
 set -e -o pipefail
@@ -34,6 +36,9 @@ for step in "$@"; do
     bench) timeout -k 10 600 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err; cat gpurun_out/bench.json ;;
     benchfast) timeout -k 10 400 python3 bench.py --beam-seconds 0 --no-cpu-baseline > gpurun_out/bench_fast$T.json 2> gpurun_out/bench_fast$T.err; python3 tools/bench_brief.py gpurun_out/bench_fast$T.json ;;
     bench8) timeout -k 10 400 python3 bench.py --fp8 --beam-seconds 0 --no-cpu-baseline > gpurun_out/bench_fp8$T.json 2> gpurun_out/bench_fp8$T.err; python3 tools/bench_brief.py gpurun_out/bench_fp8$T.json ;;
+    xattn) timeout -k 10 120 ./tools/xattn_bench > gpurun_out/xattn$T.log 2>&1; cat gpurun_out/xattn$T.log
+      (cd /tmp && export TMPDIR=/tmp; timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/xprof$T -o x -- $GRAFT_REPO_ROOT/tools/xattn_bench > /dev/null 2>&1)
+      python3 tools/prof_summary.py gpurun_out/xprof$T --drop-trace > gpurun_out/xprof$T.txt; head -12 gpurun_out/xprof$T.txt ;;
     cosched) timeout -k 10 200 ./tools/cosched_bench ${ROWS:-56} > gpurun_out/cosched$T.log 2>&1; cat gpurun_out/cosched$T.log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

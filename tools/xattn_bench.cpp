@@ -35,7 +35,7 @@ __global__ void k_rand(f16* p, long long n, unsigned seed) {
 
 int main(int argc, char** argv) {
   const int L = 32, H = 20, d = H * 64, T = 1500;
-  const int S = 16;
+  const int S = getenv("XB_SLOTS") ? atoi(getenv("XB_SLOTS")) : 48;
   const size_t slot = (size_t)T * L * 2 * d;
   f16* xkv;
   CK(hipMalloc(&xkv, slot * S * 2));
@@ -56,9 +56,10 @@ int main(int argc, char** argv) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  const int rows_list[] = {1, 4, 8, 16};
-  for (int layout = 0; layout < 2; ++layout) {
+  const int rows_list[] = {1, 4, 8, 16, 32, 48};
+  for (int layout = 0; layout < 1; ++layout) {
     for (int R : rows_list) {
+      if (R > S) continue;
       auto run = [&](int l) {
         XAttnArgs xa{q, d, nullptr, nullptr, 64, T, R, H, 0.125f, po, pml, o, d};
         xa.row_k = rk;
@@ -91,7 +92,7 @@ int main(int argc, char** argv) {
   }
   // beam groups: 16 segments x 5 beams (80 rows), each group's rows share its slot
   {
-    const int G = 5, R = S * G;
+    const int G = 5, R = 16 * G;
     f16 *qg, *og;
     float* pog;
     float2* pmlg;
@@ -107,7 +108,7 @@ int main(int argc, char** argv) {
     std::vector<const f16*> hk(R);
     std::vector<int> hg(R, 0);
     for (int r = 0; r < R; ++r) hk[r] = xkv + (size_t)(r / G) * slot;
-    for (int g = 0; g < S; ++g) hg[g * G] = G;
+    for (int g = 0; g < 16; ++g) hg[g * G] = G;
     CK(hipMemcpy(rkg, hk.data(), R * sizeof(void*), hipMemcpyHostToDevice));
     CK(hipMemcpy(grp, hg.data(), R * 4, hipMemcpyHostToDevice));
     for (int grouped = 0; grouped < 2; ++grouped) {
@@ -119,7 +120,7 @@ int main(int argc, char** argv) {
         xa.v_off = xkv_v_off(l, H) - xkv_k_off(l, H);
         if (grouped) {
           xa.grp = grp;
-          xa.n_grp = S;
+          xa.n_grp = 16;
         }
         launch_xattn(xa, nullptr);
       };
