@@ -53,6 +53,16 @@ int main(int argc, char** argv) {
   std::vector<const f16*> h(S);
   for (int r = 0; r < S; ++r) h[r] = xkv + (size_t)r * slot;
   CK(hipMemcpy(rk, h.data(), S * sizeof(void*), hipMemcpyHostToDevice));
+  // the batched step's tables (launch_xattn_rows): every row its own group, leaders 0..S-1
+  int *grp1, *lead1;
+  CK(hipMalloc(&grp1, S * 4));
+  CK(hipMalloc(&lead1, S * 4));
+  {
+    std::vector<int> g1(S, 1), l1(S);
+    for (int r = 0; r < S; ++r) l1[r] = r;
+    CK(hipMemcpy(grp1, g1.data(), S * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(lead1, l1.data(), S * 4, hipMemcpyHostToDevice));
+  }
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
@@ -73,7 +83,15 @@ int main(int argc, char** argv) {
           xa.layer_off = (long long)l * 2 * d;
           xa.v_off = d;
         }
-        launch_xattn(xa, nullptr);
+        if (layout == 0) {   // the batched step's path (rows_forward)
+          xa.grp = grp1;
+          xa.lead = lead1;
+          xa.n_grp = xa.n_vgrp = R;
+          xa.vgrp_max = 1;
+          launch_xattn_rows(xa, nullptr);
+        } else {
+          launch_xattn(xa, nullptr);
+        }
       };
       for (int l = 0; l < L; ++l) run(l);
       CK(hipEventRecord(a, nullptr));
