@@ -127,6 +127,45 @@ def test_rows_projection_bit_identical_any_m(lib, N, K, epi):
     np.testing.assert_array_equal(one, full[257:258])
 
 
+def _proj_ln(lib, x, g, b, w, bias, epi, fused):
+    M, K = x.shape
+    N = w.shape[0]
+    out = np.zeros((M, N), np.float32)
+    xc, gc, bc = (np.ascontiguousarray(v, np.float32) for v in (x, g, b))
+    wb = _f16bits(w)
+    bb = np.ascontiguousarray(bias, np.float32)
+    _lib.check(lib.wdr_dbg_proj_ln(xc.ctypes.data_as(F32), gc.ctypes.data_as(F32), bc.ctypes.data_as(F32),
+                                   wb.ctypes.data_as(U16), bb.ctypes.data_as(F32), M, N, K, epi, int(fused),
+                                   out.ctypes.data_as(F32)))
+    return out
+
+
+@pytest.mark.parametrize("N,epi", [(3840, 0), (1280, 0), (5120, 1), (51866, 3)])
+def test_rows_ln_fused_equals_split(lib, N, epi):
+    """rows_forward normalises the projection's input rows inside the row kernel up to 64 rows
+    (csrc/rows.cpp; every batched step and prompt prefill of the step batcher): LayerNorm fused
+    into the prologue -- 16-row tiles on the narrow projections (qkv 3d, xq d), 32-row tiles on
+    fc1 (4d, GELU) and the logits (V) -- must equal the separate k_layernorm launch into f16 rows
+    followed by the same projection, bit for bit, at R = 1 .. 64 (16, 48 and 64 among them)."""
+    rng = np.random.default_rng(N + epi)
+    K = 1280
+    x = (rng.standard_normal((64, K)) * 2.0 + 0.3).astype(np.float32)
+    g = (1.0 + 0.1 * rng.standard_normal(K)).astype(np.float32)
+    b = (0.1 * rng.standard_normal(K)).astype(np.float32)
+    w = (rng.standard_normal((N, K)) * 0.03).astype(np.float16).astype(np.float32)
+    bias = (rng.standard_normal(N) * 0.1).astype(np.float32)
+    for M in (1, 16, 17, 33, 48, 64):
+        fused = _proj_ln(lib, x[:M], g, b, w, bias, epi, True)
+        split = _proj_ln(lib, x[:M], g, b, w, bias, epi, False)
+        np.testing.assert_array_equal(fused, split, err_msg="M=%d" % M)
+    # and against an fp64 LayerNorm + projection
+    xm = x[:16].astype(np.float64)
+    ln = (xm - xm.mean(1, keepdims=True)) / np.sqrt(xm.var(1, keepdims=True) + 1e-5) * g + b
+    ref = ln.astype(np.float16).astype(np.float64) @ w.T.astype(np.float64) + bias
+    want = _gelu(ref) if epi == 1 else ref
+    np.testing.assert_allclose(fused[:16], want, rtol=2e-3, atol=3e-3)
+
+
 def test_projection_logits_shape(lib):
     """decoder logits: N not a multiple of the tile (51866 x d), M = 1 (the row kernel)."""
     rng = np.random.default_rng(7)

@@ -2266,6 +2266,42 @@ int wdr_dbg_proj(const uint16_t* a16, const uint16_t* w16, const float* bias, in
   })
 }
 
+int wdr_dbg_proj_ln(const float* x, const float* gamma, const float* beta, const uint16_t* w16, const float* bias,
+                    int32_t M, int32_t N, int32_t K, int32_t epi, int32_t fused, float* out) {
+  WDR_GUARD({
+    if (M < 1 || N < 1 || K < 4 || K > 1280 || K % 32) return fail("dbg_proj_ln: M >= 1, K % 32 == 0, K <= 1280");
+    if (epi != EPI_F16 && epi != EPI_F16_GELU && epi != EPI_F32) return fail("dbg_proj_ln: epi 0, 1 or 3");
+    DevMem dx((size_t)M * K * 4), dg((size_t)K * 4), dbt((size_t)K * 4), dw((size_t)N * K * 2),
+        db(bias ? (size_t)N * 4 : 0), dh((size_t)M * K * 2), dout((size_t)M * N * 4);
+    WDR_HIP(hipMemcpy(dx.p, x, dx.bytes, hipMemcpyHostToDevice));
+    WDR_HIP(hipMemcpy(dg.p, gamma, dg.bytes, hipMemcpyHostToDevice));
+    WDR_HIP(hipMemcpy(dbt.p, beta, dbt.bytes, hipMemcpyHostToDevice));
+    WDR_HIP(hipMemcpy(dw.p, w16, dw.bytes, hipMemcpyHostToDevice));
+    if (bias) WDR_HIP(hipMemcpy(db.p, bias, db.bytes, hipMemcpyHostToDevice));
+    ProjArgs a{nullptr, K, dw.as<f16>(), K, bias ? db.as<float>() : nullptr, dout.p, N, nullptr, 0, M, N, K, epi};
+    a.rows_mma = 1;
+    if (fused) {   // rows_forward's fused form (csrc/rows.cpp)
+      a.ln_x = dx.as<float>();
+      a.ldln = K;
+      a.ln_g = dg.as<float>();
+      a.ln_b = dbt.as<float>();
+    } else {
+      launch_layernorm(dx.as<float>(), K, dg.as<float>(), dbt.as<float>(), dh.as<f16>(), K, M, K, nullptr);
+      a.A = dh.as<f16>();
+    }
+    launch_proj(a, nullptr);
+    WDR_HIP(hipDeviceSynchronize());
+    if (epi == EPI_F32) {
+      WDR_HIP(hipMemcpy(out, dout.p, dout.bytes, hipMemcpyDeviceToHost));
+    } else {
+      std::vector<f16> h((size_t)M * N);
+      WDR_HIP(hipMemcpy(h.data(), dout.p, h.size() * 2, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < h.size(); ++i) out[i] = (float)h[i];
+    }
+    return 0;
+  })
+}
+
 int wdr_dbg_attn(const uint16_t* q, const uint16_t* k, const uint16_t* v, int32_t Tq, int32_t Tk, int32_t H,
                  int32_t causal, float* out) {
   WDR_GUARD({

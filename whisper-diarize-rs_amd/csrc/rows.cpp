@@ -169,16 +169,18 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, in
   const int d = hp.n_text_state, L = hp.n_text_layer, H = hp.n_text_head;
   const float scale = 1.0f / 8.0f;
   WDR_CHECK(R >= 1 && io.tok && io.xkv, "rows forward: no rows / tables");
-  // the projection's input rows LayerNorm(x): inside the row kernel up to 32 rows (every
-  // workgroup normalises its own row tiles), above that one k_layernorm launch into io.hd -- the
-  // same arithmetic either way.  Fused at every row count the redundant per-column-tile LN cost
-  // more than the launch it saves (1-h trace: decoder rows class 4.98 vs 4.83 s over two runs).
-  // (Writing LN(x) from the residual launch's last workgroup per row tile -- an in-launch
+  // the projection's input rows LayerNorm(x): inside the row kernel up to 64 rows -- every batched
+  // step and prompt prefill the step batcher makes (every workgroup normalises its own row tiles,
+  // 16 rows on the narrow tiles, 32 on fc1's) -- above that (DTW passes, long prefills) one
+  // k_layernorm launch into io.hd; the same arithmetic either way (wdr_dbg_proj_ln,
+  // test_rows_ln_fused_equals_split).  Fused at every row count the redundant per-column-tile LN
+  // cost more than the launch it saves (1-h trace: decoder rows class 4.98 vs 4.83 s over two
+  // runs).  (Writing LN(x) from the residual launch's last workgroup per row tile -- an in-launch
   // hand-off -- measured slower still: 529 vs 557 xRT, profiles/r03/ab_lno_xfc.txt; a separate
   // residual + LayerNorm launch after split-K residual projections: profiles/r04/ab_epi4.txt.)
-  // WDR_ROWS_LN_FUSE (read once) moves the threshold: 64 measured even with 32 on the 1-h bench
-  // (737-739 vs 740-741 xRT, profiles/r04/ab_lnfuse.txt)
-  static const int ln_fuse_max = getenv("WDR_ROWS_LN_FUSE") ? atoi(getenv("WDR_ROWS_LN_FUSE")) : 32;
+  // WDR_ROWS_LN_FUSE (read once) moves the threshold (32: the round-4 default, even with 64 on the
+  // 1-h bench: 737-739 vs 740-741 xRT, profiles/r04/ab_lnfuse.txt)
+  static const int ln_fuse_max = getenv("WDR_ROWS_LN_FUSE") ? atoi(getenv("WDR_ROWS_LN_FUSE")) : 64;
   const bool fuse_ln = R <= ln_fuse_max;
   auto P = [&](const f16* A, int lda, const f16* W, const float* b, void* out, int ldo, int N, int K, int epi,
                const float* lng = nullptr, const float* lnb = nullptr) {
@@ -252,7 +254,7 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, in
     // final LayerNorm + logits of the logit rows only, gathered by lrow (compact output)
     ProjArgs a{nullptr, d, md.tok_emb, d, nullptr, io.logits, io.ldlogits, nullptr, 0, io.n_logit, hp.n_vocab, d, EPI_F32};
     a.rows_mma = 1;
-    if (io.n_logit <= 32) {
+    if (io.n_logit <= ln_fuse_max) {
       a.ln_x = io.xd;
       a.ldln = d;
       a.ln_g = md.ln_g;

@@ -177,6 +177,7 @@ _SIGS = {
     "wdr_dbg_discrete": (C.c_int, [P(f32), sz, C.c_uint32, i32, P(i32)]),
     "wdr_dbg_dtw_dp": (C.c_int, [P(f32), i32, i32, i32, P(i32), P(i32)]),
     "wdr_dbg_proj": (C.c_int, [P(C.c_uint16), P(C.c_uint16), P(f32), i32, i32, i32, i32, P(f32)]),
+    "wdr_dbg_proj_ln": (C.c_int, [P(f32), P(f32), P(f32), P(C.c_uint16), P(f32), i32, i32, i32, i32, i32, P(f32)]),
     "wdr_dbg_proj_fp8": (C.c_int, [P(C.c_uint16), P(C.c_uint16), P(f32), i32, i32, i32, i32, P(f32), P(C.c_uint8),
                                    P(C.c_uint8), P(C.c_uint8), P(C.c_uint8)]),
     "wdr_dbg_attn": (C.c_int, [P(C.c_uint16), P(C.c_uint16), P(C.c_uint16), i32, i32, i32, i32, P(f32)]),
