@@ -124,11 +124,17 @@ def test_c3_900s_fp8_encoder_agreement(tmp_path, monkeypatch):
             dts += [abs(a.start - b[1]) for a, b in zip(gw, ww)] + [abs(a.end - b[2]) for a, b in zip(gw, ww)]
         dts += [abs(g.start - w["start"]), abs(g.end - w["end"])]
     dts = np.array(dts) if dts else np.zeros(1)
-    rec = dict(test="c3_900s_fp8", cues=len(got), cues_oracle=len(want), same_text=len(same),
+    import difflib
+    gw_all = " ".join(g.text for g in got).split()
+    ww_all = " ".join(w["text"] for w in want).split()
+    wset = {w["text"] for w in want}
+    rec = dict(test="c3_900s_fp8", cues=len(got), cues_oracle=len(want), same_text_in_order=len(same),
+               same_text_anywhere=sum(g.text in wset for g in got),
+               word_seq_ratio=round(difflib.SequenceMatcher(None, gw_all, ww_all, autojunk=False).ratio(), 4),
                bounds_within_20ms=float((dts <= TOL).mean()), bound_max_dt=float(dts.max()))
     print(rec)
     os.makedirs("gpurun_out", exist_ok=True)
-    with open(os.path.join("gpurun_out", "fp8_parity.jsonl"), "a") as f:
+    with open(os.path.join("gpurun_out", "fp8_c3_agreement.jsonl"), "a") as f:
         f.write(json.dumps(rec) + "\n")
 
 
