@@ -1747,6 +1747,14 @@ static void launch_rows_epi(const ProjArgs& a, hipStream_t s) {
     // dependent batches: fc2 at 1 row 9.8 us against 5.4 us)
     if (a.K > 2048) {
       WDR_CHECK(!ln, "row projection: LN prologue needs K <= 1280");
+      if (mt >= 4 && rows_pair_tiles()) {
+        // above 48 rows two row tiles per workgroup: N/16 x mt one-CU workgroups would take a
+        // second round on 256 CUs (tools/rows_bench fc2 at 56 / 64 rows: 16.8 / 17.8 vs 20.3 /
+        // 22.1 us; at 33-48 rows the mt <= 3 tiles fit one round and stay faster alone, 12.2 vs
+        // 16.6 us).  Each wave's 10 k-steps as two batches of 5 (10 at MT = 2 spills)
+        wdr_launch(prof, bytes, flops, k_skinny<EPI, 2, 1, 16, false, 5>, dim3(cdiv(a.N, 16), cdiv(mt, 2)), dim3(1024), 0, s, a);
+        return;
+      }
       wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 16, false, 12>, dim3(cdiv(a.N, 16), mt), dim3(1024), 0, s, a);
       return;
     }

@@ -169,25 +169,25 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, in
   const int d = hp.n_text_state, L = hp.n_text_layer, H = hp.n_text_head;
   const float scale = 1.0f / 8.0f;
   WDR_CHECK(R >= 1 && io.tok && io.xkv, "rows forward: no rows / tables");
-  // the projection's input rows LayerNorm(x): inside the row kernel up to 64 rows -- every batched
-  // step and prompt prefill the step batcher makes (every workgroup normalises its own row tiles,
-  // 16 rows on the narrow tiles, 32 on fc1's) -- above that (DTW passes, long prefills) one
-  // k_layernorm launch into io.hd; the same arithmetic either way (wdr_dbg_proj_ln,
-  // test_rows_ln_fused_equals_split).  Fused at every row count the redundant per-column-tile LN
-  // cost more than the launch it saves (1-h trace: decoder rows class 4.98 vs 4.83 s over two
-  // runs).  (Writing LN(x) from the residual launch's last workgroup per row tile -- an in-launch
-  // hand-off -- measured slower still: 529 vs 557 xRT, profiles/r03/ab_lno_xfc.txt; a separate
-  // residual + LayerNorm launch after split-K residual projections: profiles/r04/ab_epi4.txt.)
-  // WDR_ROWS_LN_FUSE (read once) moves the threshold (32: the round-4 default, even with 64 on the
-  // 1-h bench: 737-739 vs 740-741 xRT, profiles/r04/ab_lnfuse.txt)
-  static const int ln_fuse_max = getenv("WDR_ROWS_LN_FUSE") ? atoi(getenv("WDR_ROWS_LN_FUSE")) : 64;
-  const bool fuse_ln = R <= ln_fuse_max;
+  // the projection's input rows LayerNorm(x): inside the row kernel's prologue (every workgroup
+  // normalises its own 16- / 32-row tiles into LDS) up to a per-projection row count, above it
+  // one k_layernorm launch into io.hd -- the same arithmetic either way (wdr_dbg_proj_ln,
+  // test_rows_ln_fused_equals_split).  The thresholds are where the fused form stops being the
+  // faster one alone (tools/rows_bench, profiles/r05/rows_ln_fc2.txt, LN launch included in the
+  // split figure): the fused prologue caps a workgroup's row tiles (LDS), so its weights are
+  // re-read once per 16 (32) rows -- xq (N = d) fused 7.1-9.2 vs 9.3 us at 40-64 rows; qkv fused
+  // 11.4 / 12.2 vs 12.0 / 12.5 us at 40 / 48 rows, 14.8 / 16.5 vs 12.9 / 13.3 at 56 / 64; fc1 fused
+  // 13.0 vs 13.5 at 40, 16.0-22.5 vs 14.2-16.0 at 48-64; the logits 117 vs 64 us at 40 rows.
+  // WDR_ROWS_LN_FUSE (read once): one threshold for all four (A/B; round 4 fused <= 32 rows).
+  static const int ln_env = getenv("WDR_ROWS_LN_FUSE") ? atoi(getenv("WDR_ROWS_LN_FUSE")) : -1;
+  const int fuse_qkv = ln_env >= 0 ? ln_env : 48, fuse_xq = ln_env >= 0 ? ln_env : 64,
+            fuse_fc1 = ln_env >= 0 ? ln_env : 40, fuse_logits = ln_env >= 0 ? ln_env : 32;
   auto P = [&](const f16* A, int lda, const f16* W, const float* b, void* out, int ldo, int N, int K, int epi,
-               const float* lng = nullptr, const float* lnb = nullptr) {
+               const float* lng = nullptr, const float* lnb = nullptr, int fuse_max = 0) {
     ProjArgs a{A, lda, W, K, b, out, ldo, nullptr, 0, R, N, K, epi};
     a.rows_mma = 1;
     if (lng) {
-      if (fuse_ln) {
+      if (R <= fuse_max) {
         a.ln_x = io.xd;
         a.ldln = d;
         a.ln_g = lng;
@@ -207,7 +207,7 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, in
     const DecLayer& e = md.dec[l];
     f16* kc = io.kc + (size_t)l * io.layer_stride;
     f16* vc = io.vc + (size_t)l * io.layer_stride;
-    ProjArgs q = P(nullptr, d, e.w_qkv, e.b_qkv, io.qkvd, 3 * d, 3 * d, d, EPI_QKV_CACHE, e.ln1_g, e.ln1_b);
+    ProjArgs q = P(nullptr, d, e.w_qkv, e.b_qkv, io.qkvd, 3 * d, 3 * d, d, EPI_QKV_CACHE, e.ln1_g, e.ln1_b, fuse_qkv);
     q.kc = kc;
     q.vc = vc;
     q.seq_stride = io.seq_stride;
@@ -220,7 +220,7 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, in
     DecSelfArgs sa{io.qkvd, 3 * d, kc, vc, io.seq_stride, d, io.seq, io.pos, io.attd, d, scale};
     launch_dec_self_attn(sa, R, H, s);
     launch_proj(P(io.attd, d, e.w_o, e.b_o, io.xd, d, d, d, EPI_F32_RESID), s);
-    launch_proj(P(nullptr, d, e.w_xq, e.b_xq, io.qx, d, d, d, EPI_F16, e.ln2_g, e.ln2_b), s);
+    launch_proj(P(nullptr, d, e.w_xq, e.b_xq, io.qx, d, d, d, EPI_F16, e.ln2_g, e.ln2_b, fuse_xq), s);
     XAttnArgs xa{io.qx, d, nullptr, nullptr, 64, XKV_T, R, H, scale, io.part_o, io.part_ml, io.attd, d};
     xa.row_k = io.xkv;
     xa.layer_off = xkv_k_off(l, H);
@@ -247,14 +247,14 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, in
     if (ctx.aheads_per_layer.size() == (size_t)L) cap_slot0 += (int)ctx.aheads_per_layer[l].size();
     if (l + 1 >= l_stop) return;   // a DTW pass: nothing after this layer's capture matters
     launch_proj(P(io.attd, d, e.w_xo, e.b_xo, io.xd, d, d, d, EPI_F32_RESID), s);
-    launch_proj(P(nullptr, d, e.w_fc1, e.b_fc1, io.mlpd, 4 * d, 4 * d, d, EPI_F16_GELU, e.ln3_g, e.ln3_b), s);
+    launch_proj(P(nullptr, d, e.w_fc1, e.b_fc1, io.mlpd, 4 * d, 4 * d, d, EPI_F16_GELU, e.ln3_g, e.ln3_b, fuse_fc1), s);
     launch_proj(P(io.mlpd, 4 * d, e.w_fc2, e.b_fc2, io.xd, d, d, 4 * d, EPI_F32_RESID), s);
   }
   if (io.n_logit > 0) {
     // final LayerNorm + logits of the logit rows only, gathered by lrow (compact output)
     ProjArgs a{nullptr, d, md.tok_emb, d, nullptr, io.logits, io.ldlogits, nullptr, 0, io.n_logit, hp.n_vocab, d, EPI_F32};
     a.rows_mma = 1;
-    if (io.n_logit <= ln_fuse_max) {
+    if (io.n_logit <= fuse_logits) {
       a.ln_x = io.xd;
       a.ldln = d;
       a.ln_g = md.ln_g;
