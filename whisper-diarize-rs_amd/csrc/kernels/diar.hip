@@ -560,53 +560,62 @@ __device__ __forceinline__ int seg_of(const int* off, int B, int r) {
   return lo;
 }
 
-__global__ void k_im2col_2d_b(const float* X, SegRows sr, int Ttot, int F, int C, int kf, int kt, int sf, int Fo,
-                              float* col) {
+// One wave per output row (t, f): the utterance lookup and the row's position once per row, its
+// C*kf*kt columns written by the wave's lanes (coalesced); 32-bit index math (the element-wise form
+// -- a 64-bit division and a binary search per element -- moved 0.6 TB/s: 530 us per call,
+// profiles/r05/prof_graph).  The same values in the same places.
+__global__ __launch_bounds__(256) void k_im2col_2d_b(const float* X, SegRows sr, int Ttot, int F, int C, int kf,
+                                                     int kt, int sf, int Fo, float* col) {
   const int pf = (kf - 1) / 2, pt = (kt - 1) / 2;
-  const int K = C * kf * kt;
-  const long long total = (long long)Ttot * Fo * K;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const long long row = i / K;
-    const int r = (int)(i - row * K);
-    const int tg = (int)(row / Fo), f = (int)(row - (long long)tg * Fo);
+  const int kq = kf * kt, K = C * kq;
+  const int lane = threadIdx.x & 63;
+  const int nrows = Ttot * Fo;
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < nrows; row += gridDim.x * 4) {
+    const int tg = row / Fo, f = row - tg * Fo;
     const int b = seg_of(sr.off, sr.B, tg);
-    const int t = tg - sr.off[b], T = sr.len[b];
-    const int c = r / (kf * kt), q = r - c * kf * kt;
-    const int aa = q / kt, bb = q - aa * kt;
-    const int tt = t + bb - pt, ff = f * sf + aa - pf;
-    col[i] = (tt >= 0 && tt < T && ff >= 0 && ff < F) ? X[((long long)(sr.off[b] + tt) * F + ff) * C + c] : 0.f;
+    const int t = tg - sr.off[b], T = sr.len[b], o = sr.off[b];
+    float* dst = col + (long long)row * K;
+    for (int r = lane; r < K; r += 64) {
+      const int c = r / kq, q = r - c * kq;
+      const int aa = q / kt, bb = q - aa * kt;
+      const int tt = t + bb - pt, ff = f * sf + aa - pf;
+      dst[r] = (tt >= 0 && tt < T && ff >= 0 && ff < F) ? X[((long long)(o + tt) * F + ff) * C + c] : 0.f;
+    }
   }
 }
 
 void launch_im2col_2d_b(const float* X, const SegRows& sr, int Ttot, int F, int C, int kf, int kt, int sf, int Fo,
                         float* col, hipStream_t s) {
-  const long long total = (long long)Ttot * Fo * C * kf * kt;
-  if (total <= 0) return;
-  const int grid = (int)std::min<long long>((total + 255) / 256, 16384);
+  const long long rows = (long long)Ttot * Fo;
+  if (rows <= 0 || C * kf * kt <= 0) return;
+  WDR_CHECK(rows < (1ll << 31), "im2col 2d: too many rows");
+  const int grid = (int)std::min<long long>((rows + 3) / 4, 16384);
   WDR_KLAUNCH(k_im2col_2d_b, dim3(grid), dim3(256), 0, s, X, sr, Ttot, F, C, kf, kt, sf, Fo, col);
   WDR_HIP(hipGetLastError());
 }
 
 // col[u][c*k + j] = X[in.off[b] + u_local*stride + j*dil - pad][c] within utterance b's input rows
-__global__ void k_im2col_1d_b(const float* X, int ldx, SegRows in, SegRows out, int Ttot_out, int C, int k, int stride,
-                              int dil, int pad, float* col) {
-  const long long total = (long long)Ttot_out * C * k;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const int tg = (int)(i / (C * k));
-    const int r = (int)(i - (long long)tg * C * k);
-    const int c = r / k, j = r - c * k;
+__global__ __launch_bounds__(256) void k_im2col_1d_b(const float* X, int ldx, SegRows in, SegRows out, int Ttot_out,
+                                                     int C, int k, int stride, int dil, int pad, float* col) {
+  // one wave per output row, as k_im2col_2d_b
+  const int K = C * k;
+  const int lane = threadIdx.x & 63;
+  for (int tg = blockIdx.x * 4 + (threadIdx.x >> 6); tg < Ttot_out; tg += gridDim.x * 4) {
     const int b = seg_of(out.off, out.B, tg);
-    const int t = tg - out.off[b];
-    const int u = t * stride + j * dil - pad;
-    col[i] = (u >= 0 && u < in.len[b]) ? X[(long long)(in.off[b] + u) * ldx + c] : 0.f;
+    const int t = tg - out.off[b], L = in.len[b], o = in.off[b];
+    float* dst = col + (long long)tg * K;
+    for (int r = lane; r < K; r += 64) {
+      const int c = r / k, j = r - c * k;
+      const int u = t * stride + j * dil - pad;
+      dst[r] = (u >= 0 && u < L) ? X[(long long)(o + u) * ldx + c] : 0.f;
+    }
   }
 }
 
 void launch_im2col_1d_b(const float* X, int ldx, const SegRows& in, const SegRows& out, int Ttot_out, int C, int k,
                         int stride, int dil, int pad, float* col, hipStream_t s) {
-  const long long total = (long long)Ttot_out * C * k;
-  if (total <= 0) return;
-  const int grid = (int)std::min<long long>((total + 255) / 256, 16384);
+  if (Ttot_out <= 0 || C * k <= 0) return;
+  const int grid = std::min((Ttot_out + 3) / 4, 16384);
   WDR_KLAUNCH(k_im2col_1d_b, dim3(grid), dim3(256), 0, s, X, ldx, in, out, Ttot_out, C, k, stride, dil, pad,
                      col);
   WDR_HIP(hipGetLastError());
