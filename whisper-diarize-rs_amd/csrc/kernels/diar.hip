@@ -417,9 +417,14 @@ __global__ __launch_bounds__(256) void k_fbank(const float* x, int T, const floa
                                                const float* sin_t, const float* banks, float* out) {
   __shared__ float fr[512];
   __shared__ float pw[256];
+  __shared__ float cs[512], sn[512];   // the twiddles in LDS: the DFT's 400 dependent-index reads
   __shared__ double red[4];
   const int t = blockIdx.x, tid = threadIdx.x;
   const float* src = x + (long long)t * 160;
+  for (int i = tid; i < 512; i += 256) {
+    cs[i] = cos_t[i];
+    sn[i] = sin_t[i];
+  }
   double s = 0.0;
   for (int i = tid; i < 400; i += 256) s += src[i];
   s = wave_sum_d(s);
@@ -444,8 +449,8 @@ __global__ __launch_bounds__(256) void k_fbank(const float* x, int T, const floa
     int idx = 0;
     for (int j = 0; j < 400; ++j) {
       const float v = fr[j];
-      re += v * cos_t[idx];
-      im -= v * sin_t[idx];
+      re += v * cs[idx];
+      im -= v * sn[idx];
       idx = (idx + kb) & 511;
     }
     pw[kb] = re * re + im * im;

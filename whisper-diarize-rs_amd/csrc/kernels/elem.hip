@@ -71,7 +71,10 @@ __device__ __forceinline__ int f2ord(float f) {
 }
 __device__ __forceinline__ float ord2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7FFFFFFF); }
 
-constexpr int MEL_FB = 8;   // frames per workgroup
+// frames per workgroup: 2 -- a 5-s segment (~500 frames) is 250 workgroups, the chip's width (8
+// per workgroup left ~190 of 256 CUs idle: 151 us per call, profiles/r05/prof_graph); each
+// thread's arithmetic is unchanged
+constexpr int MEL_FB = 2;
 
 __global__ __launch_bounds__(256) void k_mel_frames(MelArgs a) {
   __shared__ float xs[MEL_FB][400];
