@@ -44,3 +44,10 @@ print("chains %d, calls %d; per chain (s) and per call (ms):" % (len(by), n_call
 for k in ("wall", "decode loops", "top_up", "  DTW-queue wait", "  encoder launch", "ready wait", "energy", "post",
           "rest of full", "between calls"):
     print("  %-14s %7.3f s  %8.3f ms/call" % (k, tot[k] / nc, tot[k] * 1e3 / max(1, n_calls)))
+# the tail: when each chain's last call ends, relative to the run's first call
+t0 = min(xs[0][2] for xs in by.values())
+ends = sorted(xs[-1][3] - t0 for xs in by.values())
+if ends:
+    print("chain ends (s after the run's first call): first %.3f, median %.3f, last %.3f; last - median %.3f s"
+          % (ends[0], ends[len(ends) // 2], ends[-1], ends[-1] - ends[len(ends) // 2]))
+    print("  " + " ".join("%.2f" % e for e in ends))

@@ -59,7 +59,7 @@ int main(int argc, char** argv) {
   const int L = getenv("RB_LAYERS") ? atoi(getenv("RB_LAYERS")) : 32, d = 1280, MX = 256;
   const int copies = getenv("RB_COPIES") ? atoi(getenv("RB_COPIES")) : L;
   // rows_forward fuses the LayerNorm into the row kernel up to a per-projection row count (qkv 48,
-  // xq 64, fc1 40, logits 32: csrc/rows.cpp); RB_LN_FUSE: one threshold for all
+  // xq 64, fc1 24, logits never: csrc/rows.cpp); RB_LN_FUSE: one threshold for all
   const int ln_env = getenv("RB_LN_FUSE") ? atoi(getenv("RB_LN_FUSE")) : -1;
   Shape shapes[] = {{"qkv  +LN", 3 * d, d, EPI_F16, true},        {"o    resid", d, d, EPI_F32_RESID, false},
                     {"xq   +LN", d, d, EPI_F16, true},            {"fc1  +LN gelu", 4 * d, d, EPI_F16_GELU, true},
@@ -103,7 +103,7 @@ int main(int argc, char** argv) {
           ProjArgs a{xa, sh.K, W[l % nw], sh.K, bias, out, sh.N, nullptr, 0, M, sh.N, sh.K, sh.epi};
           a.rows_mma = 1;
           if (sh.ln) {
-            const int ln_fuse = ln_env >= 0 ? ln_env : sh.N == 3 * d ? 48 : sh.N == d ? 64 : sh.N == 4 * d ? 40 : 32;
+            const int ln_fuse = ln_env >= 0 ? ln_env : sh.N == 3 * d ? 48 : sh.N == d ? 64 : sh.N == 4 * d ? 24 : 0;
             if (M <= ln_fuse) {
               a.ln_x = xf; a.ldln = sh.K; a.ln_g = g; a.ln_b = b;
             } else {

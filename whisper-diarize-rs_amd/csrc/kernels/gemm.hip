@@ -1482,14 +1482,25 @@ void launch_layernorm_f8(const float* x, int ldx, const float* g, const float* b
 // HBM into v_mfma_f32_16x16x32_f16 (B operand = 16 contiguous bytes of one weight row per
 // lane) and reduce through LDS.  N/16 workgroups instead of N/128 keep every CU streaming.
 // LN: the A rows are LayerNorm(ln_x rows) -- each workgroup normalises its 16*MT rows into LDS
-// first (k_layernorm's arithmetic, so the f16 operands are bit-identical to the unfused path;
-// row stride K + 8 halfs keeps the 16-row fragment reads conflict-free) -- which removes the
-// separate LayerNorm launch and its f16 round trip from the prefill / DTW passes.
+// first (k_layernorm's arithmetic, so the f16 operands are bit-identical to the unfused path) --
+// which removes the separate LayerNorm launch and its f16 round trip.  The rows sit unpadded,
+// [16*MT][K] with the 16-B chunk index XOR (row & 15) (the 16-row fragment reads stay
+// conflict-free), and the waves' partial sums reuse that LDS after the K loop: 32 rows of K = 1280
+// are exactly 80 KB, so two such workgroups share a CU (with padded rows and a separate
+// reduction buffer one did).
+template <int EPI, int MT, int NT, int W>
+constexpr uint32_t skinny_red_bytes() { return (uint32_t)W * MT * NT * 4 * 64 * 4; }
+template <int EPI, int MT, int NT, int W>
+static uint32_t skinny_ln_lds(int K) {
+  return std::max((uint32_t)16 * MT * K * 2, skinny_red_bytes<EPI, MT, NT, W>());
+}
+
 template <int EPI, int MT, int NT, int W = 4, bool LN = false, int UU = 0>
 __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
   ProfClock prof_clock_(a.ts);   // sampled launches only (csrc/prof.cpp)
-  __shared__ float red[W][MT][NT][4][64];
-  extern __shared__ __attribute__((aligned(16))) f16 xln[];   // LN: [16*MT][K + 8]
+  __shared__ float red_s[LN ? 1 : W * MT * NT * 4 * 64];
+  extern __shared__ __attribute__((aligned(16))) f16 xln[];   // LN: [16*MT][K], chunk-swizzled
+  float* red = LN ? (float*)xln : red_s;   // [W][MT][NT][4][64]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 16 * NT;
   const int m0 = blockIdx.y * 16 * MT;   // row tiles split over gridDim.y workgroups (narrow N)
@@ -1499,7 +1510,7 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const int lds_ld = a.K + 8;
+  const int lds_ld = a.K;
   if constexpr (LN) {
     const int d = a.K;
     // rows past M are never stored (an MFMA output row depends on its own A row only): only
@@ -1543,7 +1554,7 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
         f16x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = (f16)((v[j][e] - mean) * scale * gg[e] + bb[e]);
-        *(f16x4*)(xln + rr * lds_ld + c) = o;
+        *(f16x4*)(xln + rr * lds_ld + ((((c >> 3) ^ (rr & 15))) << 3) + (c & 7)) = o;
       }
     }
     __syncthreads();
@@ -1554,7 +1565,7 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
     int m = m0 + i * 16 + fr;
     m = m < a.M ? m : a.M - 1;
     if (!LN && a.row_map) m = a.row_map[m];
-    arow[i] = LN ? xln + (i * 16 + fr) * lds_ld + fk : a.A + (size_t)m * a.lda + fk;
+    arow[i] = LN ? xln + (i * 16 + fr) * lds_ld : a.A + (size_t)m * a.lda + fk;
   }
   const f16* brow[NT];
 #pragma unroll
@@ -1581,7 +1592,9 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
       }
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
-        const f16x8 t = *(const f16x8*)(arow[i] + kk);
+        // LN: the fragment's 16-B chunk (kk + fk) / 8 of row i*16 + fr, swizzled by the row
+        const f16x8 t = LN ? *(const f16x8*)(arow[i] + ((((kk >> 3) | (lane >> 4)) ^ fr) << 3))
+                           : *(const f16x8*)(arow[i] + kk);
         af[u][i] = ok ? t : (f16x8){};
       }
     }
@@ -1593,18 +1606,19 @@ __global__ __launch_bounds__(W * 64) void k_skinny(ProjArgs a) {
         for (int j = 0; j < NT; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[u][i], bf[u][j], acc[i][j], 0, 0, 0);
   }
+  if constexpr (LN) __syncthreads();   // every wave's reads of the rows done before red reuses them
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) red[wid][i][j][r][lane] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r) red[(((wid * MT + i) * NT + j) * 4 + r) * 64 + lane] = acc[i][j][r];
   __syncthreads();
   for (int e = threadIdx.x; e < MT * NT * 4 * 64; e += W * 64) {
     const int l = e & 63, r = (e >> 6) & 3, j = (e >> 8) % NT, i = (e >> 8) / NT;
     float v = 0.f;
 #pragma unroll
-    for (int w = 0; w < W; ++w) v += red[w][i][j][r][l];
+    for (int w = 0; w < W; ++w) v += red[(((w * MT + i) * NT + j) * 4 + r) * 64 + l];
     const int row = m0 + i * 16 + (l >> 4) * 4 + r, col = n0 + j * 16 + (l & 15);
     epi_store<EPI>(a, row, col, v);
   }
@@ -1765,16 +1779,15 @@ static void launch_rows_epi(const ProjArgs& a, hipStream_t s) {
       return;
     }
     dim3 grid(cdiv(a.N, 16), mt), blk(512);
-    if (ln) wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 8, true>, grid, blk, (uint32_t)16 * (a.K + 8) * 2, s, a);
+    if (ln) wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 8, true>, grid, blk, skinny_ln_lds<EPI, 1, 1, 8>(a.K), s, a);
     else wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 8>, grid, blk, 0, s, a);
     return;
   }
   // wide N (fc1, logits): 32 columns per workgroup, up to 4 row tiles per workgroup
   const int mtw = std::min(mt, ln ? 2 : 4);
   dim3 grid(cdiv(a.N, 32), cdiv(mt, mtw)), blk(512);
-  const uint32_t lds = ln ? (uint32_t)16 * mtw * (a.K + 8) * 2 : 0;
 #define WDR_RW(MTV)                                                                                        \
-  if (ln) wdr_launch(prof, bytes, flops, k_skinny<EPI, MTV, 2, 8, true>, grid, blk, lds, s, a);            \
+  if (ln) wdr_launch(prof, bytes, flops, k_skinny<EPI, MTV, 2, 8, true>, grid, blk, skinny_ln_lds<EPI, MTV, 2, 8>(a.K), s, a); \
   else wdr_launch(prof, bytes, flops, k_skinny<EPI, MTV, 2, 8>, grid, blk, 0, s, a);
   if (mtw == 1) { WDR_RW(1) }
   else if (mtw == 2) { WDR_RW(2) }
@@ -1786,7 +1799,7 @@ static void launch_rows_epi(const ProjArgs& a, hipStream_t s) {
 static void launch_rows(const ProjArgs& a, hipStream_t s) {
   WDR_CHECK(a.K % 32 == 0 && a.lda % 8 == 0 && a.ldb % 8 == 0, "row projection: K % 32, lda / ldb % 8");
   // LN prologue: every workgroup normalises only its own <= 32 rows (any M)
-  WDR_CHECK(!a.ln_x || (a.K <= 1280 && a.K % 4 == 0), "row projection LN prologue: K <= 1280");
+  WDR_CHECK(!a.ln_x || (a.K <= 1280 && a.K % 128 == 0), "row projection LN prologue: K <= 1280, K % 128 == 0");
   WDR_CHECK(a.epi != EPI_QKV_CACHE || (a.kc && a.vc && a.row_seq && a.row_pos && a.d > 0), "qkv-cache epilogue args");
   switch (a.epi) {
     case EPI_F16: launch_rows_epi<EPI_F16>(a, s); break;

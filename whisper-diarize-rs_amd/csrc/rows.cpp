@@ -173,15 +173,17 @@ void rows_forward(const Context& ctx, const RowsIO& io, int R, hipStream_t s, in
   // normalises its own 16- / 32-row tiles into LDS) up to a per-projection row count, above it
   // one k_layernorm launch into io.hd -- the same arithmetic either way (wdr_dbg_proj_ln,
   // test_rows_ln_fused_equals_split).  The thresholds are where the fused form stops being the
-  // faster one alone (tools/rows_bench, profiles/r05/rows_ln_fc2.txt, LN launch included in the
-  // split figure): the fused prologue caps a workgroup's row tiles (LDS), so its weights are
-  // re-read once per 16 (32) rows -- xq (N = d) fused 7.1-9.2 vs 9.3 us at 40-64 rows; qkv fused
-  // 11.4 / 12.2 vs 12.0 / 12.5 us at 40 / 48 rows, 14.8 / 16.5 vs 12.9 / 13.3 at 56 / 64; fc1 fused
-  // 13.0 vs 13.5 at 40, 16.0-22.5 vs 14.2-16.0 at 48-64; the logits 117 vs 64 us at 40 rows.
+  // faster one alone (tools/rows_bench; profiles/r05/rows_ln_fc2.txt, rows_tilings.txt,
+  // rows_ln2.txt; the split figures include the LayerNorm launch): the fused prologue caps a
+  // workgroup's row tiles (LDS), so its weights are re-read once per 16 (32) rows, and each of the
+  // logits' 1621 column workgroups would normalise every row -- xq (N = d) fused 5.2-9.2 vs
+  // 6.7-9.4 us at 1-64 rows; qkv fused 6.0-12.2 vs 7.5-12.6 us up to 48 rows, 14.8 / 16.5 vs
+  // 12.9 / 13.4 at 56 / 64; fc1 fused 7.3-11.5 vs 8.8-11.6 up to 24 rows, 13.1-16.2 vs 12.2-14.2 at
+  // 32-48; the logits split at every count (32 rows: 48.7 vs 83.7 us).
   // WDR_ROWS_LN_FUSE (read once): one threshold for all four (A/B; round 4 fused <= 32 rows).
   static const int ln_env = getenv("WDR_ROWS_LN_FUSE") ? atoi(getenv("WDR_ROWS_LN_FUSE")) : -1;
   const int fuse_qkv = ln_env >= 0 ? ln_env : 48, fuse_xq = ln_env >= 0 ? ln_env : 64,
-            fuse_fc1 = ln_env >= 0 ? ln_env : 40, fuse_logits = ln_env >= 0 ? ln_env : 32;
+            fuse_fc1 = ln_env >= 0 ? ln_env : 24, fuse_logits = ln_env >= 0 ? ln_env : 0;
   auto P = [&](const f16* A, int lda, const f16* W, const float* b, void* out, int ldo, int N, int K, int epi,
                const float* lng = nullptr, const float* lnb = nullptr, int fuse_max = 0) {
     ProjArgs a{A, lda, W, K, b, out, ldo, nullptr, 0, R, N, K, epi};
