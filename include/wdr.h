@@ -309,14 +309,17 @@ int wdr_context_set_chains(wdr_context* c, int32_t n);
  * them (chain k on GPU k % n) with the same exact prompt fix-up; device_ids (nullable) receives
  * the ordinals, at most `cap` */
 int wdr_context_devices(const wdr_context* c, int32_t* n, int32_t* device_ids, int32_t cap);
-/* fp8 (OCP e4m3) encoder GEMMs (BASELINE configs[4]): projections and cross-K/V on the block-scaled
- * fp8 MFMA, activations quantised per row and weights per output channel (made on first use);
- * LayerNorm, attention, residuals and the decoder stay f16/f32.  Default off (WDR_FP8_ENCODER=1
- * turns it on at creation).  Not in the Rust API. */
+/* fp8 encoder GEMMs (BASELINE configs[4]): the encoder's qkv / o / fc1 / fc2 projections on the
+ * block-scaled fp8 MFMA with MX operands -- OCP e4m3 values, one E8M0 scale per 32 k (weights
+ * quantised on first use, activations by the LayerNorm / GELU kernels that produce them);
+ * attention, residuals, the cross-K/V projection and the decoder stay f16/f32.  Default off
+ * (WDR_FP8_ENCODER=1 turns it on at creation).  Not in the Rust API. */
 int wdr_context_set_encoder_fp8(wdr_context* c, int8_t on);
-/* test seam: early prompt fix-up 0 off, 1 when the predecessor chain already finished (default),
- * 2 always (chain k waits for chain k-1, then redoes its first segments from the known prompt);
- * -1 restores the WDR_EARLY_FIXUP environment default */
+/* test seam: early prompt fix-up 0 off, 1 when the predecessor chain already finished, 2 always
+ * (chain k waits for chain k-1 to finish, then redoes its first segments from the known prompt),
+ * 3 (default) chain k waits only for chain k-1's speculative pass and redoes from the prompt it
+ * left; -1 restores the WDR_EARLY_FIXUP environment default.  The fix-up rounds keep every mode
+ * exact. */
 int wdr_dbg_set_early_fixup(wdr_context* c, int32_t mode);
 /* test seam: the diarization contractions on the f32 MFMA kernel (1, default) or the VALU f32
  * kernel (0) for every later launch in the process */

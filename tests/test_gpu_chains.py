@@ -126,6 +126,10 @@ def test_forced_early_fixup_is_exact(fallback):
     if fallback:
         assert st["replay_segments"] > 0, st
     assert lang == lang1 and got == ref
+    ctx.set_early_fixup(3)   # the default: from the predecessor's speculative prompt
+    got3, _ = _run(ctx, segs, opts, 4)
+    assert ctx.stage_times()["early_fixup_segments"] > 0
+    assert got3 == ref
     ctx.set_early_fixup(0)
     got0, _ = _run(ctx, segs, opts, 4)
     assert ctx.stage_times()["early_fixup_segments"] == 0

@@ -231,8 +231,10 @@ struct wdr_context {
   std::vector<std::unique_ptr<Context>> peers;
   std::map<int, std::unique_ptr<State>> chain_st; // decode chains 1.. (multi-chain pipeline)
   int chains = 1;                                 // decode chains per GPU and run_pipeline call
-  // early prompt fix-up: 0 off, 1 when the predecessor chain has already finished (default;
-  // WDR_EARLY_FIXUP=0 turns it off), 2 always (a chain waits for its predecessor: test seam)
+  // early prompt fix-up: 0 off, 1 when the predecessor chain has already finished, 2 always (a
+  // chain waits for its predecessor to finish: test seam), 3 from the prompt the predecessor's
+  // speculative pass left (a chain waits for that pass, not for the predecessor's own fix-up; the
+  // default: WDR_EARLY_FIXUP=0..3 picks another)
   int early_fixup = -1;
   struct ChainStats {
     long long chains = 1, launches = 0, rows = 0, fixups = 0, replays = 0, early = 0;
@@ -776,9 +778,14 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
       if (converged) break;
     }
   };
-  // done[k]: chain k finished its speculative block (and its early fix-up)
+  // done[k]: chain k finished its speculative block (and its early fix-up); spec_done[k]: its
+  // speculative pass ended, spec_last[k] the prompt leaving the block then (under spec_mu: the
+  // chain's own early fix-up may rewrite spec_out of its block meanwhile)
   std::unique_ptr<std::atomic<int>[]> done(new std::atomic<int>[C]);
-  for (int k = 0; k < C; ++k) done[k] = 0;
+  std::unique_ptr<std::atomic<int>[]> spec_done(new std::atomic<int>[C]);
+  for (int k = 0; k < C; ++k) done[k] = spec_done[k] = 0;
+  std::vector<Prompt> spec_last(C, e0);
+  std::mutex spec_mu;
   auto worker = [&](int k) {
     State& st = state(k);
     try {
@@ -839,21 +846,37 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
       }
       for (auto& p : tks)
         for (auto& t : p.second) st.resolve_dtw(t, out[p.first].res);
+      std::lock_guard<std::mutex> g(spec_mu);
+      spec_last[k] = e;
     } catch (...) {
       errs[k] = std::current_exception();
       stop = true;
     }
+    spec_done[k] = 1;
     // early fix-up: if chain k-1 has already finished, the prompt leaving its block is known
     // now (as it stands) -- redo block k from it while the other chains' steps are still
     // running, its rows joining their batches instead of a fix-up round after them.  The
     // rounds below re-check it against the final prompt, so the result stays exact.
+    // Mode 3 (default): a chain that finishes before its predecessor's speculative pass waits for
+    // it (nothing else is left for it to do) and redoes from the prompt that pass left, instead of
+    // idling until the rounds -- which start only after every chain is done and then run the
+    // redone blocks as small batches at the end.  If the predecessor's own early fix-up later
+    // changes that prompt, the rounds redo this block again: exact either way.
     try {
-      const int mode = c->early_fixup >= 0 ? c->early_fixup
-                                           : !(getenv("WDR_EARLY_FIXUP") && getenv("WDR_EARLY_FIXUP")[0] == '0');
+      static const int env_mode = getenv("WDR_EARLY_FIXUP") ? atoi(getenv("WDR_EARLY_FIXUP")) : 3;
+      const int mode = c->early_fixup >= 0 ? c->early_fixup : env_mode;
       if (mode == 2 && k > 0)
         while (!done[k - 1].load() && !stop) std::this_thread::sleep_for(std::chrono::microseconds(200));
-      if (mode > 0 && !errs[k] && !stop && k > 0 && done[k - 1].load()) {
-        const Prompt et = spec_out[cut[k] - 1];
+      if (mode == 3 && k > 0)
+        while (!spec_done[k - 1].load() && !stop) std::this_thread::sleep_for(std::chrono::microseconds(200));
+      if (mode > 0 && !errs[k] && !stop && k > 0 && (mode == 3 ? spec_done[k - 1].load() : done[k - 1].load())) {
+        Prompt et;
+        if (done[k - 1].load()) {
+          et = spec_out[cut[k] - 1];   // the predecessor finished: its block no longer changes
+        } else {
+          std::lock_guard<std::mutex> g(spec_mu);
+          et = spec_last[k - 1];
+        }
         if (et != dec_in[k]) {
           redo_block(k, et, C > 1, &early_n);
           dec_in[k] = et;
@@ -1902,7 +1925,7 @@ void wdr_segment_list_free(wdr_segment_list* l) {
 int wdr_dbg_set_early_fixup(wdr_context* c, int32_t mode) {
   WDR_GUARD({
     WDR_USE(ctx, c);
-    if (mode < -1 || mode > 2) return fail("early fix-up mode: -1 (env default), 0, 1 or 2");
+    if (mode < -1 || mode > 3) return fail("early fix-up mode: -1 (env default), 0, 1, 2 or 3");
     c->early_fixup = mode;
     return 0;
   })

@@ -655,7 +655,9 @@ class WhisperContext:
         L.check(self._lib.wdr_context_set_chains(self.h, int(n)))
 
     def set_early_fixup(self, mode: int):
-        """Test seam (wdr_dbg_set_early_fixup): 0 off, 1 default, 2 forced, -1 env default."""
+        """Test seam (wdr_dbg_set_early_fixup): 0 off, 1 after the predecessor finished, 2 forced
+        (wait for the predecessor to finish), 3 from the predecessor's speculative prompt (the
+        default), -1 env default."""
         L.check(self._lib.wdr_dbg_set_early_fixup(self.h, int(mode)))
 
     def stage_times(self) -> dict:
