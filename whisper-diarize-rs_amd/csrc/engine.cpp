@@ -703,13 +703,22 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
   // contiguous blocks balanced by estimated decode cost (each chain at least one segment):
   // tokens grow with the segment's duration, plus a per-segment overhead (prompt prefill,
   // the SOT / timestamp / EOT steps, DTW re-forward) worth WDR_BALANCE_SEG_S seconds of audio
+  // WDR_BALANCE_SKEW = s (default 0.08): chain k's share of the cost scaled by 1 + s (1 - 2k /
+  // (C - 1)) -- the first encode batches are issued in chain order (below), so chain k starts
+  // decoding about k batch-times after chain 0 (1-h bench: 0.03 ... 0.69 s over 40 chains) and,
+  // one token per batched step like every chain, would end that much later on an equal share
+  // (profiles/r05/ab_balance_skew.txt: 805.6 vs 790.0 (no skew) vs 775.7 xRT (neither) mean of 3;
+  // with the skew the chains' ends show no trend in k)
   std::vector<size_t> cut(C + 1, 0);
   {
     static const double seg_s = getenv("WDR_BALANCE_SEG_S") ? atof(getenv("WDR_BALANCE_SEG_S")) : 0.0;
+    static const double skew = getenv("WDR_BALANCE_SKEW") ? atof(getenv("WDR_BALANCE_SKEW")) : 0.08;
     std::vector<double> P(N + 1, 0.0);
     for (size_t i = 0; i < N; ++i) P[i + 1] = P[i] + (double)segs[i].n_samples + seg_s * 16000.0;
+    std::vector<double> F(C + 1, 0.0);   // cumulative share of chains 0 .. k-1
+    for (int k = 0; k < C; ++k) F[k + 1] = F[k] + 1.0 + (C > 1 ? skew * (1.0 - 2.0 * k / (C - 1)) : 0.0);
     for (int k = 1; k < C; ++k) {
-      const double t = P[N] * k / C;
+      const double t = P[N] * F[k] / F[C];
       size_t x = std::lower_bound(P.begin(), P.end(), t) - P.begin();
       if (x > 0 && t - P[x - 1] <= P[std::min(x, N)] - t) --x;
       cut[k] = std::min(std::max(x, cut[k - 1] + 1), N - (size_t)(C - k));
@@ -778,6 +787,8 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
       if (converged) break;
     }
   };
+  // plan_turn: the chains issue their first encode batch in chain order (st.plan)
+  std::atomic<int> plan_turn{0};
   // done[k]: chain k finished its speculative block (and its early fix-up); spec_done[k]: its
   // speculative pass ended, spec_last[k] the prompt leaving the block then (under spec_mu: the
   // chain's own early fix-up may rewrite spec_out of its block meanwhile)
@@ -800,7 +811,17 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
         pcm.push_back(segs[i].samples);
         ns.push_back((int)segs[i].n_samples);
       }
-      st.plan(pcm.data(), ns.data(), (int)(b - a), auto_lang);
+      {
+        // the first encode batches in chain order: the shared encode streams run them first-in
+        // first-out, so chain k starts decoding about k batch-times in (WDR_BALANCE_SKEW)
+        struct Turn {
+          std::atomic<int>& t;
+          int k;
+          ~Turn() { t.store(k + 1); }
+        } turn{plan_turn, k};
+        while (plan_turn.load() < k && !stop) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        st.plan(pcm.data(), ns.data(), (int)(b - a), auto_lang);
+      }
       struct Guard {
         State& st;
         ~Guard() {
