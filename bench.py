@@ -326,7 +326,7 @@ def beam5_record(ctx, dia, vad, pcm, segs, opts, dopts, diarize, args):
 
     def run():
         if diarize:
-            dia.get_segments(pcm[:n])
+            dia.get_segments(pcm[:n], materialize=False)
         else:
             vad.get_segments(pcm[:n], materialize=False)
         return ctx.run_pipeline(sub, bopts, diarize_options=dopts)
@@ -545,8 +545,8 @@ def main():
             # segment list handed downstream is the generator's ground-truth spurt table
             # (BASELINE.md §2 pin)
             t = time.perf_counter()
-            if diarize:
-                n_seg = len(dia.get_segments(pcm))
+            if diarize:   # libwdr makes every segment's samples; the Python copy of them is skipped
+                n_seg = len(dia.get_segments(pcm, materialize=False))
             else:
                 n_seg = len(vad.get_segments(pcm, materialize=False)[1])
             vad_t[0] += time.perf_counter() - t

@@ -443,12 +443,17 @@ class Diarizer:
         cls = cls.reshape(nw, 589)
         return (cls, lp.reshape(nw, 589, 7)) if logprobs else cls
 
-    def get_segments(self, samples: np.ndarray):
+    def get_segments(self, samples: np.ndarray, materialize: bool = True):
+        """pyannote_rs::get_segments (wdr_diarize_get_segments: the segments and their samples are
+        made in libwdr).  materialize=False returns (start, end) pairs without copying every
+        segment's samples a second time into Python arrays (as Vad.get_segments)."""
         smp = np.ascontiguousarray(samples, np.int16)
         sp, ns = C.POINTER(L.SpeechSegment)(), C.c_size_t()
         L.check(self._lib.wdr_diarize_get_segments(self.h, smp.ctypes.data_as(C.POINTER(C.c_int16)), smp.size,
                                                    C.byref(sp), C.byref(ns)))
         try:
+            if not materialize:
+                return [(sp[i].start, sp[i].end) for i in range(ns.value)]
             return [SpeechSegment(sp[i].start, sp[i].end, np.ctypeslib.as_array(sp[i].samples, (sp[i].n_samples,)).copy()
                                   if sp[i].n_samples else np.zeros(0, np.int16)) for i in range(ns.value)]
         finally:
