@@ -258,22 +258,33 @@ __global__ __launch_bounds__(256, 8) void k_dec_self_attn(DecSelfArgs a) {   // 
   float qv[16];
 #pragma unroll
   for (int e = 0; e < 16; ++e) qv[e] = qs[qd * 16 + e];
+  // two 64-key passes per iteration: both passes' key loads in flight before either is scored
+  // (each key's dot is unchanged, so the scores are the same bits)
 #pragma unroll 1
-  for (int k0 = 0; k0 < nk; k0 += 64) {
-    const int k = k0 + kq;
-    const f16* kr = K + (long long)(k < nk ? k : nk - 1) * a.d + qd * 16;
-    const f16x8 k0v = *(const f16x8*)kr, k1v = *(const f16x8*)(kr + 8);
-    float t = 0.f;
+  for (int k0 = 0; k0 < nk; k0 += 128) {
+    f16x8 kv[2][2];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) t += qv[e] * (float)k0v[e];
+    for (int p = 0; p < 2; ++p) {
+      const int k = k0 + 64 * p + kq;
+      const f16* kr = K + (long long)(k < nk ? k : nk - 1) * a.d + qd * 16;
+      kv[p][0] = *(const f16x8*)kr;
+      kv[p][1] = *(const f16x8*)(kr + 8);
+    }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) t += qv[8 + e] * (float)k1v[e];
-    t += __shfl_xor(t, 1, 64);
-    t += __shfl_xor(t, 2, 64);
-    if (k < nk) {
-      t *= a.scale;
-      if (qd == 0) sc[k] = t;
-      mx = fmaxf(mx, t);
+    for (int p = 0; p < 2; ++p) {
+      const int k = k0 + 64 * p + kq;
+      float t = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t += qv[e] * (float)kv[p][0][e];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t += qv[8 + e] * (float)kv[p][1][e];
+      t += __shfl_xor(t, 1, 64);
+      t += __shfl_xor(t, 2, 64);
+      if (k < nk) {
+        t *= a.scale;
+        if (qd == 0) sc[k] = t;
+        mx = fmaxf(mx, t);
+      }
     }
   }
   mx = wave_max(mx);
@@ -290,10 +301,18 @@ __global__ __launch_bounds__(256, 8) void k_dec_self_attn(DecSelfArgs a) {   // 
   if (lane == 0) red[1][wid] = sum;
   __syncthreads();
   const float inv = 1.f / (red[1][0] + red[1][1] + red[1][2] + red[1][3]);
-  // P.V: wave w takes keys w, w+4, ... in the same order as before, with 8 independent V
-  // loads in flight per lane instead of one dependent load per key
+  // P.V: wave w takes keys w, w+4, ... in the same order as before, with 16 independent V
+  // loads in flight per lane (then 8) instead of one dependent load per key
   float acc = 0.f;
   int k = wid;
+#pragma unroll 1
+  for (; k + 60 < nk; k += 64) {
+    f16 vv[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) vv[j] = V[(long long)(k + 4 * j) * a.d + lane];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc += (float)(f16)(sc[k + 4 * j] * inv) * (float)vv[j];
+  }
 #pragma unroll 1
   for (; k + 28 < nk; k += 32) {
     f16 vv[8];
