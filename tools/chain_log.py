@@ -51,3 +51,11 @@ if ends:
     print("chain ends (s after the run's first call): first %.3f, median %.3f, last %.3f; last - median %.3f s"
           % (ends[0], ends[len(ends) // 2], ends[-1], ends[-1] - ends[len(ends) // 2]))
     print("  " + " ".join("%.2f" % e for e in ends))
+# the start: each chain's first call -- its ready wait is the wait for its first encode batch
+firsts = sorted((xs[0][2] - t0 + xs[0][5] / 1e3, c) for c, xs in by.items())
+if firsts:
+    print("first decode (s after the run's first call, entry + ready wait of the chain's first call): "
+          "first %.3f, median %.3f, last %.3f" % (firsts[0][0], firsts[len(firsts) // 2][0], firsts[-1][0]))
+    print("  " + " ".join("%d:%.2f" % (c, t) for t, c in firsts))
+    endc = {c: xs[-1][3] - t0 for c, xs in by.items()}
+    print("ends by chain: " + " ".join("%d:%.2f" % (c, endc[c]) for c in sorted(endc)))

@@ -225,6 +225,13 @@ class StepBatcher {
     const f16* dxkv = nullptr;
     float* dcap = nullptr;
     int dl_end = 1 << 30;
+    // language detection of a later segment (ln = 1): SOT at position 0 of sequence lseq on slot
+    // lxkv, one row whose language logits (the n_lang tokens after SOT) come back in lout --
+    // whisper.cpp's detection pass riding in a batched step instead of a pass of its own
+    int ln = 0;
+    int lseq = 0;
+    const f16* lxkv = nullptr;
+    float lout[100];
     // set by the launch that carried this request (under the batcher's lock)
     bool done = false;
     std::exception_ptr err;

@@ -603,6 +603,10 @@ struct State::Impl {
   std::atomic<long long> enc_windows{0};
   std::atomic<long long> lang_passes{0}, lang_rows{0};   // encode-ahead language-detection passes
   float* h_lang = nullptr;      // [(S + 1)][100]
+  // lang_src[slot]: the plan segment whose language logits h_lang[slot] holds (-1: none yet) --
+  // from the encode-ahead batch's detection pass, or from a detection row that rode in one of
+  // the chain's batched steps (lang_piggyback)
+  std::vector<int> lang_src;    // [S + 1]
   DevMem energy_d; int energy_cap = 0;
   const f16* xkv() const { return xkv_ring.as<f16>() + (size_t)cur * xkv_slot_elems; }
   // decoder: this state's own rows forwards (prompt prefills, beam / sampling steps, test seams)
@@ -806,6 +810,7 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
     D.xdtw = DevMem((size_t)RMAX * 1500 * 4);
     D.times = DevMem((RMAX + 8) * 4);
     WDR_HIP(hipHostMalloc((void**)&m.h_lang, (size_t)(kSlots + 1) * 100 * 4, hipHostMallocDefault));
+    m.lang_src.assign(kSlots + 1, -1);
     int lo = 0, hi = 0;
     WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
     WDR_HIP(hipStreamCreateWithPriority(&m.sd, hipStreamNonBlocking, lo));
@@ -1114,6 +1119,7 @@ void State::plan(const int16_t* const* pcm, const int* n, int count, bool detect
     m.plan.n.assign(n, n + count);
     m.plan.next_enq = 0;
     m.enc_err = nullptr;
+    std::fill(m.lang_src.begin(), m.lang_src.end(), -1);
   }
   top_up(0);
 }
@@ -1231,6 +1237,16 @@ void State::top_up(int j) {
   if (m.enc_err) std::rethrow_exception(m.enc_err);
 }
 
+// WDR_LANG_PIGGYBACK (default 1; read once): in a multi-chain run, a plan's later segments get
+// their language from a detection row (SOT, the segment's cross-K/V) riding in one of the chain's
+// batched steps during the segment before (StepBatcher::Req::ln) instead of a 32-layer pass of
+// their own on the encode-ahead stream per 4-window batch; the same arithmetic, so the same
+// language logits
+static bool lang_piggyback() {
+  static const bool on = !(getenv("WDR_LANG_PIGGYBACK") && atoi(getenv("WDR_LANG_PIGGYBACK")) == 0);
+  return on;
+}
+
 // issue the plan's next encode-ahead batch if the lookahead of segment j allows it: every group
 // of segments whose slots' previous occupants (j - S ...) have finished
 bool State::top_up_batch(int j) {
@@ -1305,9 +1321,14 @@ bool State::top_up_batch(int j) {
     // it runs here, off the decode chain: the batch's windows as the rows of ONE decode step,
     // each with its own cross-K/V slot and sequence (every window a one-row group: the
     // arithmetic of decoder_prefill(SOT) on the decode stream)
+    // a multi-chain run detects the language of a plan's later segments in its batched steps
+    // (lang_piggyback): the pass here only for the plan's first batch
+    const bool lang_here = m.plan.detect_lang && (g0 == 0 || !(batched && lang_piggyback()));
+    if (m.plan.detect_lang)
+      for (int k = g0; k < g1; ++k) m.lang_src[k % m.S] = lang_here ? k : -1;
     auto body = [&](RowBatch& tl, bool capturing, hipStream_t es) {
       encoder_body(ctx_, m, m.eb, g1 - g0, m.xkv_ring.as<f16>() + (size_t)slot0 * m.xkv_slot_elems, es);
-      if (!m.plan.detect_lang) return;
+      if (!lang_here) return;
       const int R = g1 - g0;
       tl.clear();   // waits for the previous batch's table copy
       const int sot = ctx_.vocab.sot;
@@ -1343,7 +1364,7 @@ bool State::top_up_batch(int j) {
     const bool sampled = graphable && prof_enc_batch();
     if (graphable && !sampled) {
       const bool f8 = ctx_.fp8_encoder.load();
-      const int key = slot0 * 4 + (f8 ? 2 : 0) + (m.plan.detect_lang ? 1 : 0);   // the batch's slots
+      const int key = slot0 * 4 + (f8 ? 2 : 0) + (lang_here ? 1 : 0);   // the batch's slots
       Impl::EncGraph& eg = m.enc_graphs[key];
       if (!eg.exec) {
         if (f8) {   // lazily built weights: not inside the capture
@@ -1392,7 +1413,7 @@ bool State::top_up_batch(int j) {
       m.plan.next_enq = g1;
     }
     m.enc_windows += g1 - g0;
-    if (m.plan.detect_lang) {
+    if (lang_here) {
       m.lang_passes++;
       m.lang_rows += g1 - g0;
     }
@@ -2501,7 +2522,8 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
     encode(seek_start);
     const double t = now_s();
     std::vector<float> ll(100);
-    if (planned && m.plan.detect_lang) {   // computed on the encode stream before `ready`
+    if (planned && m.plan.detect_lang && m.lang_src[m.cur] == job) {
+      // computed on the encode stream before `ready`, or by a detection row of an earlier batched step
       memcpy(ll.data(), m.h_lang + (size_t)m.cur * 100, 100 * 4);
     } else {
       const int sot = v.sot;
@@ -2538,6 +2560,36 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
     m.vids.max_initial_tid = -1;
   }
   m.vids.suppress_blank = params.suppress_blank ? 1 : 0;
+
+  // lang_piggyback: the next plan segment's detection row rides in one of this segment's batched
+  // steps once its window is encoded (its slot's `ready` has passed); at most one per segment
+  const int lang_nx = job + 1;
+  const bool lang_want = planned && batched && m.plan.detect_lang && lang_piggyback() &&
+                         lang_nx < (int)m.plan.n.size();
+  bool lang_done = !lang_want;
+  auto lang_ride = [&](StepBatcher::Req& rq) {
+    if (lang_done) return false;
+    {
+      std::lock_guard<std::mutex> g(m.enc_mu);   // lang_src of the segment is written before next_enq
+      if ((int)m.plan.next_enq <= lang_nx) return false;
+    }
+    const int sl = lang_nx % m.S;
+    if (m.lang_src[sl] == lang_nx) {   // the encode-ahead batch's own pass (a plan's first batch)
+      lang_done = true;
+      return false;
+    }
+    if (hipEventQuery(m.slots[sl].ready) != hipSuccess) return false;
+    rq.ln = 1;
+    rq.lseq = chain * NSLOT + LANG_SEQ;
+    rq.lxkv = m.xkv_ring.as<f16>() + (size_t)sl * m.xkv_slot_elems;
+    return true;
+  };
+  auto lang_after = [&](const StepBatcher::Req& rq) {
+    const int sl = lang_nx % m.S;
+    memcpy(m.h_lang + (size_t)sl * 100, rq.lout, 100 * 4);
+    m.lang_src[sl] = lang_nx;   // (its row and slot read are counted with the batched step's)
+    lang_done = true;
+  };
 
   int seek = seek_start;
   const int n_text_ctx = hp.n_text_ctx;
@@ -2629,8 +2681,10 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
           rq.pctl = c;
           rq.vids = m.vids;
           dtw_attach(rq);   // the previous window's re-forward rides along
+          const bool lr = lang_ride(rq);
           (pb ? pb : lockstep.b)->step(rq);
           dtw_after_step();
+          if (lr) lang_after(rq);
           tok = rq.pout;
           nosp = rq.pnosp;
           times.prefills++;
@@ -2647,7 +2701,9 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
               lockstep.b->enter();
             }
             StepBatcher::Req rq = row_req(prev_id, chain * NSLOT + seq0, pos, m.xkv(), c, m.vids);
+            const bool lr = lang_ride(rq);
             lockstep.b->step(rq);
+            if (lr) lang_after(rq);
             tok = rq.out[0];
             times.decode_steps++;
           } else {
@@ -2799,6 +2855,7 @@ struct StepBatcher::Impl {
   LogitsCtl* h_ctl = nullptr;     // [LB]
   TokOut* h_tok = nullptr;        // [LB]
   BeamCand* h_beam = nullptr;     // [LB][BEAM_KMAX]
+  float* h_lang = nullptr;        // [LB][100]: language logits of the batch's detection rows
   struct G {
     hipGraphExec_t exec = nullptr;
     VocabIds vids{};
@@ -2834,6 +2891,7 @@ StepBatcher::StepBatcher(Context& ctx) : ctx_(ctx), m_(new Impl) {
   WDR_HIP(hipHostMalloc((void**)&m.h_beam, (size_t)LB * BEAM_KMAX * sizeof(BeamCand), hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_ctl, LB * sizeof(LogitsCtl), hipHostMallocDefault));
   WDR_HIP(hipHostMalloc((void**)&m.h_tok, LB * sizeof(TokOut), hipHostMallocDefault));
+  WDR_HIP(hipHostMalloc((void**)&m.h_lang, (size_t)LB * 100 * 4, hipHostMallocDefault));
   WDR_HIP(hipEventCreate(&m.ev0));
   WDR_HIP(hipEventCreate(&m.ev1));
 }
@@ -2849,6 +2907,7 @@ StepBatcher::~StepBatcher() {
   (void)hipHostFree(m_->h_ctl);
   (void)hipHostFree(m_->h_tok);
   (void)hipHostFree(m_->h_beam);
+  (void)hipHostFree(m_->h_lang);
   if (m_->ev0) (void)hipEventDestroy(m_->ev0);
   if (m_->ev1) (void)hipEventDestroy(m_->ev1);
 }
@@ -2954,12 +3013,12 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
   Impl& m = *m_;
   RowBatch& tb = *m.tb;
   tb.clear();
-  int K = 0, n_pre = 0, n_dtw = 0;
-  std::vector<int> lidx(batch.size(), -1), lpre(batch.size(), -1);
+  int K = 0, n_pre = 0, n_dtw = 0, n_lang = 0;
+  std::vector<int> lidx(batch.size(), -1), lpre(batch.size(), -1), llang(batch.size(), -1);
   for (size_t i = 0; i < batch.size(); ++i) {
     Req* q = batch[i];
     WDR_CHECK(q->n >= 0 && q->n <= kRows && q->K >= 0 && q->K <= BEAM_KMAX && q->pn >= 0 && q->dn >= 0 &&
-                  q->n + q->pn + q->dn > 0,
+                  (q->ln == 0 || (q->ln == 1 && q->lxkv)) && q->n + q->pn + q->dn > 0,
               "step batcher: bad request");
     if (q->dn > 0) {
       RowGroupDesc g;
@@ -2997,6 +3056,17 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
       n_pre += q->pn;
       prefills++;
     }
+    if (q->ln > 0) {   // language detection row: SOT at position 0 (whisper.cpp's detection pass)
+      RowGroupDesc g;
+      g.n = 1;
+      g.tok = &q->vids.sot;
+      g.seq0 = q->lseq;
+      g.xkv = q->lxkv;
+      g.logits = 1;
+      llang[i] = tb.add(g);
+      m.h_ctl[llang[i]] = LogitsCtl{};   // its pick runs and is ignored: the language logits are read raw
+      n_lang++;
+    }
   }
   const int R = tb.R, NL = tb.n_logit;
   const VocabIds& vids = batch[0]->vids;
@@ -3008,6 +3078,11 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
     launch_logits_process(m.bufs.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), vids, NL, m.work.as<float>(),
                           m.tokout.as<TokOut>(), m.s);
     WDR_HIP(wdr_memcpy_async(m.h_tok, m.tokout.p, NL * sizeof(TokOut), hipMemcpyDeviceToHost, m.s));
+    for (size_t i = 0; i < batch.size(); ++i)
+      if (llang[i] >= 0)
+        WDR_HIP(wdr_memcpy_async(m.h_lang + (size_t)llang[i] * 100,
+                                 m.bufs.logits.as<float>() + (size_t)llang[i] * m.V + vids.sot + 1, 100 * 4,
+                                 hipMemcpyDeviceToHost, m.s));
     if (K > 0) {
       launch_logits_topk(m.bufs.logits.as<float>(), m.V, m.ctl.as<LogitsCtl>(), vids, NL, K, m.work.as<float>(),
                          m.beamc.as<BeamCand>(), m.s);
@@ -3015,7 +3090,7 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
     }
   };
   const double t_step = now_s();
-  const bool decode_only = n_pre == 0 && n_dtw == 0;
+  const bool decode_only = n_pre == 0 && n_dtw == 0 && n_lang == 0;
   // only a batch that would replay a graph draws an eager sampled run (prof.h): mixed batches
   // always run eagerly and are sampled at the base rate
   const bool sampled = decode_only && !no_graph() && prof_step();
@@ -3085,6 +3160,7 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
         if (q->K > 0)
           for (int k = 0; k < q->K; ++k) q->cand[j * q->K + k] = m.h_beam[(size_t)(lidx[i] + j) * K + k];
       }
+    if (llang[i] >= 0) memcpy(q->lout, m.h_lang + (size_t)llang[i] * 100, 100 * 4);
     if (lpre[i] >= 0) {
       q->pout = tok_of(lpre[i]);
       q->pnosp = m.h_tok[lpre[i]].nosp_prob;
