@@ -1247,6 +1247,16 @@ static bool lang_piggyback() {
   return on;
 }
 
+// WDR_LANG_FIRST (default 1; read once; with lang_piggyback): 1 = a plan's first encode batch
+// carries the detection pass; 0 = its segment 0 detects in a one-row batched step of its own
+// (full()) and segments 1..3 ride in the steps of the segments before, like every later one
+// (profiles/r05/ab_lang_first.txt: 855.4 vs 848.2 xRT mean, 4 of 4 pairs ahead but inside the
+// +-1.5 % bar, so the default stays)
+static bool lang_first() {
+  static const bool on = !lang_piggyback() || !(getenv("WDR_LANG_FIRST") && atoi(getenv("WDR_LANG_FIRST")) == 0);
+  return on;
+}
+
 // issue the plan's next encode-ahead batch if the lookahead of segment j allows it: every group
 // of segments whose slots' previous occupants (j - S ...) have finished
 bool State::top_up_batch(int j) {
@@ -1323,7 +1333,7 @@ bool State::top_up_batch(int j) {
     // arithmetic of decoder_prefill(SOT) on the decode stream)
     // a multi-chain run detects the language of a plan's later segments in its batched steps
     // (lang_piggyback): the pass here only for the plan's first batch
-    const bool lang_here = m.plan.detect_lang && (g0 == 0 || !(batched && lang_piggyback()));
+    const bool lang_here = m.plan.detect_lang && (g0 == 0 ? lang_first() : !(batched && lang_piggyback()));
     if (m.plan.detect_lang)
       for (int k = g0; k < g1; ++k) m.lang_src[k % m.S] = lang_here ? k : -1;
     auto body = [&](RowBatch& tl, bool capturing, hipStream_t es) {
@@ -2517,6 +2527,16 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
     }
   };
 
+  // (before the language detection: its row may ride in a batched step, which applies batch[0]'s
+  // vocabulary rules to every row)
+  if (params.max_initial_ts > 0.0f) {
+    const float precision = 30.0f / hp.n_audio_ctx;
+    m.vids.max_initial_tid = (int)std::round(params.max_initial_ts / precision);
+  } else {
+    m.vids.max_initial_tid = -1;
+  }
+  m.vids.suppress_blank = params.suppress_blank ? 1 : 0;
+
   std::string language = params.language;
   if (language.empty() || language == "auto") {
     encode(seek_start);
@@ -2525,6 +2545,23 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
     if (planned && m.plan.detect_lang && m.lang_src[m.cur] == job) {
       // computed on the encode stream before `ready`, or by a detection row of an earlier batched step
       memcpy(ll.data(), m.h_lang + (size_t)m.cur * 100, 100 * 4);
+    } else if (planned && batched && m.plan.detect_lang && lang_piggyback()) {
+      // not detected yet (a plan's segment 0, or its window was encoded only after the segment
+      // before had decoded): the detection row alone in a batched step, beside the other chains'
+      StepBatcher& b = ctx_.step_batcher(chain);
+      b.enter();
+      struct Leave {
+        StepBatcher* b;
+        ~Leave() { b->leave(); }
+      } leave_b{&b};
+      StepBatcher::Req rq;
+      rq.n = 0;
+      rq.ln = 1;
+      rq.lseq = chain * NSLOT + LANG_SEQ;
+      rq.lxkv = m.xkv();
+      rq.vids = m.vids;
+      b.step(rq);
+      memcpy(ll.data(), rq.lout, 100 * 4);
     } else {
       const int sot = v.sot;
       decoder_prefill(&sot, 1, 0, true, false);
@@ -2553,13 +2590,6 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
   } else {
     temps.push_back(params.temperature);
   }
-  if (params.max_initial_ts > 0.0f) {
-    const float precision = 30.0f / hp.n_audio_ctx;
-    m.vids.max_initial_tid = (int)std::round(params.max_initial_ts / precision);
-  } else {
-    m.vids.max_initial_tid = -1;
-  }
-  m.vids.suppress_blank = params.suppress_blank ? 1 : 0;
 
   // lang_piggyback: the next plan segment's detection row rides in one of this segment's batched
   // steps once its window is encoded (its slot's `ready` has passed); at most one per segment
@@ -3018,7 +3048,7 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
   for (size_t i = 0; i < batch.size(); ++i) {
     Req* q = batch[i];
     WDR_CHECK(q->n >= 0 && q->n <= kRows && q->K >= 0 && q->K <= BEAM_KMAX && q->pn >= 0 && q->dn >= 0 &&
-                  (q->ln == 0 || (q->ln == 1 && q->lxkv)) && q->n + q->pn + q->dn > 0,
+                  (q->ln == 0 || (q->ln == 1 && q->lxkv)) && q->n + q->pn + q->dn + q->ln > 0,
               "step batcher: bad request");
     if (q->dn > 0) {
       RowGroupDesc g;
