@@ -168,7 +168,9 @@ typedef struct {
    * chain) -- passes launched, the rows they carried, windows queued */
   int64_t dtwq_passes, dtwq_rows, dtwq_jobs;
   /* ABI 5: language-detection decoder passes (lang "auto": one per encode-ahead batch, its
-   * windows as one-row groups; or one SOT prefill per on-demand segment) and their rows */
+   * windows as one-row groups; or one SOT prefill per on-demand segment) and their rows.  A
+   * multi-chain run keeps the encode-ahead pass for a plan's first batch only (WDR_LANG_PIGGYBACK,
+   * default 1): later segments' detection rows ride in the batched steps and are counted there */
   int64_t lang_passes, lang_rows;
 } wdr_stage_times;
 

@@ -181,3 +181,28 @@ def test_default_forty_chains_eight_slots_equal_single_chain(monkeypatch):
     assert lang == lang1
     assert got == ref
     ctx.close()
+
+
+def test_language_detection_rides_in_batched_steps():
+    """Multi-chain runs (WDR_LANG_PIGGYBACK, default): only a plan's first encode-ahead batch
+    carries a detection pass; every later segment's SOT row rides in one of its chain's batched
+    steps (whisper_ctx.cpp lang_ride) or, when its window was encoded too late, in a batched step
+    of its own.  Per-segment languages decide each segment's prompt, so texts equal to the
+    one-chain run (a detection pass per encode batch) show the same languages."""
+    syn = wdr.Synthetic(weight_std=0.02, emb_std=0.5, force_len_rate=3.3, disable_fallback=True)
+    ctx = wdr.WhisperContext("tiny-test", synthetic=syn)
+    pcm, spurts = synth_speech(150.0, seed=7, n_speakers=2)
+    segs = _segs(pcm, spurts)
+    assert len(segs) >= 16
+    opts = wdr.TranscribeOptions(lang="auto", advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy"))
+    ref, lang1 = _run(ctx, segs, opts, 1)
+    one = ctx.stage_times()
+    got, lang = _run(ctx, segs, opts, 3)
+    three = ctx.stage_times()
+    assert lang == lang1
+    assert got == ref
+    assert one["lang_passes"] >= len(segs) // 4
+    assert three["chains"] == 3
+    # the plans' first batches (a fix-up round re-plans the segments it redoes)
+    assert 1 <= three["lang_passes"] <= 2 * 3 < one["lang_passes"], (three["lang_passes"], one["lang_passes"])
+    ctx.close()
