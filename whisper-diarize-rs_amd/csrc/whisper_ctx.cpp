@@ -7,6 +7,7 @@
 #include "prof.h"
 
 #include <algorithm>
+#include <functional>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -607,6 +608,10 @@ struct State::Impl {
   // from the encode-ahead batch's detection pass, or from a detection row that rode in one of
   // the chain's batched steps (lang_piggyback)
   std::vector<int> lang_src;    // [S + 1]
+  // set by full() for the segment's decode (lang_piggyback): attach the next segment's detection
+  // row to a batched request / take its logits after the step (decode_beam uses them too)
+  std::function<bool(StepBatcher::Req&)> lang_ride;
+  std::function<void(const StepBatcher::Req&)> lang_after;
   DevMem energy_d; int energy_cap = 0;
   const f16* xkv() const { return xkv_ring.as<f16>() + (size_t)cur * xkv_slot_elems; }
   // decoder: this state's own rows forwards (prompt prefills, beam / sampling steps, test seams)
@@ -2165,7 +2170,9 @@ Seq State::decode_beam(const std::vector<int>& prompt, const FullParams& params,
         q.xkv = m_->xkv();
         q.vids = m_->vids;
         q.K = K;
+        const bool lr = m_->lang_ride && m_->lang_ride(q);   // the next segment's detection row
         seat.b->step(q);
+        if (lr) m_->lang_after(q);
         for (int r = 0; r < q.n; ++r) {
           td[r] = q.out[r];
           for (int k = 0; k < K; ++k) bc[(size_t)r * K + k] = q.cand[r * K + k];
@@ -2620,6 +2627,15 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
     m.lang_src[sl] = lang_nx;   // (its row and slot read are counted with the batched step's)
     lang_done = true;
   };
+  m.lang_ride = lang_ride;   // for decode_beam's batched steps, cleared when this call ends
+  m.lang_after = lang_after;
+  struct LangClear {
+    Impl& m;
+    ~LangClear() {
+      m.lang_ride = nullptr;
+      m.lang_after = nullptr;
+    }
+  } lang_clear{m};
 
   int seek = seek_start;
   const int n_text_ctx = hp.n_text_ctx;
