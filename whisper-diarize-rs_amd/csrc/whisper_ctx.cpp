@@ -1144,13 +1144,17 @@ void State::unplan() {
 }
 
 // Segments the encode-ahead stream may run ahead of the decoder (WDR_ENC_AHEAD, kBatch..S;
-// default 8 = two batches).  With 16 chains planned at once, a 16-segment lookahead queues 256
-// windows up front and each chain's FIRST batch waits behind other chains' later ones: 8 lets
-// every chain start decoding sooner (1-h bench: 461 vs 446 xRT, mean of 3 / 2 runs; 4: 457).
+// default 6: a chain's next batch is issued once it is 2 segments into the current one).  With
+// 16 chains planned at once, a 16-segment lookahead queues 256 windows up front and each chain's
+// FIRST batch waits behind other chains' later ones: 8 let every chain start decoding sooner
+// (1-h bench: 461 vs 446 xRT, mean of 3 / 2 runs; 4: 457).  At 40 chains 8 still queued 320 of a
+// run's 674 windows in its first second, slowing the batched launches beside them; 6 together
+// with no detection pass on the encode stream (lang_first) measured 835.1 vs 810.9 xRT, 4 of 4
+// pairs ahead (profiles/r05/ab_ahead6_langfirst0.txt).
 static int enc_ahead(int S) {
   static const int a = [] {
     const char* e = getenv("WDR_ENC_AHEAD");
-    return e ? atoi(e) : 8;
+    return e ? atoi(e) : 6;
   }();
   return std::max(kBatch, std::min(a > 0 ? a : S, S));
 }
@@ -1252,13 +1256,13 @@ static bool lang_piggyback() {
   return on;
 }
 
-// WDR_LANG_FIRST (default 1; read once; with lang_piggyback): 1 = a plan's first encode batch
+// WDR_LANG_FIRST (default 0; read once; with lang_piggyback): 1 = a plan's first encode batch
 // carries the detection pass; 0 = its segment 0 detects in a one-row batched step of its own
 // (full()) and segments 1..3 ride in the steps of the segments before, like every later one
-// (profiles/r05/ab_lang_first.txt: 855.4 vs 848.2 xRT mean, 4 of 4 pairs ahead but inside the
-// +-1.5 % bar, so the default stays)
+// (alone: profiles/r05/ab_lang_first.txt, 855.4 vs 848.2 xRT, inside the +-1.5 % bar; with the
+// 6-segment encode-ahead, enc_ahead: 835.1 vs 810.9, ab_ahead6_langfirst0.txt)
 static bool lang_first() {
-  static const bool on = !lang_piggyback() || !(getenv("WDR_LANG_FIRST") && atoi(getenv("WDR_LANG_FIRST")) == 0);
+  static const bool on = !lang_piggyback() || (getenv("WDR_LANG_FIRST") && atoi(getenv("WDR_LANG_FIRST")) != 0);
   return on;
 }
 
