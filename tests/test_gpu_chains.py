@@ -184,9 +184,9 @@ def test_default_forty_chains_eight_slots_equal_single_chain(monkeypatch):
 
 
 def test_language_detection_rides_in_batched_steps():
-    """Multi-chain runs (WDR_LANG_PIGGYBACK, default): only a plan's first encode-ahead batch
-    carries a detection pass; every later segment's SOT row rides in one of its chain's batched
-    steps (whisper_ctx.cpp lang_ride) or, when its window was encoded too late, in a batched step
+    """Multi-chain runs (WDR_LANG_PIGGYBACK, default): no encode-ahead batch carries a detection
+    pass (WDR_LANG_FIRST=0); a plan's segment 0 detects in a one-row batched step, every later
+    segment's SOT row rides in one of its chain's batched steps (whisper_ctx.cpp lang_ride) or, when its window was encoded too late, in a batched step
     of its own.  Per-segment languages decide each segment's prompt, so texts equal to the
     one-chain run (a detection pass per encode batch) show the same languages."""
     syn = wdr.Synthetic(weight_std=0.02, emb_std=0.5, force_len_rate=3.3, disable_fallback=True)
@@ -203,6 +203,8 @@ def test_language_detection_rides_in_batched_steps():
     assert got == ref
     assert one["lang_passes"] >= len(segs) // 4
     assert three["chains"] == 3
-    # the plans' first batches (a fix-up round re-plans the segments it redoes)
-    assert 1 <= three["lang_passes"] <= 2 * 3 < one["lang_passes"], (three["lang_passes"], one["lang_passes"])
+    # none on the encode stream by default (WDR_LANG_FIRST=0: a plan's segment 0 detects in a
+    # one-row batched step); the plans' first batches with WDR_LANG_FIRST=1 (a fix-up round
+    # re-plans the segments it redoes)
+    assert three["lang_passes"] <= 2 * 3 < one["lang_passes"], (three["lang_passes"], one["lang_passes"])
     ctx.close()
