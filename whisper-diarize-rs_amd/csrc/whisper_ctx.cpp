@@ -1262,7 +1262,7 @@ static bool lang_piggyback() {
 // (alone: profiles/r05/ab_lang_first.txt, 855.4 vs 848.2 xRT, inside the +-1.5 % bar; with the
 // 6-segment encode-ahead, enc_ahead: 835.1 vs 810.9, ab_ahead6_langfirst0.txt)
 static bool lang_first() {
-  static const bool on = !lang_piggyback() || (getenv("WDR_LANG_FIRST") && atoi(getenv("WDR_LANG_FIRST")) != 0);
+  static const bool on = getenv("WDR_LANG_FIRST") && atoi(getenv("WDR_LANG_FIRST")) != 0;
   return on;
 }
 
@@ -1340,9 +1340,10 @@ bool State::top_up_batch(int j) {
     // it runs here, off the decode chain: the batch's windows as the rows of ONE decode step,
     // each with its own cross-K/V slot and sequence (every window a one-row group: the
     // arithmetic of decoder_prefill(SOT) on the decode stream)
-    // a multi-chain run detects the language of a plan's later segments in its batched steps
-    // (lang_piggyback): the pass here only for the plan's first batch
-    const bool lang_here = m.plan.detect_lang && (g0 == 0 ? lang_first() : !(batched && lang_piggyback()));
+    // a multi-chain run detects the language in its batched steps (lang_piggyback): no pass here,
+    // or only for a plan's first batch with WDR_LANG_FIRST=1; a one-chain run keeps it per batch
+    const bool ride = batched && lang_piggyback();
+    const bool lang_here = m.plan.detect_lang && (!ride || (g0 == 0 && lang_first()));
     if (m.plan.detect_lang)
       for (int k = g0; k < g1; ++k) m.lang_src[k % m.S] = lang_here ? k : -1;
     auto body = [&](RowBatch& tl, bool capturing, hipStream_t es) {
