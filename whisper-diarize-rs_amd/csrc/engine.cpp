@@ -645,6 +645,7 @@ static void emit_segment(const wdr_callbacks* cb, const Seg& s) {
 struct SegOut {
   std::vector<ResultSeg> res;
   int lang_id = 0;
+  bool lang_known = false;         // lang_id detected by the speculative pass (lang "auto")
   bool sampled = false;            // a t > 0 decoder drew random numbers
   bool rng_clean = true;           // decoded from decoder 0's initial RNG state (nothing drew before it)
   std::string rng_after;           // decoder 0's RNG right after this segment (when sampled)
@@ -770,9 +771,18 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
       ~Guard() { st.batched = false; }
     } guard{st};
     Prompt e = e_in;
+    struct Hint {
+      State& st;
+      ~Hint() { st.lang_hint = -1; }
+    } hint{st};
     for (size_t j = a; j < b && !stop; ++j) {
       const std::vector<float> x = seg_f32(segs[j]);
       st.set_rng_state(rng0);
+      // the speculative pass detected this segment's language from its window 0 alone: the
+      // re-decode keeps it instead of a detection pass of its own
+      // (WDR_LANG_HINT=0: detect again, A/B)
+      static const bool hint_on = !(getenv("WDR_LANG_HINT") && atoi(getenv("WDR_LANG_HINT")) == 0);
+      st.lang_hint = hint_on && out[j].lang_known ? out[j].lang_id : -1;
       if (st.full(with_prompt(params, e), x.data(), (int)x.size(), -1, false) != 0)
         throw std::runtime_error("failed to transcribe");
       out[j].res = st.result_all;
@@ -857,6 +867,7 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
           throw std::runtime_error("failed to transcribe");
         out[i].res = st.result_all;
         out[i].lang_id = st.lang_id;
+        out[i].lang_known = auto_lang;
         out[i].sampled = st.sampled;
         out[i].rng_clean = !drew;
         drew = drew || st.sampled;

@@ -328,6 +328,9 @@ class State {
   std::vector<float> energy;
   int chain = 0;                // decode chain (KV pool sequences chain*NSLOT ..)
   bool batched = false;         // greedy steps go through ctx.step_batcher() (multi-chain run)
+  // lang "auto": the language window 0 of this segment already detected (the engine's fix-up
+  // re-decodes; -1: detect)
+  int lang_hint = -1;
   bool sampled = false;         // the last full() drew random numbers (t > 0 decoders)
   void reset_rng();             // decoder 0's std::mt19937 back to its per-state seed
   std::string rng_state() const;

@@ -2554,7 +2554,12 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
     encode(seek_start);
     const double t = now_s();
     std::vector<float> ll(100);
-    if (planned && m.plan.detect_lang && m.lang_src[m.cur] == job) {
+    if (lang_hint >= 0 && lang_hint < 100) {
+      // the engine's fix-up re-decode of a segment whose window 0 was already detected: the
+      // detection depends on nothing but that window, so its argmax stands (lang_hint)
+      ll.assign(100, 0.f);
+      ll[lang_hint] = 1.f;
+    } else if (planned && m.plan.detect_lang && m.lang_src[m.cur] == job) {
       // computed on the encode stream before `ready`, or by a detection row of an earlier batched step
       memcpy(ll.data(), m.h_lang + (size_t)m.cur * 100, 100 * 4);
     } else if (planned && batched && m.plan.detect_lang && lang_piggyback()) {
