@@ -216,6 +216,7 @@ class StepBatcher {
     LogitsCtl pctl{};
     TokenData pout;
     float pnosp = 0.f;
+    BeamCand pcand[BEAM_KMAX];   // with K > 0: the top-K candidates of the prefill's logit row
     // DTW re-forward (dn > 0): tokens dtok at positions 0.. of sequence dseq on slot dxkv, the
     // alignment heads' probabilities captured into dcap ([n_aheads][dn][1500], device); the
     // cross-attention stops at layer dl_end
@@ -366,8 +367,9 @@ class State {
   void enc_quiesce();                // no batch in flight on the encode-ahead thread
   Seq decode_sample(const std::vector<int>& prompt, const FullParams& params, float t_cur, int seek, int seek_end,
                     int Lf, int window, float* nosp);
+  // pre_batched: the prompt is not prefilled yet -- its prefill rides in the first batched step
   Seq decode_beam(const std::vector<int>& prompt, const FullParams& params, float t_cur, int seek, int seek_end, int Lf,
-                  int window, float* nosp);
+                  int window, float* nosp, bool pre_batched = false);
   void decoder_prefill(const int* toks, int n, int seq, bool want_logits, bool capture);
   void prefill_on(const int* toks, int n, int seq, bool want_logits, bool capture, bool dtw_set, hipStream_t st,
                   const f16* xkv_base);

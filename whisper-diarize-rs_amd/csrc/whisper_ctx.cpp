@@ -2098,7 +2098,7 @@ static void score_sequence(Seq& s, const FullParams& p) {
 // there are fewer), their KV caches following their new parents.  Mirrors
 // oracle/whisper_full.py WhisperState.decode_beam.
 Seq State::decode_beam(const std::vector<int>& prompt, const FullParams& params, float t_cur, int seek, int seek_end,
-                       int Lf, int window, float* nosp) {
+                       int Lf, int window, float* nosp, bool pre_batched) {
   const Vocab& v = ctx_.vocab;
   const int K = std::max(1, std::min(params.beam_size, std::min(NSEQ, BEAM_KMAX)));
   const int n_max = ctx_.model.hp.n_text_ctx / 2 - 4;
@@ -2106,11 +2106,14 @@ Seq State::decode_beam(const std::vector<int>& prompt, const FullParams& params,
   const int delta_min = 10;
   std::vector<Seq> dec(K);
   std::vector<double> sum_all(K, 0.0);
-  {
+  // the prompt is in sequence 0 (prefilled by full(), or below in the first batched step): every
+  // decoder starts from a copy of it
+  auto share_prompt = [&]() {
     std::vector<std::pair<int, int>> share;
     for (int j = 1; j < K; ++j) share.push_back({0, j});
     kv_reorder(share, P);
-  }
+  };
+  if (!pre_batched) share_prompt();
   std::vector<BeamCand> bc((size_t)NSEQ * K);
   std::vector<TokenData> td(NSEQ);
   // multi-chain run: from the second token on, the live beams join the batched step
@@ -2143,7 +2146,37 @@ Seq State::decode_beam(const std::vector<int>& prompt, const FullParams& params,
         else { c.force_kind = 1; c.force_tok = v.eot; }
       }
     }
-    if (i == 0) {
+    if (i == 0 && pre_batched) {
+      // multi-chain run: the prompt prefill rides in the other chains' batched step; its last
+      // row's logits give the rules' pick and the top-K candidates, replicated below
+      if (!seat.b) {
+        seat.b = &ctx_.step_batcher(chain);
+        seat.b->enter();
+      }
+      StepBatcher::Req rq;
+      rq.n = 0;
+      rq.pn = P;
+      rq.ptok = prompt.data();
+      rq.pseq = chain * NSLOT + 0;
+      rq.pxkv = m_->xkv();
+      rq.pctl = ctl[0];
+      rq.vids = m_->vids;
+      rq.K = K;
+      dtw_attach(rq);   // the previous window's re-forward rides along
+      const bool lr = m_->lang_ride && m_->lang_ride(rq);
+      seat.b->step(rq);
+      dtw_after_step();
+      if (lr) m_->lang_after(rq);
+      times.prefills++;
+      td[0] = rq.pout;
+      *nosp = rq.pnosp;
+      for (int k = 0; k < K; ++k) bc[k] = rq.pcand[k];
+      share_prompt();
+      for (size_t r = 1; r < act.size(); ++r) {
+        td[r] = td[0];
+        for (int k = 0; k < K; ++k) bc[r * K + k] = bc[k];
+      }
+    } else if (i == 0) {
       // every decoder holds the prompt's logits: process once, replicate
       float ns = 0.f;
       run_logits(1, ctl.data(), td.data(), &ns);
@@ -2670,7 +2703,12 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
       // multi-chain greedy run: the prompt prefill rides in the batched step (its last row's
       // logits give the first token), so the chain never leaves the batch
       const bool pre_batched = batched && single;
-      if (!pre_batched) {
+      // multi-chain beam search at t = 0: its prompt prefill rides in a batched step too, with the
+      // prompt's top-K candidates (decode_beam)
+      // (WDR_BEAM_PREFILL=0: on the chain's own stream as before, A/B; read once)
+      static const bool beam_pre_on = !(getenv("WDR_BEAM_PREFILL") && atoi(getenv("WDR_BEAM_PREFILL")) == 0);
+      const bool beam_pre = beam_pre_on && batched && !params.greedy && t_cur <= 0.f;
+      if (!pre_batched && !beam_pre) {
         flush_dtw();
         WDR_HIP(hipEventRecord(m.ev_p0, s_));
         decoder_prefill(prompt.data(), (int)prompt.size(), 0, true, false);
@@ -2686,7 +2724,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
       if (t_cur > 0.f) {
         sq = decode_sample(prompt, params, t_cur, seek, seek_end, Lf, window, &nosp);
       } else if (!params.greedy) {
-        sq = decode_beam(prompt, params, t_cur, seek, seek_end, Lf, window, &nosp);
+        sq = decode_beam(prompt, params, t_cur, seek, seek_end, Lf, window, &nosp, beam_pre);
       }
       // multi-chain run: from the second token on, this chain's row joins the batched step
       struct Lockstep {
@@ -3098,8 +3136,8 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
       g.logits = 2;
       lidx[i] = tb.add(g);
       for (int j = 0; j < q->n; ++j) m.h_ctl[lidx[i] + j] = q->ctl[j];
-      K = std::max(K, q->K);
     }
+    if (q->n > 0 || q->pn > 0) K = std::max(K, q->K);
     if (q->pn > 0) {
       RowGroupDesc g;
       g.n = q->pn;
@@ -3220,6 +3258,7 @@ void StepBatcher::launch(std::vector<Req*>& batch) {
     if (lpre[i] >= 0) {
       q->pout = tok_of(lpre[i]);
       q->pnosp = m.h_tok[lpre[i]].nosp_prob;
+      for (int k = 0; k < q->K; ++k) q->pcand[k] = m.h_beam[(size_t)lpre[i] * K + k];
     }
   }
   launches++;
