@@ -634,22 +634,15 @@ def main():
         roof = dict(roof, dominant_by="rocprofv3 kernel-time share of the benched configuration (%s)"
                     % ((trace or {}).get("source", "no committed trace")))
         if trace and roof["kernel"] in trace:
-            # the same class over the whole traced run (class-wide work / summed kernel time)
+            # the same class over the whole committed traced run (class-wide work / summed kernel
+            # time), reported beside this run's own figures and never in their place:
+            # the trace is an earlier command's, taken with host launches serialised
+            # (WDR_LAUNCH_LOCK, DESIGN.md "Faults"), so its kernels ran almost one at a time while
+            # this run overlaps the encoder with the decode chain
             roof["trace_achieved"] = trace[roof["kernel"]]["achieved"]
             roof["trace_frac"] = trace[roof["kernel"]]["frac"]
-            if not args.fp8 and args.strategy == "greedy":
-                # the committed trace is of this configuration (the default line): its class-wide
-                # figures are `roofline`'s, the live sampler's beside them.  They cannot agree: the
-                # trace runs with host launches serialised (rocprofv3's dispatch interception
-                # faults when threads launch at once, DESIGN.md "Faults") and its kernels execute
-                # almost one at a time (mean concurrency 1.03), while the live run overlaps the
-                # encoder with the decode chain (~2), so a live launch takes longer
-                roof["live_achieved"], roof["live_frac"] = roof["achieved"], roof["frac"]
-                roof["live_avg_launch_us"] = roof["avg_launch_us"]
-                roof["achieved"], roof["frac"] = roof["trace_achieved"], roof["trace_frac"]
-                roof["avg_launch_us"] = trace[roof["kernel"]]["avg_us"]
-                roof["timing"] = ("rocprofv3 kernel trace of this command (%s: class-wide algorithmic work / summed "
-                                  "kernel time); live_*: the in-run kernel clock" % trace.get("source"))
+            roof["trace_avg_launch_us"] = trace[roof["kernel"]].get("avg_us")
+            roof["trace_source"] = "%s (committed rocprofv3 trace, launch-locked)" % trace.get("source")
 
     pipe = pipeline_roofline(args.model, times, dt / args.steps)
 

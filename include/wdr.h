@@ -404,7 +404,7 @@ int wdr_dbg_proj(const uint16_t* a_f16, const uint16_t* w_f16, const float* bias
 /* epi | WDR_DBG_PROJ_GEMM1: M > 64 on the register-staged reference tile (k_gemm) whatever the
  * dispatch rule picks -- the tiled GEMM family is bit-identical to it */
 #define WDR_DBG_PROJ_GEMM1 0x800
-/* A decoder-rows projection of LayerNorm(x) (x [M][K] f32, gamma / beta [K], K <= 1280): fused = 1
+/* A decoder-rows projection of LayerNorm(x) (x [M][K] f32, gamma / beta [K], K % 128 == 0, K <= 1280): fused = 1
  * normalises inside the row kernel's prologue (every workgroup its own row tiles), 0 = a separate
  * LayerNorm launch into f16 rows first; the two must agree bit for bit at every M (rows_forward
  * fuses up to 64 rows).  epi as wdr_dbg_proj (0 / 1 / 3; out [M][N] f32) */

@@ -327,6 +327,21 @@ def cam_weights() -> dict:
     return W
 
 
+def cam_weights_conditioned(path: str) -> dict:
+    """cam_weights() with a speaker-conditioned last layer (tests/golden/make_cam_conditioning.py:
+    e = R P (dense.linear @ stats - mu), fitted on a calibration recording): dense.linear' =
+    R P dense.linear, its BN scale 1 and shift -R P mu.  Test infrastructure: the diarized
+    fixtures' embedding network, written for the GPU by tests/model_writers.py."""
+    W = cam_weights()
+    c = np.load(path)
+    RP = c["R"].astype(np.float64) @ c["P"].astype(np.float64)                  # [512][512]
+    dl = W["dense.linear"]
+    W["dense.linear"] = (RP @ dl.reshape(512, -1).astype(np.float64)).astype(np.float32).reshape(dl.shape)
+    W["dense.bn.scale"] = np.ones(512, np.float32)
+    W["dense.bn.shift"] = (-(RP @ c["mu"].astype(np.float64))).astype(np.float32)
+    return W
+
+
 def _affine(x, W, name, axis=0):
     s, b = W[name + ".scale"], W[name + ".shift"]
     shape = [1] * x.ndim

@@ -193,7 +193,8 @@ def interpolate_word_timestamps(line: str, start: float, end: float):
 def setup_params(options: dict) -> FullParams:
     """src/transcribe.rs:20-87 (the subset the options drive)."""
     adv = options.get("advanced") or {}
-    n = max(1, adv.get("best_of_or_beam_size") or 5)
+    v = adv.get("best_of_or_beam_size")
+    n = max(1, 5 if v is None else v)   # unwrap_or(5).max(1): Some(0) -> 1, None -> 5
     p = FullParams()
     p.strategy = "greedy" if adv.get("sampling_strategy") == "greedy" else "beam"
     p.best_of = n

@@ -171,19 +171,27 @@ def write_segmentation_onnx(path, seed=1, gemm=False):
 # ---------------------------------------------------------------- CAM++
 
 
-def write_campplus_onnx(path, seed=2, fused=False):
+def write_campplus_onnx(path, seed=2, fused=False, weights=None):
     """wespeaker CAMPPlus with the oracle's cam_weights().  Unfused: every BN a
     BatchNormalization node with seeded (gamma, beta, mean, var); fused: the conv+BN pairs
     become one Conv with a bias (the exporter's eval-mode fusion), standalone BNs stay.
+    weights (an oracle dict, e.g. oracle/diarize.py cam_weights_conditioned()): written exactly --
+    every BN as (gamma, beta) = (scale, shift) with mean 0, var 1, epsilon 0 (folded bit-exact by
+    the loader), the dense layer as a Conv with its bias (its BN scale must be 1).
     Returns the oracle dict of the effective weights (BN folded in double, as the loader)."""
     from oracle import diarize as D
-    W = D.cam_weights()
+    exact = weights is not None
+    W = weights if exact else D.cam_weights()
     rng = np.random.default_rng(seed)
-    eps = np.float32(1e-5)
+    eps = np.float32(0.0 if exact else 1e-5)
     g = Graph()
     out_W = {}
 
     def bn_params(name, C):
+        if exact:
+            out_W[name + ".scale"] = W[name + ".scale"]
+            out_W[name + ".shift"] = W[name + ".shift"]
+            return W[name + ".scale"], W[name + ".shift"], np.zeros(C, np.float32), np.ones(C, np.float32)
         gamma = (1.0 + 0.2 * rng.standard_normal(C)).astype(np.float32)
         beta = (0.1 * rng.standard_normal(C)).astype(np.float32)
         mean = (0.1 * rng.standard_normal(C)).astype(np.float32)
@@ -199,7 +207,7 @@ def write_campplus_onnx(path, seed=2, fused=False):
 
     def conv_bn(x, wname, bnname, w, **attrs):
         C = w.shape[0]
-        if fused:
+        if fused and not exact:
             wf = (w * (1.0 + 0.1 * rng.standard_normal((C,) + (1,) * (w.ndim - 1)))).astype(np.float32)
             b = (0.1 * rng.standard_normal(C)).astype(np.float32)
             out_W[wname] = wf
@@ -252,8 +260,12 @@ def write_campplus_onnx(path, seed=2, fused=False):
                           g.node("ReduceMean", [x], axes=[-1], keepdims=0)], axis=1)   # stats pool (shape only)
     x = g.node("Unsqueeze", [x, g.init(np.array([-1]), "i64")])
     y = conv(x, "dense.linear", W["dense.linear"])
-    if fused:   # dense conv + BN(affine=False) fused by the exporter
-        b = (0.1 * rng.standard_normal(512)).astype(np.float32)
+    if fused or exact:   # dense conv + BN(affine=False) fused by the exporter
+        if exact:
+            assert (W["dense.bn.scale"] == 1).all()
+            b = W["dense.bn.shift"]
+        else:
+            b = (0.1 * rng.standard_normal(512)).astype(np.float32)
         out_W["dense.bn.scale"] = np.ones(512, np.float32)
         out_W["dense.bn.shift"] = b
         g.nodes.pop()   # rebuild the dense conv with the fused bias

@@ -208,3 +208,36 @@ print("ok")
     env = dict(os.environ, PYTHONPATH=os.pathsep.join([os.path.join(root, "whisper-diarize-rs_amd"), root]))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, (r.stdout, r.stderr)
+
+
+@pytest.mark.parametrize("v,n", [(None, 5), (0, 1), (-3, 1), (1, 1), (3, 3), (8, 8)])
+def test_oracle_beam_size_default_matches_reference(v, n):
+    """src/transcribe.rs:22: best_of_or_beam_size.unwrap_or(5).max(1) -- Some(0) is 1, not 5
+    (libwdr csrc/engine.cpp setup_params reads it the same way)."""
+    from oracle.pipeline import setup_params
+    adv = {} if v is None else dict(best_of_or_beam_size=v)
+    for strat in (None, "greedy"):
+        if strat:
+            adv = dict(adv, sampling_strategy=strat)
+        p = setup_params(dict(advanced=adv))
+        assert p.beam_size == p.best_of == n
+
+
+def test_every_handle_entry_point_holds_its_handle():
+    """every C entry point that takes an engine / vad / diarizer / speakers / context
+    handle (other than *_free) takes a WDR_USE hold, so a released handle is rejected and an
+    in-flight call is counted busy by wdr_shutdown (a source check: no GPU needed)."""
+    import re
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "whisper-diarize-rs_amd", "csrc", "engine.cpp")).read()
+    missing, n = [], 0
+    for m in re.finditer(r"\n(?:int|void|size_t|double) (wdr_\w+)\(([^)]*)\)\s*\{", src):
+        name, args = m.group(1), m.group(2)
+        hs = re.findall(r"wdr_(engine|vad|diarizer|speakers|context)\*\s*(\w+)", args)
+        if not hs or name.endswith("_free"):
+            continue
+        n += 1
+        body = src[m.end():src.find("\n}\n", m.end())]
+        if not all(re.search(r"WDR_USE\(\w+,\s*%s\)" % h, body) for _, h in hs):
+            missing.append(name)
+    assert n >= 25 and not missing, (n, missing)

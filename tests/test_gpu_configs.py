@@ -95,6 +95,15 @@ def test_c3_large_v3_vad_greedy_dtw_900s(tmp_path):
     print(dict(test="c3_900s", seconds=900, cues=n, word_max_dt=dw))
 
 
+def test_c3_large_v3_vad_beam5_dtw_120s(tmp_path):
+    """configs[2]'s audio with the reference's DEFAULT decode (VERDICT r5 missing 4): beam search,
+    5 beams (src/transcribe.rs:22-33: best_of_or_beam_size None -> 5, no sampling strategy ->
+    BeamSearch), large-v3, Silero VAD, DTW, lang auto, through Engine::transcribe_audio against
+    the oracle's committed output."""
+    n, dw = fixture_vs_transcribe_audio(tmp_path, "c3_large_v3_beam5_120s.json")
+    print(dict(test="c3_beam5", seconds=120, cues=n, word_max_dt=dw))
+
+
 def test_c3_900s_fp8_encoder_agreement(tmp_path, monkeypatch):
     """configs[4]'s fp8 encoder (MX e4m3 GEMMs, WDR_FP8_ENCODER=1) on the alignment-conditioned C3
     fixture (900 s, large-v3, VAD, greedy, DTW) against the oracle's f16-path output: fp8 is a
@@ -139,7 +148,7 @@ def test_c3_900s_fp8_encoder_agreement(tmp_path, monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["c4_large_v3_diarize_300s.json", "c4_large_v3_diarize_300s_w02.json"])
-def test_c4_diarized_large_v3_300s_against_oracle(name):
+def test_c4_diarized_large_v3_300s_against_oracle(name, tmp_path):
     """configs[3] diarized at large-v3 (VERDICT r4 missing 3): 300 s, 3 speakers, greedy, lang auto,
     DTW, speaker embeddings (CAM++) + assignment (max_speakers 3, threshold 0.9999 -- the
     synthetic CAM++ puts every embedding within cosine 0.9997..1 of every other, see
@@ -151,8 +160,9 @@ def test_c4_diarized_large_v3_300s_against_oracle(name):
     (the segment re-run on the oracle, tests/dtw_neartie.py: round 5, 2 of 1720 bounds 40 ms off,
     both in segment 21, path margin 0.073 against a perturbation of 0.66).  On
     the bench's own N(0, 0.02) weights the alignment heads attend near-uniformly over the 1500
-    frames, and DTW anchors move on near-ties of the path cost (tests/dtw_neartie.py; this
-    fixture: words up to 1.7 s apart) -- their deviations are reported, not bounded."""
+    frames, and DTW anchors move on near-ties of the path cost (this fixture: words up to 1.7 s
+    apart in 5 segments): the same near-tie proof is asserted on every segment with a bound past
+    20 ms, on both weight sets."""
     fx = json.load(open(os.path.join(GOLDEN, name)))
     c = fx["config"]
     pcm, spurts = synth_speech(c["seconds"], seed=c["seed"], n_speakers=c["n_speakers"])
@@ -165,7 +175,16 @@ def test_c4_diarized_large_v3_300s_against_oracle(name):
                                  max_speakers=c["max_speakers"],
                                  advanced=wdr.AdvancedTranscribe(sampling_strategy="greedy",
                                                                  diarize_threshold=c["threshold"]))
-    got, lang = ctx.run_pipeline(segs, opts, diarize_options=wdr.DiarizeOptions.from_options(opts))
+    emb_path = None
+    if c.get("cam") == "conditioned":
+        # the speaker-conditioned CAM++ (tests/golden/make_cam_conditioning.py) through the ONNX
+        # loader, written exactly as the oracle's weights
+        from oracle.diarize import cam_weights_conditioned
+        from tests.model_writers import write_campplus_onnx
+        emb_path = str(tmp_path / "campplus_conditioned.onnx")
+        write_campplus_onnx(emb_path, weights=cam_weights_conditioned(os.path.join(GOLDEN, "cam_conditioning.npz")))
+    got, lang = ctx.run_pipeline(segs, opts, diarize_options=wdr.DiarizeOptions.from_options(
+        opts, embedding_model_path=emb_path))
     ctx.close()
     want = fx["raw"]
     assert lang == fx["lang"]
@@ -181,19 +200,35 @@ def test_c4_diarized_large_v3_300s_against_oracle(name):
                        [abs(g.start - w["start"]), abs(g.end - w["end"])])
     dts = np.array([v for d in seg_dts for v in d])
     off = [i for i, d in enumerate(seg_dts) if max(d) > TOL]
-    print(dict(test="c4_diarized_300s", weights=c["weight_std"], segments=len(got),
-               speakers="".join(s.speaker_id for s in got), word_max_dt=float(dts.max()),
-               within_20ms=float((dts <= TOL).mean()), segments_off=off, speaker_mismatches=spk_diff))
+    margins = [m for m in fx["speaker_margins"] if m is not None]
+    print(dict(test="c4_diarized_300s", weights=c["weight_std"], threshold=c["threshold"],
+               max_speakers=c["max_speakers"], cam=c.get("cam", "synthetic"), segments=len(got),
+               speakers="".join(s.speaker_id for s in got), speaker_margin_min=min(margins) if margins else None,
+               word_max_dt=float(dts.max()), within_20ms=float((dts <= TOL).mean()), segments_off=off,
+               speaker_mismatches=spk_diff))
     assert not spk_diff, spk_diff
-    if c["weight_std"] >= 0.05 and off:
+    if c.get("cam") == "conditioned":
+        # the reference's defaults separate the speakers with decisive margins
+        assert c["threshold"] == 0.5 and c["max_speakers"] is None
+        assert len(set(s.speaker_id for s in got)) == c["n_speakers"] and min(margins) >= 1e-2, min(margins)
+    if off:
         # a bound off by more than one DTW frame must sit at a DTW near-tie: the segment's window
         # re-run on the oracle (same prompt, weights and tokens) and priced by tests/dtw_neartie.py
+        moved_in = set()
         for i, a in _oracle_dtw_windows(c, fx, segs, off, syn):
-            print(dict(test="c4_diarized_near_tie", segment=i, moved=a["moved"], path_margin=a["path_margin"],
-                       perturbation=a["perturbation"], path_cost=a["path_cost"], x_spread=a["x_spread"]))
-            assert a["moved"], ("a bound moved but no DTW anchor did", i, seg_dts[i])
+            rec = dict(test="c4_diarized_near_tie", weights=c["weight_std"], segment=i, moved=a["moved"],
+                       path_margin=a["path_margin"], perturbation=a["perturbation"], path_cost=a["path_cost"],
+                       x_spread=a["x_spread"], bound_max_dt=max(seg_dts[i]))
+            print(rec)
+            os.makedirs("gpurun_out", exist_ok=True)
+            with open(os.path.join("gpurun_out", "c4_near_ties.jsonl"), "a") as f:
+                f.write(json.dumps(rec) + "\n")
+            if a["moved"]:
+                moved_in.add(i)
             assert a["path_margin"] <= a["perturbation"], ("anchor moved off a near-tie", i, a["moved"],
                                                            a["path_margin"], a["perturbation"])
+        # every segment past 20 ms has a moved anchor in one of its windows
+        assert moved_in == set(off), ("a bound moved but no DTW anchor did", sorted(set(off) - moved_in))
 
 
 def _oracle_dtw_windows(c, fx, segs, idx, syn):

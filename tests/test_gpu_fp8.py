@@ -30,7 +30,7 @@ pytestmark = [pytest.mark.gpu, pytest.mark.timeout(1200)]
 
 EMB_STD = 0.5
 PIN = wdr.Synthetic(weight_std=0.02, emb_std=EMB_STD, force_len_rate=3.3, disable_fallback=True)
-FLIP_MARGIN = {"base.en": 1.0, "large-v3": 1.0}
+FLIP_MARGIN = {"tiny.en": 1.0, "tiny-test": 1.0, "base.en": 1.0, "large-v3": 1.0}
 REPORT = os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", "fp8_parity.jsonl")
 
 
@@ -54,8 +54,10 @@ def _row_cos_min(a, b):
     return float((num / den).min())
 
 
-@pytest.mark.parametrize("name", ["base.en", "large-v3"])
+@pytest.mark.parametrize("name", ["tiny-test", "tiny.en", "base.en", "large-v3"])
 def test_fp8_encoder_against_oracle(name):
+    """tiny-test (d = 128) and tiny.en (d = 384: qkv N = 1152, o / fc2 N = 384, not multiples of
+    256 -- ADVICE r5) run on k_gemm8n's 256 x 128 tiles; base.en / large-v3 as the bench."""
     hp = hparams_for(name)
     m = Whisper(hp, synth_weights(hp, std=0.02, emb_std=EMB_STD))
     ctx = wdr.WhisperContext(name, synthetic=PIN)

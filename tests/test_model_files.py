@@ -61,3 +61,18 @@ def test_model_file_errors(tmp_path):
         wdr.model_file_tensors("silero", seg)
     with pytest.raises(wdr.WdrError, match="doesn't exist"):
         wdr.model_file_tensors("silero", str(tmp_path / "none.bin"))
+
+
+def test_campplus_onnx_conditioned_weights_exact(tmp_path):
+    """The diarized fixtures' speaker-conditioned CAM++ (tests/golden/make_cam_conditioning.py)
+    written as an ONNX file: the loader must reproduce the oracle's weights bit for bit (BN as
+    scale / shift with mean 0, var 1, epsilon 0; the conditioned dense layer with its bias)."""
+    import os
+    from oracle.diarize import cam_weights_conditioned
+    W = cam_weights_conditioned(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                             "cam_conditioning.npz"))
+    p = str(tmp_path / "cam_cond.onnx")
+    out = write_campplus_onnx(p, weights=W)
+    _same(wdr.model_file_tensors("campplus", p), out)
+    for k in W:
+        np.testing.assert_array_equal(out[k], W[k], err_msg=k)

@@ -15,6 +15,7 @@
 #   bench8      the same with --fp8 (configs[4] encoder)
 #   xattn       tools/xattn_bench (cross-attention partial + combine by row count), then its
 #               rocprofv3 kernel stats -> gpurun_out/xattn$T.log, gpurun_out/xprof$T/
+#   fp8abl      tools/fp8_ablation.py (fp8 plans on the C3 900-s fixture; FP8_PLANS = its arguments)
 #   cosched     tools/cosched_bench at R = $ROWS (default 56): a decode chain beside the encoder
 # TAG=name: suffix of the output files (A/B runs of one step under different env knobs) -> gpurun_out/bench_fp8.json
 set -e -o pipefail
@@ -39,6 +40,7 @@ for step in "$@"; do
     xattn) timeout -k 10 120 ./tools/xattn_bench > gpurun_out/xattn$T.log 2>&1; cat gpurun_out/xattn$T.log
       (cd /tmp && export TMPDIR=/tmp; timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/xprof$T -o x -- $GRAFT_REPO_ROOT/tools/xattn_bench > /dev/null 2>&1)
       python3 tools/prof_summary.py gpurun_out/xprof$T --drop-trace > gpurun_out/xprof$T.txt; head -12 gpurun_out/xprof$T.txt ;;
+    fp8abl) timeout -k 10 1100 python3 -u tools/fp8_ablation.py $FP8_PLANS > gpurun_out/fp8abl$T.log 2>&1 || { tail -30 gpurun_out/fp8abl$T.log; exit 1; }; cat gpurun_out/fp8abl$T.log ;;
     cosched) timeout -k 10 200 ./tools/cosched_bench ${ROWS:-56} > gpurun_out/cosched$T.log 2>&1; cat gpurun_out/cosched$T.log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -797,8 +797,11 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
       if (converged) break;
     }
   };
-  // plan_turn: the chains issue their first encode batch in chain order (st.plan)
-  std::atomic<int> plan_turn{0};
+  // planned[k]: chain k issued its first encode batch (st.plan).  The chains of one device issue
+  // theirs in chain order -- chain k after chain k - G, its predecessor on the same GPU, whose
+  // encode streams it shares (chain k runs on GPU k % G); chains on other devices do not wait
+  std::unique_ptr<std::atomic<int>[]> planned(new std::atomic<int>[C]);
+  for (int k = 0; k < C; ++k) planned[k] = 0;
   // done[k]: chain k finished its speculative block (and its early fix-up); spec_done[k]: its
   // speculative pass ended, spec_last[k] the prompt leaving the block then (under spec_mu: the
   // chain's own early fix-up may rewrite spec_out of its block meanwhile)
@@ -826,10 +829,9 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
         // first-out, so chain k starts decoding about k batch-times in (WDR_BALANCE_SKEW)
         struct Turn {
           std::atomic<int>& t;
-          int k;
-          ~Turn() { t.store(k + 1); }
-        } turn{plan_turn, k};
-        while (plan_turn.load() < k && !stop) std::this_thread::sleep_for(std::chrono::microseconds(20));
+          ~Turn() { t.store(1); }
+        } turn{planned[k]};
+        while (k >= G && !planned[k - G].load() && !stop) std::this_thread::sleep_for(std::chrono::microseconds(20));
         st.plan(pcm.data(), ns.data(), (int)(b - a), auto_lang);
       }
       struct Guard {
@@ -1657,7 +1659,10 @@ int wdr_diarize_frame_classes(wdr_diarizer* d, const int16_t* samples, size_t n,
 
 int wdr_diarize_get_segments(wdr_diarizer* d, const int16_t* samples, size_t n, wdr_speech_segment** segs_out,
                              size_t* n_segs) {
-  WDR_GUARD({ return diar_segments_out(d->S().get_segments(samples, n), samples, n, segs_out, n_segs); })
+  WDR_GUARD({
+    WDR_USE(dia, d);
+    return diar_segments_out(d->S().get_segments(samples, n), samples, n, segs_out, n_segs);
+  })
 }
 
 int wdr_diarize_segments_from_classes(const int32_t* cls, size_t n_windows, const int16_t* samples, size_t n,
@@ -2324,7 +2329,8 @@ int wdr_dbg_proj(const uint16_t* a16, const uint16_t* w16, const float* bias, in
 int wdr_dbg_proj_ln(const float* x, const float* gamma, const float* beta, const uint16_t* w16, const float* bias,
                     int32_t M, int32_t N, int32_t K, int32_t epi, int32_t fused, float* out) {
   WDR_GUARD({
-    if (M < 1 || N < 1 || K < 4 || K > 1280 || K % 32) return fail("dbg_proj_ln: M >= 1, K % 32 == 0, K <= 1280");
+    // K % 128: the fused prologue's 16-chunk row swizzle (csrc/rows.cpp launch_rows)
+    if (M < 1 || N < 1 || K < 128 || K > 1280 || K % 128) return fail("dbg_proj_ln: M >= 1, K % 128 == 0, K <= 1280");
     if (epi != EPI_F16 && epi != EPI_F16_GELU && epi != EPI_F32) return fail("dbg_proj_ln: epi 0, 1 or 3");
     DevMem dx((size_t)M * K * 4), dg((size_t)K * 4), dbt((size_t)K * 4), dw((size_t)N * K * 2),
         db(bias ? (size_t)N * 4 : 0), dh((size_t)M * K * 2), dout((size_t)M * N * 4);

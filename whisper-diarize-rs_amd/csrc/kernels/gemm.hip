@@ -1318,8 +1318,9 @@ static void launch_epi8(const ProjArgs& a, hipStream_t s) {
   if constexpr (EPI != EPI_F8_GELU) {
     // the narrow projections (o, fc2: N = 1280) on 256 x 128 tiles: 240 at M = 6000 where 256 x 256
     // tiles fill 120 CUs (WDR_GEMM8N=0: k_gemm8 for every shape)
+    // N % 256 != 0 (tiny's qkv, N = 1152) has only the 256 x 128 tiling
     static const bool narrow_on = !getenv("WDR_GEMM8N") || atoi(getenv("WDR_GEMM8N")) != 0;
-    if (narrow_on && a.N < 2048 && a.N % 128 == 0) {
+    if ((narrow_on && a.N < 2048) || a.N % G3_N != 0) {
       static bool attrn = [] {
         WDR_HIP(hipFuncSetAttribute((const void*)k_gemm8n<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G8N_LDS));
         return true;
@@ -1336,8 +1337,12 @@ static void launch_epi8(const ProjArgs& a, hipStream_t s) {
 
 void launch_proj_fp8(const ProjArgs& a, hipStream_t s) {
   WDR_CHECK(a.A8 && a.B8 && a.a_sc && a.b_sc, "fp8 projection: operands / scales missing");
-  WDR_CHECK(a.M > 64 && a.N % G3_N == 0 && a.K % G8_BK == 0 && a.lda % 16 == 0 && a.ldb % 16 == 0,
-            "fp8 projection: M > 64, N % 256 == 0, K % 128 == 0, lda / ldb % 16 required");
+  // N % 128: k_gemm8n's 256 x 128 tiles; the 256 x 256 k_gemm8 (every N >= 2048, and fc1's GELU ->
+  // fp8 epilogue) needs N % 256
+  WDR_CHECK(a.M > 64 && a.N % 128 == 0 && (a.epi != EPI_F8_GELU || a.N % G3_N == 0) && a.K % G8_BK == 0 &&
+                a.lda % 16 == 0 && a.ldb % 16 == 0,
+            "fp8 projection: M > 64, N % 128 == 0 (N % 256 for the GELU -> fp8 epilogue), K % 128 == 0, "
+            "lda / ldb % 16 required");
   WDR_CHECK(a.ld_asc >= cdiv(a.M, G3_M) * G3_M && a.ld_bsc >= a.N && a.ld_asc % 4 == 0 && a.ld_bsc % 4 == 0,
             "fp8 projection: scale images need the rows rounded up to 256");
   WDR_CHECK(a.epi != EPI_F8_GELU || (a.o_sc && a.ld_osc >= cdiv(a.M, G3_M) * G3_M && a.ldo % 16 == 0),

@@ -78,6 +78,9 @@ struct Model {
   size_t weight_bytes = 0;
 };
 
+// the encoder's fp8 plan from the environment (whisper_ctx.cpp): one nibble per layer
+std::vector<uint8_t> fp8_plan_for(int n_layer);
+
 struct ContextParams {
   bool use_gpu = true;
   int gpu_device = 0;
@@ -136,6 +139,11 @@ class Context {
   // WDR_FP8_ENCODER): the encoder layers' projection weights as e4m3 with one E8M0 scale per 32 k,
   // made once on first use; the activations are quantised by their producers in the encoder
   std::atomic<bool> fp8_encoder{false};
+  // which projections of which encoder layers run fp8 when fp8_encoder is on: one nibble per
+  // layer, bit 0 qkv, 1 o, 2 fc1, 3 fc2 (fp8_plan_for; WDR_FP8_PLAN / WDR_FP8_PROJ /
+  // WDR_FP8_F16_HEAD / WDR_FP8_F16_TAIL select other plans for the parity ablation)
+  std::vector<uint8_t> fp8_plan;
+  enum { F8_QKV = 1, F8_O = 2, F8_FC1 = 4, F8_FC2 = 8 };
   struct Fp8W {
     DevMem w, s;   // [N][K] e4m3, scale words [K/128][N] (byte b of word (t, n): k 128t + 32b ..)
   };
@@ -342,7 +350,7 @@ class State {
   // R-row batched step (StepBatcher) on this state's window, `iters` times: host ms per step
   double dbg_batch_step(const int* toks, int n, int R, int iters);
   void read_mel_window(int seek, float* out);              // [n_mels][3000] normalised
-  void encode_window(int seek);
+  hipStream_t encode_window(int seek);   // the stream it ran on (the caller synchronises)
   void encode_from_mel_window(const float* mel_window);    // [n_mels][3000] normalised, host
   void read_encoder_out(float* out);                       // [1500][d] (ln_post output, f16 -> f32)
   void read_cross_kv(float* out);                          // [1500][L][2][d] of the last encoded window

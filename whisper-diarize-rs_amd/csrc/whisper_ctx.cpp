@@ -118,6 +118,25 @@ static bool no_graph() {
   return v;
 }
 
+// WDR_HOST_FENCE (default 1): a state's own (decode) stream does not carry barrier packets.  HIP
+// maps the 40 states' highest-priority streams and the step batcher's onto GPU_MAX_HW_QUEUES
+// shared hardware queues, and a queue runs its packets in order: a hipStreamWaitEvent on a state
+// stream waiting for a low-priority DTW pass held back every batched step queued behind it on
+// that queue (configs[2]'s VAD line: long segments, windows encoded on demand on the state
+// stream after such a wait; profiles/r05/vad_line_queues.txt).  The chain's host thread waits
+// for the event instead -- it synchronises on that stream right after anyway.
+static bool host_fence() {
+  static const bool v = !(getenv("WDR_HOST_FENCE") && atoi(getenv("WDR_HOST_FENCE")) == 0);
+  return v;
+}
+
+static void stream_fence(hipStream_t s, hipEvent_t ev, bool host) {
+  if (host)
+    WDR_HIP(hipEventSynchronize(ev));
+  else
+    WDR_HIP(hipStreamWaitEvent(s, ev, 0));
+}
+
 hipStream_t dedicated_stream(const char* knob, bool def, int prio) {
   const char* e = getenv(knob);
   const bool on = e ? atoi(e) != 0 : def;
@@ -243,6 +262,25 @@ static hipStream_t own_masked_stream(bool* shared) {
   *shared = false;
   if (pool < 0) return nullptr;
   return masked_pool_stream("own", n_res, pool, shared);
+}
+
+// WDR_ODM_POOL (default 4): a long segment's later windows (encoded on demand: they depend on
+// the decoded seek) run on P CU-masked streams (dedicated hardware queues, WDR_ODM_MASK CUs left
+// free, default 32 as the encode-ahead pool), not on the state's own highest-priority stream.  A
+// window's encoder (~70 launches, several ms) on the state stream shared a hardware queue with
+// the step batcher, which runs its packets in order, so every batched step queued behind it
+// waited (configs[2]'s VAD line: long merged segments; profiles/r05/vad_line_queues.txt,
+// profiles/r06/ab_lines_hwq.txt).  -1: the state stream (as before).
+static hipStream_t odm_masked_stream(bool* shared) {
+  static const int pool = getenv("WDR_ODM_POOL") ? atoi(getenv("WDR_ODM_POOL")) : 4;
+  static const int n_res = getenv("WDR_ODM_MASK") ? atoi(getenv("WDR_ODM_MASK")) : 32;
+  *shared = false;
+  if (pool < 0) return nullptr;
+  int dev = 0, ncu = 0;
+  WDR_HIP(hipGetDevice(&dev));
+  WDR_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  if (ncu != 256 && !getenv("WDR_ODM_POOL")) return nullptr;   // tuned on MI355X
+  return masked_pool_stream("odm", n_res, pool, shared);
 }
 
 DevMem::DevMem(size_t n) : bytes(n) {
@@ -512,6 +550,7 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
     n_batchers = std::max(1, std::min(8, nb ? atoi(nb) : 1));
     prefill_split = getenv("WDR_PREFILL_SPLIT") && atoi(getenv("WDR_PREFILL_SPLIT")) != 0;
     fp8_encoder = getenv("WDR_FP8_ENCODER") && atoi(getenv("WDR_FP8_ENCODER")) != 0;
+    fp8_plan = fp8_plan_for(hp.n_audio_layer);
     const size_t per = (size_t)hp.n_text_layer * 21 * hp.n_text_ctx * hp.n_text_state;   // NSLOT = 21
     kv_k = DevMem(per * max_chains * 2);
     kv_v = DevMem(per * max_chains * 2);
@@ -631,6 +670,9 @@ struct State::Impl {
   int nslot_tot = 0;          // sequences per layer in the pool (layer stride / seq_stride)
   long long seq_stride = 0;   // elements per (layer, seq)
   hipStream_t own = nullptr;  // this state's decode stream
+  hipStream_t eo = nullptr;   // on-demand window encodes (WDR_ODM_POOL; null: the decode stream)
+  bool eo_shared = false;
+  hipEvent_t ev_eo = nullptr;   // the decode stream's work before an on-demand encode
   // dtw
   DevMem nrm, xdtw, times;
   struct DtwSet {
@@ -674,6 +716,36 @@ struct State::Impl {
 };
 
 // ------------------------------------------------------------------ fp8 encoder weights
+// The fp8 plan: one nibble per encoder layer (Context::F8_*).  Default: every projection of every
+// layer.  WDR_FP8_PLAN = one hex digit per layer (layer 0 first; missing layers take the last
+// digit); else WDR_FP8_PROJ (hex nibble, default f) on every layer but the first WDR_FP8_F16_HEAD
+// and the last WDR_FP8_F16_TAIL, which stay f16.
+std::vector<uint8_t> fp8_plan_for(int n_layer) {
+  std::vector<uint8_t> plan(n_layer, 0xf);
+  if (const char* e = getenv("WDR_FP8_PLAN"); e && *e) {
+    uint8_t last = 0xf;
+    for (int l = 0; l < n_layer; ++l) {
+      if (e[l] && isxdigit((unsigned char)e[l])) {
+        const char c = (char)tolower(e[l]);
+        last = (uint8_t)(c <= '9' ? c - '0' : c - 'a' + 10);
+      } else if (e[l]) {
+        throw std::runtime_error("WDR_FP8_PLAN: one hex digit per encoder layer");
+      }
+      plan[l] = last;
+      if (!e[l]) {
+        for (int r = l + 1; r < n_layer; ++r) plan[r] = last;
+        break;
+      }
+    }
+    return plan;
+  }
+  const uint8_t proj = getenv("WDR_FP8_PROJ") ? (uint8_t)(strtol(getenv("WDR_FP8_PROJ"), nullptr, 16) & 0xf) : 0xf;
+  const int head = getenv("WDR_FP8_F16_HEAD") ? atoi(getenv("WDR_FP8_F16_HEAD")) : 0;
+  const int tail = getenv("WDR_FP8_F16_TAIL") ? atoi(getenv("WDR_FP8_F16_TAIL")) : 0;
+  for (int l = 0; l < n_layer; ++l) plan[l] = (l < head || l >= n_layer - tail) ? 0 : proj;
+  return plan;
+}
+
 void Context::fp8_build() {
   WDR_HIP(hipSetDevice(cp.gpu_device));
   const HParams& hp = model.hp;
@@ -783,6 +855,8 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
     const int prio = ep == 2 ? hi : ep == 1 ? (lo + hi) / 2 : lo;
     m.es = enc_masked_stream(&m.es_shared);
     if (!m.es) WDR_HIP(hipStreamCreateWithPriority(&m.es, hipStreamNonBlocking, prio));
+    m.eo = odm_masked_stream(&m.eo_shared);
+    WDR_HIP(hipEventCreateWithFlags(&m.ev_eo, hipEventDisableTiming));
   }
   // this state's rows forwards: prompt prefills / DTW re-forwards up to RMAX rows, steps of up
   // to NSEQ logit rows; the DTW set captures; language detection kBatch rows
@@ -873,6 +947,11 @@ State::~State() {
       (void)hipStreamSynchronize(m_->own);
       if (!m_->own_shared) (void)hipStreamDestroy(m_->own);
     }
+    if (m_->eo) {
+      (void)hipStreamSynchronize(m_->eo);
+      if (!m_->eo_shared) (void)hipStreamDestroy(m_->eo);
+    }
+    if (m_->ev_eo) (void)hipEventDestroy(m_->ev_eo);
     for (auto& j : m_->jobs) {
       if (j.blk) m_->blk_pool.push_back(j.blk);
       if (j.done) m_->ev_pool.push_back(j.done);
@@ -945,7 +1024,7 @@ static void slot_reserve_all(State::Impl::Slot& sl, int n, int n_mels) {
 void State::compute_mel(const float* x_host, int n) {
   Impl& m = *m_;
   m.cur = m.S;
-  WDR_HIP(hipStreamWaitEvent(s_, m.ev_dtw, 0));   // the scratch slot may still feed a DTW job
+  stream_fence(s_, m.ev_dtw, host_fence());   // the scratch slot may still feed a DTW job
   Impl::Slot& sl = m.slots[m.S];
   slot_reserve_x(sl, n);
   if (n > 0) WDR_HIP(wdr_memcpy_async(sl.x.p, x_host, (size_t)n * 4, hipMemcpyHostToDevice, s_));
@@ -991,56 +1070,66 @@ static void encoder_body(Context& ctx, State::Impl& m, State::Impl::EncBufs& e, 
   // quantised once behind the attention (k_quant_f8); the weights were quantised once
   // (Context::fp8_layers).  The residual stream, attention, the final LayerNorm and the cross-K/V
   // projection the decoder reads stay f16 / f32.
+  // per layer and projection (Context::fp8_plan): an fp8 projection's A operand is written as
+  // e4m3 + scales by its producer (LN1 / LN2 -> k_layernorm_f8; fc1's GELU -> EPI_F8_GELU when fc2
+  // is fp8 too; the attention output, or an f16 GELU output, -> k_quant_f8), an f16 one as f16
   const bool f8 = ctx.fp8_encoder.load() && d % 128 == 0;
-  if (f8) {
-    const std::vector<Context::Fp8Layer>& F8 = ctx.fp8_layers();
-    const int mp = cdiv(M, 256) * 256;
-    uint8_t* qa = e.q8a.as<uint8_t>();
-    uint8_t* qm = e.q8m.as<uint8_t>();
-    uint32_t* sa = e.qsa.as<uint32_t>();
-    uint32_t* sm = e.qsm.as<uint32_t>();
-    auto gemm8 = [&](const uint8_t* A, const uint32_t* asc, int K, const Context::Fp8W& W, const float* bias, void* out,
-                     int ldo, int N, int epi) {
-      ProjArgs p{nullptr, K, nullptr, K, bias, out, ldo, nullptr, 0, M, N, K, epi};
-      p.A8 = A;
-      p.a_sc = asc;
-      p.ld_asc = mp;
-      p.B8 = W.w.as<uint8_t>();
-      p.b_sc = W.s.as<uint32_t>();
-      p.ld_bsc = N;
-      if (epi == EPI_F8_GELU) {
-        p.o_sc = sm;
-        p.ld_osc = mp;
-      }
-      launch_proj_fp8(p, s);
-    };
-    for (int l = 0; l < hp.n_audio_layer; ++l) {
-      const EncLayer& w = md.enc[l];
-      const Context::Fp8Layer& w8 = F8[l];
-      launch_layernorm_f8(e.ex.as<float>(), d, w.ln1_g, w.ln1_b, qa, d, sa, mp, M, d, s);
-      gemm8(qa, sa, d, w8.qkv, w.b_qkv, e.eqkv.p, 3 * d, 3 * d, EPI_F16);
-      FlashArgs fa{e.eqkv.as<f16>(), 3 * d, bs, e.eqkv.as<f16>() + d, 3 * d, bs, e.eqkv.as<f16>() + 2 * d, 3 * d, bs,
-                   e.eatt.as<f16>(), d, obs, nullptr, 1500, 1500, hp.n_audio_head, 0, scale};
-      launch_flash_attn(fa, nb, s);
-      launch_quant_f8(e.eatt.as<f16>(), d, M, d, qa, d, sa, mp, s);
-      gemm8(qa, sa, d, w8.o, w.b_o, e.ex.p, d, d, EPI_F32_RESID);
-      launch_layernorm_f8(e.ex.as<float>(), d, w.ln2_g, w.ln2_b, qa, d, sa, mp, M, d, s);
-      gemm8(qa, sa, d, w8.fc1, w.b_fc1, qm, 4 * d, 4 * d, EPI_F8_GELU);
-      gemm8(qm, sm, 4 * d, w8.fc2, w.b_fc2, e.ex.p, d, d, EPI_F32_RESID);
+  const std::vector<Context::Fp8Layer>* F8 = f8 ? &ctx.fp8_layers() : nullptr;
+  const int mp = cdiv(M, 256) * 256;
+  uint8_t* qa = e.q8a.as<uint8_t>();
+  uint8_t* qm = e.q8m.as<uint8_t>();
+  uint32_t* sa = e.qsa.as<uint32_t>();
+  uint32_t* sm = e.qsm.as<uint32_t>();
+  auto gemm8 = [&](const uint8_t* A, const uint32_t* asc, int K, const Context::Fp8W& W, const float* bias, void* out,
+                   int ldo, int N, int epi) {
+    ProjArgs p{nullptr, K, nullptr, K, bias, out, ldo, nullptr, 0, M, N, K, epi};
+    p.A8 = A;
+    p.a_sc = asc;
+    p.ld_asc = mp;
+    p.B8 = W.w.as<uint8_t>();
+    p.b_sc = W.s.as<uint32_t>();
+    p.ld_bsc = N;
+    if (epi == EPI_F8_GELU) {
+      p.o_sc = sm;
+      p.ld_osc = mp;
     }
-  } else {
-    for (int l = 0; l < hp.n_audio_layer; ++l) {
-      const EncLayer& w = md.enc[l];
+    launch_proj_fp8(p, s);
+  };
+  for (int l = 0; l < hp.n_audio_layer; ++l) {
+    const EncLayer& w = md.enc[l];
+    const int pl = f8 ? ctx.fp8_plan[l] : 0;
+    const Context::Fp8Layer* w8 = pl ? &(*F8)[l] : nullptr;
+    if (pl & Context::F8_QKV) {
+      launch_layernorm_f8(e.ex.as<float>(), d, w.ln1_g, w.ln1_b, qa, d, sa, mp, M, d, s);
+      gemm8(qa, sa, d, w8->qkv, w.b_qkv, e.eqkv.p, 3 * d, 3 * d, EPI_F16);
+    } else {
       launch_layernorm(e.ex.as<float>(), d, w.ln1_g, w.ln1_b, e.eh.as<f16>(), d, M, d, s);
       proj(s, e.eh.as<f16>(), d, w.w_qkv, d, w.b_qkv, e.eqkv.p, 3 * d, M, 3 * d, d, EPI_F16);
-      FlashArgs fa{e.eqkv.as<f16>(), 3 * d, bs, e.eqkv.as<f16>() + d, 3 * d, bs, e.eqkv.as<f16>() + 2 * d, 3 * d, bs,
-                   e.eatt.as<f16>(), d, obs, nullptr, 1500, 1500, hp.n_audio_head, 0, scale};
-      launch_flash_attn(fa, nb, s);
+    }
+    FlashArgs fa{e.eqkv.as<f16>(), 3 * d, bs, e.eqkv.as<f16>() + d, 3 * d, bs, e.eqkv.as<f16>() + 2 * d, 3 * d, bs,
+                 e.eatt.as<f16>(), d, obs, nullptr, 1500, 1500, hp.n_audio_head, 0, scale};
+    launch_flash_attn(fa, nb, s);
+    if (pl & Context::F8_O) {
+      launch_quant_f8(e.eatt.as<f16>(), d, M, d, qa, d, sa, mp, s);
+      gemm8(qa, sa, d, w8->o, w.b_o, e.ex.p, d, d, EPI_F32_RESID);
+    } else {
       proj(s, e.eatt.as<f16>(), d, w.w_o, d, w.b_o, e.ex.p, d, M, d, d, EPI_F32_RESID);
+    }
+    if (pl & Context::F8_FC1) {
+      launch_layernorm_f8(e.ex.as<float>(), d, w.ln2_g, w.ln2_b, qa, d, sa, mp, M, d, s);
+      if (pl & Context::F8_FC2)
+        gemm8(qa, sa, d, w8->fc1, w.b_fc1, qm, 4 * d, 4 * d, EPI_F8_GELU);
+      else
+        gemm8(qa, sa, d, w8->fc1, w.b_fc1, e.emlp.p, 4 * d, 4 * d, EPI_F16_GELU);
+    } else {
       launch_layernorm(e.ex.as<float>(), d, w.ln2_g, w.ln2_b, e.eh.as<f16>(), d, M, d, s);
       proj(s, e.eh.as<f16>(), d, w.w_fc1, d, w.b_fc1, e.emlp.p, 4 * d, M, 4 * d, d, EPI_F16_GELU);
-      proj(s, e.emlp.as<f16>(), 4 * d, w.w_fc2, 4 * d, w.b_fc2, e.ex.p, d, M, d, 4 * d, EPI_F32_RESID);
+      if (pl & Context::F8_FC2) launch_quant_f8(e.emlp.as<f16>(), 4 * d, M, 4 * d, qm, 4 * d, sm, mp, s);
     }
+    if (pl & Context::F8_FC2)
+      gemm8(qm, sm, 4 * d, w8->fc2, w.b_fc2, e.ex.p, d, d, EPI_F32_RESID);
+    else
+      proj(s, e.emlp.as<f16>(), 4 * d, w.w_fc2, 4 * d, w.b_fc2, e.ex.p, d, M, d, 4 * d, EPI_F32_RESID);
   }
   launch_layernorm(e.ex.as<float>(), d, md.ln_post_g, md.ln_post_b, e.eh.as<f16>(), d, M, d, s);
   // cross K/V for every decoder layer in one GEMM (N = L*2d), scattered by the epilogue into the
@@ -1052,12 +1141,24 @@ static void encoder_body(Context& ctx, State::Impl& m, State::Impl::EncBufs& e, 
 }
 
 // one window of the current slot's segment on the decode stream (on-demand path)
-void State::encode_window(int seek) {
+// (on m.eo when set -- after the decode stream's earlier work -- else on the decode stream; the
+// caller synchronises the stream it returns)
+hipStream_t State::encode_window(int seek) {
   Impl& m = *m_;
   Impl::Slot& sl = m.slots[m.cur];
+  hipStream_t s = s_;
+  if (m.eo) {
+    WDR_HIP(hipEventRecord(m.ev_eo, s_));
+    WDR_HIP(hipStreamWaitEvent(m.eo, m.ev_eo, 0));
+    s = m.eo;
+  }
+  // a shared stream: the window's launches issued as one unit (as the encode-ahead batches)
+  std::unique_lock<std::mutex> issue_lk;
+  if (m.eo_shared) issue_lk = std::unique_lock<std::mutex>(stream_issue_mutex(m.eo));
   Im2colMelArgs ia{sl.mel.as<float>(), m.n_mels, sl.n_fft_frames, sl.gmax.as<int>(), seek, m.kp1, m.e1.im2col.as<f16>()};
-  launch_im2col_mel(ia, s_);
-  encoder_body(ctx_, m, m.e1, 1, const_cast<f16*>(m.xkv()), s_);
+  launch_im2col_mel(ia, s);
+  encoder_body(ctx_, m, m.e1, 1, const_cast<f16*>(m.xkv()), s);
+  return s;
 }
 
 void State::encode_from_mel_window(const float* w) {
@@ -1168,7 +1269,7 @@ void State::slot_dtw_fence(int k, hipStream_t s) {
   const double t = now_s();
   ctx_.dtw_queue().wait_issued(q);
   m.t_fence += (long long)((now_s() - t) * 1e9);
-  WDR_HIP(hipStreamWaitEvent(s, q->fwd, 0));
+  stream_fence(s, q->fwd, s == s_ && host_fence());
   q.reset();
 }
 
@@ -2562,10 +2663,9 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
     if (encoded_seek != seek) {
       const double t = now_s();
       flush_dtw();   // a pending re-forward reads the slot this encode overwrites
-      WDR_HIP(hipStreamWaitEvent(s_, m.ev_dtw, 0));   // a DTW job may still read this slot
-      slot_dtw_fence(m.cur, s_);                       // ... or a queued pass
-      encode_window(seek);
-      WDR_HIP(hipStreamSynchronize(s_));
+      stream_fence(s_, m.ev_dtw, host_fence());   // a DTW job may still read this slot
+      slot_dtw_fence(m.cur, s_);                   // ... or a queued pass
+      WDR_HIP(hipStreamSynchronize(encode_window(seek)));
       times.encode += now_s() - t;
       times.windows++;
       encoded_seek = seek;
