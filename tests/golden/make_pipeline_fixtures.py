@@ -21,9 +21,10 @@ so anchors flip on f32 rounding alone; trained alignment heads are peaked, as at
   c3_large_v3_900s.json  configs[2] at a real size: 900 s, 35 VAD segments,
                          ~50 windows, same options
   c3_large_v3_beam5_120s.json  configs[2]'s audio with the reference's default beam-5 decode
+  c3_large_v3_beam5_300s.json  the same decode on 300 s of another recording (seed 53)
   c4_large_v3_diarize_300s[_w02].json  configs[3] diarized (DIAR / DIAR_W02 below)
 
-Usage:  python tests/golden/make_pipeline_fixtures.py [c1|c2|c3|c3l|c3b|c4d|c4dw02 ...]
+Usage:  python tests/golden/make_pipeline_fixtures.py [c1|c2|c3|c3l|c3b|c3b3|c4d|c4dw02 ...]
 """
 from __future__ import annotations
 
@@ -56,6 +57,8 @@ CONFIGS = {
     # VAD segments (VERDICT r5 missing 4): c3's audio with the default strategy
     "c3b": dict(file="c3_large_v3_beam5_120s.json", model="large-v3", seconds=120.0, seed=52, vad=True, greedy=False,
                 fallback=False),
+    "c3b3": dict(file="c3_large_v3_beam5_300s.json", model="large-v3", seconds=300.0, seed=53, vad=True, greedy=False,
+                 fallback=False),
 }
 
 # configs[3] (C4) diarized: large-v3, 300 s, 3 speakers, seed 1, greedy, lang auto, DTW, speaker

@@ -104,6 +104,12 @@ def test_c3_large_v3_vad_beam5_dtw_120s(tmp_path):
     print(dict(test="c3_beam5", seconds=120, cues=n, word_max_dt=dw))
 
 
+def test_c3_large_v3_vad_beam5_dtw_300s(tmp_path):
+    """The reference's default beam-5 decode at large-v3 on 300 s of another recording (seed 53)."""
+    n, dw = fixture_vs_transcribe_audio(tmp_path, "c3_large_v3_beam5_300s.json")
+    print(dict(test="c3_beam5_300s", seconds=300, cues=n, word_max_dt=dw))
+
+
 def test_c3_900s_fp8_encoder_agreement(tmp_path, monkeypatch):
     """configs[4]'s fp8 encoder (MX e4m3 GEMMs, WDR_FP8_ENCODER=1) on the alignment-conditioned C3
     fixture (900 s, large-v3, VAD, greedy, DTW) against the oracle's f16-path output: fp8 is a

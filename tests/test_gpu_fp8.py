@@ -105,3 +105,29 @@ def test_fp8_pipeline_agreement():
     _report(test="fp8_pipeline", model="large-v3", segments=len(ref), same_text=same)
     assert len(got) == len(ref)
     ctx.close()
+
+
+def test_fp8_plan_mixes_projections(monkeypatch):
+    """Context::fp8_plan (round 6 ablation, DESIGN.md "configs[4]"): an all-f16 plan with the fp8
+    switch on is the f16 encoder bit for bit; a mixed plan (fc2 only / every projection of the
+    middle layers) lands between the f16 and the all-fp8 errors against the oracle."""
+    name = "base.en"
+    hp = hparams_for(name)
+    m = Whisper(hp, synth_weights(hp, std=0.02, emb_std=EMB_STD))
+    rng = np.random.default_rng(5)
+    mel = (rng.standard_normal((hp.n_mels, 3000)) * 0.4).astype(np.float32)
+    ref = m.encode(mel)
+    errs = {}
+    for plan in ("0", "8", "0ff0", "f"):
+        monkeypatch.setenv("WDR_FP8_PLAN", plan)   # read when the context is created
+        ctx = wdr.WhisperContext(name, synthetic=PIN)
+        e16 = ctx.encode(mel)
+        ctx.set_encoder_fp8(True)
+        e8 = ctx.encode(mel)
+        ctx.close()
+        if plan == "0":
+            np.testing.assert_array_equal(e8, e16)
+        errs[plan] = _rel(e8, ref)
+    _report(test="fp8_plan", model=name, rel_err=errs)
+    assert errs["0"] < errs["8"] < errs["f"], errs
+    assert errs["0"] < errs["0ff0"] < errs["f"], errs

@@ -86,6 +86,11 @@ __device__ __forceinline__ float wave_max(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
+// A workgroup barrier that orders LDS only: waits for this wave's LDS operations, not for its
+// outstanding global loads (__syncthreads' workgroup fence waits vmcnt(0), which in a recurrence
+// with prefetched inputs stalls every step on the prefetch it just issued)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ double wave_sum_d(double v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;

@@ -328,47 +328,58 @@ __global__ __launch_bounds__(512) void k_lstm_scan(const float* __restrict__ xg,
   float c = 0.f;
   const float* xb = xg + b * xbs + dir * 512;
   float* ob = out + b * obs + dir * 128;
-  float nx[4];
-  {
-    const int t0 = dir ? T - 1 : 0;
+  // W_ih x + b_ih of the next kLPF steps in flight (registers), one LDS-only barrier per step:
+  // the arithmetic of every step is unchanged (round 6: a one-step lookahead behind
+  // __syncthreads waited for each step's load)
+  constexpr int kLPF = 8;
+  float pf[kLPF][4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) nx[g] = T > 0 ? xb[(long long)t0 * ldxg + g * 128 + u] : 0.f;
+  for (int q = 0; q < kLPF; ++q) {
+    const int tq = dir ? T - 1 - q : q;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) pf[q][g] = q < T ? xb[(long long)tq * ldxg + g * 128 + u] : 0.f;
   }
   __syncthreads();
-  for (int s = 0; s < T; ++s) {
-    const int t = dir ? T - 1 - s : s;
-    float cur[4];
+  for (int s0 = 0; s0 < T; s0 += kLPF) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) cur[g] = nx[g];
-    if (s + 1 < T) {
-      const int tn = dir ? t - 1 : t + 1;
+    for (int q = 0; q < kLPF; ++q) {
+      const int s = s0 + q;
+      if (s >= T) break;
+      const int t = dir ? T - 1 - s : s;
+      float cur[4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) nx[g] = xb[(long long)tn * ldxg + g * 128 + u];
+      for (int g = 0; g < 4; ++g) cur[g] = pf[q][g];
+      if (s + kLPF < T) {
+        const int tn = dir ? t - kLPF : t + kLPF;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) pf[q][g] = xb[(long long)tn * ldxg + g * 128 + u];
+      }
+      const float* h = hs[s & 1] + part * KC;
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int qq = 0; qq < KC / 4; ++qq) {
+        const float4 hv = *reinterpret_cast<const float4*>(h + qq * 4);
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          acc[g] += w[g][qq].x * hv.x + w[g][qq].y * hv.y + w[g][qq].z * hv.z + w[g][qq].w * hv.w;
+      }
+      float pre[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        acc[g] += __shfl_xor(acc[g], 1, 64);
+        acc[g] += __shfl_xor(acc[g], 2, 64);
+        pre[g] = cur[g] + (acc[g] + bh[g]);
+      }
+      const float ig = 1.f / (1.f + expf(-pre[0])), fg = 1.f / (1.f + expf(-pre[1]));
+      const float gg = tanhf(pre[2]), og = 1.f / (1.f + expf(-pre[3]));
+      c = fg * c + ig * gg;
+      const float hn = og * tanhf(c);
+      if (part == 0) {
+        hs[(s + 1) & 1][u] = hn;
+        ob[(long long)t * ldo + u] = hn;
+      }
+      lds_barrier();
     }
-    const float* h = hs[s & 1] + part * KC;
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int q = 0; q < KC / 4; ++q) {
-      const float4 hv = *reinterpret_cast<const float4*>(h + q * 4);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) acc[g] += w[g][q].x * hv.x + w[g][q].y * hv.y + w[g][q].z * hv.z + w[g][q].w * hv.w;
-    }
-    float pre[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      acc[g] += __shfl_xor(acc[g], 1, 64);
-      acc[g] += __shfl_xor(acc[g], 2, 64);
-      pre[g] = cur[g] + (acc[g] + bh[g]);
-    }
-    const float ig = 1.f / (1.f + expf(-pre[0])), fg = 1.f / (1.f + expf(-pre[1]));
-    const float gg = tanhf(pre[2]), og = 1.f / (1.f + expf(-pre[3]));
-    c = fg * c + ig * gg;
-    const float hn = og * tanhf(c);
-    if (part == 0) {
-      hs[(s + 1) & 1][u] = hn;
-      ob[(long long)t * ldo + u] = hn;
-    }
-    __syncthreads();
   }
 }
 

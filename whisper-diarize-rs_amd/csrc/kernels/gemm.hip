@@ -1695,7 +1695,13 @@ static void launch_epi(const ProjArgs& a, hipStream_t s) {
     dim3 grid(kn.cus > 0 && kn.cus < ntiles5 ? kn.cus : ntiles5);
     wdr_launch(PROF_GEMM, bytes, flops, k_gemm5<EPI>, grid, dim3(512), G5_LDS, s, g);
   } else if (a.N % G3_N == 0 && a.K % G3_BK == 0 && !ref && vec4 &&
-             (kn.gemm4 == 1 || (kn.gemm4 != 0 && (a.M >= 4096 || a.N >= 16384)))) {
+             (kn.gemm4 == 1 ||
+              (kn.gemm4 != 0 && (a.M >= 4096 || a.N >= 16384 || (a.N >= 4096 && a.M > 1024) ||
+                                 (a.N >= 3072 && a.M >= 2560))))) {
+    // round 6, partial encode batches and on-demand windows (profiles/r06/gemm_bench_mid_m.txt,
+    // bit-identical outputs): fc1 (N = 4d) at M = 1500 / 3000 39.7 / 44.4 us on k_gemm4 vs 45.0 /
+    // 67.3 on k_gemm / k_gemm3; qkv (3d) at M = 3000 41.9 vs 50.2 (k_gemm2), at M = 1500 29.2 on
+    // k_gemm2 stays; o / fc2 (N = d) below M = 4096 stay on k_gemm2 (25.7 / 68.5 vs 43.3 / 110.4)
     // ping-pong 256 x 256 tiles (tools/gemm_bench, large-v3, alone on the GPU): M = 6000 qkv 600
     // vs 557 (k_gemm2), fc1 616 vs 574 (k_gemm3), cross-K/V 818 vs 742 TFLOP/s; M = 12000 every
     // shape (o 394 vs 382, fc2 811 vs 743); M = 1500 cross-K/V 773 vs 616.  The N = 1280 shapes
@@ -1748,6 +1754,14 @@ static bool rows_pair_tiles() {
   static const bool v = env_int("WDR_ROWS_PAIR", 1) != 0;
   return v;
 }
+// WDR_ROWS_MT (A/B, read once): the most 16-row tiles one workgroup of a narrow projection
+// (N < 4096, no LayerNorm prologue) takes above 32 rows, 2..5 (default 2).  A row's k order
+// depends on (N, K) only, so every value gives the same bits; fewer workgroups stream each
+// column tile's weights fewer times and take fewer rounds of the CUs the encoder leaves free.
+static int rows_mt_max() {
+  static const int v = std::max(2, std::min(5, env_int("WDR_ROWS_MT", 2)));
+  return v;
+}
 
 template <int EPI>
 static void launch_rows_epi(const ProjArgs& a, hipStream_t s) {
@@ -1771,16 +1785,25 @@ static void launch_rows_epi(const ProjArgs& a, hipStream_t s) {
         // second round on 256 CUs (tools/rows_bench fc2 at 56 / 64 rows: 16.8 / 17.8 vs 20.3 /
         // 22.1 us; at 33-48 rows the mt <= 3 tiles fit one round and stay faster alone, 12.2 vs
         // 16.6 us).  Each wave's 10 k-steps as two batches of 5 (10 at MT = 2 spills)
-        wdr_launch(prof, bytes, flops, k_skinny<EPI, 2, 1, 16, false, 5>, dim3(cdiv(a.N, 16), cdiv(mt, 2)), dim3(1024), 0, s, a);
+        const int m2 = std::min(mt, rows_mt_max());
+        const dim3 g2(cdiv(a.N, 16), cdiv(mt, m2));
+        if (m2 >= 4) wdr_launch(prof, bytes, flops, k_skinny<EPI, 4, 1, 16, false, 2>, g2, dim3(1024), 0, s, a);
+        else if (m2 == 3) wdr_launch(prof, bytes, flops, k_skinny<EPI, 3, 1, 16, false, 5>, g2, dim3(1024), 0, s, a);
+        else wdr_launch(prof, bytes, flops, k_skinny<EPI, 2, 1, 16, false, 5>, g2, dim3(1024), 0, s, a);
         return;
       }
       wdr_launch(prof, bytes, flops, k_skinny<EPI, 1, 1, 16, false, 12>, dim3(cdiv(a.N, 16), mt), dim3(1024), 0, s, a);
       return;
     }
     if (!ln && mt > 2 && rows_pair_tiles()) {
-      // above 32 rows (the batched steps that carry a prompt prefill, ~56 rows): two row tiles
-      // per workgroup, so a column tile's weights are read half as often
-      wdr_launch(prof, bytes, flops, k_skinny<EPI, 2, 1, 8>, dim3(cdiv(a.N, 16), cdiv(mt, 2)), dim3(512), 0, s, a);
+      // above 32 rows (the batched steps that carry a prompt prefill, ~56 rows): two (up to
+      // WDR_ROWS_MT) row tiles per workgroup, so a column tile's weights are read half as often
+      const int m2 = std::min(mt, rows_mt_max());
+      const dim3 g2(cdiv(a.N, 16), cdiv(mt, m2));
+      if (m2 >= 5) wdr_launch(prof, bytes, flops, k_skinny<EPI, 5, 1, 8>, g2, dim3(512), 0, s, a);
+      else if (m2 == 4) wdr_launch(prof, bytes, flops, k_skinny<EPI, 4, 1, 8>, g2, dim3(512), 0, s, a);
+      else if (m2 == 3) wdr_launch(prof, bytes, flops, k_skinny<EPI, 3, 1, 8>, g2, dim3(512), 0, s, a);
+      else wdr_launch(prof, bytes, flops, k_skinny<EPI, 2, 1, 8>, g2, dim3(512), 0, s, a);
       return;
     }
     dim3 grid(cdiv(a.N, 16), mt), blk(512);
