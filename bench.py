@@ -77,6 +77,8 @@ def parse():
                     help="N=1 greedy runs: also time the reference's default decode (beam search, 5 beams, "
                          "src/transcribe.rs:22-33) over the first this-many seconds of the shard (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--speakers", type=int, default=0,
+                    help="voices in the synthetic audio (default: 3 for --seg diarize, 1 for --seg vad)")
     ap.add_argument("--cpu-audio", type=float, default=60.0,
                     help="audio seconds of the workload the CPU baseline is extrapolated over (rank 0, N=1)")
     return ap.parse_args()
@@ -376,7 +378,7 @@ def main_inproc(args):
     if args.fp8:
         ctx.set_encoder_fp8(True)
     t_load = time.perf_counter() - t_load
-    parts = [synth_speech(args.seconds, seed=r, n_speakers=3 if diarize else 1) for r in range(N)]
+    parts = [synth_speech(args.seconds, seed=r, n_speakers=args.speakers or (3 if diarize else 1)) for r in range(N)]
     pcm = np.concatenate([p for p, _ in parts])
     spurts = [(a + r * args.seconds, b + r * args.seconds) for r, (_, sp) in enumerate(parts) for a, b, _ in sp]
     del parts
@@ -505,7 +507,7 @@ def main():
         # ONE file of world x seconds: rank r synthesises hour r (seed r) in parallel, rank 0
         # assembles the file (not timed); the timed step transcribes it across all ranks
         from wdr import distributed as D
-        pcm_r, spurts_r = synth_speech(args.seconds, seed=rank, n_speakers=3 if diarize else 1)
+        pcm_r, spurts_r = synth_speech(args.seconds, seed=rank, n_speakers=args.speakers or (3 if diarize else 1))
         parts = [None] * world if rank == 0 else None
         dist.gather_object((pcm_r, [(a + rank * args.seconds, b + rank * args.seconds) for a, b, _ in spurts_r]),
                            parts, dst=0)
@@ -534,7 +536,7 @@ def main():
             return res if res is not None else ([], None)
         segs = None
     else:
-        pcm, spurts = synth_speech(args.seconds, seed=rank, n_speakers=3 if diarize else 1)
+        pcm, spurts = synth_speech(args.seconds, seed=rank, n_speakers=args.speakers or (3 if diarize else 1))
         segs = [wdr.SpeechSegment(a, b, pcm[int(round(a * 16000)):int(round(b * 16000))]) for a, b, _ in spurts]
         audio_s = float(sum(s.samples.size for s in segs)) / 16000.0   # speech seconds handed to the pipeline
         shard_s = pcm.size / 16000.0                                  # wall-clock audio covered (xRT basis)

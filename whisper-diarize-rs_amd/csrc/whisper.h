@@ -324,6 +324,7 @@ class State {
   // full() resolves them into result_all before returning.
   int full(const FullParams& p, const float* samples, int n, int job = -1, bool async_dtw = false);
   std::vector<DtwTicket> take_dtw_jobs();
+  void alt_dtw_fence();                           // queued DTW pass reading the spare cross-K/V -> host waits
   void slot_dtw_fence(int slot, hipStream_t s);   // queued DTW pass reading the slot -> s waits
   void dtw_queue_fence(hipStream_t s);            // queued passes writing the DTW sequence -> s waits
   void resolve_dtw(DtwTicket& t, std::vector<ResultSeg>& segs);

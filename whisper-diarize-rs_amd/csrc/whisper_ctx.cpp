@@ -652,7 +652,12 @@ struct State::Impl {
   std::function<bool(StepBatcher::Req&)> lang_ride;
   std::function<void(const StepBatcher::Req&)> lang_after;
   DevMem energy_d; int energy_cap = 0;
-  const f16* xkv() const { return xkv_ring.as<f16>() + (size_t)cur * xkv_slot_elems; }
+  const f16* xkv() const { return xkv_ring.as<f16>() + (size_t)(xsel >= 0 ? S + 1 : cur) * xkv_slot_elems; }
+  // a segment's later windows (encoded on demand) alternate between the slot's cross-K/V and
+  // the chain's spare one (ring index S + 1; WDR_ODM_ALT): xsel >= 0 -> the spare, alt_dtw the
+  // queued DTW pass that reads it
+  int xsel = -1;
+  std::shared_ptr<DtwQJob> alt_dtw;
   // decoder: this state's own rows forwards (prompt prefills, beam / sampling steps, test seams)
   // on the decode stream, and the DTW re-forwards on the DTW stream, each with its own working
   // set and row tables (rows.h)
@@ -672,7 +677,6 @@ struct State::Impl {
   hipStream_t own = nullptr;  // this state's decode stream
   hipStream_t eo = nullptr;   // on-demand window encodes (WDR_ODM_POOL; null: the decode stream)
   bool eo_shared = false;
-  hipEvent_t ev_eo = nullptr;   // the decode stream's work before an on-demand encode
   // dtw
   DevMem nrm, xdtw, times;
   struct DtwSet {
@@ -844,7 +848,7 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
     WDR_HIP(hipEventCreateWithFlags(&sl.freed, hipEventDisableTiming));
   }
   m.xkv_slot_elems = (size_t)1500 * m.L * 2 * d;
-  m.xkv_ring = DevMem((m.S + 1) * m.xkv_slot_elems * 2);
+  m.xkv_ring = DevMem((m.S + 2) * m.xkv_slot_elems * 2);   // + the on-demand spare (xsel)
   m.cur = m.S;
   {
     // the encode-ahead stream at the lowest priority (WDR_ENC_PRIO=1: the middle of the range,
@@ -856,7 +860,6 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
     m.es = enc_masked_stream(&m.es_shared);
     if (!m.es) WDR_HIP(hipStreamCreateWithPriority(&m.es, hipStreamNonBlocking, prio));
     m.eo = odm_masked_stream(&m.eo_shared);
-    WDR_HIP(hipEventCreateWithFlags(&m.ev_eo, hipEventDisableTiming));
   }
   // this state's rows forwards: prompt prefills / DTW re-forwards up to RMAX rows, steps of up
   // to NSEQ logit rows; the DTW set captures; language detection kBatch rows
@@ -951,7 +954,6 @@ State::~State() {
       (void)hipStreamSynchronize(m_->eo);
       if (!m_->eo_shared) (void)hipStreamDestroy(m_->eo);
     }
-    if (m_->ev_eo) (void)hipEventDestroy(m_->ev_eo);
     for (auto& j : m_->jobs) {
       if (j.blk) m_->blk_pool.push_back(j.blk);
       if (j.done) m_->ev_pool.push_back(j.done);
@@ -1141,15 +1143,19 @@ static void encoder_body(Context& ctx, State::Impl& m, State::Impl::EncBufs& e, 
 }
 
 // one window of the current slot's segment on the decode stream (on-demand path)
-// (on m.eo when set -- after the decode stream's earlier work -- else on the decode stream; the
-// caller synchronises the stream it returns)
+// (on m.eo when set, else on the decode stream; the caller synchronises the stream it returns).
+// The decode stream's earlier work (the scratch slot's log-mel) is awaited on the HOST, and only
+// if any is pending: an event recorded on the decode stream would sit behind every step the
+// batcher has queued on the hardware queue the two share (in order), and the encode would wait
+// for them -- round 6's first on-demand pool did that and left the VAD line where it was.
 hipStream_t State::encode_window(int seek) {
   Impl& m = *m_;
   Impl::Slot& sl = m.slots[m.cur];
   hipStream_t s = s_;
   if (m.eo) {
-    WDR_HIP(hipEventRecord(m.ev_eo, s_));
-    WDR_HIP(hipStreamWaitEvent(m.eo, m.ev_eo, 0));
+    const hipError_t q = hipStreamQuery(s_);
+    if (q == hipErrorNotReady) WDR_HIP(hipStreamSynchronize(s_));
+    else WDR_HIP(q);
     s = m.eo;
   }
   // a shared stream: the window's launches issued as one unit (as the encode-ahead batches)
@@ -1270,6 +1276,24 @@ void State::slot_dtw_fence(int k, hipStream_t s) {
   ctx_.dtw_queue().wait_issued(q);
   m.t_fence += (long long)((now_s() - t) * 1e9);
   stream_fence(s, q->fwd, s == s_ && host_fence());
+  q.reset();
+}
+
+// WDR_ODM_ALT (default 1; read once): see Impl::xsel
+static bool odm_alt() {
+  static const bool v = !(getenv("WDR_ODM_ALT") && atoi(getenv("WDR_ODM_ALT")) == 0);
+  return v;
+}
+
+// the host waits until the queued DTW pass reading the spare cross-K/V has read it
+void State::alt_dtw_fence() {
+  Impl& m = *m_;
+  std::shared_ptr<DtwQJob>& q = m.alt_dtw;
+  if (!q) return;
+  const double t = now_s();
+  ctx_.dtw_queue().wait_issued(q);
+  m.t_fence += (long long)((now_s() - t) * 1e9);
+  WDR_HIP(hipEventSynchronize(q->fwd));
   q.reset();
 }
 
@@ -2034,7 +2058,8 @@ void State::dtw_timestamps(int i_segment, int n_segments, int seek, int n_frames
     dq.submit(q);
     job.q = q;
     m.jobs.push_back(job);
-    m.slots[m.cur].dtw = q;
+    if (m.xsel >= 0) m.alt_dtw = q;
+    else m.slots[m.cur].dtw = q;
     // passes already run no longer write the DTW sequence
     m.qlive.erase(std::remove_if(m.qlive.begin(), m.qlive.end(),
                                  [&](const std::shared_ptr<DtwQJob>& x) {
@@ -2607,6 +2632,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
     }
   } release{m, s_, planned};
   int encoded_seek = -1;
+  m.xsel = -1;   // window 0 reads the segment's own slot
   // WDR_CHAIN_LOG=<file>: one line per full() call -- chain, job, wall at entry and exit (s), top_up ms,
   // ready-wait ms, energy ms, decode ms (windows' decode loops), post ms (results, heuristic
   // timestamps, DTW submit) -- where a chain spends the time between its batched steps
@@ -2662,9 +2688,15 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
   auto encode = [&](int seek) {
     if (encoded_seek != seek) {
       const double t = now_s();
+      // a later window of the segment: into the other of (slot, spare) when the DTW queue runs
+      // the re-forwards -- the one the previous window's queued pass is still reading stays
+      // untouched, so the encode does not wait for that pass (configs[2]'s long VAD segments:
+      // every later window did)
+      if (encoded_seek >= 0 && batched && dtw_queue_on() && odm_alt()) m.xsel = m.xsel < 0 ? 0 : -1;
       flush_dtw();   // a pending re-forward reads the slot this encode overwrites
       stream_fence(s_, m.ev_dtw, host_fence());   // a DTW job may still read this slot
-      slot_dtw_fence(m.cur, s_);                   // ... or a queued pass
+      if (m.xsel >= 0) alt_dtw_fence();   // ... or a queued pass
+      else slot_dtw_fence(m.cur, s_);
       WDR_HIP(hipStreamSynchronize(encode_window(seek)));
       times.encode += now_s() - t;
       times.windows++;
