@@ -77,6 +77,11 @@ def parse():
                     help="N=1 greedy runs: also time the reference's default decode (beam search, 5 beams, "
                          "src/transcribe.rs:22-33) over the first this-many seconds of the shard (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--keepalive", type=int, default=0,
+                    help="A/B diagnostic: a host thread keeps a low-priority stream busy with 1-workgroup "
+                         "spin kernels of this many cycles during the timed steps (0: off)")
+    ap.add_argument("--no-embed", action="store_true",
+                    help="A/B: --seg diarize without speaker embeddings / assignment in the pipeline")
     ap.add_argument("--speakers", type=int, default=0,
                     help="voices in the synthetic audio (default: 3 for --seg diarize, 1 for --seg vad)")
     ap.add_argument("--cpu-audio", type=float, default=60.0,
@@ -495,7 +500,7 @@ def main():
                                  enable_diarize=True if diarize else None,
                                  advanced=wdr.AdvancedTranscribe(
                                      sampling_strategy="greedy" if args.strategy == "greedy" else None))
-    dopts = wdr.DiarizeOptions.from_options(opts) if diarize else None   # src/engine.rs:101-111
+    dopts = wdr.DiarizeOptions.from_options(opts) if diarize and not args.no_embed else None   # src/engine.rs:101-111
     vad = None if diarize else wdr.Vad(gpu_device=local)
     dia = wdr.Diarizer(gpu_device=local) if diarize else None
     lib = wdr._lib.load()
@@ -555,6 +560,20 @@ def main():
             vad_t[1] = n_seg
             return ctx.run_pipeline(segs, opts, diarize_options=dopts)
 
+    if args.keepalive > 0:
+        # diagnostic only (profiles/r06/ab_lines_hwq.txt): does activity on a low-priority queue,
+        # like the speaker-embedding worker's, change the batched steps' speed?
+        import threading
+        ka_stop = threading.Event()
+
+        def keepalive():
+            st = torch.cuda.Stream(device=local, priority=0)
+            with torch.cuda.stream(st):
+                while not ka_stop.is_set():
+                    torch.cuda._sleep(args.keepalive)
+                    st.synchronize()
+        ka = threading.Thread(target=keepalive, daemon=True)
+        ka.start()
     vad_t = [0.0, 0]
     for _ in range(args.warmup):
         step()
@@ -568,6 +587,9 @@ def main():
         n_out += len(out)
     barrier()
     dt = time.perf_counter() - t0
+    if args.keepalive > 0:
+        ka_stop.set()
+        ka.join()
     import ctypes as C
     live, live_ev = {}, {}
     for c in prof:

@@ -364,6 +364,17 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
     int lo = 0, hi = 0;
     WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
     WDR_HIP(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, hi));
+    // WDR_PRIME_LOWQ (A/B): a lowest-priority stream created -- and its hardware queue
+    // instantiated by one launch -- right after the context's own, before the step batcher's
+    // and the states' streams
+    if (getenv("WDR_PRIME_LOWQ") && atoi(getenv("WDR_PRIME_LOWQ")) != 0) {
+      WDR_HIP(hipStreamCreateWithPriority(&low_prime, hipStreamNonBlocking, lo));
+      DevMem one(16);
+      WDR_HIP(hipMemsetAsync(one.p, 0, 16, low_prime));
+      WDR_HIP(hipStreamSynchronize(low_prime));
+    }
+    // WDR_DTWQ_EARLY (A/B): the DTW queue (its lowest-priority stream) made at the end of the
+    // constructor, before the batcher and the states
   }
   Model& m = model;
   m.hp = hp;
@@ -557,6 +568,10 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
     kv_seq_stride = (long long)hp.n_text_ctx * hp.n_text_state;
     kv_layer_stride = (long long)max_chains * 21 * kv_seq_stride;
   }
+  if (getenv("WDR_DTWQ_EARLY") && atoi(getenv("WDR_DTWQ_EARLY")) != 0 && !aheads.empty()) {
+    DtwQueue& q = dtw_queue();
+    (void)q;
+  }
 }
 
 Context::~Context() {
@@ -564,6 +579,7 @@ Context::~Context() {
   batchers.clear();
   prefill_b.reset();
   if (stream) (void)hipStreamDestroy(stream);
+  if (low_prime) (void)hipStreamDestroy(low_prime);
 }
 
 // ------------------------------------------------------------------ state buffers
