@@ -73,6 +73,7 @@ SegModel::SegModel(int dev, const std::string& path) : device(dev) {
   };
   WDR_HIP(hipSetDevice(dev));
   WDR_HIP(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking));
+  stream_note("seg", s_);
   WDR_HIP(hipEventCreate(&e0_));
   WDR_HIP(hipEventCreate(&e1_));
   w_ = new W;
@@ -319,6 +320,7 @@ CamModel::CamModel(int dev, const std::string& path) : device(dev) {
   int lo = 0, hi = 0;
   WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
   WDR_HIP(hipStreamCreateWithPriority(&s_, hipStreamNonBlocking, lo));
+  stream_note("cam", s_);
   WDR_HIP(hipEventCreate(&e0_));
   WDR_HIP(hipEventCreate(&e1_));
   w_ = new W;

@@ -242,10 +242,14 @@ struct wdr_context {
     long long dq_passes = 0, dq_rows = 0, dq_jobs = 0;   // DTW queue
     double spec_s = 0, fixup_s = 0, step_s = 0;
   } cs;                                           // the last run_pipeline's multi-chain figures
+  hipStream_t low_dummy = nullptr;  // WDR_LOWQ_AT_PIPE (A/B, run_pipeline)
   std::unique_ptr<CamModel> cam;   // EmbeddingExtractor, created on the first diarized run
   std::string cam_path;            // ... from this embedding model file ("" = synthetic weights)
   double load_s = 0;
   double embed_s = 0;              // wall time the decode chain waited on speaker embeddings
+  ~wdr_context() {
+    if (low_dummy) (void)hipStreamDestroy(low_dummy);
+  }
 };
 
 // Speaker embeddings of every speech segment, computed in segment order on a host worker
@@ -1076,6 +1080,17 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
       c->cam = std::make_unique<CamModel>(c->ctx->cp.gpu_device, path);
       c->cam_path = path;
     }
+  }
+  if (!diarize && !c->low_dummy && getenv("WDR_LOWQ_AT_PIPE") && atoi(getenv("WDR_LOWQ_AT_PIPE")) != 0) {
+    // A/B: a lowest-priority stream made where the embedding model's would be (before the decode
+    // chains' states on the first call), its hardware queue instantiated by one memset
+    int lo = 0, hi = 0;
+    WDR_HIP(hipSetDevice(c->devices[0]));
+    WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    WDR_HIP(hipStreamCreateWithPriority(&c->low_dummy, hipStreamNonBlocking, lo));
+    DevMem one(16);
+    WDR_HIP(hipMemsetAsync(one.p, 0, 16, c->low_dummy));
+    WDR_HIP(hipStreamSynchronize(c->low_dummy));
   }
   std::unique_ptr<EmbedAhead> embeds;
   if (diarize) embeds = std::make_unique<EmbedAhead>(*c->cam, segs);

@@ -277,6 +277,14 @@ void prof_push(int cls, hipEvent_t a, hipEvent_t b, unsigned long long* ts, doub
   if (g_pending.size() > 4096) drain_locked(false);
 }
 
+void stream_note(const char* what, hipStream_t s) {
+  static const bool on = getenv("WDR_STREAM_LOG") && atoi(getenv("WDR_STREAM_LOG")) != 0;
+  if (on) {
+    fprintf(stderr, "[wdr-stream] %s %p\n", what, (void*)s);
+    fflush(stderr);
+  }
+}
+
 }  // namespace wdr
 
 extern "C" {

@@ -26,6 +26,9 @@ int prof_class();
 bool prof_step();
 bool prof_enc_batch();
 void prof_capture(bool on);
+// WDR_STREAM_LOG=1: every libwdr stream creation noted on stderr (with AMD_LOG_LEVEL=3 the
+// runtime's hardware-queue choice is printed just before it; tools/queue_log.py pairs them)
+void stream_note(const char* what, hipStream_t s);
 void prof_in_step(bool on);    // around the eager launches of a step prof_step() picked
 void prof_in_enc(bool on);     // around the eager launches of a batch prof_enc_batch() picked
 hipEvent_t prof_event();

@@ -35,6 +35,7 @@ VadModel::VadModel(int dev, const std::string& path) : device(dev) {
   const TensorMap file = path.empty() ? TensorMap() : load_silero_ggml(path);   // before any GPU work
   WDR_HIP(hipSetDevice(dev));
   WDR_HIP(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking));
+  stream_note("vad", s_);
   WDR_HIP(hipEventCreate(&e0_));
   WDR_HIP(hipEventCreate(&e1_));
   const VadLayout L = layout();

@@ -143,6 +143,7 @@ hipStream_t dedicated_stream(const char* knob, bool def, int prio) {
   hipStream_t s = nullptr;
   if (!on) {
     WDR_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio));
+    stream_note(knob, s);
     return s;
   }
   int dev = 0, ncu = 0;
@@ -151,6 +152,7 @@ hipStream_t dedicated_stream(const char* knob, bool def, int prio) {
   std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
   for (int c = 0; c < ncu; ++c) mask[c / 32] |= 1u << (c % 32);
   WDR_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+  stream_note(knob, s);
   return s;
 }
 
@@ -209,6 +211,7 @@ static hipStream_t masked_pool_stream(const char* tag, int n_res, int pool, bool
       if (!res[c]) mask[c / 32] |= 1u << (c % 32);
     hipStream_t st = nullptr;
     WDR_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+    stream_note(tag, st);
     return st;
   };
   *shared = false;
@@ -364,6 +367,7 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
     int lo = 0, hi = 0;
     WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
     WDR_HIP(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, hi));
+    stream_note("context", stream);
     // WDR_PRIME_LOWQ (A/B): a lowest-priority stream created -- and its hardware queue
     // instantiated by one launch -- right after the context's own, before the step batcher's
     // and the states' streams
@@ -846,6 +850,7 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
     } else if (op == 1) WDR_HIP(hipStreamCreateWithFlags(&m.own, hipStreamNonBlocking));
     else WDR_HIP(hipStreamCreateWithPriority(&m.own, hipStreamNonBlocking, op == 2 ? lo : hi));
     s_ = m.own;
+    stream_note("state-own", s_);
   }
   m.d = hp.n_text_state;
   m.L = hp.n_text_layer;
@@ -875,6 +880,7 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
     const int prio = ep == 2 ? hi : ep == 1 ? (lo + hi) / 2 : lo;
     m.es = enc_masked_stream(&m.es_shared);
     if (!m.es) WDR_HIP(hipStreamCreateWithPriority(&m.es, hipStreamNonBlocking, prio));
+    stream_note("state-es", m.es);
     m.eo = odm_masked_stream(&m.eo_shared);
   }
   // this state's rows forwards: prompt prefills / DTW re-forwards up to RMAX rows, steps of up
@@ -912,6 +918,7 @@ State::State(Context& ctx, int chain_) : ctx_(ctx), s_(nullptr), m_(new Impl) {
     int lo = 0, hi = 0;
     WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
     WDR_HIP(hipStreamCreateWithPriority(&m.sd, hipStreamNonBlocking, lo));
+    stream_note("state-sd", m.sd);
     WDR_HIP(hipEventCreateWithFlags(&m.ev_sync, hipEventDisableTiming));
     WDR_HIP(hipEventCreateWithFlags(&m.ev_dtw, hipEventDisableTiming));
     WDR_HIP(hipEventCreate(&m.ev_p0));
@@ -1536,6 +1543,7 @@ bool State::top_up_batch(int j) {
         // captured on a stream of its own: the chain thread waits on events recorded on m.es,
         // which HIP refuses while m.es itself is capturing
         if (!m.es_cap) WDR_HIP(hipStreamCreateWithFlags(&m.es_cap, hipStreamNonBlocking));
+        stream_note("state-es_cap", m.es_cap);
         hipGraph_t graph;
         prof_capture(true);
         WDR_HIP(hipStreamBeginCapture(m.es_cap, hipStreamCaptureModeRelaxed));
