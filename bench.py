@@ -80,6 +80,9 @@ def parse():
     ap.add_argument("--keepalive", type=int, default=0,
                     help="A/B diagnostic: a host thread keeps a low-priority stream busy with 1-workgroup "
                          "spin kernels of this many cycles during the timed steps (0: off)")
+    ap.add_argument("--keepalive-mb", type=int, default=0,
+                    help="A/B diagnostic: the keep-alive thread copies buffers of this many MB (HBM "
+                         "traffic) instead of spinning")
     ap.add_argument("--no-embed", action="store_true",
                     help="A/B: --seg diarize without speaker embeddings / assignment in the pipeline")
     ap.add_argument("--speakers", type=int, default=0,
@@ -560,7 +563,7 @@ def main():
             vad_t[1] = n_seg
             return ctx.run_pipeline(segs, opts, diarize_options=dopts)
 
-    if args.keepalive > 0:
+    if args.keepalive > 0 or args.keepalive_mb > 0:
         # diagnostic only (profiles/r06/ab_lines_hwq.txt): does activity on a low-priority queue,
         # like the speaker-embedding worker's, change the batched steps' speed?
         import threading
@@ -569,8 +572,16 @@ def main():
         def keepalive():
             st = torch.cuda.Stream(device=local, priority=0)
             with torch.cuda.stream(st):
+                if args.keepalive_mb > 0:
+                    a = torch.empty(args.keepalive_mb << 18, dtype=torch.float32, device=local)
+                    b = torch.empty_like(a)
                 while not ka_stop.is_set():
-                    torch.cuda._sleep(args.keepalive)
+                    if args.keepalive_mb > 0:
+                        b.copy_(a)
+                        st.synchronize()
+                        time.sleep(2e-4)
+                    else:
+                        torch.cuda._sleep(args.keepalive)
                     st.synchronize()
         ka = threading.Thread(target=keepalive, daemon=True)
         ka.start()
@@ -587,7 +598,7 @@ def main():
         n_out += len(out)
     barrier()
     dt = time.perf_counter() - t0
-    if args.keepalive > 0:
+    if args.keepalive > 0 or args.keepalive_mb > 0:
         ka_stop.set()
         ka.join()
     import ctypes as C

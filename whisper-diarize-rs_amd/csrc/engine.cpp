@@ -1081,9 +1081,14 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
       c->cam_path = path;
     }
   }
-  if (!diarize && !c->low_dummy && getenv("WDR_LOWQ_AT_PIPE") && atoi(getenv("WDR_LOWQ_AT_PIPE")) != 0) {
-    // A/B: a lowest-priority stream made where the embedding model's would be (before the decode
-    // chains' states on the first call), its hardware queue instantiated by one memset
+  static const bool lowq_at_pipe = !(getenv("WDR_LOWQ_AT_PIPE") && atoi(getenv("WDR_LOWQ_AT_PIPE")) == 0);
+  if (!diarize && !c->low_dummy && lowq_at_pipe) {
+    // WDR_LOWQ_AT_PIPE (default 1): an un-diarized pipeline gets a lowest-priority stream where the
+    // embedding model's would be (before the decode chains' states on the first call), its
+    // hardware queue instantiated by one memset.  It changes how the runtime spreads the states'
+    // lowest-priority DTW streams over its 4 low queues; measured: configs[2]'s VAD line 632 ->
+    // 737-740 xRT, the diarized line unaffected (it never takes this branch);
+    // profiles/r06/ab_lines_hwq.txt, DESIGN.md §5 "Hardware queues, round 6"
     int lo = 0, hi = 0;
     WDR_HIP(hipSetDevice(c->devices[0]));
     WDR_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
