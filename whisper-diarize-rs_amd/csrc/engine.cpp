@@ -1099,6 +1099,21 @@ static std::vector<Seg> run_pipeline(wdr_context* c, const std::vector<wdr_speec
   }
   std::unique_ptr<EmbedAhead> embeds;
   if (diarize) embeds = std::make_unique<EmbedAhead>(*c->cam, segs);
+  // WDR_HOST_SPIN=N (diagnostic, A/B): N host threads spin for the duration of the call (does
+  // keeping host cores awake change the batched steps' pace?)
+  struct Spin {
+    std::atomic<bool> stop{false};
+    std::vector<std::thread> th;
+    ~Spin() {
+      stop = true;
+      for (auto& t : th) t.join();
+    }
+  } spin;
+  if (const char* e = getenv("WDR_HOST_SPIN"))
+    for (int i = 0; i < std::max(0, std::min(8, atoi(e))); ++i)
+      spin.th.emplace_back([&spin] {
+        while (!spin.stop.load(std::memory_order_relaxed)) __builtin_ia32_pause();
+      });
   FullParams params = setup_params(o, syn);
   const Vocab& v = c->ctx->vocab;
   const double user_offset = (o && o->has_offset) ? o->offset : 0.0;
