@@ -187,8 +187,10 @@ __global__ __launch_bounds__(256) void k_vad_lstm(const float* __restrict__ xg, 
         hs[(s + 1) & 1][u] = (f16)h;
         hout[t * 128 + u] = h;
       }
-      // LDS-only: the xg prefetch kPF steps ahead stays in flight (round 6: __syncthreads waited
-      // for it every step, 1.78 us per chunk)
+      // LDS-only: the xg prefetch kPF steps ahead stays in flight (round 6; measured unchanged
+      // here, 1.77 us per chunk -- the step's own dependent FMA / transcendental chain on one wave
+      // per SIMD is the cost -- while the same change took pyannote's BiLSTM scans, k_lstm_scan,
+      // from 45 to 12 ms of GPU time per hour)
       lds_barrier();
     }
   }
