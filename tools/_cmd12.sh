@@ -1,4 +1,5 @@
 set -e -o pipefail
+mkdir -p gpurun_out/ab
 for v in "vad3:vad:3" "dia1:diarize:1" "vad1:vad:1" "dia3:diarize:3"; do
   n=${v%%:*}; r=${v#*:}; seg=${r%%:*}; sp=${r#*:}
   timeout -k 10 300 python3 bench.py --seg $seg --speakers $sp --no-cpu-baseline --prof none --beam-seconds 0 > gpurun_out/ab/sp_$n.json 2> gpurun_out/ab/sp_$n.err
