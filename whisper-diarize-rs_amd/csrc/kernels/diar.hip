@@ -576,27 +576,48 @@ __device__ __forceinline__ int seg_of(const int* off, int B, int r) {
   return lo;
 }
 
-// One wave per output row (t, f): the utterance lookup and the row's position once per row, its
-// C*kf*kt columns written by the wave's lanes (coalesced); 32-bit index math (the element-wise form
-// -- a 64-bit division and a binary search per element -- moved 0.6 TB/s: 530 us per call,
-// profiles/r05/prof_graph).  The same values in the same places.
-__global__ __launch_bounds__(256) void k_im2col_2d_b(const float* X, SegRows sr, int Ttot, int F, int C, int kf,
-                                                     int kt, int sf, int Fo, float* col) {
-  const int pf = (kf - 1) / 2, pt = (kt - 1) / 2;
-  const int kq = kf * kt, K = C * kq;
-  const int lane = threadIdx.x & 63;
+// A block per RB consecutive output rows (t, f): each row's utterance lookup and position once,
+// into LDS; the rows' taps are read channel-fastest (C = 32 consecutive floats of one (t, f)
+// position: coalesced) into an LDS image of the block's RB * K columns, which is then written as
+// one contiguous run of the col buffer, every lane busy.  The wave-per-row form left 55 of 64 lanes
+// idle on the 1-channel stem (K = 9), read tap-fastest and split columns by runtime divisions.
+// Alone, 16 000 frames (tools/im2col_bench, profiles/r06/im2col_bench.txt): stem 336 -> 25 us,
+// 1x1 shortcut 198 -> 50 us, 3x3 blocks 8-15 % faster (1.4-1.9 TB/s written).  The same values in
+// the same places as the one-utterance k_im2col_2d (column c * KF * KT + aa * KT + bb).
+template <int C, int KF, int KT>
+__global__ __launch_bounds__(256) void k_im2col_2d_b(const float* X, SegRows sr, int Ttot, int F, int sf, int Fo,
+                                                     float* col) {
+  constexpr int KQ = KF * KT, K = C * KQ, RB = K >= 64 ? 32 : 256;
+  constexpr int PF = (KF - 1) / 2, PT = (KT - 1) / 2;
+  __shared__ int s_t[RB], s_T[RB], s_o[RB], s_f[RB];
+  __shared__ float s_col[RB * K];
   const int nrows = Ttot * Fo;
-  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < nrows; row += gridDim.x * 4) {
-    const int tg = row / Fo, f = row - tg * Fo;
-    const int b = seg_of(sr.off, sr.B, tg);
-    const int t = tg - sr.off[b], T = sr.len[b], o = sr.off[b];
-    float* dst = col + (long long)row * K;
-    for (int r = lane; r < K; r += 64) {
-      const int c = r / kq, q = r - c * kq;
-      const int aa = q / kt, bb = q - aa * kt;
-      const int tt = t + bb - pt, ff = f * sf + aa - pf;
-      dst[r] = (tt >= 0 && tt < T && ff >= 0 && ff < F) ? X[((long long)(o + tt) * F + ff) * C + c] : 0.f;
+  for (int r0 = blockIdx.x * RB; r0 < nrows; r0 += gridDim.x * RB) {
+    for (int rl = threadIdx.x; rl < RB; rl += 256) {
+      const int row = r0 + rl;
+      if (row < nrows) {
+        const int tg = row / Fo;
+        const int b = seg_of(sr.off, sr.B, tg);
+        s_t[rl] = tg - sr.off[b];
+        s_T[rl] = sr.len[b];
+        s_o[rl] = sr.off[b];
+        s_f[rl] = row - tg * Fo;
+      }
     }
+    __syncthreads();
+    const int n = min(RB, nrows - r0) * K;
+    for (int e = threadIdx.x; e < n; e += 256) {   // channel-fastest reads
+      const int rl = e / K, r = e - rl * K;
+      const int q = r / C, c = r - q * C;
+      const int aa = q / KT, bb = q - aa * KT;
+      const int tt = s_t[rl] + bb - PT, ff = s_f[rl] * sf + aa - PF;
+      s_col[rl * K + c * KQ + q] =
+          (tt >= 0 && tt < s_T[rl] && ff >= 0 && ff < F) ? X[((long long)(s_o[rl] + tt) * F + ff) * C + c] : 0.f;
+    }
+    __syncthreads();
+    float* dst = col + (long long)r0 * K;
+    for (int e = threadIdx.x; e < n; e += 256) dst[e] = s_col[e];
+    __syncthreads();
   }
 }
 
@@ -604,9 +625,15 @@ void launch_im2col_2d_b(const float* X, const SegRows& sr, int Ttot, int F, int 
                         float* col, hipStream_t s) {
   const long long rows = (long long)Ttot * Fo;
   if (rows <= 0 || C * kf * kt <= 0) return;
-  WDR_CHECK(rows < (1ll << 31), "im2col 2d: too many rows");
-  const int grid = (int)std::min<long long>((rows + 3) / 4, 16384);
-  WDR_KLAUNCH(k_im2col_2d_b, dim3(grid), dim3(256), 0, s, X, sr, Ttot, F, C, kf, kt, sf, Fo, col);
+  WDR_CHECK(rows < (1ll << 31) && rows * C * kf * kt < (1ll << 40), "im2col 2d: too many rows");
+  auto go = [&](auto kern, int rb) {
+    const int grid = (int)std::min<long long>((rows + rb - 1) / rb, 8192);
+    WDR_KLAUNCH(kern, dim3(grid), dim3(256), 0, s, X, sr, Ttot, F, sf, Fo, col);
+  };
+  if (C == 1 && kf == 3 && kt == 3) go(k_im2col_2d_b<1, 3, 3>, 256);
+  else if (C == 32 && kf == 3 && kt == 3) go(k_im2col_2d_b<32, 3, 3>, 32);
+  else if (C == 32 && kf == 1 && kt == 1) go(k_im2col_2d_b<32, 1, 1>, 256);
+  else WDR_CHECK(false, "im2col 2d: shape without an instantiation (CAM++ FCM: C 1 / 32, 3x3 / 1x1)");
   WDR_HIP(hipGetLastError());
 }
 

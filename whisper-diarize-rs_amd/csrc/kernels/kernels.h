@@ -25,7 +25,7 @@ struct Im2colMelArgs {
   f16* out;                        // [3000][kp]
 };
 void launch_im2col_mel(const Im2colMelArgs& a, hipStream_t s);
-void launch_im2col_conv2(const f16* x, int d, f16* out, hipStream_t s);
+void launch_im2col_conv2(const f16* x, int d, int nb, f16* out, hipStream_t s);   // nb windows
 void launch_mel_window(const float* mel, int n_mels, int n_fft_frames, const int* gmax, int seek, float* out,
                        hipStream_t s);
 void launch_energy(const float* x, int n, float* e, hipStream_t s);

@@ -150,7 +150,15 @@ hipStream_t dedicated_stream(const char* knob, bool def, int prio) {
   WDR_HIP(hipGetDevice(&dev));
   WDR_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
   std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-  for (int c = 0; c < ncu; ++c) mask[c / 32] |= 1u << (c % 32);
+  // knob = 2 (A/B, MI355X): only the CUs the encode-ahead pool leaves free (WDR_ENC_MASK under
+  // WDR_ENC_MASK_PAT=1: 4 per XCD), so this stream's workgroups never wait behind encoder tiles
+  const int n_res = getenv("WDR_ENC_MASK") ? atoi(getenv("WDR_ENC_MASK")) : 32;
+  const bool reserved = atoi(e) == 2 && ncu == 256 && n_res > 0 && n_res <= 32 && n_res % 8 == 0;
+  for (int c = 0; c < ncu; ++c) {
+    const int x = c / 32, r = c % 32;   // the encoder pool's pattern-1 reservation
+    const bool res = r % 8 == x && r / 8 < n_res / 8;
+    if (!reserved || res) mask[c / 32] |= 1u << (c % 32);
+  }
   WDR_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
   stream_note(knob, s);
   return s;
@@ -1082,8 +1090,7 @@ static void encoder_body(Context& ctx, State::Impl& m, State::Impl::EncBufs& e, 
   const int M = nb * 1500;
   // conv1 (+GELU) -> c1 f16 [nb*3000][d]
   proj(s, e.im2col.as<f16>(), md.kp1, md.conv1_w, md.kp1, md.conv1_b, e.c1.p, d, 2 * M, d, md.kp1, EPI_F16_GELU);
-  for (int b = 0; b < nb; ++b)
-    launch_im2col_conv2(e.c1.as<f16>() + (size_t)b * 3000 * d, d, e.im2col.as<f16>() + (size_t)b * 1500 * 3 * d, s);
+  launch_im2col_conv2(e.c1.as<f16>(), d, nb, e.im2col.as<f16>(), s);
   // conv2 (+GELU) + positional -> ex f32 [nb*1500][d]
   proj(s, e.im2col.as<f16>(), 3 * d, md.conv2_w, 3 * d, md.conv2_b, e.ex.p, d, M, d, 3 * d, EPI_F32_GELU_POS,
        md.enc_pos, hp.n_audio_ctx);
