@@ -947,3 +947,17 @@ void launch_dtw_dp_only(const float* x, int rows, int M, int seek, int* times, i
 }
 
 }  // namespace wdr
+
+namespace wdr {
+// A launch that only instantiates its stream's hardware queue (Context: WDR_PRIME_POOLS):
+// `iters` dependent FMAs per lane, nothing read, a store that never happens for finite inputs.
+__global__ __launch_bounds__(256) void k_busy(int iters, float* sink) {
+  float x = (float)threadIdx.x * 1e-3f;
+  for (int i = 0; i < iters; ++i) x = fmaf(x, 0.999f, 1e-4f);
+  if (x != x && threadIdx.x == 0) sink[blockIdx.x] = x;
+}
+void launch_busy(int blocks, int iters, float* sink, hipStream_t s) {
+  WDR_KLAUNCH(k_busy, dim3(blocks), dim3(256), 0, s, iters, sink);
+  WDR_HIP(hipGetLastError());
+}
+}  // namespace wdr

@@ -25,6 +25,7 @@ struct Im2colMelArgs {
   f16* out;                        // [3000][kp]
 };
 void launch_im2col_mel(const Im2colMelArgs& a, hipStream_t s);
+void launch_busy(int blocks, int iters, float* sink, hipStream_t s);   // queue priming (Context)
 void launch_im2col_conv2(const f16* x, int d, int nb, f16* out, hipStream_t s);   // nb windows
 void launch_mel_window(const float* mel, int n_mels, int n_fft_frames, const int* gmax, int seek, float* out,
                        hipStream_t s);

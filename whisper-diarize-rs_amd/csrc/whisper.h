@@ -106,6 +106,7 @@ class Context {
   std::vector<int> aheads_dev_off;
   hipStream_t stream = nullptr;
   hipStream_t low_prime = nullptr;   // WDR_PRIME_LOWQ (whisper_ctx.cpp)
+  std::vector<hipStream_t> prime_streams;   // WDR_PRIME_POOLS (whisper_ctx.cpp)
   // self-attention KV caches of every decode chain (State), one pool so that the step
   // batcher can address rows of several chains: [L][max_chains * NSLOT][n_text_ctx][d] f16
   int max_chains = 1;

@@ -385,6 +385,34 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
       WDR_HIP(hipMemsetAsync(one.p, 0, 16, low_prime));
       WDR_HIP(hipStreamSynchronize(low_prime));
     }
+    // Hardware queues in a fixed order (WDR_PRIME_POOLS, default "lnh" on MI355X; "0" = off):
+    // HIP serves each stream priority from a pool of 4 hardware queues and instantiates a queue at
+    // its first use, so which queue came up when depended on which thread launched first.  Every
+    // queue of the pools is instantiated here, lowest priority first, then normal, then highest,
+    // by one 1-block launch on each of 4 streams per level (kept, so the pools' refcounts stay
+    // even).  Measured (profiles/r06/ab_lines_hwq.txt "queue pools"): this order runs both the
+    // diarized line and configs[2]'s VAD line at ~890 xRT; highest-first runs both at ~720-740,
+    // lowest-only fixes the VAD line (883) and costs the diarized one (754) -- the spread the
+    // stream-placement experiments of this round kept landing on.
+    const char* po_env = getenv("WDR_PRIME_POOLS");
+    int ncu_p = 0;
+    WDR_HIP(hipDeviceGetAttribute(&ncu_p, hipDeviceAttributeMultiprocessorCount, cp.gpu_device));
+    const char* po = po_env ? po_env : (ncu_p == 256 ? "lnh" : "");
+    if (po[0] && std::string(po) != "0") {
+      DevMem sink(4096);
+      for (const char* c = po; *c; ++c) {
+        for (int k = 0; k < 4; ++k) {
+          hipStream_t ps = nullptr;
+          if (*c == 'n') WDR_HIP(hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
+          else WDR_HIP(hipStreamCreateWithPriority(&ps, hipStreamNonBlocking, *c == 'l' ? lo : hi));
+          WDR_CHECK(*c == 'l' || *c == 'n' || *c == 'h', "WDR_PRIME_POOLS: letters l / n / h");
+          stream_note(*c == 'l' ? "prime-low" : *c == 'n' ? "prime-normal" : "prime-high", ps);
+          launch_busy(1, 1000, sink.as<float>(), ps);
+          prime_streams.push_back(ps);
+        }
+      }
+      for (hipStream_t ps : prime_streams) WDR_HIP(hipStreamSynchronize(ps));
+    }
     // WDR_DTWQ_EARLY (A/B): the DTW queue (its lowest-priority stream) made at the end of the
     // constructor, before the batcher and the states
   }
@@ -592,6 +620,7 @@ Context::~Context() {
   prefill_b.reset();
   if (stream) (void)hipStreamDestroy(stream);
   if (low_prime) (void)hipStreamDestroy(low_prime);
+  for (hipStream_t ps : prime_streams) (void)hipStreamDestroy(ps);
 }
 
 // ------------------------------------------------------------------ state buffers
