@@ -390,9 +390,10 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
     // its first use, so which queue came up when depended on which thread launched first.  Every
     // queue of the pools is instantiated here, lowest priority first, then normal, then highest,
     // by one 1-block launch on each of 4 streams per level (kept, so the pools' refcounts stay
-    // even).  Measured (profiles/r06/ab_lines_hwq.txt "queue pools"): this order runs both the
-    // diarized line and configs[2]'s VAD line at ~890 xRT; highest-first runs both at ~720-740,
-    // lowest-only fixes the VAD line (883) and costs the diarized one (754) -- the spread the
+    // even).  Measured (profiles/r06/ab_lines_hwq.txt, "Finding the cause" and after): any order
+    // with the lowest pool before the highest (lnh / nlh / lhn) runs both the diarized line and
+    // configs[2]'s VAD line at 882-895 xRT; highest first (hnl / hln) runs both at 715-742;
+    // lowest only fixes the VAD line (883) and costs the diarized one (754) -- the spread the
     // stream-placement experiments of this round kept landing on.
     const char* po_env = getenv("WDR_PRIME_POOLS");
     int ncu_p = 0;
