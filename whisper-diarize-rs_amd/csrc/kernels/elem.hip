@@ -928,6 +928,139 @@ __global__ __launch_bounds__(256) void k_dtw_dp(const float* x, int N, int M, in
   }
 }
 
+// One wave per window: lane l owns rows l*R + 1 .. l*R + R (R = ceil(N / 64) <= 4) and keeps
+// their last two anti-diagonals in registers; row i-1's values for a lane's first row come from
+// lane l-1 by a lane shuffle, so a step of the N + M - 1 anti-diagonals needs no barrier (the
+// 256-thread form above paid an LDS round trip and a workgroup barrier per step: 134 us per
+// window in the 1-h trace).  The cell arithmetic, its tie rules and the 2-bit trace are the same
+// (bit-identical times).  The backtrace keeps the current trace word in a register (a path moves
+// along a row for most of its steps) and collects the token times as it walks; the lanes write
+// them out in forward order.
+// lane l <- lane l-1 across the whole wave (DPP wave_shr:1, a VALU modifier: no LDS round trip)
+__device__ __forceinline__ float wave_shr1(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, false));
+}
+
+template <int R>
+__global__ __launch_bounds__(64) void k_dtw_dp_wave(const float* x, int N, int M, int seek, int* times, int* n_times) {
+  __shared__ uint32_t tr[DTW_NMAX * DTW_WPR];
+  __shared__ int em[DTW_NMAX + DTW_MMAX + 4];
+  __shared__ int s_ne;
+  const int lane = threadIdx.x;
+  float D1[R], D2[R], w[R][8];
+  uint32_t acc[R];
+  const float* xr[R];
+  bool live[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int i = lane * R + r + 1;
+    live[r] = i <= N;
+    xr[r] = x + (long long)(live[r] ? i - 1 : 0) * M;
+    D1[r] = INFINITY;
+    D2[r] = INFINITY;
+    acc[r] = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) w[r][q] = (live[r] && q < M) ? xr[r][q] : 0.f;
+  }
+  for (int s = 2; s <= N + M; ++s) {
+    // row i-1 of this lane's first row: the previous lane's last row (row 0 = the boundary:
+    // cost[0][0] = 0 on diagonal 0, cost[0][j > 0] = inf)
+    float up0 = wave_shr1(D1[R - 1]), diag0 = wave_shr1(D2[R - 1]);
+    if (lane == 0) {
+      up0 = INFINITY;
+      diag0 = s == 2 ? 0.f : INFINITY;
+    }
+    float nv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int i = lane * R + r + 1, j = s - i;
+      const float c0 = r == 0 ? diag0 : D2[r - 1], c1 = r == 0 ? up0 : D1[r - 1], c2 = D1[r];
+      nv[r] = INFINITY;
+      if (live[r] && j >= 1 && j <= M) {
+        float c;
+        uint32_t t;
+        if (c0 < c1 && c0 < c2) { c = c0; t = 0; }
+        else if (c1 < c0 && c1 < c2) { c = c1; t = 1; }
+        else { c = c2; t = 2; }
+        nv[r] = w[r][0] + c;
+#pragma unroll
+        for (int q = 0; q < 7; ++q) w[r][q] = w[r][q + 1];
+        w[r][7] = (j - 1 + 8 < M) ? xr[r][j - 1 + 8] : 0.f;
+        acc[r] |= t << (2 * ((j - 1) & 15));
+        if (((j - 1) & 15) == 15 || j == M) {
+          tr[(i - 1) * DTW_WPR + ((j - 1) >> 4)] = acc[r];
+          acc[r] = 0;
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      D2[r] = D1[r];
+      D1[r] = nv[r];
+    }
+  }
+  __syncthreads();
+  if (lane == 0) {
+    // backtrace from (N, M) (trace[0][:] = 2, trace[:][0] = 1).  Path point k = (ii - 1, jj - 1);
+    // walked forward (k descending) a token time is emitted where the row index changes (from
+    // 0 before the first point), so point k is emitted iff its row differs from point k+1's.
+    int ii = N, jj = M, ne = 0, pv = 0, pj = 0;
+    bool have = false;
+    int wr = -1, wc = -1;
+    uint32_t word = 0;
+    while (ii > 0 || jj > 0) {
+      const int vi = ii - 1, vj = jj - 1;
+      if (have && pv != vi) em[ne++] = 2 * pj + seek;
+      pv = vi;
+      pj = vj;
+      have = true;
+      int t;
+      if (ii == 0) t = 2;
+      else if (jj == 0) t = 1;
+      else {
+        const int r = ii - 1, c = (jj - 1) >> 4;
+        if (r != wr || c != wc) {
+          word = tr[r * DTW_WPR + c];
+          wr = r;
+          wc = c;
+        }
+        t = (word >> (2 * ((jj - 1) & 15))) & 3;
+      }
+      if (t == 0) { --ii; --jj; }
+      else if (t == 1) --ii;
+      else --jj;
+    }
+    if (have && pv != 0) em[ne++] = 2 * pj + seek;
+    s_ne = ne;
+    *n_times = ne;
+  }
+  __syncthreads();
+  const int ne = s_ne;
+  for (int k = lane; k < ne; k += 64) times[k] = em[ne - 1 - k];
+}
+
+static void launch_dtw_dp(const float* x, int rows, int M, int seek, int* times, int* n_times, hipStream_t s) {
+  static const bool old = getenv("WDR_DTW_DP_OLD") && atoi(getenv("WDR_DTW_DP_OLD")) != 0;   // A/B
+  if (old) {
+    WDR_KLAUNCH(k_dtw_dp, dim3(1), dim3(256), 0, s, x, rows, M, seek, times, n_times);
+    return;
+  }
+  // WDR_DTW_WAVE_MAX = the most rows per lane the one-wave form takes (default 1: it serialises
+  // a lane's rows, so above 64 rows the 256-thread form is faster; tools/dtw_bench)
+  static const int rmax = getenv("WDR_DTW_WAVE_MAX") ? atoi(getenv("WDR_DTW_WAVE_MAX")) : 1;
+  const int R = (rows + 63) / 64;
+  if (R > rmax) {
+    WDR_KLAUNCH(k_dtw_dp, dim3(1), dim3(256), 0, s, x, rows, M, seek, times, n_times);
+    return;
+  }
+  switch (R) {
+    case 1: WDR_KLAUNCH(k_dtw_dp_wave<1>, dim3(1), dim3(64), 0, s, x, rows, M, seek, times, n_times); break;
+    case 2: WDR_KLAUNCH(k_dtw_dp_wave<2>, dim3(1), dim3(64), 0, s, x, rows, M, seek, times, n_times); break;
+    case 3: WDR_KLAUNCH(k_dtw_dp_wave<3>, dim3(1), dim3(64), 0, s, x, rows, M, seek, times, n_times); break;
+    default: WDR_KLAUNCH(k_dtw_dp_wave<4>, dim3(1), dim3(64), 0, s, x, rows, M, seek, times, n_times); break;
+  }
+}
+
 void launch_dtw(const float* cap, int A, int N_tok, int Tk, int n_audio, int sot_len, int seek, float* nrm, float* x,
                 int* times, int* n_times, hipStream_t s) {
   const int M = n_audio;
@@ -936,13 +1069,13 @@ void launch_dtw(const float* cap, int A, int N_tok, int Tk, int n_audio, int sot
   WDR_CHECK(M >= 1 && M <= 1500, "DTW: frame count out of range");
   WDR_KLAUNCH(k_dtw_norm, dim3(cdiv(A * M, 256)), dim3(256), 0, s, cap, A, N_tok, Tk, M, nrm);
   WDR_KLAUNCH(k_dtw_medmean, dim3(cdiv(rows * M, 256)), dim3(256), 0, s, nrm, A, N_tok, M, sot_len, x);
-  WDR_KLAUNCH(k_dtw_dp, dim3(1), dim3(256), 0, s, x, rows, M, seek, times, n_times);
+  launch_dtw_dp(x, rows, M, seek, times, n_times, s);
   WDR_HIP(hipGetLastError());
 }
 
 void launch_dtw_dp_only(const float* x, int rows, int M, int seek, int* times, int* n_times, hipStream_t s) {
   WDR_CHECK(rows >= 1 && rows <= DTW_NMAX && M >= 1 && M <= 1500, "DTW: shape out of range");
-  WDR_KLAUNCH(k_dtw_dp, dim3(1), dim3(256), 0, s, x, rows, M, seek, times, n_times);
+  launch_dtw_dp(x, rows, M, seek, times, n_times, s);
   WDR_HIP(hipGetLastError());
 }
 
