@@ -591,6 +591,27 @@ def main():
     vad_t = [0.0, 0]
     barrier()
     lib.wdr_prof_set_mask(prof_mask)
+    def cg_throttle():
+        try:
+            kv = dict(ln.split() for ln in open("/sys/fs/cgroup/cpu.stat"))
+            return int(kv.get("nr_throttled", 0)), int(kv.get("throttled_usec", 0))
+        except (OSError, ValueError):
+            return 0, 0
+    def thread_cpu():
+        # per thread-name CPU ticks of this process (/proc/self/task/*/stat utime + stime)
+        out = {}
+        for tid in os.listdir("/proc/self/task"):
+            try:
+                st = open("/proc/self/task/%s/stat" % tid).read()
+            except OSError:
+                continue
+            name = st[st.index("(") + 1:st.rindex(")")]
+            f = st[st.rindex(")") + 2:].split()
+            out[tid] = (name, int(f[11]) + int(f[12]))
+        return out
+    tc0 = thread_cpu() if os.environ.get("WDR_BENCH_THREADS") else None
+    th0 = cg_throttle()
+    c0 = os.times()
     t0 = time.perf_counter()
     n_out = 0
     for _ in range(args.steps):
@@ -598,6 +619,19 @@ def main():
         n_out += len(out)
     barrier()
     dt = time.perf_counter() - t0
+    c1 = os.times()
+    host_cpu_s = (c1.user - c0.user) + (c1.system - c0.system)   # every thread of this process
+    th1 = cg_throttle()
+    thread_cpu_s = None
+    if tc0 is not None:
+        tc1, hz = thread_cpu(), os.sysconf("SC_CLK_TCK")
+        agg = {}
+        for tid, (name, t1) in tc1.items():
+            d = t1 - tc0.get(tid, (name, 0))[1]
+            a_ = agg.setdefault(name, [0.0, 0])
+            a_[0] += d / hz
+            a_[1] += 1
+        thread_cpu_s = {k: [round(v[0], 2), v[1]] for k, v in sorted(agg.items(), key=lambda kv: -kv[1][0])[:12]}
     if args.keepalive > 0 or args.keepalive_mb > 0:
         ka_stop.set()
         ka.join()
@@ -730,6 +764,12 @@ def main():
                               "chunks": ((n_total if world > 1 else pcm.size) + 511) // 512,
                               "us_per_chunk": round(vad.last_us_per_step, 3)}),
             "load_s": round(t_load, 2), "segments_out": n_out // max(1, args.steps),
+            # host CPU time of the timed steps (all threads of the process, user + system): the
+            # box grants one GPU's process 16 CPUs (cgroup cpu.max)
+            "host_cpu": {"cpu_s": round(host_cpu_s, 3), "wall_s": round(dt, 3),
+                         "cpus_busy": round(host_cpu_s / max(dt, 1e-9), 2),
+                         "cg_throttled": th1[0] - th0[0], "cg_throttled_s": round((th1[1] - th0[1]) * 1e-6, 3),
+                         "by_thread_name": thread_cpu_s},
         }
         print(json.dumps(line), flush=True)
     if world > 1:

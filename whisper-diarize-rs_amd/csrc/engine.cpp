@@ -25,6 +25,7 @@
 #include <exception>
 #include <mutex>
 #include <set>
+#include <pthread.h>
 #include <thread>
 #include <vector>
 
@@ -261,6 +262,7 @@ class EmbedAhead {
   EmbedAhead(CamModel& cam, const std::vector<wdr_speech_segment>& segs)
       : emb_(segs.size() * 512), ok_(segs.size(), 0) {
     th_ = std::thread([this, &cam, &segs] {
+      pthread_setname_np(pthread_self(), "wdr-embed");
       try {
         // batches of consecutive segments (CamModel::embed_batch: one forward over all their
         // frames); the first batch is small so that segment 0's embedding is ready early
@@ -931,6 +933,7 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
     std::vector<std::thread> th;
     for (int k = 0; k < C; ++k)
       th.emplace_back([&, k] {
+        pthread_setname_np(pthread_self(), "wdr-chain");
         worker(k);
         live--;
       });
@@ -976,6 +979,7 @@ static std::vector<SegOut> decode_chains(wdr_context* c, const std::vector<wdr_s
     std::vector<std::thread> th;
     for (int k : redo)
       th.emplace_back([&, k] {
+        pthread_setname_np(pthread_self(), "wdr-fixup");
         fix(k);
         live--;
       });

@@ -18,6 +18,7 @@
 #include <condition_variable>
 #include <deque>
 #include <set>
+#include <pthread.h>
 #include <thread>
 #include <mutex>
 #include <sstream>
@@ -1423,7 +1424,10 @@ void State::top_up(int j) {
     }
     return;
   }
-  if (!m.enc_th.joinable()) m.enc_th = std::thread([this] { enc_loop(); });
+  if (!m.enc_th.joinable()) m.enc_th = std::thread([this] {
+    pthread_setname_np(pthread_self(), "wdr-encode");
+    enc_loop();
+  });
   std::unique_lock<std::mutex> lk(m.enc_mu);
   m.enc_target = std::max(m.enc_target, j);
   m.enc_cv.notify_all();
@@ -3526,7 +3530,10 @@ DtwQueue::DtwQueue(Context& ctx) : m_(new Impl), ctx_(ctx) {
   m.nrm = DevMem((size_t)m.A * RMAX * 1500 * 4);
   m.xdtw = DevMem((size_t)RMAX * 1500 * 4);
   m.times = DevMem((RMAX + 8) * 4);
-  m.th = std::thread([this] { run(); });
+  m.th = std::thread([this] {
+    pthread_setname_np(pthread_self(), "wdr-dtwq");
+    run();
+  });
 }
 
 DtwQueue::~DtwQueue() {
