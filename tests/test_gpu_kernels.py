@@ -326,6 +326,19 @@ def test_dtw_dp_max_size(lib):
     assert _dtw_dp(lib, x, 3000) == odtw.token_times(x, 3000)
 
 
+def test_dtw_dp_wave_form_boundaries(lib):
+    # the one-wave DP (<= 64 token rows, kernels/elem.hip k_dtw_dp_wave) and the 256-thread form
+    # (above 64) at their edges: one row / one column, exactly 64 and 65 rows, short and full
+    # windows, tie-heavy integer costs -- token times identical to the oracle's DP
+    rng = np.random.default_rng(11)
+    for rows, cols, ties in [(1, 1, False), (1, 1500, False), (3, 2, True), (64, 7, True), (64, 1500, False),
+                             (65, 300, True), (63, 1500, True), (17, 333, False)]:
+        x = rng.standard_normal((rows, cols)).astype(np.float32)
+        if ties:
+            x = np.round(x)
+        assert _dtw_dp(lib, x, 40) == odtw.token_times(x, 40), (rows, cols, ties)
+
+
 def test_dtw_preprocessing_bit_exact(lib):
     rng = np.random.default_rng(9)
     A, N, n_audio, sot_len = 5, 23, 731, 1
