@@ -387,9 +387,11 @@ Context::Context(const std::string& model_name, const HParams& hp, const Context
       WDR_HIP(hipStreamSynchronize(low_prime));
     }
     // Hardware queues in a fixed order (WDR_PRIME_POOLS, default "lnh" on MI355X; "0" = off):
-    // HIP serves each stream priority from a pool of 4 hardware queues and instantiates a queue at
-    // its first use, so which queue came up when depended on which thread launched first.  Every
-    // queue of the pools is instantiated here, lowest priority first, then normal, then highest,
+    // HIP serves each stream priority from a pool of 4 hardware queues; which of them first carried
+    // work, and in what order, followed whichever thread launched first -- and that order set a
+    // 15-25 % difference in every batched decode launch for the rest of the process (measured;
+    // the mechanism inside the command processor is not visible from the runtime).  Every queue
+    // of the pools gets its first work here, lowest priority first, then normal, then highest,
     // by one 1-block launch on each of 4 streams per level (kept, so the pools' refcounts stay
     // even).  Measured (profiles/r06/ab_lines_hwq.txt, "Finding the cause" and after): any order
     // with the lowest pool before the highest (lnh / nlh / lhn) runs both the diarized line and
