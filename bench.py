@@ -610,9 +610,26 @@ def main():
             out[tid] = (name, int(f[11]) + int(f[12]))
         return out
     tc0 = thread_cpu() if os.environ.get("WDR_BENCH_THREADS") else None
+    thr_log = []
+    if os.environ.get("WDR_BENCH_THROTTLE_LOG"):
+        # diagnostic: when in the timed steps the cgroup's throttled-period count moves (10-ms poll)
+        import threading
+        thr_stop = threading.Event()
+
+        def thr_poll():
+            last = cg_throttle()[0]
+            while not thr_stop.is_set():
+                n_ = cg_throttle()[0]
+                if n_ != last:
+                    thr_log.append((round(time.perf_counter() - t0, 3), n_ - last))
+                    last = n_
+                time.sleep(0.01)
+        thr_th = threading.Thread(target=thr_poll, daemon=True)
     th0 = cg_throttle()
     c0 = os.times()
     t0 = time.perf_counter()
+    if os.environ.get("WDR_BENCH_THROTTLE_LOG"):
+        thr_th.start()
     n_out = 0
     for _ in range(args.steps):
         out, _ = step()
@@ -622,6 +639,9 @@ def main():
     c1 = os.times()
     host_cpu_s = (c1.user - c0.user) + (c1.system - c0.system)   # every thread of this process
     th1 = cg_throttle()
+    if os.environ.get("WDR_BENCH_THROTTLE_LOG"):
+        thr_stop.set()
+        thr_th.join()
     thread_cpu_s = None
     if tc0 is not None:
         tc1, hz = thread_cpu(), os.sysconf("SC_CLK_TCK")
@@ -769,7 +789,8 @@ def main():
             "host_cpu": {"cpu_s": round(host_cpu_s, 3), "wall_s": round(dt, 3),
                          "cpus_busy": round(host_cpu_s / max(dt, 1e-9), 2),
                          "cg_throttled": th1[0] - th0[0], "cg_throttled_s": round((th1[1] - th0[1]) * 1e-6, 3),
-                         "by_thread_name": thread_cpu_s},
+                         "by_thread_name": thread_cpu_s, "throttle_at_s": thr_log or None,
+                         "segmentation_s": round(vad_t[0], 3)},
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -126,6 +126,26 @@ static bool no_graph() {
 // that queue (configs[2]'s VAD line: long segments, windows encoded on demand on the state
 // stream after such a wait; profiles/r05/vad_line_queues.txt).  The chain's host thread waits
 // for the event instead -- it synchronises on that stream right after anyway.
+// A chain's wait for its encoded window: hipEventQuery every WDR_READY_POLL_US (default 50 us)
+// with the thread asleep in between, instead of hipEventSynchronize, which spins.  At a run's
+// start all 40 chains wait for their first encode batches together (0.1-0.6 s in); spinning, they
+// spent the process's CPU quota (16 CPUs a 100-ms period on the box) in each of those periods and
+// the kernel froze every thread of the process for the rest of it -- 5 throttled periods in a row
+// (bench.py host_cpu.throttle_at_s).  0: hipEventSynchronize.
+static void wait_event_polled(hipEvent_t ev) {
+  static const int us = getenv("WDR_READY_POLL_US") ? atoi(getenv("WDR_READY_POLL_US")) : 50;
+  if (us <= 0) {
+    WDR_HIP(hipEventSynchronize(ev));
+    return;
+  }
+  for (;;) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) WDR_HIP(q);
+    std::this_thread::sleep_for(std::chrono::microseconds(us));
+  }
+}
+
 static bool host_fence() {
   static const bool v = !(getenv("WDR_HOST_FENCE") && atoi(getenv("WDR_HOST_FENCE")) == 0);
   return v;
@@ -2718,7 +2738,7 @@ int State::full(const FullParams& params, const float* samples, int n, int job, 
     }
     m.cur = job % m.S;
     n = m.plan.n[job];
-    WDR_HIP(hipEventSynchronize(m.slots[m.cur].ready));
+    wait_event_polled(m.slots[m.cur].ready);
     times.encode += now_s() - t_start;   // time the decoder waited on the encode-ahead stream
     c_ready = now_s() - c_t0 - c_top;
     t_start = now_s();
